@@ -1,0 +1,259 @@
+#!/usr/bin/env python3
+"""bench.py — pod-node evals/s and pods placed/s of the batched scheduling core on MI355X.
+
+Metric (BASELINE.json): "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X".
+A step = one pass of the hot path (filter -> prescore -> score -> select, i.e.
+minisched/minisched.go:50-87 for every pod of a batch) over one batch of synthetic pods with
+inputs already resident in HBM.
+
+Modes
+  batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per GPU. With N GPUs the pods
+              are sharded (each rank its own 100k batch; no data-path collective) -> weak scaling.
+  sequential  BASELINE C5: same sizes, one pod at a time with node-state commits.
+  nodeshard   BASELINE C4 shape: the node table split over the ranks, per-shard best keys
+              merged with an RCCL all-reduce(MAX), then decoded (--nodes 100000 --pods 1000000).
+
+Launch: `python bench.py` (1 GPU) or
+`python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N`.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
+VALU_PEAK_LANE_OPS = 157.3e12 / 2  # MI355X_MICROARCH.md: FP32 vector peak 157.3 TFLOPS = 2 x lane-ops/s
+HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+LANE_OPS_PER_EVAL = 2.5            # compare + select + half a v_max3 per (pod, node) pair
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mode", choices=["batch", "sequential", "nodeshard"], default="batch")
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--pods", type=int, default=None, help="pods per GPU (batch/sequential) or total (nodeshard)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-check", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    build = importlib.import_module("mini-kube-scheduler_amd.build")
+    if not build.LIB.exists():
+        build.build()
+    msh = importlib.import_module("mini-kube-scheduler_amd")
+    synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
+
+    mode = args.mode
+    if mode == "nodeshard":
+        n_total = args.nodes or 100_000
+        p_total = args.pods or 1_000_000
+    else:
+        n_total = args.nodes or 5_000
+        p_total = args.pods or 100_000
+
+    ctx = msh.DeviceContext(local)
+    ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+    unsched, node_digit = synth.make_nodes(n_total)[1:]
+    if mode == "nodeshard":
+        a, b = n_total * rank // world, n_total * (rank + 1) // world
+        ctx.upload_nodes(unsched[a:b], node_digit[a:b])
+        node_base = a
+        pod_digit, pod_tol = synth._make_pods_fast(p_total, synth.SEED)[1:]
+    else:
+        ctx.upload_nodes(unsched, node_digit)
+        node_base = 0
+        # pod-sharded weak scaling: rank r owns pods [r*P, (r+1)*P) of one global stream
+        pod_digit, pod_tol = synth._make_pods_fast(p_total * world, synth.SEED)[1:]
+        pod_digit = np.ascontiguousarray(pod_digit[rank * p_total:(rank + 1) * p_total])
+        pod_tol = np.ascontiguousarray(pod_tol[rank * p_total:(rank + 1) * p_total])
+    p = len(pod_digit)
+    d_pd = torch.from_numpy(pod_digit).to(dev)
+    d_pt = torch.from_numpy(pod_tol).to(dev)
+    d_idx = torch.empty(p, dtype=torch.int32, device=dev)
+    d_score = torch.empty(p, dtype=torch.int64, device=dev)
+    d_status = torch.empty(p, dtype=torch.int32, device=dev)
+    d_keys = torch.zeros(2 * p, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(ev0=None, ev1=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        if mode == "batch":
+            ctx.schedule_batch_device(p, d_pd.data_ptr(), d_pt.data_ptr(), d_idx.data_ptr(), d_score.data_ptr(),
+                                      d_status.data_ptr(), sh)
+        elif mode == "sequential":
+            ctx.schedule_sequential_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, d_idx.data_ptr(),
+                                           d_score.data_ptr(), d_status.data_ptr(), sh)
+        else:
+            ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), node_base, d_keys.data_ptr(), sh)
+        if ev1 is not None:
+            ev1.record(stream)
+        if mode == "nodeshard":
+            if world > 1:
+                dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)
+            ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), d_keys.data_ptr(), d_idx.data_ptr(),
+                                   d_score.data_ptr(), d_status.data_ptr(), sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        step(e0, e1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    # ---- correctness spot-check of the last step against the independent closed form ----
+    check = "skipped"
+    if rank == 0 and not args.no_check:
+        sys.path.insert(0, str(ROOT / "tests"))
+        from closed_form import closed_form  # independent checker, not the oracle
+        ci, cs, cst = closed_form(unsched, node_digit, pod_digit, pod_tol)
+        gi, gs, gst = d_idx.cpu().numpy(), d_score.cpu().numpy(), d_status.cpu().numpy()
+        ok = (gi == ci).all() and (gs == cs).all() and (gst == cst).all()
+        check = "bit-exact vs closed form" if ok else "MISMATCH"
+
+    n_local = ctx.n_nodes
+    evals_total = float(n_total) * float(p if mode != "nodeshard" else p_total) * args.steps * (world if mode != "nodeshard" else 1)
+    pods_total = float(p) * args.steps * (world if mode != "nodeshard" else 1)
+    value = evals_total / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # ---- roofline of the dominant kernel (batch_kernel), per launch, from HIP events ----
+    kern_s = kernel_ms * 1e-3
+    evals_launch = float(n_local) * p
+    lane_ops = LANE_OPS_PER_EVAL * evals_launch
+    uniq_bytes = 2.0 * n_local + 18.0 * p           # node records + pod records + outputs, once
+    survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts LDS re-reads)
+    traffic = None
+    pmc = ROOT / "profiles" / "pmc_latest.json"
+    if pmc.exists():
+        try:
+            pj = json.loads(pmc.read_text())
+            if pj.get("mode") == mode and pj.get("nodes") == n_local and pj.get("pods") == p:
+                traffic = pj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {
+        "bound": "valu",
+        "achieved": lane_ops / kern_s / 1e9,
+        "peak": VALU_PEAK_LANE_OPS / 1e9,
+        "unit": "Glane-op/s",
+        "frac": lane_ops / kern_s / VALU_PEAK_LANE_OPS,
+        "traffic": traffic,
+        "kernel": "batch_kernel" if mode != "sequential" else "seq_kernel",
+        "kernel_ms": kernel_ms,
+        "lane_ops_per_eval": LANE_OPS_PER_EVAL,
+        "hbm": {"bound": "hbm", "achieved": uniq_bytes / kern_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": uniq_bytes / kern_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
+                "survey_8d_bytes_per_launch": survey_bytes,
+                "survey_8d_frac": survey_bytes / kern_s / HBM_PEAK},
+    }
+
+    cpu = None
+    if rank == 0 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(unsched, node_digit, pod_digit, pod_tol, args.cpu_seconds, mode)
+
+    if rank == 0:
+        if mode == "batch":
+            wl = f"C3 batched: {n_total} nodes x {p} pods per GPU (pod-sharded over {world} GPU)"
+        elif mode == "sequential":
+            wl = f"C5 sequential-commit: {n_total} nodes x {p} pods per GPU, one pod at a time"
+        else:
+            wl = f"C4 node-sharded: {n_total} nodes over {world} GPU x {p_total} pods, RCCL allreduce(MAX) merge"
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "pod-node evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak" if mode != "nodeshard" else "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 seed 0x6d696e69: 10% unschedulable nodes, 1% non-digit pods, 5% tolerating)",
+            "config": {"workload": wl, "nodes": n_total, "pods_per_step": int(p if mode != "nodeshard" else p_total),
+                       "plugins": "filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber w=1]",
+                       "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}"},
+            "pods_per_s": pods_total / elapsed,
+            "check": check,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode: str):
+    """The C restatement (oracle/msh_oracle.c) on this host's cores, on a bounded sample of the
+    same workload: pods in chunks against the full node table until the budget is spent."""
+    O = importlib.import_module("oracle.oracle")
+    build = importlib.import_module("mini-kube-scheduler_amd.build")
+    build.build_oracle()
+    n = len(unsched)
+    chunk = 2000
+    done, t = 0, 0.0
+    while t < budget_s and done < len(pod_digit):
+        sl = slice(done, min(done + chunk, len(pod_digit)))
+        t0 = time.perf_counter()
+        if mode == "sequential":
+            O.c_schedule_sequential(unsched, node_digit, pod_digit[sl], pod_tol[sl])
+        else:
+            O.c_schedule_batch(unsched, node_digit, pod_digit[sl], pod_tol[sl])
+        t += time.perf_counter() - t0
+        done = sl.stop
+    evals = float(n) * done
+    return {"value": evals / t, "unit": "pod-node evals/s", "cores": 1, "kind": "port",
+            "sample": f"{done} pods x {n} nodes (first {done} pods of the batch), scalar C restatement, "
+                      f"{t:.1f} s on {os.cpu_count()} visible host CPUs",
+            "pods_per_s": done / t}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,205 @@
+/*
+ * minisched_hip.h — C-ABI of libminisched_hip.so, the MI355X (gfx950) scheduling core.
+ *
+ * This is the drop-in boundary for the reference's per-pod hot path
+ * (shopetan/mini-kube-scheduler, Go, k8s v1.22.0):
+ *
+ *   minisched/minisched.go:32-87   Scheduler.scheduleOne (selection part)
+ *   minisched/minisched.go:115-151 RunFilterPlugins   -> feasibility stage
+ *   minisched/minisched.go:153-162 RunPreScorePlugins -> per-pod prescore (pod digit)
+ *   minisched/minisched.go:164-199 RunScorePlugins    -> score + normalize + sum stage
+ *   minisched/minisched.go:304-325 selectHost         -> argmax stage (first max, see below)
+ *   minisched/plugins/score/nodenumber/nodenumber.go:50-100  NodeNumber PreScore/Score
+ *   k8s.io/kubernetes@v1.22.0 .../nodeunschedulable Filter (wired minisched/initialize.go:193-202)
+ *
+ * The reference evaluates ONE pod against a freshly LISTed []v1.Node per cycle.
+ * Here a whole batch of pods is evaluated against a device-resident node table.
+ * A cgo binding replaces scheduleOne's :40-80 segment for a batch
+ * drained from activeQ; Permit/Bind stay per pod on the host.
+ *
+ * Conventions
+ *  - Every function returns an int: MSH_OK (0) or a negative msh_err code.
+ *    Per-pod outcomes are NOT errors: they go to out_status (MSH_PLACED /
+ *    MSH_FIT_ERROR / MSH_SCORE_ERROR), mirroring minisched.go:50-80 + ErrorFunc :283-298.
+ *  - Host pointers are caller-owned; the library copies them in/out and keeps
+ *    no pointer past the call. "_device" entry points take device pointers and a
+ *    hipStream_t passed as void* (NULL = the null stream) and are asynchronous.
+ *  - A ctx is bound to one device and is not thread-safe; every entry point
+ *    calls hipSetDevice(ctx->device) first (cgo calls land on arbitrary OS threads).
+ *  - Node tables are in the reference's LIST order: byte-wise sorted node names
+ *    (etcd key order, minisched.go:40). msh_pack_nodes produces that order.
+ *  - Tie-break: the reference's selectHost reservoir-samples ties with math/rand
+ *    (minisched.go:316-321). This library's contract is deterministic: the
+ *    LOWEST node index among the maximum total score (first max in List order).
+ */
+#ifndef MINISCHED_HIP_H
+#define MINISCHED_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSH_ABI_VERSION 1
+
+/* ---- error codes (return values) ---- */
+typedef enum msh_err {
+  MSH_OK = 0,
+  MSH_ERR_INVALID = -1,     /* bad argument (null pointer, negative size, bad plugin id, ...) */
+  MSH_ERR_NO_DEVICE = -2,   /* no HIP device / bad device ordinal */
+  MSH_ERR_HIP = -3,         /* a HIP runtime call failed (message in msh_last_error) */
+  MSH_ERR_STATE = -4,       /* call order: e.g. schedule before msh_upload_nodes */
+  MSH_ERR_UNSUPPORTED = -5, /* plugin combination / size the device path does not implement */
+  MSH_ERR_NOMEM = -6
+} msh_err;
+
+/* ---- per-pod outcome (out_status) ---- */
+typedef enum msh_status {
+  MSH_PLACED = 0,      /* selectHost returned a node (minisched.go:80-87) */
+  MSH_FIT_ERROR = 1,   /* no feasible node: *framework.FitError (minisched.go:143-148) */
+  MSH_SCORE_ERROR = 2  /* a Score plugin failed (minisched.go:70-75); e.g. NodeNumber with
+                          no PreScore state (nodenumber.go:74-77) */
+} msh_status;
+
+/* ---- device plugin ids (framework.Plugin.Name() -> id) ---- */
+typedef enum msh_plugin_id {
+  MSH_PLUGIN_NODE_UNSCHEDULABLE = 1, /* "NodeUnschedulable" (Filter) */
+  MSH_PLUGIN_NODE_NUMBER = 2         /* "NodeNumber" (PreScore, Score) */
+} msh_plugin_id;
+
+/* ---- per-score-plugin normalize stage ----
+ * NONE reproduces the reference (NodeNumber.ScoreExtensions() == nil, nodenumber.go:98-100).
+ * The others are build extensions (parity unpinned by the reference), applied once per
+ * pod over the feasible list (upstream framework order: Score -> NormalizeScore -> weight):
+ *   DEFAULT         upstream helper.DefaultNormalizeScore(MaxNodeScore=100, reverse=false)
+ *   DEFAULT_REVERSE upstream helper.DefaultNormalizeScore(MaxNodeScore=100, reverse=true)
+ *   MINMAX          100*(s-min)/(max-min) over the feasible list; 0 when max==min           */
+typedef enum msh_normalize {
+  MSH_NORMALIZE_NONE = 0,
+  MSH_NORMALIZE_DEFAULT = 1,
+  MSH_NORMALIZE_DEFAULT_REVERSE = 2,
+  MSH_NORMALIZE_MINMAX = 3
+} msh_normalize;
+
+typedef struct msh_ctx msh_ctx;
+
+/* Library ABI version (MSH_ABI_VERSION). */
+int msh_abi_version(void);
+
+/* Number of visible HIP devices (0 on a machine without a GPU). */
+int msh_device_count(int* out_count);
+
+/* Create/destroy a context on `device`. Default plugin set = the reference's
+ * (initialize.go:80-123): filter=[NodeUnschedulable], prescore=[NodeNumber],
+ * score=[NodeNumber] weight 1, normalize NONE. */
+int msh_create(int device, msh_ctx** out_ctx);
+void msh_destroy(msh_ctx* ctx);
+
+/* Message for the last failing call on this ctx ("" if none). Valid until the next call. */
+const char* msh_last_error(const msh_ctx* ctx);
+
+/* Plugin lists (Scheduler.filterPlugins / preScorePlugins / scorePlugins,
+ * minisched/initialize.go:25-27). Ids must be unique within a list (the reference keys
+ * score maps by plugin Name(), minisched.go:173, so duplicates collapse; rejected here).
+ * weights[i] in [1, 2^32]; "TODO: plugin weight" (minisched.go:187): weight 1 == reference.
+ * msh_set_plugins: prescore list = the score plugins that implement PreScore. */
+int msh_set_plugins(msh_ctx* ctx, const int32_t* filter_ids, int32_t nf,
+                    const int32_t* score_ids, const int64_t* weights, int32_t ns);
+int msh_set_plugins_ex(msh_ctx* ctx, const int32_t* filter_ids, int32_t nf,
+                       const int32_t* prescore_ids, int32_t npre,
+                       const int32_t* score_ids, const int64_t* weights,
+                       const int32_t* normalize, int32_t ns);
+
+/* Node table in List order (name-sorted). unsched[i] = node.Spec.Unschedulable (0/1);
+ * digit[i] = last byte of node.Name as '0'..'9' -> 0..9, else -1 (nodenumber.go:81-87).
+ * 0 <= n < 2^24. Replaces the per-cycle Nodes().List (minisched.go:40). */
+int msh_upload_nodes(msh_ctx* ctx, int32_t n, const uint8_t* unsched, const int8_t* digit);
+int msh_num_nodes(const msh_ctx* ctx, int32_t* out_n);
+
+/* Batched hot path: p pods against the uploaded node table.
+ * pod_digit[j] = last byte of pod.Name as digit or -1 (nodenumber.go:50-55);
+ * pod_tol[j]   = pod tolerates taint {node.kubernetes.io/unschedulable, NoSchedule} (0/1).
+ * Outputs per pod: out_idx (node index, -1 unless PLACED), out_score (total int64 score of
+ * the selected node, 0 unless PLACED), out_status (msh_status). Synchronous. */
+int msh_schedule_batch(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                       int32_t* out_idx, int64_t* out_score, int32_t* out_status);
+
+/* Same, device-resident inputs/outputs, asynchronous on `stream` (hipStream_t). */
+int msh_schedule_batch_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
+                              const uint8_t* d_pod_tol, int32_t* d_out_idx,
+                              int64_t* d_out_score, int32_t* d_out_status, void* stream);
+
+/* Sequential-commit mode (one pod at a time, node state committed between placements).
+ * The commit increments the selected node's assigned-pod count on the device (the
+ * NodeInfo.AddPod analogue). max_pods_per_node > 0 additionally makes a node infeasible
+ * once it holds that many pods (build extension); 0 = reference semantics, where the
+ * placements equal msh_schedule_batch's. `commit_cb` (may be NULL) is replayed on the host
+ * after the device run, in placement order, once per PLACED pod. */
+typedef void (*msh_commit_cb)(void* user, int32_t pod, int32_t node_idx, int64_t score);
+int msh_schedule_sequential(msh_ctx* ctx, int32_t p, const int8_t* pod_digit,
+                            const uint8_t* pod_tol, int32_t max_pods_per_node,
+                            int32_t* out_idx, int64_t* out_score, int32_t* out_status,
+                            msh_commit_cb commit_cb, void* user);
+int msh_schedule_sequential_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
+                                   const uint8_t* d_pod_tol, int32_t max_pods_per_node,
+                                   int32_t* d_out_idx, int64_t* d_out_score,
+                                   int32_t* d_out_status, void* stream);
+/* Per-node assigned-pod counts accumulated by the sequential commits (n entries). */
+int msh_node_pod_counts(msh_ctx* ctx, int32_t* out_counts);
+int msh_reset_node_pod_counts(msh_ctx* ctx);
+
+/* ---- node-sharded mode (a cluster's node table split over devices) ----
+ * Each shard holds a contiguous slice [node_base, node_base + n) of the global List order.
+ * msh_shard_keys_device writes per pod two int64 keys (layout [2][p]):
+ *   keys[0][j] = first feasible node whose NodeNumber class is "match"   (0 = none)
+ *   keys[1][j] = first feasible "non-match" node, or (identity-like modes) the first
+ *                feasible node of any class                                (0 = none)
+ * encoded as INT64 key = 2^32 - 1 - global_idx (+1 offset so 0 means none).
+ * Element-wise MAX over shards (RCCL allreduce MAX) yields the global keys; then
+ * msh_decode_keys_device produces idx/score/status exactly as msh_schedule_batch. */
+int msh_shard_keys_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
+                          const uint8_t* d_pod_tol, int64_t node_base, int64_t* d_keys,
+                          void* stream);
+int msh_decode_keys_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
+                           const uint8_t* d_pod_tol, const int64_t* d_keys,
+                           int32_t* d_out_idx, int64_t* d_out_score, int32_t* d_out_status,
+                           void* stream);
+/* Whether keys[1] holds "first feasible of any class" (1) or "first feasible non-match" (0)
+ * under the ctx's current plugin set. */
+int msh_keys_slot1_is_any(const msh_ctx* ctx, int32_t* out_flag);
+
+/* ---- snapshot packer (host, no device needed) ----
+ * Names are given as one byte blob + n+1 offsets (name i = blob[off[i]:off[i+1]]).
+ * msh_pack_nodes sorts nodes byte-wise by name (the apiserver LIST order), and writes
+ * out_order[k] = input index of the k-th node in List order, plus the SoA columns.
+ * Empty names are rejected (the reference would panic on name[len-1:]). Duplicate names
+ * are rejected (apiserver names are unique). */
+int msh_pack_nodes(int32_t n, const char* names, const int64_t* name_off,
+                   const uint8_t* unschedulable, int32_t* out_order, uint8_t* out_unsched,
+                   int8_t* out_digit);
+
+/* One toleration of pod.Spec.Tolerations (k8s.io/api core/v1 Toleration). NULL == "". */
+typedef struct msh_toleration {
+  const char* key;
+  const char* op;     /* "", "Equal", "Exists" */
+  const char* value;
+  const char* effect; /* "", "NoSchedule", "PreferNoSchedule", "NoExecute" */
+} msh_toleration;
+
+/* Pods: digit from the name's last byte; tolerates from tolerations
+ * [tol_off[j], tol_off[j+1]) of `tols` (upstream v1helper.TolerationsTolerateTaint with the
+ * taint {Key: node.kubernetes.io/unschedulable, Effect: NoSchedule}). */
+int msh_pack_pods(int32_t p, const char* names, const int64_t* name_off,
+                  const msh_toleration* tols, const int64_t* tol_off, int8_t* out_digit,
+                  uint8_t* out_tol);
+
+/* Single-toleration predicate (Toleration.ToleratesTaint against the unschedulable taint). */
+int msh_toleration_tolerates_unschedulable(const msh_toleration* t);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MINISCHED_HIP_H */

@@ -1,0 +1,140 @@
+"""ctypes binding of libminisched_hip.so (the C-ABI declared in include/minisched_hip.h).
+
+The product path has no CPU fallback: if the library cannot be loaded, `lib()` raises.
+Only plain pointers and sizes cross the boundary (numpy arrays for host buffers, integer
+device addresses — e.g. `torch.Tensor.data_ptr()` — for the `_device` entry points).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("MSH_LIBRARY", PKG_DIR / "libminisched_hip.so"))
+
+# ---- mirrors of the header's enums ----
+MSH_OK = 0
+MSH_ERR_INVALID = -1
+MSH_ERR_NO_DEVICE = -2
+MSH_ERR_HIP = -3
+MSH_ERR_STATE = -4
+MSH_ERR_UNSUPPORTED = -5
+MSH_ERR_NOMEM = -6
+ERR_NAMES = {
+    MSH_ERR_INVALID: "MSH_ERR_INVALID",
+    MSH_ERR_NO_DEVICE: "MSH_ERR_NO_DEVICE",
+    MSH_ERR_HIP: "MSH_ERR_HIP",
+    MSH_ERR_STATE: "MSH_ERR_STATE",
+    MSH_ERR_UNSUPPORTED: "MSH_ERR_UNSUPPORTED",
+    MSH_ERR_NOMEM: "MSH_ERR_NOMEM",
+}
+
+MSH_PLACED = 0
+MSH_FIT_ERROR = 1
+MSH_SCORE_ERROR = 2
+
+MSH_PLUGIN_NODE_UNSCHEDULABLE = 1
+MSH_PLUGIN_NODE_NUMBER = 2
+
+MSH_NORMALIZE_NONE = 0
+MSH_NORMALIZE_DEFAULT = 1
+MSH_NORMALIZE_DEFAULT_REVERSE = 2
+MSH_NORMALIZE_MINMAX = 3
+
+# Every symbol include/minisched_hip.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "msh_abi_version", "msh_device_count", "msh_create", "msh_destroy", "msh_last_error",
+    "msh_set_plugins", "msh_set_plugins_ex", "msh_upload_nodes", "msh_num_nodes",
+    "msh_schedule_batch", "msh_schedule_batch_device", "msh_schedule_sequential",
+    "msh_schedule_sequential_device", "msh_node_pod_counts", "msh_reset_node_pod_counts",
+    "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
+    "msh_pack_nodes", "msh_pack_pods", "msh_toleration_tolerates_unschedulable",
+)
+
+
+class MshError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Toleration(C.Structure):
+    """msh_toleration (k8s.io/api core/v1 Toleration subset)."""
+    _fields_ = [("key", C.c_char_p), ("op", C.c_char_p), ("value", C.c_char_p), ("effect", C.c_char_p)]
+
+
+COMMIT_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.c_int64)
+
+_P = C.c_void_p
+_I32 = C.c_int32
+_I64 = C.c_int64
+
+_SIGS = {
+    "msh_abi_version": (C.c_int, []),
+    "msh_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "msh_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "msh_destroy": (None, [_P]),
+    "msh_last_error": (C.c_char_p, [_P]),
+    "msh_set_plugins": (C.c_int, [_P, _P, _I32, _P, _P, _I32]),
+    "msh_set_plugins_ex": (C.c_int, [_P, _P, _I32, _P, _I32, _P, _P, _P, _I32]),
+    "msh_upload_nodes": (C.c_int, [_P, _I32, _P, _P]),
+    "msh_num_nodes": (C.c_int, [_P, C.POINTER(_I32)]),
+    "msh_schedule_batch": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P]),
+    "msh_schedule_batch_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P]),
+    "msh_schedule_sequential": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, COMMIT_CB, _P]),
+    "msh_schedule_sequential_device": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, _P]),
+    "msh_node_pod_counts": (C.c_int, [_P, _P]),
+    "msh_reset_node_pod_counts": (C.c_int, [_P]),
+    "msh_shard_keys_device": (C.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
+    "msh_decode_keys_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "msh_keys_slot1_is_any": (C.c_int, [_P, C.POINTER(_I32)]),
+    "msh_pack_nodes": (C.c_int, [_I32, C.c_char_p, _P, _P, _P, _P, _P]),
+    "msh_pack_pods": (C.c_int, [_I32, C.c_char_p, _P, C.POINTER(Toleration), _P, _P, _P]),
+    "msh_toleration_tolerates_unschedulable": (C.c_int, [C.POINTER(Toleration)]),
+}
+
+_LIB: C.CDLL | None = None
+
+
+def lib() -> C.CDLL:
+    """Load libminisched_hip.so (in-tree). Raises if it is missing: no fallback path."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        h = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = h
+    return _LIB
+
+
+def ptr(a: np.ndarray | None):
+    """Host numpy array -> void* (None for an absent optional array)."""
+    if a is None:
+        return None
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("array must be C-contiguous")
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def check(rc: int, ctx=None) -> None:
+    if rc != MSH_OK:
+        msg = ""
+        if ctx is not None:
+            raw = lib().msh_last_error(ctx)
+            msg = raw.decode() if raw else ""
+        raise MshError(rc, msg)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().msh_device_count(C.byref(n)))
+    return n.value

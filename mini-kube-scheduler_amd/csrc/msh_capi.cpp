@@ -1,0 +1,493 @@
+// msh_capi.cpp — implementation of include/minisched_hip.h (the drop-in C-ABI).
+//
+// One msh_ctx per device. The ctx owns the device-resident node table (the replacement for
+// the per-cycle Nodes().List at minisched/minisched.go:40), the plugin descriptor
+// (minisched/initialize.go:80-123) and scratch buffers for the host-buffer entry points.
+// There is no CPU fallback: every schedule call runs the gfx950 kernels, and a missing
+// device is an error (MSH_ERR_NO_DEVICE).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/minisched_hip.h"
+#include "msh_internal.h"
+
+using msh::PluginParams;
+
+struct msh_ctx {
+  int device = 0;
+  std::string err;
+  msh::DeviceInfo dev;
+  hipStream_t stream = nullptr;  // used by the synchronous host-buffer entry points
+
+  // plugin descriptor
+  std::vector<int32_t> filter_ids, prescore_ids, score_ids, normalize;
+  std::vector<int64_t> weights;
+  PluginParams pp{1, 1, 1, 0, 1};
+
+  // node table
+  bool have_nodes = false;
+  bool dirty = true;
+  int32_t n_nodes = 0, n_pad = 0;
+  uint8_t* d_unsched = nullptr;
+  int8_t* d_digit = nullptr;
+  uint32_t* d_kn = nullptr;
+  uint8_t* d_dig = nullptr;
+  unsigned long long* d_mask = nullptr;
+  uint32_t* d_ball = nullptr;
+  int32_t* d_counts = nullptr;
+  size_t node_cap = 0;
+
+  // host-path scratch
+  size_t pod_cap = 0;
+  int8_t* d_pd = nullptr;
+  uint8_t* d_pt = nullptr;
+  int32_t* d_oi = nullptr;
+  int64_t* d_os = nullptr;
+  int32_t* d_ost = nullptr;
+  size_t partial_cap = 0;
+  uint32_t* d_partial = nullptr;  // multi-tile node tables only
+};
+
+namespace {
+
+constexpr int32_t NODE_PAD = 64 * 16;  // node table padded to whole 16-chunk blocks
+
+int fail(msh_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+  return fail(c, MSH_ERR_HIP, m);
+}
+
+#define MSH_HIP(ctx, call)                               \
+  do {                                                   \
+    hipError_t e_ = (call);                              \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+  } while (0)
+
+void free_nodes(msh_ctx* c) {
+  hipFree(c->d_unsched); hipFree(c->d_digit); hipFree(c->d_kn); hipFree(c->d_dig);
+  hipFree(c->d_mask); hipFree(c->d_counts);
+  c->d_unsched = nullptr; c->d_digit = nullptr; c->d_kn = nullptr; c->d_dig = nullptr;
+  c->d_mask = nullptr; c->d_counts = nullptr;
+  c->node_cap = 0;
+}
+
+void free_pods(msh_ctx* c) {
+  hipFree(c->d_pd); hipFree(c->d_pt); hipFree(c->d_oi); hipFree(c->d_os); hipFree(c->d_ost);
+  c->d_pd = nullptr; c->d_pt = nullptr; c->d_oi = nullptr; c->d_os = nullptr; c->d_ost = nullptr;
+  c->pod_cap = 0;
+}
+
+int ensure_pod_scratch(msh_ctx* c, int32_t p) {
+  if ((size_t)p <= c->pod_cap) return MSH_OK;
+  free_pods(c);
+  size_t cap = std::max<size_t>((size_t)p, 1024);
+  MSH_HIP(c, hipMalloc(&c->d_pd, cap));
+  MSH_HIP(c, hipMalloc(&c->d_pt, cap));
+  MSH_HIP(c, hipMalloc(&c->d_oi, cap * sizeof(int32_t)));
+  MSH_HIP(c, hipMalloc(&c->d_os, cap * sizeof(int64_t)));
+  MSH_HIP(c, hipMalloc(&c->d_ost, cap * sizeof(int32_t)));
+  c->pod_cap = cap;
+  return MSH_OK;
+}
+
+bool contains(const std::vector<int32_t>& v, int32_t id) {
+  return std::find(v.begin(), v.end(), id) != v.end();
+}
+
+int check_ids(msh_ctx* c, const int32_t* ids, int32_t n, bool filter, const char* what) {
+  if (n < 0 || n > 8) return fail(c, MSH_ERR_INVALID, std::string(what) + ": bad list length");
+  if (n > 0 && !ids) return fail(c, MSH_ERR_INVALID, std::string(what) + ": null list");
+  for (int32_t i = 0; i < n; i++) {
+    const int32_t id = ids[i];
+    const bool ok = filter ? id == MSH_PLUGIN_NODE_UNSCHEDULABLE : id == MSH_PLUGIN_NODE_NUMBER;
+    if (!ok)
+      return fail(c, MSH_ERR_UNSUPPORTED,
+                  std::string(what) + ": plugin id " + std::to_string(id) + " has no device implementation");
+    for (int32_t k = 0; k < i; k++)
+      if (ids[k] == id) return fail(c, MSH_ERR_INVALID, std::string(what) + ": duplicate plugin id");
+  }
+  return MSH_OK;
+}
+
+int prepare(msh_ctx* c, hipStream_t s) {
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  if (!c->dirty) return MSH_OK;
+  hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad,
+                                       c->pp.has_nu_filter, c->d_kn, c->d_dig, c->d_mask,
+                                       c->d_ball, s);
+  if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
+  c->dirty = false;
+  return MSH_OK;
+}
+
+int ensure_partial(msh_ctx* c, int32_t p) {
+  if (msh::batch_tile_chunks(c->n_pad / 64) >= c->n_pad / 64) return MSH_OK;
+  if ((size_t)p <= c->partial_cap) return MSH_OK;
+  (void)hipFree(c->d_partial);
+  c->d_partial = nullptr;
+  c->partial_cap = 0;
+  const size_t cap = std::max<size_t>((size_t)p, 1024);
+  MSH_HIP(c, hipMalloc(&c->d_partial, 2 * cap * sizeof(uint32_t)));
+  c->partial_cap = cap;
+  return MSH_OK;
+}
+
+msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t* pt) {
+  msh::BatchArgs a{};
+  a.kn = c->d_kn;
+  a.dig = c->d_dig;
+  a.n_nodes = c->n_nodes;
+  a.n_chunks = c->n_pad / 64;
+  a.pod_digit = pd;
+  a.pod_tol = pt;
+  a.n_pods = p;
+  a.ball = c->d_ball;
+  a.pp = c->pp;
+  a.partial = c->d_partial;
+  return a;
+}
+
+struct DeviceGuard {
+  explicit DeviceGuard(int d) { (void)hipSetDevice(d); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int msh_abi_version(void) { return MSH_ABI_VERSION; }
+
+int msh_device_count(int* out_count) {
+  if (!out_count) return MSH_ERR_INVALID;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *out_count = (e == hipSuccess) ? n : 0;
+  return MSH_OK;
+}
+
+int msh_create(int device, msh_ctx** out_ctx) {
+  if (!out_ctx) return MSH_ERR_INVALID;
+  *out_ctx = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MSH_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return MSH_ERR_NO_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return MSH_ERR_NO_DEVICE;
+  msh_ctx* c = new (std::nothrow) msh_ctx();
+  if (!c) return MSH_ERR_NOMEM;
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->dev.cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return MSH_ERR_HIP;
+  }
+  if (hipMalloc(&c->d_ball, 2 * sizeof(uint32_t)) != hipSuccess) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return MSH_ERR_HIP;
+  }
+  // Reference plugin set (minisched/initialize.go:80-123).
+  c->filter_ids = {MSH_PLUGIN_NODE_UNSCHEDULABLE};
+  c->prescore_ids = {MSH_PLUGIN_NODE_NUMBER};
+  c->score_ids = {MSH_PLUGIN_NODE_NUMBER};
+  c->weights = {1};
+  c->normalize = {MSH_NORMALIZE_NONE};
+  c->pp = PluginParams{1, 1, 1, MSH_NORMALIZE_NONE, 1};
+  *out_ctx = c;
+  return MSH_OK;
+}
+
+void msh_destroy(msh_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  free_nodes(c);
+  free_pods(c);
+  (void)hipFree(c->d_partial);
+  (void)hipFree(c->d_ball);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* msh_last_error(const msh_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+int msh_set_plugins_ex(msh_ctx* c, const int32_t* filter_ids, int32_t nf,
+                       const int32_t* prescore_ids, int32_t npre, const int32_t* score_ids,
+                       const int64_t* weights, const int32_t* normalize, int32_t ns) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  int rc;
+  if ((rc = check_ids(c, filter_ids, nf, true, "filter")) != MSH_OK) return rc;
+  if ((rc = check_ids(c, prescore_ids, npre, false, "prescore")) != MSH_OK) return rc;
+  if ((rc = check_ids(c, score_ids, ns, false, "score")) != MSH_OK) return rc;
+  for (int32_t i = 0; i < ns; i++) {
+    const int64_t w = weights ? weights[i] : 1;
+    if (w < 1 || w > (int64_t(1) << 32)) return fail(c, MSH_ERR_INVALID, "score weight outside [1, 2^32]");
+    const int32_t m = normalize ? normalize[i] : MSH_NORMALIZE_NONE;
+    if (m < MSH_NORMALIZE_NONE || m > MSH_NORMALIZE_MINMAX) return fail(c, MSH_ERR_INVALID, "bad normalize mode");
+  }
+  c->filter_ids.assign(filter_ids, filter_ids + nf);
+  c->prescore_ids.assign(prescore_ids, prescore_ids + npre);
+  c->score_ids.assign(score_ids, score_ids + ns);
+  c->weights.clear();
+  c->normalize.clear();
+  for (int32_t i = 0; i < ns; i++) {
+    c->weights.push_back(weights ? weights[i] : 1);
+    c->normalize.push_back(normalize ? normalize[i] : MSH_NORMALIZE_NONE);
+  }
+  PluginParams pp{};
+  pp.has_nu_filter = contains(c->filter_ids, MSH_PLUGIN_NODE_UNSCHEDULABLE) ? 1 : 0;
+  pp.nn_prescore = contains(c->prescore_ids, MSH_PLUGIN_NODE_NUMBER) ? 1 : 0;
+  pp.has_nn_score = 0;
+  pp.mode = MSH_NORMALIZE_NONE;
+  pp.weight = 1;
+  for (int32_t i = 0; i < ns; i++) {
+    if (c->score_ids[i] == MSH_PLUGIN_NODE_NUMBER) {
+      pp.has_nn_score = 1;
+      pp.mode = c->normalize[i];
+      pp.weight = c->weights[i];
+    }
+  }
+  if (pp.has_nu_filter != c->pp.has_nu_filter) c->dirty = true;
+  c->pp = pp;
+  return MSH_OK;
+}
+
+int msh_set_plugins(msh_ctx* c, const int32_t* filter_ids, int32_t nf, const int32_t* score_ids,
+                    const int64_t* weights, int32_t ns) {
+  // NodeNumber implements PreScore too (nodenumber.go:50), so it is its own prescore plugin.
+  std::vector<int32_t> pre;
+  for (int32_t i = 0; i < ns && score_ids; i++)
+    if (score_ids[i] == MSH_PLUGIN_NODE_NUMBER) pre.push_back(score_ids[i]);
+  return msh_set_plugins_ex(c, filter_ids, nf, pre.data(), (int32_t)pre.size(), score_ids, weights,
+                            nullptr, ns);
+}
+
+int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t* digit) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (n < 0 || n > msh::MAX_NODES) return fail(c, MSH_ERR_INVALID, "node count outside [0, 2^24-2]");
+  if (n > 0 && (!unsched || !digit)) return fail(c, MSH_ERR_INVALID, "null node arrays");
+  DeviceGuard g(c->device);
+  const int32_t n_pad = ((n + NODE_PAD - 1) / NODE_PAD) * NODE_PAD;
+  if ((size_t)n_pad > c->node_cap || c->d_kn == nullptr) {
+    free_nodes(c);
+    const size_t cap = std::max<size_t>((size_t)n_pad, NODE_PAD);
+    MSH_HIP(c, hipMalloc(&c->d_unsched, cap));
+    MSH_HIP(c, hipMalloc(&c->d_digit, cap));
+    MSH_HIP(c, hipMalloc(&c->d_kn, cap * sizeof(uint32_t)));
+    MSH_HIP(c, hipMalloc(&c->d_dig, cap));
+    MSH_HIP(c, hipMalloc(&c->d_mask, 2 * (cap / 64) * sizeof(unsigned long long)));
+    MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
+    c->node_cap = cap;
+  }
+  if (n > 0) {
+    MSH_HIP(c, hipMemcpyAsync(c->d_unsched, unsched, (size_t)n, hipMemcpyHostToDevice, c->stream));
+    MSH_HIP(c, hipMemcpyAsync(c->d_digit, digit, (size_t)n, hipMemcpyHostToDevice, c->stream));
+  }
+  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->node_cap * sizeof(int32_t), c->stream));
+  c->n_nodes = n;
+  c->n_pad = n_pad;
+  c->have_nodes = true;
+  c->dirty = true;
+  int rc = prepare(c, c->stream);
+  if (rc != MSH_OK) return rc;
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  return MSH_OK;
+}
+
+int msh_num_nodes(const msh_ctx* c, int32_t* out_n) {
+  if (!c || !out_n) return MSH_ERR_INVALID;
+  *out_n = c->have_nodes ? c->n_nodes : 0;
+  return MSH_OK;
+}
+
+int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
+                              const uint8_t* d_pod_tol, int32_t* d_out_idx, int64_t* d_out_score,
+                              int32_t* d_out_status, void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_out_idx || !d_out_score || !d_out_status))
+    return fail(c, MSH_ERR_INVALID, "null device pointer");
+  DeviceGuard g(c->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int rc = prepare(c, s);
+  if (rc != MSH_OK) return rc;
+  if ((rc = ensure_partial(c, p)) != MSH_OK) return rc;
+  msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
+  a.out_idx = d_out_idx;
+  a.out_score = d_out_score;
+  a.out_status = d_out_status;
+  hipError_t e = msh::launch_batch(a, false, c->dev, s, &c->err);
+  if (e != hipSuccess) return hip_fail(c, e, "batch_kernel");
+  return MSH_OK;
+}
+
+int msh_schedule_batch(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                       int32_t* out_idx, int64_t* out_score, int32_t* out_status) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  if (p > 0 && (!pod_digit || !pod_tol || !out_idx || !out_score || !out_status))
+    return fail(c, MSH_ERR_INVALID, "null host pointer");
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  if (p == 0) return MSH_OK;
+  DeviceGuard g(c->device);
+  int rc = ensure_pod_scratch(c, p);
+  if (rc != MSH_OK) return rc;
+  MSH_HIP(c, hipMemcpyAsync(c->d_pd, pod_digit, (size_t)p, hipMemcpyHostToDevice, c->stream));
+  MSH_HIP(c, hipMemcpyAsync(c->d_pt, pod_tol, (size_t)p, hipMemcpyHostToDevice, c->stream));
+  rc = msh_schedule_batch_device(c, p, c->d_pd, c->d_pt, c->d_oi, c->d_os, c->d_ost, c->stream);
+  if (rc != MSH_OK) return rc;
+  MSH_HIP(c, hipMemcpyAsync(out_idx, c->d_oi, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  MSH_HIP(c, hipMemcpyAsync(out_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  MSH_HIP(c, hipMemcpyAsync(out_status, c->d_ost, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  return MSH_OK;
+}
+
+int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
+                                   const uint8_t* d_pod_tol, int32_t max_pods_per_node,
+                                   int32_t* d_out_idx, int64_t* d_out_score,
+                                   int32_t* d_out_status, void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0 || max_pods_per_node < 0) return fail(c, MSH_ERR_INVALID, "negative argument");
+  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_out_idx || !d_out_score || !d_out_status))
+    return fail(c, MSH_ERR_INVALID, "null device pointer");
+  DeviceGuard g(c->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int rc = prepare(c, s);
+  if (rc != MSH_OK) return rc;
+  msh::SeqArgs a{};
+  a.kn = c->d_kn;
+  a.dig = c->d_dig;
+  a.n_nodes = c->n_nodes;
+  a.n_chunks = c->n_pad / 64;
+  a.pod_digit = d_pod_digit;
+  a.pod_tol = d_pod_tol;
+  a.n_pods = p;
+  a.pp = c->pp;
+  a.max_pods = max_pods_per_node;
+  a.counts = c->d_counts;
+  a.out_idx = d_out_idx;
+  a.out_score = d_out_score;
+  a.out_status = d_out_status;
+  std::string err;
+  hipError_t e = msh::launch_sequential(a, s, &err);
+  if (e != hipSuccess) {
+    if (!err.empty()) return fail(c, MSH_ERR_UNSUPPORTED, err);
+    return hip_fail(c, e, "seq_kernel");
+  }
+  return MSH_OK;
+}
+
+int msh_schedule_sequential(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                            int32_t max_pods_per_node, int32_t* out_idx, int64_t* out_score,
+                            int32_t* out_status, msh_commit_cb commit_cb, void* user) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  if (p > 0 && (!pod_digit || !pod_tol || !out_idx || !out_score || !out_status))
+    return fail(c, MSH_ERR_INVALID, "null host pointer");
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  if (p == 0) return MSH_OK;
+  DeviceGuard g(c->device);
+  int rc = ensure_pod_scratch(c, p);
+  if (rc != MSH_OK) return rc;
+  MSH_HIP(c, hipMemcpyAsync(c->d_pd, pod_digit, (size_t)p, hipMemcpyHostToDevice, c->stream));
+  MSH_HIP(c, hipMemcpyAsync(c->d_pt, pod_tol, (size_t)p, hipMemcpyHostToDevice, c->stream));
+  rc = msh_schedule_sequential_device(c, p, c->d_pd, c->d_pt, max_pods_per_node, c->d_oi, c->d_os,
+                                      c->d_ost, c->stream);
+  if (rc != MSH_OK) return rc;
+  MSH_HIP(c, hipMemcpyAsync(out_idx, c->d_oi, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  MSH_HIP(c, hipMemcpyAsync(out_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  MSH_HIP(c, hipMemcpyAsync(out_status, c->d_ost, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  if (commit_cb)
+    for (int32_t j = 0; j < p; j++)
+      if (out_status[j] == MSH_PLACED) commit_cb(user, j, out_idx[j], out_score[j]);
+  return MSH_OK;
+}
+
+int msh_node_pod_counts(msh_ctx* c, int32_t* out_counts) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  if (c->n_nodes > 0 && !out_counts) return fail(c, MSH_ERR_INVALID, "null output");
+  if (c->n_nodes == 0) return MSH_OK;
+  DeviceGuard g(c->device);
+  MSH_HIP(c, hipDeviceSynchronize());
+  MSH_HIP(c, hipMemcpy(out_counts, c->d_counts, (size_t)c->n_nodes * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return MSH_OK;
+}
+
+int msh_reset_node_pod_counts(msh_ctx* c) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  DeviceGuard g(c->device);
+  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->node_cap * sizeof(int32_t), c->stream));
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  return MSH_OK;
+}
+
+int msh_keys_slot1_is_any(const msh_ctx* c, int32_t* out_flag) {
+  if (!c || !out_flag) return MSH_ERR_INVALID;
+  *out_flag = msh::needs_kx(c->pp) ? 0 : 1;
+  return MSH_OK;
+}
+
+int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
+                          const uint8_t* d_pod_tol, int64_t node_base, int64_t* d_keys,
+                          void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0 || node_base < 0) return fail(c, MSH_ERR_INVALID, "negative argument");
+  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_keys)) return fail(c, MSH_ERR_INVALID, "null device pointer");
+  if (node_base + (int64_t)c->n_nodes >= msh::GKEY_MAX) return fail(c, MSH_ERR_INVALID, "global node index overflows the key");
+  DeviceGuard g(c->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int rc = prepare(c, s);
+  if (rc != MSH_OK) return rc;
+  if ((rc = ensure_partial(c, p)) != MSH_OK) return rc;
+  msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
+  a.keys = d_keys;
+  a.node_base = node_base;
+  hipError_t e = msh::launch_batch(a, true, c->dev, s, &c->err);
+  if (e != hipSuccess) return hip_fail(c, e, "batch_kernel(shard)");
+  return MSH_OK;
+}
+
+int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
+                           const uint8_t* d_pod_tol, const int64_t* d_keys, int32_t* d_out_idx,
+                           int64_t* d_out_score, int32_t* d_out_status, void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  if (p > 0 && (!d_pod_digit || !d_keys || !d_out_idx || !d_out_score || !d_out_status))
+    return fail(c, MSH_ERR_INVALID, "null device pointer");
+  DeviceGuard g(c->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int32_t slot1_any = msh::needs_kx(c->pp) ? 0 : 1;
+  hipError_t e = msh::launch_decode_keys(d_pod_digit, d_pod_tol, p, d_keys, slot1_any, c->pp,
+                                         d_out_idx, d_out_score, d_out_status, s);
+  if (e != hipSuccess) return hip_fail(c, e, "decode_keys_kernel");
+  return MSH_OK;
+}
+
+}  // extern "C"

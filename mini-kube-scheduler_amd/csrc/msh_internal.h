@@ -1,0 +1,94 @@
+// msh_internal.h — shared between the C-ABI (msh_capi.cpp) and the gfx950 kernels
+// (msh_kernels.hip). Not part of the public ABI (include/minisched_hip.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+namespace msh {
+
+// Local node key: KMAX - node_index (> 0 for every valid index), 0 = "no node".
+// A larger key is a smaller index, so an unsigned max is the reference's first-max scan
+// order (selectHost, minisched.go:304-325, with the deterministic tie-break).
+constexpr uint32_t KMAX = 0xFFFFFFu;
+constexpr int32_t MAX_NODES = 0xFFFFFE;          // node index must stay < KMAX
+constexpr uint32_t DIGIT_NONE = 0xFFu;           // node suffix is not '0'..'9'
+constexpr uint32_t POD_DIGIT_NONE = 0xFEu;       // never equals a node digit (0..9 / 0xFF)
+constexpr int WAVE = 64;
+constexpr int BATCH_THREADS = 256;               // 4 waves per workgroup
+constexpr int SEQ_THREADS = 1024;                // 16 waves, one workgroup
+constexpr int SEQ_MAX_CHUNKS_PER_WAVE = 32;      // sequential mode: node table in registers
+constexpr int64_t GKEY_MAX = 0xFFFFFFFFll;       // global (sharded) key = GKEY_MAX - global_idx
+
+// Per-ctx plugin set as the kernels see it (minisched/initialize.go:80-123 lists).
+struct PluginParams {
+  int32_t has_nu_filter;  // "NodeUnschedulable" in filter list
+  int32_t has_nn_score;   // "NodeNumber" in score list
+  int32_t nn_prescore;    // "NodeNumber" in prescore list (state written)
+  int32_t mode;           // NodeNumber normalize mode (msh_normalize)
+  int64_t weight;         // NodeNumber weight
+};
+
+// Whether the argmax needs the "first feasible NON-match" key per pod (reverse / min-max
+// normalization); otherwise the first feasible node of the pod's class suffices.
+inline bool needs_kx(const PluginParams& pp) {
+  return pp.has_nn_score && pp.nn_prescore && (pp.mode == 2 || pp.mode == 3);
+}
+
+struct DeviceInfo {
+  int cus = 256;
+};
+
+// ---- launchers (msh_kernels.hip) ----
+hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
+                            int32_t n_pad, int32_t has_nu, uint32_t* d_kn, uint8_t* d_dig,
+                            unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s);
+
+struct BatchArgs {
+  const uint32_t* kn;        // [n_pad] non-tolerating-class key per node (0 = infeasible)
+  const uint8_t* dig;        // [n_pad] node digit 0..9 / 0xFF
+  int32_t n_nodes, n_chunks; // n_chunks = n_pad / 64
+  const int8_t* pod_digit;
+  const uint8_t* pod_tol;
+  int32_t n_pods;
+  const uint32_t* ball;      // [2] first feasible key per pod class (0: !tol, 1: tol)
+  PluginParams pp;
+  int32_t* out_idx;
+  int64_t* out_score;
+  int32_t* out_status;
+  int64_t* keys;             // shard mode: [2][n_pods] global keys
+  int64_t node_base;
+  uint32_t* partial;         // [2][n_pods] running keys when the node table spans > 1 LDS tile
+};
+
+// LDS tile geometry of the batched kernel (host needs it to size the partial-key scratch).
+int32_t batch_tile_chunks(int32_t n_chunks);
+
+hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s,
+                        std::string* err);
+
+hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,
+                              const int64_t* keys, int32_t slot1_any, PluginParams pp,
+                              int32_t* out_idx, int64_t* out_score, int32_t* out_status,
+                              hipStream_t s);
+
+struct SeqArgs {
+  const uint32_t* kn;
+  const uint8_t* dig;
+  int32_t n_nodes, n_chunks;
+  const int8_t* pod_digit;
+  const uint8_t* pod_tol;
+  int32_t n_pods;
+  PluginParams pp;
+  int32_t max_pods;
+  int32_t* counts;           // [n_pad] per-node assigned pods (read at start, written back)
+  int32_t* out_idx;
+  int64_t* out_score;
+  int32_t* out_status;
+};
+
+hipError_t launch_sequential(const SeqArgs& a, hipStream_t s, std::string* err);
+
+}  // namespace msh

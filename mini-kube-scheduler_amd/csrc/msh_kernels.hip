@@ -1,0 +1,542 @@
+// msh_kernels.hip — gfx950 (MI355X, CDNA4) kernels for the batched pods x nodes hot path.
+//
+// Reference path (shopetan/mini-kube-scheduler, Go): for ONE pod per cycle,
+//   RunFilterPlugins   minisched/minisched.go:115-151  (NodeUnschedulable, upstream v1.22.0)
+//   RunPreScorePlugins minisched/minisched.go:153-162  (NodeNumber.PreScore, nodenumber.go:50-64)
+//   RunScorePlugins    minisched/minisched.go:164-199  (NodeNumber.Score, nodenumber.go:73-95)
+//   selectHost         minisched/minisched.go:304-325  (argmax; ties -> lowest index here)
+//
+// Layout: "lanes = nodes". A wave holds 64 consecutive nodes of a chunk in its lanes and a
+// group of G pods in scalar registers; every (pod, node) pair is one lane-op sequence:
+//   feasible (NodeUnschedulable) . score class (NodeNumber digit compare) . first-max.
+// Stages (north_star):
+//   1. feasibility bitmask per pod class with wavefront __ballot      -> node_prep_kernel
+//   2. int64 score with the plugin weight fused                        -> decode_pod
+//   3. per-pod normalisation (DEFAULT / REVERSE / MINMAX: needs the per-pod class extent,
+//      i.e. the min/max raw score over the feasible list)               -> bm/bx keys + decode
+//   4. argmax with a fixed lowest-index tie-break: per-lane unsigned max of
+//      key = KMAX - idx, then a wave-wide DPP max reduction              -> wave_max_u32
+//   5. node-table tile staged in LDS once per workgroup and re-read for every pod group
+// See DESIGN.md for the roofline / instruction budget of each kernel.
+#include "msh_internal.h"
+
+namespace msh {
+
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_max(uint32_t v) {
+  // Lanes whose row is masked off keep `old` = 0, the identity of an unsigned max.
+  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
+  return umax(v, t);
+}
+
+// Wave-wide unsigned max over 64 lanes; the result is returned as a wave-uniform value.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = dpp_max<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = dpp_max<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = dpp_max<0x141, 0xF>(v);  // row_half_mirror
+  v = dpp_max<0x140, 0xF>(v);  // row_mirror      -> every lane of a 16-lane row holds its max
+  v = dpp_max<0x142, 0xA>(v);  // row_bcast:15    -> rows 1,3 fold in rows 0,2
+  v = dpp_max<0x143, 0xC>(v);  // row_bcast:31    -> rows 2,3 fold in row 1 (= rows 0..1)
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// ---------------------------------------------------------------------------------------
+// Stage 1: node table preparation + feasibility bitmask (once per upload / plugin change).
+// For the only filter, NodeUnschedulable (upstream v1.22.0), feasibility depends on the
+// pod only through "tolerates the unschedulable taint", so there are exactly two pod
+// classes: 0 = does not tolerate, 1 = tolerates. Class 1 is feasible on every node.
+//   kn[i]  = KMAX - i if node i is feasible for class 0, else 0
+//   dig[i] = NodeNumber node digit (Atoi of the last byte, nodenumber.go:81-87) or 0xFF
+//   mask[c][chunk] = __ballot(feasible for class c)   (64-node feasibility bitmask)
+//   ball[c] = key of the first feasible node of class c (0 = none)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restrict__ unsched,
+                                                        const int8_t* __restrict__ digit,
+                                                        int32_t n, int32_t n_pad, int32_t has_nu,
+                                                        uint32_t* __restrict__ kn,
+                                                        uint8_t* __restrict__ dig,
+                                                        unsigned long long* __restrict__ mask,
+                                                        uint32_t* __restrict__ ball) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pad) return;  // n_pad is a multiple of 64: whole waves exit together
+  const bool valid = i < n;
+  const bool u = valid && unsched[i] != 0;
+  const int d = valid ? (int)digit[i] : -1;
+  // NodeUnschedulable.Filter: Spec.Unschedulable && !tolerates -> UnschedulableAndUnresolvable
+  const bool feas0 = valid && !(has_nu && u);
+  const bool feas1 = valid;
+  kn[i] = feas0 ? (KMAX - (uint32_t)i) : 0u;
+  dig[i] = (d >= 0 && d <= 9) ? (uint8_t)d : (uint8_t)DIGIT_NONE;
+  const unsigned long long m0 = __ballot(feas0);
+  const unsigned long long m1 = __ballot(feas1);
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) {
+    const int32_t chunk = i >> 6;
+    const int32_t n_chunks = n_pad >> 6;
+    mask[chunk] = m0;
+    mask[n_chunks + chunk] = m1;
+    if (m0) atomicMax(&ball[0], KMAX - (uint32_t)(i + __builtin_ctzll(m0)));
+    if (m1) atomicMax(&ball[1], KMAX - (uint32_t)(i + __builtin_ctzll(m1)));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Stage 2+3 epilogue: status / selected node / int64 score for one pod.
+// im / ix / ia: first feasible match / first feasible non-match / first feasible of any
+// class (node index, -1 = none). ix is only read by the modes that need it (needs_kx).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void decode_pod(int64_t im, int64_t ix, int64_t ia, bool pd_valid,
+                                           const PluginParams& pp, int32_t* out_idx,
+                                           int64_t* out_score, int32_t* out_status) {
+  int64_t sel = -1, sc = 0;
+  int32_t st = 0;
+  if (ia < 0) {
+    st = 1;  // FitError: no feasible node (minisched.go:143-148)
+  } else if (pp.has_nn_score && (!pp.nn_prescore || !pd_valid)) {
+    st = 2;  // NodeNumber.Score: state.Read -> ErrNotFound (nodenumber.go:74-77), F > 0
+  } else if (!pp.has_nn_score) {
+    sel = ia;  // all totals 0: first feasible
+  } else {
+    const int64_t w = pp.weight;
+    switch (pp.mode) {
+      case 1:  // DefaultNormalizeScore: match -> 100, rest 0 (max 10), or all 0 (max 0)
+        sel = im >= 0 ? im : ia;
+        sc = im >= 0 ? 100 * w : 0;
+        break;
+      case 2:  // DefaultNormalizeScore reverse: non-match -> 100, match -> 0 (or all 100)
+        sel = ix >= 0 ? ix : im;
+        sc = ix >= 0 ? 100 * w : 0;
+        break;
+      case 3:  // min-max: (s-min)*100/(max-min); 0 when only one class is feasible
+        sel = im >= 0 ? im : ix;
+        sc = (im >= 0 && ix >= 0) ? 100 * w : 0;
+        break;
+      default:  // NONE (the reference): raw 10 on match, 0 otherwise, times weight
+        sel = im >= 0 ? im : ia;
+        sc = im >= 0 ? 10 * w : 0;
+        break;
+    }
+  }
+  *out_idx = (int32_t)sel;
+  *out_score = sc;
+  *out_status = st;
+}
+
+__device__ __forceinline__ int64_t key_to_idx(uint32_t k) {
+  return k ? (int64_t)(KMAX - k) : (int64_t)-1;
+}
+
+// ---------------------------------------------------------------------------------------
+// Batched kernel. Workgroup = 4 waves; the node table (or a tile of it) is staged in LDS
+// once per tile and re-read by every pod group of every wave. Each wave owns a contiguous
+// pod range, walked in windows of 64 pods (one pod per lane). Within a window the pods are
+// split by class with __ballot (class = tolerates the unschedulable taint), and each class
+// is processed in groups of up to G pods whose digits sit in SGPRs. For every R-chunk
+// sub-tile the wave loads R node records per lane (digit D, class key K), then for every
+// pod g of the group:
+//     m = (D == pod digit);  bm[g] = max(bm[g], m ? K : 0)   [2.5 VALU per 64 pairs]
+// (+ bx[g] = max(bx[g], m ? 0 : K) when the normalize mode needs the non-match extent).
+// K is KMAX-idx for nodes feasible for the class, else 0, so the unsigned max is the
+// first feasible match in List order. Results land in the pod's lane (lane-select) and
+// are decoded and stored once per window (coalesced).
+// ---------------------------------------------------------------------------------------
+template <int R, int G, bool NEED_KX, bool SHARD>
+__global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32_t tile_chunks) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  uint32_t* lds_k = reinterpret_cast<uint32_t*>(lds_raw);
+  uint8_t* lds_d = lds_raw + (size_t)tile_chunks * WAVE * sizeof(uint32_t);
+
+  constexpr int WPG = BATCH_THREADS / WAVE;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t W = (int64_t)gridDim.x * WPG;
+  const int64_t gw = (int64_t)blockIdx.x * WPG + wv;
+  const int32_t p0 = (int32_t)((int64_t)a.n_pods * gw / W);
+  const int32_t p1 = (int32_t)((int64_t)a.n_pods * (gw + 1) / W);
+  const int32_t ntiles = (a.n_chunks + tile_chunks - 1) / tile_chunks;
+  const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
+
+  for (int32_t t = 0; t < ntiles; ++t) {
+    // ---- stage node tile t in LDS (stage 5) ----
+    const int32_t c0t = t * tile_chunks;
+    const int32_t nc = min(tile_chunks, a.n_chunks - c0t);  // multiple of 16 (host pads)
+    if (t > 0) __syncthreads();
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(a.kn + (size_t)c0t * WAVE);
+      uint4* dst = reinterpret_cast<uint4*>(lds_k);
+      for (int32_t i = threadIdx.x; i < nc * (WAVE / 4); i += BATCH_THREADS) dst[i] = src[i];
+      const uint4* srcd = reinterpret_cast<const uint4*>(a.dig + (size_t)c0t * WAVE);
+      uint4* dstd = reinterpret_cast<uint4*>(lds_d);
+      for (int32_t i = threadIdx.x; i < nc * (WAVE / 16); i += BATCH_THREADS) dstd[i] = srcd[i];
+    }
+    __syncthreads();
+    const uint32_t ktbase = KMAX - (uint32_t)(c0t * WAVE + lane);
+    const bool last_tile = (t == ntiles - 1);
+
+    for (int32_t w0 = p0; w0 < p1; w0 += WAVE) {
+      const int32_t nwin = min((int32_t)WAVE, p1 - w0);
+      const bool act = lane < nwin;
+      uint32_t pdv = POD_DIGIT_NONE, tolv = 0;
+      if (act) {
+        const int d = a.pod_digit[w0 + lane];
+        pdv = (d >= 0 && d <= 9) ? (uint32_t)d : POD_DIGIT_NONE;
+        tolv = a.pod_tol[w0 + lane] ? 1u : 0u;
+      }
+      uint32_t res_m = 0u, res_x = 0u;
+      if (t > 0 && act) {
+        res_m = a.partial[w0 + lane];
+        if (NEED_KX) res_x = a.partial[(size_t)a.n_pods + w0 + lane];
+      }
+      const unsigned long long cls_mask[2] = {__ballot(act && tolv == 0u), __ballot(act && tolv != 0u)};
+
+#pragma unroll
+      for (int cls = 0; cls < 2; ++cls) {
+        unsigned long long mask = cls_mask[cls];
+        while (mask) {
+          // ---- form a class-homogeneous group of up to G pods (scalar) ----
+          uint32_t spd[G];
+          int32_t lsel[G];
+          int32_t cnt = 0;
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            if (mask) {
+              const int32_t l = (int32_t)__builtin_ctzll(mask);
+              mask &= mask - 1;
+              lsel[g] = l;
+              spd[g] = (uint32_t)__builtin_amdgcn_readlane((int)pdv, l);
+              cnt = g + 1;
+            } else {
+              lsel[g] = 0;
+              spd[g] = POD_DIGIT_NONE;
+            }
+          }
+          uint32_t bm[G], bx[G];
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            bm[g] = 0u;
+            bx[g] = 0u;
+          }
+          const uint32_t* pk = lds_k + lane;
+          const uint8_t* pdg = lds_d + lane;
+          for (int32_t c0 = 0; c0 < nc; c0 += R) {
+            uint32_t D[R], K[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const int32_t c = c0 + r;
+              D[r] = pdg[c * WAVE];
+              if (cls == 0) {
+                K[r] = pk[c * WAVE];
+              } else {
+                uint32_t kt = ktbase - (uint32_t)(c * WAVE);
+                if (NEED_KX) kt = ((c0t + c) * WAVE + lane < a.n_nodes) ? kt : 0u;
+                K[r] = kt;  // padding nodes carry digit 0xFF, so they never match
+              }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+              if (g < cnt) {
+                const uint32_t pd = spd[g];
+#pragma unroll
+                for (int r = 0; r < R; r += 2) {
+                  // Two selects then one v_max3_u32: 2.5 VALU per 64 (pod, node) pairs. The
+                  // empty asm keeps the selects materialised (otherwise instcombine folds
+                  // max(bm, m ? K : 0) into select(m, max(bm, K), bm): 3 VALU, one serial chain).
+                  uint32_t t0 = (D[r] == pd) ? K[r] : 0u;
+                  uint32_t t1 = (D[r + 1] == pd) ? K[r + 1] : 0u;
+                  asm("" : "+v"(t0), "+v"(t1));
+                  bm[g] = umax(umax(bm[g], t0), t1);
+                  if (NEED_KX) {
+                    uint32_t x0 = (D[r] == pd) ? 0u : K[r];
+                    uint32_t x1 = (D[r + 1] == pd) ? 0u : K[r + 1];
+                    asm("" : "+v"(x0), "+v"(x1));
+                    bx[g] = umax(umax(bx[g], x0), x1);
+                  }
+                }
+              }
+            }
+          }
+          // ---- stage 4: wave-wide first-max, result into the pod's lane ----
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            if (g < cnt) {
+              const uint32_t vm = wave_max_u32(bm[g]);
+              res_m = (lane == lsel[g]) ? umax(vm, res_m) : res_m;
+              if (NEED_KX) {
+                const uint32_t vx = wave_max_u32(bx[g]);
+                res_x = (lane == lsel[g]) ? umax(vx, res_x) : res_x;
+              }
+            }
+          }
+        }
+      }
+
+      if (!act) continue;
+      const int32_t j = w0 + lane;
+      if (!last_tile) {
+        a.partial[j] = res_m;
+        if (NEED_KX) a.partial[(size_t)a.n_pods + j] = res_x;
+        continue;
+      }
+      const uint32_t ball = tolv ? ball1 : ball0;
+      if (SHARD) {
+        const uint32_t k1 = NEED_KX ? res_x : ball;
+        a.keys[j] = res_m ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - res_m))) : 0;
+        a.keys[(size_t)a.n_pods + j] = k1 ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - k1))) : 0;
+      } else {
+        decode_pod(key_to_idx(res_m), key_to_idx(res_x), key_to_idx(ball), pdv != POD_DIGIT_NONE,
+                   a.pp, &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
+      }
+    }
+  }
+}
+
+// Decode globally merged shard keys (after an element-wise MAX across node shards).
+__global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restrict__ pod_digit,
+                                                          const uint8_t* __restrict__ pod_tol,
+                                                          int32_t p, const int64_t* __restrict__ keys,
+                                                          int32_t slot1_any, PluginParams pp,
+                                                          int32_t* __restrict__ out_idx,
+                                                          int64_t* __restrict__ out_score,
+                                                          int32_t* __restrict__ out_status) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p) return;
+  (void)pod_tol;
+  const int64_t k0 = keys[j], k1 = keys[(size_t)p + j];
+  const int64_t ka = slot1_any ? k1 : (k0 > k1 ? k0 : k1);
+  auto idx_of = [](int64_t k) -> int64_t { return k ? GKEY_MAX - k : -1; };
+  const int d = pod_digit[j];
+  decode_pod(idx_of(k0), idx_of(k1), idx_of(ka), d >= 0 && d <= 9, pp, &out_idx[j],
+             &out_score[j], &out_status[j]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Sequential-commit kernel: ONE workgroup (16 waves) walks the pods in order; node state
+// lives in registers (chunk c is owned by wave c % 16, slot c / 16). Per pod: every wave
+// scans its chunks (bm / first-feasible / bx keys), wave DPP max, one LDS exchange + one
+// barrier (double-buffered by pod parity), every wave finishes the reduction redundantly,
+// then the owner lane commits: count += 1 and, with a capacity, the node turns infeasible.
+// ---------------------------------------------------------------------------------------
+template <int RS, bool NEED_KX>
+__global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
+  constexpr int NW = SEQ_THREADS / WAVE;
+  __shared__ uint32_t red[2][3][NW];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  uint32_t D[RS], KN[RS], KT[RS];
+  int32_t CNT[RS];
+#pragma unroll
+  for (int r = 0; r < RS; ++r) {
+    const int32_t c = wv + NW * r;
+    D[r] = DIGIT_NONE;
+    KN[r] = 0u;
+    KT[r] = 0u;
+    CNT[r] = 0;
+    if (c < a.n_chunks) {
+      const int32_t i = c * WAVE + lane;
+      D[r] = a.dig[i];
+      KN[r] = a.kn[i];
+      KT[r] = i < a.n_nodes ? KMAX - (uint32_t)i : 0u;
+      CNT[r] = a.counts[i];
+      if (a.max_pods > 0 && CNT[r] >= a.max_pods) {
+        KN[r] = 0u;
+        KT[r] = 0u;
+      }
+    }
+  }
+
+  uint32_t pdv = POD_DIGIT_NONE, tolv = 0;
+  for (int32_t j = 0; j < a.n_pods; ++j) {
+    const int jl = j & (WAVE - 1);
+    if (jl == 0) {  // prefetch the next 64 pods into lanes
+      const int32_t jj = j + lane;
+      pdv = POD_DIGIT_NONE;
+      tolv = 0;
+      if (jj < a.n_pods) {
+        const int d = a.pod_digit[jj];
+        pdv = (d >= 0 && d <= 9) ? (uint32_t)d : POD_DIGIT_NONE;
+        tolv = a.pod_tol[jj] ? 1u : 0u;
+      }
+    }
+    const uint32_t pd = (uint32_t)__builtin_amdgcn_readlane((int)pdv, jl);
+    const uint32_t tol = (uint32_t)__builtin_amdgcn_readlane((int)tolv, jl);
+    uint32_t bm = 0u, ba = 0u, bx = 0u;
+    if (tol) {
+#pragma unroll
+      for (int r = 0; r < RS; ++r) {
+        const bool m = D[r] == pd;
+        bm = umax(bm, m ? KT[r] : 0u);
+        ba = umax(ba, KT[r]);
+        if (NEED_KX) bx = umax(bx, m ? 0u : KT[r]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < RS; ++r) {
+        const bool m = D[r] == pd;
+        bm = umax(bm, m ? KN[r] : 0u);
+        ba = umax(ba, KN[r]);
+        if (NEED_KX) bx = umax(bx, m ? 0u : KN[r]);
+      }
+    }
+    bm = wave_max_u32(bm);
+    ba = wave_max_u32(ba);
+    if (NEED_KX) bx = wave_max_u32(bx);
+    const int par = j & 1;
+    if (lane == 0) {
+      red[par][0][wv] = bm;
+      red[par][1][wv] = ba;
+      red[par][2][wv] = bx;
+    }
+    __syncthreads();
+    const uint32_t gm = wave_max_u32(lane < NW ? red[par][0][lane] : 0u);
+    const uint32_t ga = wave_max_u32(lane < NW ? red[par][1][lane] : 0u);
+    const uint32_t gx = NEED_KX ? wave_max_u32(lane < NW ? red[par][2][lane] : 0u) : 0u;
+    int32_t sel, st;
+    int64_t sc;
+    decode_pod(key_to_idx(gm), key_to_idx(gx), key_to_idx(ga), pd != POD_DIGIT_NONE, a.pp, &sel,
+               &sc, &st);
+    if (wv == 0 && lane == 0) {
+      a.out_idx[j] = sel;
+      a.out_score[j] = sc;
+      a.out_status[j] = st;
+    }
+    if (st == 0) {  // commit (NodeInfo.AddPod analogue) by the owning lane
+      const int32_t c = sel >> 6;
+      if ((c % NW) == wv) {
+        const int rs = c / NW;
+        const bool mine = lane == (sel & (WAVE - 1));
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+          if (r == rs && mine) {
+            CNT[r] += 1;
+            if (a.max_pods > 0 && CNT[r] >= a.max_pods) {
+              KN[r] = 0u;
+              KT[r] = 0u;
+            }
+          }
+        }
+      }
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < RS; ++r) {
+    const int32_t c = wv + NW * r;
+    if (c < a.n_chunks) a.counts[c * WAVE + lane] = CNT[r];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------------------
+hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
+                            int32_t n_pad, int32_t has_nu, uint32_t* d_kn, uint8_t* d_dig,
+                            unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(d_ball, 0, 2 * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  if (n_pad == 0) return hipSuccess;
+  const int blocks = (n_pad + 255) / 256;
+  hipLaunchKernelGGL(node_prep_kernel, dim3(blocks), dim3(256), 0, s, d_unsched, d_digit, n, n_pad,
+                     has_nu, d_kn, d_dig, d_mask, d_ball);
+  return hipGetLastError();
+}
+
+namespace {
+constexpr int BATCH_R = 8;
+constexpr int BATCH_G = 32;
+constexpr size_t LDS_BYTES_PER_NODE = sizeof(uint32_t) + sizeof(uint8_t);
+constexpr size_t BATCH_LDS_MAX = 80 * 1024;  // 2 workgroups per CU at the largest tile
+
+template <bool NEED_KX, bool SHARD>
+hipError_t launch_batch_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
+                          std::string* err) {
+  auto kern = batch_kernel<BATCH_R, BATCH_G, NEED_KX, SHARD>;
+  const int32_t tile_chunks = batch_tile_chunks(a.n_chunks);
+  if (tile_chunks < a.n_chunks && a.partial == nullptr) {
+    if (err) *err = "batch kernel: multi-tile node table needs partial-key scratch";
+    return hipErrorInvalidValue;
+  }
+  const size_t lds = (size_t)tile_chunks * WAVE * LDS_BYTES_PER_NODE;
+  int occ = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BATCH_THREADS, lds);
+  if (e != hipSuccess) return e;
+  if (occ < 1) {
+    if (err) *err = "batch kernel: zero occupancy";
+    return hipErrorInvalidConfiguration;
+  }
+  // Grid: enough waves for ~one pod group each, capped at what is resident at once, and a
+  // whole number of workgroups per CU when the cap binds (balanced XCD/CU load).
+  const int64_t waves_wanted = ((int64_t)a.n_pods + BATCH_G - 1) / BATCH_G;
+  int64_t grid = (waves_wanted + 3) / 4;
+  const int64_t cap = (int64_t)dev.cus * occ;
+  if (const char* env = getenv("MSH_BATCH_WG_PER_CU")) {
+    const int k = atoi(env);
+    if (k > 0) grid = (int64_t)dev.cus * (k < occ ? k : occ);
+  } else if (grid > cap) {
+    grid = cap;
+  } else if (grid > dev.cus) {
+    grid = ((grid + dev.cus - 1) / dev.cus) * dev.cus;
+    if (grid > cap) grid = cap;
+  }
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BATCH_THREADS), lds, s, a, tile_chunks);
+  return hipGetLastError();
+}
+}  // namespace
+
+int32_t batch_tile_chunks(int32_t n_chunks) {
+  const int32_t max_tile = (int32_t)(BATCH_LDS_MAX / (LDS_BYTES_PER_NODE * WAVE)) / 16 * 16;
+  return n_chunks <= max_tile ? n_chunks : max_tile;
+}
+
+hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s,
+                        std::string* err) {
+  if (a.n_pods == 0) return hipSuccess;
+  const bool kx = needs_kx(a.pp);
+  if (shard) return kx ? launch_batch_t<true, true>(a, dev, s, err) : launch_batch_t<false, true>(a, dev, s, err);
+  return kx ? launch_batch_t<true, false>(a, dev, s, err) : launch_batch_t<false, false>(a, dev, s, err);
+}
+
+hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,
+                              const int64_t* keys, int32_t slot1_any, PluginParams pp,
+                              int32_t* out_idx, int64_t* out_score, int32_t* out_status,
+                              hipStream_t s) {
+  if (p == 0) return hipSuccess;
+  hipLaunchKernelGGL(decode_keys_kernel, dim3((p + 255) / 256), dim3(256), 0, s, pod_digit, pod_tol,
+                     p, keys, slot1_any, pp, out_idx, out_score, out_status);
+  return hipGetLastError();
+}
+
+namespace {
+template <int RS>
+hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
+  if (needs_kx(a.pp))
+    hipLaunchKernelGGL((seq_kernel<RS, true>), dim3(1), dim3(SEQ_THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL((seq_kernel<RS, false>), dim3(1), dim3(SEQ_THREADS), 0, s, a);
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_sequential(const SeqArgs& a, hipStream_t s, std::string* err) {
+  if (a.n_pods == 0) return hipSuccess;
+  const int nw = SEQ_THREADS / WAVE;
+  const int rs = (a.n_chunks + nw - 1) / nw;
+  if (rs <= 1) return launch_seq_rs<1>(a, s);
+  if (rs <= 2) return launch_seq_rs<2>(a, s);
+  if (rs <= 3) return launch_seq_rs<3>(a, s);
+  if (rs <= 4) return launch_seq_rs<4>(a, s);
+  if (rs <= 5) return launch_seq_rs<5>(a, s);
+  if (rs <= 6) return launch_seq_rs<6>(a, s);
+  if (rs <= 8) return launch_seq_rs<8>(a, s);
+  if (rs <= 12) return launch_seq_rs<12>(a, s);
+  if (rs <= 16) return launch_seq_rs<16>(a, s);
+  if (rs <= 24) return launch_seq_rs<24>(a, s);
+  if (rs <= 32) return launch_seq_rs<32>(a, s);
+  if (err) *err = "sequential mode supports at most 32768 nodes per device";
+  return hipErrorInvalidValue;
+}
+
+}  // namespace msh

@@ -1,0 +1,226 @@
+"""Host-side mirror of minisched.Scheduler's selection path, driving the gfx950 device path.
+
+Reference (shopetan/mini-kube-scheduler, Go):
+  Scheduler struct + plugin lists   minisched/initialize.go:18-29, :80-123
+  scheduleOne (selection part)      minisched/minisched.go:32-87
+  RunFilterPlugins / RunPreScorePlugins / RunScorePlugins / selectHost
+                                    minisched/minisched.go:115-199, :304-325
+  ErrorFunc routing                 minisched/minisched.go:283-298
+
+`DeviceContext` wraps one msh_ctx (one GPU). `Scheduler` keeps the reference's plugin
+configuration by plugin *name* (framework.Plugin.Name()), maps the names the device path
+implements to device ids, and schedules a whole batch of pods in one call. Unknown plugin
+names raise MshError(MSH_ERR_UNSUPPORTED): there is no silent host fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Any, Callable, Iterable, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .framework import (NODE_NUMBER, NODE_UNSCHEDULABLE, Normalize, Outcome, ScheduleResult)
+from .snapshot import NodeTable, PodTable, pack_nodes, pack_pods
+
+FILTER_IDS = {NODE_UNSCHEDULABLE: N.MSH_PLUGIN_NODE_UNSCHEDULABLE}
+SCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER}
+PRESCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER}
+
+
+@dataclass(frozen=True)
+class ScorePluginConfig:
+    name: str
+    weight: int = 1
+    normalize: Normalize = Normalize.NONE
+
+
+def _ids(names: Sequence[str], table: dict, what: str) -> np.ndarray:
+    out = []
+    for n in names:
+        if n not in table:
+            raise N.MshError(N.MSH_ERR_UNSUPPORTED, f"{what} plugin {n!r} has no device implementation")
+        out.append(table[n])
+    return np.array(out, np.int32)
+
+
+class DeviceContext:
+    """One msh_ctx bound to one HIP device."""
+
+    def __init__(self, device: int = 0):
+        self._lib = N.lib()
+        h = C.c_void_p()
+        N.check(self._lib.msh_create(device, C.byref(h)))
+        self.handle = h
+        self.device = device
+        self.n_nodes = 0
+
+    # -- lifecycle --
+    def close(self) -> None:
+        if self.handle:
+            self._lib.msh_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int) -> None:
+        N.check(rc, self.handle)
+
+    # -- configuration --
+    def set_plugins(self, filters: Sequence[str], prescore: Sequence[str],
+                    score: Sequence[ScorePluginConfig]) -> None:
+        f = _ids(filters, FILTER_IDS, "filter")
+        pre = _ids(prescore, PRESCORE_IDS, "prescore")
+        s = _ids([c.name for c in score], SCORE_IDS, "score")
+        w = np.array([int(c.weight) for c in score], np.int64)
+        nm = np.array([int(c.normalize) for c in score], np.int32)
+        self._check(self._lib.msh_set_plugins_ex(self.handle, N.ptr(f), len(f), N.ptr(pre), len(pre),
+                                                 N.ptr(s), N.ptr(w), N.ptr(nm), len(s)))
+
+    def upload_nodes(self, unsched: np.ndarray, digit: np.ndarray) -> None:
+        unsched = np.ascontiguousarray(unsched, np.uint8)
+        digit = np.ascontiguousarray(digit, np.int8)
+        self._check(self._lib.msh_upload_nodes(self.handle, len(unsched), N.ptr(unsched), N.ptr(digit)))
+        self.n_nodes = len(unsched)
+
+    # -- host-buffer entry points --
+    def schedule_batch(self, pod_digit: np.ndarray, pod_tol: np.ndarray):
+        pod_digit = np.ascontiguousarray(pod_digit, np.int8)
+        pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
+        p = len(pod_digit)
+        idx = np.empty(p, np.int32)
+        score = np.empty(p, np.int64)
+        status = np.empty(p, np.int32)
+        self._check(self._lib.msh_schedule_batch(self.handle, p, N.ptr(pod_digit), N.ptr(pod_tol),
+                                                 N.ptr(idx), N.ptr(score), N.ptr(status)))
+        return idx, score, status
+
+    def schedule_sequential(self, pod_digit: np.ndarray, pod_tol: np.ndarray, max_pods_per_node: int = 0,
+                            on_commit: Callable[[int, int, int], None] | None = None):
+        pod_digit = np.ascontiguousarray(pod_digit, np.int8)
+        pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
+        p = len(pod_digit)
+        idx = np.empty(p, np.int32)
+        score = np.empty(p, np.int64)
+        status = np.empty(p, np.int32)
+        cb = N.COMMIT_CB(lambda _u, j, i, s: on_commit(j, i, s)) if on_commit else N.COMMIT_CB()
+        self._check(self._lib.msh_schedule_sequential(self.handle, p, N.ptr(pod_digit), N.ptr(pod_tol),
+                                                      int(max_pods_per_node), N.ptr(idx), N.ptr(score),
+                                                      N.ptr(status), cb, None))
+        return idx, score, status
+
+    def node_pod_counts(self) -> np.ndarray:
+        out = np.zeros(self.n_nodes, np.int32)
+        self._check(self._lib.msh_node_pod_counts(self.handle, N.ptr(out) if self.n_nodes else None))
+        return out
+
+    def reset_node_pod_counts(self) -> None:
+        self._check(self._lib.msh_reset_node_pod_counts(self.handle))
+
+    # -- device-resident entry points (integer device addresses, hipStream_t as int) --
+    def schedule_batch_device(self, p: int, d_pod_digit: int, d_pod_tol: int, d_idx: int, d_score: int,
+                              d_status: int, stream: int = 0) -> None:
+        self._check(self._lib.msh_schedule_batch_device(self.handle, p, d_pod_digit, d_pod_tol, d_idx,
+                                                        d_score, d_status, stream or None))
+
+    def schedule_sequential_device(self, p: int, d_pod_digit: int, d_pod_tol: int, max_pods_per_node: int,
+                                   d_idx: int, d_score: int, d_status: int, stream: int = 0) -> None:
+        self._check(self._lib.msh_schedule_sequential_device(self.handle, p, d_pod_digit, d_pod_tol,
+                                                             int(max_pods_per_node), d_idx, d_score,
+                                                             d_status, stream or None))
+
+    def shard_keys_device(self, p: int, d_pod_digit: int, d_pod_tol: int, node_base: int, d_keys: int,
+                          stream: int = 0) -> None:
+        self._check(self._lib.msh_shard_keys_device(self.handle, p, d_pod_digit, d_pod_tol, int(node_base),
+                                                    d_keys, stream or None))
+
+    def decode_keys_device(self, p: int, d_pod_digit: int, d_pod_tol: int, d_keys: int, d_idx: int,
+                           d_score: int, d_status: int, stream: int = 0) -> None:
+        self._check(self._lib.msh_decode_keys_device(self.handle, p, d_pod_digit, d_pod_tol, d_keys, d_idx,
+                                                     d_score, d_status, stream or None))
+
+    def keys_slot1_is_any(self) -> bool:
+        v = C.c_int32(0)
+        self._check(self._lib.msh_keys_slot1_is_any(self.handle, C.byref(v)))
+        return bool(v.value)
+
+
+class Scheduler:
+    """Batched mirror of minisched.Scheduler (initialize.go:18-29).
+
+    Defaults are the reference's hardcoded plugin lists (initialize.go:80-123):
+    filter=[NodeUnschedulable], preScore=[NodeNumber], score=[NodeNumber] (weight 1,
+    no NormalizeScore: nodenumber.go:98-100).
+    """
+
+    def __init__(self, filter_plugins: Sequence[str] = (NODE_UNSCHEDULABLE,),
+                 pre_score_plugins: Sequence[str] = (NODE_NUMBER,),
+                 score_plugins: Sequence[ScorePluginConfig | str] = (NODE_NUMBER,),
+                 device: int = 0, ctx: DeviceContext | None = None):
+        self.filter_plugins = list(filter_plugins)
+        self.pre_score_plugins = list(pre_score_plugins)
+        self.score_plugins = [c if isinstance(c, ScorePluginConfig) else ScorePluginConfig(c)
+                              for c in score_plugins]
+        self.ctx = ctx or DeviceContext(device)
+        self.ctx.set_plugins(self.filter_plugins, self.pre_score_plugins, self.score_plugins)
+        self.nodes: NodeTable | None = None
+
+    def close(self) -> None:
+        self.ctx.close()
+
+    # Replaces the per-cycle Nodes().List (minisched.go:40) with one device upload.
+    def update_nodes(self, nodes: Iterable[Any]) -> NodeTable:
+        self.nodes = pack_nodes(nodes)
+        self.ctx.upload_nodes(self.nodes.unsched, self.nodes.digit)
+        return self.nodes
+
+    def _results(self, pods: PodTable, idx, score, status) -> list[ScheduleResult]:
+        assert self.nodes is not None
+        n_nodes = len(self.nodes)
+        fit_plugins = frozenset(
+            # FitError diagnosis: the filter plugins that rejected at least one node. With the
+            # device plugin set that is NodeUnschedulable whenever any node exists.
+            [self.filter_plugins[0]] if (self.filter_plugins and n_nodes > 0) else [])
+        out = []
+        for j, name in enumerate(pods.names):
+            st = int(status[j])
+            if st == N.MSH_PLACED:
+                i = int(idx[j])
+                out.append(ScheduleResult(name, Outcome.PLACED, self.nodes.names[i], i, int(score[j])))
+            elif st == N.MSH_FIT_ERROR:
+                out.append(ScheduleResult(name, Outcome.FIT_ERROR, unschedulable_plugins=fit_plugins))
+            else:
+                out.append(ScheduleResult(name, Outcome.SCORE_ERROR))
+        return out
+
+    def schedule_batch(self, pods: Iterable[Any], nodes: Iterable[Any] | None = None) -> list[ScheduleResult]:
+        """scheduleOne's selection part for every pod of the batch against one snapshot."""
+        if nodes is not None:
+            self.update_nodes(nodes)
+        if self.nodes is None:
+            raise N.MshError(N.MSH_ERR_STATE, "no node snapshot: call update_nodes() first")
+        table = pack_pods(pods)
+        idx, score, status = self.ctx.schedule_batch(table.digit, table.tolerates)
+        return self._results(table, idx, score, status)
+
+    def schedule_sequential(self, pods: Iterable[Any], nodes: Iterable[Any] | None = None,
+                            max_pods_per_node: int = 0) -> list[ScheduleResult]:
+        """One pod at a time, committing each placement to node state before the next."""
+        if nodes is not None:
+            self.update_nodes(nodes)
+        if self.nodes is None:
+            raise N.MshError(N.MSH_ERR_STATE, "no node snapshot: call update_nodes() first")
+        table = pack_pods(pods)
+        idx, score, status = self.ctx.schedule_sequential(table.digit, table.tolerates, max_pods_per_node)
+        return self._results(table, idx, score, status)

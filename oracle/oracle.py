@@ -1,0 +1,298 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module,
+as the checker (or the timed CPU baseline). The product path (the package
+`mini-kube-scheduler_amd`) never imports it.
+
+Two restatements of the reference hot path (shopetan/mini-kube-scheduler, Go):
+
+1. `ObjectOracle` — pure Python over v1.Node / v1.Pod-like objects (names, Spec.Unschedulable,
+   Spec.Tolerations). It follows the Go code line by line, strings included:
+     - List order: etcd key order = byte-wise sorted names (minisched/minisched.go:40)
+     - RunFilterPlugins  minisched/minisched.go:115-151 (first failure breaks, order kept)
+     - NodeUnschedulable.Filter + v1helper.TolerationsTolerateTaint / Toleration.ToleratesTaint
+       (k8s.io/kubernetes v1.22.0, k8s.io/api v0.22.0 — absent here, restated)
+     - RunPreScorePlugins minisched/minisched.go:153-162; NodeNumber.PreScore nodenumber.go:50-64
+     - RunScorePlugins   minisched/minisched.go:164-199; NodeNumber.Score nodenumber.go:73-95
+     - selectHost        minisched/minisched.go:304-325 with the first-max tie-break
+   Used for small cases and to generate / pin the golden fixtures.
+
+2. `c_schedule_batch` / `c_schedule_sequential` — ctypes entry to oracle/msh_oracle.c, the
+   same restatement in C over SoA columns, fast enough for full-size parity checks and the
+   CPU baseline (1 thread, or OpenMP pod-parallel).
+
+Parity status: pinned by the reference's only known answer, the sched.go:70-143 scenario
+(tests/golden/scenario.json); everything else is restatement-derived and cross-checked
+against an independent closed form (tests/closed_form.py). See msh_oracle.c's header.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+ORACLE_LIB = ORACLE_DIR / "build" / "libmsh_oracle.so"
+
+PLACED, FIT_ERROR, SCORE_ERROR = 0, 1, 2
+NODE_UNSCHEDULABLE, NODE_NUMBER = 1, 2
+NORM_NONE, NORM_DEFAULT, NORM_DEFAULT_REVERSE, NORM_MINMAX = 0, 1, 2, 3
+PLUGIN_IDS = {"NodeUnschedulable": NODE_UNSCHEDULABLE, "NodeNumber": NODE_NUMBER}
+PLUGIN_NAMES = {v: k for k, v in PLUGIN_IDS.items()}
+MAX_NODE_SCORE = 100
+TAINT_KEY = "node.kubernetes.io/unschedulable"
+TAINT_EFFECT = "NoSchedule"
+
+
+# ---------------------------------------------------------------------------------------
+# Object-level restatement
+# ---------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class Toleration:
+    key: str = ""
+    operator: str = ""
+    value: str = ""
+    effect: str = ""
+
+
+@dataclass(frozen=True)
+class Node:
+    name: str
+    unschedulable: bool = False
+
+
+@dataclass(frozen=True)
+class Pod:
+    name: str
+    tolerations: tuple = ()
+    namespace: str = "default"
+
+
+@dataclass
+class PluginSet:
+    """Scheduler.filterPlugins / preScorePlugins / scorePlugins (initialize.go:25-27)."""
+    filters: list = field(default_factory=lambda: ["NodeUnschedulable"])
+    prescore: list = field(default_factory=lambda: ["NodeNumber"])
+    score: list = field(default_factory=lambda: ["NodeNumber"])
+    weights: list = field(default_factory=lambda: [1])
+    normalize: list = field(default_factory=lambda: [NORM_NONE])
+
+
+def atoi_last_byte(name: str) -> int:
+    """strconv.Atoi(name[len(name)-1:]) -> digit or -1 (error). Empty name panics in Go."""
+    b = name.encode("utf-8")
+    if not b:
+        raise ValueError("empty name: the reference panics on name[len(name)-1:]")
+    c = b[-1]
+    return c - 48 if 48 <= c <= 57 else -1
+
+
+def tolerates_taint(t: Toleration, key: str = TAINT_KEY, value: str = "", effect: str = TAINT_EFFECT) -> bool:
+    """(*v1.Toleration).ToleratesTaint (k8s.io/api v0.22.0 core/v1/toleration.go)."""
+    if t.effect and t.effect != effect:
+        return False
+    if t.key and t.key != key:
+        return False
+    if t.operator in ("", "Equal"):
+        return t.value == value
+    if t.operator == "Exists":
+        return True
+    return False
+
+
+def pod_tolerates_unschedulable(pod: Pod) -> bool:
+    """v1helper.TolerationsTolerateTaint(pod.Spec.Tolerations, unschedulable taint)."""
+    return any(tolerates_taint(t) for t in pod.tolerations)
+
+
+def list_order(nodes: list[Node]) -> list[Node]:
+    """Nodes().List() with no ResourceVersion: etcd key order == byte order of names."""
+    return sorted(nodes, key=lambda n: n.name.encode("utf-8"))
+
+
+def go_div(a: int, b: int) -> int:
+    """Go int64 division truncates toward zero."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def default_normalize(scores: list[int], reverse: bool) -> list[int]:
+    """helper.DefaultNormalizeScore (k8s.io/kubernetes v1.22.0, plugins/helper/normalize_score.go)."""
+    mx = 0
+    for s in scores:
+        if s > mx:
+            mx = s
+    if mx == 0:
+        return [MAX_NODE_SCORE] * len(scores) if reverse else list(scores)
+    out = []
+    for s in scores:
+        v = go_div(MAX_NODE_SCORE * s, mx)
+        out.append(MAX_NODE_SCORE - v if reverse else v)
+    return out
+
+
+def minmax_normalize(scores: list[int]) -> list[int]:
+    """Build extension: 100*(s-min)/(max-min) over the feasible list; 0 when max == min."""
+    if not scores:
+        return []
+    lo, hi = min(scores), max(scores)
+    return [0 if hi == lo else go_div((s - lo) * MAX_NODE_SCORE, hi - lo) for s in scores]
+
+
+def normalize(mode: int, scores: list[int]) -> list[int]:
+    if mode == NORM_DEFAULT:
+        return default_normalize(scores, False)
+    if mode == NORM_DEFAULT_REVERSE:
+        return default_normalize(scores, True)
+    if mode == NORM_MINMAX:
+        return minmax_normalize(scores)
+    return list(scores)
+
+
+@dataclass
+class ObjectResult:
+    pod: str
+    status: int
+    node: str | None = None
+    index: int = -1
+    score: int = 0
+    unschedulable_plugins: frozenset = frozenset()
+
+
+class ObjectOracle:
+    """scheduleOne's selection part over objects (minisched/minisched.go:32-87)."""
+
+    def __init__(self, plugins: PluginSet | None = None):
+        self.plugins = plugins or PluginSet()
+
+    def run_filter_plugins(self, pod: Pod, nodes: list[Node]):
+        feasible, diag = [], set()
+        tol = pod_tolerates_unschedulable(pod)
+        for i, n in enumerate(nodes):
+            ok = True
+            for name in self.plugins.filters:
+                if name == "NodeUnschedulable":
+                    ok = not (n.unschedulable and not tol)
+                if not ok:
+                    diag.add(name)
+                    break
+            if ok:
+                feasible.append(i)
+        return feasible, frozenset(diag)
+
+    def schedule_one(self, pod: Pod, nodes: list[Node]) -> ObjectResult:
+        feasible, diag = self.run_filter_plugins(pod, nodes)
+        if not feasible:
+            return ObjectResult(pod.name, FIT_ERROR, unschedulable_plugins=diag)
+        state = {}
+        for name in self.plugins.prescore:  # RunPreScorePlugins
+            if name == "NodeNumber":
+                d = atoi_last_byte(pod.name)
+                if d >= 0:
+                    state["PreScoreNodeNumber"] = d
+        per_plugin = []
+        for k, name in enumerate(self.plugins.score):  # RunScorePlugins
+            lst = []
+            for i in feasible:
+                if name == "NodeNumber":
+                    if "PreScoreNodeNumber" not in state:
+                        return ObjectResult(pod.name, SCORE_ERROR)
+                    nd = atoi_last_byte(nodes[i].name)
+                    lst.append(0 if nd < 0 else (10 if nd == state["PreScoreNodeNumber"] else 0))
+                else:
+                    raise ValueError(f"unknown score plugin {name}")
+            per_plugin.append(normalize(self.plugins.normalize[k], lst))
+        total = [sum(per_plugin[k][f] * self.plugins.weights[k] for k in range(len(per_plugin)))
+                 for f in range(len(feasible))]
+        best = 0
+        for f in range(1, len(feasible)):  # selectHost, first max
+            if total[f] > total[best]:
+                best = f
+        i = feasible[best]
+        return ObjectResult(pod.name, PLACED, nodes[i].name, i, total[best])
+
+    def schedule(self, pods: list[Pod], nodes: list[Node]) -> list[ObjectResult]:
+        ordered = list_order(nodes)
+        return [self.schedule_one(p, ordered) for p in pods]
+
+
+# ---------------------------------------------------------------------------------------
+# C restatement (ctypes)
+# ---------------------------------------------------------------------------------------
+_CLIB = None
+
+
+def clib():
+    global _CLIB
+    if _CLIB is None:
+        if not ORACLE_LIB.exists():
+            raise RuntimeError(f"{ORACLE_LIB} missing: run `make -C oracle`")
+        _CLIB = C.CDLL(str(ORACLE_LIB))
+    return _CLIB
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _plugin_arrays(plugins: PluginSet):
+    f = np.array([PLUGIN_IDS[x] for x in plugins.filters], np.int32)
+    pre = np.array([PLUGIN_IDS[x] for x in plugins.prescore], np.int32)
+    s = np.array([PLUGIN_IDS[x] for x in plugins.score], np.int32)
+    w = np.array(plugins.weights, np.int64)
+    nm = np.array(plugins.normalize, np.int32)
+    return f, pre, s, w, nm
+
+
+def c_schedule_batch(unsched, node_digit, pod_digit, pod_tol, plugins: PluginSet | None = None,
+                     norm_in_loop: bool = False, threads: int = 1):
+    """Batched oracle over SoA columns -> (idx int32, score int64, status int32, diag uint32)."""
+    plugins = plugins or PluginSet()
+    unsched = np.ascontiguousarray(unsched, np.uint8)
+    node_digit = np.ascontiguousarray(node_digit, np.int8)
+    pod_digit = np.ascontiguousarray(pod_digit, np.int8)
+    pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
+    n, p = len(unsched), len(pod_digit)
+    f, pre, s, w, nm = _plugin_arrays(plugins)
+    idx = np.empty(p, np.int32)
+    score = np.empty(p, np.int64)
+    status = np.empty(p, np.int32)
+    diag = np.zeros(p, np.uint32)
+    if threads > 1:
+        rc = clib().oracle_schedule_batch_soa_omp(
+            C.c_int32(n), _p(unsched), _p(node_digit), C.c_int32(p), _p(pod_digit), _p(pod_tol),
+            _p(f), C.c_int32(len(f)), _p(pre), C.c_int32(len(pre)), _p(s), _p(w), _p(nm),
+            C.c_int32(len(s)), C.c_int32(threads), _p(idx), _p(score), _p(status))
+    else:
+        rc = clib().oracle_schedule_batch_soa(
+            C.c_int32(n), _p(unsched), _p(node_digit), C.c_int32(p), _p(pod_digit), _p(pod_tol),
+            _p(f), C.c_int32(len(f)), _p(pre), C.c_int32(len(pre)), _p(s), _p(w), _p(nm),
+            C.c_int32(len(s)), C.c_int(1 if norm_in_loop else 0), _p(idx), _p(score), _p(status),
+            _p(diag))
+    if rc != 0:
+        raise RuntimeError(f"oracle failed rc={rc}")
+    return idx, score, status, diag
+
+
+def c_schedule_sequential(unsched, node_digit, pod_digit, pod_tol, plugins: PluginSet | None = None,
+                          max_pods: int = 0, counts=None):
+    plugins = plugins or PluginSet()
+    unsched = np.ascontiguousarray(unsched, np.uint8)
+    node_digit = np.ascontiguousarray(node_digit, np.int8)
+    pod_digit = np.ascontiguousarray(pod_digit, np.int8)
+    pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
+    n, p = len(unsched), len(pod_digit)
+    f, pre, s, w, nm = _plugin_arrays(plugins)
+    counts = np.zeros(max(n, 1), np.int32) if counts is None else np.ascontiguousarray(counts, np.int32)
+    idx = np.empty(p, np.int32)
+    score = np.empty(p, np.int64)
+    status = np.empty(p, np.int32)
+    rc = clib().oracle_schedule_sequential_soa(
+        C.c_int32(n), _p(unsched), _p(node_digit), C.c_int32(p), _p(pod_digit), _p(pod_tol),
+        _p(f), C.c_int32(len(f)), _p(pre), C.c_int32(len(pre)), _p(s), _p(w), _p(nm),
+        C.c_int32(len(s)), C.c_int32(max_pods), _p(counts), _p(idx), _p(score), _p(status))
+    if rc != 0:
+        raise RuntimeError(f"oracle failed rc={rc}")
+    return idx, score, status, counts[:n]

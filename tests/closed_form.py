@@ -1,0 +1,44 @@
+"""Independent closed-form checker (NOT reference code, NOT the oracle's loop structure).
+
+For the reference plugin set (filter NodeUnschedulable, prescore+score NodeNumber, weight w,
+no normalize, first-max tie-break) the outcome per pod is:
+  - no feasible node                       -> FIT_ERROR
+  - pod name suffix not a digit            -> SCORE_ERROR (NodeNumber has no PreScore state)
+  - else the first feasible node (List order) whose suffix digit equals the pod's, score 10*w;
+    if none, the first feasible node, score 0.
+Vectorised over pods by (digit, tolerates) class: it must never be used as the kernel
+(SURVEY.md §7 hazard "degenerate closed form"), only as a cross-check.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def closed_form(unsched, node_digit, pod_digit, pod_tol, weight: int = 1):
+    unsched = np.asarray(unsched, bool)
+    node_digit = np.asarray(node_digit, np.int16)
+    p = len(pod_digit)
+    idx = np.full(p, -1, np.int32)
+    score = np.zeros(p, np.int64)
+    status = np.zeros(p, np.int32)
+    n = len(unsched)
+    for tol in (0, 1):
+        feas = np.ones(n, bool) if tol else ~unsched
+        first_feas = int(np.argmax(feas)) if feas.any() else -1
+        for d in range(-1, 10):
+            sel = (np.asarray(pod_tol) == tol) & (np.asarray(pod_digit) == d)
+            if not sel.any():
+                continue
+            if first_feas < 0:
+                status[sel] = 1
+                continue
+            if d < 0:
+                status[sel] = 2
+                continue
+            m = feas & (node_digit == d)
+            if m.any():
+                idx[sel] = int(np.argmax(m))
+                score[sel] = 10 * weight
+            else:
+                idx[sel] = first_feas
+    return idx, score, status

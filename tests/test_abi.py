@@ -1,0 +1,56 @@
+"""The C-ABI library: loads, exports every declared symbol, fails loudly without a GPU."""
+from __future__ import annotations
+
+import ctypes as C
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared_symbols():
+    hdr = (ROOT / "include" / "minisched_hip.h").read_text()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(msh_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def test_header_matches_binding_table(msh):
+    assert declared_symbols() == sorted(msh._native.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol(msh):
+    lib = msh._native.lib()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_abi_version(msh):
+    assert msh._native.lib().msh_abi_version() == 1
+
+
+def test_no_device_is_an_error_not_a_fallback(msh):
+    if msh.device_count() > 0:
+        pytest.skip("GPU present")
+    h = C.c_void_p()
+    rc = msh._native.lib().msh_create(0, C.byref(h))
+    assert rc == msh._native.MSH_ERR_NO_DEVICE and not h.value
+    with pytest.raises(msh.MshError):
+        msh.DeviceContext(0)
+
+
+def test_null_ctx_is_invalid(msh):
+    lib = msh._native.lib()
+    assert lib.msh_upload_nodes(None, 0, None, None) == msh._native.MSH_ERR_INVALID
+    assert lib.msh_schedule_batch(None, 0, None, None, None, None, None) == msh._native.MSH_ERR_INVALID
+
+
+def test_product_package_does_not_import_oracle():
+    """The product path never imports / links the oracle (only build.py compiles it)."""
+    pkg = ROOT / "mini-kube-scheduler_amd"
+    pat = re.compile(r"^\s*(import\s+\S*oracle|from\s+\S*oracle\S*\s+import|#\s*include\s+\S*oracle)", re.M)
+    for f in list(pkg.glob("*.py")) + list((pkg / "csrc").glob("*")):
+        if f.is_file():
+            assert not pat.search(f.read_text(errors="ignore")), f
+    assert "oracle" not in (pkg / "build.py").read_text().split("def build_oracle")[0].split("SOURCES")[1]

@@ -1,0 +1,260 @@
+"""GPU parity: the gfx950 path (through the C-ABI) vs the CPU oracle, bit-exact.
+
+Every test here calls libminisched_hip.so on cuda:0 and compares idx / score / status with
+oracle/msh_oracle.c (the restatement of minisched/minisched.go:115-199,304-325) on the same
+seeded inputs; large sizes additionally against the independent closed form.
+"""
+from __future__ import annotations
+
+import itertools
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from closed_form import closed_form
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def _rand_case(rng, n, p, p_unsched=0.3, p_tol=0.2, p_nd_node=0.1, p_nd_pod=0.1):
+    unsched = (rng.random(n) < p_unsched).astype(np.uint8)
+    nd = rng.integers(0, 10, n).astype(np.int8)
+    nd[rng.random(n) < p_nd_node] = -1
+    pd = rng.integers(0, 10, p).astype(np.int8)
+    pd[rng.random(p) < p_nd_pod] = -1
+    pt = (rng.random(p) < p_tol).astype(np.uint8)
+    return unsched, nd, pd, pt
+
+
+def _plugins(oracle, filters, prescore, score, weight=1, norm=0):
+    return oracle.PluginSet(filters=list(filters), prescore=list(prescore), score=list(score),
+                            weights=[weight] * len(score), normalize=[norm] * len(score))
+
+
+def _set(ctx, msh, ps):
+    ctx.set_plugins(ps.filters, ps.prescore,
+                    [msh.ScorePluginConfig(s, w, msh.Normalize(m)) for s, w, m in zip(ps.score, ps.weights, ps.normalize)])
+
+
+def _assert_same(got, want, what=""):
+    gi, gs, gst = got
+    wi, ws, wst = want[:3]
+    bad = np.nonzero((gi != wi) | (gs != ws) | (gst != wst))[0]
+    assert bad.size == 0, (f"{what}: {bad.size} pods differ; first {bad[:5]}: got "
+                           f"{[(int(gi[b]), int(gs[b]), int(gst[b])) for b in bad[:5]]} want "
+                           f"{[(int(wi[b]), int(ws[b]), int(wst[b])) for b in bad[:5]]}")
+
+
+def test_scenario_golden(msh, gpu_ctx):
+    """sched.go:70-143: the reference's only known answer."""
+    fx = json.loads((GOLDEN / "scenario.json").read_text())
+    sched = msh.Scheduler(ctx=gpu_ctx)
+    for phase in fx["phases"]:
+        res = sched.schedule_batch([{"metadata": {"name": p["name"]}, "spec": {"tolerations": p.get("tolerations", [])}}
+                                    for p in fx["pods"]],
+                                   [{"metadata": {"name": n["name"]}, "spec": {"unschedulable": n["unschedulable"]}}
+                                    for n in phase["nodes"]])
+        for r, want in zip(res, phase["expect"]):
+            assert r.outcome.name == want["outcome"]
+            assert r.node_name == want.get("node")
+            assert sorted(r.unschedulable_plugins) == sorted(want.get("unschedulable_plugins", []))
+
+
+def test_golden_fixtures(msh, gpu_ctx, oracle):
+    for path in sorted(GOLDEN.glob("case_*.json")):
+        fx = json.loads(path.read_text())
+        ps = oracle.PluginSet(**fx["plugins"])
+        _set(gpu_ctx, msh, ps)
+        gpu_ctx.upload_nodes(np.array(fx["unsched"], np.uint8), np.array(fx["node_digit"], np.int8))
+        got = gpu_ctx.schedule_batch(np.array(fx["pod_digit"], np.int8), np.array(fx["pod_tol"], np.uint8))
+        want = (np.array(fx["idx"], np.int32), np.array(fx["score"], np.int64), np.array(fx["status"], np.int32))
+        _assert_same(got, want, path.name)
+
+
+PLUGIN_COMBOS = [
+    (["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"]),   # the reference
+    ([], ["NodeNumber"], ["NodeNumber"]),
+    (["NodeUnschedulable"], [], ["NodeNumber"]),               # score without prescore state
+    (["NodeUnschedulable"], ["NodeNumber"], []),
+    ([], [], []),
+]
+
+
+@pytest.mark.parametrize("combo", range(len(PLUGIN_COMBOS)))
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+@pytest.mark.parametrize("weight", [1, 3, 1 << 32])
+def test_plugin_sets_random(msh, gpu_ctx, oracle, combo, norm, weight):
+    rng = np.random.default_rng(1000 * combo + 10 * norm + (weight % 97))
+    f, pre, s = PLUGIN_COMBOS[combo]
+    ps = _plugins(oracle, f, pre, s, weight, norm)
+    _set(gpu_ctx, msh, ps)
+    for n, p in [(1, 5), (70, 300), (1000, 2000)]:
+        u, nd, pd, pt = _rand_case(rng, n, p)
+        gpu_ctx.upload_nodes(u, nd)
+        got = gpu_ctx.schedule_batch(pd, pt)
+        want = oracle.c_schedule_batch(u, nd, pd, pt, ps)
+        _assert_same(got, want, f"combo={combo} norm={norm} w={weight} n={n} p={p}")
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, 63, 64, 65, 1023, 1024, 1025, 5000, 16384, 16385, 40000])
+def test_node_sizes(msh, gpu_ctx, oracle, n):
+    """Empty / ragged / tile-boundary / multi-tile node tables (LDS tile = 16384 nodes)."""
+    rng = np.random.default_rng(n)
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = _rand_case(rng, n, 777)
+    gpu_ctx.upload_nodes(u, nd)
+    got = gpu_ctx.schedule_batch(pd, pt)
+    _assert_same(got, oracle.c_schedule_batch(u, nd, pd, pt, ps), f"n={n}")
+    _assert_same(got, closed_form(u, nd, pd, pt), f"closed form n={n}")
+
+
+@pytest.mark.parametrize("norm", [0, 2, 3])
+def test_multitile_normalize(msh, gpu_ctx, oracle, norm):
+    rng = np.random.default_rng(77 + norm)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = _rand_case(rng, 33000, 3000, p_unsched=0.9)
+    gpu_ctx.upload_nodes(u, nd)
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps), f"norm={norm}")
+
+
+@pytest.mark.parametrize("p", [0, 1, 2, 63, 64, 65, 1000, 4097, 250_000])
+def test_pod_sizes(msh, gpu_ctx, oracle, p):
+    rng = np.random.default_rng(p + 5)
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = _rand_case(rng, 300, p)
+    gpu_ctx.upload_nodes(u, nd)
+    got = gpu_ctx.schedule_batch(pd, pt)
+    _assert_same(got, oracle.c_schedule_batch(u, nd, pd, pt, ps), f"p={p}")
+
+
+def test_all_unschedulable_and_tolerations(msh, gpu_ctx, oracle):
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    n = 500
+    u = np.ones(n, np.uint8)
+    nd = (np.arange(n) % 10).astype(np.int8)
+    pd = (np.arange(200) % 11 - 1).astype(np.int8)
+    pt = (np.arange(200) % 3 == 0).astype(np.uint8)
+    gpu_ctx.upload_nodes(u, nd)
+    got = gpu_ctx.schedule_batch(pd, pt)
+    want = oracle.c_schedule_batch(u, nd, pd, pt, ps)
+    _assert_same(got, want, "all unschedulable")
+    assert (got[2][pt == 0] == 1).all()  # FitError for non-tolerating pods
+
+
+def test_c2_full(msh, gpu_ctx, oracle, synth):
+    """BASELINE config C2: 1k nodes x 10k pods, plus a 100%-unschedulable block."""
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = synth.make_soa(1000, 10_000)
+    gpu_ctx.upload_nodes(u, nd)
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps), "C2")
+    u2 = np.ones_like(u)
+    gpu_ctx.upload_nodes(u2, nd)
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u2, nd, pd, pt, ps), "C2 all-unsched")
+
+
+def test_c3_full_and_weight3(msh, gpu_ctx, oracle, synth):
+    """BASELINE config C3: 5k nodes x 100k pods; weight 3 must place identically."""
+    u, nd, pd, pt = synth.make_soa(5000, 100_000)
+    ps1 = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps1)
+    gpu_ctx.upload_nodes(u, nd)
+    got1 = gpu_ctx.schedule_batch(pd, pt)
+    _assert_same(got1, oracle.c_schedule_batch(u, nd, pd, pt, ps1, threads=8), "C3")
+    _assert_same(got1, closed_form(u, nd, pd, pt), "C3 closed form")
+    ps3 = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, 0)
+    _set(gpu_ctx, msh, ps3)
+    got3 = gpu_ctx.schedule_batch(pd, pt)
+    assert (got3[0] == got1[0]).all() and (got3[2] == got1[2]).all()
+    assert (got3[1] == 3 * got1[1]).all()
+
+
+@pytest.mark.parametrize("max_pods", [0, 1, 3])
+@pytest.mark.parametrize("n", [1, 70, 1000, 5000, 8192])
+def test_sequential(msh, gpu_ctx, oracle, n, max_pods):
+    rng = np.random.default_rng(n + max_pods)
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = _rand_case(rng, n, 3000)
+    gpu_ctx.upload_nodes(u, nd)
+    got = gpu_ctx.schedule_sequential(pd, pt, max_pods)
+    want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, max_pods)
+    _assert_same(got, (want_i, want_s, want_st), f"seq n={n} max={max_pods}")
+    assert (gpu_ctx.node_pod_counts() == want_counts).all()
+    if max_pods == 0:
+        gpu_ctx.reset_node_pod_counts()
+        _assert_same(got, gpu_ctx.schedule_batch(pd, pt), "seq == batch")
+
+
+def test_sequential_commit_callback(msh, gpu_ctx, oracle):
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = _rand_case(np.random.default_rng(3), 200, 500)
+    gpu_ctx.upload_nodes(u, nd)
+    seen = []
+    idx, _, status = gpu_ctx.schedule_sequential(pd, pt, 0, on_commit=lambda j, i, s: seen.append((j, i)))
+    assert seen == [(j, int(idx[j])) for j in range(len(pd)) if status[j] == 0]
+
+
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+def test_node_shards_merge(msh, gpu_ctx, oracle, norm):
+    """Node-sharded mode: per-shard keys, element-wise MAX, device decode == unsharded."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(11 + norm)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, norm)
+    u, nd, pd, pt = _rand_case(rng, 9000, 4000)
+    want = oracle.c_schedule_batch(u, nd, pd, pt, ps)
+    dev = torch.device("cuda:0")
+    d_pd = torch.from_numpy(pd).to(dev)
+    d_pt = torch.from_numpy(pt).to(dev)
+    p = len(pd)
+    merged = torch.zeros(2 * p, dtype=torch.int64, device=dev)
+    bounds = [0, 1234, 5000, 5001, 9000]
+    ctxs = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        c = msh.DeviceContext(0)
+        _set(c, msh, ps)
+        c.upload_nodes(u[a:b], nd[a:b])
+        keys = torch.empty(2 * p, dtype=torch.int64, device=dev)
+        c.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), a, keys.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+        merged = torch.maximum(merged, keys)
+        ctxs.append(c)
+    oi = torch.empty(p, dtype=torch.int32, device=dev)
+    osc = torch.empty(p, dtype=torch.int64, device=dev)
+    ost = torch.empty(p, dtype=torch.int32, device=dev)
+    ctxs[0].decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), merged.data_ptr(), oi.data_ptr(),
+                               osc.data_ptr(), ost.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"shards norm={norm}")
+    for c in ctxs:
+        c.close()
+
+
+def test_determinism_device_entry(msh, gpu_ctx, oracle, synth):
+    torch = pytest.importorskip("torch")
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = synth.make_soa(5000, 50_000)
+    gpu_ctx.upload_nodes(u, nd)
+    dev = torch.device("cuda:0")
+    d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+    outs = []
+    for _ in range(3):
+        oi = torch.empty(len(pd), dtype=torch.int32, device=dev)
+        osc = torch.empty(len(pd), dtype=torch.int64, device=dev)
+        ost = torch.empty(len(pd), dtype=torch.int32, device=dev)
+        gpu_ctx.schedule_batch_device(len(pd), d_pd.data_ptr(), d_pt.data_ptr(), oi.data_ptr(), osc.data_ptr(),
+                                      ost.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()))
+    for o in outs[1:]:
+        _assert_same(o, outs[0], "repeat")
+    _assert_same(outs[0], oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8), "device entry")

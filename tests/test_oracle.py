@@ -1,0 +1,94 @@
+"""The oracle pinned before it is trusted: scenario known answer, fixtures, closed form."""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from closed_form import closed_form
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def test_scenario_known_answer(oracle):
+    """sched.go:70-143 — the reference's only end-to-end known answer."""
+    fx = json.loads((GOLDEN / "scenario.json").read_text())
+    oo = oracle.ObjectOracle()
+    names = {0: "PLACED", 1: "FIT_ERROR", 2: "SCORE_ERROR"}
+    for ph in fx["phases"]:
+        res = oo.schedule([oracle.Pod(p["name"]) for p in fx["pods"]],
+                          [oracle.Node(n["name"], n["unschedulable"]) for n in ph["nodes"]])
+        for r, e in zip(res, ph["expect"]):
+            assert names[r.status] == e["outcome"]
+            assert r.node == e.get("node")
+            assert sorted(r.unschedulable_plugins) == sorted(e.get("unschedulable_plugins", []))
+
+
+@pytest.mark.parametrize("path", sorted(GOLDEN.glob("case_*.json")), ids=lambda p: p.stem)
+def test_fixture_both_restatements(oracle, path):
+    fx = json.loads(path.read_text())
+    ps = oracle.PluginSet(**fx["plugins"])
+    # C restatement on the SoA columns
+    i, s, st, _ = oracle.c_schedule_batch(np.array(fx["unsched"], np.uint8), np.array(fx["node_digit"], np.int8),
+                                          np.array(fx["pod_digit"], np.int8), np.array(fx["pod_tol"], np.uint8), ps)
+    assert i.tolist() == fx["idx"] and s.tolist() == fx["score"] and st.tolist() == fx["status"]
+    # object restatement on names / tolerations
+    T = oracle.Toleration
+    pods = [oracle.Pod(p["name"], tuple(T(**t) for t in p["tolerations"])) for p in fx["pods"]]
+    nodes = [oracle.Node(n["name"], n["unschedulable"]) for n in fx["nodes"]]
+    res = oracle.ObjectOracle(ps).schedule(pods, nodes)
+    assert [r.node for r in res] == fx["node"]
+    assert [r.score for r in res] == fx["score"]
+    assert [sorted(r.unschedulable_plugins) for r in res] == fx["unschedulable_plugins"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_c_oracle_vs_closed_form(oracle, seed):
+    rng = np.random.default_rng(seed)
+    n, p = int(rng.integers(0, 700)), int(rng.integers(1, 900))
+    u = (rng.random(n) < rng.random()).astype(np.uint8)
+    nd = rng.integers(-1, 10, n).astype(np.int8)
+    pd = rng.integers(-1, 10, p).astype(np.int8)
+    pt = (rng.random(p) < 0.3).astype(np.uint8)
+    w = int(rng.integers(1, 5))
+    got = oracle.c_schedule_batch(u, nd, pd, pt, oracle.PluginSet(weights=[w]))
+    want = closed_form(u, nd, pd, pt, w)
+    for g, e in zip(got[:3], want):
+        assert (g == e).all()
+
+
+def test_omp_matches_scalar(oracle, synth):
+    u, nd, pd, pt = synth.make_soa(1000, 20_000)
+    a = oracle.c_schedule_batch(u, nd, pd, pt)
+    b = oracle.c_schedule_batch(u, nd, pd, pt, threads=4)
+    for x, y in zip(a[:3], b[:3]):
+        assert (x == y).all()
+
+
+def test_sequential_without_capacity_equals_batch(oracle, synth):
+    u, nd, pd, pt = synth.make_soa(300, 3000)
+    a = oracle.c_schedule_batch(u, nd, pd, pt)
+    i, s, st, counts = oracle.c_schedule_sequential(u, nd, pd, pt)
+    assert (a[0] == i).all() and (a[1] == s).all() and (a[2] == st).all()
+    assert counts.sum() == (st == 0).sum()
+
+
+def test_sequential_capacity_spreads(oracle):
+    u = np.zeros(20, np.uint8)
+    nd = (np.arange(20) % 10).astype(np.int8)
+    pd = np.full(50, 3, np.int8)
+    pt = np.zeros(50, np.uint8)
+    i, s, st, counts = oracle.c_schedule_sequential(u, nd, pd, pt, max_pods=2)
+    assert counts.max() <= 2 and (st == 0).sum() == 40 and (st == 1).sum() == 10
+
+
+def test_norm_in_loop_quirk_is_identity_for_nodenumber(oracle, synth):
+    """minisched.go:178-183 calls NormalizeScore inside the node loop; NodeNumber has none
+    (nodenumber.go:98-100), so the quirk cannot change the reference plugin set's results."""
+    u, nd, pd, pt = synth.make_soa(200, 500)
+    a = oracle.c_schedule_batch(u, nd, pd, pt, norm_in_loop=False)
+    b = oracle.c_schedule_batch(u, nd, pd, pt, norm_in_loop=True)
+    for x, y in zip(a[:3], b[:3]):
+        assert (x == y).all()
