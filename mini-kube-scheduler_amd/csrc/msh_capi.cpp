@@ -282,7 +282,9 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
   if (n < 0 || n > msh::MAX_NODES) return fail(c, MSH_ERR_INVALID, "node count outside [0, 2^24-2]");
   if (n > 0 && (!unsched || !digit)) return fail(c, MSH_ERR_INVALID, "null node arrays");
   DeviceGuard g(c->device);
-  const int32_t n_pad = ((n + NODE_PAD - 1) / NODE_PAD) * NODE_PAD;
+  // Padded to whole 16-chunk blocks, and never empty: an empty cluster is a table of
+  // padding nodes (infeasible for every pod), so every pod gets FitError from the kernel.
+  const int32_t n_pad = std::max(((n + NODE_PAD - 1) / NODE_PAD) * NODE_PAD, NODE_PAD);
   if ((size_t)n_pad > c->node_cap || c->d_kn == nullptr) {
     free_nodes(c);
     const size_t cap = std::max<size_t>((size_t)n_pad, NODE_PAD);

@@ -459,6 +459,11 @@ hipError_t launch_batch_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
     return hipErrorInvalidValue;
   }
   const size_t lds = (size_t)tile_chunks * WAVE * LDS_BYTES_PER_NODE;
+  if (lds > 64 * 1024) {
+    hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (ea != hipSuccess) return ea;
+  }
   int occ = 0;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BATCH_THREADS, lds);
   if (e != hipSuccess) return e;
