@@ -97,12 +97,37 @@ _SIGS = {
 }
 
 _LIB: C.CDLL | None = None
+_HIP_RUNTIME: C.CDLL | None = None
+
+
+def _share_hip_runtime_with_torch() -> None:
+    """Make this library and PyTorch share ONE HIP runtime in the process.
+
+    PyTorch-ROCm wheels bundle their own libamdhip64 (SONAME libamdhip64.so.7, the same as
+    /opt/rocm's). If libminisched_hip.so were loaded first it would pull in /opt/rocm's copy
+    and torch would later load its bundled copy: two runtimes in one process, and torch then
+    reports "No HIP GPUs are available". Loading torch's runtime RTLD_GLOBAL first makes our
+    NEEDED libamdhip64.so.7 resolve to it (and torch's later load reuse it), so device pointers
+    and streams are interchangeable. Without torch installed, /opt/rocm's runtime is used.
+    Set MSH_HIP_RUNTIME=system to skip.
+    """
+    global _HIP_RUNTIME
+    if _HIP_RUNTIME is not None or os.environ.get("MSH_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    cand = Path(list(spec.submodule_search_locations)[0]) / "lib" / "libamdhip64.so"
+    if cand.exists():
+        _HIP_RUNTIME = C.CDLL(str(cand), mode=C.RTLD_GLOBAL)
 
 
 def lib() -> C.CDLL:
     """Load libminisched_hip.so (in-tree). Raises if it is missing: no fallback path."""
     global _LIB
     if _LIB is None:
+        _share_hip_runtime_with_torch()
         if not LIB_PATH.exists():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with __graft_entry__.build() "

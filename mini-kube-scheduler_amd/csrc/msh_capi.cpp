@@ -37,7 +37,7 @@ struct msh_ctx {
   int32_t n_nodes = 0, n_pad = 0;
   uint8_t* d_unsched = nullptr;
   int8_t* d_digit = nullptr;
-  uint32_t* d_kn = nullptr;
+  uint32_t* d_c0 = nullptr;
   uint8_t* d_dig = nullptr;
   unsigned long long* d_mask = nullptr;
   uint32_t* d_ball = nullptr;
@@ -76,9 +76,9 @@ int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
   } while (0)
 
 void free_nodes(msh_ctx* c) {
-  hipFree(c->d_unsched); hipFree(c->d_digit); hipFree(c->d_kn); hipFree(c->d_dig);
+  hipFree(c->d_unsched); hipFree(c->d_digit); hipFree(c->d_c0); hipFree(c->d_dig);
   hipFree(c->d_mask); hipFree(c->d_counts);
-  c->d_unsched = nullptr; c->d_digit = nullptr; c->d_kn = nullptr; c->d_dig = nullptr;
+  c->d_unsched = nullptr; c->d_digit = nullptr; c->d_c0 = nullptr; c->d_dig = nullptr;
   c->d_mask = nullptr; c->d_counts = nullptr;
   c->node_cap = 0;
 }
@@ -125,7 +125,7 @@ int prepare(msh_ctx* c, hipStream_t s) {
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (!c->dirty) return MSH_OK;
   hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad,
-                                       c->pp.has_nu_filter, c->d_kn, c->d_dig, c->d_mask,
+                                       c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_mask,
                                        c->d_ball, s);
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
   c->dirty = false;
@@ -146,7 +146,7 @@ int ensure_partial(msh_ctx* c, int32_t p) {
 
 msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t* pt) {
   msh::BatchArgs a{};
-  a.kn = c->d_kn;
+  a.c0 = c->d_c0;
   a.dig = c->d_dig;
   a.n_nodes = c->n_nodes;
   a.n_chunks = c->n_pad / 64;
@@ -285,12 +285,12 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
   // Padded to whole 16-chunk blocks, and never empty: an empty cluster is a table of
   // padding nodes (infeasible for every pod), so every pod gets FitError from the kernel.
   const int32_t n_pad = std::max(((n + NODE_PAD - 1) / NODE_PAD) * NODE_PAD, NODE_PAD);
-  if ((size_t)n_pad > c->node_cap || c->d_kn == nullptr) {
+  if ((size_t)n_pad > c->node_cap || c->d_c0 == nullptr) {
     free_nodes(c);
     const size_t cap = std::max<size_t>((size_t)n_pad, NODE_PAD);
     MSH_HIP(c, hipMalloc(&c->d_unsched, cap));
     MSH_HIP(c, hipMalloc(&c->d_digit, cap));
-    MSH_HIP(c, hipMalloc(&c->d_kn, cap * sizeof(uint32_t)));
+    MSH_HIP(c, hipMalloc(&c->d_c0, cap * sizeof(uint32_t)));
     MSH_HIP(c, hipMalloc(&c->d_dig, cap));
     MSH_HIP(c, hipMalloc(&c->d_mask, 2 * (cap / 64) * sizeof(unsigned long long)));
     MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
@@ -376,7 +376,7 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   int rc = prepare(c, s);
   if (rc != MSH_OK) return rc;
   msh::SeqArgs a{};
-  a.kn = c->d_kn;
+  a.c0 = c->d_c0;
   a.dig = c->d_dig;
   a.n_nodes = c->n_nodes;
   a.n_chunks = c->n_pad / 64;

@@ -21,6 +21,11 @@ constexpr int BATCH_THREADS = 256;               // 4 waves per workgroup
 constexpr int SEQ_THREADS = 1024;                // 16 waves, one workgroup
 constexpr int SEQ_MAX_CHUNKS_PER_WAVE = 32;      // sequential mode: node table in registers
 constexpr int64_t GKEY_MAX = 0xFFFFFFFFll;       // global (sharded) key = GKEY_MAX - global_idx
+// Node "cost" for the first-match search: idx if the node is feasible for the pod class,
+// NOFIT otherwise. cost + |D - pd| * 2^24 (one v_sad_u32) is < 2^24 exactly for feasible
+// nodes whose digit equals the pod's; its unsigned min is the first such node in List order.
+constexpr uint32_t NOFIT = 0x80000000u;
+constexpr uint32_t MATCH_LIMIT = 1u << 24;
 
 // Per-ctx plugin set as the kernels see it (minisched/initialize.go:80-123 lists).
 struct PluginParams {
@@ -43,11 +48,11 @@ struct DeviceInfo {
 
 // ---- launchers (msh_kernels.hip) ----
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
-                            int32_t n_pad, int32_t has_nu, uint32_t* d_kn, uint8_t* d_dig,
+                            int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
                             unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s);
 
 struct BatchArgs {
-  const uint32_t* kn;        // [n_pad] non-tolerating-class key per node (0 = infeasible)
+  const uint32_t* c0;        // [n_pad] class-0 node cost: idx if feasible for !tolerating pods, else NOFIT
   const uint8_t* dig;        // [n_pad] node digit 0..9 / 0xFF
   int32_t n_nodes, n_chunks; // n_chunks = n_pad / 64
   const int8_t* pod_digit;
@@ -75,7 +80,7 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
                               hipStream_t s);
 
 struct SeqArgs {
-  const uint32_t* kn;
+  const uint32_t* c0;
   const uint8_t* dig;
   int32_t n_nodes, n_chunks;
   const int8_t* pod_digit;

@@ -7,55 +7,79 @@
 //   selectHost         minisched/minisched.go:304-325  (argmax; ties -> lowest index here)
 //
 // Layout: "lanes = nodes". A wave holds 64 consecutive nodes of a chunk in its lanes and a
-// group of G pods in scalar registers; every (pod, node) pair is one lane-op sequence:
-//   feasible (NodeUnschedulable) . score class (NodeNumber digit compare) . first-max.
+// group of up to G pods in scalar registers; every (pod, node) pair is evaluated by lane ops.
 // Stages (north_star):
 //   1. feasibility bitmask per pod class with wavefront __ballot      -> node_prep_kernel
 //   2. int64 score with the plugin weight fused                        -> decode_pod
-//   3. per-pod normalisation (DEFAULT / REVERSE / MINMAX: needs the per-pod class extent,
-//      i.e. the min/max raw score over the feasible list)               -> bm/bx keys + decode
-//   4. argmax with a fixed lowest-index tie-break: per-lane unsigned max of
-//      key = KMAX - idx, then a wave-wide DPP max reduction              -> wave_max_u32
+//   3. per-pod normalisation (DEFAULT / REVERSE / MINMAX need the per-pod extent of the
+//      raw scores over the feasible list: first feasible match / non-match) -> KX path + decode
+//   4. argmax with a fixed lowest-index tie-break, wave-wide DPP reduction -> wave_reduce
 //   5. node-table tile staged in LDS once per workgroup and re-read for every pod group
+//
+// The score of a pair under the reference plugin set is 10*w if the node is feasible and
+// its suffix digit equals the pod's, else 0, so selectHost's first max is "first feasible
+// match, else first feasible". The IDENT path evaluates each pair with ONE v_sad_u32:
+//     t = |(D << 24) - (pd << 24)| + cost,  cost = idx (feasible) | NOFIT (infeasible)
+// t < 2^24 iff feasible AND digits equal, and then t == idx: the unsigned min over nodes is
+// the first feasible match (v_min3_u32 folds two pairs per instruction): 1.5 VALU per 64
+// pairs, no VCC/SGPR lane masks (no VALU->SGPR->VALU hazard wait states).
 // See DESIGN.md for the roofline / instruction budget of each kernel.
 #include "msh_internal.h"
 
 namespace msh {
 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp_max(uint32_t v) {
-  // Lanes whose row is masked off keep `old` = 0, the identity of an unsigned max.
-  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
-  return umax(v, t);
+// |d - p| + c in ONE v_sad_u32 (p wave-uniform, read from an SGPR). Written as asm: the
+// backend does match the generic form, but reassociates it into min/max/sub/add (4 VALU)
+// whenever c is loop-invariant.
+__device__ __forceinline__ uint32_t sad(uint32_t d, uint32_t p, uint32_t c) {
+  uint32_t r;
+  asm("v_sad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(d), "s"(p), "v"(c));
+  return r;
 }
 
-// Wave-wide unsigned max over 64 lanes; the result is returned as a wave-uniform value.
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-  v = dpp_max<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
-  v = dpp_max<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
-  v = dpp_max<0x141, 0xF>(v);  // row_half_mirror
-  v = dpp_max<0x140, 0xF>(v);  // row_mirror      -> every lane of a 16-lane row holds its max
-  v = dpp_max<0x142, 0xA>(v);  // row_bcast:15    -> rows 1,3 fold in rows 0,2
-  v = dpp_max<0x143, 0xC>(v);  // row_bcast:31    -> rows 2,3 fold in row 1 (= rows 0..1)
+template <bool IS_MIN, int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_step(uint32_t v) {
+  // Lanes whose row is masked off keep `old`: the identity of the reduction.
+  const int ident = IS_MIN ? -1 : 0;
+  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(ident, (int)v, CTRL, ROW_MASK, 0xF, false);
+  return IS_MIN ? umin(v, t) : umax(v, t);
+}
+
+// Wave-wide unsigned max (IS_MIN=false) / min (IS_MIN=true); result is wave-uniform.
+template <bool IS_MIN>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
+  v = dpp_step<IS_MIN, 0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = dpp_step<IS_MIN, 0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = dpp_step<IS_MIN, 0x141, 0xF>(v);  // row_half_mirror
+  v = dpp_step<IS_MIN, 0x140, 0xF>(v);  // row_mirror   -> each 16-lane row holds its result
+  v = dpp_step<IS_MIN, 0x142, 0xA>(v);  // row_bcast:15 -> rows 1,3 fold in rows 0,2
+  v = dpp_step<IS_MIN, 0x143, 0xC>(v);  // row_bcast:31 -> rows 2,3 fold in row 1 (= rows 0..1)
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return wave_reduce<true>(v); }
+
+// first-match cost (idx, or >= 2^24 when none) -> key (KMAX - idx, 0 when none)
+__device__ __forceinline__ uint32_t cost_to_key(uint32_t c) { return c < MATCH_LIMIT ? KMAX - c : 0u; }
 
 // ---------------------------------------------------------------------------------------
 // Stage 1: node table preparation + feasibility bitmask (once per upload / plugin change).
 // For the only filter, NodeUnschedulable (upstream v1.22.0), feasibility depends on the
 // pod only through "tolerates the unschedulable taint", so there are exactly two pod
 // classes: 0 = does not tolerate, 1 = tolerates. Class 1 is feasible on every node.
-//   kn[i]  = KMAX - i if node i is feasible for class 0, else 0
+//   c0[i]  = i if node i is feasible for class 0, else NOFIT
 //   dig[i] = NodeNumber node digit (Atoi of the last byte, nodenumber.go:81-87) or 0xFF
 //   mask[c][chunk] = __ballot(feasible for class c)   (64-node feasibility bitmask)
-//   ball[c] = key of the first feasible node of class c (0 = none)
+//   ball[c] = key (KMAX - idx) of the first feasible node of class c (0 = none)
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restrict__ unsched,
                                                         const int8_t* __restrict__ digit,
                                                         int32_t n, int32_t n_pad, int32_t has_nu,
-                                                        uint32_t* __restrict__ kn,
+                                                        uint32_t* __restrict__ c0,
                                                         uint8_t* __restrict__ dig,
                                                         unsigned long long* __restrict__ mask,
                                                         uint32_t* __restrict__ ball) {
@@ -67,7 +91,7 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
   // NodeUnschedulable.Filter: Spec.Unschedulable && !tolerates -> UnschedulableAndUnresolvable
   const bool feas0 = valid && !(has_nu && u);
   const bool feas1 = valid;
-  kn[i] = feas0 ? (KMAX - (uint32_t)i) : 0u;
+  c0[i] = feas0 ? (uint32_t)i : NOFIT;
   dig[i] = (d >= 0 && d <= 9) ? (uint8_t)d : (uint8_t)DIGIT_NONE;
   const unsigned long long m0 = __ballot(feas0);
   const unsigned long long m1 = __ballot(feas1);
@@ -134,18 +158,15 @@ __device__ __forceinline__ int64_t key_to_idx(uint32_t k) {
 // pod range, walked in windows of 64 pods (one pod per lane). Within a window the pods are
 // split by class with __ballot (class = tolerates the unschedulable taint), and each class
 // is processed in groups of up to G pods whose digits sit in SGPRs. For every R-chunk
-// sub-tile the wave loads R node records per lane (digit D, class key K), then for every
-// pod g of the group:
-//     m = (D == pod digit);  bm[g] = max(bm[g], m ? K : 0)   [2.5 VALU per 64 pairs]
-// (+ bx[g] = max(bx[g], m ? 0 : K) when the normalize mode needs the non-match extent).
-// K is KMAX-idx for nodes feasible for the class, else 0, so the unsigned max is the
-// first feasible match in List order. Results land in the pod's lane (lane-select) and
-// are decoded and stored once per window (coalesced).
+// sub-tile the wave loads R node records per lane from LDS, then for every pod of the group
+//   IDENT:  bm = min3(bm, sad(D0, pd, C0), sad(D1, pd, C1))       [1.5 VALU / 64 pairs]
+//   KX:     m = (D == pd); bm = max(bm, m ? K : 0); bx = max(bx, m ? 0 : K)   [5 VALU]
+// Results land in the pod's lane (lane select) and are decoded and stored once per window.
 // ---------------------------------------------------------------------------------------
 template <int R, int G, bool NEED_KX, bool SHARD>
 __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32_t tile_chunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-  uint32_t* lds_k = reinterpret_cast<uint32_t*>(lds_raw);
+  uint32_t* lds_c = reinterpret_cast<uint32_t*>(lds_raw);
   uint8_t* lds_d = lds_raw + (size_t)tile_chunks * WAVE * sizeof(uint32_t);
 
   constexpr int WPG = BATCH_THREADS / WAVE;
@@ -164,15 +185,15 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
     const int32_t nc = min(tile_chunks, a.n_chunks - c0t);  // multiple of 16 (host pads)
     if (t > 0) __syncthreads();
     {
-      const uint4* src = reinterpret_cast<const uint4*>(a.kn + (size_t)c0t * WAVE);
-      uint4* dst = reinterpret_cast<uint4*>(lds_k);
+      const uint4* src = reinterpret_cast<const uint4*>(a.c0 + (size_t)c0t * WAVE);
+      uint4* dst = reinterpret_cast<uint4*>(lds_c);
       for (int32_t i = threadIdx.x; i < nc * (WAVE / 4); i += BATCH_THREADS) dst[i] = src[i];
       const uint4* srcd = reinterpret_cast<const uint4*>(a.dig + (size_t)c0t * WAVE);
       uint4* dstd = reinterpret_cast<uint4*>(lds_d);
       for (int32_t i = threadIdx.x; i < nc * (WAVE / 16); i += BATCH_THREADS) dstd[i] = srcd[i];
     }
     __syncthreads();
-    const uint32_t ktbase = KMAX - (uint32_t)(c0t * WAVE + lane);
+    const uint32_t idx_base = (uint32_t)(c0t * WAVE + lane);  // global node index of chunk 0
     const bool last_tile = (t == ntiles - 1);
 
     for (int32_t w0 = p0; w0 < p1; w0 += WAVE) {
@@ -184,7 +205,7 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
         pdv = (d >= 0 && d <= 9) ? (uint32_t)d : POD_DIGIT_NONE;
         tolv = a.pod_tol[w0 + lane] ? 1u : 0u;
       }
-      uint32_t res_m = 0u, res_x = 0u;
+      uint32_t res_m = 0u, res_x = 0u;  // keys (KMAX - idx, 0 = none)
       if (t > 0 && act) {
         res_m = a.partial[w0 + lane];
         if (NEED_KX) res_x = a.partial[(size_t)a.n_pods + w0 + lane];
@@ -215,44 +236,49 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
           uint32_t bm[G], bx[G];
 #pragma unroll
           for (int g = 0; g < G; ++g) {
-            bm[g] = 0u;
+            bm[g] = NEED_KX ? 0u : 0xFFFFFFFFu;
             bx[g] = 0u;
           }
-          const uint32_t* pk = lds_k + lane;
+          const uint32_t* pc = lds_c + lane;
           const uint8_t* pdg = lds_d + lane;
           for (int32_t c0 = 0; c0 < nc; c0 += R) {
-            uint32_t D[R], K[R];
+            uint32_t D[R], C[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               const int32_t c = c0 + r;
-              D[r] = pdg[c * WAVE];
-              if (cls == 0) {
-                K[r] = pk[c * WAVE];
+              const uint32_t d = pdg[c * WAVE];
+              // class 0: staged cost; class 1 (tolerates): every real node is feasible.
+              // Padding nodes carry digit 0xFF and never match.
+              const uint32_t cost = (cls == 0) ? pc[c * WAVE] : idx_base + (uint32_t)(c * WAVE);
+              if (NEED_KX) {
+                D[r] = d;
+                const bool feas = (cls == 0) ? cost < MATCH_LIMIT : (cost < (uint32_t)a.n_nodes);
+                C[r] = feas ? KMAX - cost : 0u;  // class key
               } else {
-                uint32_t kt = ktbase - (uint32_t)(c * WAVE);
-                if (NEED_KX) kt = ((c0t + c) * WAVE + lane < a.n_nodes) ? kt : 0u;
-                K[r] = kt;  // padding nodes carry digit 0xFF, so they never match
+                D[r] = d << 24;
+                C[r] = cost;
               }
             }
 #pragma unroll
             for (int g = 0; g < G; ++g) {
               if (g < cnt) {
-                const uint32_t pd = spd[g];
+                if (NEED_KX) {
+                  const uint32_t pd = spd[g];
 #pragma unroll
-                for (int r = 0; r < R; r += 2) {
-                  // Two selects then one v_max3_u32: 2.5 VALU per 64 (pod, node) pairs. The
-                  // empty asm keeps the selects materialised (otherwise instcombine folds
-                  // max(bm, m ? K : 0) into select(m, max(bm, K), bm): 3 VALU, one serial chain).
-                  uint32_t t0 = (D[r] == pd) ? K[r] : 0u;
-                  uint32_t t1 = (D[r + 1] == pd) ? K[r + 1] : 0u;
-                  asm("" : "+v"(t0), "+v"(t1));
-                  bm[g] = umax(umax(bm[g], t0), t1);
-                  if (NEED_KX) {
-                    uint32_t x0 = (D[r] == pd) ? 0u : K[r];
-                    uint32_t x1 = (D[r + 1] == pd) ? 0u : K[r + 1];
-                    asm("" : "+v"(x0), "+v"(x1));
+                  for (int r = 0; r < R; r += 2) {
+                    uint32_t t0 = (D[r] == pd) ? C[r] : 0u;
+                    uint32_t t1 = (D[r + 1] == pd) ? C[r + 1] : 0u;
+                    uint32_t x0 = (D[r] == pd) ? 0u : C[r];
+                    uint32_t x1 = (D[r + 1] == pd) ? 0u : C[r + 1];
+                    asm("" : "+v"(t0), "+v"(t1), "+v"(x0), "+v"(x1));
+                    bm[g] = umax(umax(bm[g], t0), t1);
                     bx[g] = umax(umax(bx[g], x0), x1);
                   }
+                } else {
+                  const uint32_t pd = spd[g] << 24;
+#pragma unroll
+                  for (int r = 0; r < R; r += 2)
+                    bm[g] = umin(umin(bm[g], sad(D[r], pd, C[r])), sad(D[r + 1], pd, C[r + 1]));
                 }
               }
             }
@@ -261,7 +287,7 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
 #pragma unroll
           for (int g = 0; g < G; ++g) {
             if (g < cnt) {
-              const uint32_t vm = wave_max_u32(bm[g]);
+              const uint32_t vm = NEED_KX ? wave_max_u32(bm[g]) : cost_to_key(wave_min_u32(bm[g]));
               res_m = (lane == lsel[g]) ? umax(vm, res_m) : res_m;
               if (NEED_KX) {
                 const uint32_t vx = wave_max_u32(bx[g]);
@@ -294,7 +320,6 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
 
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
 __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restrict__ pod_digit,
-                                                          const uint8_t* __restrict__ pod_tol,
                                                           int32_t p, const int64_t* __restrict__ keys,
                                                           int32_t slot1_any, PluginParams pp,
                                                           int32_t* __restrict__ out_idx,
@@ -302,7 +327,6 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
                                                           int32_t* __restrict__ out_status) {
   const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= p) return;
-  (void)pod_tol;
   const int64_t k0 = keys[j], k1 = keys[(size_t)p + j];
   const int64_t ka = slot1_any ? k1 : (k0 > k1 ? k0 : k1);
   auto idx_of = [](int64_t k) -> int64_t { return k ? GKEY_MAX - k : -1; };
@@ -314,9 +338,11 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
 // ---------------------------------------------------------------------------------------
 // Sequential-commit kernel: ONE workgroup (16 waves) walks the pods in order; node state
 // lives in registers (chunk c is owned by wave c % 16, slot c / 16). Per pod: every wave
-// scans its chunks (bm / first-feasible / bx keys), wave DPP max, one LDS exchange + one
-// barrier (double-buffered by pod parity), every wave finishes the reduction redundantly,
-// then the owner lane commits: count += 1 and, with a capacity, the node turns infeasible.
+// scans its chunks (first-match cost, first-feasible cost, and the non-match key when the
+// normalize mode needs it), reduces across lanes with DPP, exchanges one word per wave
+// through LDS behind one barrier (double-buffered by pod parity), finishes the reduction
+// redundantly in every wave, and the owner lane commits: count += 1 and, with a
+// capacity, the node turns infeasible for both classes.
 // ---------------------------------------------------------------------------------------
 template <int RS, bool NEED_KX>
 __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
@@ -325,24 +351,24 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
-  uint32_t D[RS], KN[RS], KT[RS];
+  uint32_t D[RS], C0[RS], C1[RS];
   int32_t CNT[RS];
 #pragma unroll
   for (int r = 0; r < RS; ++r) {
     const int32_t c = wv + NW * r;
-    D[r] = DIGIT_NONE;
-    KN[r] = 0u;
-    KT[r] = 0u;
+    D[r] = DIGIT_NONE << 24;
+    C0[r] = NOFIT;
+    C1[r] = NOFIT;
     CNT[r] = 0;
     if (c < a.n_chunks) {
       const int32_t i = c * WAVE + lane;
-      D[r] = a.dig[i];
-      KN[r] = a.kn[i];
-      KT[r] = i < a.n_nodes ? KMAX - (uint32_t)i : 0u;
+      D[r] = (uint32_t)a.dig[i] << 24;
+      C0[r] = a.c0[i];
+      C1[r] = i < a.n_nodes ? (uint32_t)i : NOFIT;
       CNT[r] = a.counts[i];
       if (a.max_pods > 0 && CNT[r] >= a.max_pods) {
-        KN[r] = 0u;
-        KT[r] = 0u;
+        C0[r] = NOFIT;
+        C1[r] = NOFIT;
       }
     }
   }
@@ -362,32 +388,27 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
     }
     const uint32_t pd = (uint32_t)__builtin_amdgcn_readlane((int)pdv, jl);
     const uint32_t tol = (uint32_t)__builtin_amdgcn_readlane((int)tolv, jl);
-    uint32_t bm = 0u, ba = 0u, bx = 0u;
-    if (tol) {
+    const uint32_t pds = pd << 24;
+    uint32_t bm = 0xFFFFFFFFu, ba = 0xFFFFFFFFu, bx = 0u;
 #pragma unroll
-      for (int r = 0; r < RS; ++r) {
-        const bool m = D[r] == pd;
-        bm = umax(bm, m ? KT[r] : 0u);
-        ba = umax(ba, KT[r]);
-        if (NEED_KX) bx = umax(bx, m ? 0u : KT[r]);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < RS; ++r) {
-        const bool m = D[r] == pd;
-        bm = umax(bm, m ? KN[r] : 0u);
-        ba = umax(ba, KN[r]);
-        if (NEED_KX) bx = umax(bx, m ? 0u : KN[r]);
+    for (int r = 0; r < RS; ++r) {
+      const uint32_t cst = tol ? C1[r] : C0[r];  // wave-uniform select
+      bm = umin(bm, sad(D[r], pds, cst));
+      ba = umin(ba, cst);
+      if (NEED_KX) {
+        const bool m = D[r] == pds;
+        const uint32_t k = cst < MATCH_LIMIT ? KMAX - cst : 0u;
+        bx = umax(bx, m ? 0u : k);
       }
     }
-    bm = wave_max_u32(bm);
-    ba = wave_max_u32(ba);
-    if (NEED_KX) bx = wave_max_u32(bx);
+    const uint32_t km = cost_to_key(wave_min_u32(bm));
+    const uint32_t ka = cost_to_key(wave_min_u32(ba));
+    const uint32_t kx = NEED_KX ? wave_max_u32(bx) : 0u;
     const int par = j & 1;
     if (lane == 0) {
-      red[par][0][wv] = bm;
-      red[par][1][wv] = ba;
-      red[par][2][wv] = bx;
+      red[par][0][wv] = km;
+      red[par][1][wv] = ka;
+      red[par][2][wv] = kx;
     }
     __syncthreads();
     const uint32_t gm = wave_max_u32(lane < NW ? red[par][0][lane] : 0u);
@@ -412,8 +433,8 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
           if (r == rs && mine) {
             CNT[r] += 1;
             if (a.max_pods > 0 && CNT[r] >= a.max_pods) {
-              KN[r] = 0u;
-              KT[r] = 0u;
+              C0[r] = NOFIT;
+              C1[r] = NOFIT;
             }
           }
         }
@@ -432,14 +453,14 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
 // Host launchers
 // ---------------------------------------------------------------------------------------
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
-                            int32_t n_pad, int32_t has_nu, uint32_t* d_kn, uint8_t* d_dig,
+                            int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
                             unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s) {
   hipError_t e = hipMemsetAsync(d_ball, 0, 2 * sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   if (n_pad == 0) return hipSuccess;
   const int blocks = (n_pad + 255) / 256;
   hipLaunchKernelGGL(node_prep_kernel, dim3(blocks), dim3(256), 0, s, d_unsched, d_digit, n, n_pad,
-                     has_nu, d_kn, d_dig, d_mask, d_ball);
+                     has_nu, d_c0, d_dig, d_mask, d_ball);
   return hipGetLastError();
 }
 
@@ -472,7 +493,7 @@ hipError_t launch_batch_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
     return hipErrorInvalidConfiguration;
   }
   // Grid: enough waves for ~one pod group each, capped at what is resident at once, and a
-  // whole number of workgroups per CU when the cap binds (balanced XCD/CU load).
+  // whole number of workgroups per CU when it exceeds one round (balanced CU load).
   const int64_t waves_wanted = ((int64_t)a.n_pods + BATCH_G - 1) / BATCH_G;
   int64_t grid = (waves_wanted + 3) / 4;
   const int64_t cap = (int64_t)dev.cus * occ;
@@ -508,9 +529,10 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
                               const int64_t* keys, int32_t slot1_any, PluginParams pp,
                               int32_t* out_idx, int64_t* out_score, int32_t* out_status,
                               hipStream_t s) {
+  (void)pod_tol;
   if (p == 0) return hipSuccess;
-  hipLaunchKernelGGL(decode_keys_kernel, dim3((p + 255) / 256), dim3(256), 0, s, pod_digit, pod_tol,
-                     p, keys, slot1_any, pp, out_idx, out_score, out_status);
+  hipLaunchKernelGGL(decode_keys_kernel, dim3((p + 255) / 256), dim3(256), 0, s, pod_digit, p, keys,
+                     slot1_any, pp, out_idx, out_score, out_status);
   return hipGetLastError();
 }
 
@@ -537,10 +559,7 @@ hipError_t launch_sequential(const SeqArgs& a, hipStream_t s, std::string* err) 
   if (rs <= 6) return launch_seq_rs<6>(a, s);
   if (rs <= 8) return launch_seq_rs<8>(a, s);
   if (rs <= 12) return launch_seq_rs<12>(a, s);
-  if (rs <= 16) return launch_seq_rs<16>(a, s);
-  if (rs <= 24) return launch_seq_rs<24>(a, s);
-  if (rs <= 32) return launch_seq_rs<32>(a, s);
-  if (err) *err = "sequential mode supports at most 32768 nodes per device";
+  if (err) *err = "sequential mode supports at most 12288 nodes per device";
   return hipErrorInvalidValue;
 }
 
