@@ -39,6 +39,8 @@ struct msh_ctx {
   int8_t* d_digit = nullptr;
   uint32_t* d_c0 = nullptr;
   uint8_t* d_dig = nullptr;
+  uint32_t* d_w0 = nullptr;
+  uint16_t* d_w1 = nullptr;
   unsigned long long* d_mask = nullptr;
   uint32_t* d_ball = nullptr;
   int32_t* d_counts = nullptr;
@@ -77,7 +79,8 @@ int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
 
 void free_nodes(msh_ctx* c) {
   hipFree(c->d_unsched); hipFree(c->d_digit); hipFree(c->d_c0); hipFree(c->d_dig);
-  hipFree(c->d_mask); hipFree(c->d_counts);
+  hipFree(c->d_mask); hipFree(c->d_counts); hipFree(c->d_w0); hipFree(c->d_w1);
+  c->d_w0 = nullptr; c->d_w1 = nullptr;
   c->d_unsched = nullptr; c->d_digit = nullptr; c->d_c0 = nullptr; c->d_dig = nullptr;
   c->d_mask = nullptr; c->d_counts = nullptr;
   c->node_cap = 0;
@@ -125,7 +128,7 @@ int prepare(msh_ctx* c, hipStream_t s) {
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (!c->dirty) return MSH_OK;
   hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad,
-                                       c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_mask,
+                                       c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_w0, c->d_w1, c->d_mask,
                                        c->d_ball, s);
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
   c->dirty = false;
@@ -133,7 +136,7 @@ int prepare(msh_ctx* c, hipStream_t s) {
 }
 
 int ensure_partial(msh_ctx* c, int32_t p) {
-  if (msh::batch_tile_chunks(c->n_pad / 64) >= c->n_pad / 64) return MSH_OK;
+  if (!msh::batch_needs_partial(c->n_pad / 64)) return MSH_OK;
   if ((size_t)p <= c->partial_cap) return MSH_OK;
   (void)hipFree(c->d_partial);
   c->d_partial = nullptr;
@@ -148,6 +151,8 @@ msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t
   msh::BatchArgs a{};
   a.c0 = c->d_c0;
   a.dig = c->d_dig;
+  a.w0 = c->d_w0;
+  a.w1 = c->d_w1;
   a.n_nodes = c->n_nodes;
   a.n_chunks = c->n_pad / 64;
   a.pod_digit = pd;
@@ -292,6 +297,8 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
     MSH_HIP(c, hipMalloc(&c->d_digit, cap));
     MSH_HIP(c, hipMalloc(&c->d_c0, cap * sizeof(uint32_t)));
     MSH_HIP(c, hipMalloc(&c->d_dig, cap));
+    MSH_HIP(c, hipMalloc(&c->d_w0, cap * sizeof(uint32_t)));
+    MSH_HIP(c, hipMalloc(&c->d_w1, cap * sizeof(uint16_t)));
     MSH_HIP(c, hipMalloc(&c->d_mask, 2 * (cap / 64) * sizeof(unsigned long long)));
     MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
     c->node_cap = cap;

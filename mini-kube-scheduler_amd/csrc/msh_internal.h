@@ -47,13 +47,26 @@ struct DeviceInfo {
 };
 
 // ---- launchers (msh_kernels.hip) ----
+// Packed-16 first-match words (IDENT batch path): per node and pod class c,
+//   w16 = (code_c << 12) | (idx & 4095),  code_c = node digit if feasible for class c and the
+//   name ends in '0'..'9', else 15 (never equals a pod code: 0..9, or 14 for no digit).
+// w0 holds the class-0 word in both 16-bit halves (one v_xor_b32 serves two pods), w1 the
+// class-1 word once. Compute tiles are 4096 nodes (12-bit local index).
+constexpr int TILE_NODES = 4096;
+constexpr int TILE_CHUNKS = TILE_NODES / 64;
+constexpr uint32_t CODE_NONE_NODE = 15u;
+constexpr uint32_t CODE_NONE_POD = 14u;
+
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
                             int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
+                            uint32_t* d_w0, uint16_t* d_w1,
                             unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s);
 
 struct BatchArgs {
   const uint32_t* c0;        // [n_pad] class-0 node cost: idx if feasible for !tolerating pods, else NOFIT
   const uint8_t* dig;        // [n_pad] node digit 0..9 / 0xFF
+  const uint32_t* w0;        // [n_pad] packed-16 class-0 word, duplicated in both halves
+  const uint16_t* w1;        // [n_pad] packed-16 class-1 word
   int32_t n_nodes, n_chunks; // n_chunks = n_pad / 64
   const int8_t* pod_digit;
   const uint8_t* pod_tol;
@@ -70,6 +83,7 @@ struct BatchArgs {
 
 // LDS tile geometry of the batched kernel (host needs it to size the partial-key scratch).
 int32_t batch_tile_chunks(int32_t n_chunks);
+bool batch_needs_partial(int32_t n_chunks);
 
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s,
                         std::string* err);

@@ -73,6 +73,7 @@ __device__ __forceinline__ uint32_t cost_to_key(uint32_t c) { return c < MATCH_L
 // classes: 0 = does not tolerate, 1 = tolerates. Class 1 is feasible on every node.
 //   c0[i]  = i if node i is feasible for class 0, else NOFIT
 //   dig[i] = NodeNumber node digit (Atoi of the last byte, nodenumber.go:81-87) or 0xFF
+//   w0[i], w1[i] = packed-16 first-match words of class 0 / 1 (see msh_internal.h)
 //   mask[c][chunk] = __ballot(feasible for class c)   (64-node feasibility bitmask)
 //   ball[c] = key (KMAX - idx) of the first feasible node of class c (0 = none)
 // ---------------------------------------------------------------------------------------
@@ -81,6 +82,8 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
                                                         int32_t n, int32_t n_pad, int32_t has_nu,
                                                         uint32_t* __restrict__ c0,
                                                         uint8_t* __restrict__ dig,
+                                                        uint32_t* __restrict__ w0,
+                                                        uint16_t* __restrict__ w1,
                                                         unsigned long long* __restrict__ mask,
                                                         uint32_t* __restrict__ ball) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -91,8 +94,14 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
   // NodeUnschedulable.Filter: Spec.Unschedulable && !tolerates -> UnschedulableAndUnresolvable
   const bool feas0 = valid && !(has_nu && u);
   const bool feas1 = valid;
+  const bool has_digit = d >= 0 && d <= 9;
   c0[i] = feas0 ? (uint32_t)i : NOFIT;
-  dig[i] = (d >= 0 && d <= 9) ? (uint8_t)d : (uint8_t)DIGIT_NONE;
+  dig[i] = has_digit ? (uint8_t)d : (uint8_t)DIGIT_NONE;
+  const uint32_t local = (uint32_t)i & (TILE_NODES - 1);
+  const uint32_t wd0 = ((feas0 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << 12) | local;
+  const uint32_t wd1 = ((feas1 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << 12) | local;
+  w0[i] = wd0 | (wd0 << 16);
+  w1[i] = (uint16_t)wd1;
   const unsigned long long m0 = __ballot(feas0);
   const unsigned long long m1 = __ballot(feas1);
   const int lane = threadIdx.x & 63;
@@ -318,6 +327,189 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// IDENT batched kernel (normalize NONE / DEFAULT, i.e. the reference plugin set): packed-16.
+// Workgroup = 8 waves sharing one LDS copy of the node words (6 B/node). Each wave owns a
+// contiguous pod range, walked in windows of 64 pods; each window is split by class with
+// __ballot and processed in groups of G2 pod PAIRS. A pair's two pod codes sit in one SGPR
+//   PP = (code_B << 28) | (code_A << 12)
+// and every node word holds its 16-bit (code << 12 | local idx) in both halves, so
+//   x = W ^ PP        -> low half: (pod A, node) pair, high half: (pod B, node) pair;
+//                        a half is < 4096 exactly when the node is feasible for the class
+//                        and its digit equals the pod's, and then it IS the local index
+//   bm = v_pk_min_u16(bm, x)   -> first feasible match per pod, per lane
+// = 2 VALU per 2 x 64 (pod, node) pairs (1.0 per 64 pairs). Per 4096-node compute tile the
+// halves are widened to global indices; one DPP min per pod at the end.
+// ---------------------------------------------------------------------------------------
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  const u16x2 x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(x, y));
+}
+
+constexpr int IDENT_THREADS = 512;
+constexpr int QB = 4;  // pod pairs per interleaved block (4 independent v_pk_min chains)
+
+// One class-homogeneous group of up to GQ pod pairs taken from `mask` (lanes of the window),
+// scanned against the LDS-resident node words [0, nc) chunks of this stage.
+template <int CLS, int R, int GQ>
+__device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t pcv, uint32_t& res,
+                                            const uint32_t* lw0, const uint16_t* lw1, int32_t nc,
+                                            int32_t s0, int lane) {
+  static_assert(GQ % QB == 0, "GQ must be a multiple of QB");
+  uint32_t pp[GQ];
+  int32_t la[GQ], lb[GQ];
+  int32_t cnt = 0;
+#pragma unroll
+  for (int q = 0; q < GQ; ++q) {
+    uint32_t ca = CODE_NONE_POD, cb = CODE_NONE_POD;
+    la[q] = -1;
+    lb[q] = -1;
+    if (mask) {
+      la[q] = (int32_t)__builtin_ctzll(mask);
+      mask &= mask - 1;
+      ca = (uint32_t)__builtin_amdgcn_readlane((int)pcv, la[q]);
+      cnt = q + 1;
+      if (mask) {
+        lb[q] = (int32_t)__builtin_ctzll(mask);
+        mask &= mask - 1;
+        cb = (uint32_t)__builtin_amdgcn_readlane((int)pcv, lb[q]);
+      }
+    }
+    pp[q] = (cb << 28) | (ca << 12);
+  }
+  uint32_t ga[GQ], gb[GQ];
+#pragma unroll
+  for (int q = 0; q < GQ; ++q) {
+    ga[q] = NOFIT;
+    gb[q] = NOFIT;
+  }
+  for (int32_t ct = 0; ct < nc; ct += TILE_CHUNKS) {
+    const int32_t cte = min(ct + TILE_CHUNKS, nc);
+    uint32_t bm[GQ];
+#pragma unroll
+    for (int q = 0; q < GQ; ++q) bm[q] = 0xFFFFFFFFu;
+    for (int32_t c0 = ct; c0 < cte; c0 += R) {
+      uint32_t w[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (CLS == 0) {
+          w[r] = lw0[(c0 + r) * WAVE + lane];
+        } else {
+          const uint32_t h = lw1[(c0 + r) * WAVE + lane];
+          w[r] = h | (h << 16);
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < GQ; qb += QB) {
+        if (qb < cnt) {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = qb; q < qb + QB; ++q) bm[q] = pk_min_u16(bm[q], w[r] ^ pp[q]);
+        }
+      }
+    }
+    // widen the 12-bit local indices of this compute tile to global indices
+    const uint32_t base = (uint32_t)(s0 + ct) * WAVE;
+#pragma unroll
+    for (int q = 0; q < GQ; ++q) {
+      const uint32_t lo = bm[q] & 0xFFFFu, hi = bm[q] >> 16;
+      ga[q] = umin(ga[q], lo < (uint32_t)TILE_NODES ? base + lo : NOFIT);
+      gb[q] = umin(gb[q], hi < (uint32_t)TILE_NODES ? base + hi : NOFIT);
+    }
+  }
+  // ---- stage 4: wave-wide first match per pod, into the pod's lane ----
+#pragma unroll
+  for (int q = 0; q < GQ; ++q) {
+    if (q < cnt) {
+      const uint32_t ra = wave_min_u32(ga[q]);
+      res = (lane == la[q]) ? umin(res, ra) : res;
+      if (lb[q] >= 0) {
+        const uint32_t rb = wave_min_u32(gb[q]);
+        res = (lane == lb[q]) ? umin(res, rb) : res;
+      }
+    }
+  }
+}
+
+template <int R, int G2, int G2T, bool SHARD>
+__global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32_t lds_chunks) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  uint32_t* lw0 = reinterpret_cast<uint32_t*>(lds_raw);
+  uint16_t* lw1 = reinterpret_cast<uint16_t*>(lds_raw + (size_t)lds_chunks * WAVE * sizeof(uint32_t));
+
+  constexpr int WPG = IDENT_THREADS / WAVE;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t W = (int64_t)gridDim.x * WPG;
+  const int64_t gw = (int64_t)blockIdx.x * WPG + wv;
+  const int32_t p0 = (int32_t)((int64_t)a.n_pods * gw / W);
+  const int32_t p1 = (int32_t)((int64_t)a.n_pods * (gw + 1) / W);
+  const int32_t nstages = (a.n_chunks + lds_chunks - 1) / lds_chunks;
+  const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
+
+  for (int32_t st = 0; st < nstages; ++st) {
+    // ---- stage the node words of this LDS tile (stage 5); loads batched 4 deep ----
+    const int32_t s0 = st * lds_chunks;                  // multiple of TILE_CHUNKS when nstages > 1
+    const int32_t nc = min(lds_chunks, a.n_chunks - s0);  // multiple of 16
+    if (st > 0) __syncthreads();
+    {
+      const uint4* src0 = reinterpret_cast<const uint4*>(a.w0 + (size_t)s0 * WAVE);
+      uint4* dst0 = reinterpret_cast<uint4*>(lw0);
+      const int32_t n0 = nc * (WAVE / 4);
+      for (int32_t i = threadIdx.x; i < n0; i += 4 * IDENT_THREADS) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (i + k * IDENT_THREADS < n0) v[k] = src0[i + k * IDENT_THREADS];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (i + k * IDENT_THREADS < n0) dst0[i + k * IDENT_THREADS] = v[k];
+      }
+      const uint4* src1 = reinterpret_cast<const uint4*>(a.w1 + (size_t)s0 * WAVE);
+      uint4* dst1 = reinterpret_cast<uint4*>(lw1);
+      const int32_t n1 = nc * (WAVE / 8);
+      for (int32_t i = threadIdx.x; i < n1; i += IDENT_THREADS) dst1[i] = src1[i];
+    }
+    __syncthreads();
+    const bool last_stage = (st == nstages - 1);
+
+    for (int32_t w0 = p0; w0 < p1; w0 += WAVE) {
+      const int32_t nwin = min((int32_t)WAVE, p1 - w0);
+      const bool act = lane < nwin;
+      uint32_t pcv = CODE_NONE_POD, tolv = 0;
+      if (act) {
+        const int d = a.pod_digit[w0 + lane];
+        pcv = (d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
+        tolv = a.pod_tol[w0 + lane] ? 1u : 0u;
+      }
+      uint32_t res = NOFIT;  // global index of the first feasible match, NOFIT = none
+      if (st > 0 && act) res = a.partial[w0 + lane];
+      unsigned long long m0 = __ballot(act && tolv == 0u);
+      unsigned long long m1 = __ballot(act && tolv != 0u);
+      while (m0) ident_group<0, R, G2>(m0, pcv, res, lw0, lw1, nc, s0, lane);
+      while (m1) ident_group<1, R, G2T>(m1, pcv, res, lw0, lw1, nc, s0, lane);
+
+      if (!act) continue;
+      const int32_t j = w0 + lane;
+      if (!last_stage) {
+        a.partial[j] = res;
+        continue;
+      }
+      const uint32_t ball = tolv ? ball1 : ball0;
+      if (SHARD) {
+        a.keys[j] = res != NOFIT ? (GKEY_MAX - (a.node_base + (int64_t)res)) : 0;
+        a.keys[(size_t)a.n_pods + j] = ball ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - ball))) : 0;
+      } else {
+        decode_pod(res != NOFIT ? (int64_t)res : -1, -1, key_to_idx(ball), pcv != CODE_NONE_POD, a.pp,
+                   &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
+      }
+    }
+  }
+}
+
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
 __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restrict__ pod_digit,
                                                           int32_t p, const int64_t* __restrict__ keys,
@@ -454,13 +646,14 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
 // ---------------------------------------------------------------------------------------
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
                             int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
+                            uint32_t* d_w0, uint16_t* d_w1,
                             unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s) {
   hipError_t e = hipMemsetAsync(d_ball, 0, 2 * sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   if (n_pad == 0) return hipSuccess;
   const int blocks = (n_pad + 255) / 256;
   hipLaunchKernelGGL(node_prep_kernel, dim3(blocks), dim3(256), 0, s, d_unsched, d_digit, n, n_pad,
-                     has_nu, d_c0, d_dig, d_mask, d_ball);
+                     has_nu, d_c0, d_dig, d_w0, d_w1, d_mask, d_ball);
   return hipGetLastError();
 }
 
@@ -510,6 +703,61 @@ hipError_t launch_batch_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BATCH_THREADS), lds, s, a, tile_chunks);
   return hipGetLastError();
 }
+
+int32_t ident_stage_chunks(int32_t n_chunks);
+
+constexpr int IDENT_R = 8;
+constexpr int IDENT_G2 = 8;   // pod pairs per class-0 group
+constexpr int IDENT_G2T = 4;  // pod pairs per class-1 (tolerating) group
+constexpr size_t IDENT_LDS_BYTES_PER_NODE = sizeof(uint32_t) + sizeof(uint16_t);
+constexpr size_t IDENT_LDS_MAX = 80 * 1024;
+
+int32_t ident_stage_chunks(int32_t n_chunks) {
+  // whole table if it fits, else whole 4096-node compute tiles per LDS stage
+  const int32_t max_chunks = (int32_t)(IDENT_LDS_MAX / (IDENT_LDS_BYTES_PER_NODE * WAVE));
+  if (n_chunks <= max_chunks) return n_chunks;
+  return (max_chunks / TILE_CHUNKS) * TILE_CHUNKS;
+}
+
+template <bool SHARD>
+hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
+                          std::string* err) {
+  auto kern = ident_kernel<IDENT_R, IDENT_G2, IDENT_G2T, SHARD>;
+  const int32_t lds_chunks = ident_stage_chunks(a.n_chunks);
+  if (lds_chunks < a.n_chunks && a.partial == nullptr) {
+    if (err) *err = "ident kernel: multi-stage node table needs partial scratch";
+    return hipErrorInvalidValue;
+  }
+  const size_t lds = (size_t)lds_chunks * WAVE * IDENT_LDS_BYTES_PER_NODE;
+  if (lds > 64 * 1024) {
+    hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (ea != hipSuccess) return ea;
+  }
+  int occ = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, IDENT_THREADS, lds);
+  if (e != hipSuccess) return e;
+  if (occ < 1) {
+    if (err) *err = "ident kernel: zero occupancy";
+    return hipErrorInvalidConfiguration;
+  }
+  constexpr int WPG = IDENT_THREADS / WAVE;
+  const int64_t waves_wanted = ((int64_t)a.n_pods + 2 * IDENT_G2 - 1) / (2 * IDENT_G2);
+  int64_t grid = (waves_wanted + WPG - 1) / WPG;
+  const int64_t cap = (int64_t)dev.cus * occ;
+  if (const char* env = getenv("MSH_BATCH_WG_PER_CU")) {
+    const int k = atoi(env);
+    if (k > 0) grid = (int64_t)dev.cus * (k < occ ? k : occ);
+  } else if (grid > cap) {
+    grid = cap;
+  } else if (grid > dev.cus) {
+    grid = ((grid + dev.cus - 1) / dev.cus) * dev.cus;
+    if (grid > cap) grid = cap;
+  }
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(IDENT_THREADS), lds, s, a, lds_chunks);
+  return hipGetLastError();
+}
 }  // namespace
 
 int32_t batch_tile_chunks(int32_t n_chunks) {
@@ -517,10 +765,16 @@ int32_t batch_tile_chunks(int32_t n_chunks) {
   return n_chunks <= max_tile ? n_chunks : max_tile;
 }
 
+bool batch_needs_partial(int32_t n_chunks) {
+  return batch_tile_chunks(n_chunks) < n_chunks || ident_stage_chunks(n_chunks) < n_chunks;
+}
+
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s,
                         std::string* err) {
   if (a.n_pods == 0) return hipSuccess;
   const bool kx = needs_kx(a.pp);
+  if (!kx && !(getenv("MSH_BATCH_KERNEL") && atoi(getenv("MSH_BATCH_KERNEL")) == 1))
+    return shard ? launch_ident_t<true>(a, dev, s, err) : launch_ident_t<false>(a, dev, s, err);
   if (shard) return kx ? launch_batch_t<true, true>(a, dev, s, err) : launch_batch_t<false, true>(a, dev, s, err);
   return kx ? launch_batch_t<true, false>(a, dev, s, err) : launch_batch_t<false, false>(a, dev, s, err);
 }

@@ -19,7 +19,8 @@ synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
 
 n = int(os.environ.get("NODES", 5000))
 p = int(os.environ.get("PODS", 100000))
-variants = [v for v in os.environ.get("VARIANTS", "0,1,2,3,4,5,6,8").split(",")]
+# variant = "<kernel>/<wg_per_cu>": kernel 0 = packed-16 IDENT, 1 = compare/select kernel; wg 0 = auto
+variants = [v for v in os.environ.get("VARIANTS", "0/0,1/0,0/1,0/2,0/3,0/4").split(",")]
 ctx = msh.DeviceContext(0)
 u, nd, pd, pt = synth.make_soa(n, p)
 ctx.upload_nodes(u, nd)
@@ -32,10 +33,12 @@ s = torch.cuda.current_stream()
 res = {v: [] for v in variants}
 for rnd in range(20):
     for v in variants:
-        if v == "0":
+        kern, wg = v.split("/")
+        os.environ["MSH_BATCH_KERNEL"] = kern
+        if wg == "0":
             os.environ.pop("MSH_BATCH_WG_PER_CU", None)
         else:
-            os.environ["MSH_BATCH_WG_PER_CU"] = v
+            os.environ["MSH_BATCH_WG_PER_CU"] = wg
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         for _ in range(5):
@@ -47,5 +50,5 @@ for rnd in range(20):
             res[v].append(e0.elapsed_time(e1) / 5)
 for v in variants:
     a = np.array(res[v])
-    print(json.dumps({"wg_per_cu": v, "nodes": n, "pods": p, "median_ms": float(np.median(a)), "min_ms": float(a.min()),
+    print(json.dumps({"variant": v, "nodes": n, "pods": p, "median_ms": float(np.median(a)), "min_ms": float(a.min()),
                       "evals_per_s_median": n * p / (np.median(a) * 1e-3)}))
