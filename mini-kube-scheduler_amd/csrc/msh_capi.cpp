@@ -40,7 +40,8 @@ struct msh_ctx {
   uint32_t* d_c0 = nullptr;
   uint8_t* d_dig = nullptr;
   uint32_t* d_w0 = nullptr;
-  uint16_t* d_w1 = nullptr;
+  uint32_t* d_ulist = nullptr;
+  uint32_t* d_ucount = nullptr;
   unsigned long long* d_mask = nullptr;
   uint32_t* d_ball = nullptr;
   int32_t* d_counts = nullptr;
@@ -79,8 +80,8 @@ int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
 
 void free_nodes(msh_ctx* c) {
   hipFree(c->d_unsched); hipFree(c->d_digit); hipFree(c->d_c0); hipFree(c->d_dig);
-  hipFree(c->d_mask); hipFree(c->d_counts); hipFree(c->d_w0); hipFree(c->d_w1);
-  c->d_w0 = nullptr; c->d_w1 = nullptr;
+  hipFree(c->d_mask); hipFree(c->d_counts); hipFree(c->d_w0); hipFree(c->d_ulist);
+  c->d_w0 = nullptr; c->d_ulist = nullptr;
   c->d_unsched = nullptr; c->d_digit = nullptr; c->d_c0 = nullptr; c->d_dig = nullptr;
   c->d_mask = nullptr; c->d_counts = nullptr;
   c->node_cap = 0;
@@ -128,7 +129,7 @@ int prepare(msh_ctx* c, hipStream_t s) {
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (!c->dirty) return MSH_OK;
   hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad,
-                                       c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_w0, c->d_w1, c->d_mask,
+                                       c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_w0, c->d_ulist, c->d_ucount, c->d_mask,
                                        c->d_ball, s);
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
   c->dirty = false;
@@ -152,7 +153,8 @@ msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t
   a.c0 = c->d_c0;
   a.dig = c->d_dig;
   a.w0 = c->d_w0;
-  a.w1 = c->d_w1;
+  a.ulist = c->d_ulist;
+  a.ucount = c->d_ucount;
   a.n_nodes = c->n_nodes;
   a.n_chunks = c->n_pad / 64;
   a.pod_digit = pd;
@@ -199,11 +201,12 @@ int msh_create(int device, msh_ctx** out_ctx) {
     delete c;
     return MSH_ERR_HIP;
   }
-  if (hipMalloc(&c->d_ball, 2 * sizeof(uint32_t)) != hipSuccess) {
+  if (hipMalloc(&c->d_ball, 4 * sizeof(uint32_t)) != hipSuccess) {
     hipStreamDestroy(c->stream);
     delete c;
     return MSH_ERR_HIP;
   }
+  c->d_ucount = c->d_ball + 2;  // shares the small scalar allocation
   // Reference plugin set (minisched/initialize.go:80-123).
   c->filter_ids = {MSH_PLUGIN_NODE_UNSCHEDULABLE};
   c->prescore_ids = {MSH_PLUGIN_NODE_NUMBER};
@@ -298,7 +301,7 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
     MSH_HIP(c, hipMalloc(&c->d_c0, cap * sizeof(uint32_t)));
     MSH_HIP(c, hipMalloc(&c->d_dig, cap));
     MSH_HIP(c, hipMalloc(&c->d_w0, cap * sizeof(uint32_t)));
-    MSH_HIP(c, hipMalloc(&c->d_w1, cap * sizeof(uint16_t)));
+    MSH_HIP(c, hipMalloc(&c->d_ulist, cap * sizeof(uint32_t)));
     MSH_HIP(c, hipMalloc(&c->d_mask, 2 * (cap / 64) * sizeof(unsigned long long)));
     MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
     c->node_cap = cap;

@@ -47,11 +47,15 @@ struct DeviceInfo {
 };
 
 // ---- launchers (msh_kernels.hip) ----
-// Packed-16 first-match words (IDENT batch path): per node and pod class c,
-//   w16 = (code_c << 12) | (idx & 4095),  code_c = node digit if feasible for class c and the
-//   name ends in '0'..'9', else 15 (never equals a pod code: 0..9, or 14 for no digit).
-// w0 holds the class-0 word in both 16-bit halves (one v_xor_b32 serves two pods), w1 the
-// class-1 word once. Compute tiles are 4096 nodes (12-bit local index).
+// Packed-16 first-match words (IDENT batch path): per node,
+//   w16 = (code << 12) | (idx & 4095),  code = node digit if the node is feasible for pods
+//   that do NOT tolerate the unschedulable taint (class 0) and its name ends in '0'..'9',
+//   else 15 (never equals a pod code: 0..9, or 14 for no digit).
+// w0 holds w16 in both 16-bit halves, so one v_xor_b32 serves two pods. Compute tiles are
+// 4096 nodes (12-bit local index). The only pairs whose feasibility differs for tolerating
+// pods (class 1) are the nodes infeasible for class 0 but feasible for class 1 (the
+// unschedulable ones): they are listed once in `ulist` as (code1 << 24) | idx, in any
+// order (the search is a min), and scanned for tolerating pods only.
 constexpr int TILE_NODES = 4096;
 constexpr int TILE_CHUNKS = TILE_NODES / 64;
 constexpr uint32_t CODE_NONE_NODE = 15u;
@@ -59,14 +63,15 @@ constexpr uint32_t CODE_NONE_POD = 14u;
 
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
                             int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
-                            uint32_t* d_w0, uint16_t* d_w1,
+                            uint32_t* d_w0, uint32_t* d_ulist, uint32_t* d_ucount,
                             unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s);
 
 struct BatchArgs {
   const uint32_t* c0;        // [n_pad] class-0 node cost: idx if feasible for !tolerating pods, else NOFIT
   const uint8_t* dig;        // [n_pad] node digit 0..9 / 0xFF
   const uint32_t* w0;        // [n_pad] packed-16 class-0 word, duplicated in both halves
-  const uint16_t* w1;        // [n_pad] packed-16 class-1 word
+  const uint32_t* ulist;     // [ucount] (code1 << 24) | idx of class-0-infeasible, class-1-feasible nodes
+  const uint32_t* ucount;    // device scalar
   int32_t n_nodes, n_chunks; // n_chunks = n_pad / 64
   const int8_t* pod_digit;
   const uint8_t* pod_tol;

@@ -73,7 +73,7 @@ __device__ __forceinline__ uint32_t cost_to_key(uint32_t c) { return c < MATCH_L
 // classes: 0 = does not tolerate, 1 = tolerates. Class 1 is feasible on every node.
 //   c0[i]  = i if node i is feasible for class 0, else NOFIT
 //   dig[i] = NodeNumber node digit (Atoi of the last byte, nodenumber.go:81-87) or 0xFF
-//   w0[i], w1[i] = packed-16 first-match words of class 0 / 1 (see msh_internal.h)
+//   w0[i]  = packed-16 first-match word (see msh_internal.h); ulist = class-1-only nodes
 //   mask[c][chunk] = __ballot(feasible for class c)   (64-node feasibility bitmask)
 //   ball[c] = key (KMAX - idx) of the first feasible node of class c (0 = none)
 // ---------------------------------------------------------------------------------------
@@ -83,7 +83,8 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
                                                         uint32_t* __restrict__ c0,
                                                         uint8_t* __restrict__ dig,
                                                         uint32_t* __restrict__ w0,
-                                                        uint16_t* __restrict__ w1,
+                                                        uint32_t* __restrict__ ulist,
+                                                        uint32_t* __restrict__ ucount,
                                                         unsigned long long* __restrict__ mask,
                                                         uint32_t* __restrict__ ball) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -99,12 +100,22 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
   dig[i] = has_digit ? (uint8_t)d : (uint8_t)DIGIT_NONE;
   const uint32_t local = (uint32_t)i & (TILE_NODES - 1);
   const uint32_t wd0 = ((feas0 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << 12) | local;
-  const uint32_t wd1 = ((feas1 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << 12) | local;
   w0[i] = wd0 | (wd0 << 16);
-  w1[i] = (uint16_t)wd1;
   const unsigned long long m0 = __ballot(feas0);
   const unsigned long long m1 = __ballot(feas1);
   const int lane = threadIdx.x & 63;
+  // nodes whose feasibility differs between the classes -> ulist (order irrelevant: min search)
+  const bool diff = feas1 && !feas0;
+  const unsigned long long md = __ballot(diff);
+  if (md) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(ucount, (uint32_t)__builtin_popcountll(md));
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    if (diff) {
+      const uint32_t rank = (uint32_t)__builtin_popcountll(md & ((1ull << lane) - 1ull));
+      ulist[base + rank] = ((has_digit ? (uint32_t)d : CODE_NONE_NODE) << 24) | (uint32_t)i;
+    }
+  }
   if (lane == 0) {
     const int32_t chunk = i >> 6;
     const int32_t n_chunks = n_pad >> 6;
@@ -329,17 +340,19 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
 
 // ---------------------------------------------------------------------------------------
 // IDENT batched kernel (normalize NONE / DEFAULT, i.e. the reference plugin set): packed-16.
-// Workgroup = 8 waves sharing one LDS copy of the node words (6 B/node). Each wave owns a
-// contiguous pod range, walked in windows of 64 pods; each window is split by class with
-// __ballot and processed in groups of G2 pod PAIRS. A pair's two pod codes sit in one SGPR
+// Workgroup = 8 waves sharing one LDS copy of the node words (4 B/node). Each wave owns a
+// contiguous pod range, walked in windows of 64 pods, processed in groups of G2 pod PAIRS.
+// A pair's two pod codes sit in one SGPR
 //   PP = (code_B << 28) | (code_A << 12)
 // and every node word holds its 16-bit (code << 12 | local idx) in both halves, so
 //   x = W ^ PP        -> low half: (pod A, node) pair, high half: (pod B, node) pair;
-//                        a half is < 4096 exactly when the node is feasible for the class
-//                        and its digit equals the pod's, and then it IS the local index
+//                        a half is < 4096 exactly when the node is feasible and its digit
+//                        equals the pod's, and then it IS the node's local index
 //   bm = v_pk_min_u16(bm, x)   -> first feasible match per pod, per lane
 // = 2 VALU per 2 x 64 (pod, node) pairs (1.0 per 64 pairs). Per 4096-node compute tile the
-// halves are widened to global indices; one DPP min per pod at the end.
+// packed minima are reduced across the wave with DPP and widened to global indices on the
+// scalar unit. Pods that tolerate the unschedulable taint additionally scan `ulist` (the
+// nodes only they may use), 1.5 VALU per 64 pairs, so every pair is evaluated once.
 // ---------------------------------------------------------------------------------------
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -348,15 +361,31 @@ __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(x, y));
 }
 
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_pkmin(uint32_t v) {
+  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, CTRL, ROW_MASK, 0xF, false);
+  return pk_min_u16(v, t);
+}
+
+// Wave-wide packed u16 min (both halves at once); result wave-uniform.
+__device__ __forceinline__ uint32_t wave_pkmin_u16(uint32_t v) {
+  v = dpp_pkmin<0xB1, 0xF>(v);
+  v = dpp_pkmin<0x4E, 0xF>(v);
+  v = dpp_pkmin<0x141, 0xF>(v);
+  v = dpp_pkmin<0x140, 0xF>(v);
+  v = dpp_pkmin<0x142, 0xA>(v);
+  v = dpp_pkmin<0x143, 0xC>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 constexpr int IDENT_THREADS = 512;
 constexpr int QB = 4;  // pod pairs per interleaved block (4 independent v_pk_min chains)
 
-// One class-homogeneous group of up to GQ pod pairs taken from `mask` (lanes of the window),
-// scanned against the LDS-resident node words [0, nc) chunks of this stage.
-template <int CLS, int R, int GQ>
+// One group of up to GQ pod pairs taken from `mask` (lanes of the window), scanned against
+// the LDS-resident node words [0, nc) chunks of this stage; results min-merged into `res`.
+template <int R, int GQ>
 __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t pcv, uint32_t& res,
-                                            const uint32_t* lw0, const uint16_t* lw1, int32_t nc,
-                                            int32_t s0, int lane) {
+                                            const uint32_t* lw0, int32_t nc, int32_t s0, int lane) {
   static_assert(GQ % QB == 0, "GQ must be a multiple of QB");
   uint32_t pp[GQ];
   int32_t la[GQ], lb[GQ];
@@ -379,7 +408,7 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
     }
     pp[q] = (cb << 28) | (ca << 12);
   }
-  uint32_t ga[GQ], gb[GQ];
+  uint32_t ga[GQ], gb[GQ];  // wave-uniform running first match (global index) per pod
 #pragma unroll
   for (int q = 0; q < GQ; ++q) {
     ga[q] = NOFIT;
@@ -393,14 +422,7 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
     for (int32_t c0 = ct; c0 < cte; c0 += R) {
       uint32_t w[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (CLS == 0) {
-          w[r] = lw0[(c0 + r) * WAVE + lane];
-        } else {
-          const uint32_t h = lw1[(c0 + r) * WAVE + lane];
-          w[r] = h | (h << 16);
-        }
-      }
+      for (int r = 0; r < R; ++r) w[r] = lw0[(c0 + r) * WAVE + lane];
 #pragma unroll
       for (int qb = 0; qb < GQ; qb += QB) {
         if (qb < cnt) {
@@ -411,34 +433,32 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
         }
       }
     }
-    // widen the 12-bit local indices of this compute tile to global indices
+    // reduce the packed minima across the wave, widen the 12-bit local indices (scalar)
     const uint32_t base = (uint32_t)(s0 + ct) * WAVE;
 #pragma unroll
     for (int q = 0; q < GQ; ++q) {
-      const uint32_t lo = bm[q] & 0xFFFFu, hi = bm[q] >> 16;
-      ga[q] = umin(ga[q], lo < (uint32_t)TILE_NODES ? base + lo : NOFIT);
-      gb[q] = umin(gb[q], hi < (uint32_t)TILE_NODES ? base + hi : NOFIT);
+      if (q < cnt) {
+        const uint32_t v = wave_pkmin_u16(bm[q]);
+        const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
+        ga[q] = umin(ga[q], lo < (uint32_t)TILE_NODES ? base + lo : NOFIT);
+        gb[q] = umin(gb[q], hi < (uint32_t)TILE_NODES ? base + hi : NOFIT);
+      }
     }
   }
-  // ---- stage 4: wave-wide first match per pod, into the pod's lane ----
+  // ---- stage 4: first match per pod into the pod's lane ----
 #pragma unroll
   for (int q = 0; q < GQ; ++q) {
     if (q < cnt) {
-      const uint32_t ra = wave_min_u32(ga[q]);
-      res = (lane == la[q]) ? umin(res, ra) : res;
-      if (lb[q] >= 0) {
-        const uint32_t rb = wave_min_u32(gb[q]);
-        res = (lane == lb[q]) ? umin(res, rb) : res;
-      }
+      res = (lane == la[q]) ? umin(res, ga[q]) : res;
+      res = (lane == lb[q]) ? umin(res, gb[q]) : res;
     }
   }
 }
 
-template <int R, int G2, int G2T, bool SHARD>
+template <int R, int G2, bool SHARD>
 __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32_t lds_chunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   uint32_t* lw0 = reinterpret_cast<uint32_t*>(lds_raw);
-  uint16_t* lw1 = reinterpret_cast<uint16_t*>(lds_raw + (size_t)lds_chunks * WAVE * sizeof(uint32_t));
 
   constexpr int WPG = IDENT_THREADS / WAVE;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -449,6 +469,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
   const int32_t p1 = (int32_t)((int64_t)a.n_pods * (gw + 1) / W);
   const int32_t nstages = (a.n_chunks + lds_chunks - 1) / lds_chunks;
   const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
+  const uint32_t ucnt = *a.ucount;
 
   for (int32_t st = 0; st < nstages; ++st) {
     // ---- stage the node words of this LDS tile (stage 5); loads batched 4 deep ----
@@ -468,10 +489,6 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
         for (int k = 0; k < 4; ++k)
           if (i + k * IDENT_THREADS < n0) dst0[i + k * IDENT_THREADS] = v[k];
       }
-      const uint4* src1 = reinterpret_cast<const uint4*>(a.w1 + (size_t)s0 * WAVE);
-      uint4* dst1 = reinterpret_cast<uint4*>(lw1);
-      const int32_t n1 = nc * (WAVE / 8);
-      for (int32_t i = threadIdx.x; i < n1; i += IDENT_THREADS) dst1[i] = src1[i];
     }
     __syncthreads();
     const bool last_stage = (st == nstages - 1);
@@ -487,10 +504,26 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       }
       uint32_t res = NOFIT;  // global index of the first feasible match, NOFIT = none
       if (st > 0 && act) res = a.partial[w0 + lane];
-      unsigned long long m0 = __ballot(act && tolv == 0u);
-      unsigned long long m1 = __ballot(act && tolv != 0u);
-      while (m0) ident_group<0, R, G2>(m0, pcv, res, lw0, lw1, nc, s0, lane);
-      while (m1) ident_group<1, R, G2T>(m1, pcv, res, lw0, lw1, nc, s0, lane);
+      unsigned long long m = __ballot(act);
+      while (m) ident_group<R, G2>(m, pcv, res, lw0, nc, s0, lane);
+
+      // tolerating pods: the class-1-only nodes (ulist), once (first stage)
+      unsigned long long mt = __ballot(act && tolv != 0u);
+      if (st == 0) {
+        while (mt) {
+          const int32_t l = (int32_t)__builtin_ctzll(mt);
+          mt &= mt - 1;
+          const uint32_t pc24 = (uint32_t)__builtin_amdgcn_readlane((int)pcv, l) << 24;
+          uint32_t bu = 0xFFFFFFFFu;
+          for (uint32_t u0 = 0; u0 < ucnt; u0 += WAVE) {
+            const uint32_t u = u0 + (uint32_t)lane;
+            const uint32_t x = (u < ucnt ? a.ulist[u] : (CODE_NONE_NODE << 24)) ^ pc24;
+            bu = umin(bu, x);  // < 2^24 exactly on a digit match, then == node index
+          }
+          const uint32_t vu = wave_min_u32(bu);
+          if (vu < MATCH_LIMIT) res = (lane == l) ? umin(res, vu) : res;
+        }
+      }
 
       if (!act) continue;
       const int32_t j = w0 + lane;
@@ -646,14 +679,16 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
 // ---------------------------------------------------------------------------------------
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
                             int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
-                            uint32_t* d_w0, uint16_t* d_w1,
+                            uint32_t* d_w0, uint32_t* d_ulist, uint32_t* d_ucount,
                             unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s) {
   hipError_t e = hipMemsetAsync(d_ball, 0, 2 * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(d_ucount, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   if (n_pad == 0) return hipSuccess;
   const int blocks = (n_pad + 255) / 256;
   hipLaunchKernelGGL(node_prep_kernel, dim3(blocks), dim3(256), 0, s, d_unsched, d_digit, n, n_pad,
-                     has_nu, d_c0, d_dig, d_w0, d_w1, d_mask, d_ball);
+                     has_nu, d_c0, d_dig, d_w0, d_ulist, d_ucount, d_mask, d_ball);
   return hipGetLastError();
 }
 
@@ -707,9 +742,8 @@ hipError_t launch_batch_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
 int32_t ident_stage_chunks(int32_t n_chunks);
 
 constexpr int IDENT_R = 8;
-constexpr int IDENT_G2 = 8;   // pod pairs per class-0 group
-constexpr int IDENT_G2T = 4;  // pod pairs per class-1 (tolerating) group
-constexpr size_t IDENT_LDS_BYTES_PER_NODE = sizeof(uint32_t) + sizeof(uint16_t);
+constexpr int IDENT_G2 = 8;   // pod pairs per group
+constexpr size_t IDENT_LDS_BYTES_PER_NODE = sizeof(uint32_t);
 constexpr size_t IDENT_LDS_MAX = 80 * 1024;
 
 int32_t ident_stage_chunks(int32_t n_chunks) {
@@ -722,7 +756,7 @@ int32_t ident_stage_chunks(int32_t n_chunks) {
 template <bool SHARD>
 hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
                           std::string* err) {
-  auto kern = ident_kernel<IDENT_R, IDENT_G2, IDENT_G2T, SHARD>;
+  auto kern = ident_kernel<IDENT_R, IDENT_G2, SHARD>;
   const int32_t lds_chunks = ident_stage_chunks(a.n_chunks);
   if (lds_chunks < a.n_chunks && a.partial == nullptr) {
     if (err) *err = "ident kernel: multi-stage node table needs partial scratch";
