@@ -693,6 +693,24 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
 }
 
 namespace {
+// Occupancy is a pure function of (kernel, block size, LDS bytes): query once per triple.
+// The query costs microseconds of host time, which would otherwise sit between the caller's
+// start event and the kernel on every launch.
+int cached_occupancy(const void* kern, int threads, size_t lds) {
+  struct Entry { const void* k; int t; size_t l; int occ; };
+  static Entry cache[32];
+  static int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (cache[i].k == kern && cache[i].t == threads && cache[i].l == lds) return cache[i].occ;
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -1;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, threads, lds) != hipSuccess) return -1;
+  if (n < 32) cache[n++] = Entry{kern, threads, lds, occ};
+  return occ;
+}
+
 constexpr int BATCH_R = 8;
 constexpr int BATCH_G = 32;
 constexpr size_t LDS_BYTES_PER_NODE = sizeof(uint32_t) + sizeof(uint8_t);
@@ -708,14 +726,7 @@ hipError_t launch_batch_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
     return hipErrorInvalidValue;
   }
   const size_t lds = (size_t)tile_chunks * WAVE * LDS_BYTES_PER_NODE;
-  if (lds > 64 * 1024) {
-    hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (ea != hipSuccess) return ea;
-  }
-  int occ = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BATCH_THREADS, lds);
-  if (e != hipSuccess) return e;
+  const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), BATCH_THREADS, lds);
   if (occ < 1) {
     if (err) *err = "batch kernel: zero occupancy";
     return hipErrorInvalidConfiguration;
@@ -763,14 +774,7 @@ hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
     return hipErrorInvalidValue;
   }
   const size_t lds = (size_t)lds_chunks * WAVE * IDENT_LDS_BYTES_PER_NODE;
-  if (lds > 64 * 1024) {
-    hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (ea != hipSuccess) return ea;
-  }
-  int occ = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, IDENT_THREADS, lds);
-  if (e != hipSuccess) return e;
+  const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), IDENT_THREADS, lds);
   if (occ < 1) {
     if (err) *err = "ident kernel: zero occupancy";
     return hipErrorInvalidConfiguration;
