@@ -70,6 +70,31 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return LIB
 
 
+def build_diagnostic(verbose: bool = False) -> Path:
+    """Diagnostic variant with per-wave phase stamps (-DMSH_STAMPS): libminisched_hip_stamps.so.
+    Used only by scripts/stamps.py; never loaded by the product path."""
+    out = PKG_DIR / "libminisched_hip_stamps.so"
+    objs = []
+    for src, cc, extra in SOURCES:
+        s = CSRC / src
+        o = OBJ / (s.stem + ".stamps.o")
+        objs.append(o)
+        if not _stale(o, [s, *HEADERS]):
+            continue
+        if cc == "hipcc":
+            cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-DMSH_STAMPS",
+                   "-Wno-unused-result", "-Wno-unused-value", *extra, "-c", str(s), "-o", str(o)]
+        else:
+            cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-c", str(s), "-o", str(o)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    if _stale(out, objs):
+        subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(out)],
+                       check=True)
+    return out
+
+
 def build_oracle(verbose: bool = False) -> Path:
     """Compile the C oracle (test infrastructure) into oracle/build/libmsh_oracle.so."""
     odir = REPO / "oracle"

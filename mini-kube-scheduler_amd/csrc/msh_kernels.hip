@@ -63,6 +63,25 @@ __device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return wave_reduce<false>(v); }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return wave_reduce<true>(v); }
 
+#ifdef MSH_STAMPS
+// Diagnostic build only (-DMSH_STAMPS): per-wave s_memrealtime / s_memtime stamps of the
+// IDENT kernel phases. Never compiled into the product library.
+constexpr int STAMPS_PER_WAVE = 8;
+constexpr int STAMP_WAVES = 16384;
+__device__ unsigned long long msh_stamp_buf[STAMP_WAVES * STAMPS_PER_WAVE * 2];
+#define MSH_STAMP(slot)                                                                   \
+  do {                                                                                    \
+    if (lane == 0 && gw < STAMP_WAVES) {                                                  \
+      msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + (slot)) * 2] = __builtin_amdgcn_s_memrealtime(); \
+      msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + (slot)) * 2 + 1] = __builtin_amdgcn_s_memtime(); \
+    }                                                                                     \
+  } while (0)
+#else
+#define MSH_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
+
 // first-match cost (idx, or >= 2^24 when none) -> key (KMAX - idx, 0 when none)
 __device__ __forceinline__ uint32_t cost_to_key(uint32_t c) { return c < MATCH_LIMIT ? KMAX - c : 0u; }
 
@@ -470,6 +489,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
   const int32_t nstages = (a.n_chunks + lds_chunks - 1) / lds_chunks;
   const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
   const uint32_t ucnt = *a.ucount;
+  MSH_STAMP(0);
 
   for (int32_t st = 0; st < nstages; ++st) {
     // ---- stage the node words of this LDS tile (stage 5); loads batched 4 deep ----
@@ -491,6 +511,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       }
     }
     __syncthreads();
+    MSH_STAMP(1);
     const bool last_stage = (st == nstages - 1);
 
     for (int32_t w0 = p0; w0 < p1; w0 += WAVE) {
@@ -505,7 +526,9 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       uint32_t res = NOFIT;  // global index of the first feasible match, NOFIT = none
       if (st > 0 && act) res = a.partial[w0 + lane];
       unsigned long long m = __ballot(act);
+      MSH_STAMP(2);
       while (m) ident_group<R, G2>(m, pcv, res, lw0, nc, s0, lane);
+      MSH_STAMP(3);
 
       // tolerating pods: the class-1-only nodes (ulist), once (first stage)
       unsigned long long mt = __ballot(act && tolv != 0u);
@@ -524,6 +547,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
           if (vu < MATCH_LIMIT) res = (lane == l) ? umin(res, vu) : res;
         }
       }
+      MSH_STAMP(4);
 
       if (!act) continue;
       const int32_t j = w0 + lane;
@@ -541,6 +565,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       }
     }
   }
+  MSH_STAMP(5);
 }
 
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
@@ -856,3 +881,16 @@ hipError_t launch_sequential(const SeqArgs& a, hipStream_t s, std::string* err) 
 }
 
 }  // namespace msh
+
+#ifdef MSH_STAMPS
+extern "C" int msh_debug_read_stamps(unsigned long long* out, int n_waves) {
+  if (n_waves > msh::STAMP_WAVES) n_waves = msh::STAMP_WAVES;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(msh::msh_stamp_buf),
+                                  sizeof(unsigned long long) * 2 * msh::STAMPS_PER_WAVE * n_waves, 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int msh_debug_clear_stamps(void) {
+  static unsigned long long zero[msh::STAMP_WAVES * msh::STAMPS_PER_WAVE * 2];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(msh::msh_stamp_buf), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
