@@ -404,7 +404,8 @@ constexpr int QB = 4;  // pod pairs per interleaved block (4 independent v_pk_mi
 // the LDS-resident node words [0, nc) chunks of this stage; results min-merged into `res`.
 template <int R, int GQ>
 __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t pcv, uint32_t& res,
-                                            const uint32_t* lw0, int32_t nc, int32_t s0, int lane) {
+                                            const uint32_t* __restrict__ lw0, int32_t nc, int32_t s0,
+                                            int lane) {
   static_assert(GQ % QB == 0, "GQ must be a multiple of QB");
   uint32_t pp[GQ];
   int32_t la[GQ], lb[GQ];
@@ -474,7 +475,9 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
   }
 }
 
-template <int R, int G2, bool SHARD>
+// DIRECT: node words are read straight from global memory (L1/L2-resident: 4 B/node) in the
+// sub-tile loop, with no LDS staging and no workgroup barrier; otherwise staged in LDS.
+template <int R, int G2, bool SHARD, bool DIRECT>
 __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32_t lds_chunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   uint32_t* lw0 = reinterpret_cast<uint32_t*>(lds_raw);
@@ -496,7 +499,8 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
     const int32_t s0 = st * lds_chunks;                  // multiple of TILE_CHUNKS when nstages > 1
     const int32_t nc = min(lds_chunks, a.n_chunks - s0);  // multiple of 16
     if (st > 0) __syncthreads();
-    {
+    const uint32_t* words = DIRECT ? a.w0 + (size_t)s0 * WAVE : lw0;
+    if (!DIRECT) {
       const uint4* src0 = reinterpret_cast<const uint4*>(a.w0 + (size_t)s0 * WAVE);
       uint4* dst0 = reinterpret_cast<uint4*>(lw0);
       const int32_t n0 = nc * (WAVE / 4);
@@ -510,7 +514,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
           if (i + k * IDENT_THREADS < n0) dst0[i + k * IDENT_THREADS] = v[k];
       }
     }
-    __syncthreads();
+    if (!DIRECT) __syncthreads();
     MSH_STAMP(1);
     const bool last_stage = (st == nstages - 1);
 
@@ -527,7 +531,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       if (st > 0 && act) res = a.partial[w0 + lane];
       unsigned long long m = __ballot(act);
       MSH_STAMP(2);
-      while (m) ident_group<R, G2>(m, pcv, res, lw0, nc, s0, lane);
+      while (m) ident_group<R, G2>(m, pcv, res, words, nc, s0, lane);
       MSH_STAMP(3);
 
       // tolerating pods: the class-1-only nodes (ulist), once (first stage)
@@ -566,6 +570,15 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
     }
   }
   MSH_STAMP(5);
+#ifdef MSH_STAMPS
+  if (lane == 0 && gw < STAMP_WAVES) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + 7) * 2] = hw;
+    msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + 7) * 2 + 1] = xcc;
+  }
+#endif
 }
 
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
@@ -789,16 +802,16 @@ int32_t ident_stage_chunks(int32_t n_chunks) {
   return (max_chunks / TILE_CHUNKS) * TILE_CHUNKS;
 }
 
-template <bool SHARD>
+template <bool SHARD, bool DIRECT>
 hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
                           std::string* err) {
-  auto kern = ident_kernel<IDENT_R, IDENT_G2, SHARD>;
-  const int32_t lds_chunks = ident_stage_chunks(a.n_chunks);
+  auto kern = ident_kernel<IDENT_R, IDENT_G2, SHARD, DIRECT>;
+  const int32_t lds_chunks = DIRECT ? a.n_chunks : ident_stage_chunks(a.n_chunks);
   if (lds_chunks < a.n_chunks && a.partial == nullptr) {
     if (err) *err = "ident kernel: multi-stage node table needs partial scratch";
     return hipErrorInvalidValue;
   }
-  const size_t lds = (size_t)lds_chunks * WAVE * IDENT_LDS_BYTES_PER_NODE;
+  const size_t lds = DIRECT ? 0 : (size_t)lds_chunks * WAVE * IDENT_LDS_BYTES_PER_NODE;
   const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), IDENT_THREADS, lds);
   if (occ < 1) {
     if (err) *err = "ident kernel: zero occupancy";
@@ -836,8 +849,13 @@ hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, h
                         std::string* err) {
   if (a.n_pods == 0) return hipSuccess;
   const bool kx = needs_kx(a.pp);
-  if (!kx && !(getenv("MSH_BATCH_KERNEL") && atoi(getenv("MSH_BATCH_KERNEL")) == 1))
-    return shard ? launch_ident_t<true>(a, dev, s, err) : launch_ident_t<false>(a, dev, s, err);
+  const char* kenv = getenv("MSH_BATCH_KERNEL");
+  const int kv = kenv ? atoi(kenv) : 0;
+  if (!kx && kv != 1) {
+    if (kv == 2)  // direct (L1/L2) node-word reads
+      return shard ? launch_ident_t<true, true>(a, dev, s, err) : launch_ident_t<false, true>(a, dev, s, err);
+    return shard ? launch_ident_t<true, false>(a, dev, s, err) : launch_ident_t<false, false>(a, dev, s, err);
+  }
   if (shard) return kx ? launch_batch_t<true, true>(a, dev, s, err) : launch_batch_t<false, true>(a, dev, s, err);
   return kx ? launch_batch_t<true, false>(a, dev, s, err) : launch_batch_t<false, false>(a, dev, s, err);
 }
