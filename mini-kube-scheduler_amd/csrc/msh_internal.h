@@ -47,17 +47,21 @@ struct DeviceInfo {
 };
 
 // ---- launchers (msh_kernels.hip) ----
-// Packed-16 first-match words (IDENT batch path): per node,
-//   w16 = (code << 12) | (idx & 4095),  code = node digit if the node is feasible for pods
-//   that do NOT tolerate the unschedulable taint (class 0) and its name ends in '0'..'9',
-//   else 15 (never equals a pod code: 0..9, or 14 for no digit).
-// w0 holds w16 in both 16-bit halves, so one v_xor_b32 serves two pods. Compute tiles are
-// 4096 nodes (12-bit local index). The only pairs whose feasibility differs for tolerating
-// pods (class 1) are the nodes infeasible for class 0 but feasible for class 1 (the
-// unschedulable ones): they are listed once in `ulist` as (code1 << 24) | idx, in any
-// order (the search is a min), and scanned for tolerating pods only.
-constexpr int TILE_NODES = 4096;
-constexpr int TILE_CHUNKS = TILE_NODES / 64;
+// Packed-16 first-match words (IDENT batch path): per node i (chunk c = i / 64, lane i % 64),
+//   w16 = (code << 12) | (c mod TILE_CHUNKS),  code = node digit if the node is feasible for
+//   pods that do NOT tolerate the unschedulable taint (class 0) and its name ends in '0'..'9',
+//   else 15 (never equals a pod code 0..9).
+// w0 holds w16 in both 16-bit halves, so one v_xor_b32 serves two pods. Within one lane the
+// nodes are ordered by chunk, so the per-lane minimum only needs the chunk number; the lane
+// is folded back in (chunk << 6 | lane = node index in the tile) before the cross-lane min.
+// A compute tile is TILE_CHUNKS chunks (64,512 nodes: chunk < 1023 keeps chunk<<6|lane in 16
+// bits). The only pairs whose feasibility differs for tolerating pods (class 1) are the nodes
+// infeasible for class 0 but feasible for class 1 (the unschedulable ones): they are listed
+// once in `ulist` as (code1 << 24) | idx, in any order (the search is a min), and scanned for
+// tolerating pods only.
+constexpr int TILE_CHUNKS = 1008;                 // 16 * 63
+constexpr int TILE_NODES = TILE_CHUNKS * 64;
+constexpr int STAGE_CHUNKS = TILE_CHUNKS / 3;     // LDS stage: 336 chunks = 86,016 B
 constexpr uint32_t CODE_NONE_NODE = 15u;
 constexpr uint32_t CODE_NONE_POD = 14u;
 

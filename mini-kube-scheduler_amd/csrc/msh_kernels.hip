@@ -117,8 +117,8 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
   const bool has_digit = d >= 0 && d <= 9;
   c0[i] = feas0 ? (uint32_t)i : NOFIT;
   dig[i] = has_digit ? (uint8_t)d : (uint8_t)DIGIT_NONE;
-  const uint32_t local = (uint32_t)i & (TILE_NODES - 1);
-  const uint32_t wd0 = ((feas0 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << 12) | local;
+  const uint32_t local_chunk = (uint32_t)(i >> 6) % (uint32_t)TILE_CHUNKS;
+  const uint32_t wd0 = ((feas0 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << 12) | local_chunk;
   w0[i] = wd0 | (wd0 << 16);
   const unsigned long long m0 = __ballot(feas0);
   const unsigned long long m1 = __ballot(feas1);
@@ -359,25 +359,32 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
 
 // ---------------------------------------------------------------------------------------
 // IDENT batched kernel (normalize NONE / DEFAULT, i.e. the reference plugin set): packed-16.
-// Workgroup = 8 waves sharing one LDS copy of the node words (4 B/node). Each wave owns a
-// contiguous pod range, walked in windows of 64 pods, processed in groups of G2 pod PAIRS.
-// A pair's two pod codes sit in one SGPR
+// Workgroup = 8 waves. Each wave owns a contiguous pod range, walked in windows of 64 pods,
+// processed in groups of G2 pod PAIRS. A pair's two pod codes sit in one SGPR
 //   PP = (code_B << 28) | (code_A << 12)
-// and every node word holds its 16-bit (code << 12 | local idx) in both halves, so
+// and every node word holds (code << 12 | chunk) in both 16-bit halves, so
 //   x = W ^ PP        -> low half: (pod A, node) pair, high half: (pod B, node) pair;
 //                        a half is < 4096 exactly when the node is feasible and its digit
-//                        equals the pod's, and then it IS the node's local index
-//   bm = v_pk_min_u16(bm, x)   -> first feasible match per pod, per lane
-// = 2 VALU per 2 x 64 (pod, node) pairs (1.0 per 64 pairs). Per 4096-node compute tile the
-// packed minima are reduced across the wave with DPP and widened to global indices on the
-// scalar unit. Pods that tolerate the unschedulable taint additionally scan `ulist` (the
-// nodes only they may use), 1.5 VALU per 64 pairs, so every pair is evaluated once.
+//                        equals the pod's, and then it IS the node's chunk in the tile
+//   bm = v_pk_min_u16(bm, x)   -> per lane, the first matching chunk for both pods
+// = 2 VALU per 2 x 64 (pod, node) pairs (1.0 VALU per 64 pairs). At the end of a tile the
+// lane is folded in (chunk << 6 | lane = node index) and one packed DPP min per pair gives
+// both pods' first feasible match. Node words come from LDS (staged once per workgroup,
+// 4 B/node) or, DIRECT, straight from L1/L2. Pods that tolerate the unschedulable taint
+// additionally scan `ulist` (the nodes only they may use), so every pair is evaluated once;
+// pods whose name has no digit suffix get SCORE_ERROR whenever a node is feasible (the
+// reference's Score fails on the first feasible node), so they skip the scan.
 // ---------------------------------------------------------------------------------------
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
   const u16x2 x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(x, y));
+}
+
+__device__ __forceinline__ uint32_t pk_shl6(uint32_t a) {
+  const u16x2 x = __builtin_bit_cast(u16x2, a);
+  return __builtin_bit_cast(uint32_t, (u16x2)(x << (u16x2){6, 6}));
 }
 
 template <int CTRL, int ROW_MASK>
@@ -399,13 +406,15 @@ __device__ __forceinline__ uint32_t wave_pkmin_u16(uint32_t v) {
 
 constexpr int IDENT_THREADS = 512;
 constexpr int QB = 4;  // pod pairs per interleaved block (4 independent v_pk_min chains)
+constexpr uint32_t NOMATCH16 = 0xFFC0u;  // (1023 << 6): above every chunk<<6|lane of a tile
 
 // One group of up to GQ pod pairs taken from `mask` (lanes of the window), scanned against
-// the LDS-resident node words [0, nc) chunks of this stage; results min-merged into `res`.
+// node words [0, nc) chunks of the current tile slice; results min-merged into `res`.
+// `node_base` = global index of chunk 0 of the compute tile the slice belongs to.
 template <int R, int GQ>
 __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t pcv, uint32_t& res,
-                                            const uint32_t* __restrict__ lw0, int32_t nc, int32_t s0,
-                                            int lane) {
+                                            const uint32_t* __restrict__ words, int32_t nc,
+                                            uint32_t node_base, int lane) {
   static_assert(GQ % QB == 0, "GQ must be a multiple of QB");
   uint32_t pp[GQ];
   int32_t la[GQ], lb[GQ];
@@ -428,57 +437,43 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
     }
     pp[q] = (cb << 28) | (ca << 12);
   }
-  uint32_t ga[GQ], gb[GQ];  // wave-uniform running first match (global index) per pod
+  uint32_t bm[GQ];
 #pragma unroll
-  for (int q = 0; q < GQ; ++q) {
-    ga[q] = NOFIT;
-    gb[q] = NOFIT;
-  }
-  for (int32_t ct = 0; ct < nc; ct += TILE_CHUNKS) {
-    const int32_t cte = min(ct + TILE_CHUNKS, nc);
-    uint32_t bm[GQ];
+  for (int q = 0; q < GQ; ++q) bm[q] = 0xFFFFFFFFu;
+  for (int32_t c0 = 0; c0 < nc; c0 += R) {
+    uint32_t w[R];
 #pragma unroll
-    for (int q = 0; q < GQ; ++q) bm[q] = 0xFFFFFFFFu;
-    for (int32_t c0 = ct; c0 < cte; c0 += R) {
-      uint32_t w[R];
+    for (int r = 0; r < R; ++r) w[r] = words[(c0 + r) * WAVE + lane];
 #pragma unroll
-      for (int r = 0; r < R; ++r) w[r] = lw0[(c0 + r) * WAVE + lane];
+    for (int qb = 0; qb < GQ; qb += QB) {
+      if (qb < cnt) {
 #pragma unroll
-      for (int qb = 0; qb < GQ; qb += QB) {
-        if (qb < cnt) {
+        for (int r = 0; r < R; ++r)
 #pragma unroll
-          for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int q = qb; q < qb + QB; ++q) bm[q] = pk_min_u16(bm[q], w[r] ^ pp[q]);
-        }
-      }
-    }
-    // reduce the packed minima across the wave, widen the 12-bit local indices (scalar)
-    const uint32_t base = (uint32_t)(s0 + ct) * WAVE;
-#pragma unroll
-    for (int q = 0; q < GQ; ++q) {
-      if (q < cnt) {
-        const uint32_t v = wave_pkmin_u16(bm[q]);
-        const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
-        ga[q] = umin(ga[q], lo < (uint32_t)TILE_NODES ? base + lo : NOFIT);
-        gb[q] = umin(gb[q], hi < (uint32_t)TILE_NODES ? base + hi : NOFIT);
+          for (int q = qb; q < qb + QB; ++q) bm[q] = pk_min_u16(bm[q], w[r] ^ pp[q]);
       }
     }
   }
-  // ---- stage 4: first match per pod into the pod's lane ----
+  // ---- stage 4: fold in the lane, packed DPP min across the wave, into the pods' lanes ----
+  const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);
 #pragma unroll
   for (int q = 0; q < GQ; ++q) {
     if (q < cnt) {
-      res = (lane == la[q]) ? umin(res, ga[q]) : res;
-      res = (lane == lb[q]) ? umin(res, gb[q]) : res;
+      // halves >= 4096 (no match) saturate to chunk 1023 -> 0xFFC0 | lane after the shift
+      const uint32_t v = wave_pkmin_u16(pk_shl6(pk_min_u16(bm[q], 0x03FF03FFu)) | lane2);
+      const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
+      const uint32_t ga = lo < NOMATCH16 ? node_base + lo : NOFIT;
+      const uint32_t gb = hi < NOMATCH16 ? node_base + hi : NOFIT;
+      res = (lane == la[q]) ? umin(res, ga) : res;
+      res = (lane == lb[q]) ? umin(res, gb) : res;
     }
   }
 }
 
-// DIRECT: node words are read straight from global memory (L1/L2-resident: 4 B/node) in the
-// sub-tile loop, with no LDS staging and no workgroup barrier; otherwise staged in LDS.
+// DIRECT: node words are read straight from global memory (L1/L2-resident: 4 B/node) with no
+// LDS staging and no workgroup barrier; otherwise staged in LDS slices of STAGE_CHUNKS.
 template <int R, int G2, bool SHARD, bool DIRECT>
-__global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32_t lds_chunks) {
+__global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32_t stage_chunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   uint32_t* lw0 = reinterpret_cast<uint32_t*>(lds_raw);
 
@@ -489,18 +484,22 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
   const int64_t gw = (int64_t)blockIdx.x * WPG + wv;
   const int32_t p0 = (int32_t)((int64_t)a.n_pods * gw / W);
   const int32_t p1 = (int32_t)((int64_t)a.n_pods * (gw + 1) / W);
-  const int32_t nstages = (a.n_chunks + lds_chunks - 1) / lds_chunks;
+  // stage_chunks divides TILE_CHUNKS, so a stage never straddles two compute tiles
+  const int32_t nstages = (a.n_chunks + stage_chunks - 1) / stage_chunks;
   const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
   const uint32_t ucnt = *a.ucount;
   MSH_STAMP(0);
 
   for (int32_t st = 0; st < nstages; ++st) {
-    // ---- stage the node words of this LDS tile (stage 5); loads batched 4 deep ----
-    const int32_t s0 = st * lds_chunks;                  // multiple of TILE_CHUNKS when nstages > 1
-    const int32_t nc = min(lds_chunks, a.n_chunks - s0);  // multiple of 16
-    if (st > 0) __syncthreads();
-    const uint32_t* words = DIRECT ? a.w0 + (size_t)s0 * WAVE : lw0;
-    if (!DIRECT) {
+    const int32_t s0 = st * stage_chunks;
+    const int32_t nc = min(stage_chunks, a.n_chunks - s0);  // multiple of 16
+    // global index of chunk 0 of this stage's compute tile (words hold tile-relative chunks)
+    const uint32_t tile_node_base = (uint32_t)(s0 / TILE_CHUNKS) * (uint32_t)TILE_NODES;
+    const uint32_t* words;
+    if (DIRECT) {
+      words = a.w0 + (size_t)s0 * WAVE;
+    } else {
+      if (st > 0) __syncthreads();
       const uint4* src0 = reinterpret_cast<const uint4*>(a.w0 + (size_t)s0 * WAVE);
       uint4* dst0 = reinterpret_cast<uint4*>(lw0);
       const int32_t n0 = nc * (WAVE / 4);
@@ -513,8 +512,9 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
         for (int k = 0; k < 4; ++k)
           if (i + k * IDENT_THREADS < n0) dst0[i + k * IDENT_THREADS] = v[k];
       }
+      __syncthreads();
+      words = lw0;
     }
-    if (!DIRECT) __syncthreads();
     MSH_STAMP(1);
     const bool last_stage = (st == nstages - 1);
 
@@ -529,13 +529,13 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       }
       uint32_t res = NOFIT;  // global index of the first feasible match, NOFIT = none
       if (st > 0 && act) res = a.partial[w0 + lane];
-      unsigned long long m = __ballot(act);
+      unsigned long long m = __ballot(act && pcv != CODE_NONE_POD);
       MSH_STAMP(2);
-      while (m) ident_group<R, G2>(m, pcv, res, words, nc, s0, lane);
+      while (m) ident_group<R, G2>(m, pcv, res, words, nc, tile_node_base, lane);
       MSH_STAMP(3);
 
       // tolerating pods: the class-1-only nodes (ulist), once (first stage)
-      unsigned long long mt = __ballot(act && tolv != 0u);
+      unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
       if (st == 0) {
         while (mt) {
           const int32_t l = (int32_t)__builtin_ctzll(mt);
@@ -788,25 +788,23 @@ hipError_t launch_batch_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
   return hipGetLastError();
 }
 
-int32_t ident_stage_chunks(int32_t n_chunks);
+int32_t ident_stage_chunks(int32_t n_chunks, bool direct);
 
 constexpr int IDENT_R = 8;
 constexpr int IDENT_G2 = 8;   // pod pairs per group
 constexpr size_t IDENT_LDS_BYTES_PER_NODE = sizeof(uint32_t);
-constexpr size_t IDENT_LDS_MAX = 80 * 1024;
 
-int32_t ident_stage_chunks(int32_t n_chunks) {
-  // whole table if it fits, else whole 4096-node compute tiles per LDS stage
-  const int32_t max_chunks = (int32_t)(IDENT_LDS_MAX / (IDENT_LDS_BYTES_PER_NODE * WAVE));
-  if (n_chunks <= max_chunks) return n_chunks;
-  return (max_chunks / TILE_CHUNKS) * TILE_CHUNKS;
+int32_t ident_stage_chunks(int32_t n_chunks, bool direct) {
+  // DIRECT: one compute tile per pass; LDS: whole table if it fits a stage, else stages
+  const int32_t cap = direct ? TILE_CHUNKS : STAGE_CHUNKS;
+  return n_chunks <= cap ? n_chunks : cap;
 }
 
 template <bool SHARD, bool DIRECT>
 hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
                           std::string* err) {
   auto kern = ident_kernel<IDENT_R, IDENT_G2, SHARD, DIRECT>;
-  const int32_t lds_chunks = DIRECT ? a.n_chunks : ident_stage_chunks(a.n_chunks);
+  const int32_t lds_chunks = ident_stage_chunks(a.n_chunks, DIRECT);
   if (lds_chunks < a.n_chunks && a.partial == nullptr) {
     if (err) *err = "ident kernel: multi-stage node table needs partial scratch";
     return hipErrorInvalidValue;
@@ -842,7 +840,7 @@ int32_t batch_tile_chunks(int32_t n_chunks) {
 }
 
 bool batch_needs_partial(int32_t n_chunks) {
-  return batch_tile_chunks(n_chunks) < n_chunks || ident_stage_chunks(n_chunks) < n_chunks;
+  return batch_tile_chunks(n_chunks) < n_chunks || ident_stage_chunks(n_chunks, false) < n_chunks;
 }
 
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s,

@@ -99,9 +99,11 @@ def test_plugin_sets_random(msh, gpu_ctx, oracle, combo, norm, weight):
         _assert_same(got, want, f"combo={combo} norm={norm} w={weight} n={n} p={p}")
 
 
-@pytest.mark.parametrize("n", [0, 1, 5, 63, 64, 65, 1023, 1024, 1025, 5000, 16384, 16385, 40000])
+@pytest.mark.parametrize("n", [0, 1, 5, 63, 64, 65, 1023, 1024, 1025, 5000, 16384, 16385, 21504, 21505, 40000,
+                               64512, 64513, 70000, 140000])
 def test_node_sizes(msh, gpu_ctx, oracle, n):
-    """Empty / ragged / tile-boundary / multi-tile node tables (LDS tile = 16384 nodes)."""
+    """Empty / ragged / tile-boundary / multi-stage node tables (IDENT: LDS stage 21,504 nodes,
+    compute tile 64,512 nodes; compare/select kernel: LDS tile 16,384 nodes)."""
     rng = np.random.default_rng(n)
     ps = oracle.PluginSet()
     _set(gpu_ctx, msh, ps)
@@ -124,6 +126,7 @@ def test_multitile_normalize(msh, gpu_ctx, oracle, norm):
 
 @pytest.mark.parametrize("p", [0, 1, 2, 63, 64, 65, 1000, 4097, 250_000])
 def test_pod_sizes(msh, gpu_ctx, oracle, p):
+    """Empty / ragged pod batches, including windows that end mid-group."""
     rng = np.random.default_rng(p + 5)
     ps = oracle.PluginSet()
     _set(gpu_ctx, msh, ps)
