@@ -405,7 +405,10 @@ __device__ __forceinline__ uint32_t wave_pkmin_u16(uint32_t v) {
 }
 
 constexpr int IDENT_THREADS = 512;
-constexpr int QB = 4;  // pod pairs per interleaved block (4 independent v_pk_min chains)
+#ifndef MSH_QB
+#define MSH_QB 8
+#endif
+constexpr int QB = MSH_QB;  // pod pairs per interleaved block (independent v_pk_min chains)
 constexpr uint32_t NOMATCH16 = 0xFFC0u;  // (1023 << 6): above every chunk<<6|lane of a tile
 
 // One group of up to GQ pod pairs taken from `mask` (lanes of the window), scanned against
@@ -440,19 +443,29 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
   uint32_t bm[GQ];
 #pragma unroll
   for (int q = 0; q < GQ; ++q) bm[q] = 0xFFFFFFFFu;
-  for (int32_t c0 = 0; c0 < nc; c0 += R) {
-    uint32_t w[R];
+  // software-pipelined: the next sub-tile's words are in flight while this one is scanned
+  uint32_t w[R], wn[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) w[r] = words[(c0 + r) * WAVE + lane];
+  for (int r = 0; r < R; ++r) w[r] = words[r * WAVE + lane];
+  for (int32_t c0 = 0; c0 < nc; c0 += R) {
+    const int32_t cn = (c0 + R < nc) ? c0 + R : c0;  // last round re-reads (harmless, cached)
+#pragma unroll
+    for (int r = 0; r < R; ++r) wn[r] = words[(cn + r) * WAVE + lane];
 #pragma unroll
     for (int qb = 0; qb < GQ; qb += QB) {
       if (qb < cnt) {
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r) {
+          uint32_t x[QB];
 #pragma unroll
-          for (int q = qb; q < qb + QB; ++q) bm[q] = pk_min_u16(bm[q], w[r] ^ pp[q]);
+          for (int q = 0; q < QB; ++q) x[q] = w[r] ^ pp[qb + q];
+#pragma unroll
+          for (int q = 0; q < QB; ++q) bm[qb + q] = pk_min_u16(bm[qb + q], x[q]);
+        }
       }
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r) w[r] = wn[r];
   }
   // ---- stage 4: fold in the lane, packed DPP min across the wave, into the pods' lanes ----
   const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);
@@ -816,7 +829,9 @@ hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
     return hipErrorInvalidConfiguration;
   }
   constexpr int WPG = IDENT_THREADS / WAVE;
-  const int64_t waves_wanted = ((int64_t)a.n_pods + 2 * IDENT_G2 - 1) / (2 * IDENT_G2);
+  // ~two full groups of G2 pod pairs per wave: enough pods per wave to amortise the per-group
+  // costs, enough waves (>= 4 per SIMD at C3) to keep the VALU fed
+  const int64_t waves_wanted = ((int64_t)a.n_pods + 4 * IDENT_G2 - 1) / (4 * IDENT_G2);
   int64_t grid = (waves_wanted + WPG - 1) / WPG;
   const int64_t cap = (int64_t)dev.cus * occ;
   if (const char* env = getenv("MSH_BATCH_WG_PER_CU")) {
@@ -847,12 +862,14 @@ hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, h
                         std::string* err) {
   if (a.n_pods == 0) return hipSuccess;
   const bool kx = needs_kx(a.pp);
+  // MSH_BATCH_KERNEL (tuning / A-B only): 2 = IDENT direct (default), 0 = IDENT LDS-staged,
+  // 1 = compare/select kernel for every mode
   const char* kenv = getenv("MSH_BATCH_KERNEL");
-  const int kv = kenv ? atoi(kenv) : 0;
+  const int kv = kenv ? atoi(kenv) : 2;
   if (!kx && kv != 1) {
-    if (kv == 2)  // direct (L1/L2) node-word reads
-      return shard ? launch_ident_t<true, true>(a, dev, s, err) : launch_ident_t<false, true>(a, dev, s, err);
-    return shard ? launch_ident_t<true, false>(a, dev, s, err) : launch_ident_t<false, false>(a, dev, s, err);
+    if (kv == 0)
+      return shard ? launch_ident_t<true, false>(a, dev, s, err) : launch_ident_t<false, false>(a, dev, s, err);
+    return shard ? launch_ident_t<true, true>(a, dev, s, err) : launch_ident_t<false, true>(a, dev, s, err);
   }
   if (shard) return kx ? launch_batch_t<true, true>(a, dev, s, err) : launch_batch_t<false, true>(a, dev, s, err);
   return kx ? launch_batch_t<true, false>(a, dev, s, err) : launch_batch_t<false, false>(a, dev, s, err);
