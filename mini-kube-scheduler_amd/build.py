@@ -73,16 +73,21 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 def build_diagnostic(verbose: bool = False) -> Path:
     """Diagnostic variant with per-wave phase stamps (-DMSH_STAMPS): libminisched_hip_stamps.so.
     Used only by scripts/stamps.py; never loaded by the product path."""
-    out = PKG_DIR / "libminisched_hip_stamps.so"
+    return build_variant(["-DMSH_STAMPS"], "stamps", verbose)
+
+
+def build_variant(defines: list[str], tag: str, verbose: bool = False) -> Path:
+    """A/B build of the library with extra -D flags: libminisched_hip_<tag>.so (tuning only)."""
+    out = PKG_DIR / f"libminisched_hip_{tag}.so"
     objs = []
     for src, cc, extra in SOURCES:
         s = CSRC / src
-        o = OBJ / (s.stem + ".stamps.o")
+        o = OBJ / (s.stem + f".{tag}.o")
         objs.append(o)
         if not _stale(o, [s, *HEADERS]):
             continue
         if cc == "hipcc":
-            cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-DMSH_STAMPS",
+            cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *defines,
                    "-Wno-unused-result", "-Wno-unused-value", *extra, "-c", str(s), "-o", str(o)]
         else:
             cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-c", str(s), "-o", str(o)]

@@ -15,6 +15,8 @@ import torch
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 msh = importlib.import_module("mini-kube-scheduler_amd")
+if os.environ.get("MSH_LIBRARY"):
+    msh._native.LIB_PATH = Path(os.environ["MSH_LIBRARY"])
 synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
 
 n = int(os.environ.get("NODES", 5000))
