@@ -406,7 +406,10 @@ __device__ __forceinline__ uint32_t wave_pkmin_u16(uint32_t v) {
 
 constexpr int IDENT_THREADS = 512;
 #ifndef MSH_QB
-#define MSH_QB 8
+#define MSH_QB 4
+#endif
+#ifndef MSH_PREFETCH
+#define MSH_PREFETCH 0
 #endif
 constexpr int QB = MSH_QB;  // pod pairs per interleaved block (independent v_pk_min chains)
 constexpr uint32_t NOMATCH16 = 0xFFC0u;  // (1023 << 6): above every chunk<<6|lane of a tile
@@ -443,14 +446,17 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
   uint32_t bm[GQ];
 #pragma unroll
   for (int q = 0; q < GQ; ++q) bm[q] = 0xFFFFFFFFu;
-  // software-pipelined: the next sub-tile's words are in flight while this one is scanned
+  // MSH_PREFETCH: software-pipelined, the next sub-tile's words are in flight while this one
+  // is scanned (A/B option; the default relies on the other waves of the SIMD instead)
   uint32_t w[R], wn[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) w[r] = words[r * WAVE + lane];
   for (int32_t c0 = 0; c0 < nc; c0 += R) {
     const int32_t cn = (c0 + R < nc) ? c0 + R : c0;  // last round re-reads (harmless, cached)
+    if (MSH_PREFETCH) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) wn[r] = words[(cn + r) * WAVE + lane];
+      for (int r = 0; r < R; ++r) wn[r] = words[(cn + r) * WAVE + lane];
+    }
 #pragma unroll
     for (int qb = 0; qb < GQ; qb += QB) {
       if (qb < cnt) {
@@ -464,8 +470,13 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
         }
       }
     }
+    if (MSH_PREFETCH) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) w[r] = wn[r];
+      for (int r = 0; r < R; ++r) w[r] = wn[r];
+    } else if (c0 + R < nc) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) w[r] = words[(cn + r) * WAVE + lane];
+    }
   }
   // ---- stage 4: fold in the lane, packed DPP min across the wave, into the pods' lanes ----
   const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);

@@ -1,0 +1,109 @@
+"""Multi-GPU modes of the scheduling core (one process per GPU, torch.distributed over RCCL).
+
+SURVEY.md §8(e). The reference has no distribution at all (one goroutine schedules one pod
+at a time, minisched/minisched.go:28-30); both modes below are new:
+
+* Pod sharding (BASELINE C2/C3/C5 at 2/4/8 GPUs). Pods are independent: no plugin reads
+  placement-dependent state (NodeInfo is rebuilt per cycle, minisched.go:126; Bind only
+  touches the pod, :266-277). Every rank holds the whole node table and schedules its
+  contiguous pod range. No data-path collective ("scaling": "weak").
+
+* Node sharding (BASELINE C4: 100k nodes x 1M pods over 8 GPUs). Rank r holds the List-order
+  slice [r*N/W, (r+1)*N/W) of the node table and computes, for every pod, two int64 keys
+  (msh_shard_keys_device): first feasible match and first feasible node (or first feasible
+  non-match for the REVERSE / MINMAX normalizers), each encoded as 2^32-1-global_idx. Because
+  the slices are contiguous and ascending, the element-wise MAX over ranks is the global
+  first match / first feasible node, i.e. exactly the single-GPU answer. One RCCL
+  all-reduce(MAX) of 16 B per pod replaces the all-gather of per-shard bests + merge
+  (same result, ~1/W the bytes per link on a ring); msh_decode_keys_device then yields
+  idx / score / status on every rank.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+GKEY_MAX = 0xFFFFFFFF  # key = GKEY_MAX - global node index, 0 = none (include/minisched_hip.h)
+
+
+def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous, balanced [lo, hi) slice of `total` items for `rank` of `world`."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    return total * rank // world, total * (rank + 1) // world
+
+
+def encode_key(global_idx: np.ndarray) -> np.ndarray:
+    """Node index (or -1) -> shard key (0 = none)."""
+    g = np.asarray(global_idx, np.int64)
+    return np.where(g >= 0, GKEY_MAX - g, 0).astype(np.int64)
+
+
+def decode_key(key: np.ndarray) -> np.ndarray:
+    """Shard key -> node index (or -1)."""
+    k = np.asarray(key, np.int64)
+    return np.where(k > 0, GKEY_MAX - k, -1).astype(np.int64)
+
+
+def merge_shard_keys_(keys, group=None):
+    """In-place element-wise MAX of per-shard keys over the process group (RCCL on GPU
+    tensors, gloo on CPU tensors). `keys` is an int64 tensor of shape [2 * P]."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(keys, op=dist.ReduceOp.MAX, group=group)
+    return keys
+
+
+@dataclass
+class NodeShard:
+    """This rank's slice of the List-order node table."""
+    lo: int
+    hi: int
+
+    @property
+    def n(self) -> int:
+        return self.hi - self.lo
+
+
+class NodeShardedScheduler:
+    """Node-sharded batch scheduling on this rank's GPU (C4 shape).
+
+    `ctx` is a DeviceContext already configured with the plugin set; `unsched` / `digit` are
+    the FULL List-order node columns (each rank uploads only its slice)."""
+
+    def __init__(self, ctx, unsched: np.ndarray, digit: np.ndarray, world: int, rank: int, group=None):
+        lo, hi = shard_range(len(unsched), world, rank)
+        self.shard = NodeShard(lo, hi)
+        self.ctx = ctx
+        self.group = group
+        ctx.upload_nodes(np.ascontiguousarray(unsched[lo:hi]), np.ascontiguousarray(digit[lo:hi]))
+
+    def schedule(self, d_pod_digit, d_pod_tol, d_keys, d_idx, d_score, d_status, stream: int = 0) -> None:
+        """All tensors on this rank's GPU; every rank ends with the global decisions."""
+        p = d_pod_digit.numel()
+        self.ctx.shard_keys_device(p, d_pod_digit.data_ptr(), d_pod_tol.data_ptr(), self.shard.lo,
+                                   d_keys.data_ptr(), stream)
+        merge_shard_keys_(d_keys, self.group)
+        self.ctx.decode_keys_device(p, d_pod_digit.data_ptr(), d_pod_tol.data_ptr(), d_keys.data_ptr(),
+                                    d_idx.data_ptr(), d_score.data_ptr(), d_status.data_ptr(), stream)
+
+
+class PodShardedScheduler:
+    """Pod-sharded batch (or sequential) scheduling: full node table, this rank's pods."""
+
+    def __init__(self, ctx, unsched: np.ndarray, digit: np.ndarray, world: int, rank: int, group=None):
+        self.ctx = ctx
+        self.world, self.rank, self.group = world, rank, group
+        ctx.upload_nodes(unsched, digit)
+
+    def pod_range(self, p_total: int) -> tuple[int, int]:
+        return shard_range(p_total, self.world, self.rank)
+
+    def merge_node_counts(self, counts):
+        """Sequential mode: the commit state (pods per node) summed over ranks. Exact only when
+        no filter reads it (max_pods_per_node == 0), i.e. the reference plugin set."""
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=self.group)
+        return counts

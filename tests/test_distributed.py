@@ -1,0 +1,120 @@
+"""Multi-process (gloo, world_size 2 and 3) tests of the N>1 paths, on CPU.
+
+The device kernels cannot run here, so each rank's per-shard keys are produced by the
+oracle on that rank's node slice (the contract of msh_shard_keys_device: first feasible
+match / first feasible node of the slice, as 2^32-1-global_idx). What is tested is the
+product's sharding arithmetic and collective (merge_shard_keys_ = all_reduce MAX): merged
+keys must decode to exactly the unsharded oracle answer. The GPU side of the same contract
+is tests/test_gpu_parity.py::test_node_shards_merge.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _case(seed, n, p):
+    rng = np.random.default_rng(seed)
+    u = (rng.random(n) < 0.4).astype(np.uint8)
+    nd = rng.integers(-1, 10, n).astype(np.int8)
+    pd = rng.integers(-1, 10, p).astype(np.int8)
+    pt = (rng.random(p) < 0.3).astype(np.uint8)
+    return u, nd, pd, pt
+
+
+def _shard_keys_oracle(O, dist_mod, u, nd, pd, pt, lo, hi):
+    """Per-shard keys exactly as msh_shard_keys_device defines them (reference plugin set)."""
+    us, ns = u[lo:hi], nd[lo:hi]
+    p = len(pd)
+    first_match = np.full(p, -1, np.int64)
+    first_feas = np.full(p, -1, np.int64)
+    for j in range(p):
+        feas = np.ones(hi - lo, bool) if pt[j] else (us == 0)
+        if feas.any():
+            first_feas[j] = lo + int(np.argmax(feas))
+            m = feas & (ns == pd[j]) & (pd[j] >= 0)
+            if m.any():
+                first_match[j] = lo + int(np.argmax(m))
+    return np.concatenate([dist_mod.encode_key(first_match), dist_mod.encode_key(first_feas)])
+
+
+def _worker(rank, world, port, seed, n, p, out_q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D = importlib.import_module("mini-kube-scheduler_amd.distributed")
+    O = importlib.import_module("oracle.oracle")
+    u, nd, pd, pt = _case(seed, n, p)
+    lo, hi = D.shard_range(n, world, rank)
+    keys = torch.from_numpy(_shard_keys_oracle(O, D, u, nd, pd, pt, lo, hi))
+    D.merge_shard_keys_(keys)
+    k = keys.numpy()
+    im, ia = D.decode_key(k[:p]), D.decode_key(k[p:])
+    # decode exactly as decode_pod (NONE mode, reference plugin set)
+    idx = np.where(ia < 0, -1, np.where(pd < 0, -1, np.where(im >= 0, im, ia)))
+    status = np.where(ia < 0, 1, np.where(pd < 0, 2, 0))
+    score = np.where((status == 0) & (im >= 0), 10, 0)
+    # pod sharding: every rank schedules its slice; gather reassembles the batch
+    plo, phi = D.shard_range(p, world, rank)
+    gi, gs, gst, _ = O.c_schedule_batch(u, nd, pd[plo:phi], pt[plo:phi])
+    parts = [None] * world
+    dist.all_gather_object(parts, (plo, gi.tolist()))
+    if rank == 0:
+        pod_idx = np.concatenate([np.array(x[1], np.int64) for x in sorted(parts)])
+        out_q.put((idx, score, status, pod_idx))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_node_and_pod_sharding_gloo(oracle, world):
+    n, p, seed = 777, 300, 41 + world
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, seed, n, p, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    idx, score, status, pod_idx = q.get(timeout=120)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    u, nd, pd, pt = _case(seed, n, p)
+    wi, ws, wst, _ = oracle.c_schedule_batch(u, nd, pd, pt)
+    assert (idx == wi).all() and (score == ws).all() and (status == wst).all()
+    assert (pod_idx == wi).all()
+
+
+def test_shard_range_covers_everything():
+    D = importlib.import_module("mini-kube-scheduler_amd.distributed")
+    for total in (0, 1, 7, 100_000, 1_000_003):
+        for world in (1, 2, 3, 8):
+            spans = [D.shard_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def test_key_encoding_roundtrip():
+    D = importlib.import_module("mini-kube-scheduler_amd.distributed")
+    g = np.array([-1, 0, 1, 12345, 2**31 - 2])
+    assert (D.decode_key(D.encode_key(g)) == g).all()
+    assert D.encode_key(np.array([3]))[0] > D.encode_key(np.array([4]))[0]  # MAX = lowest index
