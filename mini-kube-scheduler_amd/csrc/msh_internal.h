@@ -18,8 +18,6 @@ constexpr uint32_t DIGIT_NONE = 0xFFu;           // node suffix is not '0'..'9'
 constexpr uint32_t POD_DIGIT_NONE = 0xFEu;       // never equals a node digit (0..9 / 0xFF)
 constexpr int WAVE = 64;
 constexpr int BATCH_THREADS = 256;               // 4 waves per workgroup
-constexpr int SEQ_THREADS = 1024;                // 16 waves, one workgroup
-constexpr int SEQ_MAX_CHUNKS_PER_WAVE = 32;      // sequential mode: node table in registers
 constexpr int64_t GKEY_MAX = 0xFFFFFFFFll;       // global (sharded) key = GKEY_MAX - global_idx
 // Node "cost" for the first-match search: idx if the node is feasible for the pod class,
 // NOFIT otherwise. cost + |D - pd| * 2^24 (one v_sad_u32) is < 2^24 exactly for feasible

@@ -623,17 +623,18 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
 }
 
 // ---------------------------------------------------------------------------------------
-// Sequential-commit kernel: ONE workgroup (16 waves) walks the pods in order; node state
-// lives in registers (chunk c is owned by wave c % 16, slot c / 16). Per pod: every wave
-// scans its chunks (first-match cost, first-feasible cost, and the non-match key when the
-// normalize mode needs it), reduces across lanes with DPP, exchanges one word per wave
-// through LDS behind one barrier (double-buffered by pod parity), finishes the reduction
-// redundantly in every wave, and the owner lane commits: count += 1 and, with a
-// capacity, the node turns infeasible for both classes.
+// Sequential-commit kernel: ONE workgroup of NW waves walks the pods in order; node state
+// lives in registers (chunk c is owned by wave c % NW, slot c / NW). Per pod: every wave
+// scans its chunks -- first-match cost (v_sad_u32, as the compare/select-free IDENT form),
+// first-feasible cost, and the non-match key when the normalize mode needs it --, reduces
+// across lanes with DPP (the two costs packed in one u16x2 chain when the table has fewer
+// than 65535 nodes), exchanges one word per wave through LDS behind one barrier
+// (double-buffered by pod parity), finishes the reduction redundantly in every wave, and the
+// owner lane commits: count += 1 and, with a capacity, the node turns infeasible for both
+// classes. The per-pod latency (scan + 2 reductions + 1 barrier), not throughput, bounds it.
 // ---------------------------------------------------------------------------------------
-template <int RS, bool NEED_KX>
-__global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
-  constexpr int NW = SEQ_THREADS / WAVE;
+template <int RS, int NW, bool NEED_KX, bool PACK16>
+__global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
   __shared__ uint32_t red[2][3][NW];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -677,19 +678,39 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
     const uint32_t tol = (uint32_t)__builtin_amdgcn_readlane((int)tolv, jl);
     const uint32_t pds = pd << 24;
     uint32_t bm = 0xFFFFFFFFu, ba = 0xFFFFFFFFu, bx = 0u;
+    if (tol) {
 #pragma unroll
-    for (int r = 0; r < RS; ++r) {
-      const uint32_t cst = tol ? C1[r] : C0[r];  // wave-uniform select
-      bm = umin(bm, sad(D[r], pds, cst));
-      ba = umin(ba, cst);
-      if (NEED_KX) {
-        const bool m = D[r] == pds;
-        const uint32_t k = cst < MATCH_LIMIT ? KMAX - cst : 0u;
-        bx = umax(bx, m ? 0u : k);
+      for (int r = 0; r < RS; ++r) {
+        bm = umin(bm, sad(D[r], pds, C1[r]));
+        ba = umin(ba, C1[r]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < RS; ++r) {
+        bm = umin(bm, sad(D[r], pds, C0[r]));
+        ba = umin(ba, C0[r]);
       }
     }
-    const uint32_t km = cost_to_key(wave_min_u32(bm));
-    const uint32_t ka = cost_to_key(wave_min_u32(ba));
+    if (NEED_KX) {
+#pragma unroll
+      for (int r = 0; r < RS; ++r) {
+        const uint32_t cst = tol ? C1[r] : C0[r];
+        const uint32_t k = cst < MATCH_LIMIT ? KMAX - cst : 0u;
+        bx = umax(bx, D[r] == pds ? 0u : k);
+      }
+    }
+    uint32_t km, ka;
+    if (PACK16) {  // both costs in one u16x2 DPP chain (indices < 65535 here)
+      const uint32_t m16 = bm < MATCH_LIMIT ? bm : 0xFFFFu;
+      const uint32_t a16 = ba < MATCH_LIMIT ? ba : 0xFFFFu;
+      const uint32_t v = wave_pkmin_u16(m16 | (a16 << 16));
+      const uint32_t vm = v & 0xFFFFu, va = v >> 16;
+      km = vm != 0xFFFFu ? KMAX - vm : 0u;
+      ka = va != 0xFFFFu ? KMAX - va : 0u;
+    } else {
+      km = cost_to_key(wave_min_u32(bm));
+      ka = cost_to_key(wave_min_u32(ba));
+    }
     const uint32_t kx = NEED_KX ? wave_max_u32(bx) : 0u;
     const int par = j & 1;
     if (lane == 0) {
@@ -698,8 +719,19 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_kernel(SeqArgs a) {
       red[par][2][wv] = kx;
     }
     __syncthreads();
-    const uint32_t gm = wave_max_u32(lane < NW ? red[par][0][lane] : 0u);
-    const uint32_t ga = wave_max_u32(lane < NW ? red[par][1][lane] : 0u);
+    uint32_t gm, ga;
+    if (PACK16) {  // keys < 2^24 here: reduce (km, ka) as two u16 halves of (KMAX - key)...
+      const uint32_t xm = lane < NW ? red[par][0][lane] : 0u;
+      const uint32_t xa = lane < NW ? red[par][1][lane] : 0u;
+      const uint32_t im = xm ? KMAX - xm : 0xFFFFu, ia = xa ? KMAX - xa : 0xFFFFu;  // back to indices
+      const uint32_t v = wave_pkmin_u16(im | (ia << 16));
+      const uint32_t vm = v & 0xFFFFu, va = v >> 16;
+      gm = vm != 0xFFFFu ? KMAX - vm : 0u;
+      ga = va != 0xFFFFu ? KMAX - va : 0u;
+    } else {
+      gm = wave_max_u32(lane < NW ? red[par][0][lane] : 0u);
+      ga = wave_max_u32(lane < NW ? red[par][1][lane] : 0u);
+    }
     const uint32_t gx = NEED_KX ? wave_max_u32(lane < NW ? red[par][2][lane] : 0u) : 0u;
     int32_t sel, st;
     int64_t sc;
@@ -898,30 +930,52 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
 }
 
 namespace {
-template <int RS>
+template <int RS, int NW>
 hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
-  if (needs_kx(a.pp))
-    hipLaunchKernelGGL((seq_kernel<RS, true>), dim3(1), dim3(SEQ_THREADS), 0, s, a);
-  else
-    hipLaunchKernelGGL((seq_kernel<RS, false>), dim3(1), dim3(SEQ_THREADS), 0, s, a);
+  const bool pack = a.n_nodes < 0xFFFF;
+  const dim3 blk(NW * 64);
+  if (needs_kx(a.pp)) {
+    if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, true, true>), dim3(1), blk, 0, s, a);
+    else hipLaunchKernelGGL((seq_kernel<RS, NW, true, false>), dim3(1), blk, 0, s, a);
+  } else {
+    if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, false, true>), dim3(1), blk, 0, s, a);
+    else hipLaunchKernelGGL((seq_kernel<RS, NW, false, false>), dim3(1), blk, 0, s, a);
+  }
   return hipGetLastError();
+}
+
+// Register-resident node state: RS chunks per lane. Spill-free on gfx950 up to RS = 24 at
+// 4 waves, 16 at 8 waves, 12 at 16 waves (checked with -Rpass-analysis=kernel-resource-usage).
+template <int NW, int RS_MAX>
+hipError_t launch_seq_nw(const SeqArgs& a, hipStream_t s) {
+  const int rs = (a.n_chunks + NW - 1) / NW;
+  if (rs <= 1) return launch_seq_rs<1, NW>(a, s);
+  if (rs <= 2) return launch_seq_rs<2, NW>(a, s);
+  if (rs <= 3) return launch_seq_rs<3, NW>(a, s);
+  if (rs <= 4) return launch_seq_rs<4, NW>(a, s);
+  if (rs <= 6) return launch_seq_rs<6, NW>(a, s);
+  if (rs <= 8) return launch_seq_rs<8, NW>(a, s);
+  if (rs <= 12 || RS_MAX <= 12) return launch_seq_rs<12, NW>(a, s);
+  if (rs <= 16 || RS_MAX <= 16) return launch_seq_rs<(RS_MAX < 16 ? RS_MAX : 16), NW>(a, s);
+  return launch_seq_rs<(RS_MAX < 24 ? RS_MAX : 24), NW>(a, s);
 }
 }  // namespace
 
 hipError_t launch_sequential(const SeqArgs& a, hipStream_t s, std::string* err) {
   if (a.n_pods == 0) return hipSuccess;
-  const int nw = SEQ_THREADS / WAVE;
-  const int rs = (a.n_chunks + nw - 1) / nw;
-  if (rs <= 1) return launch_seq_rs<1>(a, s);
-  if (rs <= 2) return launch_seq_rs<2>(a, s);
-  if (rs <= 3) return launch_seq_rs<3>(a, s);
-  if (rs <= 4) return launch_seq_rs<4>(a, s);
-  if (rs <= 5) return launch_seq_rs<5>(a, s);
-  if (rs <= 6) return launch_seq_rs<6>(a, s);
-  if (rs <= 8) return launch_seq_rs<8>(a, s);
-  if (rs <= 12) return launch_seq_rs<12>(a, s);
-  if (err) *err = "sequential mode supports at most 12288 nodes per device";
-  return hipErrorInvalidValue;
+  // Workgroup size: MSH_SEQ_WAVES (4, 8 or 16) for tuning; default 8 (smallest that fits).
+  const char* env = getenv("MSH_SEQ_WAVES");
+  int nw = env ? atoi(env) : 8;
+  if (nw == 4 && a.n_chunks > 4 * 24) nw = 8;
+  if (nw == 8 && a.n_chunks > 8 * 16) nw = 16;
+  if (nw != 4 && nw != 8) nw = 16;
+  if (a.n_chunks > 16 * 12) {
+    if (err) *err = "sequential mode supports at most 12288 nodes per device";
+    return hipErrorInvalidValue;
+  }
+  if (nw == 4) return launch_seq_nw<4, 24>(a, s);
+  if (nw == 8) return launch_seq_nw<8, 16>(a, s);
+  return launch_seq_nw<16, 12>(a, s);
 }
 
 }  // namespace msh

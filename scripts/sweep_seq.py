@@ -1,0 +1,41 @@
+"""Per-pod latency of the sequential-commit kernel for MSH_SEQ_WAVES in {4, 8, 16}."""
+import importlib
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+msh = importlib.import_module("mini-kube-scheduler_amd")
+synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
+n = int(os.environ.get("NODES", 5000))
+p = int(os.environ.get("PODS", 20000))
+ctx = msh.DeviceContext(0)
+u, nd, pd, pt = synth.make_soa(n, p)
+ctx.upload_nodes(u, nd)
+dev = torch.device("cuda:0")
+d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+oi = torch.empty(p, dtype=torch.int32, device=dev)
+osc = torch.empty(p, dtype=torch.int64, device=dev)
+ost = torch.empty(p, dtype=torch.int32, device=dev)
+s = torch.cuda.current_stream()
+res = {}
+for rnd in range(4):
+    for w in ("4", "8", "16"):
+        os.environ["MSH_SEQ_WAVES"] = w
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        ctx.schedule_sequential_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, oi.data_ptr(), osc.data_ptr(),
+                                       ost.data_ptr(), s.cuda_stream)
+        e1.record(s)
+        torch.cuda.synchronize()
+        if rnd:
+            res.setdefault(w, []).append(e0.elapsed_time(e1))
+for w, t in res.items():
+    ms = float(np.median(t))
+    print(json.dumps({"seq_waves": w, "nodes": n, "pods": p, "ms": ms, "us_per_pod": ms * 1e3 / p,
+                      "evals_per_s": n * p / (ms * 1e-3)}))

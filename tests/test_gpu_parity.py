@@ -179,9 +179,11 @@ def test_c3_full_and_weight3(msh, gpu_ctx, oracle, synth):
     assert (got3[1] == 3 * got1[1]).all()
 
 
+@pytest.mark.parametrize("seq_waves", ["4", "8", "16"])
 @pytest.mark.parametrize("max_pods", [0, 1, 3])
-@pytest.mark.parametrize("n", [1, 70, 1000, 5000, 8192])
-def test_sequential(msh, gpu_ctx, oracle, n, max_pods):
+@pytest.mark.parametrize("n", [1, 70, 1000, 5000, 8192, 12288])
+def test_sequential(msh, gpu_ctx, oracle, n, max_pods, seq_waves, monkeypatch):
+    monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)  # read by the launcher at each call
     rng = np.random.default_rng(n + max_pods)
     ps = oracle.PluginSet()
     _set(gpu_ctx, msh, ps)
