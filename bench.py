@@ -35,7 +35,18 @@ sys.path.insert(0, str(ROOT))
 METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
 VALU_PEAK_LANE_OPS = 157.3e12 / 2  # MI355X_MICROARCH.md: FP32 vector peak 157.3 TFLOPS = 2 x lane-ops/s
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-LANE_OPS_PER_EVAL = 2.5            # compare + select + half a v_max3 per (pod, node) pair
+# IDENT kernel inner loop: one v_xor_b32 + one v_pk_min_u16 per lane per TWO (pod, node) pairs
+LANE_OPS_PER_EVAL = 1.0
+# measured integer-VALU issue ceiling (scripts/ubench_valu.hip -> profiles/r1_ubench_valu.jsonl)
+UBENCH = ROOT / "profiles" / "r1_ubench_valu.jsonl"
+
+
+def measured_int_valu_ceiling() -> float | None:
+    try:
+        rows = [json.loads(l) for l in UBENCH.read_text().splitlines() if l.startswith("{") and "op" in l]
+        return max(r["lane_ops_per_s"] for r in rows if r["op"] == "xor+pk_min")
+    except Exception:
+        return None
 
 
 def parse():
@@ -78,13 +89,14 @@ def main():
         n_total = args.nodes or 5_000
         p_total = args.pods or 100_000
 
+    D = importlib.import_module("mini-kube-scheduler_amd.distributed")
     ctx = msh.DeviceContext(local)
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
     unsched, node_digit = synth.make_nodes(n_total)[1:]
+    sharded = None
     if mode == "nodeshard":
-        a, b = n_total * rank // world, n_total * (rank + 1) // world
-        ctx.upload_nodes(unsched[a:b], node_digit[a:b])
-        node_base = a
+        sharded = D.NodeShardedScheduler(ctx, unsched, node_digit, world, rank)
+        node_base = sharded.shard.lo
         pod_digit, pod_tol = synth._make_pods_fast(p_total, synth.SEED)[1:]
     else:
         ctx.upload_nodes(unsched, node_digit)
@@ -116,9 +128,8 @@ def main():
             ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), node_base, d_keys.data_ptr(), sh)
         if ev1 is not None:
             ev1.record(stream)
-        if mode == "nodeshard":
-            if world > 1:
-                dist.all_reduce(d_keys, op=dist.ReduceOp.MAX)
+        if mode == "nodeshard":  # RCCL all-reduce(MAX) of the per-shard keys, then decode
+            D.merge_shard_keys_(d_keys)
             ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), d_keys.data_ptr(), d_idx.data_ptr(),
                                    d_score.data_ptr(), d_status.data_ptr(), sh)
 
@@ -161,12 +172,12 @@ def main():
     value = evals_total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # ---- roofline of the dominant kernel (batch_kernel), per launch, from HIP events ----
+    # ---- roofline of the dominant kernel, per launch, from HIP events on the launch stream ----
     kern_s = kernel_ms * 1e-3
     evals_launch = float(n_local) * p
     lane_ops = LANE_OPS_PER_EVAL * evals_launch
     uniq_bytes = 2.0 * n_local + 18.0 * p           # node records + pod records + outputs, once
-    survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts LDS re-reads)
+    survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts L1/L2 re-reads)
     traffic = None
     pmc = ROOT / "profiles" / "pmc_latest.json"
     if pmc.exists():
@@ -176,25 +187,39 @@ def main():
                 traffic = pj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = {
-        "bound": "valu",
-        "achieved": lane_ops / kern_s / 1e9,
-        "peak": VALU_PEAK_LANE_OPS / 1e9,
-        "unit": "Glane-op/s",
-        "frac": lane_ops / kern_s / VALU_PEAK_LANE_OPS,
-        "traffic": traffic,
-        "kernel": "batch_kernel" if mode != "sequential" else "seq_kernel",
-        "kernel_ms": kernel_ms,
-        "lane_ops_per_eval": LANE_OPS_PER_EVAL,
-        "hbm": {"bound": "hbm", "achieved": uniq_bytes / kern_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": uniq_bytes / kern_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
-                "survey_8d_bytes_per_launch": survey_bytes,
-                "survey_8d_frac": survey_bytes / kern_s / HBM_PEAK},
-    }
+    ceiling = measured_int_valu_ceiling()
+    if mode == "sequential":
+        roofline = {
+            "bound": "latency",
+            "achieved": kernel_ms * 1e3 / p, "peak": None, "unit": "us/pod (serial)", "frac": None,
+            "traffic": traffic, "kernel": "seq_kernel", "kernel_ms": kernel_ms,
+            "note": "one pod at a time: scan + 2 wave reductions + 1 workgroup barrier per pod",
+        }
+    else:
+        roofline = {
+            "bound": "valu",
+            "achieved": lane_ops / kern_s / 1e9,
+            "peak": VALU_PEAK_LANE_OPS / 1e9,
+            "unit": "Glane-op/s",
+            "frac": lane_ops / kern_s / VALU_PEAK_LANE_OPS,
+            "traffic": traffic,
+            "kernel": "ident_kernel",
+            "kernel_ms": kernel_ms,
+            "lane_ops_per_eval": LANE_OPS_PER_EVAL,
+            "measured_int_valu_ceiling": ceiling / 1e9 if ceiling else None,
+            "frac_vs_measured_int_ceiling": (lane_ops / kern_s / ceiling) if ceiling else None,
+            "hbm": {"bound": "hbm", "achieved": uniq_bytes / kern_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                    "frac": uniq_bytes / kern_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
+                    "survey_8d_bytes_per_launch": survey_bytes,
+                    "survey_8d_frac": survey_bytes / kern_s / HBM_PEAK},
+        }
 
-    cpu = None
+    cpu = cpu_omp = None
     if rank == 0 and args.cpu_seconds > 0:
         cpu = cpu_baseline(unsched, node_digit, pod_digit, pod_tol, args.cpu_seconds, mode)
+        if mode != "sequential":
+            cpu_omp = cpu_baseline(unsched, node_digit, pod_digit, pod_tol, args.cpu_seconds / 2, mode,
+                                   threads=min(16, os.cpu_count() or 1))
 
     if rank == 0:
         if mode == "batch":
@@ -223,6 +248,7 @@ def main():
             "check": check,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "cpu_baseline_omp": cpu_omp,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
@@ -230,14 +256,14 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode: str):
+def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode: str, threads: int = 1):
     """The C restatement (oracle/msh_oracle.c) on this host's cores, on a bounded sample of the
     same workload: pods in chunks against the full node table until the budget is spent."""
     O = importlib.import_module("oracle.oracle")
     build = importlib.import_module("mini-kube-scheduler_amd.build")
     build.build_oracle()
     n = len(unsched)
-    chunk = 2000
+    chunk = 2000 * threads
     done, t = 0, 0.0
     while t < budget_s and done < len(pod_digit):
         sl = slice(done, min(done + chunk, len(pod_digit)))
@@ -245,13 +271,14 @@ def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode:
         if mode == "sequential":
             O.c_schedule_sequential(unsched, node_digit, pod_digit[sl], pod_tol[sl])
         else:
-            O.c_schedule_batch(unsched, node_digit, pod_digit[sl], pod_tol[sl])
+            O.c_schedule_batch(unsched, node_digit, pod_digit[sl], pod_tol[sl], threads=threads)
         t += time.perf_counter() - t0
         done = sl.stop
     evals = float(n) * done
-    return {"value": evals / t, "unit": "pod-node evals/s", "cores": 1, "kind": "port",
-            "sample": f"{done} pods x {n} nodes (first {done} pods of the batch), scalar C restatement, "
-                      f"{t:.1f} s on {os.cpu_count()} visible host CPUs",
+    return {"value": evals / t, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} pods of the batch x {n} nodes, C restatement "
+                      f"({'scalar' if threads == 1 else f'OpenMP {threads} threads'}), {t:.2f} s; "
+                      f"{os.cpu_count()} host CPUs visible",
             "pods_per_s": done / t}
 
 
