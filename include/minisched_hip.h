@@ -118,6 +118,14 @@ int msh_set_plugins_ex(msh_ctx* ctx, const int32_t* filter_ids, int32_t nf,
 int msh_upload_nodes(msh_ctx* ctx, int32_t n, const uint8_t* unsched, const int8_t* digit);
 int msh_num_nodes(const msh_ctx* ctx, int32_t* out_n);
 
+/* In-place update of `count` entries of the uploaded table (an informer Update event that
+ * leaves the List order alone, e.g. a cordon flipping Spec.Unschedulable; eventhandler.go:45-50).
+ * idx[k] in [0, n) and pairwise distinct; unsched[k] / digit[k] as in msh_upload_nodes.
+ * O(count) host->device traffic; the per-node pod counts of sequential mode are kept.
+ * Adds and deletes shift List positions: re-upload with msh_upload_nodes. */
+int msh_patch_nodes(msh_ctx* ctx, int32_t count, const int32_t* idx, const uint8_t* unsched,
+                    const int8_t* digit);
+
 /* Batched hot path: p pods against the uploaded node table.
  * pod_digit[j] = last byte of pod.Name as digit or -1 (nodenumber.go:50-55);
  * pod_tol[j]   = pod tolerates taint {node.kubernetes.io/unschedulable, NoSchedule} (0/1).

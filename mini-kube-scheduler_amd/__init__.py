@@ -13,9 +13,16 @@ from .framework import (MAX_NODE_SCORE, NODE_NUMBER, NODE_UNSCHEDULABLE, Code, N
                         Outcome, ScheduleResult)
 from .scheduler import DeviceContext, Scheduler, ScorePluginConfig
 from .snapshot import NodeTable, PodTable, pack_nodes, pack_pods
+from .queue import (ActionType, ClusterEvent, PodBatch, SchedulingQueue, calculate_backoff_duration,
+                    events_to_register)
+from .nodecache import NodeCache
+from .binder import PermitBinder
+from .loop import CycleReport, SchedulingLoop
 
 __all__ = [
     "MAX_NODE_SCORE", "NODE_NUMBER", "NODE_UNSCHEDULABLE", "Code", "NodeScore", "Normalize", "Outcome",
     "ScheduleResult", "DeviceContext", "Scheduler", "ScorePluginConfig", "NodeTable", "PodTable",
     "pack_nodes", "pack_pods", "MshError", "device_count", "_native",
+    "ActionType", "ClusterEvent", "PodBatch", "SchedulingQueue", "calculate_backoff_duration",
+    "events_to_register", "NodeCache", "PermitBinder", "CycleReport", "SchedulingLoop",
 ]

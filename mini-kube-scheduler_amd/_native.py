@@ -48,6 +48,7 @@ MSH_NORMALIZE_MINMAX = 3
 EXPORTED = (
     "msh_abi_version", "msh_device_count", "msh_create", "msh_destroy", "msh_last_error",
     "msh_set_plugins", "msh_set_plugins_ex", "msh_upload_nodes", "msh_num_nodes",
+    "msh_patch_nodes",
     "msh_schedule_batch", "msh_schedule_batch_device", "msh_schedule_sequential",
     "msh_schedule_sequential_device", "msh_node_pod_counts", "msh_reset_node_pod_counts",
     "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
@@ -82,6 +83,7 @@ _SIGS = {
     "msh_set_plugins_ex": (C.c_int, [_P, _P, _I32, _P, _I32, _P, _P, _P, _I32]),
     "msh_upload_nodes": (C.c_int, [_P, _I32, _P, _P]),
     "msh_num_nodes": (C.c_int, [_P, C.POINTER(_I32)]),
+    "msh_patch_nodes": (C.c_int, [_P, _I32, _P, _P, _P]),
     "msh_schedule_batch": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P]),
     "msh_schedule_batch_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P]),
     "msh_schedule_sequential": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, COMMIT_CB, _P]),

@@ -56,6 +56,9 @@ struct msh_ctx {
   int32_t* d_ost = nullptr;
   size_t partial_cap = 0;
   uint32_t* d_partial = nullptr;  // multi-tile node tables only
+  size_t patch_cap = 0;
+  unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
+  std::vector<unsigned long long> h_patch;
 };
 
 namespace {
@@ -225,6 +228,7 @@ void msh_destroy(msh_ctx* c) {
   free_nodes(c);
   free_pods(c);
   (void)hipFree(c->d_partial);
+  (void)hipFree(c->d_patch);
   (void)hipFree(c->d_ball);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -314,6 +318,45 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
   c->n_nodes = n;
   c->n_pad = n_pad;
   c->have_nodes = true;
+  c->dirty = true;
+  int rc = prepare(c, c->stream);
+  if (rc != MSH_OK) return rc;
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  return MSH_OK;
+}
+
+int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t* unsched,
+                    const int8_t* digit) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  if (count < 0) return fail(c, MSH_ERR_INVALID, "negative patch count");
+  if (count == 0) return MSH_OK;
+  if (!idx || !unsched || !digit) return fail(c, MSH_ERR_INVALID, "null patch arrays");
+  std::vector<int32_t> sorted(idx, idx + count);
+  std::sort(sorted.begin(), sorted.end());
+  if (sorted.front() < 0 || sorted.back() >= c->n_nodes)
+    return fail(c, MSH_ERR_INVALID, "patch index outside [0, n)");
+  if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+    return fail(c, MSH_ERR_INVALID, "duplicate patch index");
+  c->h_patch.resize((size_t)count);
+  for (int32_t k = 0; k < count; ++k)
+    c->h_patch[k] = (unsigned long long)(uint32_t)idx[k] |
+                    ((unsigned long long)(unsched[k] ? 1u : 0u) << 32) |
+                    ((unsigned long long)(uint8_t)digit[k] << 40);
+  DeviceGuard g(c->device);
+  if ((size_t)count > c->patch_cap) {
+    (void)hipFree(c->d_patch);
+    c->d_patch = nullptr;
+    c->patch_cap = 0;
+    const size_t cap = std::max<size_t>((size_t)count, 256);
+    MSH_HIP(c, hipMalloc(&c->d_patch, cap * sizeof(unsigned long long)));
+    c->patch_cap = cap;
+  }
+  MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_patch.data(), (size_t)count * sizeof(unsigned long long),
+                            hipMemcpyHostToDevice, c->stream));
+  hipError_t e = msh::launch_patch_nodes(c->d_patch, count, c->d_unsched, c->d_digit, c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "patch_nodes_kernel");
   c->dirty = true;
   int rc = prepare(c, c->stream);
   if (rc != MSH_OK) return rc;

@@ -68,6 +68,10 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
                             uint32_t* d_w0, uint32_t* d_ulist, uint32_t* d_ucount,
                             unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s);
 
+// entries[k] = idx | unsched << 32 | (uint8)digit << 40
+hipError_t launch_patch_nodes(const unsigned long long* d_entries, int32_t count, uint8_t* d_unsched,
+                              int8_t* d_digit, hipStream_t s);
+
 struct BatchArgs {
   const uint32_t* c0;        // [n_pad] class-0 node cost: idx if feasible for !tolerating pods, else NOFIT
   const uint8_t* dig;        // [n_pad] node digit 0..9 / 0xFF

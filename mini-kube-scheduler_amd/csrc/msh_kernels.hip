@@ -786,6 +786,25 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void patch_nodes_kernel(const unsigned long long* __restrict__ entries,
+                                                          int32_t count, uint8_t* __restrict__ unsched,
+                                                          int8_t* __restrict__ digit) {
+  const int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const unsigned long long e = entries[k];
+  const uint32_t i = (uint32_t)e;
+  unsched[i] = (uint8_t)(e >> 32);
+  digit[i] = (int8_t)(uint8_t)(e >> 40);
+}
+
+hipError_t launch_patch_nodes(const unsigned long long* d_entries, int32_t count, uint8_t* d_unsched,
+                              int8_t* d_digit, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(patch_nodes_kernel, dim3((count + 255) / 256), dim3(256), 0, s, d_entries, count,
+                     d_unsched, d_digit);
+  return hipGetLastError();
+}
+
 namespace {
 // Occupancy is a pure function of (kernel, block size, LDS bytes): query once per triple.
 // The query costs microseconds of host time, which would otherwise sit between the caller's

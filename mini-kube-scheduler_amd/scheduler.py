@@ -94,6 +94,15 @@ class DeviceContext:
         self._check(self._lib.msh_upload_nodes(self.handle, len(unsched), N.ptr(unsched), N.ptr(digit)))
         self.n_nodes = len(unsched)
 
+    def patch_nodes(self, idx: np.ndarray, unsched: np.ndarray, digit: np.ndarray) -> None:
+        """In-place update of table entries (List order unchanged): msh_patch_nodes."""
+        idx = np.ascontiguousarray(idx, np.int32)
+        unsched = np.ascontiguousarray(unsched, np.uint8)
+        digit = np.ascontiguousarray(digit, np.int8)
+        if not (len(idx) == len(unsched) == len(digit)):
+            raise ValueError("idx / unsched / digit length mismatch")
+        self._check(self._lib.msh_patch_nodes(self.handle, len(idx), N.ptr(idx), N.ptr(unsched), N.ptr(digit)))
+
     # -- host-buffer entry points --
     def schedule_batch(self, pod_digit: np.ndarray, pod_tol: np.ndarray):
         pod_digit = np.ascontiguousarray(pod_digit, np.int8)
