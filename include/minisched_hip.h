@@ -118,6 +118,19 @@ int msh_set_plugins_ex(msh_ctx* ctx, const int32_t* filter_ids, int32_t nf,
 int msh_upload_nodes(msh_ctx* ctx, int32_t n, const uint8_t* unsched, const int8_t* digit);
 int msh_num_nodes(const msh_ctx* ctx, int32_t* out_n);
 
+/* Per-pair plugin results for a small batch: the matrices the simulator's result store
+ * turns into pod annotations (scheduler/plugin/resultstore/store.go:170-234, recorded by the
+ * wrapped plugins in scheduler/plugin/plugins.go:278-325). Row j, column i (List order):
+ *   out_filter[j*n+i] = 1 if node i passes the filter plugins for pod j ("passed"), else 0;
+ *   out_score[j*n+i]  = NodeNumber.Score raw value (AddScoreResult);
+ *   out_final[j*n+i]  = NormalizeScore(raw) * weight (AddNormalizedScoreResult ->
+ *                       applyWeightOnScore, store.go:231-234);
+ * score/final = MSH_EXPORT_NONE (INT64_MIN) where no score is recorded (node filtered out, or
+ * the pod never reaches Score). Host buffers; p*n <= 2^28. Debug path, not the hot path. */
+#define MSH_EXPORT_NONE ((int64_t)(-9223372036854775807LL - 1))
+int msh_export_results(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                       uint8_t* out_filter, int64_t* out_score, int64_t* out_final);
+
 /* In-place update of `count` entries of the uploaded table (an informer Update event that
  * leaves the List order alone, e.g. a cordon flipping Spec.Unschedulable; eventhandler.go:45-50).
  * idx[k] in [0, n) and pairwise distinct; unsched[k] / digit[k] as in msh_upload_nodes.

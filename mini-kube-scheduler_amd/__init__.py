@@ -18,6 +18,7 @@ from .queue import (ActionType, ClusterEvent, PodBatch, SchedulingQueue, calcula
 from .nodecache import NodeCache
 from .binder import PermitBinder
 from .loop import CycleReport, SchedulingLoop
+from .resultstore import ResultStore
 
 __all__ = [
     "MAX_NODE_SCORE", "NODE_NUMBER", "NODE_UNSCHEDULABLE", "Code", "NodeScore", "Normalize", "Outcome",
@@ -25,4 +26,5 @@ __all__ = [
     "pack_nodes", "pack_pods", "MshError", "device_count", "_native",
     "ActionType", "ClusterEvent", "PodBatch", "SchedulingQueue", "calculate_backoff_duration",
     "events_to_register", "NodeCache", "PermitBinder", "CycleReport", "SchedulingLoop",
+    "ResultStore",
 ]

@@ -39,6 +39,8 @@ MSH_SCORE_ERROR = 2
 MSH_PLUGIN_NODE_UNSCHEDULABLE = 1
 MSH_PLUGIN_NODE_NUMBER = 2
 
+MSH_EXPORT_NONE = -(1 << 63)  # msh_export_results: no score recorded
+
 MSH_NORMALIZE_NONE = 0
 MSH_NORMALIZE_DEFAULT = 1
 MSH_NORMALIZE_DEFAULT_REVERSE = 2
@@ -48,7 +50,7 @@ MSH_NORMALIZE_MINMAX = 3
 EXPORTED = (
     "msh_abi_version", "msh_device_count", "msh_create", "msh_destroy", "msh_last_error",
     "msh_set_plugins", "msh_set_plugins_ex", "msh_upload_nodes", "msh_num_nodes",
-    "msh_patch_nodes",
+    "msh_patch_nodes", "msh_export_results",
     "msh_schedule_batch", "msh_schedule_batch_device", "msh_schedule_sequential",
     "msh_schedule_sequential_device", "msh_node_pod_counts", "msh_reset_node_pod_counts",
     "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
@@ -84,6 +86,7 @@ _SIGS = {
     "msh_upload_nodes": (C.c_int, [_P, _I32, _P, _P]),
     "msh_num_nodes": (C.c_int, [_P, C.POINTER(_I32)]),
     "msh_patch_nodes": (C.c_int, [_P, _I32, _P, _P, _P]),
+    "msh_export_results": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P]),
     "msh_schedule_batch": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P]),
     "msh_schedule_batch_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P]),
     "msh_schedule_sequential": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, COMMIT_CB, _P]),

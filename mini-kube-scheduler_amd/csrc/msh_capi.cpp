@@ -364,6 +364,48 @@ int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t
   return MSH_OK;
 }
 
+int msh_export_results(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                       uint8_t* out_filter, int64_t* out_score, int64_t* out_final) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  const size_t pairs = (size_t)p * (size_t)c->n_nodes;
+  if (pairs > ((size_t)1 << 28)) return fail(c, MSH_ERR_UNSUPPORTED, "export limited to p*n <= 2^28 pairs");
+  if (pairs == 0) return MSH_OK;
+  if (!pod_digit || !pod_tol || !out_filter || !out_score || !out_final)
+    return fail(c, MSH_ERR_INVALID, "null pointer");
+  DeviceGuard g(c->device);
+  int8_t* d_pd = nullptr;
+  uint8_t* d_pt = nullptr;
+  uint8_t* d_f = nullptr;
+  int64_t* d_r = nullptr;
+  int64_t* d_o = nullptr;
+  int rc = MSH_OK;
+  auto step = [&](hipError_t e, const char* what) {
+    if (rc == MSH_OK && e != hipSuccess) rc = hip_fail(c, e, what);
+  };
+  step(hipMalloc(&d_pd, (size_t)p), "hipMalloc");
+  step(hipMalloc(&d_pt, (size_t)p), "hipMalloc");
+  step(hipMalloc(&d_f, pairs), "hipMalloc");
+  step(hipMalloc(&d_r, pairs * sizeof(int64_t)), "hipMalloc");
+  step(hipMalloc(&d_o, pairs * sizeof(int64_t)), "hipMalloc");
+  if (rc == MSH_OK) {
+    step(hipMemcpyAsync(d_pd, pod_digit, (size_t)p, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync");
+    step(hipMemcpyAsync(d_pt, pod_tol, (size_t)p, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync");
+    step(msh::launch_export(c->d_unsched, c->d_digit, c->n_nodes, d_pd, d_pt, p, c->pp, d_f, d_r, d_o,
+                            c->stream), "export_kernel");
+    step(hipMemcpyAsync(out_filter, d_f, pairs, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync");
+    step(hipMemcpyAsync(out_score, d_r, pairs * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream),
+         "hipMemcpyAsync");
+    step(hipMemcpyAsync(out_final, d_o, pairs * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream),
+         "hipMemcpyAsync");
+    step(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  }
+  (void)hipFree(d_pd); (void)hipFree(d_pt); (void)hipFree(d_f); (void)hipFree(d_r); (void)hipFree(d_o);
+  return rc;
+}
+
 int msh_num_nodes(const msh_ctx* c, int32_t* out_n) {
   if (!c || !out_n) return MSH_ERR_INVALID;
   *out_n = c->have_nodes ? c->n_nodes : 0;

@@ -68,6 +68,12 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
                             uint32_t* d_w0, uint32_t* d_ulist, uint32_t* d_ucount,
                             unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s);
 
+constexpr int64_t EXPORT_NONE = INT64_MIN;  // msh_export_results: no score recorded
+hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
+                         const int8_t* d_pod_digit, const uint8_t* d_pod_tol, int32_t p,
+                         const PluginParams& pp, uint8_t* d_filter, int64_t* d_raw, int64_t* d_fin,
+                         hipStream_t s);
+
 // entries[k] = idx | unsched << 32 | (uint8)digit << 40
 hipError_t launch_patch_nodes(const unsigned long long* d_entries, int32_t count, uint8_t* d_unsched,
                               int8_t* d_digit, hipStream_t s);

@@ -786,6 +786,73 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// Per-pair plugin results (debug / simulator result store). One workgroup
+// per pod: pass 1 ORs "feasible match" / "feasible non-match" over the List to get the
+// extent NormalizeScore needs; pass 2 writes, for every node i,
+//   filter[i] = 1 passed / 0 rejected by NodeUnschedulable,
+//   raw[i]    = NodeNumber.Score (10 on a digit match, else 0),
+//   final[i]  = NormalizeScore(raw)[i] * weight,
+// with raw/final = EXPORT_NONE where the reference records no score (infeasible node, or the
+// pod never reaches Score: no feasible node / PreScore failed / no score plugin).
+// Not a hot path: O(P*N) writes of 17 B per pair.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void export_kernel(const uint8_t* __restrict__ unsched,
+                                                     const int8_t* __restrict__ digit, int32_t n,
+                                                     const int8_t* __restrict__ pod_digit,
+                                                     const uint8_t* __restrict__ pod_tol,
+                                                     PluginParams pp, uint8_t* __restrict__ filter,
+                                                     int64_t* __restrict__ raw,
+                                                     int64_t* __restrict__ fin) {
+  __shared__ int flags;  // bit0 feasible match, bit1 feasible non-match
+  const int32_t j = blockIdx.x;
+  const int pd = pod_digit[j];
+  const bool pd_valid = pd >= 0 && pd <= 9;
+  const bool tol = pod_tol[j] != 0;
+  if (threadIdx.x == 0) flags = 0;
+  __syncthreads();
+  int f = 0;
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const bool feas = !(pp.has_nu_filter && unsched[i] && !tol);
+    const int d = digit[i];
+    if (feas) f |= (pd_valid && d == pd) ? 1 : 2;
+  }
+  if (f) atomicOr(&flags, f);
+  __syncthreads();
+  const bool hm = flags & 1, hx = flags & 2;
+  const bool scored = (hm || hx) && pp.has_nn_score && pp.nn_prescore && pd_valid;
+  const int64_t w = pp.weight;
+  const size_t row = (size_t)j * (size_t)n;
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const bool feas = !(pp.has_nu_filter && unsched[i] && !tol);
+    filter[row + i] = feas ? 1 : 0;
+    int64_t r = EXPORT_NONE, o = EXPORT_NONE;
+    if (scored && feas) {
+      const bool m = digit[i] == pd;
+      r = m ? 10 : 0;
+      switch (pp.mode) {
+        case 1: o = m ? 100 : 0; break;                      // max is 10 whenever a match exists
+        case 2: o = hm ? (m ? 0 : 100) : 100; break;         // reverse; max 0 -> all 100
+        case 3: o = (hm && hx) ? (m ? 100 : 0) : 0; break;   // min-max; max == min -> 0
+        default: o = r; break;
+      }
+      o *= w;
+    }
+    raw[row + i] = r;
+    fin[row + i] = o;
+  }
+}
+
+hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
+                         const int8_t* d_pod_digit, const uint8_t* d_pod_tol, int32_t p,
+                         const PluginParams& pp, uint8_t* d_filter, int64_t* d_raw, int64_t* d_fin,
+                         hipStream_t s) {
+  if (p <= 0 || n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(export_kernel, dim3(p), dim3(256), 0, s, d_unsched, d_digit, n, d_pod_digit,
+                     d_pod_tol, pp, d_filter, d_raw, d_fin);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void patch_nodes_kernel(const unsigned long long* __restrict__ entries,
                                                           int32_t count, uint8_t* __restrict__ unsched,
                                                           int8_t* __restrict__ digit) {

@@ -103,6 +103,19 @@ class DeviceContext:
             raise ValueError("idx / unsched / digit length mismatch")
         self._check(self._lib.msh_patch_nodes(self.handle, len(idx), N.ptr(idx), N.ptr(unsched), N.ptr(digit)))
 
+    def export_results(self, pod_digit: np.ndarray, pod_tol: np.ndarray):
+        """Per-pair plugin results [p, n]: (filter uint8, raw score int64, final score int64);
+        scores are N.MSH_EXPORT_NONE where none is recorded (msh_export_results)."""
+        pod_digit = np.ascontiguousarray(pod_digit, np.int8)
+        pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
+        p, n = len(pod_digit), int(self.n_nodes)
+        filt = np.empty((p, n), np.uint8)
+        raw = np.empty((p, n), np.int64)
+        fin = np.empty((p, n), np.int64)
+        self._check(self._lib.msh_export_results(self.handle, p, N.ptr(pod_digit), N.ptr(pod_tol),
+                                                 N.ptr(filt), N.ptr(raw), N.ptr(fin)))
+        return filt, raw, fin
+
     # -- host-buffer entry points --
     def schedule_batch(self, pod_digit: np.ndarray, pod_tol: np.ndarray):
         pod_digit = np.ascontiguousarray(pod_digit, np.int8)
