@@ -18,11 +18,15 @@
 //
 // The score of a pair under the reference plugin set is 10*w if the node is feasible and
 // its suffix digit equals the pod's, else 0, so selectHost's first max is "first feasible
-// match, else first feasible". The IDENT path evaluates each pair with ONE v_sad_u32:
-//     t = |(D << 24) - (pd << 24)| + cost,  cost = idx (feasible) | NOFIT (infeasible)
-// t < 2^24 iff feasible AND digits equal, and then t == idx: the unsigned min over nodes is
-// the first feasible match (v_min3_u32 folds two pairs per instruction): 1.5 VALU per 64
-// pairs, no VCC/SGPR lane masks (no VALU->SGPR->VALU hazard wait states).
+// match, else first feasible". The IDENT path (ident_kernel, the default) packs two nodes
+// per 32-bit word, 16 bits each: (code << 12) | (chunk mod 1008), code = the node's digit if
+// it is feasible for non-tolerating pods, else 15. A pod pair sits in one SGPR as
+// (codeB << 28) | (codeA << 12); per word the pair costs
+//     x = W ^ PP      (v_xor_b32)      -> a half is < 2^12 iff that node matches that pod
+//     bm = pk_min(bm, x)  (v_pk_min_u16) -> running first match per pod, both halves at once
+// i.e. ONE lane-op per (pod, node) evaluation. Nodes feasible only for tolerating pods are
+// corrected afterwards from a short list (ulist). The KX path (batch_kernel) serves the
+// REVERSE / MINMAX normalizers, which also need the first feasible non-match.
 // See DESIGN.md for the roofline / instruction budget of each kernel.
 #include "msh_internal.h"
 

@@ -1,0 +1,25 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py: kernel-trace stats of the bench command itself, then one
+# --pmc pass per HBM counter (FETCH_SIZE, WRITE_SIZE; never combined with tracing domains).
+# Every GPU step has its own limit; the script stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/prof_r1
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+BENCH="bench.py --steps ${STEPS:-50} --warmup ${WARMUP:-5}"
+step() {  # $1 = tag, $2.. = rocprofv3 options (before --)
+  local tag=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$tag" -o run --output-format csv -- python $BENCH ${MODE_ARGS:-} > "$OUT/$tag.log" 2>&1
+  local rc=$?
+  echo "[$tag] rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+  tail -1 "$OUT/$tag.log" | cut -c1-200
+}
+step stats --kernel-trace --stats
+step fetch --pmc FETCH_SIZE
+step write --pmc WRITE_SIZE
+MODE_ARGS="--mode sequential" step seq_stats --kernel-trace --stats
+MODE_ARGS="--mode sequential" step seq_fetch --pmc FETCH_SIZE
+MODE_ARGS="--mode sequential" step seq_write --pmc WRITE_SIZE
+echo profile-done
