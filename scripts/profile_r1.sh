@@ -16,6 +16,9 @@ step() {  # $1 = tag, $2.. = rocprofv3 options (before --)
   [ $rc -eq 0 ] || exit $rc
   tail -1 "$OUT/$tag.log" | cut -c1-200
 }
+# FETCH_SIZE calibration for 1 / 4 / 16 B-per-lane streaming reads (known byte counts)
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib" -o run --output-format csv -- ./scripts/calib_fetch > "$OUT/calib.log" 2>&1
+rc=$?; echo "[calib] rc=$rc"; [ $rc -eq 0 ] || exit $rc
 step stats --kernel-trace --stats
 step fetch --pmc FETCH_SIZE
 step write --pmc WRITE_SIZE
