@@ -393,7 +393,9 @@ __device__ __forceinline__ uint32_t pk_shl6(uint32_t a) {
 
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ uint32_t dpp_pkmin(uint32_t v) {
-  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, CTRL, ROW_MASK, 0xF, false);
+  // Rows masked off by ROW_MASK (row_bcast steps) get an undefined `t`; the min then leaves
+  // garbage only in rows whose values never reach lane 63, the one lane read at the end.
+  const uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, ROW_MASK, 0xF, false);
   return pk_min_u16(v, t);
 }
 
@@ -408,24 +410,80 @@ __device__ __forceinline__ uint32_t wave_pkmin_u16(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Two independent wave-wide packed u16 mins, interleaved step by step.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void dpp_pkmin_x2(uint32_t& a, uint32_t& b) {
+  const uint32_t ta = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, CTRL, ROW_MASK, 0xF, false);
+  const uint32_t tb = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, CTRL, ROW_MASK, 0xF, false);
+  a = pk_min_u16(a, ta);
+  b = pk_min_u16(b, tb);
+}
+
+__device__ __forceinline__ void wave_pkmin_u16_x2(uint32_t& a, uint32_t& b) {
+  dpp_pkmin_x2<0xB1, 0xF>(a, b);
+  dpp_pkmin_x2<0x4E, 0xF>(a, b);
+  dpp_pkmin_x2<0x141, 0xF>(a, b);
+  dpp_pkmin_x2<0x140, 0xF>(a, b);
+  dpp_pkmin_x2<0x142, 0xA>(a, b);
+  dpp_pkmin_x2<0x143, 0xC>(a, b);
+  a = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
+  b = (uint32_t)__builtin_amdgcn_readlane((int)b, 63);
+}
+
 constexpr int IDENT_THREADS = 512;
 #ifndef MSH_QB
 #define MSH_QB 4
 #endif
-#ifndef MSH_PREFETCH
-#define MSH_PREFETCH 0
-#endif
 constexpr int QB = MSH_QB;  // pod pairs per interleaved block (independent v_pk_min chains)
 constexpr uint32_t NOMATCH16 = 0xFFC0u;  // (1023 << 6): above every chunk<<6|lane of a tile
+
+// R chunks of node words (one dword per lane each) starting at chunk c0 of the slice.
+// DIRECT: buffer loads off a wave-uniform descriptor; the per-lane offsets are loop-invariant
+// VGPRs and the block offset an SGPR, so the scan loop spends no VALU on addressing.
+template <bool DIRECT, int R>
+__device__ __forceinline__ void load_words(uint32_t (&w)[R], const uint32_t* __restrict__ words,
+                                           __amdgpu_buffer_rsrc_t rs, int32_t c0, int lane) {
+  if constexpr (DIRECT) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      w[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, (lane + r * WAVE) * 4, c0 * (WAVE * 4), 0);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) w[r] = words[(c0 + r) * WAVE + lane];
+  }
+}
+
+// 2 VALU per 2 x 64 pairs: x = W ^ PP (pod pair in an SGPR), bm = pk_min(bm, x).
+template <int R, int GQ>
+__device__ __forceinline__ void scan_words(const uint32_t (&w)[R], const uint32_t (&pp)[GQ],
+                                           uint32_t (&bm)[GQ], int32_t cnt) {
+#pragma unroll
+  for (int qb = 0; qb < GQ; qb += QB) {
+    if (qb < cnt) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        uint32_t x[QB];
+#pragma unroll
+        for (int q = 0; q < QB; ++q) x[q] = w[r] ^ pp[qb + q];
+#pragma unroll
+        for (int q = 0; q < QB; ++q) bm[qb + q] = pk_min_u16(bm[qb + q], x[q]);
+      }
+    }
+  }
+}
 
 // One group of up to GQ pod pairs taken from `mask` (lanes of the window), scanned against
 // node words [0, nc) chunks of the current tile slice; results min-merged into `res`.
 // `node_base` = global index of chunk 0 of the compute tile the slice belongs to.
-template <int R, int GQ>
+// nc is a multiple of 2R: two register blocks alternate (load one, scan the other) with no
+// copies between them.
+template <int R, int GQ, bool DIRECT>
 __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t pcv, uint32_t& res,
-                                            const uint32_t* __restrict__ words, int32_t nc,
+                                            const uint32_t* __restrict__ words,
+                                            __amdgpu_buffer_rsrc_t rs, int32_t nc,
                                             uint32_t node_base, int lane) {
   static_assert(GQ % QB == 0, "GQ must be a multiple of QB");
+  static_assert(GQ % 2 == 0, "pairs are reduced two at a time");
   uint32_t pp[GQ];
   int32_t la[GQ], lb[GQ];
   int32_t cnt = 0;
@@ -450,50 +508,35 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
   uint32_t bm[GQ];
 #pragma unroll
   for (int q = 0; q < GQ; ++q) bm[q] = 0xFFFFFFFFu;
-  // MSH_PREFETCH: software-pipelined, the next sub-tile's words are in flight while this one
-  // is scanned (A/B option; the default relies on the other waves of the SIMD instead)
-  uint32_t w[R], wn[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) w[r] = words[r * WAVE + lane];
-  for (int32_t c0 = 0; c0 < nc; c0 += R) {
-    const int32_t cn = (c0 + R < nc) ? c0 + R : c0;  // last round re-reads (harmless, cached)
-    if (MSH_PREFETCH) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) wn[r] = words[(cn + r) * WAVE + lane];
-    }
-#pragma unroll
-    for (int qb = 0; qb < GQ; qb += QB) {
-      if (qb < cnt) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          uint32_t x[QB];
-#pragma unroll
-          for (int q = 0; q < QB; ++q) x[q] = w[r] ^ pp[qb + q];
-#pragma unroll
-          for (int q = 0; q < QB; ++q) bm[qb + q] = pk_min_u16(bm[qb + q], x[q]);
-        }
-      }
-    }
-    if (MSH_PREFETCH) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) w[r] = wn[r];
-    } else if (c0 + R < nc) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) w[r] = words[(cn + r) * WAVE + lane];
-    }
+  uint32_t wa[R], wb[R];
+  load_words<DIRECT>(wa, words, rs, 0, lane);
+  for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
+    load_words<DIRECT>(wb, words, rs, c0 + R, lane);
+    scan_words<R, GQ>(wa, pp, bm, cnt);
+    if (c0 + 2 * R < nc) load_words<DIRECT>(wa, words, rs, c0 + 2 * R, lane);
+    scan_words<R, GQ>(wb, pp, bm, cnt);
   }
   // ---- stage 4: fold in the lane, packed DPP min across the wave, into the pods' lanes ----
+  // Two pairs at a time: the two DPP chains fill each other's VALU->DPP hazard slots.
   const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);
 #pragma unroll
-  for (int q = 0; q < GQ; ++q) {
+  for (int q = 0; q < GQ; q += 2) {
     if (q < cnt) {
       // halves >= 4096 (no match) saturate to chunk 1023 -> 0xFFC0 | lane after the shift
-      const uint32_t v = wave_pkmin_u16(pk_shl6(pk_min_u16(bm[q], 0x03FF03FFu)) | lane2);
-      const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
-      const uint32_t ga = lo < NOMATCH16 ? node_base + lo : NOFIT;
-      const uint32_t gb = hi < NOMATCH16 ? node_base + hi : NOFIT;
-      res = (lane == la[q]) ? umin(res, ga) : res;
-      res = (lane == lb[q]) ? umin(res, gb) : res;
+      uint32_t v0 = pk_shl6(pk_min_u16(bm[q], 0x03FF03FFu)) | lane2;
+      uint32_t v1 = pk_shl6(pk_min_u16(bm[q + 1], 0x03FF03FFu)) | lane2;
+      wave_pkmin_u16_x2(v0, v1);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (q + k < cnt) {
+          const uint32_t v = k ? v1 : v0;
+          const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
+          const uint32_t ga = lo < NOMATCH16 ? node_base + lo : NOFIT;
+          const uint32_t gb = hi < NOMATCH16 ? node_base + hi : NOFIT;
+          res = (lane == la[q + k]) ? umin(res, ga) : res;
+          res = (lane == lb[q + k]) ? umin(res, gb) : res;
+        }
+      }
     }
   }
 }
@@ -545,6 +588,9 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
     }
     MSH_STAMP(1);
     const bool last_stage = (st == nstages - 1);
+    // wave-uniform descriptor over this slice's words (DIRECT); unused for the LDS variant
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)words, (short)0, DIRECT ? nc * WAVE * (int32_t)sizeof(uint32_t) : 0, 0x00020000);
 
     for (int32_t w0 = p0; w0 < p1; w0 += WAVE) {
       const int32_t nwin = min((int32_t)WAVE, p1 - w0);
@@ -559,7 +605,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       if (st > 0 && act) res = a.partial[w0 + lane];
       unsigned long long m = __ballot(act && pcv != CODE_NONE_POD);
       MSH_STAMP(2);
-      while (m) ident_group<R, G2>(m, pcv, res, words, nc, tile_node_base, lane);
+      while (m) ident_group<R, G2, DIRECT>(m, pcv, res, words, rs, nc, tile_node_base, lane);
       MSH_STAMP(3);
 
       // tolerating pods: the class-1-only nodes (ulist), once (first stage)
