@@ -46,9 +46,13 @@ struct DeviceInfo {
 
 // ---- launchers (msh_kernels.hip) ----
 // Packed-16 first-match words (IDENT batch path): per node i (chunk c = i / 64, lane i % 64),
-//   w16 = (code << 12) | (c mod TILE_CHUNKS),  code = node digit if the node is feasible for
-//   pods that do NOT tolerate the unschedulable taint (class 0) and its name ends in '0'..'9',
-//   else 15 (never equals a pod code 0..9).
+//   w16 = (code << CODE_SHIFT) | (c mod TILE_CHUNKS),  code = node digit if the node is feasible
+//   for pods that do NOT tolerate the unschedulable taint (class 0) and its name ends in
+//   '0'..'9', else 15 (never equals a pod code 0..9 or 14).
+// With the 4-bit code in bits 10..13 and bits 14..15 zero, w16 ^ (pod code << 10) read as an
+// f16 is a subnormal equal to the chunk exactly on a match and a finite normal number (exponent
+// 1..15) otherwise, never inf or NaN: its f16 order is its integer order, so the IEEE
+// v_pk_minimum3_f16 folds two node words per instruction.
 // w0 holds w16 in both 16-bit halves, so one v_xor_b32 serves two pods. Within one lane the
 // nodes are ordered by chunk, so the per-lane minimum only needs the chunk number; the lane
 // is folded back in (chunk << 6 | lane = node index in the tile) before the cross-lane min.
@@ -61,6 +65,7 @@ constexpr int TILE_CHUNKS = 1008;                 // 16 * 63
 constexpr int TILE_NODES = TILE_CHUNKS * 64;
 constexpr int STAGE_CHUNKS = TILE_CHUNKS / 3;     // LDS stage: 336 chunks = 86,016 B
 constexpr uint32_t CODE_NONE_NODE = 15u;
+constexpr int CODE_SHIFT = 10;                    // code bits 10..13 of a w16 half
 constexpr uint32_t CODE_NONE_POD = 14u;
 
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,

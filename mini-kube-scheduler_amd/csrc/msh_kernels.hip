@@ -18,15 +18,17 @@
 //
 // The score of a pair under the reference plugin set is 10*w if the node is feasible and
 // its suffix digit equals the pod's, else 0, so selectHost's first max is "first feasible
-// match, else first feasible". The IDENT path (ident_kernel, the default) packs two nodes
-// per 32-bit word, 16 bits each: (code << 12) | (chunk mod 1008), code = the node's digit if
-// it is feasible for non-tolerating pods, else 15. A pod pair sits in one SGPR as
-// (codeB << 28) | (codeA << 12); per word the pair costs
-//     x = W ^ PP      (v_xor_b32)      -> a half is < 2^12 iff that node matches that pod
-//     bm = pk_min(bm, x)  (v_pk_min_u16) -> running first match per pod, both halves at once
-// i.e. ONE lane-op per (pod, node) evaluation. Nodes feasible only for tolerating pods are
-// corrected afterwards from a short list (ulist). The KX path (batch_kernel) serves the
-// REVERSE / MINMAX normalizers, which also need the first feasible non-match.
+// match, else first feasible". The IDENT path keeps one node per 16-bit half of a word,
+// duplicated in both halves: (code << 10) | (chunk mod 1008), code = the node's digit if it
+// is feasible for non-tolerating pods, else 15. A pod pair sits in one SGPR as
+// (codeB << 26) | (codeA << 10); per word and pair
+//     x = W ^ PP      (v_xor_b32)  -> a half is < 1024 iff that node matches that pod
+// and two such words fold into the running first match of both pods with ONE
+//     bm = v_pk_minimum3_f16(bm, x_r, x_r+1)
+// (every half is a non-negative finite f16, so its f16 order is its integer order): 0.75
+// lane-ops per (pod, node) evaluation. Nodes feasible only for tolerating pods are corrected
+// afterwards from a short list (ulist). The KX path (batch_kernel) serves the REVERSE /
+// MINMAX normalizers, which also need the first feasible non-match.
 // See DESIGN.md for the roofline / instruction budget of each kernel.
 #include "msh_internal.h"
 
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
   c0[i] = feas0 ? (uint32_t)i : NOFIT;
   dig[i] = has_digit ? (uint8_t)d : (uint8_t)DIGIT_NONE;
   const uint32_t local_chunk = (uint32_t)(i >> 6) % (uint32_t)TILE_CHUNKS;
-  const uint32_t wd0 = ((feas0 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << 12) | local_chunk;
+  const uint32_t wd0 = ((feas0 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << CODE_SHIFT) | local_chunk;
   w0[i] = wd0 | (wd0 << 16);
   const unsigned long long m0 = __ballot(feas0);
   const unsigned long long m1 = __ballot(feas1);
@@ -365,13 +367,13 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
 // IDENT batched kernel (normalize NONE / DEFAULT, i.e. the reference plugin set): packed-16.
 // Workgroup = 8 waves. Each wave owns a contiguous pod range, walked in windows of 64 pods,
 // processed in groups of G2 pod PAIRS. A pair's two pod codes sit in one SGPR
-//   PP = (code_B << 28) | (code_A << 12)
-// and every node word holds (code << 12 | chunk) in both 16-bit halves, so
+//   PP = (code_B << 26) | (code_A << 10)
+// and every node word holds (code << 10 | chunk) in both 16-bit halves, so
 //   x = W ^ PP        -> low half: (pod A, node) pair, high half: (pod B, node) pair;
-//                        a half is < 4096 exactly when the node is feasible and its digit
+//                        a half is < 1024 exactly when the node is feasible and its digit
 //                        equals the pod's, and then it IS the node's chunk in the tile
-//   bm = v_pk_min_u16(bm, x)   -> per lane, the first matching chunk for both pods
-// = 2 VALU per 2 x 64 (pod, node) pairs (1.0 VALU per 64 pairs). At the end of a tile the
+//   bm = v_pk_minimum3_f16(bm, x_r, x_r+1) -> per lane, the first matching chunk for both pods
+// = 3 VALU per 4 x 64 (pod, node) pairs. At the end of a tile the
 // lane is folded in (chunk << 6 | lane = node index) and one packed DPP min per pair gives
 // both pods' first feasible match. Node words come from LDS (staged once per workgroup,
 // 4 B/node) or, DIRECT, straight from L1/L2. Pods that tolerate the unschedulable taint
@@ -431,6 +433,10 @@ __device__ __forceinline__ void wave_pkmin_u16_x2(uint32_t& a, uint32_t& b) {
 }
 
 constexpr int IDENT_THREADS = 512;
+#ifndef MSH_UNIT
+#define MSH_UNIT 8
+#endif
+constexpr int IDENT_UNIT = MSH_UNIT;  // pods per work-queue unit (ident_dyn_kernel): 2*QB
 #ifndef MSH_QB
 #define MSH_QB 4
 #endif
@@ -453,20 +459,46 @@ __device__ __forceinline__ void load_words(uint32_t (&w)[R], const uint32_t* __r
   }
 }
 
-// 2 VALU per 2 x 64 pairs: x = W ^ PP (pod pair in an SGPR), bm = pk_min(bm, x).
+#ifndef MSH_MIN3
+#define MSH_MIN3 1
+#endif
+// Largest finite f16 in both halves: "no match yet", and never a NaN for v_pk_minimum3_f16.
+constexpr uint32_t BM_INIT = 0x7BFF7BFFu;
+
+// Packed IEEE minimum of three f16 pairs, used as an integer min: every operand is a
+// non-negative finite f16 (see the w16 layout in msh_internal.h), whose order is its bit order.
+__device__ __forceinline__ uint32_t pk_min3_f16bits(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Per pod pair (SGPR PP) and two node words: x = W ^ PP (v_xor_b32, a half is < 1024 iff that
+// node matches that pod), bm = min3(bm, x_r, x_r+1) -> 3 VALU per 4 x 64 pairs (0.75 lane-op
+// per pair). MSH_MIN3=0: bm = pk_min_u16(bm, x), 1.0 lane-op per pair.
 template <int R, int GQ>
 __device__ __forceinline__ void scan_words(const uint32_t (&w)[R], const uint32_t (&pp)[GQ],
                                            uint32_t (&bm)[GQ], int32_t cnt) {
+  static_assert(R % 2 == 0, "chunks are folded two at a time");
 #pragma unroll
   for (int qb = 0; qb < GQ; qb += QB) {
     if (qb < cnt) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        uint32_t x[QB];
+      for (int r = 0; r < R; r += 2) {
+        uint32_t x[QB], y[QB];
 #pragma unroll
-        for (int q = 0; q < QB; ++q) x[q] = w[r] ^ pp[qb + q];
+        for (int q = 0; q < QB; ++q) {
+          x[q] = w[r] ^ pp[qb + q];
+          y[q] = w[r + 1] ^ pp[qb + q];
+        }
 #pragma unroll
-        for (int q = 0; q < QB; ++q) bm[qb + q] = pk_min_u16(bm[qb + q], x[q]);
+        for (int q = 0; q < QB; ++q) {
+          if (MSH_MIN3) {
+            bm[qb + q] = pk_min3_f16bits(bm[qb + q], x[q], y[q]);
+          } else {
+            bm[qb + q] = pk_min_u16(pk_min_u16(bm[qb + q], x[q]), y[q]);
+          }
+        }
       }
     }
   }
@@ -503,11 +535,11 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
         cb = (uint32_t)__builtin_amdgcn_readlane((int)pcv, lb[q]);
       }
     }
-    pp[q] = (cb << 28) | (ca << 12);
+    pp[q] = (cb << (16 + CODE_SHIFT)) | (ca << CODE_SHIFT);
   }
   uint32_t bm[GQ];
 #pragma unroll
-  for (int q = 0; q < GQ; ++q) bm[q] = 0xFFFFFFFFu;
+  for (int q = 0; q < GQ; ++q) bm[q] = BM_INIT;
   uint32_t wa[R], wb[R];
   load_words<DIRECT>(wa, words, rs, 0, lane);
   for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
@@ -653,6 +685,78 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
     msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + 7) * 2 + 1] = xcc;
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------------------
+// Work-queue IDENT kernel (default for single-tile node tables, DIRECT reads). Same per-pair
+// arithmetic as ident_kernel; the difference is how pods reach waves. With a static pod range
+// per wave, age-priority issue leaves the youngest wave of every SIMD running alone at the end
+// of the launch (per-wave stamps at C3: 18k..58k cycles for equal work), and a wave's last
+// partial group wastes pair slots. Here one workgroup of 16 waves per CU (4 per SIMD) owns a
+// contiguous pod range and its waves draw IDENT_UNIT-pod units (one QB block of pod pairs) from
+// an LDS counter until the range is spent: the SIMDs of a CU drain together, the tail is one
+// unit, and no global atomics or cross-launch state are involved.
+// ---------------------------------------------------------------------------------------
+constexpr int DYN_THREADS = 1024;
+
+template <int R, bool SHARD>
+__global__ __launch_bounds__(DYN_THREADS) void ident_dyn_kernel(BatchArgs a) {
+  __shared__ uint32_t next_unit;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int32_t nc = a.n_chunks;  // one compute tile: tile_node_base = 0
+  const uint32_t* words = a.w0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)words, (short)0, nc * WAVE * (int32_t)sizeof(uint32_t), 0x00020000);
+  const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
+  const uint32_t ucnt = *a.ucount;
+  const int32_t g0 = (int32_t)((int64_t)a.n_pods * blockIdx.x / gridDim.x);
+  const int32_t g1 = (int32_t)((int64_t)a.n_pods * (blockIdx.x + 1) / gridDim.x);
+  const int32_t n_units = (g1 - g0 + IDENT_UNIT - 1) / IDENT_UNIT;
+  if (threadIdx.x == 0) next_unit = 0;
+  __syncthreads();
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(&next_unit, 1u);
+    u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
+    if (u >= (uint32_t)n_units) break;
+    const int32_t w0 = g0 + (int32_t)u * IDENT_UNIT;
+    const int32_t nwin = min((int32_t)IDENT_UNIT, g1 - w0);
+    const bool act = lane < nwin;
+    uint32_t pcv = CODE_NONE_POD, tolv = 0;
+    if (act) {
+      const int d = a.pod_digit[w0 + lane];
+      pcv = (d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
+      tolv = a.pod_tol[w0 + lane] ? 1u : 0u;
+    }
+    uint32_t res = NOFIT;
+    unsigned long long m = __ballot(act && pcv != CODE_NONE_POD);
+    while (m) ident_group<R, IDENT_UNIT / 2, true>(m, pcv, res, words, rs, nc, 0u, lane);
+    unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
+    while (mt) {
+      const int32_t l = (int32_t)__builtin_ctzll(mt);
+      mt &= mt - 1;
+      const uint32_t pc24 = (uint32_t)__builtin_amdgcn_readlane((int)pcv, l) << 24;
+      uint32_t bu = 0xFFFFFFFFu;
+      for (uint32_t u0 = 0; u0 < ucnt; u0 += WAVE) {
+        const uint32_t k = u0 + (uint32_t)lane;
+        const uint32_t x = (k < ucnt ? a.ulist[k] : (CODE_NONE_NODE << 24)) ^ pc24;
+        bu = umin(bu, x);
+      }
+      const uint32_t vu = wave_min_u32(bu);
+      if (vu < MATCH_LIMIT) res = (lane == l) ? umin(res, vu) : res;
+    }
+    if (act) {
+      const int32_t j = w0 + lane;
+      const uint32_t ball = tolv ? ball1 : ball0;
+      if (SHARD) {
+        a.keys[j] = res != NOFIT ? (GKEY_MAX - (a.node_base + (int64_t)res)) : 0;
+        a.keys[(size_t)a.n_pods + j] = ball ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - ball))) : 0;
+      } else {
+        decode_pod(res != NOFIT ? (int64_t)res : -1, -1, key_to_idx(ball), pcv != CODE_NONE_POD, a.pp,
+                   &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
+      }
+    }
+  }
 }
 
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
@@ -1026,6 +1130,29 @@ hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(IDENT_THREADS), lds, s, a, lds_chunks);
   return hipGetLastError();
 }
+template <bool SHARD>
+hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
+                              std::string* err) {
+  auto kern = ident_dyn_kernel<IDENT_R, SHARD>;
+  const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), DYN_THREADS, 0);
+  if (occ < 1) {
+    if (err) *err = "ident work-queue kernel: zero occupancy";
+    return hipErrorInvalidConfiguration;
+  }
+  // two workgroups (32 waves) per CU: 8 waves per SIMD measured ~3% faster than 4 at C3;
+  // fewer when the batch is too small to give every wave a unit
+  const int64_t n_units = ((int64_t)a.n_pods + IDENT_UNIT - 1) / IDENT_UNIT;
+  int64_t grid = (int64_t)dev.cus * (occ < 2 ? occ : 2);
+  if (const char* env = getenv("MSH_BATCH_WG_PER_CU")) {
+    const int k = atoi(env);
+    if (k > 0) grid = (int64_t)dev.cus * (k < occ ? k : occ);
+  }
+  const int64_t grid_units = (n_units + DYN_THREADS / WAVE - 1) / (DYN_THREADS / WAVE);
+  if (grid > grid_units) grid = grid_units;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(DYN_THREADS), 0, s, a);
+  return hipGetLastError();
+}
 }  // namespace
 
 int32_t batch_tile_chunks(int32_t n_chunks) {
@@ -1041,10 +1168,12 @@ hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, h
                         std::string* err) {
   if (a.n_pods == 0) return hipSuccess;
   const bool kx = needs_kx(a.pp);
-  // MSH_BATCH_KERNEL (tuning / A-B only): 2 = IDENT direct (default), 0 = IDENT LDS-staged,
-  // 1 = compare/select kernel for every mode
+  // MSH_BATCH_KERNEL (tuning / A-B only): 3 = IDENT work queue (default when the table is one
+  // compute tile), 2 = IDENT direct static, 0 = IDENT LDS-staged, 1 = compare/select kernel
   const char* kenv = getenv("MSH_BATCH_KERNEL");
-  const int kv = kenv ? atoi(kenv) : 2;
+  const int kv = kenv ? atoi(kenv) : 3;
+  if (!kx && kv == 3 && a.n_chunks <= TILE_CHUNKS)
+    return shard ? launch_ident_dyn_t<true>(a, dev, s, err) : launch_ident_dyn_t<false>(a, dev, s, err);
   if (!kx && kv != 1) {
     if (kv == 0)
       return shard ? launch_ident_t<true, false>(a, dev, s, err) : launch_ident_t<false, false>(a, dev, s, err);
