@@ -36,7 +36,9 @@ METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
 VALU_PEAK_LANE_OPS = 157.3e12 / 2  # MI355X_MICROARCH.md: FP32 vector peak 157.3 TFLOPS = 2 x lane-ops/s
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # IDENT kernel inner loop: one v_xor_b32 + one v_pk_min_u16 per lane per TWO (pod, node) pairs
-LANE_OPS_PER_EVAL = 1.0
+# IDENT scan: per node word and pod pair one v_xor_b32, and one v_pk_minimum3_f16 per two
+# words -> 3 wave-instructions per 4 x 64 (pod, node) pairs
+LANE_OPS_PER_EVAL = 0.75
 # measured integer-VALU issue ceiling (scripts/ubench_valu.hip -> profiles/r1_ubench_valu.jsonl)
 UBENCH = ROOT / "profiles" / "r1_ubench_valu.jsonl"
 
@@ -44,7 +46,9 @@ UBENCH = ROOT / "profiles" / "r1_ubench_valu.jsonl"
 def measured_int_valu_ceiling() -> float | None:
     try:
         rows = [json.loads(l) for l in UBENCH.read_text().splitlines() if l.startswith("{") and "op" in l]
-        return max(r["lane_ops_per_s"] for r in rows if r["op"] == "xor+pk_min")
+        ops = {r["op"] for r in rows}
+        op = "2xor+pk_minimum3" if "2xor+pk_minimum3" in ops else "xor+pk_min"
+        return max(r["lane_ops_per_s"] for r in rows if r["op"] == op)
     except Exception:
         return None
 

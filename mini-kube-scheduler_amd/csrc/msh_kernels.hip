@@ -412,24 +412,34 @@ __device__ __forceinline__ uint32_t wave_pkmin_u16(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-// Two independent wave-wide packed u16 mins, interleaved step by step.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ void dpp_pkmin_x2(uint32_t& a, uint32_t& b) {
-  const uint32_t ta = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, CTRL, ROW_MASK, 0xF, false);
-  const uint32_t tb = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, CTRL, ROW_MASK, 0xF, false);
-  a = pk_min_u16(a, ta);
-  b = pk_min_u16(b, tb);
+// chunk << 6 | lane in both halves, "no match" halves (>= 1024) saturated to chunk 1023 first
+// (-> 0xFFC0 | lane, >= NOMATCH16): v_pk_min_u16 + v_pk_mad_u16 (bm * 64 + lane). Plain vector
+// arithmetic, not asm: the permlane swaps that read the result need the compiler to see the
+// VALU write (hazard wait states).
+__device__ __forceinline__ uint32_t pk_fold_lane(uint32_t bm, uint32_t lane2) {
+  const u16x2 c = __builtin_bit_cast(u16x2, pk_min_u16(bm, 0x03FF03FFu));
+  const u16x2 l = __builtin_bit_cast(u16x2, lane2);
+  const u16x2 k = {64, 64};
+  return __builtin_bit_cast(uint32_t, (u16x2)(c * k + l));
 }
 
-__device__ __forceinline__ void wave_pkmin_u16_x2(uint32_t& a, uint32_t& b) {
-  dpp_pkmin_x2<0xB1, 0xF>(a, b);
-  dpp_pkmin_x2<0x4E, 0xF>(a, b);
-  dpp_pkmin_x2<0x141, 0xF>(a, b);
-  dpp_pkmin_x2<0x140, 0xF>(a, b);
-  dpp_pkmin_x2<0x142, 0xA>(a, b);
-  dpp_pkmin_x2<0x143, 0xC>(a, b);
-  a = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
-  b = (uint32_t)__builtin_amdgcn_readlane((int)b, 63);
+// Wave-wide packed u16 min of FOUR registers at once. v_permlane32_swap folds a and b into one
+// register (a's 32-lane partial in lanes 0..31, b's in 32..63), likewise c and d; one
+// v_permlane16_swap folds those two into one register whose rows hold a, c, b, d; four in-row
+// DPP steps finish all four: 14 VALU for four pairs where four DPP trees take 48.
+// Row r of the result (any lane of it) holds: r=0 a, r=1 c, r=2 b, r=3 d.
+__device__ __forceinline__ uint32_t wave_pkmin_u16_x4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const auto ab = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  const auto cd = __builtin_amdgcn_permlane32_swap(c, d, false, false);
+  const uint32_t x = pk_min_u16(ab[0], ab[1]);
+  const uint32_t y = pk_min_u16(cd[0], cd[1]);
+  const auto xy = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+  uint32_t v = pk_min_u16(xy[0], xy[1]);
+  v = dpp_pkmin<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = dpp_pkmin<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = dpp_pkmin<0x141, 0xF>(v);  // row_half_mirror
+  v = dpp_pkmin<0x140, 0xF>(v);  // row_mirror: every lane of a row holds the row's min
+  return v;
 }
 
 constexpr int IDENT_THREADS = 512;
@@ -515,7 +525,7 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
                                             __amdgpu_buffer_rsrc_t rs, int32_t nc,
                                             uint32_t node_base, int lane) {
   static_assert(GQ % QB == 0, "GQ must be a multiple of QB");
-  static_assert(GQ % 2 == 0, "pairs are reduced two at a time");
+  static_assert(GQ % 4 == 0, "pairs are reduced four at a time");
   uint32_t pp[GQ];
   int32_t la[GQ], lb[GQ];
   int32_t cnt = 0;
@@ -548,25 +558,23 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
     if (c0 + 2 * R < nc) load_words<DIRECT>(wa, words, rs, c0 + 2 * R, lane);
     scan_words<R, GQ>(wb, pp, bm, cnt);
   }
-  // ---- stage 4: fold in the lane, packed DPP min across the wave, into the pods' lanes ----
-  // Two pairs at a time: the two DPP chains fill each other's VALU->DPP hazard slots.
+  // ---- stage 4: fold in the lane, then one transposed cross-lane min per 4 pairs ----
   const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);
 #pragma unroll
-  for (int q = 0; q < GQ; q += 2) {
-    if (q < cnt) {
-      // halves >= 4096 (no match) saturate to chunk 1023 -> 0xFFC0 | lane after the shift
-      uint32_t v0 = pk_shl6(pk_min_u16(bm[q], 0x03FF03FFu)) | lane2;
-      uint32_t v1 = pk_shl6(pk_min_u16(bm[q + 1], 0x03FF03FFu)) | lane2;
-      wave_pkmin_u16_x2(v0, v1);
+  for (int q0 = 0; q0 < GQ; q0 += 4) {
+    if (q0 < cnt) {
+      const uint32_t x = wave_pkmin_u16_x4(pk_fold_lane(bm[q0], lane2), pk_fold_lane(bm[q0 + 1], lane2),
+                                           pk_fold_lane(bm[q0 + 2], lane2), pk_fold_lane(bm[q0 + 3], lane2));
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        if (q + k < cnt) {
-          const uint32_t v = k ? v1 : v0;
+      for (int k = 0; k < 4; ++k) {
+        if (q0 + k < cnt) {
+          // pair k's two results sit in row {0, 2, 1, 3}[k]
+          const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)x, 16 * ((k & 1) * 2 + (k >> 1)));
           const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
           const uint32_t ga = lo < NOMATCH16 ? node_base + lo : NOFIT;
           const uint32_t gb = hi < NOMATCH16 ? node_base + hi : NOFIT;
-          res = (lane == la[q + k]) ? umin(res, ga) : res;
-          res = (lane == lb[q + k]) ? umin(res, gb) : res;
+          res = (lane == la[q0 + k]) ? umin(res, ga) : res;
+          res = (lane == lb[q0 + k]) ? umin(res, gb) : res;
         }
       }
     }

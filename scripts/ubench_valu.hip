@@ -34,6 +34,7 @@
 
 template <int KIND>
 __global__ void kern(uint32_t* out, int iters, uint32_t k) {
+  // small non-negative values: finite f16 bit patterns for the pk_minimum3 kind
   uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5,
            a6 = a0 + 6, a7 = a0 + 7;
   for (int i = 0; i < iters; ++i) {
@@ -43,9 +44,14 @@ __global__ void kern(uint32_t* out, int iters, uint32_t k) {
     if (KIND == 3) BLOCK16("v_pk_min_u16");
     if (KIND == 4) BLOCK16_3("v_sad_u32");
     if (KIND == 5) BLOCK16_3("v_min3_u32");
-    if (KIND == 6) {  // the IDENT inner pattern: xor then pk_min, 8 chains
+    if (KIND == 6) {  // the former IDENT inner pattern: xor then pk_min, 8 chains
       BLOCK16("v_xor_b32");
       BLOCK16("v_pk_min_u16");
+    }
+    if (KIND == 7) {  // the IDENT inner pattern: two xors per pk_minimum3, 8 chains
+      BLOCK16("v_xor_b32");
+      BLOCK16("v_xor_b32");
+      BLOCK16_3("v_pk_minimum3_f16");
     }
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
@@ -53,7 +59,7 @@ __global__ void kern(uint32_t* out, int iters, uint32_t k) {
 
 int main() {
   const char* names[] = {"v_add_u32", "v_xor_b32", "v_min_u32", "v_pk_min_u16", "v_sad_u32",
-                         "v_min3_u32", "xor+pk_min"};
+                         "v_min3_u32", "xor+pk_min", "2xor+pk_minimum3"};
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, 0);
   const int cus = prop.multiProcessorCount;
@@ -65,7 +71,7 @@ int main() {
   hipEventCreate(&e1);
   int clk_khz = 0;
   hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
-  for (int kind = 0; kind < 7; ++kind) {
+  for (int kind = 0; kind < 8; ++kind) {
     for (int waves_per_simd : {1, 2, 4, 8}) {
       const int threads = 256;  // 4 waves = 1 per SIMD per block
       const int blocks = cus * waves_per_simd;
@@ -78,6 +84,7 @@ int main() {
           case 4: hipLaunchKernelGGL(kern<4>, dim3(blocks), dim3(threads), 0, 0, out, iters, 3u); break;
           case 5: hipLaunchKernelGGL(kern<5>, dim3(blocks), dim3(threads), 0, 0, out, iters, 3u); break;
           case 6: hipLaunchKernelGGL(kern<6>, dim3(blocks), dim3(threads), 0, 0, out, iters, 3u); break;
+          case 7: hipLaunchKernelGGL(kern<7>, dim3(blocks), dim3(threads), 0, 0, out, iters, 3u); break;
         }
       };
       launch();
@@ -88,7 +95,7 @@ int main() {
       hipEventSynchronize(e1);
       float ms = 0;
       hipEventElapsedTime(&ms, e0, e1);
-      const double instr_per_wave = 16.0 * iters * (kind == 6 ? 2 : 1);
+      const double instr_per_wave = 16.0 * iters * (kind == 6 ? 2 : kind == 7 ? 3 : 1);
       const double total_wave_instr = instr_per_wave * blocks * 4;
       const double simd_cycles = ms * 1e-3 * 2.4e9;  // nominal 2.4 GHz
       const double ipc_simd = total_wave_instr / (cus * 4) / simd_cycles;
