@@ -66,6 +66,12 @@ constexpr int TILE_NODES = TILE_CHUNKS * 64;
 constexpr int STAGE_CHUNKS = TILE_CHUNKS / 3;     // LDS stage: 336 chunks = 86,016 B
 constexpr uint32_t CODE_NONE_NODE = 15u;
 constexpr int CODE_SHIFT = 10;                    // code bits 10..13 of a w16 half
+
+// Position of node i's word in w0: 4-chunk groups of 256 words, lane-major inside a group
+// (lane l's words for chunks 4g..4g+3 are contiguous: one 16-byte load per lane).
+__host__ __device__ inline uint32_t word_pos(uint32_t i) {
+  return (i & ~255u) | ((i & 63u) << 2) | ((i >> 6) & 3u);
+}
 constexpr uint32_t CODE_NONE_POD = 14u;
 
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,

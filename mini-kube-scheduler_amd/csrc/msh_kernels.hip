@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
   dig[i] = has_digit ? (uint8_t)d : (uint8_t)DIGIT_NONE;
   const uint32_t local_chunk = (uint32_t)(i >> 6) % (uint32_t)TILE_CHUNKS;
   const uint32_t wd0 = ((feas0 && has_digit ? (uint32_t)d : CODE_NONE_NODE) << CODE_SHIFT) | local_chunk;
-  w0[i] = wd0 | (wd0 << 16);
+  w0[word_pos(i)] = wd0 | (wd0 << 16);
   const unsigned long long m0 = __ballot(feas0);
   const unsigned long long m1 = __ballot(feas1);
   const int lane = threadIdx.x & 63;
@@ -453,19 +453,29 @@ constexpr int IDENT_UNIT = MSH_UNIT;  // pods per work-queue unit (ident_dyn_ker
 constexpr int QB = MSH_QB;  // pod pairs per interleaved block (independent v_pk_min chains)
 constexpr uint32_t NOMATCH16 = 0xFFC0u;  // (1023 << 6): above every chunk<<6|lane of a tile
 
-// R chunks of node words (one dword per lane each) starting at chunk c0 of the slice.
-// DIRECT: buffer loads off a wave-uniform descriptor; the per-lane offsets are loop-invariant
-// VGPRs and the block offset an SGPR, so the scan loop spends no VALU on addressing.
+// R chunks of node words (one dword per lane each) starting at chunk c0 of the slice (c0 and
+// R multiples of 4). The table is laid out in 4-chunk groups, lane-major (word_pos), so one
+// 16-byte load per lane brings 4 chunks. DIRECT: buffer_load_dwordx4 off a wave-uniform
+// descriptor; the per-lane offsets are loop-invariant VGPRs and the block offset an SGPR, so
+// the scan loop spends no VALU on addressing.
 template <bool DIRECT, int R>
 __device__ __forceinline__ void load_words(uint32_t (&w)[R], const uint32_t* __restrict__ words,
                                            __amdgpu_buffer_rsrc_t rs, int32_t c0, int lane) {
-  if constexpr (DIRECT) {
+  static_assert(R % 4 == 0, "whole 4-chunk groups");
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      w[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, (lane + r * WAVE) * 4, c0 * (WAVE * 4), 0);
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; ++r) w[r] = words[(c0 + r) * WAVE + lane];
+  for (int g = 0; g < R / 4; ++g) {
+    uint4 v;
+    if constexpr (DIRECT) {
+      const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + g * (4 * WAVE * 4),
+                                                           c0 * (WAVE * 4), 0);
+      v = __builtin_bit_cast(uint4, t);
+    } else {
+      v = reinterpret_cast<const uint4*>(words)[(c0 / 4 + g) * WAVE + lane];
+    }
+    w[4 * g + 0] = v.x;
+    w[4 * g + 1] = v.y;
+    w[4 * g + 2] = v.z;
+    w[4 * g + 3] = v.w;
   }
 }
 
@@ -552,12 +562,21 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
   for (int q = 0; q < GQ; ++q) bm[q] = BM_INIT;
   uint32_t wa[R], wb[R];
   load_words<DIRECT>(wa, words, rs, 0, lane);
+#ifdef MSH_DIAG_REUSE  // timing diagnostic only (wrong results): no node-word loads in the loop
+  load_words<DIRECT>(wb, words, rs, R, lane);
+  for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
+    scan_words<R, GQ>(wa, pp, bm, cnt);
+    scan_words<R, GQ>(wb, pp, bm, cnt);
+    wa[c0 & (R - 1)] += 1u;
+  }
+#else
   for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
     load_words<DIRECT>(wb, words, rs, c0 + R, lane);
     scan_words<R, GQ>(wa, pp, bm, cnt);
     if (c0 + 2 * R < nc) load_words<DIRECT>(wa, words, rs, c0 + 2 * R, lane);
     scan_words<R, GQ>(wb, pp, bm, cnt);
   }
+#endif
   // ---- stage 4: fold in the lane, then one transposed cross-lane min per 4 pairs ----
   const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);
 #pragma unroll
