@@ -43,7 +43,7 @@ struct msh_ctx {
   uint32_t* d_ulist = nullptr;
   uint32_t* d_ucount = nullptr;
   unsigned long long* d_mask = nullptr;
-  uint32_t* d_ball = nullptr;
+  uint32_t* d_ball = nullptr;      // [0..1] first-feasible keys, [2] ulist count
   int32_t* d_counts = nullptr;
   size_t node_cap = 0;
 
@@ -204,7 +204,10 @@ int msh_create(int device, msh_ctx** out_ctx) {
     delete c;
     return MSH_ERR_HIP;
   }
-  if (hipMalloc(&c->d_ball, 4 * sizeof(uint32_t)) != hipSuccess) {
+  const size_t scalar_bytes = 4 * sizeof(uint32_t);  // ball[2] + ucount
+  if (hipMalloc(&c->d_ball, scalar_bytes) != hipSuccess ||
+      hipMemset(c->d_ball, 0, scalar_bytes) != hipSuccess) {
+    (void)hipFree(c->d_ball);
     hipStreamDestroy(c->stream);
     delete c;
     return MSH_ERR_HIP;

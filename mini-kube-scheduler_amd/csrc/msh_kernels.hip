@@ -493,9 +493,35 @@ __device__ __forceinline__ uint32_t pk_min3_f16bits(uint32_t a, uint32_t b, uint
   return r;
 }
 
-// Per pod pair (SGPR PP) and two node words: x = W ^ PP (v_xor_b32, a half is < 1024 iff that
-// node matches that pod), bm = min3(bm, x_r, x_r+1) -> 3 VALU per 4 x 64 pairs (0.75 lane-op
-// per pair). MSH_MIN3=0: bm = pk_min_u16(bm, x), 1.0 lane-op per pair.
+// v_xor_b32 with both sources in VGPRs. gfx950 issues the all-VGPR VOP2 form of xor / add / and
+// at ~2 cycles per wave64 instruction on a SIMD32, but every form with an SGPR (or constant)
+// source, and v_min*/VOP3/VOP3P, at ~4 (scripts/ubench_valu3.hip, profiles/r1_ubench_valu3.jsonl):
+// the pod-pair code is therefore held in a VGPR (same value in every lane), not an SGPR.
+#ifndef MSH_XOR_VV
+#define MSH_XOR_VV 1
+#endif
+__device__ __forceinline__ uint32_t xor_vv(uint32_t a, uint32_t b) {
+  uint32_t r;
+  if (MSH_XOR_VV)
+    asm("v_xor_b32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  else
+    r = a ^ b;
+  return r;
+}
+
+// A wave-uniform value copied into a VGPR (one v_mov per group, outside the scan loop).
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t s) {
+  uint32_t r;
+  if (MSH_XOR_VV)
+    asm("v_mov_b32_e32 %0, %1" : "=v"(r) : "s"(s));
+  else
+    r = s;
+  return r;
+}
+
+// Per pod pair (PP, held in a VGPR) and two node words: x = W ^ PP (v_xor_b32, a half is < 1024
+// iff that node matches that pod), bm = min3(bm, x_r, x_r+1) -> 3 VALU per 4 x 64 pairs (0.75
+// lane-op per pair). MSH_MIN3=0: bm = pk_min_u16(bm, x), 1.0 lane-op per pair.
 template <int R, int GQ>
 __device__ __forceinline__ void scan_words(const uint32_t (&w)[R], const uint32_t (&pp)[GQ],
                                            uint32_t (&bm)[GQ], int32_t cnt) {
@@ -508,8 +534,8 @@ __device__ __forceinline__ void scan_words(const uint32_t (&w)[R], const uint32_
         uint32_t x[QB], y[QB];
 #pragma unroll
         for (int q = 0; q < QB; ++q) {
-          x[q] = w[r] ^ pp[qb + q];
-          y[q] = w[r + 1] ^ pp[qb + q];
+          x[q] = xor_vv(w[r], pp[qb + q]);
+          y[q] = xor_vv(w[r + 1], pp[qb + q]);
         }
 #pragma unroll
         for (int q = 0; q < QB; ++q) {
@@ -555,7 +581,7 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
         cb = (uint32_t)__builtin_amdgcn_readlane((int)pcv, lb[q]);
       }
     }
-    pp[q] = (cb << (16 + CODE_SHIFT)) | (ca << CODE_SHIFT);
+    pp[q] = to_vgpr((cb << (16 + CODE_SHIFT)) | (ca << CODE_SHIFT));
   }
   uint32_t bm[GQ];
 #pragma unroll
@@ -573,7 +599,10 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
   for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
     load_words<DIRECT>(wb, words, rs, c0 + R, lane);
     scan_words<R, GQ>(wa, pp, bm, cnt);
-    if (c0 + 2 * R < nc) load_words<DIRECT>(wa, words, rs, c0 + 2 * R, lane);
+    // DIRECT: the next block's load is issued unconditionally; past the slice the buffer
+    // descriptor's range check returns zeros, which are never scanned. A branch around it
+    // would merge two vmcnt states and make the wait before scan(wb) cover this load too.
+    if (DIRECT || c0 + 2 * R < nc) load_words<DIRECT>(wa, words, rs, c0 + 2 * R, lane);
     scan_words<R, GQ>(wb, pp, bm, cnt);
   }
 #endif
@@ -726,10 +755,17 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
 // ---------------------------------------------------------------------------------------
 constexpr int DYN_THREADS = 1024;
 
-template <int R, bool SHARD>
-__global__ __launch_bounds__(DYN_THREADS) void ident_dyn_kernel(BatchArgs a) {
+template <int R, bool SHARD, int NT = DYN_THREADS>
+__global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
   __shared__ uint32_t next_unit;
   const int lane = threadIdx.x & (WAVE - 1);
+#ifdef MSH_STAMPS
+  // diagnostic stamps: 0 entry, 1 first unit fetched, 2 its pods loaded, 3 its groups scanned,
+  // 4 its ulist scanned, 5 exit; slot 6 = units taken by this wave; 7 = hardware ids
+  const int64_t gw = (int64_t)blockIdx.x * (NT / WAVE) + (threadIdx.x >> 6);
+  uint32_t n_taken = 0;
+#endif
+  MSH_STAMP(0);
   const int32_t nc = a.n_chunks;  // one compute tile: tile_node_base = 0
   const uint32_t* words = a.w0;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -746,6 +782,10 @@ __global__ __launch_bounds__(DYN_THREADS) void ident_dyn_kernel(BatchArgs a) {
     if (lane == 0) u = atomicAdd(&next_unit, 1u);
     u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
     if (u >= (uint32_t)n_units) break;
+#ifdef MSH_STAMPS
+    const bool first_unit = n_taken++ == 0;
+    if (first_unit) MSH_STAMP(1);
+#endif
     const int32_t w0 = g0 + (int32_t)u * IDENT_UNIT;
     const int32_t nwin = min((int32_t)IDENT_UNIT, g1 - w0);
     const bool act = lane < nwin;
@@ -757,7 +797,13 @@ __global__ __launch_bounds__(DYN_THREADS) void ident_dyn_kernel(BatchArgs a) {
     }
     uint32_t res = NOFIT;
     unsigned long long m = __ballot(act && pcv != CODE_NONE_POD);
+#ifdef MSH_STAMPS
+    if (first_unit) MSH_STAMP(2);
+#endif
     while (m) ident_group<R, IDENT_UNIT / 2, true>(m, pcv, res, words, rs, nc, 0u, lane);
+#ifdef MSH_STAMPS
+    if (first_unit) MSH_STAMP(3);
+#endif
     unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
     while (mt) {
       const int32_t l = (int32_t)__builtin_ctzll(mt);
@@ -772,6 +818,9 @@ __global__ __launch_bounds__(DYN_THREADS) void ident_dyn_kernel(BatchArgs a) {
       const uint32_t vu = wave_min_u32(bu);
       if (vu < MATCH_LIMIT) res = (lane == l) ? umin(res, vu) : res;
     }
+#ifdef MSH_STAMPS
+    if (first_unit) MSH_STAMP(4);
+#endif
     if (act) {
       const int32_t j = w0 + lane;
       const uint32_t ball = tolv ? ball1 : ball0;
@@ -784,6 +833,17 @@ __global__ __launch_bounds__(DYN_THREADS) void ident_dyn_kernel(BatchArgs a) {
       }
     }
   }
+  MSH_STAMP(5);
+#ifdef MSH_STAMPS
+  if (lane == 0 && gw < STAMP_WAVES) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + 6) * 2] = n_taken;
+    msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + 7) * 2] = hw;
+    msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + 7) * 2 + 1] = xcc;
+  }
+#endif
 }
 
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
@@ -1157,28 +1217,40 @@ hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(IDENT_THREADS), lds, s, a, lds_chunks);
   return hipGetLastError();
 }
-template <bool SHARD>
-hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
-                              std::string* err) {
-  auto kern = ident_dyn_kernel<IDENT_R, SHARD>;
-  const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), DYN_THREADS, 0);
+template <bool SHARD, int NT>
+hipError_t launch_ident_dyn_nt(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err) {
+  auto kern = ident_dyn_kernel<IDENT_R, SHARD, NT>;
+  const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), NT, 0);
   if (occ < 1) {
     if (err) *err = "ident work-queue kernel: zero occupancy";
     return hipErrorInvalidConfiguration;
   }
-  // two workgroups (32 waves) per CU: 8 waves per SIMD measured ~3% faster than 4 at C3;
-  // fewer when the batch is too small to give every wave a unit
+  // 32 waves per CU (8 per SIMD) measured ~3% faster than 16 at C3; fewer workgroups when the
+  // batch is too small to give every wave a unit
+  constexpr int WPG = NT / WAVE;
+  const int wg_per_cu = 32 / WPG;
   const int64_t n_units = ((int64_t)a.n_pods + IDENT_UNIT - 1) / IDENT_UNIT;
-  int64_t grid = (int64_t)dev.cus * (occ < 2 ? occ : 2);
+  int64_t grid = (int64_t)dev.cus * (occ < wg_per_cu ? occ : wg_per_cu);
   if (const char* env = getenv("MSH_BATCH_WG_PER_CU")) {
     const int k = atoi(env);
     if (k > 0) grid = (int64_t)dev.cus * (k < occ ? k : occ);
   }
-  const int64_t grid_units = (n_units + DYN_THREADS / WAVE - 1) / (DYN_THREADS / WAVE);
+  const int64_t grid_units = (n_units + WPG - 1) / WPG;
   if (grid > grid_units) grid = grid_units;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(DYN_THREADS), 0, s, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, a);
   return hipGetLastError();
+}
+
+template <bool SHARD>
+hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
+                              std::string* err) {
+  // MSH_DYN_THREADS (tuning / A-B only): workgroup size of the work-queue kernel
+  const char* env = getenv("MSH_DYN_THREADS");
+  const int nt = env ? atoi(env) : DYN_THREADS;
+  if (nt == 256) return launch_ident_dyn_nt<SHARD, 256>(a, dev, s, err);
+  if (nt == 512) return launch_ident_dyn_nt<SHARD, 512>(a, dev, s, err);
+  return launch_ident_dyn_nt<SHARD, 1024>(a, dev, s, err);
 }
 }  // namespace
 

@@ -27,9 +27,21 @@ for k, v in per_kernel("calib").items():
 res = {"source": str(src), "method": "FETCH_SIZE, WRITE_SIZE in separate --pmc passes; KiB*1024; "
        "FETCH x2 (gfx950 streaming-read correction, calibrated 4/16 B per lane)",
        "fetch_calibration_bytes_per_fetch_byte": calib, "kernels": {}}
-for mode, (ft, wt, name, pods) in {"batch": ("fetch", "write", "void msh::ident_kernel<8, 8, false, true>", 100000),
-                                   "sequential": ("seq_fetch", "seq_write", "void msh::seq_kernel<12, 8, false, true>", 100000)}.items():
-    f, w = per_kernel(ft)[name], per_kernel(wt)[name]
+
+
+def pick(d, prefix):
+    """The hot kernel of a pass: the msh kernel whose name starts with `prefix`."""
+    names = [k for k in d if k.startswith(prefix)]
+    if len(names) != 1:
+        raise SystemExit(f"expected one {prefix}* kernel, found {names}")
+    return names[0]
+
+
+for mode, (ft, wt, prefix, pods) in {"batch": ("fetch", "write", "void msh::ident", 100000),
+                                     "sequential": ("seq_fetch", "seq_write", "void msh::seq_kernel", 100000)}.items():
+    fd, wd = per_kernel(ft), per_kernel(wt)
+    name = pick(fd, prefix)
+    f, w = fd[name], wd[name]
     res["kernels"][mode] = {"kernel": name, "fetch_raw_bytes": f, "fetch_bytes": 2 * f, "write_bytes": w,
                             "hbm_bytes_per_launch": 2 * f + w, "nodes": 5000, "pods": pods}
 # bench.py reads the batch entry (default mode)

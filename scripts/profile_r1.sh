@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/prof_r1
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="bench.py --steps ${STEPS:-50} --warmup ${WARMUP:-5}"
+BENCH="bench.py --steps ${STEPS:-50} --warmup ${WARMUP:-5} --cpu-seconds ${CPU_S:-0}"
 step() {  # $1 = tag, $2.. = rocprofv3 options (before --)
   local tag=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$tag" -o run --output-format csv -- python $BENCH ${MODE_ARGS:-} > "$OUT/$tag.log" 2>&1
