@@ -35,20 +35,22 @@ sys.path.insert(0, str(ROOT))
 METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
 VALU_PEAK_LANE_OPS = 157.3e12 / 2  # MI355X_MICROARCH.md: FP32 vector peak 157.3 TFLOPS = 2 x lane-ops/s
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# IDENT kernel inner loop: one v_xor_b32 + one v_pk_min_u16 per lane per TWO (pod, node) pairs
-# IDENT scan: per node word and pod pair one v_xor_b32, and one v_pk_minimum3_f16 per two
-# words -> 3 wave-instructions per 4 x 64 (pod, node) pairs
+# IDENT scan: per node word and pod pair one v_xor_b32 (all-VGPR form), and one
+# v_pk_minimum3_f16 per two words -> 3 wave-instructions per 4 x 64 (pod, node) pairs
 LANE_OPS_PER_EVAL = 0.75
-# measured integer-VALU issue ceiling (scripts/ubench_valu.hip -> profiles/r1_ubench_valu.jsonl)
-UBENCH = ROOT / "profiles" / "r1_ubench_valu.jsonl"
+# measured issue ceiling of exactly that instruction mix (2 x v_xor_b32 v,v + 1 v_pk_minimum3_f16,
+# 8 waves per SIMD): scripts/ubench_valu3.hip -> profiles/r1_ubench_valu3.jsonl
+UBENCH = ROOT / "profiles" / "r1_ubench_valu3.jsonl"
+UBENCH_OP = "v_xor_b32 vv x2 + v_pk_minimum3_f16"
+N_SIMD = 256 * 4
 
 
 def measured_int_valu_ceiling() -> float | None:
+    """Lane-ops/s of the scan's instruction mix at the best measured occupancy."""
     try:
-        rows = [json.loads(l) for l in UBENCH.read_text().splitlines() if l.startswith("{") and "op" in l]
-        ops = {r["op"] for r in rows}
-        op = "2xor+pk_minimum3" if "2xor+pk_minimum3" in ops else "xor+pk_min"
-        return max(r["lane_ops_per_s"] for r in rows if r["op"] == op)
+        rows = [json.loads(l) for l in UBENCH.read_text().splitlines() if l.startswith("{")]
+        ipc = max(r["wave_instr_per_simd_cycle@2.4GHz"] for r in rows if r.get("op") == UBENCH_OP)
+        return ipc * 2.4e9 * N_SIMD * 64
     except Exception:
         return None
 
@@ -63,6 +65,8 @@ def parse():
     ap.add_argument("--pods", type=int, default=None, help="pods per GPU (batch/sequential) or total (nodeshard)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="batch mode: independent batches pipelined over this many HIP streams")
     return ap.parse_args()
 
 
@@ -97,67 +101,98 @@ def main():
     ctx = msh.DeviceContext(local)
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
     unsched, node_digit = synth.make_nodes(n_total)[1:]
+    # Batch mode pipelines consecutive, independent batches over `nstreams` HIP streams (each with
+    # its own pod batch and output buffers): a launch reaches the 8 XCDs up to ~4.5 us apart
+    # (scripts/stamps_dyn.py), and on one stream every batch pays that skew plus the slowest XCD's
+    # tail before the next may start. Sequential mode carries node state from batch to batch and
+    # node-shard mode has a collective per step: both stay on one stream.
+    nstreams = args.streams if mode == "batch" else 1
     sharded = None
     if mode == "nodeshard":
         sharded = D.NodeShardedScheduler(ctx, unsched, node_digit, world, rank)
         node_base = sharded.shard.lo
         pod_digit, pod_tol = synth._make_pods_fast(p_total, synth.SEED)[1:]
+        batches = [(pod_digit, pod_tol)]
     else:
         ctx.upload_nodes(unsched, node_digit)
         node_base = 0
-        # pod-sharded weak scaling: rank r owns pods [r*P, (r+1)*P) of one global stream
-        pod_digit, pod_tol = synth._make_pods_fast(p_total * world, synth.SEED)[1:]
-        pod_digit = np.ascontiguousarray(pod_digit[rank * p_total:(rank + 1) * p_total])
-        pod_tol = np.ascontiguousarray(pod_tol[rank * p_total:(rank + 1) * p_total])
-    p = len(pod_digit)
-    d_pd = torch.from_numpy(pod_digit).to(dev)
-    d_pt = torch.from_numpy(pod_tol).to(dev)
-    d_idx = torch.empty(p, dtype=torch.int32, device=dev)
-    d_score = torch.empty(p, dtype=torch.int64, device=dev)
-    d_status = torch.empty(p, dtype=torch.int32, device=dev)
-    d_keys = torch.zeros(2 * p, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
+        # pod-sharded weak scaling: rank r owns pods [r*P*S, (r+1)*P*S) of one global stream,
+        # split into S batches of P pods (one per stream)
+        pd_all, pt_all = synth._make_pods_fast(p_total * world * nstreams, synth.SEED)[1:]
+        batches = []
+        for i in range(nstreams):
+            lo = (rank * nstreams + i) * p_total
+            batches.append((np.ascontiguousarray(pd_all[lo:lo + p_total]), np.ascontiguousarray(pt_all[lo:lo + p_total])))
+    p = len(batches[0][0])
+    bufs = []
+    for pod_digit, pod_tol in batches:
+        bufs.append({"pd": torch.from_numpy(pod_digit).to(dev), "pt": torch.from_numpy(pod_tol).to(dev),
+                     "idx": torch.empty(p, dtype=torch.int32, device=dev),
+                     "score": torch.empty(p, dtype=torch.int64, device=dev),
+                     "status": torch.empty(p, dtype=torch.int32, device=dev),
+                     "keys": torch.zeros(2 * p, dtype=torch.int64, device=dev)})
+    main_stream = torch.cuda.current_stream(dev)
+    streams = [main_stream] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
 
-    def step(ev0=None, ev1=None):
+    def step(k, ev0=None, ev1=None, single=False):
+        b = bufs[0] if single else bufs[k % nstreams]
+        st = main_stream if single else streams[k % nstreams]
+        sh = st.cuda_stream
         if ev0 is not None:
-            ev0.record(stream)
+            ev0.record(st)
         if mode == "batch":
-            ctx.schedule_batch_device(p, d_pd.data_ptr(), d_pt.data_ptr(), d_idx.data_ptr(), d_score.data_ptr(),
-                                      d_status.data_ptr(), sh)
+            ctx.schedule_batch_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["idx"].data_ptr(),
+                                      b["score"].data_ptr(), b["status"].data_ptr(), sh)
         elif mode == "sequential":
-            ctx.schedule_sequential_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, d_idx.data_ptr(),
-                                           d_score.data_ptr(), d_status.data_ptr(), sh)
+            ctx.schedule_sequential_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), 0, b["idx"].data_ptr(),
+                                           b["score"].data_ptr(), b["status"].data_ptr(), sh)
         else:
-            ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), node_base, d_keys.data_ptr(), sh)
+            ctx.shard_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), node_base, b["keys"].data_ptr(), sh)
         if ev1 is not None:
-            ev1.record(stream)
+            ev1.record(st)
         if mode == "nodeshard":  # RCCL all-reduce(MAX) of the per-shard keys, then decode
-            D.merge_shard_keys_(d_keys)
-            ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), d_keys.data_ptr(), d_idx.data_ptr(),
-                                   d_score.data_ptr(), d_status.data_ptr(), sh)
+            D.merge_shard_keys_(b["keys"])
+            ctx.decode_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["keys"].data_ptr(), b["idx"].data_ptr(),
+                                   b["score"].data_ptr(), b["status"].data_ptr(), sh)
 
-    for _ in range(args.warmup):
-        step()
+    def fork():  # the side streams start after everything already queued on the main stream
+        ev = torch.cuda.Event()
+        ev.record(main_stream)
+        for st in streams[1:]:
+            st.wait_event(ev)
+
+    def join():
+        for st in streams[1:]:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            main_stream.wait_event(ev)
+
+    fork()
+    for k in range(args.warmup):
+        step(k)
+    join()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
-    # Kernel time from HIP events on the launch stream. For batch / sequential one event pair
-    # brackets the whole timed region: every step is one launch of the hot kernel, and an event
-    # record between launches is itself a barrier + timestamp packet that costs ~3.5 us of GPU
-    # time and breaks back-to-back dispatch (scripts/host_overhead.py). Node-shard steps hold
-    # an RCCL all-reduce and a decode launch too, so there the shard kernel is bracketed per step.
+    # Device time from HIP events on the main stream bracketing the whole timed region (side
+    # streams fork from / join into it), divided by K: the interval at which batches complete.
+    # No event between launches: an event record is itself a barrier + timestamp packet that
+    # costs ~3.5 us of GPU time and breaks back-to-back dispatch (scripts/host_overhead.py).
+    # Node-shard steps hold an RCCL all-reduce and a decode launch too, so there the shard kernel
+    # is bracketed per step.
     per_step = mode == "nodeshard"
     evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
            if per_step else [(None, None)] * args.steps)
     r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    r0.record(stream)
-    for e0, e1 in evs:
-        step(e0, e1)
-    r1.record(stream)
+    r0.record(main_stream)
+    fork()
+    for k, (e0, e1) in enumerate(evs):
+        step(k, e0, e1)
+    join()
+    r1.record(main_stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -168,20 +203,35 @@ def main():
     else:
         kernel_ms = r0.elapsed_time(r1) / args.steps
 
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+    # Isolated launch time (outside the timed region): the same launches back to back on ONE
+    # stream, which is what rocprofv3's per-kernel average measures.
+    kernel_ms_isolated = kernel_ms
+    if nstreams > 1:
+        q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        q0.record(main_stream)
+        for k in range(args.steps):
+            step(k, single=True)
+        q1.record(main_stream)
+        torch.cuda.synchronize()
+        kernel_ms_isolated = q0.elapsed_time(q1) / args.steps
 
-    # ---- correctness spot-check of the last step against the independent closed form ----
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms, kernel_ms_isolated], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms, kernel_ms_isolated = float(t[0]), float(t[1]), float(t[2])
+
+    # ---- correctness spot-check of every buffer's last batch against the independent closed form ----
     check = "skipped"
     if rank == 0 and not args.no_check:
         sys.path.insert(0, str(ROOT / "tests"))
         from closed_form import closed_form  # independent checker, not the oracle
-        ci, cs, cst = closed_form(unsched, node_digit, pod_digit, pod_tol)
-        gi, gs, gst = d_idx.cpu().numpy(), d_score.cpu().numpy(), d_status.cpu().numpy()
-        ok = (gi == ci).all() and (gs == cs).all() and (gst == cst).all()
+        ok = True
+        for (pod_digit, pod_tol), b in zip(batches, bufs):
+            ci, cs, cst = closed_form(unsched, node_digit, pod_digit, pod_tol)
+            gi, gs, gst = b["idx"].cpu().numpy(), b["score"].cpu().numpy(), b["status"].cpu().numpy()
+            ok = ok and (gi == ci).all() and (gs == cs).all() and (gst == cst).all()
         check = "bit-exact vs closed form" if ok else "MISMATCH"
+    pod_digit, pod_tol = batches[0]
 
     n_local = ctx.n_nodes
     evals_total = float(n_total) * float(p if mode != "nodeshard" else p_total) * args.steps * (world if mode != "nodeshard" else 1)
@@ -214,6 +264,12 @@ def main():
             "note": "one pod at a time: scan + 2 wave reductions + 1 workgroup barrier per pod",
         }
     else:
+        shard = mode == "nodeshard"
+        # launcher dispatch (msh_kernels.hip launch_batch): one compute tile (<= 64,512 nodes) ->
+        # the work-queue kernel, else the tiled static kernel
+        kname = (f"ident_dyn_kernel<8, {str(shard).lower()}, 1024>" if n_local <= 64512
+                 else f"ident_kernel<8, 8, {str(shard).lower()}, true>")
+        iso_s = kernel_ms_isolated * 1e-3
         roofline = {
             "bound": "valu",
             "achieved": lane_ops / kern_s / 1e9,
@@ -221,8 +277,13 @@ def main():
             "unit": "Glane-op/s",
             "frac": lane_ops / kern_s / VALU_PEAK_LANE_OPS,
             "traffic": traffic,
-            "kernel": "ident_kernel",
+            "kernel": kname,
             "kernel_ms": kernel_ms,
+            "kernel_ms_note": (f"interval at which launches complete with {nstreams} streams in flight; "
+                               "kernel_ms_isolated = the same launches back to back on one stream "
+                               "(= rocprofv3's per-kernel average)") if nstreams > 1 else "one stream",
+            "kernel_ms_isolated": kernel_ms_isolated,
+            "frac_isolated": lane_ops / iso_s / VALU_PEAK_LANE_OPS,
             "lane_ops_per_eval": LANE_OPS_PER_EVAL,
             "measured_int_valu_ceiling": ceiling / 1e9 if ceiling else None,
             "frac_vs_measured_int_ceiling": (lane_ops / kern_s / ceiling) if ceiling else None,
@@ -241,7 +302,8 @@ def main():
 
     if rank == 0:
         if mode == "batch":
-            wl = f"C3 batched: {n_total} nodes x {p} pods per GPU (pod-sharded over {world} GPU)"
+            wl = (f"C3 batched: {n_total} nodes x {p} pods per batch per GPU (pod-sharded over {world} GPU; "
+                  f"{nstreams} independent batches in flight on {nstreams} HIP streams)")
         elif mode == "sequential":
             wl = f"C5 sequential-commit: {n_total} nodes x {p} pods per GPU, one pod at a time"
         else:
@@ -261,7 +323,8 @@ def main():
             "data": "synthetic (splitmix64 seed 0x6d696e69: 10% unschedulable nodes, 1% non-digit pods, 5% tolerating)",
             "config": {"workload": wl, "nodes": n_total, "pods_per_step": int(p if mode != "nodeshard" else p_total),
                        "plugins": "filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber w=1]",
-                       "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}"},
+                       "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}",
+                       "streams": nstreams},
             "pods_per_s": pods_total / elapsed,
             "check": check,
             "roofline": roofline,

@@ -45,6 +45,8 @@ def _stale(target: Path, deps: list[Path]) -> bool:
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the kernels + C-ABI for gfx950 and link libminisched_hip.so."""
+    if not force and not _stale(LIB, [CSRC / src for src, _, _ in SOURCES] + HEADERS):
+        return LIB  # up to date (objects need not be present, e.g. on the GPU box)
     OBJ.mkdir(exist_ok=True)
     objs = []
     for src, cc, extra in SOURCES:
@@ -79,6 +81,9 @@ def build_diagnostic(verbose: bool = False) -> Path:
 def build_variant(defines: list[str], tag: str, verbose: bool = False) -> Path:
     """A/B build of the library with extra -D flags: libminisched_hip_<tag>.so (tuning only)."""
     out = PKG_DIR / f"libminisched_hip_{tag}.so"
+    if not _stale(out, [CSRC / src for src, _, _ in SOURCES] + HEADERS):
+        return out
+    OBJ.mkdir(exist_ok=True)
     objs = []
     for src, cc, extra in SOURCES:
         s = CSRC / src

@@ -1,7 +1,8 @@
 #!/bin/bash
-# rocprofv3 evidence for bench.py: kernel-trace stats of the bench command itself, then one
-# --pmc pass per HBM counter (FETCH_SIZE, WRITE_SIZE; never combined with tracing domains).
-# Every GPU step has its own limit; the script stops at the first failure.
+# rocprofv3 evidence for bench.py: kernel-trace stats of the bench command itself (default =
+# 2 streams, and --streams 1 for the isolated per-launch time), then one --pmc pass per HBM
+# counter (FETCH_SIZE, WRITE_SIZE; never combined with tracing domains), plus the VALU issue-rate
+# microbenchmarks. Every GPU step has its own limit; the script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/prof_r1
@@ -20,9 +21,14 @@ step() {  # $1 = tag, $2.. = rocprofv3 options (before --)
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib" -o run --output-format csv -- ./scripts/calib_fetch > "$OUT/calib.log" 2>&1
 rc=$?; echo "[calib] rc=$rc"; [ $rc -eq 0 ] || exit $rc
 step stats --kernel-trace --stats
-step fetch --pmc FETCH_SIZE
-step write --pmc WRITE_SIZE
+MODE_ARGS="--streams 1" step stats_1stream --kernel-trace --stats
+MODE_ARGS="--streams 1" step fetch --pmc FETCH_SIZE
+MODE_ARGS="--streams 1" step write --pmc WRITE_SIZE
 MODE_ARGS="--mode sequential" step seq_stats --kernel-trace --stats
 MODE_ARGS="--mode sequential" step seq_fetch --pmc FETCH_SIZE
 MODE_ARGS="--mode sequential" step seq_write --pmc WRITE_SIZE
+if [ "${UBENCH:-1}" = 1 ]; then
+  timeout -k 10 200 ./scripts/ubench_valu2 > "$OUT/ubench_valu2.jsonl" || exit $?
+  timeout -k 10 200 ./scripts/ubench_valu3 > "$OUT/ubench_valu3.jsonl" || exit $?
+fi
 echo profile-done

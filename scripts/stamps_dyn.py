@@ -80,6 +80,20 @@ for case in os.environ.get("CASES", "64x100000,5000x100000,5000x1000000").split(
                               "first_entry_by_se_us": [round(float((rt[(xcc == x) & (se == k), 0] - t0).min() / 100), 2)
                                                        if ((xcc == x) & (se == k)).any() else None for k in range(8)]}
                      for x in np.unique(xcc)}
+    cu = (hw >> 8) & 0xF
+    cukey = (xcc * 8 + se) * 16 + cu
+    cu_in, cu_out, cu_x = [], [], []
+    for k in np.unique(cukey):
+        sel = cukey == k
+        cu_in.append((rt[sel, 0].min() - t0) / 100)
+        cu_out.append((rt[sel, 5].max() - t0) / 100)
+        cu_x.append(int(xcc[sel][0]))
+    cu_in, cu_out, cu_x = np.array(cu_in), np.array(cu_out), np.array(cu_x)
+    out["cus"] = int(len(cu_in))
+    out["cu_span_us"] = pct(cu_out - cu_in)
+    out["cu_exit_by_xcc_min_p50_max"] = {int(x): [round(float(np.min(cu_out[cu_x == x])), 2),
+                                                  round(float(np.median(cu_out[cu_x == x])), 2),
+                                                  round(float(np.max(cu_out[cu_x == x])), 2)] for x in np.unique(cu_x)}
     last = np.argsort(-(rt[:, 5]))[:3]
     out["last_waves"] = [{"exit_us": float((rt[i, 5] - t0) / 100), "entry_us": float((rt[i, 0] - t0) / 100),
                           "units": int(units[i]), "life_kcyc": float((cy[i, 5] - cy[i, 0]) / 1e3)} for i in last]
