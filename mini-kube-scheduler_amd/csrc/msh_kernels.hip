@@ -755,6 +755,49 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
 // ---------------------------------------------------------------------------------------
 constexpr int DYN_THREADS = 1024;
 
+// One 8-pod unit of the work-queue kernel, pods in lanes 0..7 with FIXED pairs: pair q = lanes
+// 2q (low half) and 2q+1 (high half), pods without a digit included (their code 14 never
+// matches; decode turns them into SCORE_ERROR). Compared with ident_group (pairs formed from a
+// ballot mask, each pod's result picked out by readlane + compare + select), the pair codes come
+// from one DPP step and four readlanes, and the four reduced pairs reach their pods' lanes with
+// ONE ds_bpermute. Returns, in lanes 0..7, the pod's first feasible matching node index in the
+// tile, or NOFIT.
+#ifndef MSH_UNIT8
+#define MSH_UNIT8 1
+#endif
+template <int R>
+__device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, const uint32_t* __restrict__ words,
+                                                __amdgpu_buffer_rsrc_t rs, int32_t nc, int lane) {
+  static_assert(IDENT_UNIT == 8 && QB == 4, "ident_unit8 scans exactly 4 pod pairs");
+  const uint32_t c = pcv << CODE_SHIFT;
+  // quad_perm [1,0,3,2]: lane 2q receives lane 2q+1's code
+  const uint32_t partner = (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0xB1, 0xF, 0xF, false);
+  const uint32_t ppl = c | (partner << 16);  // pair code, valid in even lanes
+  uint32_t pp[4], bm[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    pp[q] = to_vgpr((uint32_t)__builtin_amdgcn_readlane((int)ppl, 2 * q));
+    bm[q] = BM_INIT;
+  }
+  uint32_t wa[R], wb[R];
+  load_words<true>(wa, words, rs, 0, lane);
+  for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
+    load_words<true>(wb, words, rs, c0 + R, lane);
+    scan_words<R, 4>(wa, pp, bm, 4);
+    load_words<true>(wa, words, rs, c0 + 2 * R, lane);  // past the slice: zeros, never scanned
+    scan_words<R, 4>(wb, pp, bm, 4);
+  }
+  const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);
+  const uint32_t x = wave_pkmin_u16_x4(pk_fold_lane(bm[0], lane2), pk_fold_lane(bm[1], lane2),
+                                       pk_fold_lane(bm[2], lane2), pk_fold_lane(bm[3], lane2));
+  // pair q's two results sit in row {0, 2, 1, 3}[q] of x; every lane of a row holds them
+  const int q = (lane >> 1) & 3;
+  const int row = ((q & 1) << 1) | (q >> 1);
+  const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(row * 16 * 4, (int)x);
+  const uint32_t h = (lane & 1) ? (v >> 16) : (v & 0xFFFFu);
+  return h < NOMATCH16 ? h : NOFIT;
+}
+
 template <int R, bool SHARD, int NT = DYN_THREADS>
 __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
   __shared__ uint32_t next_unit;
@@ -800,7 +843,11 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
 #ifdef MSH_STAMPS
     if (first_unit) MSH_STAMP(2);
 #endif
-    while (m) ident_group<R, IDENT_UNIT / 2, true>(m, pcv, res, words, rs, nc, 0u, lane);
+    if (MSH_UNIT8) {
+      if (m) res = ident_unit8<R>(pcv, words, rs, nc, lane);
+    } else {
+      while (m) ident_group<R, IDENT_UNIT / 2, true>(m, pcv, res, words, rs, nc, 0u, lane);
+    }
 #ifdef MSH_STAMPS
     if (first_unit) MSH_STAMP(3);
 #endif
