@@ -917,10 +917,33 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
 // first-feasible cost, and the non-match key when the normalize mode needs it --, reduces
 // across lanes with DPP (the two costs packed in one u16x2 chain when the table has fewer
 // than 65535 nodes), exchanges one word per wave through LDS behind one barrier
-// (double-buffered by pod parity), finishes the reduction redundantly in every wave, and the
-// owner lane commits: count += 1 and, with a capacity, the node turns infeasible for both
-// classes. The per-pod latency (scan + 2 reductions + 1 barrier), not throughput, bounds it.
+// (double-buffered by pod parity), finishes the reduction redundantly in every wave (NW lanes:
+// log2(NW) DPP steps), and the owner lane commits: count += 1 and, with a capacity, the node
+// turns infeasible for both classes. The per-pod latency (scan + 2 reductions + 1 barrier), not
+// throughput, bounds it, so nothing else may wait on memory inside the loop:
+//   * the barrier fences LDS only (a plain __syncthreads() is a workgroup fence over global
+//     memory too: `s_waitcnt vmcnt(0)`, i.e. every pod would wait for the previous pod's stores);
+//   * results collect in lanes (lane jl of wave 0 holds pod j0 + jl) and leave as one coalesced
+//     store per 64 pods;
+//   * the next 64 pods are prefetched one block ahead.
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Packed u16 min over lanes 0..NW-1 (others hold the identity); result in every lane of row 0.
+template <int NW>
+__device__ __forceinline__ uint32_t small_pkmin_u16(uint32_t v) {
+  static_assert(NW == 4 || NW == 8 || NW == 16, "NW must be 4, 8 or 16");
+  v = dpp_pkmin<0xB1, 0xF>(v);                  // quad_perm [1,0,3,2]
+  v = dpp_pkmin<0x4E, 0xF>(v);                  // quad_perm [2,3,0,1]
+  if (NW >= 8) v = dpp_pkmin<0x141, 0xF>(v);    // row_half_mirror: lanes 0..7
+  if (NW >= 16) v = dpp_pkmin<0x140, 0xF>(v);   // row_mirror: lanes 0..15
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+}
+
 template <int RS, int NW, bool NEED_KX, bool PACK16>
 __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
   __shared__ uint32_t red[2][3][NW];
@@ -949,18 +972,42 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     }
   }
 
+  // Drain the node-state loads here: otherwise the waitcnt pass, unsure they have landed on the
+  // loop's class-0 path, waits for every outstanding load (the pod prefetch included) there.
+  __builtin_amdgcn_s_waitcnt(0);
+  // Pods in lanes, 64 at a time: raw bytes are loaded one block ahead (clamped index, so the
+  // load needs no branch) and converted only when their block starts, so the loop never waits
+  // on them.
+  auto load_raw = [&](int32_t j0, int32_t& dr, int32_t& tr) {
+    const int32_t jj = min(j0 + lane, a.n_pods - 1);
+    dr = a.pod_digit[jj];
+    tr = a.pod_tol[jj];
+  };
+  auto convert = [&](int32_t j0, int32_t dr, int32_t tr, uint32_t& pdl, uint32_t& tll) {
+    const bool ok = j0 + lane < a.n_pods;
+    pdl = (ok && dr >= 0 && dr <= 9) ? (uint32_t)dr : POD_DIGIT_NONE;
+    tll = (ok && tr != 0) ? 1u : 0u;
+  };
   uint32_t pdv = POD_DIGIT_NONE, tolv = 0;
+  int32_t dn = 0, tn = 0;
+  if (a.n_pods > 0) load_raw(0, dn, tn);
+  int32_t o_idx = -1, o_st = 0;  // wave 0: lane jl holds pod j0 + jl of the current block
+  int64_t o_sc = 0;
+  auto store_block = [&](int32_t j0, int32_t cnt) {  // wave 0: one coalesced store per array
+    if (lane < cnt) {
+      a.out_idx[j0 + lane] = o_idx;
+      a.out_score[j0 + lane] = o_sc;
+      a.out_status[j0 + lane] = o_st;
+    }
+  };
   for (int32_t j = 0; j < a.n_pods; ++j) {
     const int jl = j & (WAVE - 1);
-    if (jl == 0) {  // prefetch the next 64 pods into lanes
-      const int32_t jj = j + lane;
-      pdv = POD_DIGIT_NONE;
-      tolv = 0;
-      if (jj < a.n_pods) {
-        const int d = a.pod_digit[jj];
-        pdv = (d >= 0 && d <= 9) ? (uint32_t)d : POD_DIGIT_NONE;
-        tolv = a.pod_tol[jj] ? 1u : 0u;
-      }
+    if (jl == 0) {
+      // order matters for vmcnt (in-order): the conversion waits only for the loads issued one
+      // block ago, then the previous block's results leave, then the next block is requested
+      convert(j, dn, tn, pdv, tolv);
+      if (wv == 0 && j > 0) store_block(j - WAVE, WAVE);
+      load_raw(j + WAVE, dn, tn);  // one block ahead (clamped: no branch around it)
     }
     const uint32_t pd = (uint32_t)__builtin_amdgcn_readlane((int)pdv, jl);
     const uint32_t tol = (uint32_t)__builtin_amdgcn_readlane((int)tolv, jl);
@@ -987,48 +1034,43 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
         bx = umax(bx, D[r] == pds ? 0u : k);
       }
     }
-    uint32_t km, ka;
-    if (PACK16) {  // both costs in one u16x2 DPP chain (indices < 65535 here)
+    const int par = j & 1;
+    int64_t im, ia;
+    if (PACK16) {  // both costs as u16 node indices (< 65535 here) in one DPP chain per level
       const uint32_t m16 = bm < MATCH_LIMIT ? bm : 0xFFFFu;
       const uint32_t a16 = ba < MATCH_LIMIT ? ba : 0xFFFFu;
       const uint32_t v = wave_pkmin_u16(m16 | (a16 << 16));
-      const uint32_t vm = v & 0xFFFFu, va = v >> 16;
-      km = vm != 0xFFFFu ? KMAX - vm : 0u;
-      ka = va != 0xFFFFu ? KMAX - va : 0u;
+      const uint32_t kx = NEED_KX ? wave_max_u32(bx) : 0u;
+      if (lane == 0) {
+        red[par][0][wv] = v;
+        if (NEED_KX) red[par][2][wv] = kx;
+      }
+      lds_barrier();
+      const uint32_t g = small_pkmin_u16<NW>(lane < NW ? red[par][0][lane] : 0xFFFFFFFFu);
+      im = (g & 0xFFFFu) != 0xFFFFu ? (int64_t)(g & 0xFFFFu) : -1;
+      ia = (g >> 16) != 0xFFFFu ? (int64_t)(g >> 16) : -1;
     } else {
-      km = cost_to_key(wave_min_u32(bm));
-      ka = cost_to_key(wave_min_u32(ba));
+      const uint32_t km = cost_to_key(wave_min_u32(bm));
+      const uint32_t ka = cost_to_key(wave_min_u32(ba));
+      const uint32_t kx = NEED_KX ? wave_max_u32(bx) : 0u;
+      if (lane == 0) {
+        red[par][0][wv] = km;
+        red[par][1][wv] = ka;
+        red[par][2][wv] = kx;
+      }
+      lds_barrier();
+      im = key_to_idx(wave_max_u32(lane < NW ? red[par][0][lane] : 0u));
+      ia = key_to_idx(wave_max_u32(lane < NW ? red[par][1][lane] : 0u));
     }
-    const uint32_t kx = NEED_KX ? wave_max_u32(bx) : 0u;
-    const int par = j & 1;
-    if (lane == 0) {
-      red[par][0][wv] = km;
-      red[par][1][wv] = ka;
-      red[par][2][wv] = kx;
-    }
-    __syncthreads();
-    uint32_t gm, ga;
-    if (PACK16) {  // keys < 2^24 here: reduce (km, ka) as two u16 halves of (KMAX - key)...
-      const uint32_t xm = lane < NW ? red[par][0][lane] : 0u;
-      const uint32_t xa = lane < NW ? red[par][1][lane] : 0u;
-      const uint32_t im = xm ? KMAX - xm : 0xFFFFu, ia = xa ? KMAX - xa : 0xFFFFu;  // back to indices
-      const uint32_t v = wave_pkmin_u16(im | (ia << 16));
-      const uint32_t vm = v & 0xFFFFu, va = v >> 16;
-      gm = vm != 0xFFFFu ? KMAX - vm : 0u;
-      ga = va != 0xFFFFu ? KMAX - va : 0u;
-    } else {
-      gm = wave_max_u32(lane < NW ? red[par][0][lane] : 0u);
-      ga = wave_max_u32(lane < NW ? red[par][1][lane] : 0u);
-    }
-    const uint32_t gx = NEED_KX ? wave_max_u32(lane < NW ? red[par][2][lane] : 0u) : 0u;
+    const int64_t ix = NEED_KX ? key_to_idx(wave_max_u32(lane < NW ? red[par][2][lane] : 0u)) : -1;
     int32_t sel, st;
     int64_t sc;
-    decode_pod(key_to_idx(gm), key_to_idx(gx), key_to_idx(ga), pd != POD_DIGIT_NONE, a.pp, &sel,
-               &sc, &st);
-    if (wv == 0 && lane == 0) {
-      a.out_idx[j] = sel;
-      a.out_score[j] = sc;
-      a.out_status[j] = st;
+    decode_pod(im, ix, ia, pd != POD_DIGIT_NONE, a.pp, &sel, &sc, &st);
+    if (wv == 0) {
+      const bool mine = lane == jl;
+      o_idx = mine ? sel : o_idx;
+      o_sc = mine ? sc : o_sc;
+      o_st = mine ? st : o_st;
     }
     if (st == 0) {  // commit (NodeInfo.AddPod analogue) by the owning lane
       const int32_t c = sel >> 6;
@@ -1049,6 +1091,10 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     }
   }
 
+  if (wv == 0 && a.n_pods > 0) {
+    const int32_t j0 = (a.n_pods - 1) & ~(WAVE - 1);
+    store_block(j0, a.n_pods - j0);
+  }
 #pragma unroll
   for (int r = 0; r < RS; ++r) {
     const int32_t c = wv + NW * r;
