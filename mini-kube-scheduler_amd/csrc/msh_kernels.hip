@@ -442,6 +442,7 @@ __device__ __forceinline__ uint32_t wave_pkmin_u16_x4(uint32_t a, uint32_t b, ui
   return v;
 }
 
+constexpr int ULIST_STEP = 256;  // ulist entries per block of independent loads (divides NODE_PAD)
 constexpr int IDENT_THREADS = 512;
 #ifndef MSH_UNIT
 #define MSH_UNIT 8
@@ -629,6 +630,39 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
   }
 }
 
+// Tolerating pods (set bits of `mt`): a pass over ulist, the nodes feasible for
+// them alone. The list is read in whole ULIST_STEP-entry blocks (sentinel-padded, no bounds
+// check) with ULIST_STEP / 64 independent loads in flight, so a pass pays one L2 round trip
+// per block instead of one per 64 entries. Entry ^ (digit << 24) is < 2^24 exactly on a digit
+// match, and then it is the node index.
+__device__ __forceinline__ uint32_t ulist_pass(unsigned long long mt, uint32_t pcv, uint32_t res,
+                                               const uint32_t* __restrict__ ulist, uint32_t ucnt,
+                                               int lane) {
+  constexpr int NL = ULIST_STEP / WAVE;
+  // wave-uniform descriptor: block offset in an SGPR, lane offset one loop-invariant VGPR
+  const uint32_t n_rd = (ucnt + ULIST_STEP - 1) / ULIST_STEP * ULIST_STEP;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)ulist, (short)0, (int32_t)(n_rd * sizeof(uint32_t)), 0x00020000);
+  while (mt) {
+    const int32_t l = (int32_t)__builtin_ctzll(mt);
+    mt &= mt - 1;
+    const uint32_t pc24 = (uint32_t)__builtin_amdgcn_readlane((int)pcv, l) << 24;
+    uint32_t bu = 0xFFFFFFFFu;
+#pragma unroll 1
+    for (uint32_t u0 = 0; u0 < ucnt; u0 += ULIST_STEP) {
+      uint32_t x[NL];
+#pragma unroll
+      for (int i = 0; i < NL; ++i)
+        x[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4 + i * WAVE * 4, (int)(u0 * 4), 0);
+#pragma unroll
+      for (int i = 0; i < NL; i += 2) bu = umin(bu, umin(x[i] ^ pc24, x[i + 1] ^ pc24));
+    }
+    const uint32_t vu = wave_min_u32(bu);
+    if (vu < MATCH_LIMIT) res = (lane == l) ? umin(res, vu) : res;
+  }
+  return res;
+}
+
 // DIRECT: node words are read straight from global memory (L1/L2-resident: 4 B/node) with no
 // LDS staging and no workgroup barrier; otherwise staged in LDS slices of STAGE_CHUNKS.
 template <int R, int G2, bool SHARD, bool DIRECT>
@@ -697,22 +731,8 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       MSH_STAMP(3);
 
       // tolerating pods: the class-1-only nodes (ulist), once (first stage)
-      unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
-      if (st == 0) {
-        while (mt) {
-          const int32_t l = (int32_t)__builtin_ctzll(mt);
-          mt &= mt - 1;
-          const uint32_t pc24 = (uint32_t)__builtin_amdgcn_readlane((int)pcv, l) << 24;
-          uint32_t bu = 0xFFFFFFFFu;
-          for (uint32_t u0 = 0; u0 < ucnt; u0 += WAVE) {
-            const uint32_t u = u0 + (uint32_t)lane;
-            const uint32_t x = (u < ucnt ? a.ulist[u] : (CODE_NONE_NODE << 24)) ^ pc24;
-            bu = umin(bu, x);  // < 2^24 exactly on a digit match, then == node index
-          }
-          const uint32_t vu = wave_min_u32(bu);
-          if (vu < MATCH_LIMIT) res = (lane == l) ? umin(res, vu) : res;
-        }
-      }
+      const unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
+      if (st == 0 && mt) res = ulist_pass(mt, pcv, res, a.ulist, ucnt, lane);
       MSH_STAMP(4);
 
       if (!act) continue;
@@ -754,6 +774,12 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
 // unit, and no global atomics or cross-launch state are involved.
 // ---------------------------------------------------------------------------------------
 constexpr int DYN_THREADS = 1024;
+// LDS size class of the LDS-resident variant: 288 chunks (18,432 nodes incl. the pad) = 72 KiB,
+// two 1024-thread workgroups per CU
+constexpr int DYN_LDS_CHUNKS = 288;
+#ifndef MSH_DYN_LDS_DEFAULT
+#define MSH_DYN_LDS_DEFAULT 0
+#endif
 
 // One 8-pod unit of the work-queue kernel, pods in lanes 0..7 with FIXED pairs: pair q = lanes
 // 2q (low half) and 2q+1 (high half), pods without a digit included (their code 14 never
@@ -765,9 +791,26 @@ constexpr int DYN_THREADS = 1024;
 #ifndef MSH_UNIT8
 #define MSH_UNIT8 1
 #endif
+// R chunks of node words from the workgroup's LDS copy of the table (same lane-major 4-chunk
+// groups as in global memory): one conflict-free ds_read_b128 per lane per 4 chunks.
 template <int R>
-__device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, const uint32_t* __restrict__ words,
-                                                __amdgpu_buffer_rsrc_t rs, int32_t nc, int lane) {
+__device__ __forceinline__ void load_words_lds(uint32_t (&w)[R], const uint4* lw, int32_t c0, int lane) {
+  static_assert(R % 4 == 0, "whole 4-chunk groups");
+#pragma unroll
+  for (int g = 0; g < R / 4; ++g) {
+    const uint4 v = lw[(c0 / 4 + g) * WAVE + lane];
+    w[4 * g + 0] = v.x;
+    w[4 * g + 1] = v.y;
+    w[4 * g + 2] = v.z;
+    w[4 * g + 3] = v.w;
+  }
+}
+
+// `wa` holds chunks [0, R) on entry (requested by the caller together with the pod bytes).
+template <int R, bool LDSW>
+__device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, uint32_t (&wa)[R], const uint32_t* __restrict__ words,
+                                                __amdgpu_buffer_rsrc_t rs, const uint4* lw, int32_t nc,
+                                                int lane) {
   static_assert(IDENT_UNIT == 8 && QB == 4, "ident_unit8 scans exactly 4 pod pairs");
   const uint32_t c = pcv << CODE_SHIFT;
   // quad_perm [1,0,3,2]: lane 2q receives lane 2q+1's code
@@ -779,14 +822,31 @@ __device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, const uint32_t* __
     pp[q] = to_vgpr((uint32_t)__builtin_amdgcn_readlane((int)ppl, 2 * q));
     bm[q] = BM_INIT;
   }
-  uint32_t wa[R], wb[R];
-  load_words<true>(wa, words, rs, 0, lane);
+  uint32_t wb[R];
+#ifdef MSH_DIAG_NOLOAD  // timing diagnostic only (wrong results): node words loaded once
+  load_words<true>(wb, words, rs, R, lane);
   for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
-    load_words<true>(wb, words, rs, c0 + R, lane);
     scan_words<R, 4>(wa, pp, bm, 4);
-    load_words<true>(wa, words, rs, c0 + 2 * R, lane);  // past the slice: zeros, never scanned
     scan_words<R, 4>(wb, pp, bm, 4);
+    wa[0] += 1u;
   }
+#else
+  if (LDSW) {
+    for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
+      load_words_lds<R>(wb, lw, c0 + R, lane);
+      scan_words<R, 4>(wa, pp, bm, 4);
+      load_words_lds<R>(wa, lw, c0 + 2 * R, lane);  // past the table: the LDS pad, never scanned
+      scan_words<R, 4>(wb, pp, bm, 4);
+    }
+  } else {
+    for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
+      load_words<true>(wb, words, rs, c0 + R, lane);
+      scan_words<R, 4>(wa, pp, bm, 4);
+      load_words<true>(wa, words, rs, c0 + 2 * R, lane);  // past the slice: zeros, never scanned
+      scan_words<R, 4>(wb, pp, bm, 4);
+    }
+  }
+#endif
   const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);
   const uint32_t x = wave_pkmin_u16_x4(pk_fold_lane(bm[0], lane2), pk_fold_lane(bm[1], lane2),
                                        pk_fold_lane(bm[2], lane2), pk_fold_lane(bm[3], lane2));
@@ -798,9 +858,12 @@ __device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, const uint32_t* __
   return h < NOMATCH16 ? h : NOFIT;
 }
 
-template <int R, bool SHARD, int NT = DYN_THREADS>
+template <int R, bool SHARD, int NT = DYN_THREADS, bool LDSW = false>
 __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
   __shared__ uint32_t next_unit;
+  // LDSW: the workgroup's copy of the node words (nc + R chunks, the last R a zero pad that the
+  // scan loop's one-block-ahead read may touch but never scans)
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_words[];
   const int lane = threadIdx.x & (WAVE - 1);
 #ifdef MSH_STAMPS
   // diagnostic stamps: 0 entry, 1 first unit fetched, 2 its pods loaded, 3 its groups scanned,
@@ -813,18 +876,36 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
   const uint32_t* words = a.w0;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)words, (short)0, nc * WAVE * (int32_t)sizeof(uint32_t), 0x00020000);
-  const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
-  const uint32_t ucnt = *a.ucount;
-  const int32_t g0 = (int32_t)((int64_t)a.n_pods * blockIdx.x / gridDim.x);
-  const int32_t g1 = (int32_t)((int64_t)a.n_pods * (blockIdx.x + 1) / gridDim.x);
-  const int32_t n_units = (g1 - g0 + IDENT_UNIT - 1) / IDENT_UNIT;
+  // Per-launch scalars written by the prep kernel, requested as VECTOR loads so that nothing
+  // waits for them before the first unit: a scalar load would share lgkmcnt with the LDS work
+  // counter and put two dependent round trips in front of every wave's first claim.
+  const uint32_t bvec = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ball, (short)0, 8, 0x00020000), (lane & 1) * 4, 0, 0);
+  const uint32_t uvec = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ucount, (short)0, 4, 0x00020000), 0, 0, 0);
+  // this workgroup's contiguous unit range (host-computed quotient/remainder: no 64-bit division)
+  const int32_t b = (int32_t)blockIdx.x;
+  const int32_t ub = b * a.unit_q + min(b, a.unit_r);
+  const int32_t n_units = a.unit_q + (b < a.unit_r ? 1 : 0);
+  const int32_t g0 = ub * IDENT_UNIT;
+  const int32_t g1 = min(g0 + n_units * IDENT_UNIT, a.n_pods);
+  const uint4* lw = reinterpret_cast<const uint4*>(lds_words);
+  if (LDSW) {
+    const uint4* src = reinterpret_cast<const uint4*>(words);
+    uint4* dst = reinterpret_cast<uint4*>(lds_words);
+    const int32_t n16 = nc * (WAVE / 4), pad16 = (nc + R) * (WAVE / 4);
+    for (int32_t i = threadIdx.x; i < pad16; i += NT) dst[i] = i < n16 ? src[i] : make_uint4(0, 0, 0, 0);
+  }
   if (threadIdx.x == 0) next_unit = 0;
   __syncthreads();
-  for (;;) {
-    uint32_t u = 0;
-    if (lane == 0) u = atomicAdd(&next_unit, 1u);
-    u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
-    if (u >= (uint32_t)n_units) break;
+  auto claim = [&]() -> uint32_t {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(&next_unit, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+  };
+  // (claiming the next unit and requesting its pod bytes before scanning the current one was
+  // measured 1 us slower isolated at C3, and no faster pipelined)
+  for (uint32_t u = claim(); u < (uint32_t)n_units; u = claim()) {
 #ifdef MSH_STAMPS
     const bool first_unit = n_taken++ == 0;
     if (first_unit) MSH_STAMP(1);
@@ -832,6 +913,12 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
     const int32_t w0 = g0 + (int32_t)u * IDENT_UNIT;
     const int32_t nwin = min((int32_t)IDENT_UNIT, g1 - w0);
     const bool act = lane < nwin;
+    // the unit's first block of node words is requested before the pod bytes are waited for
+    uint32_t wa[R];
+    if (LDSW)
+      load_words_lds<R>(wa, lw, 0, lane);
+    else
+      load_words<true>(wa, words, rs, 0, lane);
     uint32_t pcv = CODE_NONE_POD, tolv = 0;
     if (act) {
       const int d = a.pod_digit[w0 + lane];
@@ -844,33 +931,22 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
     if (first_unit) MSH_STAMP(2);
 #endif
     if (MSH_UNIT8) {
-      if (m) res = ident_unit8<R>(pcv, words, rs, nc, lane);
+      if (m) res = ident_unit8<R, LDSW>(pcv, wa, words, rs, lw, nc, lane);
     } else {
       while (m) ident_group<R, IDENT_UNIT / 2, true>(m, pcv, res, words, rs, nc, 0u, lane);
     }
 #ifdef MSH_STAMPS
     if (first_unit) MSH_STAMP(3);
 #endif
-    unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
-    while (mt) {
-      const int32_t l = (int32_t)__builtin_ctzll(mt);
-      mt &= mt - 1;
-      const uint32_t pc24 = (uint32_t)__builtin_amdgcn_readlane((int)pcv, l) << 24;
-      uint32_t bu = 0xFFFFFFFFu;
-      for (uint32_t u0 = 0; u0 < ucnt; u0 += WAVE) {
-        const uint32_t k = u0 + (uint32_t)lane;
-        const uint32_t x = (k < ucnt ? a.ulist[k] : (CODE_NONE_NODE << 24)) ^ pc24;
-        bu = umin(bu, x);
-      }
-      const uint32_t vu = wave_min_u32(bu);
-      if (vu < MATCH_LIMIT) res = (lane == l) ? umin(res, vu) : res;
-    }
+    const unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
+    if (mt) res = ulist_pass(mt, pcv, res, a.ulist, (uint32_t)__builtin_amdgcn_readfirstlane((int)uvec), lane);
 #ifdef MSH_STAMPS
     if (first_unit) MSH_STAMP(4);
 #endif
     if (act) {
       const int32_t j = w0 + lane;
-      const uint32_t ball = tolv ? ball1 : ball0;
+      const uint32_t ball = tolv ? (uint32_t)__builtin_amdgcn_readlane((int)bvec, 1)
+                                 : (uint32_t)__builtin_amdgcn_readlane((int)bvec, 0);
       if (SHARD) {
         a.keys[j] = res != NOFIT ? (GKEY_MAX - (a.node_base + (int64_t)res)) : 0;
         a.keys[(size_t)a.n_pods + j] = ball ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - ball))) : 0;
@@ -1114,6 +1190,11 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
   e = hipMemsetAsync(d_ucount, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   if (n_pad == 0) return hipSuccess;
+  // every ulist slot past the count holds the never-matching entry (CODE_NONE_NODE << 24): the
+  // batch kernels read whole ULIST_STEP-entry blocks with no bounds check (count <= n <= n_pad,
+  // and n_pad is a multiple of ULIST_STEP)
+  e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_ulist), (int)(CODE_NONE_NODE << 24), (size_t)n_pad, s);
+  if (e != hipSuccess) return e;
   const int blocks = (n_pad + 255) / 256;
   hipLaunchKernelGGL(node_prep_kernel, dim3(blocks), dim3(256), 0, s, d_unsched, d_digit, n, n_pad,
                      has_nu, d_c0, d_dig, d_w0, d_ulist, d_ucount, d_mask, d_ball);
@@ -1310,10 +1391,12 @@ hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(IDENT_THREADS), lds, s, a, lds_chunks);
   return hipGetLastError();
 }
-template <bool SHARD, int NT>
+template <bool SHARD, int NT, bool LDSW>
 hipError_t launch_ident_dyn_nt(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err) {
-  auto kern = ident_dyn_kernel<IDENT_R, SHARD, NT>;
-  const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), NT, 0);
+  auto kern = ident_dyn_kernel<IDENT_R, SHARD, NT, LDSW>;
+  // LDSW: a fixed per-launch LDS size class (occupancy is cached per size)
+  const size_t lds = LDSW ? (size_t)DYN_LDS_CHUNKS * WAVE * sizeof(uint32_t) : 0;
+  const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), NT, lds);
   if (occ < 1) {
     if (err) *err = "ident work-queue kernel: zero occupancy";
     return hipErrorInvalidConfiguration;
@@ -1331,7 +1414,10 @@ hipError_t launch_ident_dyn_nt(const BatchArgs& a, const DeviceInfo& dev, hipStr
   const int64_t grid_units = (n_units + WPG - 1) / WPG;
   if (grid > grid_units) grid = grid_units;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, a);
+  BatchArgs ka = a;
+  ka.unit_q = (int32_t)(n_units / grid);
+  ka.unit_r = (int32_t)(n_units % grid);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, s, ka);
   return hipGetLastError();
 }
 
@@ -1341,9 +1427,13 @@ hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStre
   // MSH_DYN_THREADS (tuning / A-B only): workgroup size of the work-queue kernel
   const char* env = getenv("MSH_DYN_THREADS");
   const int nt = env ? atoi(env) : DYN_THREADS;
-  if (nt == 256) return launch_ident_dyn_nt<SHARD, 256>(a, dev, s, err);
-  if (nt == 512) return launch_ident_dyn_nt<SHARD, 512>(a, dev, s, err);
-  return launch_ident_dyn_nt<SHARD, 1024>(a, dev, s, err);
+  // node words from an LDS copy when the table fits the size class (MSH_DYN_LDS=0: L1/L2 reads)
+  const char* lenv = getenv("MSH_DYN_LDS");
+  const bool ldsw = (lenv ? atoi(lenv) : MSH_DYN_LDS_DEFAULT) != 0 && a.n_chunks + IDENT_R <= DYN_LDS_CHUNKS;
+  if (ldsw) return launch_ident_dyn_nt<SHARD, 1024, true>(a, dev, s, err);
+  if (nt == 256) return launch_ident_dyn_nt<SHARD, 256, false>(a, dev, s, err);
+  if (nt == 512) return launch_ident_dyn_nt<SHARD, 512, false>(a, dev, s, err);
+  return launch_ident_dyn_nt<SHARD, 1024, false>(a, dev, s, err);
 }
 }  // namespace
 
