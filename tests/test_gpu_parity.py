@@ -114,6 +114,36 @@ def test_node_sizes(msh, gpu_ctx, oracle, n):
     _assert_same(got, closed_form(u, nd, pd, pt), f"closed form n={n}")
 
 
+@pytest.mark.parametrize("n_only", [0, 1, 63, 64, 255, 256, 257, 511, 512, 1023, 1024, 1800])
+def test_tolerating_list_blocks(msh, gpu_ctx, oracle, n_only):
+    """The tolerating pods' pass reads the class-1-only node list (ulist) in sentinel-padded
+    256-entry blocks with no bounds check: list lengths at and around the block and table-padding
+    boundaries, with every tolerating pod's only match the LAST listed node, the first, or none."""
+    rng = np.random.default_rng(4242 + n_only)
+    n = 2048
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u = np.zeros(n, np.uint8)
+    u[n - n_only:] = 1                       # the list = the last n_only nodes
+    nd = np.full(n, 9, np.int8)              # feasible nodes never match digits 0..8
+    nd[n - n_only:] = rng.integers(0, 9, n_only).astype(np.int8)
+    if n_only:
+        nd[n - 1] = 3                        # the last listed node: the only '3' -> list tail
+        nd[n - n_only] = 5 if n_only > 1 else 3
+        nd[n - n_only + 1:n - 1][nd[n - n_only + 1:n - 1] == 5] = 6
+        nd[n - n_only + 1:n - 1][nd[n - n_only + 1:n - 1] == 3] = 4
+    p = 4096
+    pd = rng.integers(0, 10, p).astype(np.int8)
+    pt = (rng.random(p) < 0.5).astype(np.uint8)
+    gpu_ctx.upload_nodes(u, nd)
+    got = gpu_ctx.schedule_batch(pd, pt)
+    _assert_same(got, oracle.c_schedule_batch(u, nd, pd, pt, ps), f"ulist={n_only}")
+    _assert_same(got, closed_form(u, nd, pd, pt), f"closed form ulist={n_only}")
+    if n_only:
+        tol3 = (pt == 1) & (pd == 3)
+        assert (got[0][tol3] == n - 1).all()
+
+
 @pytest.mark.parametrize("norm", [0, 2, 3])
 def test_multitile_normalize(msh, gpu_ctx, oracle, norm):
     rng = np.random.default_rng(77 + norm)
