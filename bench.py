@@ -265,10 +265,9 @@ def main():
         }
     else:
         shard = mode == "nodeshard"
-        # launcher dispatch (msh_kernels.hip launch_batch): one compute tile (<= 64,512 nodes) ->
-        # the work-queue kernel, else the tiled static kernel
-        kname = (f"ident_dyn_kernel<8, {str(shard).lower()}, 1024, false>" if n_local <= 64512
-                 else f"ident_kernel<8, 8, {str(shard).lower()}, true>")
+        # launcher dispatch (msh_kernels.hip launch_batch): the work-queue kernel, its MULTI form
+        # when the table spans several 64,512-node compute tiles
+        kname = f"ident_dyn_kernel<8, {str(shard).lower()}, 1024, false, {str(n_local > 64512).lower()}>"
         iso_s = kernel_ms_isolated * 1e-3
         roofline = {
             "bound": "valu",

@@ -147,7 +147,13 @@ int msh_patch_nodes(msh_ctx* ctx, int32_t count, const int32_t* idx, const uint8
 int msh_schedule_batch(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
                        int32_t* out_idx, int64_t* out_score, int32_t* out_status);
 
-/* Same, device-resident inputs/outputs, asynchronous on `stream` (hipStream_t). */
+/* Same, device-resident inputs/outputs, asynchronous on `stream` (hipStream_t).
+ * Launches on different streams may overlap (independent batches pipelined): each needs its own
+ * pod and output buffers. The ctx's node tables are read-only during batches; when an upload,
+ * patch or plugin change left them to be re-prepared, the first launch after it prepares them and
+ * waits for that before returning. The few configurations whose kernel keeps running results in
+ * per-ctx scratch (normalizers needing the non-match extent on tables above 16,384 nodes) are
+ * ordered across streams by the library. */
 int msh_schedule_batch_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
                               const uint8_t* d_pod_tol, int32_t* d_out_idx,
                               int64_t* d_out_score, int32_t* d_out_status, void* stream);

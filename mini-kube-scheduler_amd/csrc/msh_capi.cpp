@@ -56,6 +56,9 @@ struct msh_ctx {
   int32_t* d_ost = nullptr;
   size_t partial_cap = 0;
   uint32_t* d_partial = nullptr;  // multi-tile node tables only
+  // launches that keep running results in d_partial are chained across streams by this event
+  hipEvent_t partial_ev = nullptr;
+  bool partial_ev_live = false;
   size_t patch_cap = 0;
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
   std::vector<unsigned long long> h_patch;
@@ -135,7 +138,26 @@ int prepare(msh_ctx* c, hipStream_t s) {
                                        c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_w0, c->d_ulist, c->d_ucount, c->d_mask,
                                        c->d_ball, s);
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
+  // The prepared tables are read by launches on any stream: finish them before returning (this
+  // runs only after an upload, a patch or a plugin change, never per batch).
+  MSH_HIP(c, hipStreamSynchronize(s));
   c->dirty = false;
+  return MSH_OK;
+}
+
+// A launch whose kernel keeps running results in the ctx's d_partial scratch must not overlap
+// another such launch on a different stream: each waits for the previous one's completion.
+int partial_begin(msh_ctx* c, hipStream_t s, bool uses) {
+  if (!uses) return MSH_OK;
+  if (!c->partial_ev) MSH_HIP(c, hipEventCreateWithFlags(&c->partial_ev, hipEventDisableTiming));
+  if (c->partial_ev_live) MSH_HIP(c, hipStreamWaitEvent(s, c->partial_ev, 0));
+  return MSH_OK;
+}
+
+int partial_end(msh_ctx* c, hipStream_t s, bool uses) {
+  if (!uses) return MSH_OK;
+  MSH_HIP(c, hipEventRecord(c->partial_ev, s));
+  c->partial_ev_live = true;
   return MSH_OK;
 }
 
@@ -233,6 +255,7 @@ void msh_destroy(msh_ctx* c) {
   (void)hipFree(c->d_partial);
   (void)hipFree(c->d_patch);
   (void)hipFree(c->d_ball);
+  if (c->partial_ev) (void)hipEventDestroy(c->partial_ev);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -432,9 +455,11 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   a.out_idx = d_out_idx;
   a.out_score = d_out_score;
   a.out_status = d_out_status;
+  const bool up = p > 0 && msh::batch_uses_partial(c->pp, a.n_chunks);
+  if ((rc = partial_begin(c, s, up)) != MSH_OK) return rc;
   hipError_t e = msh::launch_batch(a, false, c->dev, s, &c->err);
   if (e != hipSuccess) return hip_fail(c, e, "batch_kernel");
-  return MSH_OK;
+  return partial_end(c, s, up);
 }
 
 int msh_schedule_batch(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
@@ -568,9 +593,11 @@ int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
   a.keys = d_keys;
   a.node_base = node_base;
+  const bool up = p > 0 && msh::batch_uses_partial(c->pp, a.n_chunks);
+  if ((rc = partial_begin(c, s, up)) != MSH_OK) return rc;
   hipError_t e = msh::launch_batch(a, true, c->dev, s, &c->err);
   if (e != hipSuccess) return hip_fail(c, e, "batch_kernel(shard)");
-  return MSH_OK;
+  return partial_end(c, s, up);
 }
 
 int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,

@@ -113,6 +113,9 @@ struct BatchArgs {
 // LDS tile geometry of the batched kernel (host needs it to size the partial-key scratch).
 int32_t batch_tile_chunks(int32_t n_chunks);
 bool batch_needs_partial(int32_t n_chunks);
+// does the batch kernel launch_batch picks for these plugins keep running results in `partial`
+// (a per-ctx scratch: such launches must not overlap on different streams)
+bool batch_uses_partial(const PluginParams& pp, int32_t n_chunks);
 
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s,
                         std::string* err);

@@ -858,7 +858,10 @@ __device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, uint32_t (&wa)[R],
   return h < NOMATCH16 ? h : NOFIT;
 }
 
-template <int R, bool SHARD, int NT = DYN_THREADS, bool LDSW = false>
+// MULTI: the node table spans several 64,512-node compute tiles (word halves hold tile-relative
+// chunks). A unit scans the tiles in List order and keeps the first tile with a match: the whole
+// table per unit, no running results in memory between launches or stages.
+template <int R, bool SHARD, int NT = DYN_THREADS, bool LDSW = false, bool MULTI = false>
 __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
   __shared__ uint32_t next_unit;
   // LDSW: the workgroup's copy of the node words (nc + R chunks, the last R a zero pad that the
@@ -872,7 +875,8 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
   uint32_t n_taken = 0;
 #endif
   MSH_STAMP(0);
-  const int32_t nc = a.n_chunks;  // one compute tile: tile_node_base = 0
+  // tile 0 (the whole table unless MULTI)
+  const int32_t nc = MULTI ? min(a.n_chunks, (int32_t)TILE_CHUNKS) : a.n_chunks;
   const uint32_t* words = a.w0;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)words, (short)0, nc * WAVE * (int32_t)sizeof(uint32_t), 0x00020000);
@@ -932,6 +936,18 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
 #endif
     if (MSH_UNIT8) {
       if (m) res = ident_unit8<R, LDSW>(pcv, wa, words, rs, lw, nc, lane);
+      if (MULTI && m) {
+        for (int32_t t0 = TILE_CHUNKS; t0 < a.n_chunks; t0 += TILE_CHUNKS) {
+          const int32_t nct = min(a.n_chunks - t0, (int32_t)TILE_CHUNKS);
+          const uint32_t* wt = a.w0 + (size_t)t0 * WAVE;
+          const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)wt, (short)0, nct * WAVE * (int32_t)sizeof(uint32_t), 0x00020000);
+          load_words<true>(wa, wt, rst, 0, lane);
+          const uint32_t rt = ident_unit8<R, false>(pcv, wa, wt, rst, lw, nct, lane);
+          // tiles ascend in List order: an earlier tile's match is always the smaller index
+          if (res == NOFIT && rt != NOFIT) res = (uint32_t)(t0 / TILE_CHUNKS) * (uint32_t)TILE_NODES + rt;
+        }
+      }
     } else {
       while (m) ident_group<R, IDENT_UNIT / 2, true>(m, pcv, res, words, rs, nc, 0u, lane);
     }
@@ -1391,9 +1407,9 @@ hipError_t launch_ident_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(IDENT_THREADS), lds, s, a, lds_chunks);
   return hipGetLastError();
 }
-template <bool SHARD, int NT, bool LDSW>
+template <bool SHARD, int NT, bool LDSW, bool MULTI = false>
 hipError_t launch_ident_dyn_nt(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err) {
-  auto kern = ident_dyn_kernel<IDENT_R, SHARD, NT, LDSW>;
+  auto kern = ident_dyn_kernel<IDENT_R, SHARD, NT, LDSW, MULTI>;
   // LDSW: a fixed per-launch LDS size class (occupancy is cached per size)
   const size_t lds = LDSW ? (size_t)DYN_LDS_CHUNKS * WAVE * sizeof(uint32_t) : 0;
   const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), NT, lds);
@@ -1430,6 +1446,7 @@ hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStre
   // node words from an LDS copy when the table fits the size class (MSH_DYN_LDS=0: L1/L2 reads)
   const char* lenv = getenv("MSH_DYN_LDS");
   const bool ldsw = (lenv ? atoi(lenv) : MSH_DYN_LDS_DEFAULT) != 0 && a.n_chunks + IDENT_R <= DYN_LDS_CHUNKS;
+  if (a.n_chunks > TILE_CHUNKS) return launch_ident_dyn_nt<SHARD, 1024, false, true>(a, dev, s, err);
   if (ldsw) return launch_ident_dyn_nt<SHARD, 1024, true>(a, dev, s, err);
   if (nt == 256) return launch_ident_dyn_nt<SHARD, 256, false>(a, dev, s, err);
   if (nt == 512) return launch_ident_dyn_nt<SHARD, 512, false>(a, dev, s, err);
@@ -1446,15 +1463,26 @@ bool batch_needs_partial(int32_t n_chunks) {
   return batch_tile_chunks(n_chunks) < n_chunks || ident_stage_chunks(n_chunks, false) < n_chunks;
 }
 
+// MSH_BATCH_KERNEL (tuning / A-B only): 3 = IDENT work queue (default), 2 = IDENT direct
+// static, 0 = IDENT LDS-staged, 1 = compare/select kernel
+int batch_kernel_choice() {
+  const char* kenv = getenv("MSH_BATCH_KERNEL");
+  return kenv ? atoi(kenv) : 3;
+}
+
+bool batch_uses_partial(const PluginParams& pp, int32_t n_chunks) {
+  const int kv = batch_kernel_choice();
+  if (!needs_kx(pp) && kv == 3) return false;  // the work queue scans every tile per unit
+  if (!needs_kx(pp) && kv != 1) return ident_stage_chunks(n_chunks, kv != 0) < n_chunks;
+  return batch_tile_chunks(n_chunks) < n_chunks;
+}
+
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s,
                         std::string* err) {
   if (a.n_pods == 0) return hipSuccess;
   const bool kx = needs_kx(a.pp);
-  // MSH_BATCH_KERNEL (tuning / A-B only): 3 = IDENT work queue (default when the table is one
-  // compute tile), 2 = IDENT direct static, 0 = IDENT LDS-staged, 1 = compare/select kernel
-  const char* kenv = getenv("MSH_BATCH_KERNEL");
-  const int kv = kenv ? atoi(kenv) : 3;
-  if (!kx && kv == 3 && a.n_chunks <= TILE_CHUNKS)
+  const int kv = batch_kernel_choice();
+  if (!kx && kv == 3)
     return shard ? launch_ident_dyn_t<true>(a, dev, s, err) : launch_ident_dyn_t<false>(a, dev, s, err);
   if (!kx && kv != 1) {
     if (kv == 0)

@@ -293,3 +293,35 @@ def test_determinism_device_entry(msh, gpu_ctx, oracle, synth):
     for o in outs[1:]:
         _assert_same(o, outs[0], "repeat")
     _assert_same(outs[0], oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8), "device entry")
+
+
+@pytest.mark.parametrize("n,norm", [(5000, 0), (100_000, 0), (100_000, 3), (20_000, 2)])
+def test_pipelined_streams(msh, gpu_ctx, oracle, n, norm):
+    """Independent batches in flight on several HIP streams of ONE ctx, as bench.py pipelines them:
+    the multi-tile work-queue kernel (100k nodes) and the compare/select kernel whose running
+    results live in per-ctx scratch (REVERSE / MINMAX above 16,384 nodes) must give every batch
+    the oracle's answer."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(n + norm)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, norm)
+    _set(gpu_ctx, msh, ps)
+    u, nd, _, _ = _rand_case(rng, n, 1, p_unsched=0.2, p_tol=0.3)
+    gpu_ctx.upload_nodes(u, nd)
+    dev = torch.device("cuda:0")
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    batches, outs = [], []
+    for k in range(6):
+        _, _, pd, pt = _rand_case(rng, 1, 3000 + 500 * k, p_tol=0.3)
+        batches.append((pd, pt))
+        d = (torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev))
+        o = (torch.empty(len(pd), dtype=torch.int32, device=dev), torch.empty(len(pd), dtype=torch.int64, device=dev),
+             torch.empty(len(pd), dtype=torch.int32, device=dev))
+        outs.append((d, o))
+    torch.cuda.synchronize()
+    for k, ((d_pd, d_pt), (oi, osc, ost)) in enumerate(outs):
+        gpu_ctx.schedule_batch_device(len(d_pd), d_pd.data_ptr(), d_pt.data_ptr(), oi.data_ptr(), osc.data_ptr(),
+                                      ost.data_ptr(), streams[k % 3].cuda_stream)
+    torch.cuda.synchronize()
+    for (pd, pt), (_, (oi, osc, ost)) in zip(batches, outs):
+        want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+        _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"n={n} norm={norm}")
