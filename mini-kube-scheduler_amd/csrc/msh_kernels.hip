@@ -1036,9 +1036,15 @@ __device__ __forceinline__ uint32_t small_pkmin_u16(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
 }
 
-template <int RS, int NW, bool NEED_KX, bool PACK16>
+// CAP (max_pods_per_node > 0): a commit can make a node infeasible, so every wave finishes the
+// reduction and the owning lane updates its registers before the next pod. Without a capacity a
+// commit changes nothing the next pod reads: only wave 0 finishes the reduction, decodes, keeps
+// the output and adds the commit to a per-node count held in LDS; the other waves go straight on
+// to the next pod's scan (the barrier per pod still orders every commit before the next pod).
+template <int RS, int NW, bool NEED_KX, bool PACK16, bool CAP>
 __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
   __shared__ uint32_t red[2][3][NW];
+  extern __shared__ int32_t lcnt[];  // !CAP: [n_chunks * 64] per-node pod counts
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
@@ -1056,12 +1062,17 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
       D[r] = (uint32_t)a.dig[i] << 24;
       C0[r] = a.c0[i];
       C1[r] = i < a.n_nodes ? (uint32_t)i : NOFIT;
-      CNT[r] = a.counts[i];
-      if (a.max_pods > 0 && CNT[r] >= a.max_pods) {
-        C0[r] = NOFIT;
-        C1[r] = NOFIT;
+      if (CAP) {
+        CNT[r] = a.counts[i];
+        if (CNT[r] >= a.max_pods) {
+          C0[r] = NOFIT;
+          C1[r] = NOFIT;
+        }
       }
     }
+  }
+  if (!CAP) {  // ordered before wave 0's first commit by the first pod's barrier
+    for (int32_t i = threadIdx.x; i < a.n_chunks * WAVE; i += NW * WAVE) lcnt[i] = a.counts[i];
   }
 
   // Drain the node-state loads here: otherwise the waitcnt pass, unsure they have landed on the
@@ -1138,6 +1149,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
         if (NEED_KX) red[par][2][wv] = kx;
       }
       lds_barrier();
+      if (!CAP && wv != 0) continue;  // only wave 0 finishes a pod when commits change nothing
       const uint32_t g = small_pkmin_u16<NW>(lane < NW ? red[par][0][lane] : 0xFFFFFFFFu);
       im = (g & 0xFFFFu) != 0xFFFFu ? (int64_t)(g & 0xFFFFu) : -1;
       ia = (g >> 16) != 0xFFFFu ? (int64_t)(g >> 16) : -1;
@@ -1151,6 +1163,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
         red[par][2][wv] = kx;
       }
       lds_barrier();
+      if (!CAP && wv != 0) continue;
       im = key_to_idx(wave_max_u32(lane < NW ? red[par][0][lane] : 0u));
       ia = key_to_idx(wave_max_u32(lane < NW ? red[par][1][lane] : 0u));
     }
@@ -1164,19 +1177,23 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
       o_sc = mine ? sc : o_sc;
       o_st = mine ? st : o_st;
     }
-    if (st == 0) {  // commit (NodeInfo.AddPod analogue) by the owning lane
-      const int32_t c = sel >> 6;
-      if ((c % NW) == wv) {
-        const int rs = c / NW;
-        const bool mine = lane == (sel & (WAVE - 1));
+    if (st == 0) {  // commit (NodeInfo.AddPod analogue)
+      if (!CAP) {
+        if (lane == 0) atomicAdd(&lcnt[sel], 1);  // wave 0; no return value waited for
+      } else {
+        const int32_t c = sel >> 6;
+        if ((c % NW) == wv) {
+          // the owning lane, branch-free: the register by a wave-uniform index, the lane by a
+          // compare (an unrolled `if (r == rs && mine)` became RS exec-mask branches)
+          const int rs = c / NW;
+          const bool mine = lane == (sel & (WAVE - 1));
 #pragma unroll
-        for (int r = 0; r < RS; ++r) {
-          if (r == rs && mine) {
-            CNT[r] += 1;
-            if (a.max_pods > 0 && CNT[r] >= a.max_pods) {
-              C0[r] = NOFIT;
-              C1[r] = NOFIT;
-            }
+          for (int r = 0; r < RS; ++r) {
+            const bool hit = mine && r == rs;
+            CNT[r] += hit ? 1 : 0;
+            const bool full = hit && CNT[r] >= a.max_pods;
+            C0[r] = full ? NOFIT : C0[r];
+            C1[r] = full ? NOFIT : C1[r];
           }
         }
       }
@@ -1187,10 +1204,15 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     const int32_t j0 = (a.n_pods - 1) & ~(WAVE - 1);
     store_block(j0, a.n_pods - j0);
   }
+  if (CAP) {
 #pragma unroll
-  for (int r = 0; r < RS; ++r) {
-    const int32_t c = wv + NW * r;
-    if (c < a.n_chunks) a.counts[c * WAVE + lane] = CNT[r];
+    for (int r = 0; r < RS; ++r) {
+      const int32_t c = wv + NW * r;
+      if (c < a.n_chunks) a.counts[c * WAVE + lane] = CNT[r];
+    }
+  } else {
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i < a.n_chunks * WAVE; i += NW * WAVE) a.counts[i] = lcnt[i];
   }
 }
 
@@ -1509,12 +1531,23 @@ template <int RS, int NW>
 hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
   const bool pack = a.n_nodes < 0xFFFF;
   const dim3 blk(NW * 64);
-  if (needs_kx(a.pp)) {
-    if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, true, true>), dim3(1), blk, 0, s, a);
-    else hipLaunchKernelGGL((seq_kernel<RS, NW, true, false>), dim3(1), blk, 0, s, a);
+  const size_t lds = (size_t)a.n_chunks * WAVE * sizeof(int32_t);  // !CAP count table
+  if (a.max_pods > 0) {
+    if (needs_kx(a.pp)) {
+      if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, true, true, true>), dim3(1), blk, 0, s, a);
+      else hipLaunchKernelGGL((seq_kernel<RS, NW, true, false, true>), dim3(1), blk, 0, s, a);
+    } else {
+      if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, false, true, true>), dim3(1), blk, 0, s, a);
+      else hipLaunchKernelGGL((seq_kernel<RS, NW, false, false, true>), dim3(1), blk, 0, s, a);
+    }
   } else {
-    if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, false, true>), dim3(1), blk, 0, s, a);
-    else hipLaunchKernelGGL((seq_kernel<RS, NW, false, false>), dim3(1), blk, 0, s, a);
+    if (needs_kx(a.pp)) {
+      if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, true, true, false>), dim3(1), blk, lds, s, a);
+      else hipLaunchKernelGGL((seq_kernel<RS, NW, true, false, false>), dim3(1), blk, lds, s, a);
+    } else {
+      if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, false, true, false>), dim3(1), blk, lds, s, a);
+      else hipLaunchKernelGGL((seq_kernel<RS, NW, false, false, false>), dim3(1), blk, lds, s, a);
+    }
   }
   return hipGetLastError();
 }
