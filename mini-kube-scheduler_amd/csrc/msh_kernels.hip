@@ -401,17 +401,6 @@ __device__ __forceinline__ uint32_t dpp_pkmin(uint32_t v) {
   return pk_min_u16(v, t);
 }
 
-// Wave-wide packed u16 min (both halves at once); result wave-uniform.
-__device__ __forceinline__ uint32_t wave_pkmin_u16(uint32_t v) {
-  v = dpp_pkmin<0xB1, 0xF>(v);
-  v = dpp_pkmin<0x4E, 0xF>(v);
-  v = dpp_pkmin<0x141, 0xF>(v);
-  v = dpp_pkmin<0x140, 0xF>(v);
-  v = dpp_pkmin<0x142, 0xA>(v);
-  v = dpp_pkmin<0x143, 0xC>(v);
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
 // chunk << 6 | lane in both halves, "no match" halves (>= 1024) saturated to chunk 1023 first
 // (-> 0xFFC0 | lane, >= NOMATCH16): v_pk_min_u16 + v_pk_mad_u16 (bm * 64 + lane). Plain vector
 // arithmetic, not asm: the permlane swaps that read the result need the compiler to see the
@@ -1025,22 +1014,17 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Packed u16 min over lanes 0..NW-1 (others hold the identity); result in every lane of row 0.
+// u32 min over lanes 0..NW-1 (the others hold the identity); result read from lane 0.
 template <int NW>
-__device__ __forceinline__ uint32_t small_pkmin_u16(uint32_t v) {
+__device__ __forceinline__ uint32_t small_min_u32(uint32_t v) {
   static_assert(NW == 4 || NW == 8 || NW == 16, "NW must be 4, 8 or 16");
-  v = dpp_pkmin<0xB1, 0xF>(v);                  // quad_perm [1,0,3,2]
-  v = dpp_pkmin<0x4E, 0xF>(v);                  // quad_perm [2,3,0,1]
-  if (NW >= 8) v = dpp_pkmin<0x141, 0xF>(v);    // row_half_mirror: lanes 0..7
-  if (NW >= 16) v = dpp_pkmin<0x140, 0xF>(v);   // row_mirror: lanes 0..15
+  v = dpp_step<true, 0xB1, 0xF>(v);                // quad_perm [1,0,3,2]
+  v = dpp_step<true, 0x4E, 0xF>(v);                // quad_perm [2,3,0,1]
+  if (NW >= 8) v = dpp_step<true, 0x141, 0xF>(v);  // row_half_mirror: lanes 0..7
+  if (NW >= 16) v = dpp_step<true, 0x140, 0xF>(v); // row_mirror: lanes 0..15
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
 }
 
-// CAP (max_pods_per_node > 0): a commit can make a node infeasible, so every wave finishes the
-// reduction and the owning lane updates its registers before the next pod. Without a capacity a
-// commit changes nothing the next pod reads: only wave 0 finishes the reduction, decodes, keeps
-// the output and adds the commit to a per-node count held in LDS; the other waves go straight on
-// to the next pod's scan (the barrier per pod still orders every commit before the next pod).
 template <int RS, int NW, bool NEED_KX, bool PACK16, bool CAP>
 __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
   __shared__ uint32_t red[2][3][NW];
@@ -1091,6 +1075,14 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     pdl = (ok && dr >= 0 && dr <= 9) ? (uint32_t)dr : POD_DIGIT_NONE;
     tll = (ok && tr != 0) ? 1u : 0u;
   };
+  // Loop-invariant arguments pinned in SGPRs: otherwise the backend re-loads them from the
+  // kernel-argument segment inside the per-pod loop, and each reload's lgkmcnt wait lands in
+  // front of the LDS exchange.
+  PluginParams pp = a.pp;
+  asm volatile("" : "+s"(pp.has_nu_filter), "+s"(pp.has_nn_score), "+s"(pp.nn_prescore), "+s"(pp.mode),
+               "+s"(pp.weight));
+  int32_t max_pods = a.max_pods;
+  asm volatile("" : "+s"(max_pods));
   uint32_t pdv = POD_DIGIT_NONE, tolv = 0;
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
@@ -1103,8 +1095,23 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
       a.out_status[j0 + lane] = o_st;
     }
   };
+#ifdef MSH_STAMPS  // diagnostic build only: per-wave cycles spent in each phase of the pod loop
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t t_prev = __builtin_amdgcn_s_memtime();
+#define SEQ_PH(k)                                        \
+  do {                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+    ph[k] += t_ - t_prev;                                \
+    t_prev = t_;                                         \
+  } while (0)
+#else
+#define SEQ_PH(k) \
+  do {            \
+  } while (0)
+#endif
   for (int32_t j = 0; j < a.n_pods; ++j) {
     const int jl = j & (WAVE - 1);
+    SEQ_PH(5);
     if (jl == 0) {
       // order matters for vmcnt (in-order): the conversion waits only for the loads issued one
       // block ago, then the previous block's results leave, then the next block is requested
@@ -1115,19 +1122,35 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     const uint32_t pd = (uint32_t)__builtin_amdgcn_readlane((int)pdv, jl);
     const uint32_t tol = (uint32_t)__builtin_amdgcn_readlane((int)tolv, jl);
     const uint32_t pds = pd << 24;
+    // two independent min chains per cost (even / odd registers): half the dependent depth
     uint32_t bm = 0xFFFFFFFFu, ba = 0xFFFFFFFFu, bx = 0u;
-    if (tol) {
+    {
+      uint32_t bm1 = 0xFFFFFFFFu, ba1 = 0xFFFFFFFFu;
+      if (tol) {
 #pragma unroll
-      for (int r = 0; r < RS; ++r) {
-        bm = umin(bm, sad(D[r], pds, C1[r]));
-        ba = umin(ba, C1[r]);
-      }
-    } else {
+        for (int r = 0; r < RS; ++r) {
+          if (r & 1) {
+            bm1 = umin(bm1, sad(D[r], pds, C1[r]));
+            ba1 = umin(ba1, C1[r]);
+          } else {
+            bm = umin(bm, sad(D[r], pds, C1[r]));
+            ba = umin(ba, C1[r]);
+          }
+        }
+      } else {
 #pragma unroll
-      for (int r = 0; r < RS; ++r) {
-        bm = umin(bm, sad(D[r], pds, C0[r]));
-        ba = umin(ba, C0[r]);
+        for (int r = 0; r < RS; ++r) {
+          if (r & 1) {
+            bm1 = umin(bm1, sad(D[r], pds, C0[r]));
+            ba1 = umin(ba1, C0[r]);
+          } else {
+            bm = umin(bm, sad(D[r], pds, C0[r]));
+            ba = umin(ba, C0[r]);
+          }
+        }
       }
+      bm = umin(bm, bm1);
+      ba = umin(ba, ba1);
     }
     if (NEED_KX) {
 #pragma unroll
@@ -1139,20 +1162,24 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     }
     const int par = j & 1;
     int64_t im, ia;
-    if (PACK16) {  // both costs as u16 node indices (< 65535 here) in one DPP chain per level
-      const uint32_t m16 = bm < MATCH_LIMIT ? bm : 0xFFFFu;
-      const uint32_t a16 = ba < MATCH_LIMIT ? ba : 0xFFFFu;
-      const uint32_t v = wave_pkmin_u16(m16 | (a16 << 16));
+    SEQ_PH(0);
+    if (PACK16) {  // both costs as u16 node indices (< 65535 here), exchanged in one word
+      // two independent v_min_u32_dpp chains (one instruction per step each), packed after
+      const uint32_t wm = wave_min_u32(bm), wa = wave_min_u32(ba);
+      const uint32_t v = (wm < MATCH_LIMIT ? wm : 0xFFFFu) | ((wa < MATCH_LIMIT ? wa : 0xFFFFu) << 16);
       const uint32_t kx = NEED_KX ? wave_max_u32(bx) : 0u;
+      SEQ_PH(1);
       if (lane == 0) {
         red[par][0][wv] = v;
         if (NEED_KX) red[par][2][wv] = kx;
       }
       lds_barrier();
+      SEQ_PH(2);
       if (!CAP && wv != 0) continue;  // only wave 0 finishes a pod when commits change nothing
-      const uint32_t g = small_pkmin_u16<NW>(lane < NW ? red[par][0][lane] : 0xFFFFFFFFu);
-      im = (g & 0xFFFFu) != 0xFFFFu ? (int64_t)(g & 0xFFFFu) : -1;
-      ia = (g >> 16) != 0xFFFFu ? (int64_t)(g >> 16) : -1;
+      const uint32_t x = lane < NW ? red[par][0][lane] : 0xFFFFFFFFu;
+      const uint32_t gm = small_min_u32<NW>(x & 0xFFFFu), ga = small_min_u32<NW>(x >> 16);
+      im = gm != 0xFFFFu ? (int64_t)gm : -1;
+      ia = ga != 0xFFFFu ? (int64_t)ga : -1;
     } else {
       const uint32_t km = cost_to_key(wave_min_u32(bm));
       const uint32_t ka = cost_to_key(wave_min_u32(ba));
@@ -1170,7 +1197,8 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     const int64_t ix = NEED_KX ? key_to_idx(wave_max_u32(lane < NW ? red[par][2][lane] : 0u)) : -1;
     int32_t sel, st;
     int64_t sc;
-    decode_pod(im, ix, ia, pd != POD_DIGIT_NONE, a.pp, &sel, &sc, &st);
+    SEQ_PH(3);
+    decode_pod(im, ix, ia, pd != POD_DIGIT_NONE, pp, &sel, &sc, &st);
     if (wv == 0) {
       const bool mine = lane == jl;
       o_idx = mine ? sel : o_idx;
@@ -1191,7 +1219,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
           for (int r = 0; r < RS; ++r) {
             const bool hit = mine && r == rs;
             CNT[r] += hit ? 1 : 0;
-            const bool full = hit && CNT[r] >= a.max_pods;
+            const bool full = hit && CNT[r] >= max_pods;
             C0[r] = full ? NOFIT : C0[r];
             C1[r] = full ? NOFIT : C1[r];
           }
@@ -1204,6 +1232,13 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     const int32_t j0 = (a.n_pods - 1) & ~(WAVE - 1);
     store_block(j0, a.n_pods - j0);
   }
+#ifdef MSH_STAMPS
+  if (lane == 0 && wv < 16) {
+    for (int k = 0; k < 6; ++k) msh_stamp_buf[wv * 8 + k] = ph[k];
+    msh_stamp_buf[wv * 8 + 6] = (unsigned long long)a.n_pods;
+  }
+#endif
+#undef SEQ_PH
   if (CAP) {
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
