@@ -130,7 +130,8 @@ def main():
                      "idx": torch.empty(p, dtype=torch.int32, device=dev),
                      "score": torch.empty(p, dtype=torch.int64, device=dev),
                      "status": torch.empty(p, dtype=torch.int32, device=dev),
-                     "keys": torch.zeros(2 * p, dtype=torch.int64, device=dev)})
+                     "keys": torch.zeros(2 * p, dtype=torch.int32, device=dev)})
+    klen = ctx.shard_keys_len(p) if mode == "nodeshard" else 0  # int32 keys one step all-reduces
     main_stream = torch.cuda.current_stream(dev)
     streams = [main_stream] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
 
@@ -151,7 +152,7 @@ def main():
         if ev1 is not None:
             ev1.record(st)
         if mode == "nodeshard":  # RCCL all-reduce(MAX) of the per-shard keys, then decode
-            D.merge_shard_keys_(b["keys"])
+            D.merge_shard_keys_(b["keys"][:klen])
             ctx.decode_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["keys"].data_ptr(), b["idx"].data_ptr(),
                                    b["score"].data_ptr(), b["status"].data_ptr(), sh)
 

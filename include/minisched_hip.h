@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSH_ABI_VERSION 1
+#define MSH_ABI_VERSION 2
 
 /* ---- error codes (return values) ---- */
 typedef enum msh_err {
@@ -178,23 +178,29 @@ int msh_node_pod_counts(msh_ctx* ctx, int32_t* out_counts);
 int msh_reset_node_pod_counts(msh_ctx* ctx);
 
 /* ---- node-sharded mode (a cluster's node table split over devices) ----
- * Each shard holds a contiguous slice [node_base, node_base + n) of the global List order.
- * msh_shard_keys_device writes per pod two int64 keys (layout [2][p]):
- *   keys[0][j] = first feasible node whose NodeNumber class is "match"   (0 = none)
- *   keys[1][j] = first feasible "non-match" node, or (identity-like modes) the first
- *                feasible node of any class                                (0 = none)
- * encoded as INT64 key = 2^32 - 1 - global_idx (+1 offset so 0 means none).
- * Element-wise MAX over shards (RCCL allreduce MAX) yields the global keys; then
- * msh_decode_keys_device produces idx/score/status exactly as msh_schedule_batch. */
+ * Each shard holds a contiguous slice [node_base, node_base + n) of the global List order and
+ * produces int32 keys, key = 0x7FFFFFFF - global_idx (0 = none), so that the element-wise MAX
+ * over shards (one RCCL allreduce MAX) is the global first node. Layout, msh_shard_keys_len
+ * entries = p + s1:
+ *   keys[j], j < p  first feasible node whose NodeNumber class is "match" for pod j
+ *   keys[p + ...]   s1 = 2 when keys[1] is "first feasible of any class" (the identity-like
+ *                   normalize modes: msh_keys_slot1_is_any = 1): that key depends on the pod
+ *                   only through its class, keys[p] = non-tolerating pods, keys[p + 1] =
+ *                   tolerating pods; s1 = p otherwise (REVERSE / MINMAX): keys[p + j] = first
+ *                   feasible "non-match" node of pod j.
+ * 4 B per pod cross the interconnect for the reference plugin set (selectHost over the merged
+ * keys replaces minisched.go:304-325 across shards). msh_decode_keys_device then produces
+ * idx/score/status exactly as msh_schedule_batch over the whole table. */
+int msh_shard_keys_len(const msh_ctx* ctx, int32_t p, int32_t* out_len);
 int msh_shard_keys_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
-                          const uint8_t* d_pod_tol, int64_t node_base, int64_t* d_keys,
+                          const uint8_t* d_pod_tol, int64_t node_base, int32_t* d_keys,
                           void* stream);
 int msh_decode_keys_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
-                           const uint8_t* d_pod_tol, const int64_t* d_keys,
+                           const uint8_t* d_pod_tol, const int32_t* d_keys,
                            int32_t* d_out_idx, int64_t* d_out_score, int32_t* d_out_status,
                            void* stream);
-/* Whether keys[1] holds "first feasible of any class" (1) or "first feasible non-match" (0)
- * under the ctx's current plugin set. */
+/* Whether keys[1] holds "first feasible of any class" (1, per class) or "first feasible
+ * non-match" (0, per pod) under the ctx's current plugin set. */
 int msh_keys_slot1_is_any(const msh_ctx* ctx, int32_t* out_flag);
 
 /* ---- snapshot packer (host, no device needed) ----

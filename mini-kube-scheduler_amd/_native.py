@@ -53,7 +53,7 @@ EXPORTED = (
     "msh_patch_nodes", "msh_export_results",
     "msh_schedule_batch", "msh_schedule_batch_device", "msh_schedule_sequential",
     "msh_schedule_sequential_device", "msh_node_pod_counts", "msh_reset_node_pod_counts",
-    "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
+    "msh_shard_keys_len", "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
     "msh_pack_nodes", "msh_pack_pods", "msh_toleration_tolerates_unschedulable",
 )
 
@@ -93,6 +93,7 @@ _SIGS = {
     "msh_schedule_sequential_device": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, _P]),
     "msh_node_pod_counts": (C.c_int, [_P, _P]),
     "msh_reset_node_pod_counts": (C.c_int, [_P]),
+    "msh_shard_keys_len": (C.c_int, [_P, _I32, C.POINTER(_I32)]),
     "msh_shard_keys_device": (C.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
     "msh_decode_keys_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "msh_keys_slot1_is_any": (C.c_int, [_P, C.POINTER(_I32)]),

@@ -577,8 +577,16 @@ int msh_keys_slot1_is_any(const msh_ctx* c, int32_t* out_flag) {
   return MSH_OK;
 }
 
+int msh_shard_keys_len(const msh_ctx* c, int32_t p, int32_t* out_len) {
+  if (!c || !out_len || p < 0) return MSH_ERR_INVALID;
+  const int64_t len = (int64_t)p + (msh::needs_kx(c->pp) ? (int64_t)p : 2);
+  if (len > INT32_MAX) return MSH_ERR_INVALID;
+  *out_len = (int32_t)len;
+  return MSH_OK;
+}
+
 int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
-                          const uint8_t* d_pod_tol, int64_t node_base, int64_t* d_keys,
+                          const uint8_t* d_pod_tol, int64_t node_base, int32_t* d_keys,
                           void* stream) {
   if (!c) return MSH_ERR_INVALID;
   c->err.clear();
@@ -601,12 +609,12 @@ int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
 }
 
 int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
-                           const uint8_t* d_pod_tol, const int64_t* d_keys, int32_t* d_out_idx,
+                           const uint8_t* d_pod_tol, const int32_t* d_keys, int32_t* d_out_idx,
                            int64_t* d_out_score, int32_t* d_out_status, void* stream) {
   if (!c) return MSH_ERR_INVALID;
   c->err.clear();
   if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
-  if (p > 0 && (!d_pod_digit || !d_keys || !d_out_idx || !d_out_score || !d_out_status))
+  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_keys || !d_out_idx || !d_out_score || !d_out_status))
     return fail(c, MSH_ERR_INVALID, "null device pointer");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

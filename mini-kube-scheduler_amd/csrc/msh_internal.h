@@ -18,7 +18,7 @@ constexpr uint32_t DIGIT_NONE = 0xFFu;           // node suffix is not '0'..'9'
 constexpr uint32_t POD_DIGIT_NONE = 0xFEu;       // never equals a node digit (0..9 / 0xFF)
 constexpr int WAVE = 64;
 constexpr int BATCH_THREADS = 256;               // 4 waves per workgroup
-constexpr int64_t GKEY_MAX = 0xFFFFFFFFll;       // global (sharded) key = GKEY_MAX - global_idx
+constexpr int32_t GKEY_MAX = 0x7FFFFFFF;         // global (sharded) int32 key = GKEY_MAX - global_idx
 // Node "cost" for the first-match search: idx if the node is feasible for the pod class,
 // NOFIT otherwise. cost + |D - pd| * 2^24 (one v_sad_u32) is < 2^24 exactly for feasible
 // nodes whose digit equals the pod's; its unsigned min is the first such node in List order.
@@ -104,7 +104,7 @@ struct BatchArgs {
   int32_t* out_idx;
   int64_t* out_score;
   int32_t* out_status;
-  int64_t* keys;             // shard mode: [2][n_pods] global keys
+  int32_t* keys;             // shard mode: [n_pods + slot-1 count] global keys (msh_shard_keys_len)
   int64_t node_base;
   uint32_t* partial;         // [2][n_pods] running keys when the node table spans > 1 LDS tile
   int32_t unit_q, unit_r;    // work-queue kernel: workgroup b owns unit_q (+1 if b < unit_r) units
@@ -121,7 +121,7 @@ hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, h
                         std::string* err);
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,
-                              const int64_t* keys, int32_t slot1_any, PluginParams pp,
+                              const int32_t* keys, int32_t slot1_any, PluginParams pp,
                               int32_t* out_idx, int64_t* out_score, int32_t* out_status,
                               hipStream_t s);
 

@@ -193,6 +193,19 @@ __device__ __forceinline__ void decode_pod(int64_t im, int64_t ix, int64_t ia, b
   *out_status = st;
 }
 
+// Shard keys (int32): GKEY_MAX - global node index, 0 = none. The slot-1 keys of the
+// identity-like modes are per pod CLASS (first feasible node of that class), written once per
+// launch by the first workgroup: keys[n_pods + c], c = 0 non-tolerating, 1 tolerating.
+__device__ __forceinline__ int32_t shard_key(int64_t node_base, uint32_t local_idx) {
+  return GKEY_MAX - (int32_t)(node_base + (int64_t)local_idx);
+}
+__device__ __forceinline__ void write_class_keys(const BatchArgs& a) {
+  if (blockIdx.x == 0 && threadIdx.x < 2) {
+    const uint32_t b = a.ball[threadIdx.x];
+    a.keys[(size_t)a.n_pods + threadIdx.x] = b ? shard_key(a.node_base, KMAX - b) : 0;
+  }
+}
+
 __device__ __forceinline__ int64_t key_to_idx(uint32_t k) {
   return k ? (int64_t)(KMAX - k) : (int64_t)-1;
 }
@@ -222,6 +235,7 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
   const int32_t p0 = (int32_t)((int64_t)a.n_pods * gw / W);
   const int32_t p1 = (int32_t)((int64_t)a.n_pods * (gw + 1) / W);
   const int32_t ntiles = (a.n_chunks + tile_chunks - 1) / tile_chunks;
+  if (SHARD && !NEED_KX) write_class_keys(a);
   const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
 
   for (int32_t t = 0; t < ntiles; ++t) {
@@ -352,9 +366,8 @@ __global__ __launch_bounds__(BATCH_THREADS) void batch_kernel(BatchArgs a, int32
       }
       const uint32_t ball = tolv ? ball1 : ball0;
       if (SHARD) {
-        const uint32_t k1 = NEED_KX ? res_x : ball;
-        a.keys[j] = res_m ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - res_m))) : 0;
-        a.keys[(size_t)a.n_pods + j] = k1 ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - k1))) : 0;
+        a.keys[j] = res_m ? shard_key(a.node_base, KMAX - res_m) : 0;
+        if (NEED_KX) a.keys[(size_t)a.n_pods + j] = res_x ? shard_key(a.node_base, KMAX - res_x) : 0;
       } else {
         decode_pod(key_to_idx(res_m), key_to_idx(res_x), key_to_idx(ball), pdv != POD_DIGIT_NONE,
                    a.pp, &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
@@ -668,6 +681,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
   const int32_t p1 = (int32_t)((int64_t)a.n_pods * (gw + 1) / W);
   // stage_chunks divides TILE_CHUNKS, so a stage never straddles two compute tiles
   const int32_t nstages = (a.n_chunks + stage_chunks - 1) / stage_chunks;
+  if (SHARD) write_class_keys(a);
   const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
   const uint32_t ucnt = *a.ucount;
   MSH_STAMP(0);
@@ -732,8 +746,7 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       }
       const uint32_t ball = tolv ? ball1 : ball0;
       if (SHARD) {
-        a.keys[j] = res != NOFIT ? (GKEY_MAX - (a.node_base + (int64_t)res)) : 0;
-        a.keys[(size_t)a.n_pods + j] = ball ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - ball))) : 0;
+        a.keys[j] = res != NOFIT ? shard_key(a.node_base, res) : 0;
       } else {
         decode_pod(res != NOFIT ? (int64_t)res : -1, -1, key_to_idx(ball), pcv != CODE_NONE_POD, a.pp,
                    &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
@@ -796,18 +809,20 @@ __device__ __forceinline__ void load_words_lds(uint32_t (&w)[R], const uint4* lw
 }
 
 // `wa` holds chunks [0, R) on entry (requested by the caller together with the pod bytes).
+// NP pod pairs (NP = IDENT_UNIT / 2, 4 or 8): pair q = lanes 2q (low half) and 2q+1 (high).
 template <int R, bool LDSW>
 __device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, uint32_t (&wa)[R], const uint32_t* __restrict__ words,
                                                 __amdgpu_buffer_rsrc_t rs, const uint4* lw, int32_t nc,
                                                 int lane) {
-  static_assert(IDENT_UNIT == 8 && QB == 4, "ident_unit8 scans exactly 4 pod pairs");
+  constexpr int NP = IDENT_UNIT / 2;
+  static_assert((NP == 4 || NP == 8) && QB == 4, "a unit scans 4 or 8 pod pairs, in blocks of 4");
   const uint32_t c = pcv << CODE_SHIFT;
   // quad_perm [1,0,3,2]: lane 2q receives lane 2q+1's code
   const uint32_t partner = (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0xB1, 0xF, 0xF, false);
   const uint32_t ppl = c | (partner << 16);  // pair code, valid in even lanes
-  uint32_t pp[4], bm[4];
+  uint32_t pp[NP], bm[NP];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < NP; ++q) {
     pp[q] = to_vgpr((uint32_t)__builtin_amdgcn_readlane((int)ppl, 2 * q));
     bm[q] = BM_INIT;
   }
@@ -815,34 +830,40 @@ __device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, uint32_t (&wa)[R],
 #ifdef MSH_DIAG_NOLOAD  // timing diagnostic only (wrong results): node words loaded once
   load_words<true>(wb, words, rs, R, lane);
   for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
-    scan_words<R, 4>(wa, pp, bm, 4);
-    scan_words<R, 4>(wb, pp, bm, 4);
+    scan_words<R, NP>(wa, pp, bm, NP);
+    scan_words<R, NP>(wb, pp, bm, NP);
     wa[0] += 1u;
   }
 #else
   if (LDSW) {
     for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
       load_words_lds<R>(wb, lw, c0 + R, lane);
-      scan_words<R, 4>(wa, pp, bm, 4);
+      scan_words<R, NP>(wa, pp, bm, NP);
       load_words_lds<R>(wa, lw, c0 + 2 * R, lane);  // past the table: the LDS pad, never scanned
-      scan_words<R, 4>(wb, pp, bm, 4);
+      scan_words<R, NP>(wb, pp, bm, NP);
     }
   } else {
     for (int32_t c0 = 0; c0 < nc; c0 += 2 * R) {
       load_words<true>(wb, words, rs, c0 + R, lane);
-      scan_words<R, 4>(wa, pp, bm, 4);
+      scan_words<R, NP>(wa, pp, bm, NP);
       load_words<true>(wa, words, rs, c0 + 2 * R, lane);  // past the slice: zeros, never scanned
-      scan_words<R, 4>(wb, pp, bm, 4);
+      scan_words<R, NP>(wb, pp, bm, NP);
     }
   }
 #endif
   const uint32_t lane2 = (uint32_t)lane | ((uint32_t)lane << 16);
-  const uint32_t x = wave_pkmin_u16_x4(pk_fold_lane(bm[0], lane2), pk_fold_lane(bm[1], lane2),
-                                       pk_fold_lane(bm[2], lane2), pk_fold_lane(bm[3], lane2));
-  // pair q's two results sit in row {0, 2, 1, 3}[q] of x; every lane of a row holds them
+  // pair q's two results sit in row {0, 2, 1, 3}[q % 4] of the reduction of its group of four;
+  // every lane of a row holds them, so one ds_bpermute per group brings them to the pods' lanes
   const int q = (lane >> 1) & 3;
   const int row = ((q & 1) << 1) | (q >> 1);
-  const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(row * 16 * 4, (int)x);
+  uint32_t v = 0;
+#pragma unroll
+  for (int g = 0; g < NP / 4; ++g) {
+    const uint32_t x = wave_pkmin_u16_x4(pk_fold_lane(bm[4 * g], lane2), pk_fold_lane(bm[4 * g + 1], lane2),
+                                         pk_fold_lane(bm[4 * g + 2], lane2), pk_fold_lane(bm[4 * g + 3], lane2));
+    const uint32_t vg = (uint32_t)__builtin_amdgcn_ds_bpermute(row * 16 * 4, (int)x);
+    v = (lane >> 3) == g ? vg : v;
+  }
   const uint32_t h = (lane & 1) ? (v >> 16) : (v & 0xFFFFu);
   return h < NOMATCH16 ? h : NOFIT;
 }
@@ -876,6 +897,7 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ball, (short)0, 8, 0x00020000), (lane & 1) * 4, 0, 0);
   const uint32_t uvec = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ucount, (short)0, 4, 0x00020000), 0, 0, 0);
+  if (SHARD) write_class_keys(a);
   // this workgroup's contiguous unit range (host-computed quotient/remainder: no 64-bit division)
   const int32_t b = (int32_t)blockIdx.x;
   const int32_t ub = b * a.unit_q + min(b, a.unit_r);
@@ -953,8 +975,7 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
       const uint32_t ball = tolv ? (uint32_t)__builtin_amdgcn_readlane((int)bvec, 1)
                                  : (uint32_t)__builtin_amdgcn_readlane((int)bvec, 0);
       if (SHARD) {
-        a.keys[j] = res != NOFIT ? (GKEY_MAX - (a.node_base + (int64_t)res)) : 0;
-        a.keys[(size_t)a.n_pods + j] = ball ? (GKEY_MAX - (a.node_base + (int64_t)(KMAX - ball))) : 0;
+        a.keys[j] = res != NOFIT ? shard_key(a.node_base, res) : 0;
       } else {
         decode_pod(res != NOFIT ? (int64_t)res : -1, -1, key_to_idx(ball), pcv != CODE_NONE_POD, a.pp,
                    &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
@@ -976,16 +997,19 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
 
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
 __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restrict__ pod_digit,
-                                                          int32_t p, const int64_t* __restrict__ keys,
+                                                          const uint8_t* __restrict__ pod_tol,
+                                                          int32_t p, const int32_t* __restrict__ keys,
                                                           int32_t slot1_any, PluginParams pp,
                                                           int32_t* __restrict__ out_idx,
                                                           int64_t* __restrict__ out_score,
                                                           int32_t* __restrict__ out_status) {
   const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= p) return;
-  const int64_t k0 = keys[j], k1 = keys[(size_t)p + j];
-  const int64_t ka = slot1_any ? k1 : (k0 > k1 ? k0 : k1);
-  auto idx_of = [](int64_t k) -> int64_t { return k ? GKEY_MAX - k : -1; };
+  // slot 1: the pod's class key (identity-like modes) or its own non-match key (KX modes)
+  const int32_t k0 = keys[j];
+  const int32_t k1 = slot1_any ? keys[(size_t)p + (pod_tol[j] ? 1 : 0)] : keys[(size_t)p + j];
+  const int32_t ka = slot1_any ? k1 : (k0 > k1 ? k0 : k1);
+  auto idx_of = [](int32_t k) -> int64_t { return k ? (int64_t)(GKEY_MAX - k) : -1; };
   const int d = pod_digit[j];
   decode_pod(idx_of(k0), idx_of(k1), idx_of(ka), d >= 0 && d <= 9, pp, &out_idx[j],
              &out_score[j], &out_status[j]);
@@ -1551,12 +1575,11 @@ hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, h
 }
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,
-                              const int64_t* keys, int32_t slot1_any, PluginParams pp,
+                              const int32_t* keys, int32_t slot1_any, PluginParams pp,
                               int32_t* out_idx, int64_t* out_score, int32_t* out_status,
                               hipStream_t s) {
-  (void)pod_tol;
   if (p == 0) return hipSuccess;
-  hipLaunchKernelGGL(decode_keys_kernel, dim3((p + 255) / 256), dim3(256), 0, s, pod_digit, p, keys,
+  hipLaunchKernelGGL(decode_keys_kernel, dim3((p + 255) / 256), dim3(256), 0, s, pod_digit, pod_tol, p, keys,
                      slot1_any, pp, out_idx, out_score, out_status);
   return hipGetLastError();
 }

@@ -9,14 +9,14 @@ at a time, minisched/minisched.go:28-30); both modes below are new:
   contiguous pod range. No data-path collective ("scaling": "weak").
 
 * Node sharding (BASELINE C4: 100k nodes x 1M pods over 8 GPUs). Rank r holds the List-order
-  slice [r*N/W, (r+1)*N/W) of the node table and computes, for every pod, two int64 keys
-  (msh_shard_keys_device): first feasible match and first feasible node (or first feasible
-  non-match for the REVERSE / MINMAX normalizers), each encoded as 2^32-1-global_idx. Because
-  the slices are contiguous and ascending, the element-wise MAX over ranks is the global
-  first match / first feasible node, i.e. exactly the single-GPU answer. One RCCL
-  all-reduce(MAX) of 16 B per pod replaces the all-gather of per-shard bests + merge
-  (same result, ~1/W the bytes per link on a ring); msh_decode_keys_device then yields
-  idx / score / status on every rank.
+  slice [r*N/W, (r+1)*N/W) of the node table and computes int32 keys (msh_shard_keys_device),
+  each 0x7FFFFFFF - global_idx: per pod the first feasible match, and the first feasible node
+  of each pod CLASS (2 keys per launch; per pod, the first feasible non-match, only for the
+  REVERSE / MINMAX normalizers). Because the slices are contiguous and ascending, the
+  element-wise MAX over ranks is the global first match / first feasible node, i.e. exactly
+  the single-GPU answer. One RCCL all-reduce(MAX) of 4 B per pod (+ 8 B) replaces the
+  all-gather of per-shard bests + merge (same result, ~1/W the bytes per link on a ring);
+  msh_decode_keys_device then yields idx / score / status on every rank.
 """
 from __future__ import annotations
 
@@ -24,7 +24,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-GKEY_MAX = 0xFFFFFFFF  # key = GKEY_MAX - global node index, 0 = none (include/minisched_hip.h)
+GKEY_MAX = 0x7FFFFFFF  # int32 key = GKEY_MAX - global node index, 0 = none (include/minisched_hip.h)
 
 
 def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
@@ -35,9 +35,9 @@ def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
 
 
 def encode_key(global_idx: np.ndarray) -> np.ndarray:
-    """Node index (or -1) -> shard key (0 = none)."""
+    """Node index (or -1) -> int32 shard key (0 = none)."""
     g = np.asarray(global_idx, np.int64)
-    return np.where(g >= 0, GKEY_MAX - g, 0).astype(np.int64)
+    return np.where(g >= 0, GKEY_MAX - g, 0).astype(np.int32)
 
 
 def decode_key(key: np.ndarray) -> np.ndarray:
@@ -48,7 +48,7 @@ def decode_key(key: np.ndarray) -> np.ndarray:
 
 def merge_shard_keys_(keys, group=None):
     """In-place element-wise MAX of per-shard keys over the process group (RCCL on GPU
-    tensors, gloo on CPU tensors). `keys` is an int64 tensor of shape [2 * P]."""
+    tensors, gloo on CPU tensors). `keys` is the int32 tensor of msh_shard_keys_len entries."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(keys, op=dist.ReduceOp.MAX, group=group)
@@ -80,11 +80,13 @@ class NodeShardedScheduler:
         ctx.upload_nodes(np.ascontiguousarray(unsched[lo:hi]), np.ascontiguousarray(digit[lo:hi]))
 
     def schedule(self, d_pod_digit, d_pod_tol, d_keys, d_idx, d_score, d_status, stream: int = 0) -> None:
-        """All tensors on this rank's GPU; every rank ends with the global decisions."""
+        """All tensors on this rank's GPU (d_keys: int32, >= ctx.shard_keys_len(p) entries);
+        every rank ends with the global decisions."""
         p = d_pod_digit.numel()
+        klen = self.ctx.shard_keys_len(p)
         self.ctx.shard_keys_device(p, d_pod_digit.data_ptr(), d_pod_tol.data_ptr(), self.shard.lo,
                                    d_keys.data_ptr(), stream)
-        merge_shard_keys_(d_keys, self.group)
+        merge_shard_keys_(d_keys[:klen], self.group)
         self.ctx.decode_keys_device(p, d_pod_digit.data_ptr(), d_pod_tol.data_ptr(), d_keys.data_ptr(),
                                     d_idx.data_ptr(), d_score.data_ptr(), d_status.data_ptr(), stream)
 

@@ -162,6 +162,12 @@ class DeviceContext:
                                                              int(max_pods_per_node), d_idx, d_score,
                                                              d_status, stream or None))
 
+    def shard_keys_len(self, p: int) -> int:
+        """int32 entries msh_shard_keys_device writes for p pods: p + (2 or p)."""
+        v = C.c_int32(0)
+        self._check(self._lib.msh_shard_keys_len(self.handle, int(p), C.byref(v)))
+        return int(v.value)
+
     def shard_keys_device(self, p: int, d_pod_digit: int, d_pod_tol: int, node_base: int, d_keys: int,
                           stream: int = 0) -> None:
         self._check(self._lib.msh_shard_keys_device(self.handle, p, d_pod_digit, d_pod_tol, int(node_base),

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol(msh):
 
 
 def test_abi_version(msh):
-    assert msh._native.lib().msh_abi_version() == 1
+    assert msh._native.lib().msh_abi_version() == 2
 
 
 def test_no_device_is_an_error_not_a_fallback(msh):

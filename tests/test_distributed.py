@@ -2,10 +2,12 @@
 
 The device kernels cannot run here, so each rank's per-shard keys are produced by the
 oracle on that rank's node slice (the contract of msh_shard_keys_device: first feasible
-match / first feasible node of the slice, as 2^32-1-global_idx). What is tested is the
+match / first feasible node of the slice, as 0x7FFFFFFF-global_idx). What is tested is the
 product's sharding arithmetic and collective (merge_shard_keys_ = all_reduce MAX): merged
-keys must decode to exactly the unsharded oracle answer. The GPU side of the same contract
-is tests/test_gpu_parity.py::test_node_shards_merge.
+keys must decode to exactly the unsharded oracle answer. The keys follow the int32 layout of
+msh_shard_keys_device for the reference plugin set: p per-pod match keys, then the two per-class
+first-feasible keys. The GPU side of the same contract is
+tests/test_gpu_parity.py::test_node_shards_merge.
 """
 from __future__ import annotations
 
@@ -44,14 +46,16 @@ def _shard_keys_oracle(O, dist_mod, u, nd, pd, pt, lo, hi):
     us, ns = u[lo:hi], nd[lo:hi]
     p = len(pd)
     first_match = np.full(p, -1, np.int64)
-    first_feas = np.full(p, -1, np.int64)
     for j in range(p):
         feas = np.ones(hi - lo, bool) if pt[j] else (us == 0)
+        m = feas & (ns == pd[j]) & (pd[j] >= 0)
+        if m.any():
+            first_match[j] = lo + int(np.argmax(m))
+    # first feasible node per pod class: [non-tolerating, tolerating]
+    first_feas = np.full(2, -1, np.int64)
+    for cls, feas in enumerate([(us == 0), np.ones(hi - lo, bool)]):
         if feas.any():
-            first_feas[j] = lo + int(np.argmax(feas))
-            m = feas & (ns == pd[j]) & (pd[j] >= 0)
-            if m.any():
-                first_match[j] = lo + int(np.argmax(m))
+            first_feas[cls] = lo + int(np.argmax(feas))
     return np.concatenate([dist_mod.encode_key(first_match), dist_mod.encode_key(first_feas)])
 
 
@@ -68,7 +72,8 @@ def _worker(rank, world, port, seed, n, p, out_q):
     keys = torch.from_numpy(_shard_keys_oracle(O, D, u, nd, pd, pt, lo, hi))
     D.merge_shard_keys_(keys)
     k = keys.numpy()
-    im, ia = D.decode_key(k[:p]), D.decode_key(k[p:])
+    assert keys.dtype == torch.int32 and len(k) == p + 2
+    im, ia = D.decode_key(k[:p]), D.decode_key(k[p:])[pt.astype(np.int64)]
     # decode exactly as decode_pod (NONE mode, reference plugin set)
     idx = np.where(ia < 0, -1, np.where(pd < 0, -1, np.where(im >= 0, im, ia)))
     status = np.where(ia < 0, 1, np.where(pd < 0, 2, 0))

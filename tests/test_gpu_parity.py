@@ -250,17 +250,20 @@ def test_node_shards_merge(msh, gpu_ctx, oracle, norm):
     d_pd = torch.from_numpy(pd).to(dev)
     d_pt = torch.from_numpy(pt).to(dev)
     p = len(pd)
-    merged = torch.zeros(2 * p, dtype=torch.int64, device=dev)
     bounds = [0, 1234, 5000, 5001, 9000]
-    ctxs = []
+    ctxs, merged = [], None
     for a, b in zip(bounds[:-1], bounds[1:]):
         c = msh.DeviceContext(0)
         _set(c, msh, ps)
         c.upload_nodes(u[a:b], nd[a:b])
-        keys = torch.empty(2 * p, dtype=torch.int64, device=dev)
+        klen = c.shard_keys_len(p)
+        # 4 B per pod + 2 class keys for the identity-like modes, 8 B per pod for REVERSE / MINMAX
+        assert klen == (2 * p if norm in (2, 3) else p + 2)
+        keys = torch.full((klen,), -7, dtype=torch.int32, device=dev)  # every entry must be written
         c.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), a, keys.data_ptr(),
                             torch.cuda.current_stream().cuda_stream)
-        merged = torch.maximum(merged, keys)
+        assert int(keys.min()) >= 0
+        merged = keys if merged is None else torch.maximum(merged, keys)
         ctxs.append(c)
     oi = torch.empty(p, dtype=torch.int32, device=dev)
     osc = torch.empty(p, dtype=torch.int64, device=dev)
