@@ -6,6 +6,7 @@ seeded inputs; large sizes additionally against the independent closed form.
 """
 from __future__ import annotations
 
+import importlib
 import itertools
 import json
 from pathlib import Path
@@ -207,6 +208,47 @@ def test_c3_full_and_weight3(msh, gpu_ctx, oracle, synth):
     got3 = gpu_ctx.schedule_batch(pd, pt)
     assert (got3[0] == got1[0]).all() and (got3[2] == got1[2]).all()
     assert (got3[1] == 3 * got1[1]).all()
+
+
+def test_c4_full_size_batch_and_shards(msh, gpu_ctx, synth):
+    """BASELINE config C4 at full size on one device: 100k nodes x 1M pods, checked through the
+    independent closed form (the scalar oracle would need minutes). Both the whole-table batch
+    (multi-tile work-queue kernel) and the 8-way node-sharded path (per-shard int32 keys,
+    element-wise MAX, device decode), with pods also permuted: every pod's decision must move
+    with it (pods are independent)."""
+    torch = pytest.importorskip("torch")
+    u, nd, pd, pt = synth.make_soa(100_000, 1_000_000)
+    want = closed_form(u, nd, pd, pt)
+    gpu_ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+    gpu_ctx.upload_nodes(u, nd)
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, "C4 batch")
+    perm = np.random.default_rng(5).permutation(len(pd))
+    got_p = gpu_ctx.schedule_batch(np.ascontiguousarray(pd[perm]), np.ascontiguousarray(pt[perm]))
+    _assert_same(got_p, tuple(w[perm] for w in want), "C4 permuted pods")
+
+    dev = torch.device("cuda:0")
+    d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+    p, world = len(pd), 8
+    D = importlib.import_module("mini-kube-scheduler_amd.distributed")
+    merged, ctxs = None, []
+    for r in range(world):
+        lo, hi = D.shard_range(len(u), world, r)
+        c = msh.DeviceContext(0)
+        c.upload_nodes(u[lo:hi], nd[lo:hi])
+        keys = torch.empty(c.shard_keys_len(p), dtype=torch.int32, device=dev)
+        c.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), lo, keys.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+        merged = keys if merged is None else torch.maximum(merged, keys)
+        ctxs.append(c)
+    oi = torch.empty(p, dtype=torch.int32, device=dev)
+    osc = torch.empty(p, dtype=torch.int64, device=dev)
+    ost = torch.empty(p, dtype=torch.int32, device=dev)
+    ctxs[0].decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), merged.data_ptr(), oi.data_ptr(),
+                               osc.data_ptr(), ost.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, "C4 8 shards")
+    for c in ctxs:
+        c.close()
 
 
 @pytest.mark.parametrize("seq_waves", ["4", "8", "16"])
