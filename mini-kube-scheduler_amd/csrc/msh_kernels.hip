@@ -206,6 +206,32 @@ __device__ __forceinline__ void write_class_keys(const BatchArgs& a) {
   }
 }
 
+// decode_pod for the identity-like modes (NONE, DEFAULT: everything that does not need the
+// first feasible non-match), as selects on launch-constant flags instead of a branch per mode.
+struct IdentDecode {
+  bool err_all;      // NodeNumber scores without its PreScore state: every feasible pod errors
+  bool err_nodigit;  // ... with it: pods whose name has no digit suffix error
+  bool use_im;       // NodeNumber scores at all (otherwise every total is 0: first feasible)
+  int64_t sm;        // total score of a match: weight x (10 raw, or 100 normalized)
+};
+__device__ __forceinline__ IdentDecode make_ident_decode(const PluginParams& pp) {
+  IdentDecode d;
+  d.err_all = pp.has_nn_score && !pp.nn_prescore;
+  d.err_nodigit = pp.has_nn_score && pp.nn_prescore;
+  d.use_im = pp.has_nn_score != 0;
+  d.sm = (pp.mode == 1 ? 100 : 10) * pp.weight;
+  return d;
+}
+__device__ __forceinline__ void decode_ident(int64_t im, int64_t ia, bool pd_valid, const IdentDecode& d,
+                                             int32_t* out_idx, int64_t* out_score, int32_t* out_status) {
+  const bool fit = ia < 0;                                         // FitError (minisched.go:143)
+  const bool serr = !fit && (d.err_all || (d.err_nodigit && !pd_valid));  // Score error (nodenumber.go:74-77)
+  const bool hit = d.use_im && im >= 0;
+  *out_status = fit ? 1 : (serr ? 2 : 0);
+  *out_idx = (fit || serr) ? -1 : (int32_t)(hit ? im : ia);
+  *out_score = (fit || serr || !hit) ? 0 : d.sm;
+}
+
 __device__ __forceinline__ int64_t key_to_idx(uint32_t k) {
   return k ? (int64_t)(KMAX - k) : (int64_t)-1;
 }
@@ -748,8 +774,8 @@ __global__ __launch_bounds__(IDENT_THREADS) void ident_kernel(BatchArgs a, int32
       if (SHARD) {
         a.keys[j] = res != NOFIT ? shard_key(a.node_base, res) : 0;
       } else {
-        decode_pod(res != NOFIT ? (int64_t)res : -1, -1, key_to_idx(ball), pcv != CODE_NONE_POD, a.pp,
-                   &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
+        decode_ident(res != NOFIT ? (int64_t)res : -1, key_to_idx(ball), pcv != CODE_NONE_POD,
+                     make_ident_decode(a.pp), &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
       }
     }
   }
@@ -977,8 +1003,8 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
       if (SHARD) {
         a.keys[j] = res != NOFIT ? shard_key(a.node_base, res) : 0;
       } else {
-        decode_pod(res != NOFIT ? (int64_t)res : -1, -1, key_to_idx(ball), pcv != CODE_NONE_POD, a.pp,
-                   &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
+        decode_ident(res != NOFIT ? (int64_t)res : -1, key_to_idx(ball), pcv != CODE_NONE_POD,
+                     make_ident_decode(a.pp), &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
       }
     }
   }
@@ -1107,6 +1133,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
                "+s"(pp.weight));
   int32_t max_pods = a.max_pods;
   asm volatile("" : "+s"(max_pods));
+  const IdentDecode idec = make_ident_decode(pp);
   uint32_t pdv = POD_DIGIT_NONE, tolv = 0;
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
@@ -1222,7 +1249,10 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     int32_t sel, st;
     int64_t sc;
     SEQ_PH(3);
-    decode_pod(im, ix, ia, pd != POD_DIGIT_NONE, pp, &sel, &sc, &st);
+    if (NEED_KX)
+      decode_pod(im, ix, ia, pd != POD_DIGIT_NONE, pp, &sel, &sc, &st);
+    else
+      decode_ident(im, ia, pd != POD_DIGIT_NONE, idec, &sel, &sc, &st);
     if (wv == 0) {
       const bool mine = lane == jl;
       o_idx = mine ? sel : o_idx;
