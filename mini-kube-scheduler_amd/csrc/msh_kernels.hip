@@ -1046,11 +1046,10 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
 // lives in registers (chunk c is owned by wave c % NW, slot c / NW). Per pod: every wave
 // scans its chunks -- first-match cost (v_sad_u32, as the compare/select-free IDENT form),
 // first-feasible cost, and the non-match key when the normalize mode needs it --, reduces
-// across lanes with DPP (the two costs packed in one u16x2 chain when the table has fewer
-// than 65535 nodes), exchanges one word per wave through LDS behind one barrier
-// (double-buffered by pod parity), finishes the reduction redundantly in every wave (NW lanes:
-// log2(NW) DPP steps), and the owner lane commits: count += 1 and, with a capacity, the node
-// turns infeasible for both classes. The per-pod latency (scan + 2 reductions + 1 barrier), not
+// across lanes with DPP, and lane 0 folds the wave's result into the pod's LDS slot with LDS
+// atomics (min / max; slots triple-buffered). After one barrier the pod's result is a single
+// broadcast read, decoded and committed: count += 1 and, with a capacity, the owning lane
+// retires a full node. The per-pod latency (scan + 1 reduction + 1 barrier + decode), not
 // throughput, bounds it, so nothing else may wait on memory inside the loop:
 //   * the barrier fences LDS only (a plain __syncthreads() is a workgroup fence over global
 //     memory too: `s_waitcnt vmcnt(0)`, i.e. every pod would wait for the previous pod's stores);
@@ -1064,20 +1063,17 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// u32 min over lanes 0..NW-1 (the others hold the identity); result read from lane 0.
-template <int NW>
-__device__ __forceinline__ uint32_t small_min_u32(uint32_t v) {
-  static_assert(NW == 4 || NW == 8 || NW == 16, "NW must be 4, 8 or 16");
-  v = dpp_step<true, 0xB1, 0xF>(v);                // quad_perm [1,0,3,2]
-  v = dpp_step<true, 0x4E, 0xF>(v);                // quad_perm [2,3,0,1]
-  if (NW >= 8) v = dpp_step<true, 0x141, 0xF>(v);  // row_half_mirror: lanes 0..7
-  if (NW >= 16) v = dpp_step<true, 0x140, 0xF>(v); // row_mirror: lanes 0..15
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-}
-
-template <int RS, int NW, bool NEED_KX, bool PACK16, bool CAP>
+// CAP (max_pods_per_node > 0): a commit can make a node infeasible, so every wave reads each
+// pod's result and the owning lane updates its registers before the next pod. Without a
+// capacity a commit changes nothing the next pod reads: only wave 0 reads the result, decodes,
+// keeps the output and adds the commit to a per-node count table held in LDS; the other waves
+// go straight on to the next pod's scan (the barrier per pod still orders every commit before
+// the next pod is decided).
+template <int RS, int NW, bool NEED_KX, bool CAP>
 __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
-  __shared__ uint32_t red[2][3][NW];
+  // per-pod exchange slots, triple-buffered: [slot][first-match cost, first-feasible cost,
+  // non-match key]
+  __shared__ uint32_t xs[3][3];
   extern __shared__ int32_t lcnt[];  // !CAP: [n_chunks * 64] per-node pod counts
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1108,6 +1104,9 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
   if (!CAP) {  // ordered before wave 0's first commit by the first pod's barrier
     for (int32_t i = threadIdx.x; i < a.n_chunks * WAVE; i += NW * WAVE) lcnt[i] = a.counts[i];
   }
+  if (threadIdx.x < 9) xs[threadIdx.x / 3][threadIdx.x % 3] = (threadIdx.x % 3 == 2) ? 0u : 0xFFFFFFFFu;
+  __syncthreads();  // the slots' identities before any wave's first fold
+  int sl = 0;
 
   // Drain the node-state loads here: otherwise the waitcnt pass, unsure they have landed on the
   // loop's class-0 path, waits for every outstanding load (the pod prefetch included) there.
@@ -1211,41 +1210,36 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
         bx = umax(bx, D[r] == pds ? 0u : k);
       }
     }
-    const int par = j & 1;
-    int64_t im, ia;
     SEQ_PH(0);
-    if (PACK16) {  // both costs as u16 node indices (< 65535 here), exchanged in one word
-      // two independent v_min_u32_dpp chains (one instruction per step each), packed after
-      const uint32_t wm = wave_min_u32(bm), wa = wave_min_u32(ba);
-      const uint32_t v = (wm < MATCH_LIMIT ? wm : 0xFFFFu) | ((wa < MATCH_LIMIT ? wa : 0xFFFFu) << 16);
-      const uint32_t kx = NEED_KX ? wave_max_u32(bx) : 0u;
-      SEQ_PH(1);
-      if (lane == 0) {
-        red[par][0][wv] = v;
-        if (NEED_KX) red[par][2][wv] = kx;
-      }
-      lds_barrier();
-      SEQ_PH(2);
-      if (!CAP && wv != 0) continue;  // only wave 0 finishes a pod when commits change nothing
-      const uint32_t x = lane < NW ? red[par][0][lane] : 0xFFFFFFFFu;
-      const uint32_t gm = small_min_u32<NW>(x & 0xFFFFu), ga = small_min_u32<NW>(x >> 16);
-      im = gm != 0xFFFFu ? (int64_t)gm : -1;
-      ia = ga != 0xFFFFu ? (int64_t)ga : -1;
-    } else {
-      const uint32_t km = cost_to_key(wave_min_u32(bm));
-      const uint32_t ka = cost_to_key(wave_min_u32(ba));
-      const uint32_t kx = NEED_KX ? wave_max_u32(bx) : 0u;
-      if (lane == 0) {
-        red[par][0][wv] = km;
-        red[par][1][wv] = ka;
-        red[par][2][wv] = kx;
-      }
-      lds_barrier();
-      if (!CAP && wv != 0) continue;
-      im = key_to_idx(wave_max_u32(lane < NW ? red[par][0][lane] : 0u));
-      ia = key_to_idx(wave_max_u32(lane < NW ? red[par][1][lane] : 0u));
+    // Cross-wave exchange: lane 0 of every wave folds its wave's result into this pod's slot with
+    // LDS atomics (min of the two costs, max of the non-match key), so after the barrier the pod's
+    // result is ONE broadcast read: no second reduction on the critical path.
+    const uint32_t wm = wave_min_u32(bm), wa = wave_min_u32(ba);
+    const uint32_t wx = NEED_KX ? wave_max_u32(bx) : 0u;
+    SEQ_PH(1);
+    if (lane == 0) {
+      atomicMin(&xs[sl][0], wm);
+      atomicMin(&xs[sl][1], wa);
+      if (NEED_KX) atomicMax(&xs[sl][2], wx);
     }
-    const int64_t ix = NEED_KX ? key_to_idx(wave_max_u32(lane < NW ? red[par][2][lane] : 0u)) : -1;
+    lds_barrier();
+    SEQ_PH(2);
+    const int sl_now = sl;
+    sl = sl == 2 ? 0 : sl + 1;
+    if (!CAP && wv != 0) continue;  // only wave 0 finishes a pod when commits change nothing
+    const uint32_t gm = xs[sl_now][0], ga = xs[sl_now][1];
+    const uint32_t gx = NEED_KX ? xs[sl_now][2] : 0u;
+    // the slot read one pod ago is free now (every reader passed this pod's barrier) and is next
+    // folded into two pods ahead (after the next barrier): wave 0 resets it in between
+    if (wv == 0 && lane == 0) {
+      const int sr = sl_now == 0 ? 2 : sl_now - 1;
+      xs[sr][0] = 0xFFFFFFFFu;
+      xs[sr][1] = 0xFFFFFFFFu;
+      xs[sr][2] = 0u;
+    }
+    const int64_t im = gm < MATCH_LIMIT ? (int64_t)gm : -1;  // costs: node index, or >= 2^24 = none
+    const int64_t ia = ga < MATCH_LIMIT ? (int64_t)ga : -1;
+    const int64_t ix = NEED_KX ? key_to_idx(gx) : -1;
     int32_t sel, st;
     int64_t sc;
     SEQ_PH(3);
@@ -1617,25 +1611,14 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
 namespace {
 template <int RS, int NW>
 hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
-  const bool pack = a.n_nodes < 0xFFFF;
   const dim3 blk(NW * 64);
   const size_t lds = (size_t)a.n_chunks * WAVE * sizeof(int32_t);  // !CAP count table
   if (a.max_pods > 0) {
-    if (needs_kx(a.pp)) {
-      if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, true, true, true>), dim3(1), blk, 0, s, a);
-      else hipLaunchKernelGGL((seq_kernel<RS, NW, true, false, true>), dim3(1), blk, 0, s, a);
-    } else {
-      if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, false, true, true>), dim3(1), blk, 0, s, a);
-      else hipLaunchKernelGGL((seq_kernel<RS, NW, false, false, true>), dim3(1), blk, 0, s, a);
-    }
+    if (needs_kx(a.pp)) hipLaunchKernelGGL((seq_kernel<RS, NW, true, true>), dim3(1), blk, 0, s, a);
+    else hipLaunchKernelGGL((seq_kernel<RS, NW, false, true>), dim3(1), blk, 0, s, a);
   } else {
-    if (needs_kx(a.pp)) {
-      if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, true, true, false>), dim3(1), blk, lds, s, a);
-      else hipLaunchKernelGGL((seq_kernel<RS, NW, true, false, false>), dim3(1), blk, lds, s, a);
-    } else {
-      if (pack) hipLaunchKernelGGL((seq_kernel<RS, NW, false, true, false>), dim3(1), blk, lds, s, a);
-      else hipLaunchKernelGGL((seq_kernel<RS, NW, false, false, false>), dim3(1), blk, lds, s, a);
-    }
+    if (needs_kx(a.pp)) hipLaunchKernelGGL((seq_kernel<RS, NW, true, false>), dim3(1), blk, lds, s, a);
+    else hipLaunchKernelGGL((seq_kernel<RS, NW, false, false>), dim3(1), blk, lds, s, a);
   }
   return hipGetLastError();
 }
