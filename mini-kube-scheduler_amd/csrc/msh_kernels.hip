@@ -1532,6 +1532,10 @@ hipError_t launch_ident_dyn_nt(const BatchArgs& a, const DeviceInfo& dev, hipStr
     const int k = atoi(env);
     if (k > 0) grid = (int64_t)dev.cus * (k < occ ? k : occ);
   }
+  if (const char* env = getenv("MSH_BATCH_GRID")) {  // tuning / A-B only: explicit workgroup count
+    const int k = atoi(env);
+    if (k > 0) grid = k;
+  }
   const int64_t grid_units = (n_units + WPG - 1) / WPG;
   if (grid > grid_units) grid = grid_units;
   if (grid < 1) grid = 1;
