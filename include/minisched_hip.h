@@ -93,7 +93,8 @@ int msh_device_count(int* out_count);
 
 /* Create/destroy a context on `device`. Default plugin set = the reference's
  * (initialize.go:80-123): filter=[NodeUnschedulable], prescore=[NodeNumber],
- * score=[NodeNumber] weight 1, normalize NONE. */
+ * score=[NodeNumber] weight 1, normalize NONE. msh_destroy first waits for every stream of the
+ * device (launches the caller queued with the *_device entry points read the ctx's tables). */
 int msh_create(int device, msh_ctx** out_ctx);
 void msh_destroy(msh_ctx* ctx);
 

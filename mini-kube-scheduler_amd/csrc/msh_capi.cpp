@@ -249,7 +249,8 @@ int msh_create(int device, msh_ctx** out_ctx) {
 void msh_destroy(msh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  // launches queued on caller streams (the *_device entry points) may still read the tables
+  (void)hipDeviceSynchronize();
   free_nodes(c);
   free_pods(c);
   (void)hipFree(c->d_partial);
