@@ -164,7 +164,8 @@ int msh_schedule_batch_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit
  * NodeInfo.AddPod analogue). max_pods_per_node > 0 additionally makes a node infeasible
  * once it holds that many pods (build extension); 0 = reference semantics, where the
  * placements equal msh_schedule_batch's. `commit_cb` (may be NULL) is replayed on the host
- * after the device run, in placement order, once per PLACED pod. */
+ * after the device run, in placement order, once per PLACED pod. The counts carry over from
+ * call to call, so sequential launches on one ctx must not overlap: keep them on one stream. */
 typedef void (*msh_commit_cb)(void* user, int32_t pod, int32_t node_idx, int64_t score);
 int msh_schedule_sequential(msh_ctx* ctx, int32_t p, const int8_t* pod_digit,
                             const uint8_t* pod_tol, int32_t max_pods_per_node,
