@@ -38,7 +38,7 @@ from typing import Any, Callable, Iterable, Mapping, Sequence
 import numpy as np
 
 from .framework import NODE_NUMBER, NODE_UNSCHEDULABLE
-from .snapshot import pack_pods, pod_name
+from .snapshot import pack_pods, pod_fields
 
 WILDCARD = "*"
 NODE = "Node"
@@ -250,8 +250,9 @@ class SchedulingQueue:
     def add_many(self, pods: Iterable[Any]) -> np.ndarray:
         """Add for a list of pod objects, packed once (one msh_pack_pods call)."""
         pods = list(pods)
-        table = pack_pods(pods)
-        keys = [self.key_of(pod_name(p), _namespace(p)) for p in pods]
+        fields = pod_fields(pods)
+        table = pack_pods(pods, fields)
+        keys = [f"{n}_{ns}" for n, ns in zip(fields[0], fields[1])]  # keyFunc, queue.go:152-154
         ids = self._intern(keys, table.names, pods, table.digit, table.tolerates)
         self._push_active(ids)
         return ids
@@ -384,10 +385,3 @@ class SchedulingQueue:
     def id_of(self, name: str, namespace: str = "") -> int:
         return self._key_to_id[self.key_of(name, namespace)]
 
-
-def _namespace(p: Any) -> str:
-    if isinstance(p, Mapping):
-        return (p.get("metadata") or {}).get("namespace", "") or p.get("namespace", "") or ""
-    md = getattr(p, "metadata", None)
-    ns = getattr(md, "namespace", None) if md is not None else None
-    return ns if ns is not None else getattr(p, "namespace", "") or ""

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import Any, Iterable, Sequence
+from typing import Any, Iterable, Mapping, Sequence
 
 import numpy as np
 
@@ -103,15 +103,41 @@ def pack_nodes(nodes: Iterable[Any]) -> NodeTable:
     return NodeTable([names[i] for i in order], out_u, out_d, order)
 
 
-def pack_pods(pods: Iterable[Any]) -> PodTable:
+def pod_fields(pods: Sequence[Any]) -> tuple[list[str], list[str], list[Sequence[Any]]]:
+    """(names, namespaces, tolerations) of pod objects in one pass. k8s-shaped dicts take a
+    direct path (the informer's common case); anything else goes through the accessors."""
+    names, spaces, tols = [], [], []
+    for p in pods:
+        if type(p) is dict:
+            md = p.get("metadata") or {}
+            names.append(md.get("name") or "")
+            spaces.append(md.get("namespace") or p.get("namespace") or "")
+            tols.append((p.get("spec") or {}).get("tolerations") or ())
+        else:
+            names.append(pod_name(p))
+            spaces.append(pod_namespace(p))
+            tols.append(pod_tolerations(p))
+    return names, spaces, tols
+
+
+def pod_namespace(p: Any) -> str:
+    if isinstance(p, Mapping):
+        return (p.get("metadata") or {}).get("namespace", "") or p.get("namespace", "") or ""
+    md = getattr(p, "metadata", None)
+    ns = getattr(md, "namespace", None) if md is not None else None
+    return ns if ns is not None else getattr(p, "namespace", "") or ""
+
+
+def pack_pods(pods: Iterable[Any], fields: tuple[list[str], list[str], list[Sequence[Any]]] | None = None) -> PodTable:
+    """`fields`: pod_fields(pods) when the caller already has them."""
     pods = list(pods)
-    names = [pod_name(p) for p in pods]
+    names, _, tol_lists = fields if fields is not None else pod_fields(pods)
     blob, off = _blob(names)
     tols_flat: list[N.Toleration] = []
     keep: list[bytes] = []  # keep encoded strings alive for the call
     tol_off = np.zeros(len(pods) + 1, np.int64)
-    for j, p in enumerate(pods):
-        for t in pod_tolerations(p):
+    for j, tl in enumerate(tol_lists):
+        for t in tl:
             fields = [_tol_field(t, "key"), _tol_field(t, "operator", "op"), _tol_field(t, "value"),
                       _tol_field(t, "effect")]
             enc = [f.encode("utf-8") for f in fields]
