@@ -371,3 +371,26 @@ def test_pipelined_streams(msh, gpu_ctx, oracle, n, norm):
     for (pd, pt), (_, (oi, osc, ost)) in zip(batches, outs):
         want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
         _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"n={n} norm={norm}")
+
+
+def test_maximum_node_table(msh, gpu_ctx, synth):
+    """The largest table a ctx accepts (2^24 - 2 nodes, 261 compute tiles) against the closed
+    form, with matches placed only in the last tile for some digits; one node more is
+    MSH_ERR_INVALID, never a silent truncation."""
+    n = 0xFFFFFE
+    rng = np.random.default_rng(24)
+    u = (rng.random(n) < 0.5).astype(np.uint8)
+    nd = np.full(n, 9, np.int8)
+    nd[-3000:] = rng.integers(0, 9, 3000).astype(np.int8)   # digits 0..8 only near the end
+    pd = rng.integers(-1, 10, 512).astype(np.int8)
+    pt = (rng.random(512) < 0.3).astype(np.uint8)
+    gpu_ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+    gpu_ctx.upload_nodes(u, nd)
+    got = gpu_ctx.schedule_batch(pd, pt)
+    _assert_same(got, closed_form(u, nd, pd, pt), "max table")
+    placed = (got[2] == 0) & (pd >= 0) & (pd <= 8)
+    assert placed.any() and (got[0][placed] >= n - 3000).all()
+    with pytest.raises(msh.MshError):
+        gpu_ctx.upload_nodes(np.zeros(n + 1, np.uint8), np.zeros(n + 1, np.int8))
+    gpu_ctx.upload_nodes(u[:10], nd[:10])  # the ctx stays usable after the rejected upload
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), closed_form(u[:10], nd[:10], pd, pt), "after reject")
