@@ -1021,6 +1021,94 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
 #endif
 }
 
+// ---------------------------------------------------------------------------------------
+// Node-split IDENT kernel: few pods against a large table. The work-queue kernel gives each
+// 8-pod unit to ONE wave, which then scans the whole table: with 512 pods and 100k nodes, 64
+// waves scan 1,563 chunks each while the rest of the chip idles (71 us for 5e7 evaluations).
+// Here a TEAM of SPLIT waves of one workgroup shares a unit: wave k scans the k-th slice of
+// `slice_chunks` chunks (a multiple of 16, cut at compute-tile boundaries as needed), the
+// team's per-pod firsts meet in LDS by atomicMin (slices ascend in List order, so the min is
+// the first match of the whole table), and the team's first wave runs the tolerating-pod pass
+// and the decode. 16 / SPLIT units per workgroup round, two barriers per round; no global
+// scratch, so launches on different streams stay independent.
+// ---------------------------------------------------------------------------------------
+template <int R, bool SHARD, int SPLIT>
+__global__ __launch_bounds__(DYN_THREADS) void ident_split_kernel(BatchArgs a, int32_t slice_chunks) {
+  constexpr int WPG = DYN_THREADS / WAVE;
+  constexpr int TEAMS = WPG / SPLIT;
+  static_assert(SPLIT >= 2 && WPG % SPLIT == 0, "SPLIT divides the workgroup's 16 waves");
+  __shared__ uint32_t slot[TEAMS][IDENT_UNIT];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int team = wv / SPLIT, k = wv % SPLIT;
+  const uint32_t bvec = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ball, (short)0, 8, 0x00020000), (lane & 1) * 4, 0, 0);
+  const uint32_t uvec = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ucount, (short)0, 4, 0x00020000), 0, 0, 0);
+  if (SHARD) write_class_keys(a);
+  const int32_t b = (int32_t)blockIdx.x;
+  const int32_t ub = b * a.unit_q + min(b, a.unit_r);
+  const int32_t n_units = a.unit_q + (b < a.unit_r ? 1 : 0);
+  const int32_t g0 = ub * IDENT_UNIT;
+  const int32_t g1 = min(g0 + n_units * IDENT_UNIT, a.n_pods);
+  // this wave's slice of the table, in global chunks
+  const int32_t c_lo = min(k * slice_chunks, a.n_chunks);
+  const int32_t c_hi = min(c_lo + slice_chunks, a.n_chunks);
+  if (threadIdx.x < TEAMS * IDENT_UNIT) slot[threadIdx.x / IDENT_UNIT][threadIdx.x % IDENT_UNIT] = NOFIT;
+  __syncthreads();
+  for (int32_t r0 = 0; r0 < n_units; r0 += TEAMS) {  // uniform over the workgroup
+    const int32_t u = r0 + team;
+    const bool has = u < n_units;
+    const int32_t w0 = g0 + u * IDENT_UNIT;
+    const int32_t nwin = has ? min((int32_t)IDENT_UNIT, g1 - w0) : 0;
+    const bool act = lane < nwin;
+    uint32_t pcv = CODE_NONE_POD, tolv = 0;
+    if (act) {
+      const int d = a.pod_digit[w0 + lane];
+      pcv = (d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
+      tolv = a.pod_tol[w0 + lane] ? 1u : 0u;
+    }
+    const unsigned long long m = __ballot(act && pcv != CODE_NONE_POD);
+    uint32_t res = NOFIT;
+    if (m) {
+      // the slice's pieces, one per compute tile it touches (word halves are tile-relative)
+      for (int32_t c = c_lo; c < c_hi;) {
+        const int32_t t0 = c / TILE_CHUNKS * TILE_CHUNKS;
+        const int32_t hi = min(c_hi, t0 + TILE_CHUNKS);
+        const uint32_t* wt = a.w0 + (size_t)c * WAVE;
+        const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)wt, (short)0, (hi - c) * WAVE * (int32_t)sizeof(uint32_t), 0x00020000);
+        uint32_t wa[R];
+        load_words<true>(wa, wt, rst, 0, lane);
+        const uint32_t rt = ident_unit8<R, false>(pcv, wa, wt, rst, nullptr, hi - c, lane);
+        // pieces ascend in List order: the first piece with a match holds the slice's first
+        if (res == NOFIT && rt != NOFIT) res = (uint32_t)(t0 / TILE_CHUNKS) * (uint32_t)TILE_NODES + rt;
+        c = hi;
+      }
+      if (act && res != NOFIT) atomicMin(&slot[team][lane], res);
+    }
+    __syncthreads();
+    if (k == 0 && has) {
+      res = act ? slot[team][lane] : NOFIT;
+      const unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
+      if (mt) res = ulist_pass(mt, pcv, res, a.ulist, (uint32_t)__builtin_amdgcn_readfirstlane((int)uvec), lane);
+      if (act) {
+        const int32_t j = w0 + lane;
+        if (SHARD) {
+          a.keys[j] = res != NOFIT ? shard_key(a.node_base, res) : 0;
+        } else {
+          const uint32_t ball = tolv ? (uint32_t)__builtin_amdgcn_readlane((int)bvec, 1)
+                                     : (uint32_t)__builtin_amdgcn_readlane((int)bvec, 0);
+          decode_ident(res != NOFIT ? (int64_t)res : -1, key_to_idx(ball), pcv != CODE_NONE_POD,
+                       make_ident_decode(a.pp), &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
+        }
+        slot[team][lane] = NOFIT;  // ready for the next round (ordered by the barrier below)
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
 __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restrict__ pod_digit,
                                                           const uint8_t* __restrict__ pod_tol,
@@ -1546,9 +1634,47 @@ hipError_t launch_ident_dyn_nt(const BatchArgs& a, const DeviceInfo& dev, hipStr
   return hipGetLastError();
 }
 
+template <bool SHARD, int SPLIT>
+hipError_t launch_ident_split_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s, int32_t slice_chunks) {
+  auto kern = ident_split_kernel<IDENT_R, SHARD, SPLIT>;
+  const int occ = cached_occupancy(reinterpret_cast<const void*>(kern), DYN_THREADS, 0);
+  constexpr int TEAMS = DYN_THREADS / WAVE / SPLIT;
+  const int64_t n_units = ((int64_t)a.n_pods + IDENT_UNIT - 1) / IDENT_UNIT;
+  int64_t grid = (n_units + TEAMS - 1) / TEAMS;
+  const int64_t cap = (int64_t)dev.cus * (occ < 2 ? (occ < 1 ? 1 : occ) : 2);
+  if (grid > cap) grid = cap;
+  if (grid < 1) grid = 1;
+  BatchArgs ka = a;
+  ka.unit_q = (int32_t)(n_units / grid);
+  ka.unit_r = (int32_t)(n_units % grid);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(DYN_THREADS), 0, s, ka, slice_chunks);
+  return hipGetLastError();
+}
+
+// Waves per unit for the node-split kernel: enough (unit, slice) pairs to put ~4096 waves to
+// work, slices of at least 64 chunks (4096 nodes) so the per-unit reduction stays small next to
+// the scan. 1 = the work-queue kernel (one wave per unit). MSH_SPLIT overrides (A/B).
+int choose_split(int64_t n_pods, int32_t n_chunks, const DeviceInfo& dev) {
+  if (const char* env = getenv("MSH_SPLIT")) return atoi(env);
+  const int64_t n_units = (n_pods + IDENT_UNIT - 1) / IDENT_UNIT;
+  const int64_t want = (int64_t)dev.cus * 16;
+  int split = 1;
+  while (split < 16 && n_units * split < want && n_chunks / (2 * split) >= 64) split *= 2;
+  return split;
+}
+
 template <bool SHARD>
 hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
                               std::string* err) {
+  const int split = choose_split(a.n_pods, a.n_chunks, dev);
+  if (split > 1) {
+    const int sp = split >= 16 ? 16 : split >= 8 ? 8 : split >= 4 ? 4 : 2;
+    const int32_t sc = ((a.n_chunks + sp - 1) / sp + 15) / 16 * 16;  // multiple of 2R chunks
+    if (sp == 2) return launch_ident_split_t<SHARD, 2>(a, dev, s, sc);
+    if (sp == 4) return launch_ident_split_t<SHARD, 4>(a, dev, s, sc);
+    if (sp == 8) return launch_ident_split_t<SHARD, 8>(a, dev, s, sc);
+    return launch_ident_split_t<SHARD, 16>(a, dev, s, sc);
+  }
   // MSH_DYN_THREADS (tuning / A-B only): workgroup size of the work-queue kernel
   const char* env = getenv("MSH_DYN_THREADS");
   const int nt = env ? atoi(env) : DYN_THREADS;

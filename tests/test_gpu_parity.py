@@ -394,3 +394,34 @@ def test_maximum_node_table(msh, gpu_ctx, synth):
         gpu_ctx.upload_nodes(np.zeros(n + 1, np.uint8), np.zeros(n + 1, np.int8))
     gpu_ctx.upload_nodes(u[:10], nd[:10])  # the ctx stays usable after the rejected upload
     _assert_same(gpu_ctx.schedule_batch(pd, pt), closed_form(u[:10], nd[:10], pd, pt), "after reject")
+
+
+@pytest.mark.parametrize("split", ["1", "2", "4", "8", "16"])
+@pytest.mark.parametrize("n", [20_000, 70_000])
+def test_node_split_teams(msh, gpu_ctx, oracle, n, split, monkeypatch):
+    """Few pods against a large table: SPLIT waves share each 8-pod unit, each scanning a slice
+    (cut at the 64,512-node compute-tile boundary at 70k nodes), firsts merged in LDS. Every
+    team size against the oracle, for the batch and the shard-key entry points."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_SPLIT", split)
+    rng = np.random.default_rng(n + int(split))
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = _rand_case(rng, n, 1500, p_unsched=0.2, p_tol=0.3)
+    nd[: n // 2][nd[: n // 2] == 3] = 4  # digit 3 only in the second half: late first matches
+    gpu_ctx.upload_nodes(u, nd)
+    want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, f"split={split} n={n}")
+    dev = torch.device("cuda:0")
+    d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+    p = len(pd)
+    keys = torch.empty(gpu_ctx.shard_keys_len(p), dtype=torch.int32, device=dev)
+    gpu_ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+    oi = torch.empty(p, dtype=torch.int32, device=dev)
+    osc = torch.empty(p, dtype=torch.int64, device=dev)
+    ost = torch.empty(p, dtype=torch.int32, device=dev)
+    gpu_ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), keys.data_ptr(), oi.data_ptr(),
+                               osc.data_ptr(), ost.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"keys split={split} n={n}")
