@@ -1347,17 +1347,18 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
       } else {
         const int32_t c = sel >> 6;
         if ((c % NW) == wv) {
-          // the owning lane, branch-free: the register by a wave-uniform index, the lane by a
-          // compare (an unrolled `if (r == rs && mine)` became RS exec-mask branches)
-          const int rs = c / NW;
+          // the owning lane: the register by a wave-uniform index (scalar branches), the lane
+          // by a compare (an unrolled `if (r == rs && mine)` became RS exec-mask branches)
+          const int rs = __builtin_amdgcn_readfirstlane(c / NW);
           const bool mine = lane == (sel & (WAVE - 1));
 #pragma unroll
           for (int r = 0; r < RS; ++r) {
-            const bool hit = mine && r == rs;
-            CNT[r] += hit ? 1 : 0;
-            const bool full = hit && CNT[r] >= max_pods;
-            C0[r] = full ? NOFIT : C0[r];
-            C1[r] = full ? NOFIT : C1[r];
+            if (r == rs) {  // wave-uniform: a scalar branch to the one register, 4 VALU there
+              CNT[r] += mine ? 1 : 0;
+              const bool full = mine && CNT[r] >= max_pods;
+              C0[r] = full ? NOFIT : C0[r];
+              C1[r] = full ? NOFIT : C1[r];
+            }
           }
         }
       }

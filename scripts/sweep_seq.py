@@ -24,18 +24,21 @@ osc = torch.empty(p, dtype=torch.int64, device=dev)
 ost = torch.empty(p, dtype=torch.int32, device=dev)
 s = torch.cuda.current_stream()
 res = {}
+caps = [int(c) for c in os.environ.get("CAPS", "0").split(",")]  # max_pods_per_node (0 = reference)
 for rnd in range(4):
-    for w in ("4", "8", "16"):
-        os.environ["MSH_SEQ_WAVES"] = w
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        ctx.schedule_sequential_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, oi.data_ptr(), osc.data_ptr(),
-                                       ost.data_ptr(), s.cuda_stream)
-        e1.record(s)
-        torch.cuda.synchronize()
-        if rnd:
-            res.setdefault(w, []).append(e0.elapsed_time(e1))
-for w, t in res.items():
+    for cap in caps:
+        for w in ("4", "8", "16"):
+            os.environ["MSH_SEQ_WAVES"] = w
+            ctx.reset_node_pod_counts()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            ctx.schedule_sequential_device(p, d_pd.data_ptr(), d_pt.data_ptr(), cap, oi.data_ptr(), osc.data_ptr(),
+                                           ost.data_ptr(), s.cuda_stream)
+            e1.record(s)
+            torch.cuda.synchronize()
+            if rnd:
+                res.setdefault((cap, w), []).append(e0.elapsed_time(e1))
+for (cap, w), t in res.items():
     ms = float(np.median(t))
-    print(json.dumps({"seq_waves": w, "nodes": n, "pods": p, "ms": ms, "us_per_pod": ms * 1e3 / p,
-                      "evals_per_s": n * p / (ms * 1e-3)}))
+    print(json.dumps({"seq_waves": w, "max_pods_per_node": cap, "nodes": n, "pods": p, "ms": ms,
+                      "us_per_pod": ms * 1e3 / p, "evals_per_s": n * p / (ms * 1e-3)}))
