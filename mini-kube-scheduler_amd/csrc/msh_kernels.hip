@@ -1157,14 +1157,19 @@ __device__ __forceinline__ void lds_barrier() {
 // keeps the output and adds the commit to a per-node count table held in LDS; the other waves
 // go straight on to the next pod's scan (the barrier per pod still orders every commit before
 // the next pod is decided).
+// NW = scanning waves (chunk c is owned by wave c % NW). Without a capacity one more wave, the
+// FINALIZER (wave NW), does no scanning: after each pod's barrier it reads the pod's result,
+// decodes it, keeps the output and commits, while the scanners already scan the next pod.
 template <int RS, int NW, bool NEED_KX, bool CAP>
-__global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
+__global__ __launch_bounds__((NW + (CAP ? 0 : 1)) * 64) void seq_kernel(SeqArgs a) {
+  constexpr int FINW = CAP ? 0 : NW;  // the wave that decodes, keeps the output and commits
   // per-pod exchange slots, triple-buffered: [slot][first-match cost, first-feasible cost,
   // non-match key]
   __shared__ uint32_t xs[3][3];
   extern __shared__ int32_t lcnt[];  // !CAP: [n_chunks * 64] per-node pod counts
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool scanner = CAP || wv < NW;
 
   uint32_t D[RS], C0[RS], C1[RS];
   int32_t CNT[RS];
@@ -1175,7 +1180,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     C0[r] = NOFIT;
     C1[r] = NOFIT;
     CNT[r] = 0;
-    if (c < a.n_chunks) {
+    if (scanner && c < a.n_chunks) {
       const int32_t i = c * WAVE + lane;
       D[r] = (uint32_t)a.dig[i] << 24;
       C0[r] = a.c0[i];
@@ -1189,8 +1194,8 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
       }
     }
   }
-  if (!CAP) {  // ordered before wave 0's first commit by the first pod's barrier
-    for (int32_t i = threadIdx.x; i < a.n_chunks * WAVE; i += NW * WAVE) lcnt[i] = a.counts[i];
+  if (!CAP) {  // ordered before the finalizer's first commit by the first pod's barrier
+    for (int32_t i = threadIdx.x; i < a.n_chunks * WAVE; i += blockDim.x) lcnt[i] = a.counts[i];
   }
   if (threadIdx.x < 9) xs[threadIdx.x / 3][threadIdx.x % 3] = (threadIdx.x % 3 == 2) ? 0u : 0xFFFFFFFFu;
   __syncthreads();  // the slots' identities before any wave's first fold
@@ -1224,9 +1229,9 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
   uint32_t pdv = POD_DIGIT_NONE, tolv = 0;
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
-  int32_t o_idx = -1, o_st = 0;  // wave 0: lane jl holds pod j0 + jl of the current block
+  int32_t o_idx = -1, o_st = 0;  // wave FINW: lane jl holds pod j0 + jl of the current block
   int64_t o_sc = 0;
-  auto store_block = [&](int32_t j0, int32_t cnt) {  // wave 0: one coalesced store per array
+  auto store_block = [&](int32_t j0, int32_t cnt) {  // wave FINW: one coalesced store per array
     if (lane < cnt) {
       a.out_idx[j0 + lane] = o_idx;
       a.out_score[j0 + lane] = o_sc;
@@ -1254,7 +1259,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
       // order matters for vmcnt (in-order): the conversion waits only for the loads issued one
       // block ago, then the previous block's results leave, then the next block is requested
       convert(j, dn, tn, pdv, tolv);
-      if (wv == 0 && j > 0) store_block(j - WAVE, WAVE);
+      if (wv == FINW && j > 0) store_block(j - WAVE, WAVE);
       load_raw(j + WAVE, dn, tn);  // one block ahead (clamped: no branch around it)
     }
     const uint32_t pd = (uint32_t)__builtin_amdgcn_readlane((int)pdv, jl);
@@ -1262,7 +1267,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     const uint32_t pds = pd << 24;
     // two independent min chains per cost (even / odd registers): half the dependent depth
     uint32_t bm = 0xFFFFFFFFu, ba = 0xFFFFFFFFu, bx = 0u;
-    {
+    if (scanner) {
       uint32_t bm1 = 0xFFFFFFFFu, ba1 = 0xFFFFFFFFu;
       if (tol) {
 #pragma unroll
@@ -1290,7 +1295,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
       bm = umin(bm, bm1);
       ba = umin(ba, ba1);
     }
-    if (NEED_KX) {
+    if (NEED_KX && scanner) {
 #pragma unroll
       for (int r = 0; r < RS; ++r) {
         const uint32_t cst = tol ? C1[r] : C0[r];
@@ -1302,10 +1307,14 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     // Cross-wave exchange: lane 0 of every wave folds its wave's result into this pod's slot with
     // LDS atomics (min of the two costs, max of the non-match key), so after the barrier the pod's
     // result is ONE broadcast read: no second reduction on the critical path.
-    const uint32_t wm = wave_min_u32(bm), wa = wave_min_u32(ba);
-    const uint32_t wx = NEED_KX ? wave_max_u32(bx) : 0u;
+    uint32_t wm = 0xFFFFFFFFu, wa = 0xFFFFFFFFu, wx = 0u;
+    if (scanner) {
+      wm = wave_min_u32(bm);
+      wa = wave_min_u32(ba);
+      wx = NEED_KX ? wave_max_u32(bx) : 0u;
+    }
     SEQ_PH(1);
-    if (lane == 0) {
+    if (scanner && lane == 0) {
       atomicMin(&xs[sl][0], wm);
       atomicMin(&xs[sl][1], wa);
       if (NEED_KX) atomicMax(&xs[sl][2], wx);
@@ -1314,12 +1323,12 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     SEQ_PH(2);
     const int sl_now = sl;
     sl = sl == 2 ? 0 : sl + 1;
-    if (!CAP && wv != 0) continue;  // only wave 0 finishes a pod when commits change nothing
+    if (!CAP && wv != FINW) continue;  // without a capacity only the finalizer finishes a pod
     const uint32_t gm = xs[sl_now][0], ga = xs[sl_now][1];
     const uint32_t gx = NEED_KX ? xs[sl_now][2] : 0u;
     // the slot read one pod ago is free now (every reader passed this pod's barrier) and is next
-    // folded into two pods ahead (after the next barrier): wave 0 resets it in between
-    if (wv == 0 && lane == 0) {
+    // folded into two pods ahead (after the next barrier): wave FINW resets it in between
+    if (wv == FINW && lane == 0) {
       const int sr = sl_now == 0 ? 2 : sl_now - 1;
       xs[sr][0] = 0xFFFFFFFFu;
       xs[sr][1] = 0xFFFFFFFFu;
@@ -1335,7 +1344,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
       decode_pod(im, ix, ia, pd != POD_DIGIT_NONE, pp, &sel, &sc, &st);
     else
       decode_ident(im, ia, pd != POD_DIGIT_NONE, idec, &sel, &sc, &st);
-    if (wv == 0) {
+    if (wv == FINW) {
       const bool mine = lane == jl;
       o_idx = mine ? sel : o_idx;
       o_sc = mine ? sc : o_sc;
@@ -1343,7 +1352,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     }
     if (st == 0) {  // commit (NodeInfo.AddPod analogue)
       if (!CAP) {
-        if (lane == 0) atomicAdd(&lcnt[sel], 1);  // wave 0; no return value waited for
+        if (lane == 0) atomicAdd(&lcnt[sel], 1);  // the finalizer; no return value waited for
       } else {
         const int32_t c = sel >> 6;
         if ((c % NW) == wv) {
@@ -1365,7 +1374,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     }
   }
 
-  if (wv == 0 && a.n_pods > 0) {
+  if (wv == FINW && a.n_pods > 0) {
     const int32_t j0 = (a.n_pods - 1) & ~(WAVE - 1);
     store_block(j0, a.n_pods - j0);
   }
@@ -1384,7 +1393,7 @@ __global__ __launch_bounds__(NW * 64) void seq_kernel(SeqArgs a) {
     }
   } else {
     __syncthreads();
-    for (int32_t i = threadIdx.x; i < a.n_chunks * WAVE; i += NW * WAVE) a.counts[i] = lcnt[i];
+    for (int32_t i = threadIdx.x; i < a.n_chunks * WAVE; i += blockDim.x) a.counts[i] = lcnt[i];
   }
 }
 
@@ -1740,42 +1749,41 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
 }
 
 namespace {
-template <int RS, int NW>
+template <int RS, int NW, bool CAP>
 hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
-  const dim3 blk(NW * 64);
-  const size_t lds = (size_t)a.n_chunks * WAVE * sizeof(int32_t);  // !CAP count table
-  if (a.max_pods > 0) {
-    if (needs_kx(a.pp)) hipLaunchKernelGGL((seq_kernel<RS, NW, true, true>), dim3(1), blk, 0, s, a);
-    else hipLaunchKernelGGL((seq_kernel<RS, NW, false, true>), dim3(1), blk, 0, s, a);
-  } else {
-    if (needs_kx(a.pp)) hipLaunchKernelGGL((seq_kernel<RS, NW, true, false>), dim3(1), blk, lds, s, a);
-    else hipLaunchKernelGGL((seq_kernel<RS, NW, false, false>), dim3(1), blk, lds, s, a);
-  }
+  const dim3 blk((NW + (CAP ? 0 : 1)) * 64);  // + the finalizer wave without a capacity
+  const size_t lds = CAP ? 0 : (size_t)a.n_chunks * WAVE * sizeof(int32_t);  // !CAP count table
+  if (needs_kx(a.pp)) hipLaunchKernelGGL((seq_kernel<RS, NW, true, CAP>), dim3(1), blk, lds, s, a);
+  else hipLaunchKernelGGL((seq_kernel<RS, NW, false, CAP>), dim3(1), blk, lds, s, a);
   return hipGetLastError();
 }
 
 // Register-resident node state: RS chunks per lane. Spill-free on gfx950 up to RS = 24 at
-// 4 waves, 16 at 8 waves, 12 at 16 waves (checked with -Rpass-analysis=kernel-resource-usage).
-template <int NW, int RS_MAX>
+// 4 waves, 16 at 8 waves, 12 at 16 waves, 16 at 15 scanners + the finalizer (checked with
+// -Rpass-analysis=kernel-resource-usage).
+template <int NW, int RS_MAX, bool CAP>
 hipError_t launch_seq_nw(const SeqArgs& a, hipStream_t s) {
   const int rs = (a.n_chunks + NW - 1) / NW;
-  if (rs <= 1) return launch_seq_rs<1, NW>(a, s);
-  if (rs <= 2) return launch_seq_rs<2, NW>(a, s);
-  if (rs <= 3) return launch_seq_rs<3, NW>(a, s);
-  if (rs <= 4) return launch_seq_rs<4, NW>(a, s);
-  if (rs <= 6) return launch_seq_rs<6, NW>(a, s);
-  if (rs <= 8) return launch_seq_rs<8, NW>(a, s);
-  if (rs <= 12 || RS_MAX <= 12) return launch_seq_rs<12, NW>(a, s);
-  if (rs <= 16 || RS_MAX <= 16) return launch_seq_rs<(RS_MAX < 16 ? RS_MAX : 16), NW>(a, s);
-  return launch_seq_rs<(RS_MAX < 24 ? RS_MAX : 24), NW>(a, s);
+  if (rs <= 1) return launch_seq_rs<1, NW, CAP>(a, s);
+  if (rs <= 2) return launch_seq_rs<2, NW, CAP>(a, s);
+  if (rs <= 3) return launch_seq_rs<3, NW, CAP>(a, s);
+  if (rs <= 4) return launch_seq_rs<4, NW, CAP>(a, s);
+  if (rs <= 6) return launch_seq_rs<6, NW, CAP>(a, s);
+  if (rs <= 8) return launch_seq_rs<8, NW, CAP>(a, s);
+  if (rs <= 12 || RS_MAX <= 12) return launch_seq_rs<12, NW, CAP>(a, s);
+  if (rs <= 16 || RS_MAX <= 16) return launch_seq_rs<(RS_MAX < 16 ? RS_MAX : 16), NW, CAP>(a, s);
+  return launch_seq_rs<(RS_MAX < 24 ? RS_MAX : 24), NW, CAP>(a, s);
 }
 }  // namespace
 
 hipError_t launch_sequential(const SeqArgs& a, hipStream_t s, std::string* err) {
   if (a.n_pods == 0) return hipSuccess;
-  // Workgroup size: MSH_SEQ_WAVES (4, 8 or 16) for tuning; default 8 (smallest that fits).
+  // Scanning waves: MSH_SEQ_WAVES (4, 8 or 16) for tuning; default 8 with a capacity, 4 without
+  // (scripts/sweep_seq.py at 5k nodes: 4 scanners + the finalizer 0.35 us per pod, 8 + 1 0.38),
+  // raised until the table fits the registers. Without a capacity a finalizer wave comes on
+  // top (16 -> 15 scanners + 1: the 1024-thread workgroup limit).
   const char* env = getenv("MSH_SEQ_WAVES");
-  int nw = env ? atoi(env) : 8;
+  int nw = env ? atoi(env) : (a.max_pods > 0 ? 8 : 4);
   if (nw == 4 && a.n_chunks > 4 * 24) nw = 8;
   if (nw == 8 && a.n_chunks > 8 * 16) nw = 16;
   if (nw != 4 && nw != 8) nw = 16;
@@ -1783,9 +1791,14 @@ hipError_t launch_sequential(const SeqArgs& a, hipStream_t s, std::string* err) 
     if (err) *err = "sequential mode supports at most 12288 nodes per device";
     return hipErrorInvalidValue;
   }
-  if (nw == 4) return launch_seq_nw<4, 24>(a, s);
-  if (nw == 8) return launch_seq_nw<8, 16>(a, s);
-  return launch_seq_nw<16, 12>(a, s);
+  if (a.max_pods > 0) {
+    if (nw == 4) return launch_seq_nw<4, 24, true>(a, s);
+    if (nw == 8) return launch_seq_nw<8, 16, true>(a, s);
+    return launch_seq_nw<16, 12, true>(a, s);
+  }
+  if (nw == 4) return launch_seq_nw<4, 24, false>(a, s);
+  if (nw == 8) return launch_seq_nw<8, 16, false>(a, s);
+  return launch_seq_nw<15, 16, false>(a, s);
 }
 
 }  // namespace msh
