@@ -72,6 +72,23 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return LIB
 
 
+DEMO = PKG_DIR / "abi_demo"
+DEMO_SRC = REPO / "examples" / "abi_demo.c"
+
+
+def build_demo(verbose: bool = False) -> Path:
+    """examples/abi_demo.c: a plain-C consumer of the ABI (what a cgo binding calls), linked
+    against the in-tree library; binary next to it so it travels with the snapshot."""
+    lib = build(verbose=verbose)
+    if _stale(DEMO, [DEMO_SRC, INCLUDE / "minisched_hip.h", lib]):
+        cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", f"-I{INCLUDE}", str(DEMO_SRC), f"-L{PKG_DIR}",
+               "-lminisched_hip", "-Wl,-rpath,$ORIGIN", "-o", str(DEMO)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return DEMO
+
+
 def build_diagnostic(verbose: bool = False) -> Path:
     """Diagnostic variant with per-wave phase stamps (-DMSH_STAMPS): libminisched_hip_stamps.so.
     Used only by scripts/stamps.py; never loaded by the product path."""
@@ -120,4 +137,5 @@ def build_oracle(verbose: bool = False) -> Path:
 
 if __name__ == "__main__":
     print(build(verbose=True))
+    print(build_demo(verbose=True))
     print(build_oracle(verbose=True))
