@@ -61,6 +61,7 @@ struct msh_ctx {
   bool partial_ev_live = false;
   size_t patch_cap = 0;
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
+  int32_t patch_pending = 0;              // entries in d_patch the next prepare() applies
   std::vector<unsigned long long> h_patch;
 };
 
@@ -136,7 +137,8 @@ int prepare(msh_ctx* c, hipStream_t s) {
   if (!c->dirty) return MSH_OK;
   hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad,
                                        c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_w0, c->d_ulist, c->d_ucount, c->d_mask,
-                                       c->d_ball, s);
+                                       c->d_ball, s, c->d_patch, c->patch_pending);
+  c->patch_pending = 0;
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
   // The prepared tables are read by launches on any stream: finish them before returning (this
   // runs only after an upload, a patch or a plugin change, never per batch).
@@ -382,13 +384,10 @@ int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t
   }
   MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_patch.data(), (size_t)count * sizeof(unsigned long long),
                             hipMemcpyHostToDevice, c->stream));
-  hipError_t e = msh::launch_patch_nodes(c->d_patch, count, c->d_unsched, c->d_digit, c->stream);
-  if (e != hipSuccess) return hip_fail(c, e, "patch_nodes_kernel");
+  // the entries are applied by the prep's reset launch, then the derived tables are rebuilt
+  c->patch_pending = count;
   c->dirty = true;
-  int rc = prepare(c, c->stream);
-  if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipStreamSynchronize(c->stream));
-  return MSH_OK;
+  return prepare(c, c->stream);  // synchronous
 }
 
 int msh_export_results(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,

@@ -77,7 +77,8 @@ constexpr uint32_t CODE_NONE_POD = 14u;
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
                             int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
                             uint32_t* d_w0, uint32_t* d_ulist, uint32_t* d_ucount,
-                            unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s);
+                            unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s,
+                            const unsigned long long* d_patch = nullptr, int32_t patch_count = 0);
 
 constexpr int64_t EXPORT_NONE = INT64_MIN;  // msh_export_results: no score recorded
 hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
@@ -86,8 +87,7 @@ hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_
                          hipStream_t s);
 
 // entries[k] = idx | unsched << 32 | (uint8)digit << 40
-hipError_t launch_patch_nodes(const unsigned long long* d_entries, int32_t count, uint8_t* d_unsched,
-                              int8_t* d_digit, hipStream_t s);
+
 
 struct BatchArgs {
   const uint32_t* c0;        // [n_pad] class-0 node cost: idx if feasible for !tolerating pods, else NOFIT

@@ -102,18 +102,23 @@ __device__ __forceinline__ uint32_t cost_to_key(uint32_t c) { return c < MATCH_L
 //   mask[c][chunk] = __ballot(feasible for class c)   (64-node feasibility bitmask)
 //   ball[c] = key (KMAX - idx) of the first feasible node of class c (0 = none)
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restrict__ unsched,
-                                                        const int8_t* __restrict__ digit,
-                                                        int32_t n, int32_t n_pad, int32_t has_nu,
-                                                        uint32_t* __restrict__ c0,
-                                                        uint8_t* __restrict__ dig,
-                                                        uint32_t* __restrict__ w0,
-                                                        uint32_t* __restrict__ ulist,
-                                                        uint32_t* __restrict__ ucount,
-                                                        unsigned long long* __restrict__ mask,
-                                                        uint32_t* __restrict__ ball) {
+constexpr int PREP_THREADS = 1024;  // n_pad is a multiple of 1024: every block is whole
+__global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* __restrict__ unsched,
+                                                                 const int8_t* __restrict__ digit,
+                                                                 int32_t n, int32_t n_pad, int32_t has_nu,
+                                                                 uint32_t* __restrict__ c0,
+                                                                 uint8_t* __restrict__ dig,
+                                                                 uint32_t* __restrict__ w0,
+                                                                 uint32_t* __restrict__ ulist,
+                                                                 uint32_t* __restrict__ ucount,
+                                                                 unsigned long long* __restrict__ mask,
+                                                                 uint32_t* __restrict__ ball) {
+  constexpr int NWV = PREP_THREADS / WAVE;
+  __shared__ uint32_t s_cnt[NWV], s_k0[NWV], s_k1[NWV];
+  __shared__ uint32_t s_base;
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_pad) return;  // n_pad is a multiple of 64: whole waves exit together
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
   const bool valid = i < n;
   const bool u = valid && unsched[i] != 0;
   const int d = valid ? (int)digit[i] : -1;
@@ -128,26 +133,38 @@ __global__ __launch_bounds__(256) void node_prep_kernel(const uint8_t* __restric
   w0[word_pos(i)] = wd0 | (wd0 << 16);
   const unsigned long long m0 = __ballot(feas0);
   const unsigned long long m1 = __ballot(feas1);
-  const int lane = threadIdx.x & 63;
   // nodes whose feasibility differs between the classes -> ulist (order irrelevant: min search)
   const bool diff = feas1 && !feas0;
   const unsigned long long md = __ballot(diff);
-  if (md) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(ucount, (uint32_t)__builtin_popcountll(md));
-    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-    if (diff) {
-      const uint32_t rank = (uint32_t)__builtin_popcountll(md & ((1ull << lane) - 1ull));
-      ulist[base + rank] = ((has_digit ? (uint32_t)d : CODE_NONE_NODE) << 24) | (uint32_t)i;
-    }
-  }
   if (lane == 0) {
     const int32_t chunk = i >> 6;
     const int32_t n_chunks = n_pad >> 6;
     mask[chunk] = m0;
     mask[n_chunks + chunk] = m1;
-    if (m0) atomicMax(&ball[0], KMAX - (uint32_t)(i + __builtin_ctzll(m0)));
-    if (m1) atomicMax(&ball[1], KMAX - (uint32_t)(i + __builtin_ctzll(m1)));
+    s_cnt[wv] = (uint32_t)__builtin_popcountll(md);
+    s_k0[wv] = m0 ? KMAX - (uint32_t)(i + __builtin_ctzll(m0)) : 0u;
+    s_k1[wv] = m1 ? KMAX - (uint32_t)(i + __builtin_ctzll(m1)) : 0u;
+  }
+  __syncthreads();
+  // one ulist reservation and one first-feasible update per class per BLOCK: device-scope
+  // atomics on one address serialise (~86 M/s), so per-wave atomics made the 100k-node prep ~60 us
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0, k0 = 0, k1 = 0;
+    for (int w = 0; w < NWV; ++w) {
+      tot += s_cnt[w];
+      k0 = umax(k0, s_k0[w]);
+      k1 = umax(k1, s_k1[w]);
+    }
+    s_base = tot ? atomicAdd(ucount, tot) : 0u;
+    if (k0) atomicMax(&ball[0], k0);
+    if (k1) atomicMax(&ball[1], k1);
+  }
+  __syncthreads();
+  if (diff) {
+    uint32_t base = s_base;
+    for (int w = 0; w < wv; ++w) base += s_cnt[w];
+    const uint32_t rank = (uint32_t)__builtin_popcountll(md & ((1ull << lane) - 1ull));
+    ulist[base + rank] = ((has_digit ? (uint32_t)d : CODE_NONE_NODE) << 24) | (uint32_t)i;
   }
 }
 
@@ -1400,22 +1417,42 @@ __global__ __launch_bounds__((NW + (CAP ? 0 : 1)) * 64) void seq_kernel(SeqArgs 
 // ---------------------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------------------
+// Before every prep: reset the per-launch scalars (first feasible per class, ulist count), fill
+// ulist with the never-matching entry (CODE_NONE_NODE << 24: the batch kernels read whole
+// ULIST_STEP-entry blocks with no bounds check; count <= n <= n_pad, and n_pad is a multiple of
+// ULIST_STEP), and apply pending msh_patch_nodes entries (idx | unsched << 32 | digit << 40).
+// One launch instead of three memsets and a scatter kernel.
+__global__ __launch_bounds__(256) void prep_reset_kernel(uint32_t* __restrict__ ball, uint32_t* __restrict__ ucount,
+                                                         uint32_t* __restrict__ ulist, int32_t n_pad,
+                                                         const unsigned long long* __restrict__ entries,
+                                                         int32_t count, uint8_t* __restrict__ unsched,
+                                                         int8_t* __restrict__ digit) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_pad) ulist[i] = CODE_NONE_NODE << 24;
+  if (i < 2) ball[i] = 0;
+  if (i == 0) *ucount = 0;
+  if (i < count) {
+    const unsigned long long e = entries[i];
+    const uint32_t k = (uint32_t)e;
+    unsched[k] = (uint8_t)(e >> 32);
+    digit[k] = (int8_t)(uint8_t)(e >> 40);
+  }
+}
+
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
                             int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
                             uint32_t* d_w0, uint32_t* d_ulist, uint32_t* d_ucount,
-                            unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(d_ball, 0, 2 * sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(d_ucount, 0, sizeof(uint32_t), s);
+                            unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s,
+                            const unsigned long long* d_patch, int32_t patch_count) {
+  const int32_t span = n_pad > patch_count ? n_pad : patch_count;
+  hipLaunchKernelGGL(prep_reset_kernel, dim3((span > 0 ? span + 255 : 256) / 256), dim3(256), 0, s, d_ball,
+                     d_ucount, d_ulist, n_pad, d_patch, patch_count, const_cast<uint8_t*>(d_unsched),
+                     const_cast<int8_t*>(d_digit));
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (n_pad == 0) return hipSuccess;
-  // every ulist slot past the count holds the never-matching entry (CODE_NONE_NODE << 24): the
-  // batch kernels read whole ULIST_STEP-entry blocks with no bounds check (count <= n <= n_pad,
-  // and n_pad is a multiple of ULIST_STEP)
-  e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_ulist), (int)(CODE_NONE_NODE << 24), (size_t)n_pad, s);
-  if (e != hipSuccess) return e;
-  const int blocks = (n_pad + 255) / 256;
-  hipLaunchKernelGGL(node_prep_kernel, dim3(blocks), dim3(256), 0, s, d_unsched, d_digit, n, n_pad,
+  const int blocks = (n_pad + PREP_THREADS - 1) / PREP_THREADS;
+  hipLaunchKernelGGL(node_prep_kernel, dim3(blocks), dim3(PREP_THREADS), 0, s, d_unsched, d_digit, n, n_pad,
                      has_nu, d_c0, d_dig, d_w0, d_ulist, d_ucount, d_mask, d_ball);
   return hipGetLastError();
 }
@@ -1484,25 +1521,6 @@ hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_
   if (p <= 0 || n <= 0) return hipSuccess;
   hipLaunchKernelGGL(export_kernel, dim3(p), dim3(256), 0, s, d_unsched, d_digit, n, d_pod_digit,
                      d_pod_tol, pp, d_filter, d_raw, d_fin);
-  return hipGetLastError();
-}
-
-__global__ __launch_bounds__(256) void patch_nodes_kernel(const unsigned long long* __restrict__ entries,
-                                                          int32_t count, uint8_t* __restrict__ unsched,
-                                                          int8_t* __restrict__ digit) {
-  const int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= count) return;
-  const unsigned long long e = entries[k];
-  const uint32_t i = (uint32_t)e;
-  unsched[i] = (uint8_t)(e >> 32);
-  digit[i] = (int8_t)(uint8_t)(e >> 40);
-}
-
-hipError_t launch_patch_nodes(const unsigned long long* d_entries, int32_t count, uint8_t* d_unsched,
-                              int8_t* d_digit, hipStream_t s) {
-  if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(patch_nodes_kernel, dim3((count + 255) / 256), dim3(256), 0, s, d_entries, count,
-                     d_unsched, d_digit);
   return hipGetLastError();
 }
 
