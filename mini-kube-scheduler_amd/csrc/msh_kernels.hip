@@ -20,8 +20,9 @@
 // its suffix digit equals the pod's, else 0, so selectHost's first max is "first feasible
 // match, else first feasible". The IDENT path keeps one node per 16-bit half of a word,
 // duplicated in both halves: (code << 10) | (chunk mod 1008), code = the node's digit if it
-// is feasible for non-tolerating pods, else 15. A pod pair sits in one SGPR as
-// (codeB << 26) | (codeA << 10); per word and pair
+// is feasible for non-tolerating pods, else 15. A pod pair sits in one VGPR (the all-VGPR
+// v_xor_b32 issues at twice the rate of the SGPR form) as (codeB << 26) | (codeA << 10); per
+// word and pair
 //     x = W ^ PP      (v_xor_b32)  -> a half is < 1024 iff that node matches that pod
 // and two such words fold into the running first match of both pods with ONE
 //     bm = v_pk_minimum3_f16(bm, x_r, x_r+1)
@@ -29,6 +30,18 @@
 // lane-ops per (pod, node) evaluation. Nodes feasible only for tolerating pods are corrected
 // afterwards from a short list (ulist). The KX path (batch_kernel) serves the REVERSE /
 // MINMAX normalizers, which also need the first feasible non-match.
+//
+// Kernels, by entry point:
+//   node_prep_kernel (+ prep_reset_kernel)  every upload / patch / plugin change
+//   ident_dyn_kernel     batch, IDENT modes: per-CU work queue of 8-pod units (default);
+//                        MULTI form for tables of several 64,512-node compute tiles
+//   ident_split_kernel   batch, IDENT modes, few pods against a large table: teams of waves
+//                        share a unit over table slices
+//   batch_kernel         batch, REVERSE / MINMAX (compare/select, LDS-staged tiles)
+//   ident_kernel         batch, static pod ranges (A/B only: MSH_BATCH_KERNEL=2 / 0)
+//   decode_keys_kernel   node-sharded mode: decode the merged int32 shard keys
+//   seq_kernel           sequential commit, one pod at a time, one workgroup
+//   export_kernel        per-pair result export (simulator result store)
 // See DESIGN.md for the roofline / instruction budget of each kernel.
 #include "msh_internal.h"
 
