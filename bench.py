@@ -45,6 +45,20 @@ UBENCH_OP = "v_xor_b32 vv x2 + v_pk_minimum3_f16"
 N_SIMD = 256 * 4
 
 
+def batch_kernel_label(n_nodes, n_pods, shard, cus):
+    """The kernel msh_kernels.hip launch_ident_dyn_t dispatches for this batch (default knobs):
+    one pair range per wave (ident_wave_kernel, 256-thread workgroups) when the table is one
+    64,512-node compute tile and every wave of the chip gets at most 8 pod pairs; otherwise the
+    work-queue kernel, in its MULTI form for tables of several tiles."""
+    sh = str(shard).lower()
+    pairs, full = (n_pods + 1) // 2, cus * 32
+    wave_range = os.environ.get("MSH_WAVE_RANGE", "1").strip() not in ("0", "")
+    if wave_range and n_nodes <= 64512 and 0 < pairs <= 8 * full:
+        waves = full if pairs >= 4 * full else (pairs + 3) // 4
+        return f"ident_wave_kernel<8, {sh}, {min(8, -(-pairs // waves))}, 256>"
+    return f"ident_dyn_kernel<8, {sh}, 1024, false, {str(n_nodes > 64512).lower()}>"
+
+
 def measured_int_valu_ceiling() -> float | None:
     """Lane-ops/s of the scan's instruction mix at the best measured occupancy."""
     try:
@@ -267,9 +281,7 @@ def main():
         }
     else:
         shard = mode == "nodeshard"
-        # launcher dispatch (msh_kernels.hip launch_batch): the work-queue kernel, its MULTI form
-        # when the table spans several 64,512-node compute tiles
-        kname = f"ident_dyn_kernel<8, {str(shard).lower()}, 1024, false, {str(n_local > 64512).lower()}>"
+        kname = batch_kernel_label(n_local, p, shard, torch.cuda.get_device_properties(dev).multi_processor_count)
         iso_s = kernel_ms_isolated * 1e-3
         roofline = {
             "bound": "valu",

@@ -587,17 +587,20 @@ __device__ __forceinline__ void scan_words(const uint32_t (&w)[R], const uint32_
   static_assert(R % 2 == 0, "chunks are folded two at a time");
 #pragma unroll
   for (int qb = 0; qb < GQ; qb += QB) {
+    constexpr int QB_ = QB;  // the last block may be partial when GQ is not a multiple of QB
     if (qb < cnt) {
 #pragma unroll
       for (int r = 0; r < R; r += 2) {
-        uint32_t x[QB], y[QB];
+        uint32_t x[QB_], y[QB_];
 #pragma unroll
-        for (int q = 0; q < QB; ++q) {
+        for (int q = 0; q < QB_; ++q) {
+          if (qb + q >= GQ) break;
           x[q] = xor_vv(w[r], pp[qb + q]);
           y[q] = xor_vv(w[r + 1], pp[qb + q]);
         }
 #pragma unroll
-        for (int q = 0; q < QB; ++q) {
+        for (int q = 0; q < QB_; ++q) {
+          if (qb + q >= GQ) break;
           if (MSH_MIN3) {
             bm[qb + q] = pk_min3_f16bits(bm[qb + q], x[q], y[q]);
           } else {
@@ -690,33 +693,50 @@ __device__ __forceinline__ void ident_group(unsigned long long& mask, uint32_t p
 
 // Tolerating pods (set bits of `mt`): a pass over ulist, the nodes feasible for
 // them alone. The list is read in whole ULIST_STEP-entry blocks (sentinel-padded, no bounds
-// check) with ULIST_STEP / 64 independent loads in flight, so a pass pays one L2 round trip
-// per block instead of one per 64 entries. Entry ^ (digit << 24) is < 2^24 exactly on a digit
-// match, and then it is the node index.
+// check), ULIST_WIN blocks at a time into registers: each window is loaded ONCE for all the
+// tolerating pods of the wave (the entries do not depend on the pod), which then take it two at
+// a time with two independent wave reductions in flight. Entry ^ (digit << 24) is < 2^24
+// exactly on a digit match, and then it is the node index; a window's per-pod minimum folds
+// into `res` by min, so windows and the main scan combine in any order.
+constexpr int ULIST_WIN = 2;
 __device__ __forceinline__ uint32_t ulist_pass(unsigned long long mt, uint32_t pcv, uint32_t res,
                                                const uint32_t* __restrict__ ulist, uint32_t ucnt,
                                                int lane) {
   constexpr int NL = ULIST_STEP / WAVE;
+  const uint32_t nblk = (ucnt + ULIST_STEP - 1) / ULIST_STEP;
   // wave-uniform descriptor: block offset in an SGPR, lane offset one loop-invariant VGPR
-  const uint32_t n_rd = (ucnt + ULIST_STEP - 1) / ULIST_STEP * ULIST_STEP;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)ulist, (short)0, (int32_t)(n_rd * sizeof(uint32_t)), 0x00020000);
-  while (mt) {
-    const int32_t l = (int32_t)__builtin_ctzll(mt);
-    mt &= mt - 1;
-    const uint32_t pc24 = (uint32_t)__builtin_amdgcn_readlane((int)pcv, l) << 24;
-    uint32_t bu = 0xFFFFFFFFu;
+      (void*)ulist, (short)0, (int32_t)(nblk * ULIST_STEP * sizeof(uint32_t)), 0x00020000);
 #pragma unroll 1
-    for (uint32_t u0 = 0; u0 < ucnt; u0 += ULIST_STEP) {
-      uint32_t x[NL];
+  for (uint32_t b0 = 0; b0 < nblk; b0 += ULIST_WIN) {
+    uint32_t x[ULIST_WIN * NL];
 #pragma unroll
-      for (int i = 0; i < NL; ++i)
-        x[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4 + i * WAVE * 4, (int)(u0 * 4), 0);
+    for (int b = 0; b < ULIST_WIN; ++b)
 #pragma unroll
-      for (int i = 0; i < NL; i += 2) bu = umin(bu, umin(x[i] ^ pc24, x[i + 1] ^ pc24));
+      for (int i = 0; i < NL; ++i) {
+        const uint32_t v = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+            rs, lane * 4 + i * WAVE * 4, (int)((b0 + b) * ULIST_STEP * 4), 0);
+        x[b * NL + i] = b0 + b < nblk ? v : 0xFFFFFFFFu;  // past the list: never a match
+      }
+    unsigned long long m = mt;
+#pragma unroll 1
+    while (m) {
+      const int32_t l0 = (int32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      const int32_t l1 = m ? (int32_t)__builtin_ctzll(m) : l0;  // an odd last pod goes twice
+      if (m) m &= m - 1;
+      const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)pcv, l0) << 24;
+      const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)pcv, l1) << 24;
+      uint32_t u0 = 0xFFFFFFFFu, u1 = 0xFFFFFFFFu;
+#pragma unroll
+      for (int i = 0; i < ULIST_WIN * NL; i += 2) {
+        u0 = umin(u0, umin(x[i] ^ p0, x[i + 1] ^ p0));
+        u1 = umin(u1, umin(x[i] ^ p1, x[i + 1] ^ p1));
+      }
+      const uint32_t v0 = wave_min_u32(u0), v1 = wave_min_u32(u1);
+      if (v0 < MATCH_LIMIT) res = (lane == l0) ? umin(res, v0) : res;
+      if (v1 < MATCH_LIMIT) res = (lane == l1) ? umin(res, v1) : res;
     }
-    const uint32_t vu = wave_min_u32(bu);
-    if (vu < MATCH_LIMIT) res = (lane == l) ? umin(res, vu) : res;
   }
   return res;
 }
@@ -865,13 +885,13 @@ __device__ __forceinline__ void load_words_lds(uint32_t (&w)[R], const uint4* lw
 }
 
 // `wa` holds chunks [0, R) on entry (requested by the caller together with the pod bytes).
-// NP pod pairs (NP = IDENT_UNIT / 2, 4 or 8): pair q = lanes 2q (low half) and 2q+1 (high).
-template <int R, bool LDSW>
+// NP pod pairs (1..8; IDENT_UNIT / 2 for the work queue): pair q = lanes 2q (low half) and
+// 2q+1 (high half).
+template <int R, bool LDSW, int NP = IDENT_UNIT / 2>
 __device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, uint32_t (&wa)[R], const uint32_t* __restrict__ words,
                                                 __amdgpu_buffer_rsrc_t rs, const uint4* lw, int32_t nc,
                                                 int lane) {
-  constexpr int NP = IDENT_UNIT / 2;
-  static_assert((NP == 4 || NP == 8) && QB == 4, "a unit scans 4 or 8 pod pairs, in blocks of 4");
+  static_assert(NP >= 1 && NP <= 8 && QB == 4, "1..8 pod pairs, scanned in blocks of 4");
   const uint32_t c = pcv << CODE_SHIFT;
   // quad_perm [1,0,3,2]: lane 2q receives lane 2q+1's code
   const uint32_t partner = (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0xB1, 0xF, 0xF, false);
@@ -913,10 +933,10 @@ __device__ __forceinline__ uint32_t ident_unit8(uint32_t pcv, uint32_t (&wa)[R],
   const int q = (lane >> 1) & 3;
   const int row = ((q & 1) << 1) | (q >> 1);
   uint32_t v = 0;
+  auto bmq = [&](int q) -> uint32_t { return q < NP ? pk_fold_lane(bm[q < NP ? q : 0], lane2) : 0xFFFFFFFFu; };
 #pragma unroll
-  for (int g = 0; g < NP / 4; ++g) {
-    const uint32_t x = wave_pkmin_u16_x4(pk_fold_lane(bm[4 * g], lane2), pk_fold_lane(bm[4 * g + 1], lane2),
-                                         pk_fold_lane(bm[4 * g + 2], lane2), pk_fold_lane(bm[4 * g + 3], lane2));
+  for (int g = 0; g < (NP + 3) / 4; ++g) {
+    const uint32_t x = wave_pkmin_u16_x4(bmq(4 * g), bmq(4 * g + 1), bmq(4 * g + 2), bmq(4 * g + 3));
     const uint32_t vg = (uint32_t)__builtin_amdgcn_ds_bpermute(row * 16 * 4, (int)x);
     v = (lane >> 3) == g ? vg : v;
   }
@@ -1049,6 +1069,69 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
     msh_stamp_buf[((size_t)gw * STAMPS_PER_WAVE + 7) * 2 + 1] = xcc;
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------------------
+// One-range-per-wave IDENT kernel: when the batch gives every wave of a full chip at most 8
+// pod PAIRS, each wave takes ONE contiguous range of q or q + 1 pairs and scans the table once
+// for all of them: no work-queue claims, no workgroup barrier, one cross-lane reduction per 4
+// pairs. Pairs, not pods, are dealt out so that no wave pads a half-empty pair slot, and the
+// r = Q mod W waves that take one more pair are spread across workgroups (wave rank =
+// wave-in-workgroup x grid + workgroup), so every CU gets the same work to within a pair per
+// workgroup. NP = the longest range, in pairs; the shorter ranges run the NP - 1 body.
+// ---------------------------------------------------------------------------------------
+template <int R, bool SHARD, int NP, int WT>
+__global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(8))) void ident_wave_kernel(BatchArgs a) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int32_t g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * (int32_t)gridDim.x + (int32_t)blockIdx.x;
+  const int32_t nc = a.n_chunks;  // one compute tile
+  const uint32_t* words = a.w0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)words, (short)0, nc * WAVE * (int32_t)sizeof(uint32_t), 0x00020000);
+  const uint32_t bvec = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ball, (short)0, 8, 0x00020000), (lane & 1) * 4, 0, 0);
+  const uint32_t uvec = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ucount, (short)0, 4, 0x00020000), 0, 0, 0);
+  if (SHARD) write_class_keys(a);
+  // wave rank g: pairs [g * q + min(g, r), +q (+1 if g < r)), q / r host-computed (unit_q / unit_r)
+  const int32_t np = a.unit_q + (g < a.unit_r ? 1 : 0);
+  const int32_t w0 = 2 * (g * a.unit_q + min(g, a.unit_r));
+  // ranks past the W-th start at or past P (2 (g q + r) >= 2 (W q + r) = 2Q >= P)
+  if (w0 >= a.n_pods) return;  // whole waves only; no barrier follows
+  const int32_t nwin = min(2 * np, a.n_pods - w0);
+  const bool act = lane < nwin;
+  uint32_t wa[R];
+  load_words<true>(wa, words, rs, 0, lane);  // requested before the pod bytes are waited for
+  uint32_t pcv = CODE_NONE_POD, tolv = 0;
+  if (act) {
+    const int d = a.pod_digit[w0 + lane];
+    pcv = (d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
+    tolv = a.pod_tol[w0 + lane] ? 1u : 0u;
+  }
+  // the tolerating pods' ulist pass first: its load latency overlaps the first node words'
+  // (already in flight); its per-pod minimum joins the scan's by min
+  uint32_t res = NOFIT;
+  const unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
+  if (mt) res = ulist_pass(mt, pcv, res, a.ulist, (uint32_t)__builtin_amdgcn_readfirstlane((int)uvec), lane);
+  if (__ballot(act && pcv != CODE_NONE_POD)) {
+    uint32_t rs_;
+    if (NP == 1 || np == NP)
+      rs_ = ident_unit8<R, false, NP>(pcv, wa, words, rs, nullptr, nc, lane);
+    else
+      rs_ = ident_unit8<R, false, (NP > 1 ? NP - 1 : 1)>(pcv, wa, words, rs, nullptr, nc, lane);
+    res = umin(res, rs_);
+  }
+  if (act) {
+    const int32_t j = w0 + lane;
+    if (SHARD) {
+      a.keys[j] = res != NOFIT ? shard_key(a.node_base, res) : 0;
+    } else {
+      const uint32_t ball = tolv ? (uint32_t)__builtin_amdgcn_readlane((int)bvec, 1)
+                                 : (uint32_t)__builtin_amdgcn_readlane((int)bvec, 0);
+      decode_ident(res != NOFIT ? (int64_t)res : -1, key_to_idx(ball), pcv != CODE_NONE_POD,
+                   make_ident_decode(a.pp), &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1704,6 +1787,43 @@ int choose_split(int64_t n_pods, int32_t n_chunks, const DeviceInfo& dev) {
   return split;
 }
 
+template <bool SHARD, int NP, int WT>
+hipError_t launch_ident_wave_wt(const BatchArgs& a, int64_t waves, hipStream_t s) {
+  constexpr int WPG = WT / WAVE;
+  const int64_t pairs = ((int64_t)a.n_pods + 1) / 2;
+  BatchArgs ka = a;  // pairs per wave: unit_q, and one more for the first unit_r wave ranks
+  ka.unit_q = (int32_t)(pairs / waves);
+  ka.unit_r = (int32_t)(pairs % waves);
+  const int64_t grid = (waves + WPG - 1) / WPG;
+  hipLaunchKernelGGL((ident_wave_kernel<IDENT_R, SHARD, NP, WT>), dim3((unsigned)grid), dim3(WT), 0, s, ka);
+  return hipGetLastError();
+}
+
+// Workgroup size of the wave-range kernel: small workgroups free their CU slot as soon as
+// their own few waves end, so the next launch (another stream) fills the chip sooner.
+// MSH_WAVE_THREADS (256 / 512 / 1024) is for A/B only.
+template <bool SHARD, int NP>
+hipError_t launch_ident_wave_np(const BatchArgs& a, int64_t waves, hipStream_t s) {
+  const char* env = getenv("MSH_WAVE_THREADS");
+  const int wt = env ? atoi(env) : 256;
+  if (wt == 1024) return launch_ident_wave_wt<SHARD, NP, 1024>(a, waves, s);
+  if (wt == 512) return launch_ident_wave_wt<SHARD, NP, 512>(a, waves, s);
+  return launch_ident_wave_wt<SHARD, NP, 256>(a, waves, s);
+}
+
+// Waves for one contiguous pair range per wave: every wave of a full chip (2 x 1024-thread
+// workgroups per CU), or fewer when the batch is small (4 pairs per wave); 0 = more than 8
+// pairs per wave, the work queue takes over. MSH_WAVE_RANGE=0 disables it (A/B).
+int64_t wave_range_waves(int64_t n_pods, int32_t n_chunks, const DeviceInfo& dev) {
+  if (const char* env = getenv("MSH_WAVE_RANGE"))
+    if (atoi(env) == 0) return 0;
+  if (n_chunks > TILE_CHUNKS || n_pods <= 0) return 0;
+  const int64_t full = (int64_t)dev.cus * 32;
+  const int64_t pairs = (n_pods + 1) / 2;
+  if (pairs > 8 * full) return 0;
+  return pairs >= 4 * full ? full : (pairs + 3) / 4;
+}
+
 template <bool SHARD>
 hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s,
                               std::string* err) {
@@ -1715,6 +1835,18 @@ hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStre
     if (sp == 4) return launch_ident_split_t<SHARD, 4>(a, dev, s, sc);
     if (sp == 8) return launch_ident_split_t<SHARD, 8>(a, dev, s, sc);
     return launch_ident_split_t<SHARD, 16>(a, dev, s, sc);
+  }
+  if (const int64_t waves = wave_range_waves(a.n_pods, a.n_chunks, dev)) {
+    switch ((((int64_t)a.n_pods + 1) / 2 + waves - 1) / waves) {  // the longest range, in pairs
+      case 1: return launch_ident_wave_np<SHARD, 1>(a, waves, s);
+      case 2: return launch_ident_wave_np<SHARD, 2>(a, waves, s);
+      case 3: return launch_ident_wave_np<SHARD, 3>(a, waves, s);
+      case 4: return launch_ident_wave_np<SHARD, 4>(a, waves, s);
+      case 5: return launch_ident_wave_np<SHARD, 5>(a, waves, s);
+      case 6: return launch_ident_wave_np<SHARD, 6>(a, waves, s);
+      case 7: return launch_ident_wave_np<SHARD, 7>(a, waves, s);
+      default: return launch_ident_wave_np<SHARD, 8>(a, waves, s);
+    }
   }
   // MSH_DYN_THREADS (tuning / A-B only): workgroup size of the work-queue kernel
   const char* env = getenv("MSH_DYN_THREADS");

@@ -425,3 +425,20 @@ def test_node_split_teams(msh, gpu_ctx, oracle, n, split, monkeypatch):
                                osc.data_ptr(), ost.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"keys split={split} n={n}")
+
+
+@pytest.mark.parametrize("wave_range", ["1", "0"])
+@pytest.mark.parametrize("p", [1, 2, 3, 7, 8, 9, 15, 16, 17, 1000, 8191, 65_536, 65_537, 100_003, 131_071, 131_072,
+                               131_073, 140_000])
+def test_wave_ranges(msh, gpu_ctx, oracle, p, wave_range, monkeypatch):
+    """One contiguous pair range per wave (1..8 pairs, ragged: r = Q mod W wave ranks take one
+    more, odd P leaves a half pair) on either side of the 4-pairs-per-wave and 8-pairs-per-wave
+    cuts, against the oracle; MSH_WAVE_RANGE=0 runs the same batches through the work queue."""
+    monkeypatch.setenv("MSH_WAVE_RANGE", wave_range)
+    rng = np.random.default_rng(p)
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = _rand_case(rng, 5000, p, p_unsched=0.25, p_tol=0.3)
+    gpu_ctx.upload_nodes(u, nd)
+    want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, f"wave_range={wave_range} p={p}")
