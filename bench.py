@@ -47,15 +47,18 @@ N_SIMD = 256 * 4
 
 def batch_kernel_label(n_nodes, n_pods, shard, cus):
     """The kernel msh_kernels.hip launch_ident_dyn_t dispatches for this batch (default knobs):
-    one pair range per wave (ident_wave_kernel, 256-thread workgroups) when the table is one
-    64,512-node compute tile and every wave of the chip gets at most 8 pod pairs; otherwise the
-    work-queue kernel, in its MULTI form for tables of several tiles."""
+    one pair range per wave (ident_wave_kernel, 256-thread workgroups; rounds of at most 8
+    pairs) when the table is one 64,512-node compute tile and every wave of the chip gets at
+    most 64 rounds; otherwise the work-queue kernel, in its MULTI form for tables of several
+    tiles."""
     sh = str(shard).lower()
     pairs, full = (n_pods + 1) // 2, cus * 32
     wave_range = os.environ.get("MSH_WAVE_RANGE", "1").strip() not in ("0", "")
-    if wave_range and n_nodes <= 64512 and 0 < pairs <= 8 * full:
-        waves = full if pairs >= 4 * full else (pairs + 3) // 4
-        return f"ident_wave_kernel<8, {sh}, {min(8, -(-pairs // waves))}, 256>"
+    if wave_range and n_nodes <= 64512 and 0 < pairs <= 8 * 64 * full:
+        waves = min(full, -(-pairs // (4 if pairs < 4 * full else 7)))
+        longest = -(-pairs // waves)
+        rounds = -(-longest // 8)
+        return f"ident_wave_kernel<8, {sh}, {-(-longest // rounds)}, 256>"
     return f"ident_dyn_kernel<8, {sh}, 1024, false, {str(n_nodes > 64512).lower()}>"
 
 

@@ -1081,7 +1081,8 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
 // workgroup. NP = the longest range, in pairs; the shorter ranges run the NP - 1 body.
 // ---------------------------------------------------------------------------------------
 template <int R, bool SHARD, int NP, int WT>
-__global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(8))) void ident_wave_kernel(BatchArgs a) {
+__global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(8))) void ident_wave_kernel(BatchArgs a,
+                                                                                      int32_t rounds) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int32_t g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * (int32_t)gridDim.x + (int32_t)blockIdx.x;
   const int32_t nc = a.n_chunks;  // one compute tile
@@ -1095,41 +1096,49 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(8))) void id
   if (SHARD) write_class_keys(a);
   // wave rank g: pairs [g * q + min(g, r), +q (+1 if g < r)), q / r host-computed (unit_q / unit_r)
   const int32_t np = a.unit_q + (g < a.unit_r ? 1 : 0);
-  const int32_t w0 = 2 * (g * a.unit_q + min(g, a.unit_r));
+  const int32_t ps = g * a.unit_q + min(g, a.unit_r);
   // ranks past the W-th start at or past P (2 (g q + r) >= 2 (W q + r) = 2Q >= P)
-  if (w0 >= a.n_pods) return;  // whole waves only; no barrier follows
-  const int32_t nwin = min(2 * np, a.n_pods - w0);
-  const bool act = lane < nwin;
-  uint32_t wa[R];
-  load_words<true>(wa, words, rs, 0, lane);  // requested before the pod bytes are waited for
-  uint32_t pcv = CODE_NONE_POD, tolv = 0;
-  if (act) {
-    const int d = a.pod_digit[w0 + lane];
-    pcv = (d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
-    tolv = a.pod_tol[w0 + lane] ? 1u : 0u;
-  }
-  // the tolerating pods' ulist pass first: its load latency overlaps the first node words'
-  // (already in flight); its per-pod minimum joins the scan's by min
-  uint32_t res = NOFIT;
-  const unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
-  if (mt) res = ulist_pass(mt, pcv, res, a.ulist, (uint32_t)__builtin_amdgcn_readfirstlane((int)uvec), lane);
-  if (__ballot(act && pcv != CODE_NONE_POD)) {
-    uint32_t rs_;
-    if (NP == 1 || np == NP)
-      rs_ = ident_unit8<R, false, NP>(pcv, wa, words, rs, nullptr, nc, lane);
-    else
-      rs_ = ident_unit8<R, false, (NP > 1 ? NP - 1 : 1)>(pcv, wa, words, rs, nullptr, nc, lane);
-    res = umin(res, rs_);
-  }
-  if (act) {
-    const int32_t j = w0 + lane;
-    if (SHARD) {
-      a.keys[j] = res != NOFIT ? shard_key(a.node_base, res) : 0;
-    } else {
-      const uint32_t ball = tolv ? (uint32_t)__builtin_amdgcn_readlane((int)bvec, 1)
-                                 : (uint32_t)__builtin_amdgcn_readlane((int)bvec, 0);
-      decode_ident(res != NOFIT ? (int64_t)res : -1, key_to_idx(ball), pcv != CODE_NONE_POD,
-                   make_ident_decode(a.pp), &a.out_idx[j], &a.out_score[j], &a.out_status[j]);
+  if (2 * ps >= a.n_pods) return;  // whole waves only; no barrier follows
+  // the range in `rounds` rounds of np * j / rounds .. np * (j + 1) / rounds pairs: NP or NP - 1
+  // each (the host picks rounds and NP so; one round unless the batch exceeds 8 pairs per wave)
+#pragma unroll 1
+  for (int32_t j = 0; j < rounds; ++j) {
+    const int32_t r0 = np * j / rounds, r1 = np * (j + 1) / rounds;
+    const int32_t w0 = 2 * (ps + r0);
+    if (r1 == r0 || w0 >= a.n_pods) continue;
+    const int32_t nwin = min(2 * (r1 - r0), a.n_pods - w0);
+    const bool act = lane < nwin;
+    uint32_t wa[R];
+    load_words<true>(wa, words, rs, 0, lane);  // requested before the pod bytes are waited for
+    uint32_t pcv = CODE_NONE_POD, tolv = 0;
+    if (act) {
+      const int d = a.pod_digit[w0 + lane];
+      pcv = (d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
+      tolv = a.pod_tol[w0 + lane] ? 1u : 0u;
+    }
+    // the tolerating pods' ulist pass first: its load latency overlaps the first node words'
+    // (already in flight); its per-pod minimum joins the scan's by min
+    uint32_t res = NOFIT;
+    const unsigned long long mt = __ballot(act && tolv != 0u && pcv != CODE_NONE_POD);
+    if (mt) res = ulist_pass(mt, pcv, res, a.ulist, (uint32_t)__builtin_amdgcn_readfirstlane((int)uvec), lane);
+    if (__ballot(act && pcv != CODE_NONE_POD)) {
+      uint32_t rsc;
+      if (NP == 1 || r1 - r0 == NP)
+        rsc = ident_unit8<R, false, NP>(pcv, wa, words, rs, nullptr, nc, lane);
+      else
+        rsc = ident_unit8<R, false, (NP > 1 ? NP - 1 : 1)>(pcv, wa, words, rs, nullptr, nc, lane);
+      res = umin(res, rsc);
+    }
+    if (act) {
+      const int32_t jp = w0 + lane;
+      if (SHARD) {
+        a.keys[jp] = res != NOFIT ? shard_key(a.node_base, res) : 0;
+      } else {
+        const uint32_t ball = tolv ? (uint32_t)__builtin_amdgcn_readlane((int)bvec, 1)
+                                   : (uint32_t)__builtin_amdgcn_readlane((int)bvec, 0);
+        decode_ident(res != NOFIT ? (int64_t)res : -1, key_to_idx(ball), pcv != CODE_NONE_POD,
+                     make_ident_decode(a.pp), &a.out_idx[jp], &a.out_score[jp], &a.out_status[jp]);
+      }
     }
   }
 }
@@ -1788,14 +1797,15 @@ int choose_split(int64_t n_pods, int32_t n_chunks, const DeviceInfo& dev) {
 }
 
 template <bool SHARD, int NP, int WT>
-hipError_t launch_ident_wave_wt(const BatchArgs& a, int64_t waves, hipStream_t s) {
+hipError_t launch_ident_wave_wt(const BatchArgs& a, int64_t waves, int32_t rounds, hipStream_t s) {
   constexpr int WPG = WT / WAVE;
   const int64_t pairs = ((int64_t)a.n_pods + 1) / 2;
   BatchArgs ka = a;  // pairs per wave: unit_q, and one more for the first unit_r wave ranks
   ka.unit_q = (int32_t)(pairs / waves);
   ka.unit_r = (int32_t)(pairs % waves);
   const int64_t grid = (waves + WPG - 1) / WPG;
-  hipLaunchKernelGGL((ident_wave_kernel<IDENT_R, SHARD, NP, WT>), dim3((unsigned)grid), dim3(WT), 0, s, ka);
+  hipLaunchKernelGGL((ident_wave_kernel<IDENT_R, SHARD, NP, WT>), dim3((unsigned)grid), dim3(WT), 0, s, ka,
+                     rounds);
   return hipGetLastError();
 }
 
@@ -1803,25 +1813,35 @@ hipError_t launch_ident_wave_wt(const BatchArgs& a, int64_t waves, hipStream_t s
 // their own few waves end, so the next launch (another stream) fills the chip sooner.
 // MSH_WAVE_THREADS (256 / 512 / 1024) is for A/B only.
 template <bool SHARD, int NP>
-hipError_t launch_ident_wave_np(const BatchArgs& a, int64_t waves, hipStream_t s) {
+hipError_t launch_ident_wave_np(const BatchArgs& a, int64_t waves, int32_t rounds, hipStream_t s) {
   const char* env = getenv("MSH_WAVE_THREADS");
   const int wt = env ? atoi(env) : 256;
-  if (wt == 1024) return launch_ident_wave_wt<SHARD, NP, 1024>(a, waves, s);
-  if (wt == 512) return launch_ident_wave_wt<SHARD, NP, 512>(a, waves, s);
-  return launch_ident_wave_wt<SHARD, NP, 256>(a, waves, s);
+  if (wt == 1024) return launch_ident_wave_wt<SHARD, NP, 1024>(a, waves, rounds, s);
+  if (wt == 512) return launch_ident_wave_wt<SHARD, NP, 512>(a, waves, rounds, s);
+  return launch_ident_wave_wt<SHARD, NP, 256>(a, waves, rounds, s);
 }
 
-// Waves for one contiguous pair range per wave: every wave of a full chip (2 x 1024-thread
-// workgroups per CU), or fewer when the batch is small (4 pairs per wave); 0 = more than 8
-// pairs per wave, the work queue takes over. MSH_WAVE_RANGE=0 disables it (A/B).
+// Waves for one contiguous pair range per wave: at most every wave of a full chip (8 per
+// SIMD), fewer when there are fewer than 4 or 7 pairs per wave (below); 0 = the work queue
+// takes over (a multi-tile table, or more than MSH_WAVE_MAX_ROUNDS rounds of 8 pairs per wave;
+// default 64). MSH_WAVE_RANGE=0 disables it (A/B).
 int64_t wave_range_waves(int64_t n_pods, int32_t n_chunks, const DeviceInfo& dev) {
   if (const char* env = getenv("MSH_WAVE_RANGE"))
     if (atoi(env) == 0) return 0;
   if (n_chunks > TILE_CHUNKS || n_pods <= 0) return 0;
+  const char* env = getenv("MSH_WAVE_MAX_ROUNDS");
+  const int64_t max_rounds = env ? atoi(env) : 64;
   const int64_t full = (int64_t)dev.cus * 32;
   const int64_t pairs = (n_pods + 1) / 2;
-  if (pairs > 8 * full) return 0;
-  return pairs >= 4 * full ? full : (pairs + 3) / 4;
+  if (pairs > 8 * max_rounds * full) return 0;
+  // pairs per wave at least mp (MSH_WAVE_MIN_PAIRS, A/B only). Batches that fill the chip at 4
+  // pairs per wave take 7: a wave's fixed costs (prologue, reduction, decode) and each node-word
+  // load are shared by more pairs; at C3 that leaves 7,143 of 8,192 wave slots busy and measured
+  // 1.5-2.7% faster pipelined than 6.1 pairs on all 8,192. Smaller batches take 4: shorter waves,
+  // lower latency (16k pods: 5.6 vs 6.9 us). profiles/ab/wave_min_pairs.jsonl
+  const char* menv = getenv("MSH_WAVE_MIN_PAIRS");
+  const int64_t mp = menv ? std::max(1, atoi(menv)) : pairs < 4 * full ? 4 : 7;
+  return std::min(full, (pairs + mp - 1) / mp);
 }
 
 template <bool SHARD>
@@ -1837,15 +1857,17 @@ hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStre
     return launch_ident_split_t<SHARD, 16>(a, dev, s, sc);
   }
   if (const int64_t waves = wave_range_waves(a.n_pods, a.n_chunks, dev)) {
-    switch ((((int64_t)a.n_pods + 1) / 2 + waves - 1) / waves) {  // the longest range, in pairs
-      case 1: return launch_ident_wave_np<SHARD, 1>(a, waves, s);
-      case 2: return launch_ident_wave_np<SHARD, 2>(a, waves, s);
-      case 3: return launch_ident_wave_np<SHARD, 3>(a, waves, s);
-      case 4: return launch_ident_wave_np<SHARD, 4>(a, waves, s);
-      case 5: return launch_ident_wave_np<SHARD, 5>(a, waves, s);
-      case 6: return launch_ident_wave_np<SHARD, 6>(a, waves, s);
-      case 7: return launch_ident_wave_np<SHARD, 7>(a, waves, s);
-      default: return launch_ident_wave_np<SHARD, 8>(a, waves, s);
+    const int64_t longest = (((int64_t)a.n_pods + 1) / 2 + waves - 1) / waves;  // in pairs
+    const int32_t rounds = (int32_t)((longest + 7) / 8);
+    switch ((longest + rounds - 1) / rounds) {  // the longest round, in pairs
+      case 1: return launch_ident_wave_np<SHARD, 1>(a, waves, rounds, s);
+      case 2: return launch_ident_wave_np<SHARD, 2>(a, waves, rounds, s);
+      case 3: return launch_ident_wave_np<SHARD, 3>(a, waves, rounds, s);
+      case 4: return launch_ident_wave_np<SHARD, 4>(a, waves, rounds, s);
+      case 5: return launch_ident_wave_np<SHARD, 5>(a, waves, rounds, s);
+      case 6: return launch_ident_wave_np<SHARD, 6>(a, waves, rounds, s);
+      case 7: return launch_ident_wave_np<SHARD, 7>(a, waves, rounds, s);
+      default: return launch_ident_wave_np<SHARD, 8>(a, waves, rounds, s);
     }
   }
   // MSH_DYN_THREADS (tuning / A-B only): workgroup size of the work-queue kernel

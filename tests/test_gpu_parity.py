@@ -428,12 +428,14 @@ def test_node_split_teams(msh, gpu_ctx, oracle, n, split, monkeypatch):
 
 
 @pytest.mark.parametrize("wave_range", ["1", "0"])
-@pytest.mark.parametrize("p", [1, 2, 3, 7, 8, 9, 15, 16, 17, 1000, 8191, 65_536, 65_537, 100_003, 131_071, 131_072,
-                               131_073, 140_000])
+@pytest.mark.parametrize("p", [1, 2, 3, 7, 8, 9, 15, 16, 17, 1000, 8191, 65_535, 65_536, 65_537, 100_003, 114_687,
+                               114_689, 131_071, 131_072, 131_073, 140_000, 300_001, 1_000_003])
 def test_wave_ranges(msh, gpu_ctx, oracle, p, wave_range, monkeypatch):
-    """One contiguous pair range per wave (1..8 pairs, ragged: r = Q mod W wave ranks take one
-    more, odd P leaves a half pair) on either side of the 4-pairs-per-wave and 8-pairs-per-wave
-    cuts, against the oracle; MSH_WAVE_RANGE=0 runs the same batches through the work queue."""
+    """One contiguous pair range per wave (ragged: r = Q mod W wave ranks take one more pair,
+    odd P leaves a half pair), in rounds of at most 8 pairs (2 rounds past 131,072 pods, 4 and
+    8 rounds at 300k and 1M), on either side of the cuts (4 pairs per wave below 65,536 pods, 7
+    from there, the whole chip from 114,688, 8 at 131,072), against the oracle;
+    MSH_WAVE_RANGE=0 runs the same batches through the work queue."""
     monkeypatch.setenv("MSH_WAVE_RANGE", wave_range)
     rng = np.random.default_rng(p)
     ps = oracle.PluginSet()
