@@ -108,6 +108,7 @@ struct BatchArgs {
   int64_t node_base;
   uint32_t* partial;         // [2][n_pods] running keys when the node table spans > 1 LDS tile
   int32_t unit_q, unit_r;    // work-queue kernel: workgroup b owns unit_q (+1 if b < unit_r) units
+  int32_t unit_w;            // wave-range kernel: wave count W (pairs = W * unit_q + unit_r)
 };
 
 // LDS tile geometry of the batched kernel (host needs it to size the partial-key scratch).

@@ -1082,9 +1082,28 @@ __global__ __launch_bounds__(NT) void ident_dyn_kernel(BatchArgs a) {
 // ---------------------------------------------------------------------------------------
 template <int R, bool SHARD, int NP, int WT>
 __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(8))) void ident_wave_kernel(BatchArgs a,
-                                                                                      int32_t rounds) {
+                                                                                      int32_t rounds,
+                                                                                      int32_t xcd) {
   const int lane = threadIdx.x & (WAVE - 1);
-  const int32_t g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * (int32_t)gridDim.x + (int32_t)blockIdx.x;
+  const int32_t wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int32_t gd = (int32_t)gridDim.x, b = (int32_t)blockIdx.x;
+  int32_t g, np, ps;
+  if (xcd) {
+    // XCD-contiguous ranks: workgroups are dispatched round-robin over the 8 XCDs (b mod 8), so
+    // XCD x's workgroups take one contiguous block of ranks and neighbouring ranges (whose output
+    // cache lines they share) are written through the same L2. The +1 pairs are spread evenly in
+    // rank order (Bresenham): rank g takes pairs [g q + floor(g r / W), (g + 1) q + floor((g + 1) r / W)).
+    const int32_t x = b & 7, base = gd >> 3, extra = gd & 7;
+    g = (x * base + min(x, extra) + (b >> 3)) * (WT / WAVE) + wv;
+    const uint32_t W = (uint32_t)a.unit_w, r = (uint32_t)a.unit_r;
+    const int32_t lo = (int32_t)((uint32_t)g * r / W), hi = (int32_t)((uint32_t)(g + 1) * r / W);
+    np = a.unit_q + (hi - lo);
+    ps = g * a.unit_q + lo;
+  } else {
+    g = wv * gd + b;
+    np = a.unit_q + (g < a.unit_r ? 1 : 0);
+    ps = g * a.unit_q + min(g, a.unit_r);
+  }
   const int32_t nc = a.n_chunks;  // one compute tile
   const uint32_t* words = a.w0;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1094,9 +1113,8 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(8))) void id
   const uint32_t uvec = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ucount, (short)0, 4, 0x00020000), 0, 0, 0);
   if (SHARD) write_class_keys(a);
-  // wave rank g: pairs [g * q + min(g, r), +q (+1 if g < r)), q / r host-computed (unit_q / unit_r)
-  const int32_t np = a.unit_q + (g < a.unit_r ? 1 : 0);
-  const int32_t ps = g * a.unit_q + min(g, a.unit_r);
+  // (xcd = 0, A/B: rank g = wave-in-workgroup x grid + workgroup takes pairs [g q + min(g, r),
+  // +q (+1 if g < r)); q / r / W host-computed: unit_q / unit_r / unit_w)
   // ranks past the W-th start at or past P (2 (g q + r) >= 2 (W q + r) = 2Q >= P)
   if (2 * ps >= a.n_pods) return;  // whole waves only; no barrier follows
   // the range in `rounds` rounds of np * j / rounds .. np * (j + 1) / rounds pairs: NP or NP - 1
@@ -1803,9 +1821,14 @@ hipError_t launch_ident_wave_wt(const BatchArgs& a, int64_t waves, int32_t round
   BatchArgs ka = a;  // pairs per wave: unit_q, and one more for the first unit_r wave ranks
   ka.unit_q = (int32_t)(pairs / waves);
   ka.unit_r = (int32_t)(pairs % waves);
+  ka.unit_w = (int32_t)waves;
   const int64_t grid = (waves + WPG - 1) / WPG;
+  // MSH_WAVE_XCD (A/B only): 1 = XCD-contiguous wave ranks (default), 0 = ranks interleaved
+  // across workgroups
+  const char* env = getenv("MSH_WAVE_XCD");
+  const int32_t xcd = env ? (atoi(env) != 0) : 1;
   hipLaunchKernelGGL((ident_wave_kernel<IDENT_R, SHARD, NP, WT>), dim3((unsigned)grid), dim3(WT), 0, s, ka,
-                     rounds);
+                     rounds, xcd);
   return hipGetLastError();
 }
 
