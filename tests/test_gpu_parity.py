@@ -427,16 +427,19 @@ def test_node_split_teams(msh, gpu_ctx, oracle, n, split, monkeypatch):
     _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"keys split={split} n={n}")
 
 
-@pytest.mark.parametrize("wave_range", ["1", "0"])
+@pytest.mark.parametrize("wave_range,wave_xcd", [("1", "1"), ("1", "0"), ("0", "1")])
 @pytest.mark.parametrize("p", [1, 2, 3, 7, 8, 9, 15, 16, 17, 1000, 8191, 65_535, 65_536, 65_537, 100_003, 114_687,
                                114_689, 131_071, 131_072, 131_073, 140_000, 300_001, 1_000_003])
-def test_wave_ranges(msh, gpu_ctx, oracle, p, wave_range, monkeypatch):
+def test_wave_ranges(msh, gpu_ctx, oracle, p, wave_range, wave_xcd, monkeypatch):
     """One contiguous pair range per wave (ragged: r = Q mod W wave ranks take one more pair,
     odd P leaves a half pair), in rounds of at most 8 pairs (2 rounds past 131,072 pods, 4 and
     8 rounds at 300k and 1M), on either side of the cuts (4 pairs per wave below 65,536 pods, 7
     from there, the whole chip from 114,688, 8 at 131,072), against the oracle;
-    MSH_WAVE_RANGE=0 runs the same batches through the work queue."""
+    MSH_WAVE_RANGE=0 runs the same batches through the work queue. Wave ranks are XCD-contiguous
+    with the extra pairs spread evenly in rank order (default), or interleaved across workgroups
+    with the extra pairs on the first ranks (MSH_WAVE_XCD=0)."""
     monkeypatch.setenv("MSH_WAVE_RANGE", wave_range)
+    monkeypatch.setenv("MSH_WAVE_XCD", wave_xcd)
     rng = np.random.default_rng(p)
     ps = oracle.PluginSet()
     _set(gpu_ctx, msh, ps)
