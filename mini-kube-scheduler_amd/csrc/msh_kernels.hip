@@ -33,7 +33,10 @@
 //
 // Kernels, by entry point:
 //   node_prep_kernel (+ prep_reset_kernel)  every upload / patch / plugin change
-//   ident_dyn_kernel     batch, IDENT modes: per-CU work queue of 8-pod units (default);
+//   ident_wave_kernel    batch, IDENT modes, single-tile tables (default, up to 64 rounds of
+//                        8 pairs per wave): one contiguous pod-pair range per wave,
+//                        XCD-contiguous wave ranks
+//   ident_dyn_kernel     batch, IDENT modes: per-CU work queue of 8-pod units (larger batches);
 //                        MULTI form for tables of several 64,512-node compute tiles
 //   ident_split_kernel   batch, IDENT modes, few pods against a large table: teams of waves
 //                        share a unit over table slices
