@@ -44,6 +44,7 @@ struct msh_ctx {
   uint32_t* d_ucount = nullptr;
   unsigned long long* d_mask = nullptr;
   uint32_t* d_ball = nullptr;      // [0..1] first-feasible keys, [2] ulist count
+  uint32_t* d_planes = nullptr;    // bit-sliced node table (msh_internal.h PLANE_* layout)
   int32_t* d_counts = nullptr;
   size_t node_cap = 0;
 
@@ -88,7 +89,8 @@ int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
 void free_nodes(msh_ctx* c) {
   hipFree(c->d_unsched); hipFree(c->d_digit); hipFree(c->d_c0); hipFree(c->d_dig);
   hipFree(c->d_mask); hipFree(c->d_counts); hipFree(c->d_w0); hipFree(c->d_ulist);
-  c->d_w0 = nullptr; c->d_ulist = nullptr;
+  hipFree(c->d_planes);
+  c->d_w0 = nullptr; c->d_ulist = nullptr; c->d_planes = nullptr;
   c->d_unsched = nullptr; c->d_digit = nullptr; c->d_c0 = nullptr; c->d_dig = nullptr;
   c->d_mask = nullptr; c->d_counts = nullptr;
   c->node_cap = 0;
@@ -137,7 +139,7 @@ int prepare(msh_ctx* c, hipStream_t s) {
   if (!c->dirty) return MSH_OK;
   hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad,
                                        c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_w0, c->d_ulist, c->d_ucount, c->d_mask,
-                                       c->d_ball, s, c->d_patch, c->patch_pending);
+                                       c->d_ball, c->d_planes, s, c->d_patch, c->patch_pending);
   c->patch_pending = 0;
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
   // The prepared tables are read by launches on any stream: finish them before returning (this
@@ -190,6 +192,8 @@ msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t
   a.ball = c->d_ball;
   a.pp = c->pp;
   a.partial = c->d_partial;
+  a.planes = c->d_planes;
+  a.n_groups = c->n_pad / msh::GROUP_NODES;
   return a;
 }
 
@@ -224,6 +228,9 @@ int msh_create(int device, msh_ctx** out_ctx) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->dev.cus = prop.multiProcessorCount;
+  // A/B switches, read once here (never on a launch path)
+  if (const char* e = getenv("MSH_BATCH_KERNEL")) c->dev.legacy_batch = strcmp(e, "legacy") == 0;
+  if (const char* e = getenv("MSH_BITS_SLICES")) c->dev.bits_slices = atoi(e);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return MSH_ERR_HIP;
@@ -337,6 +344,7 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
     MSH_HIP(c, hipMalloc(&c->d_ulist, cap * sizeof(uint32_t)));
     MSH_HIP(c, hipMalloc(&c->d_mask, 2 * (cap / 64) * sizeof(unsigned long long)));
     MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
+    MSH_HIP(c, hipMalloc(&c->d_planes, cap / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
     c->node_cap = cap;
   }
   if (n > 0) {
@@ -455,7 +463,7 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   a.out_idx = d_out_idx;
   a.out_score = d_out_score;
   a.out_status = d_out_status;
-  const bool up = p > 0 && msh::batch_uses_partial(c->pp, a.n_chunks);
+  const bool up = p > 0 && msh::batch_uses_partial(c->pp, a.n_chunks, c->dev);
   if ((rc = partial_begin(c, s, up)) != MSH_OK) return rc;
   hipError_t e = msh::launch_batch(a, false, c->dev, s, &c->err);
   if (e != hipSuccess) return hip_fail(c, e, "batch_kernel");
@@ -601,7 +609,7 @@ int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
   a.keys = d_keys;
   a.node_base = node_base;
-  const bool up = p > 0 && msh::batch_uses_partial(c->pp, a.n_chunks);
+  const bool up = p > 0 && msh::batch_uses_partial(c->pp, a.n_chunks, c->dev);
   if ((rc = partial_begin(c, s, up)) != MSH_OK) return rc;
   hipError_t e = msh::launch_batch(a, true, c->dev, s, &c->err);
   if (e != hipSuccess) return hip_fail(c, e, "batch_kernel(shard)");

@@ -40,8 +40,11 @@ inline bool needs_kx(const PluginParams& pp) {
   return pp.has_nn_score && pp.nn_prescore && (pp.mode == 2 || pp.mode == 3);
 }
 
+// Device facts and launch choices, resolved once in msh_create (never on the launch path).
 struct DeviceInfo {
   int cus = 256;
+  int legacy_batch = 0;  // A/B only (MSH_BATCH_KERNEL=legacy at msh_create): the packed-16 kernels
+  int bits_slices = 0;   // A/B only (MSH_BITS_SLICES at msh_create): slice waves per pod block, 0 = auto
 };
 
 // ---- launchers (msh_kernels.hip) ----
@@ -74,11 +77,30 @@ __host__ __device__ inline uint32_t word_pos(uint32_t i) {
 }
 constexpr uint32_t CODE_NONE_POD = 14u;
 
+// Bit-sliced node table (the batch kernel's input). Node i is bit (i mod 32) of word i / 32;
+// words come in groups of PLANE_GW (256 nodes), and a group holds PLANE_N planes of PLANE_GW
+// words each, plane-major, so one scalar load brings one plane of a whole group:
+//   planes[(g * PLANE_N + k) * PLANE_GW + j] = plane k of word g * PLANE_GW + j
+//   k = 0..3  bit k of the node's NodeNumber code: its suffix digit 0..9, or 15 when the name
+//             has no digit suffix or the slot is padding (15 never equals a pod code 0..9 / 14)
+//   k = 4     X: NodeUnschedulable rejects the node for pods that do not tolerate the
+//             unschedulable taint (Spec.Unschedulable with the filter in the list)
+//   k = 5     V: the slot holds a real node (i < n), i.e. it is feasible for tolerating pods
+// 0.75 B per node. A (pod, node) pair is a feasible digit match exactly when, in the node's bit,
+//   (X & ~tol) | (D0 ^ P0) | (D1 ^ P1) | (D2 ^ P2) | (D3 ^ P3) == 0
+// with P_k = all-ones when bit k of the pod's code is set.
+constexpr int PLANE_GW = 8;
+constexpr int PLANE_N = 6;
+constexpr int PLANE_X = 4, PLANE_V = 5;
+constexpr int GROUP_NODES = PLANE_GW * 32;
+constexpr int GROUP_DWORDS = PLANE_GW * PLANE_N;
+
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
                             int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
                             uint32_t* d_w0, uint32_t* d_ulist, uint32_t* d_ucount,
-                            unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s,
-                            const unsigned long long* d_patch = nullptr, int32_t patch_count = 0);
+                            unsigned long long* d_mask, uint32_t* d_ball, uint32_t* d_planes,
+                            hipStream_t s, const unsigned long long* d_patch = nullptr,
+                            int32_t patch_count = 0);
 
 constexpr int64_t EXPORT_NONE = INT64_MIN;  // msh_export_results: no score recorded
 hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
@@ -109,6 +131,9 @@ struct BatchArgs {
   uint32_t* partial;         // [2][n_pods] running keys when the node table spans > 1 LDS tile
   int32_t unit_q, unit_r;    // work-queue kernel: workgroup b owns unit_q (+1 if b < unit_r) units
   int32_t unit_w;            // wave-range kernel: wave count W (pairs = W * unit_q + unit_r)
+  const uint32_t* planes;    // bit-sliced node table (PLANE_* layout), n_pad / GROUP_NODES groups
+  int32_t n_groups;
+  int32_t gps;               // bit-sliced kernel: groups per slice wave
 };
 
 // LDS tile geometry of the batched kernel (host needs it to size the partial-key scratch).
@@ -116,7 +141,7 @@ int32_t batch_tile_chunks(int32_t n_chunks);
 bool batch_needs_partial(int32_t n_chunks);
 // does the batch kernel launch_batch picks for these plugins keep running results in `partial`
 // (a per-ctx scratch: such launches must not overlap on different streams)
-bool batch_uses_partial(const PluginParams& pp, int32_t n_chunks);
+bool batch_uses_partial(const PluginParams& pp, int32_t n_chunks, const DeviceInfo& dev);
 
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s,
                         std::string* err);

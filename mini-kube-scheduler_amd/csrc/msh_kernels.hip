@@ -128,7 +128,8 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
                                                                  uint32_t* __restrict__ ulist,
                                                                  uint32_t* __restrict__ ucount,
                                                                  unsigned long long* __restrict__ mask,
-                                                                 uint32_t* __restrict__ ball) {
+                                                                 uint32_t* __restrict__ ball,
+                                                                 uint32_t* __restrict__ planes) {
   constexpr int NWV = PREP_THREADS / WAVE;
   __shared__ uint32_t s_cnt[NWV], s_k0[NWV], s_k1[NWV];
   __shared__ uint32_t s_base;
@@ -152,6 +153,20 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
   // nodes whose feasibility differs between the classes -> ulist (order irrelevant: min search)
   const bool diff = feas1 && !feas0;
   const unsigned long long md = __ballot(diff);
+  {
+    // bit-sliced table: this wave's 64 nodes are words 2t and 2t + 1 of the PLANE_* layout
+    const uint32_t code = has_digit ? (uint32_t)d : CODE_NONE_NODE;
+    const unsigned long long pm[PLANE_N] = {__ballot(code & 1u), __ballot(code & 2u), __ballot(code & 4u),
+                                            __ballot(code & 8u), __ballot(valid && !feas0), __ballot(valid)};
+    if (lane < 2 * PLANE_N) {
+      const int k = lane >> 1, half = lane & 1;
+      unsigned long long m = pm[0];
+#pragma unroll
+      for (int q = 1; q < PLANE_N; ++q) m = (k == q) ? pm[q] : m;
+      const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;  // i - lane: the wave's first node
+      planes[((word / PLANE_GW) * PLANE_N + k) * PLANE_GW + word % PLANE_GW] = (uint32_t)(m >> (32 * half));
+    }
+  }
   if (lane == 0) {
     const int32_t chunk = i >> 6;
     const int32_t n_chunks = n_pad >> 6;
@@ -267,6 +282,186 @@ __device__ __forceinline__ void decode_ident(int64_t im, int64_t ia, bool pd_val
 
 __device__ __forceinline__ int64_t key_to_idx(uint32_t k) {
   return k ? (int64_t)(KMAX - k) : (int64_t)-1;
+}
+
+// ---------------------------------------------------------------------------------------
+// Bit-sliced batched kernel: stages 1-4 for every normalize mode (the default batch path).
+//
+// "Lanes = pods": lane l of the workgroup's waves holds pod 64 b + l. The node table is the
+// bit-sliced PLANE_* layout (msh_internal.h): one 32-bit word per plane covers 32 nodes, and the
+// planes of a word are wave-uniform, so they arrive by scalar loads and sit in SGPRs. Per lane
+// and word, with the pod's code bits as all-ones / all-zero masks P0..P3 and nT = ~tolerates:
+//   miss = (X & nT) | (D0 ^ P0) | (D1 ^ P1) | (D2 ^ P2) | (D3 ^ P3)      1 v_and + 4 v_bitop3
+// has a zero bit exactly at each node that passes NodeUnschedulable for this pod AND whose suffix
+// digit equals the pod's (NodeNumber.Score = 10): 32 (pod, node) pairs evaluated per lane-op
+// chain, 5 VALU per 32 x 64 pairs. Padding slots carry code 15, pods without a digit code 14: they
+// never match. Pairs of words AND into a per-group accumulator (v_bitop3, 3 inputs); a group of
+// PLANE_GW words with a zero bit is remembered (groups are walked in DESCENDING List order, so the
+// last one remembered is the first); afterwards the lane re-reads its own first group (vector
+// loads) and finds the exact node: first word with a zero bit, then its lowest zero bit. No
+// cross-lane reduction at all: the first maximum of selectHost (minisched.go:304-325) falls out of
+// the List order of words and bits.
+//
+// KX (REVERSE / MINMAX normalizers) also needs the first feasible NON-match:
+//   nmiss = ~dm | (X & nT) | ~V,  dm = (D0 ^ P0) | ... | (D3 ^ P3)
+// (8 VALU per word). The first feasible node of the pod's class comes from the prep (ball).
+//
+// S slice waves per workgroup split the groups of the table for the same 64 pods (small batches
+// against large tables keep the chip busy); their firsts meet in LDS (slices ascend in List
+// order, so the minimum is the first).
+// ---------------------------------------------------------------------------------------
+// t | (d ^ p) in one v_bitop3_b32 (truth table over S0 = t, S1 = d, S2 = p), d wave-uniform.
+// Written as asm: the backend prefers v_xor + v_or3 pairs, 7.75 VALU per word instead of 5.
+__device__ __forceinline__ uint32_t or_xor_s(uint32_t t, uint32_t d, uint32_t p) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xf6" : "=v"(r) : "v"(t), "s"(d), "v"(p));
+  return r;
+}
+// ~dm | xi | ~v (truth table over S0 = dm, S1 = xi, S2 = v), v wave-uniform
+__device__ __forceinline__ uint32_t nmiss_s(uint32_t dm, uint32_t xi, uint32_t v) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xdf" : "=v"(r) : "v"(dm), "v"(xi), "s"(v));
+  return r;
+}
+
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+
+// NPL planes of one group (PLANE_GW dwords each, contiguous) into SGPRs: NPL s_load_dwordx8 in
+// flight, then ONE s_waitcnt that takes the loaded registers as operands, so that no use of them
+// can be scheduled in front of it (the backend does not count asm-issued scalar loads).
+template <int NPL>
+__device__ __forceinline__ void sload_group(u32x8 (&pl)[NPL], const uint32_t* src) {
+#pragma unroll
+  for (int k = 0; k < NPL; ++k)
+    asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(pl[k]) : "s"(src), "n"(k * PLANE_GW * 4));
+  if constexpr (NPL == 5)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pl[0]), "+s"(pl[1]), "+s"(pl[2]), "+s"(pl[3]), "+s"(pl[4]));
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pl[0]), "+s"(pl[1]), "+s"(pl[2]), "+s"(pl[3]), "+s"(pl[4]),
+                 "+s"(pl[5]));
+}
+
+constexpr uint32_t NO_GROUP = 0xFFFFFFFFu;
+
+// The lane's first node in group g (per-lane vector loads of the group's planes): the first word
+// with a zero bit in the miss word, then its lowest zero bit. NONMATCH: the first feasible
+// non-match instead of the first feasible match. Returns a node index (g has one by construction).
+template <bool NONMATCH>
+__device__ __forceinline__ uint32_t group_first(const uint32_t* __restrict__ planes, uint32_t g, uint32_t P0,
+                                                uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT) {
+  const uint4* q = reinterpret_cast<const uint4*>(planes + (size_t)g * GROUP_DWORDS);
+  constexpr int NP = NONMATCH ? PLANE_N : PLANE_V;
+  uint32_t pl[NP][PLANE_GW];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const uint4 lo = q[k * 2], hi = q[k * 2 + 1];
+    pl[k][0] = lo.x; pl[k][1] = lo.y; pl[k][2] = lo.z; pl[k][3] = lo.w;
+    pl[k][4] = hi.x; pl[k][5] = hi.y; pl[k][6] = hi.z; pl[k][7] = hi.w;
+  }
+  uint32_t bw = 0;
+  int32_t bj = 0;
+#pragma unroll
+  for (int c = PLANE_GW - 1; c >= 0; --c) {
+    const uint32_t dm = (pl[0][c] ^ P0) | (pl[1][c] ^ P1) | (pl[2][c] ^ P2) | (pl[3][c] ^ P3);
+    const uint32_t xi = pl[PLANE_X][c] & nT;
+    uint32_t hit;
+    if constexpr (NONMATCH) hit = dm & ~xi & pl[PLANE_N - 1][c];
+    else hit = ~(dm | xi);
+    bj = hit ? c : bj;
+    bw = hit ? hit : bw;
+  }
+  return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
+}
+
+template <int S, bool KX, bool SHARD>
+__global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
+  __shared__ uint32_t s_res[S][KX ? 2 : 1][WAVE];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int32_t j = (int32_t)blockIdx.x * WAVE + lane;
+  const bool act = j < a.n_pods;
+  uint32_t code = CODE_NONE_POD, tol = 0;
+  if (act) {
+    const int d = a.pod_digit[j];
+    code = (d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
+    tol = a.pod_tol[j] ? 1u : 0u;
+  }
+  const uint32_t P0 = 0u - (code & 1u), P1 = 0u - ((code >> 1) & 1u), P2 = 0u - ((code >> 2) & 1u),
+                 P3 = 0u - (code >> 3);
+  const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
+  const int32_t g_lo = min(s * a.gps, a.n_groups), g_hi = min(g_lo + a.gps, a.n_groups);
+  uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group with a feasible match / non-match
+  constexpr int NPL = KX ? PLANE_N : PLANE_V;  // planes the scan reads
+  for (int32_t g = g_hi - 1; g >= g_lo; --g) {
+    // the group's planes, wave-uniform: one s_load_dwordx8 per plane, all in flight together,
+    // one wait (left to itself the backend interleaves single-dword scalar loads with the
+    // bitop3 chain, one lgkmcnt wait every few instructions)
+    u32x8 pl[NPL];
+    sload_group<NPL>(pl, a.planes + (size_t)g * GROUP_DWORDS);
+    uint32_t pg[NPL * PLANE_GW];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k)
+#pragma unroll
+      for (int c = 0; c < PLANE_GW; ++c) pg[k * PLANE_GW + c] = pl[k][c];
+    uint32_t am = 0xFFFFFFFFu, ax = 0xFFFFFFFFu;
+#pragma unroll
+    for (int w = 0; w < PLANE_GW; w += 2) {
+      uint32_t mm[2], mx[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = w + q;
+        const uint32_t xi = pg[PLANE_X * PLANE_GW + c] & nT;
+        if constexpr (KX) {
+          uint32_t dm = pg[c] ^ P0;
+          dm = or_xor_s(dm, pg[PLANE_GW + c], P1);
+          dm = or_xor_s(dm, pg[2 * PLANE_GW + c], P2);
+          dm = or_xor_s(dm, pg[3 * PLANE_GW + c], P3);
+          mm[q] = dm | xi;
+          mx[q] = nmiss_s(dm, xi, pg[PLANE_V * PLANE_GW + c]);
+        } else {
+          uint32_t t = or_xor_s(xi, pg[c], P0);
+          t = or_xor_s(t, pg[PLANE_GW + c], P1);
+          t = or_xor_s(t, pg[2 * PLANE_GW + c], P2);
+          mm[q] = or_xor_s(t, pg[3 * PLANE_GW + c], P3);
+        }
+      }
+      am &= mm[0] & mm[1];
+      if constexpr (KX) ax &= mx[0] & mx[1];
+    }
+    fm = am != 0xFFFFFFFFu ? (uint32_t)g : fm;
+    if constexpr (KX) fx = ax != 0xFFFFFFFFu ? (uint32_t)g : fx;
+  }
+  uint32_t rm = NOFIT, rx = NOFIT;  // node index of the first feasible match / non-match
+  if (fm != NO_GROUP) rm = group_first<false>(a.planes, fm, P0, P1, P2, P3, nT);
+  if (KX && fx != NO_GROUP) rx = group_first<true>(a.planes, fx, P0, P1, P2, P3, nT);
+  if constexpr (S > 1) {
+    s_res[s][0][lane] = rm;
+    if constexpr (KX) s_res[s][1][lane] = rx;
+    __syncthreads();
+    if (s != 0) return;
+#pragma unroll
+    for (int k = 1; k < S; ++k) {
+      rm = umin(rm, s_res[k][0][lane]);
+      if constexpr (KX) rx = umin(rx, s_res[k][1][lane]);
+    }
+  }
+  // after the scan: a store in front of it would keep the backend from proving the planes
+  // unclobbered, and the scalar loads would become vector loads
+  if (SHARD && !KX) write_class_keys(a);
+  if (!act) return;
+  if constexpr (SHARD) {
+    a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
+    if constexpr (KX) a.keys[(size_t)a.n_pods + j] = rx != NOFIT ? shard_key(a.node_base, rx) : 0;
+  } else {
+    const int64_t ia = key_to_idx(a.ball[tol]);
+    const int64_t im = rm != NOFIT ? (int64_t)rm : -1;
+    if constexpr (KX)
+      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, a.pp, &a.out_idx[j],
+                 &a.out_score[j], &a.out_status[j]);
+    else
+      decode_ident(im, ia, code != CODE_NONE_POD, make_ident_decode(a.pp), &a.out_idx[j], &a.out_score[j],
+                   &a.out_status[j]);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1568,8 +1763,8 @@ __global__ __launch_bounds__(256) void prep_reset_kernel(uint32_t* __restrict__ 
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n,
                             int32_t n_pad, int32_t has_nu, uint32_t* d_c0, uint8_t* d_dig,
                             uint32_t* d_w0, uint32_t* d_ulist, uint32_t* d_ucount,
-                            unsigned long long* d_mask, uint32_t* d_ball, hipStream_t s,
-                            const unsigned long long* d_patch, int32_t patch_count) {
+                            unsigned long long* d_mask, uint32_t* d_ball, uint32_t* d_planes,
+                            hipStream_t s, const unsigned long long* d_patch, int32_t patch_count) {
   const int32_t span = n_pad > patch_count ? n_pad : patch_count;
   hipLaunchKernelGGL(prep_reset_kernel, dim3((span > 0 ? span + 255 : 256) / 256), dim3(256), 0, s, d_ball,
                      d_ucount, d_ulist, n_pad, d_patch, patch_count, const_cast<uint8_t*>(d_unsched),
@@ -1579,7 +1774,7 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
   if (n_pad == 0) return hipSuccess;
   const int blocks = (n_pad + PREP_THREADS - 1) / PREP_THREADS;
   hipLaunchKernelGGL(node_prep_kernel, dim3(blocks), dim3(PREP_THREADS), 0, s, d_unsched, d_digit, n, n_pad,
-                     has_nu, d_c0, d_dig, d_w0, d_ulist, d_ucount, d_mask, d_ball);
+                     has_nu, d_c0, d_dig, d_w0, d_ulist, d_ucount, d_mask, d_ball, d_planes);
   return hipGetLastError();
 }
 
@@ -1908,6 +2103,37 @@ hipError_t launch_ident_dyn_t(const BatchArgs& a, const DeviceInfo& dev, hipStre
   if (nt == 512) return launch_ident_dyn_nt<SHARD, 512, false>(a, dev, s, err);
   return launch_ident_dyn_nt<SHARD, 1024, false>(a, dev, s, err);
 }
+// Slice waves per 64-pod block of the bit-sliced kernel: enough waves for ~6 per SIMD, each
+// slice at least two groups (512 nodes) so the per-wave fixed cost (pod bytes, the first-group
+// re-read, the LDS merge) stays small next to the scan.
+int bits_slices(int64_t n_pods, int32_t n_groups, const DeviceInfo& dev) {
+  if (dev.bits_slices > 0) return dev.bits_slices;
+  const int64_t blocks = (n_pods + WAVE - 1) / WAVE;
+  const int64_t want = (int64_t)dev.cus * 4 * 6;
+  int sl = 1;
+  while (sl < 16 && blocks * sl < want && n_groups / (2 * sl) >= 2) sl *= 2;
+  return sl;
+}
+
+template <int S, bool KX, bool SHARD>
+hipError_t launch_bits_s(const BatchArgs& a, hipStream_t s) {
+  BatchArgs ka = a;
+  ka.gps = (a.n_groups + S - 1) / S;
+  const int64_t blocks = ((int64_t)a.n_pods + WAVE - 1) / WAVE;
+  hipLaunchKernelGGL((bits_kernel<S, KX, SHARD>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  return hipGetLastError();
+}
+
+template <bool KX, bool SHARD>
+hipError_t launch_bits_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
+  switch (bits_slices(a.n_pods, a.n_groups, dev)) {
+    case 1: return launch_bits_s<1, KX, SHARD>(a, s);
+    case 2: return launch_bits_s<2, KX, SHARD>(a, s);
+    case 4: return launch_bits_s<4, KX, SHARD>(a, s);
+    case 8: return launch_bits_s<8, KX, SHARD>(a, s);
+    default: return launch_bits_s<16, KX, SHARD>(a, s);
+  }
+}
 }  // namespace
 
 int32_t batch_tile_chunks(int32_t n_chunks) {
@@ -1926,7 +2152,8 @@ int batch_kernel_choice() {
   return kenv ? atoi(kenv) : 3;
 }
 
-bool batch_uses_partial(const PluginParams& pp, int32_t n_chunks) {
+bool batch_uses_partial(const PluginParams& pp, int32_t n_chunks, const DeviceInfo& dev) {
+  if (!dev.legacy_batch) return false;  // the bit-sliced kernel keeps no running results
   const int kv = batch_kernel_choice();
   if (!needs_kx(pp) && kv == 3) return false;  // the work queue scans every tile per unit
   if (!needs_kx(pp) && kv != 1) return ident_stage_chunks(n_chunks, kv != 0) < n_chunks;
@@ -1937,6 +2164,10 @@ hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, h
                         std::string* err) {
   if (a.n_pods == 0) return hipSuccess;
   const bool kx = needs_kx(a.pp);
+  if (!dev.legacy_batch) {
+    if (shard) return kx ? launch_bits_t<true, true>(a, dev, s) : launch_bits_t<false, true>(a, dev, s);
+    return kx ? launch_bits_t<true, false>(a, dev, s) : launch_bits_t<false, false>(a, dev, s);
+  }
   const int kv = batch_kernel_choice();
   if (!kx && kv == 3)
     return shard ? launch_ident_dyn_t<true>(a, dev, s, err) : launch_ident_dyn_t<false>(a, dev, s, err);
