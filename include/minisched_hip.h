@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSH_ABI_VERSION 2
+#define MSH_ABI_VERSION 3
 
 /* ---- error codes (return values) ---- */
 typedef enum msh_err {
@@ -90,6 +90,15 @@ int msh_abi_version(void);
 
 /* Number of visible HIP devices (0 on a machine without a GPU). */
 int msh_device_count(int* out_count);
+
+/* Page-locked host memory (hipHostMalloc) for the host-buffer entry points' pod columns and
+ * outputs. With buffers from here (or registered with HIP) msh_schedule_batch / _sequential copy
+ * nothing on the host: the pod columns go to the device by DMA and the kernel writes idx / score /
+ * status straight into these buffers over PCIe. Pageable buffers work too; they are staged through
+ * a page-locked buffer of the ctx. A cgo caller allocates its batch buffers here once and reuses
+ * them. msh_host_free(NULL) is a no-op. */
+int msh_host_alloc(size_t bytes, void** out_ptr);
+void msh_host_free(void* ptr);
 
 /* Create/destroy a context on `device`. Default plugin set = the reference's
  * (initialize.go:80-123): filter=[NodeUnschedulable], prescore=[NodeNumber],
@@ -144,7 +153,8 @@ int msh_patch_nodes(msh_ctx* ctx, int32_t count, const int32_t* idx, const uint8
  * pod_digit[j] = last byte of pod.Name as digit or -1 (nodenumber.go:50-55);
  * pod_tol[j]   = pod tolerates taint {node.kubernetes.io/unschedulable, NoSchedule} (0/1).
  * Outputs per pod: out_idx (node index, -1 unless PLACED), out_score (total int64 score of
- * the selected node, 0 unless PLACED), out_status (msh_status). Synchronous. */
+ * the selected node, 0 unless PLACED), out_status (msh_status). Synchronous. Host buffers:
+ * page-locked ones (msh_host_alloc) take the zero-copy path, pageable ones are staged. */
 int msh_schedule_batch(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
                        int32_t* out_idx, int64_t* out_score, int32_t* out_status);
 
@@ -160,6 +170,8 @@ int msh_schedule_batch_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit
                               int64_t* d_out_score, int32_t* d_out_status, void* stream);
 
 /* Sequential-commit mode (one pod at a time, node state committed between placements).
+ * The node table stays in registers of one workgroup: up to 368,640 nodes without a capacity,
+ * 262,144 with one (larger tables: MSH_ERR_UNSUPPORTED).
  * The commit increments the selected node's assigned-pod count on the device (the
  * NodeInfo.AddPod analogue). max_pods_per_node > 0 additionally makes a node infeasible
  * once it holds that many pods (build extension); 0 = reference semantics, where the

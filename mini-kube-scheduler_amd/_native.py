@@ -48,7 +48,7 @@ MSH_NORMALIZE_MINMAX = 3
 
 # Every symbol include/minisched_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = (
-    "msh_abi_version", "msh_device_count", "msh_create", "msh_destroy", "msh_last_error",
+    "msh_abi_version", "msh_device_count", "msh_host_alloc", "msh_host_free", "msh_create", "msh_destroy", "msh_last_error",
     "msh_set_plugins", "msh_set_plugins_ex", "msh_upload_nodes", "msh_num_nodes",
     "msh_patch_nodes", "msh_export_results",
     "msh_schedule_batch", "msh_schedule_batch_device", "msh_schedule_sequential",
@@ -78,6 +78,8 @@ _I64 = C.c_int64
 _SIGS = {
     "msh_abi_version": (C.c_int, []),
     "msh_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "msh_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(_P)]),
+    "msh_host_free": (None, [_P]),
     "msh_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "msh_destroy": (None, [_P]),
     "msh_last_error": (C.c_char_p, [_P]),

@@ -2,23 +2,123 @@
 //
 // One msh_ctx per device. The ctx owns the device-resident node table (the replacement for
 // the per-cycle Nodes().List at minisched/minisched.go:40), the plugin descriptor
-// (minisched/initialize.go:80-123) and scratch buffers for the host-buffer entry points.
+// (minisched/initialize.go:80-123) and the buffers of the host-buffer entry points.
 // There is no CPU fallback: every schedule call runs the gfx950 kernels, and a missing
 // device is an error (MSH_ERR_NO_DEVICE).
+//
+// Host-buffer entry points (msh_schedule_batch / msh_schedule_sequential), the path a cgo caller
+// takes: the pod columns go to device scratch by DMA; the kernel writes idx / score / status
+// straight into page-locked host memory (zero-copy over PCIe, no copy after the kernel). When the
+// caller's buffers are page-locked (msh_host_alloc, or registered with HIP) they are used as they
+// are; otherwise the ctx stages through its own page-locked buffer, and the copies between the
+// caller's memory and the stage are split over a small pool of host threads.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/minisched_hip.h"
 #include "msh_internal.h"
 
 using msh::PluginParams;
+
+namespace {
+
+// Persistent host threads for the staged copies of the pageable path: run(f) calls f(0..n-1),
+// part 0 on the calling thread, the rest on the workers, and returns when all are done. A worker
+// spins on the job counter for a while after each job before it blocks, so back-to-back batches
+// do not pay a futex wake-up per call (tens of microseconds on a busy host).
+class CopyPool {
+ public:
+  explicit CopyPool(int workers) {
+    for (int w = 0; w < workers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_.store(true);
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int parts() const { return (int)th_.size() + 1; }
+  void run(const std::function<void(int)>& f) {
+    job_ = &f;
+    pending_.store((int)th_.size(), std::memory_order_relaxed);
+    gen_.fetch_add(1, std::memory_order_release);
+    { std::lock_guard<std::mutex> g(m_); }  // a worker between its check and its wait sees the new job
+    cv_.notify_all();
+    f(0);
+    while (pending_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int part) {
+    uint64_t seen = 0;
+    for (;;) {
+      uint64_t g = gen_.load(std::memory_order_acquire);
+      for (int spin = 0; g == seen && !stop_.load(std::memory_order_relaxed) && spin < (1 << 16); ++spin) {
+        std::this_thread::yield();
+        g = gen_.load(std::memory_order_acquire);
+      }
+      if (g == seen) {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_.load() || gen_.load(std::memory_order_acquire) != seen; });
+        g = gen_.load(std::memory_order_acquire);
+      }
+      if (stop_.load()) return;
+      seen = g;
+      (*job_)(part);
+      pending_.fetch_sub(1, std::memory_order_release);
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  std::atomic<int> pending_{0};
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> stop_{false};
+};
+
+struct CopyJob {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+
+// The copies, each split into pool.parts() contiguous pieces (64-byte aligned cuts), in ONE pool
+// run; small totals on the calling thread alone.
+void par_copy(CopyPool* pool, const CopyJob* jobs, int n_jobs) {
+  size_t total = 0;
+  for (int i = 0; i < n_jobs; ++i) total += jobs[i].bytes;
+  if (!pool || total < (256u << 10)) {
+    for (int i = 0; i < n_jobs; ++i) std::memcpy(jobs[i].dst, jobs[i].src, jobs[i].bytes);
+    return;
+  }
+  const int n = pool->parts();
+  pool->run([&](int k) {
+    for (int i = 0; i < n_jobs; ++i) {
+      const size_t b = jobs[i].bytes;
+      const size_t lo = (b * k / n) & ~(size_t)63, hi = k + 1 == n ? b : (b * (k + 1) / n) & ~(size_t)63;
+      if (hi > lo)
+        std::memcpy(static_cast<char*>(jobs[i].dst) + lo, static_cast<const char*>(jobs[i].src) + lo, hi - lo);
+    }
+  });
+}
+
+}  // namespace
 
 struct msh_ctx {
   int device = 0;
@@ -37,29 +137,21 @@ struct msh_ctx {
   int32_t n_nodes = 0, n_pad = 0;
   uint8_t* d_unsched = nullptr;
   int8_t* d_digit = nullptr;
-  uint32_t* d_c0 = nullptr;
-  uint8_t* d_dig = nullptr;
-  uint32_t* d_w0 = nullptr;
-  uint32_t* d_ulist = nullptr;
-  uint32_t* d_ucount = nullptr;
-  unsigned long long* d_mask = nullptr;
-  uint32_t* d_ball = nullptr;      // [0..1] first-feasible keys, [2] ulist count
-  uint32_t* d_planes = nullptr;    // bit-sliced node table (msh_internal.h PLANE_* layout)
+  uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout)
+  uint32_t* d_ball = nullptr;    // [0..1] first feasible node per pod class, as keys
   int32_t* d_counts = nullptr;
   size_t node_cap = 0;
 
-  // host-path scratch
+  // host-path buffers
   size_t pod_cap = 0;
-  int8_t* d_pd = nullptr;
+  int8_t* d_pd = nullptr;         // device scratch for the pod columns
   uint8_t* d_pt = nullptr;
-  int32_t* d_oi = nullptr;
+  int32_t* d_oi = nullptr;        // device scratch for the outputs (MSH_HOST_IO=dma only)
   int64_t* d_os = nullptr;
   int32_t* d_ost = nullptr;
-  size_t partial_cap = 0;
-  uint32_t* d_partial = nullptr;  // multi-tile node tables only
-  // launches that keep running results in d_partial are chained across streams by this event
-  hipEvent_t partial_ev = nullptr;
-  bool partial_ev_live = false;
+  size_t stage_cap = 0;
+  unsigned char* h_stage = nullptr;  // page-locked: digit p | tol p | idx 4p | score 8p | status 4p
+  CopyPool* pool = nullptr;
   size_t patch_cap = 0;
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
   int32_t patch_pending = 0;              // entries in d_patch the next prepare() applies
@@ -67,8 +159,6 @@ struct msh_ctx {
 };
 
 namespace {
-
-constexpr int32_t NODE_PAD = 64 * 16;  // node table padded to whole 16-chunk blocks
 
 int fail(msh_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -87,32 +177,89 @@ int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
   } while (0)
 
 void free_nodes(msh_ctx* c) {
-  hipFree(c->d_unsched); hipFree(c->d_digit); hipFree(c->d_c0); hipFree(c->d_dig);
-  hipFree(c->d_mask); hipFree(c->d_counts); hipFree(c->d_w0); hipFree(c->d_ulist);
-  hipFree(c->d_planes);
-  c->d_w0 = nullptr; c->d_ulist = nullptr; c->d_planes = nullptr;
-  c->d_unsched = nullptr; c->d_digit = nullptr; c->d_c0 = nullptr; c->d_dig = nullptr;
-  c->d_mask = nullptr; c->d_counts = nullptr;
+  (void)hipFree(c->d_unsched);
+  (void)hipFree(c->d_digit);
+  (void)hipFree(c->d_planes);
+  (void)hipFree(c->d_counts);
+  c->d_unsched = nullptr;
+  c->d_digit = nullptr;
+  c->d_planes = nullptr;
+  c->d_counts = nullptr;
   c->node_cap = 0;
 }
 
 void free_pods(msh_ctx* c) {
-  hipFree(c->d_pd); hipFree(c->d_pt); hipFree(c->d_oi); hipFree(c->d_os); hipFree(c->d_ost);
-  c->d_pd = nullptr; c->d_pt = nullptr; c->d_oi = nullptr; c->d_os = nullptr; c->d_ost = nullptr;
+  (void)hipFree(c->d_pd);
+  (void)hipFree(c->d_pt);
+  (void)hipFree(c->d_oi);
+  (void)hipFree(c->d_os);
+  (void)hipFree(c->d_ost);
+  c->d_pd = nullptr;
+  c->d_pt = nullptr;
+  c->d_oi = nullptr;
+  c->d_os = nullptr;
+  c->d_ost = nullptr;
   c->pod_cap = 0;
 }
 
 int ensure_pod_scratch(msh_ctx* c, int32_t p) {
   if ((size_t)p <= c->pod_cap) return MSH_OK;
   free_pods(c);
-  size_t cap = std::max<size_t>((size_t)p, 1024);
+  const size_t cap = std::max<size_t>((size_t)p, 1024);
   MSH_HIP(c, hipMalloc(&c->d_pd, cap));
   MSH_HIP(c, hipMalloc(&c->d_pt, cap));
-  MSH_HIP(c, hipMalloc(&c->d_oi, cap * sizeof(int32_t)));
-  MSH_HIP(c, hipMalloc(&c->d_os, cap * sizeof(int64_t)));
-  MSH_HIP(c, hipMalloc(&c->d_ost, cap * sizeof(int32_t)));
+  if (c->dev.host_io_dma) {
+    MSH_HIP(c, hipMalloc(&c->d_oi, cap * sizeof(int32_t)));
+    MSH_HIP(c, hipMalloc(&c->d_os, cap * sizeof(int64_t)));
+    MSH_HIP(c, hipMalloc(&c->d_ost, cap * sizeof(int32_t)));
+  }
   c->pod_cap = cap;
   return MSH_OK;
+}
+
+// layout of the page-locked stage for p pods (16-byte aligned sections)
+struct StageLayout {
+  size_t pd, pt, idx, score, status, total;
+  explicit StageLayout(size_t p) {
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    pd = 0;
+    pt = al(p);
+    idx = pt + al(p);
+    score = idx + al(4 * p);
+    status = score + 8 * p;
+    total = status + al(4 * p);
+  }
+};
+
+int ensure_stage(msh_ctx* c, int32_t p) {
+  const size_t need = StageLayout((size_t)p).total;
+  if (need > c->stage_cap) {
+    (void)hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    c->stage_cap = 0;
+    const size_t cap = StageLayout(std::max<size_t>((size_t)p, 4096)).total;
+    MSH_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), cap, hipHostMallocDefault));
+    c->stage_cap = cap;
+  }
+  if (!c->pool && (size_t)p >= 16384) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int workers = (int)std::min<unsigned>(7u, hw > 2 ? hw / 2 - 1 : 0u);
+    if (workers > 0) c->pool = new (std::nothrow) CopyPool(workers);
+  }
+  return MSH_OK;
+}
+
+// Device-visible address of page-locked host memory (hipHostMalloc'd or hipHostRegister'ed),
+// or nullptr for pageable memory. A failed query is not an error of the call: it is cleared so
+// that the next launch's hipGetLastError does not report it.
+void* pinned_device_ptr(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
+  return at.devicePointer;
 }
 
 bool contains(const std::vector<int32_t>& v, int32_t id) {
@@ -134,72 +281,118 @@ int check_ids(msh_ctx* c, const int32_t* ids, int32_t n, bool filter, const char
   return MSH_OK;
 }
 
+// Rebuild the derived tables (planes, first feasible per class) after an upload, a patch or a
+// filter-list change. Launches queued earlier on ANY stream (the *_device entry points) may still
+// be reading the tables this rewrites: wait for the whole device first (this runs only after an
+// upload, a patch or a plugin change, never per batch), and finish the rebuild before returning.
 int prepare(msh_ctx* c, hipStream_t s) {
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (!c->dirty) return MSH_OK;
-  hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad,
-                                       c->pp.has_nu_filter, c->d_c0, c->d_dig, c->d_w0, c->d_ulist, c->d_ucount, c->d_mask,
+  MSH_HIP(c, hipDeviceSynchronize());
+  hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad, c->pp.has_nu_filter,
                                        c->d_ball, c->d_planes, s, c->d_patch, c->patch_pending);
   c->patch_pending = 0;
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
-  // The prepared tables are read by launches on any stream: finish them before returning (this
-  // runs only after an upload, a patch or a plugin change, never per batch).
   MSH_HIP(c, hipStreamSynchronize(s));
   c->dirty = false;
   return MSH_OK;
 }
 
-// A launch whose kernel keeps running results in the ctx's d_partial scratch must not overlap
-// another such launch on a different stream: each waits for the previous one's completion.
-int partial_begin(msh_ctx* c, hipStream_t s, bool uses) {
-  if (!uses) return MSH_OK;
-  if (!c->partial_ev) MSH_HIP(c, hipEventCreateWithFlags(&c->partial_ev, hipEventDisableTiming));
-  if (c->partial_ev_live) MSH_HIP(c, hipStreamWaitEvent(s, c->partial_ev, 0));
-  return MSH_OK;
-}
-
-int partial_end(msh_ctx* c, hipStream_t s, bool uses) {
-  if (!uses) return MSH_OK;
-  MSH_HIP(c, hipEventRecord(c->partial_ev, s));
-  c->partial_ev_live = true;
-  return MSH_OK;
-}
-
-int ensure_partial(msh_ctx* c, int32_t p) {
-  if (!msh::batch_needs_partial(c->n_pad / 64)) return MSH_OK;
-  if ((size_t)p <= c->partial_cap) return MSH_OK;
-  (void)hipFree(c->d_partial);
-  c->d_partial = nullptr;
-  c->partial_cap = 0;
-  const size_t cap = std::max<size_t>((size_t)p, 1024);
-  MSH_HIP(c, hipMalloc(&c->d_partial, 2 * cap * sizeof(uint32_t)));
-  c->partial_cap = cap;
-  return MSH_OK;
-}
-
 msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t* pt) {
   msh::BatchArgs a{};
-  a.c0 = c->d_c0;
-  a.dig = c->d_dig;
-  a.w0 = c->d_w0;
-  a.ulist = c->d_ulist;
-  a.ucount = c->d_ucount;
-  a.n_nodes = c->n_nodes;
-  a.n_chunks = c->n_pad / 64;
+  a.planes = c->d_planes;
+  a.n_groups = c->n_pad / msh::GROUP_NODES;
   a.pod_digit = pd;
   a.pod_tol = pt;
   a.n_pods = p;
   a.ball = c->d_ball;
   a.pp = c->pp;
-  a.partial = c->d_partial;
-  a.planes = c->d_planes;
-  a.n_groups = c->n_pad / msh::GROUP_NODES;
   return a;
 }
 
 struct DeviceGuard {
   explicit DeviceGuard(int d) { (void)hipSetDevice(d); }
 };
+
+// Host-buffer I/O of one synchronous call: pod columns DMA'd into device scratch; the outputs
+// written by the kernel straight into page-locked host memory (default), or (MSH_HOST_IO=dma at
+// msh_create, A/B) into device scratch and copied there by DMA; then, for a pageable caller,
+// copied from the stage into the caller's arrays.
+struct HostIO {
+  int8_t* d_pd = nullptr;
+  uint8_t* d_pt = nullptr;
+  int32_t* o_idx = nullptr;    // what the kernel writes (device-visible)
+  int64_t* o_score = nullptr;
+  int32_t* o_status = nullptr;
+  int32_t* h_idx = nullptr;    // page-locked destination: the caller's arrays or the stage
+  int64_t* h_score = nullptr;
+  int32_t* h_status = nullptr;
+  bool staged = false;
+};
+
+int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol, int32_t* out_idx,
+                  int64_t* out_score, int32_t* out_status, HostIO& io) {
+  int rc = ensure_pod_scratch(c, p);
+  if (rc != MSH_OK) return rc;
+  io.d_pd = c->d_pd;
+  io.d_pt = c->d_pt;
+  void* di = pinned_device_ptr(out_idx);
+  void* ds = di ? pinned_device_ptr(out_score) : nullptr;
+  void* dt = ds ? pinned_device_ptr(out_status) : nullptr;
+  const bool in_pinned = pinned_device_ptr(pod_digit) && pinned_device_ptr(pod_tol);
+  io.staged = !(di && ds && dt);
+  if (io.staged || !in_pinned) {
+    if ((rc = ensure_stage(c, p)) != MSH_OK) return rc;
+  }
+  const StageLayout L((size_t)p);
+  if (in_pinned) {  // DMA straight from the caller's page-locked columns
+    MSH_HIP(c, hipMemcpyAsync(c->d_pd, pod_digit, (size_t)p, hipMemcpyHostToDevice, c->stream));
+    MSH_HIP(c, hipMemcpyAsync(c->d_pt, pod_tol, (size_t)p, hipMemcpyHostToDevice, c->stream));
+  } else {  // through the stage
+    const CopyJob jobs[2] = {{c->h_stage + L.pd, pod_digit, (size_t)p}, {c->h_stage + L.pt, pod_tol, (size_t)p}};
+    par_copy(c->pool, jobs, 2);
+    MSH_HIP(c, hipMemcpyAsync(c->d_pd, c->h_stage + L.pd, (size_t)p, hipMemcpyHostToDevice, c->stream));
+    MSH_HIP(c, hipMemcpyAsync(c->d_pt, c->h_stage + L.pt, (size_t)p, hipMemcpyHostToDevice, c->stream));
+  }
+  if (io.staged) {
+    io.h_idx = reinterpret_cast<int32_t*>(c->h_stage + L.idx);
+    io.h_score = reinterpret_cast<int64_t*>(c->h_stage + L.score);
+    io.h_status = reinterpret_cast<int32_t*>(c->h_stage + L.status);
+    io.o_idx = io.h_idx;  // hipHostMalloc memory: the host pointer is valid on the device too
+    io.o_score = io.h_score;
+    io.o_status = io.h_status;
+  } else {
+    io.h_idx = out_idx;
+    io.h_score = out_score;
+    io.h_status = out_status;
+    io.o_idx = static_cast<int32_t*>(di);
+    io.o_score = static_cast<int64_t*>(ds);
+    io.o_status = static_cast<int32_t*>(dt);
+  }
+  if (c->dev.host_io_dma) {
+    io.o_idx = c->d_oi;
+    io.o_score = c->d_os;
+    io.o_status = c->d_ost;
+  }
+  return MSH_OK;
+}
+
+int host_io_end(msh_ctx* c, int32_t p, int32_t* out_idx, int64_t* out_score, int32_t* out_status,
+                const HostIO& io) {
+  if (c->dev.host_io_dma) {
+    MSH_HIP(c, hipMemcpyAsync(io.h_idx, c->d_oi, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    MSH_HIP(c, hipMemcpyAsync(io.h_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    MSH_HIP(c, hipMemcpyAsync(io.h_status, c->d_ost, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  }
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  if (io.staged) {
+    const CopyJob jobs[3] = {{out_idx, io.h_idx, (size_t)p * sizeof(int32_t)},
+                             {out_score, io.h_score, (size_t)p * sizeof(int64_t)},
+                             {out_status, io.h_status, (size_t)p * sizeof(int32_t)}};
+    par_copy(c->pool, jobs, 3);
+  }
+  return MSH_OK;
+}
 
 }  // namespace
 
@@ -215,6 +408,22 @@ int msh_device_count(int* out_count) {
   return MSH_OK;
 }
 
+int msh_host_alloc(size_t bytes, void** out_ptr) {
+  if (!out_ptr) return MSH_ERR_INVALID;
+  *out_ptr = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MSH_ERR_NO_DEVICE;
+  if (hipHostMalloc(out_ptr, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+    *out_ptr = nullptr;
+    return MSH_ERR_NOMEM;
+  }
+  return MSH_OK;
+}
+
+void msh_host_free(void* ptr) {
+  if (ptr) (void)hipHostFree(ptr);
+}
+
 int msh_create(int device, msh_ctx** out_ctx) {
   if (!out_ctx) return MSH_ERR_INVALID;
   *out_ctx = nullptr;
@@ -228,22 +437,21 @@ int msh_create(int device, msh_ctx** out_ctx) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->dev.cus = prop.multiProcessorCount;
-  // A/B switches, read once here (never on a launch path)
-  if (const char* e = getenv("MSH_BATCH_KERNEL")) c->dev.legacy_batch = strcmp(e, "legacy") == 0;
+  // test / A-B switches, read once here (never on a launch path)
   if (const char* e = getenv("MSH_BITS_SLICES")) c->dev.bits_slices = atoi(e);
+  if (const char* e = getenv("MSH_SEQ_WAVES")) c->dev.seq_waves = atoi(e);
+  if (const char* e = getenv("MSH_HOST_IO")) c->dev.host_io_dma = strcmp(e, "dma") == 0;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return MSH_ERR_HIP;
   }
-  const size_t scalar_bytes = 4 * sizeof(uint32_t);  // ball[2] + ucount
-  if (hipMalloc(&c->d_ball, scalar_bytes) != hipSuccess ||
-      hipMemset(c->d_ball, 0, scalar_bytes) != hipSuccess) {
+  if (hipMalloc(&c->d_ball, 2 * sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(c->d_ball, 0, 2 * sizeof(uint32_t)) != hipSuccess) {
     (void)hipFree(c->d_ball);
-    hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->stream);
     delete c;
     return MSH_ERR_HIP;
   }
-  c->d_ucount = c->d_ball + 2;  // shares the small scalar allocation
   // Reference plugin set (minisched/initialize.go:80-123).
   c->filter_ids = {MSH_PLUGIN_NODE_UNSCHEDULABLE};
   c->prescore_ids = {MSH_PLUGIN_NODE_NUMBER};
@@ -260,13 +468,13 @@ void msh_destroy(msh_ctx* c) {
   (void)hipSetDevice(c->device);
   // launches queued on caller streams (the *_device entry points) may still read the tables
   (void)hipDeviceSynchronize();
+  delete c->pool;
   free_nodes(c);
   free_pods(c);
-  (void)hipFree(c->d_partial);
+  (void)hipHostFree(c->h_stage);
   (void)hipFree(c->d_patch);
   (void)hipFree(c->d_ball);
-  if (c->partial_ev) (void)hipEventDestroy(c->partial_ev);
-  if (c->stream) hipStreamDestroy(c->stream);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -330,19 +538,16 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
   if (n < 0 || n > msh::MAX_NODES) return fail(c, MSH_ERR_INVALID, "node count outside [0, 2^24-2]");
   if (n > 0 && (!unsched || !digit)) return fail(c, MSH_ERR_INVALID, "null node arrays");
   DeviceGuard g(c->device);
-  // Padded to whole 16-chunk blocks, and never empty: an empty cluster is a table of
-  // padding nodes (infeasible for every pod), so every pod gets FitError from the kernel.
-  const int32_t n_pad = std::max(((n + NODE_PAD - 1) / NODE_PAD) * NODE_PAD, NODE_PAD);
-  if ((size_t)n_pad > c->node_cap || c->d_c0 == nullptr) {
+  // launches queued earlier on any stream may still read the tables rewritten below
+  MSH_HIP(c, hipDeviceSynchronize());
+  // Padded to whole 1,024-node blocks, and never empty: an empty cluster is a table of padding
+  // slots (infeasible for every pod), so every pod gets FitError from the kernel.
+  const int32_t n_pad = std::max(((n + msh::NODE_PAD - 1) / msh::NODE_PAD) * msh::NODE_PAD, msh::NODE_PAD);
+  if ((size_t)n_pad > c->node_cap || c->d_planes == nullptr) {
     free_nodes(c);
-    const size_t cap = std::max<size_t>((size_t)n_pad, NODE_PAD);
+    const size_t cap = (size_t)n_pad;
     MSH_HIP(c, hipMalloc(&c->d_unsched, cap));
     MSH_HIP(c, hipMalloc(&c->d_digit, cap));
-    MSH_HIP(c, hipMalloc(&c->d_c0, cap * sizeof(uint32_t)));
-    MSH_HIP(c, hipMalloc(&c->d_dig, cap));
-    MSH_HIP(c, hipMalloc(&c->d_w0, cap * sizeof(uint32_t)));
-    MSH_HIP(c, hipMalloc(&c->d_ulist, cap * sizeof(uint32_t)));
-    MSH_HIP(c, hipMalloc(&c->d_mask, 2 * (cap / 64) * sizeof(unsigned long long)));
     MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
     MSH_HIP(c, hipMalloc(&c->d_planes, cap / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
     c->node_cap = cap;
@@ -356,10 +561,7 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
   c->n_pad = n_pad;
   c->have_nodes = true;
   c->dirty = true;
-  int rc = prepare(c, c->stream);
-  if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipStreamSynchronize(c->stream));
-  return MSH_OK;
+  return prepare(c, c->stream);  // synchronous
 }
 
 int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t* unsched,
@@ -382,6 +584,8 @@ int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t
                     ((unsigned long long)(unsched[k] ? 1u : 0u) << 32) |
                     ((unsigned long long)(uint8_t)digit[k] << 40);
   DeviceGuard g(c->device);
+  // launches queued earlier on any stream may still read the tables the patch rewrites
+  MSH_HIP(c, hipDeviceSynchronize());
   if ((size_t)count > c->patch_cap) {
     (void)hipFree(c->d_patch);
     c->d_patch = nullptr;
@@ -410,12 +614,13 @@ int msh_export_results(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   if (!pod_digit || !pod_tol || !out_filter || !out_score || !out_final)
     return fail(c, MSH_ERR_INVALID, "null pointer");
   DeviceGuard g(c->device);
+  int rc = prepare(c, c->stream);
+  if (rc != MSH_OK) return rc;
   int8_t* d_pd = nullptr;
   uint8_t* d_pt = nullptr;
   uint8_t* d_f = nullptr;
   int64_t* d_r = nullptr;
   int64_t* d_o = nullptr;
-  int rc = MSH_OK;
   auto step = [&](hipError_t e, const char* what) {
     if (rc == MSH_OK && e != hipSuccess) rc = hip_fail(c, e, what);
   };
@@ -458,16 +663,13 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = prepare(c, s);
   if (rc != MSH_OK) return rc;
-  if ((rc = ensure_partial(c, p)) != MSH_OK) return rc;
   msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
   a.out_idx = d_out_idx;
   a.out_score = d_out_score;
   a.out_status = d_out_status;
-  const bool up = p > 0 && msh::batch_uses_partial(c->pp, a.n_chunks, c->dev);
-  if ((rc = partial_begin(c, s, up)) != MSH_OK) return rc;
-  hipError_t e = msh::launch_batch(a, false, c->dev, s, &c->err);
-  if (e != hipSuccess) return hip_fail(c, e, "batch_kernel");
-  return partial_end(c, s, up);
+  hipError_t e = msh::launch_batch(a, false, c->dev, s);
+  if (e != hipSuccess) return hip_fail(c, e, "bits_kernel");
+  return MSH_OK;
 }
 
 int msh_schedule_batch(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
@@ -480,17 +682,13 @@ int msh_schedule_batch(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (p == 0) return MSH_OK;
   DeviceGuard g(c->device);
-  int rc = ensure_pod_scratch(c, p);
+  int rc = prepare(c, c->stream);
   if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipMemcpyAsync(c->d_pd, pod_digit, (size_t)p, hipMemcpyHostToDevice, c->stream));
-  MSH_HIP(c, hipMemcpyAsync(c->d_pt, pod_tol, (size_t)p, hipMemcpyHostToDevice, c->stream));
-  rc = msh_schedule_batch_device(c, p, c->d_pd, c->d_pt, c->d_oi, c->d_os, c->d_ost, c->stream);
+  HostIO io;
+  if ((rc = host_io_begin(c, p, pod_digit, pod_tol, out_idx, out_score, out_status, io)) != MSH_OK) return rc;
+  rc = msh_schedule_batch_device(c, p, io.d_pd, io.d_pt, io.o_idx, io.o_score, io.o_status, c->stream);
   if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipMemcpyAsync(out_idx, c->d_oi, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  MSH_HIP(c, hipMemcpyAsync(out_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  MSH_HIP(c, hipMemcpyAsync(out_status, c->d_ost, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  MSH_HIP(c, hipStreamSynchronize(c->stream));
-  return MSH_OK;
+  return host_io_end(c, p, out_idx, out_score, out_status, io);
 }
 
 int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
@@ -507,10 +705,10 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   int rc = prepare(c, s);
   if (rc != MSH_OK) return rc;
   msh::SeqArgs a{};
-  a.c0 = c->d_c0;
-  a.dig = c->d_dig;
+  a.planes = c->d_planes;
+  a.n_words = c->n_pad / 32;
+  a.ball = c->d_ball;
   a.n_nodes = c->n_nodes;
-  a.n_chunks = c->n_pad / 64;
   a.pod_digit = d_pod_digit;
   a.pod_tol = d_pod_tol;
   a.n_pods = p;
@@ -521,7 +719,7 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   a.out_score = d_out_score;
   a.out_status = d_out_status;
   std::string err;
-  hipError_t e = msh::launch_sequential(a, s, &err);
+  hipError_t e = msh::launch_sequential(a, c->dev, s, &err);
   if (e != hipSuccess) {
     if (!err.empty()) return fail(c, MSH_ERR_UNSUPPORTED, err);
     return hip_fail(c, e, "seq_kernel");
@@ -540,17 +738,14 @@ int msh_schedule_sequential(msh_ctx* c, int32_t p, const int8_t* pod_digit, cons
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (p == 0) return MSH_OK;
   DeviceGuard g(c->device);
-  int rc = ensure_pod_scratch(c, p);
+  int rc = prepare(c, c->stream);
   if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipMemcpyAsync(c->d_pd, pod_digit, (size_t)p, hipMemcpyHostToDevice, c->stream));
-  MSH_HIP(c, hipMemcpyAsync(c->d_pt, pod_tol, (size_t)p, hipMemcpyHostToDevice, c->stream));
-  rc = msh_schedule_sequential_device(c, p, c->d_pd, c->d_pt, max_pods_per_node, c->d_oi, c->d_os,
-                                      c->d_ost, c->stream);
+  HostIO io;
+  if ((rc = host_io_begin(c, p, pod_digit, pod_tol, out_idx, out_score, out_status, io)) != MSH_OK) return rc;
+  rc = msh_schedule_sequential_device(c, p, io.d_pd, io.d_pt, max_pods_per_node, io.o_idx, io.o_score,
+                                      io.o_status, c->stream);
   if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipMemcpyAsync(out_idx, c->d_oi, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  MSH_HIP(c, hipMemcpyAsync(out_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  MSH_HIP(c, hipMemcpyAsync(out_status, c->d_ost, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  if ((rc = host_io_end(c, p, out_idx, out_score, out_status, io)) != MSH_OK) return rc;
   if (commit_cb)
     for (int32_t j = 0; j < p; j++)
       if (out_status[j] == MSH_PLACED) commit_cb(user, j, out_idx[j], out_score[j]);
@@ -574,6 +769,7 @@ int msh_reset_node_pod_counts(msh_ctx* c) {
   c->err.clear();
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   DeviceGuard g(c->device);
+  MSH_HIP(c, hipDeviceSynchronize());  // sequential launches in flight update the counts
   MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->node_cap * sizeof(int32_t), c->stream));
   MSH_HIP(c, hipStreamSynchronize(c->stream));
   return MSH_OK;
@@ -605,15 +801,12 @@ int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = prepare(c, s);
   if (rc != MSH_OK) return rc;
-  if ((rc = ensure_partial(c, p)) != MSH_OK) return rc;
   msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
   a.keys = d_keys;
   a.node_base = node_base;
-  const bool up = p > 0 && msh::batch_uses_partial(c->pp, a.n_chunks, c->dev);
-  if ((rc = partial_begin(c, s, up)) != MSH_OK) return rc;
-  hipError_t e = msh::launch_batch(a, true, c->dev, s, &c->err);
-  if (e != hipSuccess) return hip_fail(c, e, "batch_kernel(shard)");
-  return partial_end(c, s, up);
+  hipError_t e = msh::launch_batch(a, true, c->dev, s);
+  if (e != hipSuccess) return hip_fail(c, e, "bits_kernel(shard)");
+  return MSH_OK;
 }
 
 int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,

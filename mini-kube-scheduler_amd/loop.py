@@ -53,7 +53,7 @@ class CycleReport:
     node_index: np.ndarray # int32, -1 unless placed
     score: np.ndarray      # int64
     status: np.ndarray     # int32 msh_status
-    node_names: list[str]  # List-order names of the snapshot used
+    node_names: tuple[str, ...]  # List-order names of the snapshot used (a copy)
     sync: str              # node table sync: "upload" / "patch" / "clean"
     bind: BindOutcome      # Permit/Bind resolutions that became due during this cycle
 
@@ -153,17 +153,19 @@ class SchedulingLoop:
         bind = self.poll_binder()
         batch = self.queue.next_batch(self.max_batch if max_pods is None else max_pods)
         sync = self.cache.sync(self.ctx)
+        # the report keeps a snapshot of the List-order names: NodeCache.add / delete change the
+        # live list in place, and node_index must keep naming this cycle's nodes
+        names = tuple(self.cache.names)
         if not len(batch):
             return CycleReport(batch.ids, [], np.empty(0, np.int32), np.empty(0, np.int64),
-                               np.empty(0, np.int32), self.cache.names, sync, bind)
+                               np.empty(0, np.int32), names, sync, bind)
         idx, score, status = self.ctx.schedule_batch(batch.digit, batch.tolerates)
         placed = status == N.MSH_PLACED
         self.error_func(batch.ids[~placed], status[~placed])
         if placed.any():
             node_idx = idx[placed]
-            names = self.cache.names
             self.binder.submit(batch.ids[placed], [names[i] for i in node_idx], self.cache.digit[node_idx])
-        return CycleReport(batch.ids, batch.names, idx, score, status, self.cache.names, sync, bind)
+        return CycleReport(batch.ids, batch.names, idx, score, status, names, sync, bind)
 
     def poll_binder(self) -> BindOutcome:
         """Resolve due Permit waits; rejected / failed binds go back through ErrorFunc."""

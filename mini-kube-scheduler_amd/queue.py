@@ -231,10 +231,14 @@ class SchedulingQueue:
             col.ensure(n)
         self._digit.a[ids] = digit
         self._tol.a[ids] = tol
-        self._ts.a[ids] = now                # newQueuedPodInfo, queue.go:156-165
-        self._t0.a[ids] = now
-        self._attempts.a[ids] = 0
-        self._plugins.a[ids] = 0
+        # newQueuedPodInfo (queue.go:156-165) for the fresh activeQ entry. A pod that also sits in
+        # unschedulableQ keeps that entry's UnschedulablePlugins and Timestamp: upstream Add appends
+        # a NEW QueuedPodInfo and leaves the map entry (and what MoveAll / backoff read) alone.
+        fresh = ids[~self._in_unsched.a[ids].astype(bool)]
+        self._ts.a[fresh] = now
+        self._t0.a[fresh] = now
+        self._attempts.a[fresh] = 0
+        self._plugins.a[fresh] = 0
         return ids
 
     def _push_active(self, ids: np.ndarray) -> None:

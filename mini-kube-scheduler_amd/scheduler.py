@@ -15,6 +15,7 @@ names raise MshError(MSH_ERR_UNSUPPORTED): there is no silent host fallback.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 from typing import Any, Callable, Iterable, Sequence
 
@@ -34,6 +35,27 @@ class ScorePluginConfig:
     name: str
     weight: int = 1
     normalize: Normalize = Normalize.NONE
+
+
+def pinned_empty(shape, dtype) -> np.ndarray:
+    """A numpy array over page-locked host memory (msh_host_alloc): pod columns and outputs in
+    such arrays take the zero-copy path of msh_schedule_batch / msh_schedule_sequential. The
+    memory is freed (msh_host_free) when the array and every view of it are gone."""
+    dt = np.dtype(dtype)
+    nbytes = max(int(np.prod(shape, dtype=np.int64)) * dt.itemsize, 1)
+    lib = N.lib()
+    ptr = C.c_void_p()
+    N.check(lib.msh_host_alloc(nbytes, C.byref(ptr)))
+    raw = (C.c_uint8 * nbytes).from_address(ptr.value)
+    weakref.finalize(raw, lib.msh_host_free, ptr)
+    return np.frombuffer(raw, np.uint8, count=int(np.prod(shape, dtype=np.int64)) * dt.itemsize).view(dt).reshape(shape)
+
+
+def _same_len(what: str, *arrays) -> int:
+    n = len(arrays[0])
+    if any(len(a) != n for a in arrays[1:]):
+        raise ValueError(f"{what}: column length mismatch {[len(a) for a in arrays]}")
+    return n
 
 
 def _ids(names: Sequence[str], table: dict, what: str) -> np.ndarray:
@@ -91,7 +113,8 @@ class DeviceContext:
     def upload_nodes(self, unsched: np.ndarray, digit: np.ndarray) -> None:
         unsched = np.ascontiguousarray(unsched, np.uint8)
         digit = np.ascontiguousarray(digit, np.int8)
-        self._check(self._lib.msh_upload_nodes(self.handle, len(unsched), N.ptr(unsched), N.ptr(digit)))
+        n = _same_len("upload_nodes", unsched, digit)
+        self._check(self._lib.msh_upload_nodes(self.handle, n, N.ptr(unsched), N.ptr(digit)))
         self.n_nodes = len(unsched)
 
     def patch_nodes(self, idx: np.ndarray, unsched: np.ndarray, digit: np.ndarray) -> None:
@@ -108,7 +131,7 @@ class DeviceContext:
         scores are N.MSH_EXPORT_NONE where none is recorded (msh_export_results)."""
         pod_digit = np.ascontiguousarray(pod_digit, np.int8)
         pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
-        p, n = len(pod_digit), int(self.n_nodes)
+        p, n = _same_len("export_results", pod_digit, pod_tol), int(self.n_nodes)
         filt = np.empty((p, n), np.uint8)
         raw = np.empty((p, n), np.int64)
         fin = np.empty((p, n), np.int64)
@@ -117,25 +140,33 @@ class DeviceContext:
         return filt, raw, fin
 
     # -- host-buffer entry points --
-    def schedule_batch(self, pod_digit: np.ndarray, pod_tol: np.ndarray):
+    @staticmethod
+    def _outputs(p: int, out):
+        if out is None:
+            return np.empty(p, np.int32), np.empty(p, np.int64), np.empty(p, np.int32)
+        idx, score, status = out
+        for a, dt in ((idx, np.int32), (score, np.int64), (status, np.int32)):
+            if a.dtype != dt or len(a) < p or not a.flags["C_CONTIGUOUS"]:
+                raise ValueError("out: (int32 idx, int64 score, int32 status), C-contiguous, >= p entries")
+        return idx, score, status
+
+    def schedule_batch(self, pod_digit: np.ndarray, pod_tol: np.ndarray, out=None):
+        """msh_schedule_batch. `out` = (idx, score, status) arrays to fill (e.g. pinned_empty ones:
+        with page-locked columns and outputs the call copies nothing on the host)."""
         pod_digit = np.ascontiguousarray(pod_digit, np.int8)
         pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
-        p = len(pod_digit)
-        idx = np.empty(p, np.int32)
-        score = np.empty(p, np.int64)
-        status = np.empty(p, np.int32)
+        p = _same_len("schedule_batch", pod_digit, pod_tol)
+        idx, score, status = self._outputs(p, out)
         self._check(self._lib.msh_schedule_batch(self.handle, p, N.ptr(pod_digit), N.ptr(pod_tol),
                                                  N.ptr(idx), N.ptr(score), N.ptr(status)))
         return idx, score, status
 
     def schedule_sequential(self, pod_digit: np.ndarray, pod_tol: np.ndarray, max_pods_per_node: int = 0,
-                            on_commit: Callable[[int, int, int], None] | None = None):
+                            on_commit: Callable[[int, int, int], None] | None = None, out=None):
         pod_digit = np.ascontiguousarray(pod_digit, np.int8)
         pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
-        p = len(pod_digit)
-        idx = np.empty(p, np.int32)
-        score = np.empty(p, np.int64)
-        status = np.empty(p, np.int32)
+        p = _same_len("schedule_sequential", pod_digit, pod_tol)
+        idx, score, status = self._outputs(p, out)
         cb = N.COMMIT_CB(lambda _u, j, i, s: on_commit(j, i, s)) if on_commit else N.COMMIT_CB()
         self._check(self._lib.msh_schedule_sequential(self.handle, p, N.ptr(pod_digit), N.ptr(pod_tol),
                                                       int(max_pods_per_node), N.ptr(idx), N.ptr(score),

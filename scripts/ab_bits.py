@@ -1,7 +1,8 @@
-"""A/B: the bit-sliced batch kernel (default) against the packed-16 kernels (MSH_BATCH_KERNEL=legacy,
-read at msh_create), per-batch time over K back-to-back launches on 1 and 2 HIP streams, several
-BASELINE shapes and normalize modes. Every config's outputs are also compared between the two
-kernels (bit-exact) as a cheap extra check. One JSON line per (config, kernel, streams)."""
+"""A/B of the bit-sliced batch kernel's slice count (MSH_BITS_SLICES, read at msh_create; 0 = the
+launcher's choice): per-batch time over K back-to-back launches on 1 and 2 HIP streams, several
+BASELINE shapes and normalize modes. Outputs of every variant are compared with the default's
+(bit-exact). One JSON line per (config, slices, streams). The packed-16 kernels this replaced
+were measured against it in profiles/ab/r2_ab_bits_vs_legacy.jsonl."""
 import importlib
 import json
 import os
@@ -27,7 +28,6 @@ SLICES = [s for s in os.environ.get("SLICES", "0").split(",")]
 
 
 def make_ctx(kernel, slices, n, norm, weight):
-    os.environ["MSH_BATCH_KERNEL"] = kernel
     os.environ["MSH_BITS_SLICES"] = slices
     ctx = msh.DeviceContext(0)
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
@@ -68,7 +68,7 @@ for n, p, norm, weight in CONFIGS:
                      torch.empty(p, dtype=torch.int32, device=dev), torch.empty(p, dtype=torch.int64, device=dev),
                      torch.empty(p, dtype=torch.int32, device=dev)))
     outs = {}
-    for kernel, sl in [("legacy", "0")] + [("bits", s) for s in SLICES]:
+    for kernel, sl in [("bits", "0")] + [("bits", s) for s in SLICES if s != "0"]:
         ctx = make_ctx(kernel, sl, n, norm, weight)
         for ns in (1, 2):
             timed(ctx, bufs, p, ns, streams)
@@ -78,8 +78,8 @@ for n, p, norm, weight in CONFIGS:
         torch.cuda.synchronize()
         outs[(kernel, sl)] = tuple(t.cpu().numpy() for t in bufs[0][2:])
         ctx.close()
-    ref = outs[("legacy", "0")]
+    ref = outs[("bits", "0")]
     for key, o in outs.items():
         same = all((a == b).all() for a, b in zip(o, ref))
-        print(json.dumps({"check": "same outputs as legacy", "kernel": key[0], "slices": key[1], "nodes": n,
+        print(json.dumps({"check": "same outputs as the default slices", "kernel": key[0], "slices": key[1], "nodes": n,
                           "pods": p, "normalize": norm, "ok": bool(same)}), flush=True)

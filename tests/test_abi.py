@@ -27,7 +27,9 @@ def test_library_exports_every_declared_symbol(msh):
 
 
 def test_abi_version(msh):
-    assert msh._native.lib().msh_abi_version() == 2
+    header = (ROOT / "include" / "minisched_hip.h").read_text()
+    assert f"#define MSH_ABI_VERSION {msh._native.lib().msh_abi_version()}" in header
+    assert msh._native.lib().msh_abi_version() == 3
 
 
 def test_no_device_is_an_error_not_a_fallback(msh):

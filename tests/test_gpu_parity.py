@@ -252,23 +252,61 @@ def test_c4_full_size_batch_and_shards(msh, gpu_ctx, synth):
             c.close()
 
 
-@pytest.mark.parametrize("seq_waves", ["4", "8", "16"])
+@pytest.mark.parametrize("seq_waves", ["0", "1", "4", "16"])
 @pytest.mark.parametrize("max_pods", [0, 1, 3])
-@pytest.mark.parametrize("n", [1, 70, 1000, 5000, 8192, 12288])
-def test_sequential(msh, gpu_ctx, oracle, n, max_pods, seq_waves, monkeypatch):
-    monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)  # read by the launcher at each call
+@pytest.mark.parametrize("n", [1, 70, 1000, 5000, 8192, 8193, 12289, 32768, 40000])
+def test_sequential(msh, oracle, n, max_pods, seq_waves, monkeypatch):
+    """Sequential commit against the oracle's serial loop, node counts included; one scanning wave
+    up to 8,192 nodes, four up to 32,768, then 15 (+ finalizer) / 16 (MSH_SEQ_WAVES, read once by
+    msh_create, forces a count; one too small for the table is raised)."""
+    monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)
     rng = np.random.default_rng(n + max_pods)
     ps = oracle.PluginSet()
-    _set(gpu_ctx, msh, ps)
     u, nd, pd, pt = _rand_case(rng, n, 3000)
+    with msh.DeviceContext(0) as ctx:
+        _set(ctx, msh, ps)
+        ctx.upload_nodes(u, nd)
+        got = ctx.schedule_sequential(pd, pt, max_pods)
+        want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, max_pods)
+        _assert_same(got, (want_i, want_s, want_st), f"seq n={n} max={max_pods} waves={seq_waves}")
+        assert (ctx.node_pod_counts() == want_counts).all()
+        if max_pods == 0:
+            ctx.reset_node_pod_counts()
+            _assert_same(got, ctx.schedule_batch(pd, pt), "seq == batch")
+
+
+@pytest.mark.parametrize("norm", [0, 3])
+def test_sequential_large_tables(msh, gpu_ctx, oracle, norm):
+    """Tables far past the round-1 cap of 12,288 nodes: 300,000 nodes (15 scanning waves x 10 words
+    per lane) without a capacity, 200,000 with one; counts carried over between calls; one node past
+    each register limit is MSH_ERR_UNSUPPORTED, never a silent truncation."""
+    rng = np.random.default_rng(300 + norm)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, norm)
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = _rand_case(rng, 300_000, 1500, p_unsched=0.3)
+    nd[: 250_000][nd[: 250_000] == 7] = 8  # digit 7 only near the end: late first matches
     gpu_ctx.upload_nodes(u, nd)
-    got = gpu_ctx.schedule_sequential(pd, pt, max_pods)
-    want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, max_pods)
-    _assert_same(got, (want_i, want_s, want_st), f"seq n={n} max={max_pods}")
+    got = gpu_ctx.schedule_sequential(pd, pt, 0)
+    want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, 0)
+    _assert_same(got, (want_i, want_s, want_st), "seq 300k")
     assert (gpu_ctx.node_pod_counts() == want_counts).all()
-    if max_pods == 0:
-        gpu_ctx.reset_node_pod_counts()
-        _assert_same(got, gpu_ctx.schedule_batch(pd, pt), "seq == batch")
+    u2, nd2 = u[:200_000], nd[:200_000]
+    gpu_ctx.upload_nodes(u2, nd2)
+    a = gpu_ctx.schedule_sequential(pd[:700], pt[:700], 2)
+    b = gpu_ctx.schedule_sequential(pd[700:], pt[700:], 2)  # continues from the carried counts
+    want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u2, nd2, pd, pt, ps, 2)
+    _assert_same(tuple(np.concatenate([x, y]) for x, y in zip(a, b)), (want_i, want_s, want_st), "seq cap 200k")
+    assert (gpu_ctx.node_pod_counts() == want_counts).all()
+    for n, cap in ((368_641, 0), (262_145, 1)):
+        gpu_ctx.upload_nodes(np.zeros(n, np.uint8), np.zeros(n, np.int8))
+        with pytest.raises(msh.MshError) as ei:
+            gpu_ctx.schedule_sequential(pd[:10], pt[:10], cap)
+        assert ei.value.code == msh._native.MSH_ERR_UNSUPPORTED
+    gpu_ctx.upload_nodes(np.zeros(368_640, np.uint8), np.zeros(368_640, np.int8))
+    got = gpu_ctx.schedule_sequential(pd[:50], pt[:50], 0)
+    _assert_same(got, closed_form(np.zeros(368_640, np.uint8), np.zeros(368_640, np.int8), pd[:50], pt[:50])
+                 if norm == 0 else oracle.c_schedule_batch(np.zeros(368_640, np.uint8), np.zeros(368_640, np.int8),
+                                                           pd[:50], pt[:50], ps), "seq at the limit")
 
 
 def test_sequential_commit_callback(msh, gpu_ctx, oracle):
@@ -396,54 +434,82 @@ def test_maximum_node_table(msh, gpu_ctx, synth):
     _assert_same(gpu_ctx.schedule_batch(pd, pt), closed_form(u[:10], nd[:10], pd, pt), "after reject")
 
 
-@pytest.mark.parametrize("split", ["1", "2", "4", "8", "16"])
+@pytest.mark.parametrize("slices", ["1", "2", "4", "8", "16"])
 @pytest.mark.parametrize("n", [20_000, 70_000])
-def test_node_split_teams(msh, gpu_ctx, oracle, n, split, monkeypatch):
-    """Few pods against a large table: SPLIT waves share each 8-pod unit, each scanning a slice
-    (cut at the 64,512-node compute-tile boundary at 70k nodes), firsts merged in LDS. Every
-    team size against the oracle, for the batch and the shard-key entry points."""
+def test_bits_slices(msh, oracle, n, slices, monkeypatch):
+    """Few pods against a large table: SLICES waves share each 64-pod block, each scanning a range
+    of 256-node groups, firsts merged by min in LDS. Every slice count (MSH_BITS_SLICES, read once
+    by msh_create) against the oracle, for the batch and the shard-key entry points, in the
+    identity-like and the non-match (MINMAX) modes."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_SPLIT", split)
-    rng = np.random.default_rng(n + int(split))
-    ps = oracle.PluginSet()
-    _set(gpu_ctx, msh, ps)
+    monkeypatch.setenv("MSH_BITS_SLICES", slices)
+    rng = np.random.default_rng(n + int(slices))
     u, nd, pd, pt = _rand_case(rng, n, 1500, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4  # digit 3 only in the second half: late first matches
-    gpu_ctx.upload_nodes(u, nd)
-    want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
-    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, f"split={split} n={n}")
     dev = torch.device("cuda:0")
     d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
     p = len(pd)
-    keys = torch.empty(gpu_ctx.shard_keys_len(p), dtype=torch.int32, device=dev)
-    gpu_ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr(),
-                              torch.cuda.current_stream().cuda_stream)
-    oi = torch.empty(p, dtype=torch.int32, device=dev)
-    osc = torch.empty(p, dtype=torch.int64, device=dev)
-    ost = torch.empty(p, dtype=torch.int32, device=dev)
-    gpu_ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), keys.data_ptr(), oi.data_ptr(),
-                               osc.data_ptr(), ost.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"keys split={split} n={n}")
+    with msh.DeviceContext(0) as ctx:
+        for norm in (0, 3):
+            ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, norm)
+            _set(ctx, msh, ps)
+            ctx.upload_nodes(u, nd)
+            want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+            _assert_same(ctx.schedule_batch(pd, pt), want, f"slices={slices} n={n} norm={norm}")
+            keys = torch.empty(ctx.shard_keys_len(p), dtype=torch.int32, device=dev)
+            ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+            oi = torch.empty(p, dtype=torch.int32, device=dev)
+            osc = torch.empty(p, dtype=torch.int64, device=dev)
+            ost = torch.empty(p, dtype=torch.int32, device=dev)
+            ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), keys.data_ptr(), oi.data_ptr(),
+                                   osc.data_ptr(), ost.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want,
+                         f"keys slices={slices} n={n} norm={norm}")
 
 
-@pytest.mark.parametrize("wave_range,wave_xcd", [("1", "1"), ("1", "0"), ("0", "1")])
-@pytest.mark.parametrize("p", [1, 2, 3, 7, 8, 9, 15, 16, 17, 1000, 8191, 65_535, 65_536, 65_537, 100_003, 114_687,
-                               114_689, 131_071, 131_072, 131_073, 140_000, 300_001, 1_000_003])
-def test_wave_ranges(msh, gpu_ctx, oracle, p, wave_range, wave_xcd, monkeypatch):
-    """One contiguous pair range per wave (ragged: r = Q mod W wave ranks take one more pair,
-    odd P leaves a half pair), in rounds of at most 8 pairs (2 rounds past 131,072 pods, 4 and
-    8 rounds at 300k and 1M), on either side of the cuts (4 pairs per wave below 65,536 pods, 7
-    from there, the whole chip from 114,688, 8 at 131,072), against the oracle;
-    MSH_WAVE_RANGE=0 runs the same batches through the work queue. Wave ranks are XCD-contiguous
-    with the extra pairs spread evenly in rank order (default), or interleaved across workgroups
-    with the extra pairs on the first ranks (MSH_WAVE_XCD=0)."""
-    monkeypatch.setenv("MSH_WAVE_RANGE", wave_range)
-    monkeypatch.setenv("MSH_WAVE_XCD", wave_xcd)
+@pytest.mark.parametrize("p", [1, 2, 3, 63, 64, 65, 127, 128, 129, 1000, 8191, 65_535, 65_536, 65_537, 100_003,
+                               131_073, 300_001, 1_000_003])
+def test_ragged_pod_blocks(msh, gpu_ctx, oracle, p):
+    """Pod counts on either side of the 64-pod block and of the slice-count cuts (one block per
+    workgroup; 4, 2 and 1 slice waves as the batch grows), against the oracle."""
     rng = np.random.default_rng(p)
     ps = oracle.PluginSet()
     _set(gpu_ctx, msh, ps)
     u, nd, pd, pt = _rand_case(rng, 5000, p, p_unsched=0.25, p_tol=0.3)
     gpu_ctx.upload_nodes(u, nd)
     want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
-    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, f"wave_range={wave_range} p={p}")
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, f"p={p}")
+
+
+@pytest.mark.parametrize("norm", [0, 3])
+def test_host_buffer_paths(msh, gpu_ctx, oracle, synth, norm):
+    """msh_schedule_batch / msh_schedule_sequential with page-locked buffers (zero-copy: the
+    kernel writes the caller's outputs over PCIe) and with pageable ones (staged), mixed, and a
+    batch large enough for the threaded copy-out: identical to the oracle every time."""
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, norm)
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = synth.make_soa(5000, 100_000)
+    gpu_ctx.upload_nodes(u, nd)
+    want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+    p = len(pd)
+    hpd, hpt = msh.pinned_empty(p, np.int8), msh.pinned_empty(p, np.uint8)
+    hpd[:], hpt[:] = pd, pt
+    outs = (msh.pinned_empty(p, np.int32), msh.pinned_empty(p, np.int64), msh.pinned_empty(p, np.int32))
+    for o in outs:
+        o.fill(-7)
+    got = gpu_ctx.schedule_batch(hpd, hpt, out=outs)
+    assert all(g is o for g, o in zip(got, outs))
+    _assert_same(got, want, "pinned in / pinned out")
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, "pageable in / pageable out")
+    _assert_same(gpu_ctx.schedule_batch(hpd, hpt), want, "pinned in / pageable out")
+    for o in outs:
+        o.fill(-7)
+    _assert_same(gpu_ctx.schedule_batch(pd, pt, out=outs), want, "pageable in / pinned out")
+    gpu_ctx.reset_node_pod_counts()
+    for o in outs:
+        o.fill(-7)
+    got = gpu_ctx.schedule_sequential(hpd[:20_000], hpt[:20_000], 0, out=outs)
+    _assert_same(tuple(g[:20_000] for g in got), tuple(w[:20_000] for w in want[:3]), "sequential pinned")
+    assert (outs[0][20_000:] == -7).all()  # nothing written past p
