@@ -6,12 +6,18 @@ A step = one pass of the hot path (filter -> prescore -> score -> select, i.e.
 minisched/minisched.go:50-87 for every pod of a batch) over one batch of synthetic pods with
 inputs already resident in HBM.
 
-Modes
+Modes (the headline line)
   batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per GPU. With N GPUs the pods
               are sharded (each rank its own 100k batch; no data-path collective) -> weak scaling.
   sequential  BASELINE C5: same sizes, one pod at a time with node-state commits.
-  nodeshard   BASELINE C4 shape: the node table split over the ranks, per-shard best keys
+  nodeshard   BASELINE C4 shape: the node table split over the ranks, per-shard first keys
               merged with an RCCL all-reduce(MAX), then decoded (--nodes 100000 --pods 1000000).
+
+With one GPU, rank 0 also measures the other BASELINE configs and paths after the timed region
+and reports them as extra keys of the same line: C3 with weight 3 + DefaultNormalizeScore, C3 with
+min-max normalisation, C5 sequential, C4 (100k nodes x 1M pods) on one GPU (whole table, and the
+node-shard keys + decode of a one-rank shard), C2, and the host-buffer path (e2e: the C-ABI call a
+cgo caller makes, PCIe included). Every one is checked bit-exact against the closed form.
 
 Launch: `python bench.py` (1 GPU) or
 `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N`.
@@ -35,41 +41,36 @@ sys.path.insert(0, str(ROOT))
 METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
 VALU_PEAK_LANE_OPS = 157.3e12 / 2  # MI355X_MICROARCH.md: FP32 vector peak 157.3 TFLOPS = 2 x lane-ops/s
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# IDENT scan: per node word and pod pair one v_xor_b32 (all-VGPR form), and one
-# v_pk_minimum3_f16 per two words -> 3 wave-instructions per 4 x 64 (pod, node) pairs
-LANE_OPS_PER_EVAL = 0.75
-# measured issue ceiling of exactly that instruction mix (2 x v_xor_b32 v,v + 1 v_pk_minimum3_f16,
-# 8 waves per SIMD): scripts/ubench_valu3.hip -> profiles/r1_ubench_valu3.jsonl
-UBENCH = ROOT / "profiles" / "r1_ubench_valu3.jsonl"
-UBENCH_OP = "v_xor_b32 vv x2 + v_pk_minimum3_f16"
 N_SIMD = 256 * 4
+# Instruction model of bits_kernel's scan (msh_kernels.hip): per pod (lane) and 32-node word,
+# 1 v_and + 4 v_bitop3 (5 VALU), plus one v_bitop3 per two words (the group AND) and a compare +
+# select per 8-word group: 46 VALU per 8 words -> 5.75 wave-instr per 32 x 64 pairs.
+VALU_PER_WORD = 46 / 8
+LANE_OPS_PER_EVAL = VALU_PER_WORD / 32
+PMC_FILE = ROOT / "profiles" / "r2_pmc_c3.json"
+UBENCH = ROOT / "profiles" / "r2_ubench_bitop3.jsonl"
 
 
-def batch_kernel_label(n_nodes, n_pods, shard, cus):
-    """The kernel msh_kernels.hip launch_ident_dyn_t dispatches for this batch (default knobs):
-    one pair range per wave (ident_wave_kernel, 256-thread workgroups; rounds of at most 8
-    pairs) when the table is one 64,512-node compute tile and every wave of the chip gets at
-    most 64 rounds; otherwise the work-queue kernel, in its MULTI form for tables of several
-    tiles."""
-    sh = str(shard).lower()
-    pairs, full = (n_pods + 1) // 2, cus * 32
-    wave_range = os.environ.get("MSH_WAVE_RANGE", "1").strip() not in ("0", "")
-    if wave_range and n_nodes <= 64512 and 0 < pairs <= 8 * 64 * full:
-        waves = min(full, -(-pairs // (4 if pairs < 4 * full else 7)))
-        longest = -(-pairs // waves)
-        rounds = -(-longest // 8)
-        return f"ident_wave_kernel<8, {sh}, {-(-longest // rounds)}, 256>"
-    return f"ident_dyn_kernel<8, {sh}, 1024, false, {str(n_nodes > 64512).lower()}>"
+def bits_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False) -> str:
+    """The kernel msh_kernels.hip launch_batch dispatches (bits_slices' choice of S)."""
+    n_pad = max(-(-n_nodes // 1024) * 1024, 1024)
+    groups = n_pad // 256
+    blocks = -(-n_pods // 64)
+    sl = 1
+    while sl < 16 and blocks * sl < cus * 4 * 6 and groups // (2 * sl) >= 2:
+        sl *= 2
+    keep = -(-groups // sl) <= 8  # KEEP_MAX_GROUPS
+    return f"void msh::bits_kernel<{sl}, {str(kx).lower()}, {str(shard).lower()}, {str(keep).lower()}>"
 
 
-def measured_int_valu_ceiling() -> float | None:
-    """Lane-ops/s of the scan's instruction mix at the best measured occupancy."""
-    try:
-        rows = [json.loads(l) for l in UBENCH.read_text().splitlines() if l.startswith("{")]
-        ipc = max(r["wave_instr_per_simd_cycle@2.4GHz"] for r in rows if r.get("op") == UBENCH_OP)
-        return ipc * 2.4e9 * N_SIMD * 64
-    except Exception:
-        return None
+def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
+    words = max(-(-n_nodes // 1024) * 1024, 1024) // 32
+    rs = lambda nw: -(-words // (nw * 64))
+    nw = 1 if rs(1) <= 4 else 4 if rs(4) <= 4 else (16 if cap else 15)
+    r = rs(nw)
+    rsv = {1: [1, 2, 4], 4: [2, 4]}.get(nw, [4, 8] if cap else [4, 8, 12])
+    r = next(v for v in rsv if r <= v)
+    return f"void msh::seq_kernel<{r}, {nw}, {str(kx).lower()}, {str(cap).lower()}>"
 
 
 def parse():
@@ -82,9 +83,66 @@ def parse():
     ap.add_argument("--pods", type=int, default=None, help="pods per GPU (batch/sequential) or total (nodeshard)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the secondary configs (one GPU only)")
     ap.add_argument("--streams", type=int, default=2,
                     help="batch mode: independent batches pipelined over this many HIP streams")
+    ap.add_argument("--launch", choices=["eager", "graph"], default="eager",
+                    help="batch mode: K host launches, or (A/B) the K timed steps captured as one hipGraph "
+                         "and replayed once; graph replay measured slower on ROCm 7.2 "
+                         "(profiles/ab/r2_sweep_bench.jsonl)")
     return ap.parse_args()
+
+
+def load_json(path: Path):
+    try:
+        return json.loads(path.read_text())
+    except Exception:
+        return None
+
+
+def measured_bitop3_ceiling():
+    """Lane-ops/s of the scan's own instruction forms (v_bitop3_b32 / v_and_b32 with an SGPR
+    source, 8 waves per SIMD), measured by scripts/ubench_valu3.hip."""
+    try:
+        rows = [json.loads(l) for l in UBENCH.read_text().splitlines() if l.startswith("{")]
+        ipc = max(r["wave_instr_per_simd_cycle@2.4GHz"] for r in rows if r.get("op") == "bits scan mix")
+        return ipc * 2.4e9 * N_SIMD * 64
+    except Exception:
+        return None
+
+
+class Streams:
+    """Consecutive independent batches over `ns` HIP streams forked from / joined into the main one."""
+
+    def __init__(self, torch, dev, ns):
+        self.torch = torch
+        self.main = torch.cuda.current_stream(dev)
+        self.all = [self.main] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+
+    def fork(self):
+        ev = self.torch.cuda.Event()
+        ev.record(self.main)
+        for st in self.all[1:]:
+            st.wait_event(ev)
+
+    def join(self):
+        for st in self.all[1:]:
+            ev = self.torch.cuda.Event()
+            ev.record(st)
+            self.main.wait_event(ev)
+
+    def time(self, launch, k: int) -> float:
+        """ms per launch over k launches, launch(i, stream) alternating the streams, HIP events
+        on the main stream around the whole region."""
+        e0, e1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
+        e0.record(self.main)
+        self.fork()
+        for i in range(k):
+            launch(i, self.all[i % len(self.all)].cuda_stream)
+        self.join()
+        e1.record(self.main)
+        self.torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / k
 
 
 def main():
@@ -106,31 +164,27 @@ def main():
         build.build()
     msh = importlib.import_module("mini-kube-scheduler_amd")
     synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
+    D = importlib.import_module("mini-kube-scheduler_amd.distributed")
+    sys.path.insert(0, str(ROOT / "tests"))
+    from closed_form import closed_form_modes  # independent checker, not the oracle
 
     mode = args.mode
-    if mode == "nodeshard":
-        n_total = args.nodes or 100_000
-        p_total = args.pods or 1_000_000
-    else:
-        n_total = args.nodes or 5_000
-        p_total = args.pods or 100_000
+    n_total = args.nodes or (100_000 if mode == "nodeshard" else 5_000)
+    p_total = args.pods or (1_000_000 if mode == "nodeshard" else 100_000)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
 
-    D = importlib.import_module("mini-kube-scheduler_amd.distributed")
     ctx = msh.DeviceContext(local)
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
     unsched, node_digit = synth.make_nodes(n_total)[1:]
     # Batch mode pipelines consecutive, independent batches over `nstreams` HIP streams (each with
-    # its own pod batch and output buffers): a launch reaches the 8 XCDs up to ~4.5 us apart
-    # (scripts/stamps_dyn.py), and on one stream every batch pays that skew plus the slowest XCD's
-    # tail before the next may start. Sequential mode carries node state from batch to batch and
-    # node-shard mode has a collective per step: both stay on one stream.
+    # its own pod and output buffers), so that one launch's ramp and tail overlap the next one's.
+    # Sequential mode carries node state from batch to batch and node-shard mode has a collective
+    # per step: both stay on one stream.
     nstreams = args.streams if mode == "batch" else 1
-    sharded = None
     if mode == "nodeshard":
         sharded = D.NodeShardedScheduler(ctx, unsched, node_digit, world, rank)
         node_base = sharded.shard.lo
-        pod_digit, pod_tol = synth._make_pods_fast(p_total, synth.SEED)[1:]
-        batches = [(pod_digit, pod_tol)]
+        batches = [tuple(synth._make_pods_fast(p_total, synth.SEED)[1:])]
     else:
         ctx.upload_nodes(unsched, node_digit)
         node_base = 0
@@ -150,12 +204,11 @@ def main():
                      "status": torch.empty(p, dtype=torch.int32, device=dev),
                      "keys": torch.zeros(2 * p, dtype=torch.int32, device=dev)})
     klen = ctx.shard_keys_len(p) if mode == "nodeshard" else 0  # int32 keys one step all-reduces
-    main_stream = torch.cuda.current_stream(dev)
-    streams = [main_stream] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
+    S = Streams(torch, dev, nstreams)
 
     def step(k, ev0=None, ev1=None, single=False):
         b = bufs[0] if single else bufs[k % nstreams]
-        st = main_stream if single else streams[k % nstreams]
+        st = S.main if single else S.all[k % nstreams]
         sh = st.cuda_stream
         if ev0 is not None:
             ev0.record(st)
@@ -174,22 +227,10 @@ def main():
             ctx.decode_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["keys"].data_ptr(), b["idx"].data_ptr(),
                                    b["score"].data_ptr(), b["status"].data_ptr(), sh)
 
-    def fork():  # the side streams start after everything already queued on the main stream
-        ev = torch.cuda.Event()
-        ev.record(main_stream)
-        for st in streams[1:]:
-            st.wait_event(ev)
-
-    def join():
-        for st in streams[1:]:
-            ev = torch.cuda.Event()
-            ev.record(st)
-            main_stream.wait_event(ev)
-
-    fork()
+    S.fork()
     for k in range(args.warmup):
         step(k)
-    join()
+    S.join()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -197,21 +238,42 @@ def main():
 
     # Device time from HIP events on the main stream bracketing the whole timed region (side
     # streams fork from / join into it), divided by K: the interval at which batches complete.
-    # No event between launches: an event record is itself a barrier + timestamp packet that
-    # costs ~3.5 us of GPU time and breaks back-to-back dispatch (scripts/host_overhead.py).
+    # No event between launches: an event record is itself a barrier + timestamp packet.
     # Node-shard steps hold an RCCL all-reduce and a decode launch too, so there the shard kernel
     # is bracketed per step.
     per_step = mode == "nodeshard"
     evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
            if per_step else [(None, None)] * args.steps)
+    # Graph launch (batch mode, A/B): the K steps -- the same K launches over the same streams --
+    # captured once, untimed, and replayed once in the timed region.
+    graph = None
+    launch = args.launch if mode == "batch" else "eager"
+    if launch == "graph":
+        graph = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(dev)
+        with torch.cuda.stream(cap):
+            S_cap = Streams(torch, dev, nstreams)  # main = the capture stream, side streams joined by events
+            saved = S.main, S.all
+            S.main, S.all = S_cap.main, S_cap.all
+            with torch.cuda.graph(graph, stream=cap):
+                S.fork()
+                for k in range(args.steps):
+                    step(k)
+                S.join()
+            S.main, S.all = saved
+        torch.cuda.synchronize()
     r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    r0.record(main_stream)
-    fork()
-    for k, (e0, e1) in enumerate(evs):
-        step(k, e0, e1)
-    join()
-    r1.record(main_stream)
+    r0.record(S.main)
+    if graph is not None:
+        with torch.cuda.stream(S.main):
+            graph.replay()
+    else:
+        S.fork()
+        for k, (e0, e1) in enumerate(evs):
+            step(k, e0, e1)
+        S.join()
+    r1.record(S.main)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -226,31 +288,22 @@ def main():
     # stream, which is what rocprofv3's per-kernel average measures.
     kernel_ms_isolated = kernel_ms
     if nstreams > 1:
-        q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        q0.record(main_stream)
-        for k in range(args.steps):
-            step(k, single=True)
-        q1.record(main_stream)
-        torch.cuda.synchronize()
-        kernel_ms_isolated = q0.elapsed_time(q1) / args.steps
+        kernel_ms_isolated = Streams(torch, dev, 1).time(lambda k, sh: step(k, single=True), args.steps)
 
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms, kernel_ms_isolated], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms, kernel_ms_isolated = float(t[0]), float(t[1]), float(t[2])
 
-    # ---- correctness spot-check of every buffer's last batch against the independent closed form ----
+    # ---- correctness of every buffer's last batch against the independent closed form ----
     check = "skipped"
     if rank == 0 and not args.no_check:
-        sys.path.insert(0, str(ROOT / "tests"))
-        from closed_form import closed_form  # independent checker, not the oracle
         ok = True
         for (pod_digit, pod_tol), b in zip(batches, bufs):
-            ci, cs, cst = closed_form(unsched, node_digit, pod_digit, pod_tol)
-            gi, gs, gst = b["idx"].cpu().numpy(), b["score"].cpu().numpy(), b["status"].cpu().numpy()
-            ok = ok and (gi == ci).all() and (gs == cs).all() and (gst == cst).all()
+            want = closed_form_modes(unsched, node_digit, pod_digit, pod_tol)
+            got = (b["idx"].cpu().numpy(), b["score"].cpu().numpy(), b["status"].cpu().numpy())
+            ok = ok and all((g == w).all() for g, w in zip(got, want))
         check = "bit-exact vs closed form" if ok else "MISMATCH"
-    pod_digit, pod_tol = batches[0]
 
     n_local = ctx.n_nodes
     evals_total = float(n_total) * float(p if mode != "nodeshard" else p_total) * args.steps * (world if mode != "nodeshard" else 1)
@@ -258,63 +311,19 @@ def main():
     value = evals_total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # ---- roofline of the dominant kernel, per launch, from HIP events on the launch stream ----
-    kern_s = kernel_ms * 1e-3
-    evals_launch = float(n_local) * p
-    lane_ops = LANE_OPS_PER_EVAL * evals_launch
-    uniq_bytes = 2.0 * n_local + 18.0 * p           # node records + pod records + outputs, once
-    survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts L1/L2 re-reads)
-    traffic = None
-    pmc = ROOT / "profiles" / "pmc_latest.json"
-    if pmc.exists():
-        try:
-            pj = json.loads(pmc.read_text())
-            kj = pj.get("kernels", {}).get(mode, pj if pj.get("mode") == mode else {})
-            if kj.get("nodes") == n_local and kj.get("pods") == p:
-                traffic = kj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    ceiling = measured_int_valu_ceiling()
-    if mode == "sequential":
-        roofline = {
-            "bound": "latency",
-            "achieved": kernel_ms * 1e3 / p, "peak": None, "unit": "us/pod (serial)", "frac": None,
-            "traffic": traffic, "kernel": "seq_kernel", "kernel_ms": kernel_ms,
-            "note": "one pod at a time: scan + 2 wave reductions + 1 workgroup barrier per pod",
-        }
-    else:
-        shard = mode == "nodeshard"
-        kname = batch_kernel_label(n_local, p, shard, torch.cuda.get_device_properties(dev).multi_processor_count)
-        iso_s = kernel_ms_isolated * 1e-3
-        roofline = {
-            "bound": "valu",
-            "achieved": lane_ops / kern_s / 1e9,
-            "peak": VALU_PEAK_LANE_OPS / 1e9,
-            "unit": "Glane-op/s",
-            "frac": lane_ops / kern_s / VALU_PEAK_LANE_OPS,
-            "traffic": traffic,
-            "kernel": kname,
-            "kernel_ms": kernel_ms,
-            "kernel_ms_note": (f"interval at which launches complete with {nstreams} streams in flight; "
-                               "kernel_ms_isolated = the same launches back to back on one stream "
-                               "(= rocprofv3's per-kernel average)") if nstreams > 1 else "one stream",
-            "kernel_ms_isolated": kernel_ms_isolated,
-            "frac_isolated": lane_ops / iso_s / VALU_PEAK_LANE_OPS,
-            "lane_ops_per_eval": LANE_OPS_PER_EVAL,
-            "measured_int_valu_ceiling": ceiling / 1e9 if ceiling else None,
-            "frac_vs_measured_int_ceiling": (lane_ops / kern_s / ceiling) if ceiling else None,
-            "hbm": {"bound": "hbm", "achieved": uniq_bytes / kern_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                    "frac": uniq_bytes / kern_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
-                    "survey_8d_bytes_per_launch": survey_bytes,
-                    "survey_8d_frac": survey_bytes / kern_s / HBM_PEAK},
-        }
+    roofline = make_roofline(mode, n_local, p, kernel_ms, kernel_ms_isolated, nstreams, cus)
+
+    extras = {}
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras = measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus)
 
     cpu = cpu_omp = None
     if rank == 0 and args.cpu_seconds > 0:
+        pod_digit, pod_tol = batches[0]
         cpu = cpu_baseline(unsched, node_digit, pod_digit, pod_tol, args.cpu_seconds, mode)
         if mode != "sequential":
             cpu_omp = cpu_baseline(unsched, node_digit, pod_digit, pod_tol, args.cpu_seconds / 2, mode,
-                                   threads=min(16, os.cpu_count() or 1))
+                                   threads=host_cpu_share())
 
     if rank == 0:
         if mode == "batch":
@@ -335,22 +344,232 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if mode != "nodeshard" else "strong",
             "vs_baseline": None,
-            "dtype": "u32",
+            "dtype": "u32 (bit-sliced: 32 pod-node pairs per lane-op)",
             "data": "synthetic (splitmix64 seed 0x6d696e69: 10% unschedulable nodes, 1% non-digit pods, 5% tolerating)",
             "config": {"workload": wl, "nodes": n_total, "pods_per_step": int(p if mode != "nodeshard" else p_total),
                        "plugins": "filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber w=1]",
                        "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}",
-                       "streams": nstreams},
+                       "streams": nstreams, "launch": launch},
             "pods_per_s": pods_total / elapsed,
             "check": check,
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_omp": cpu_omp,
         }
+        line.update(extras)
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def make_roofline(mode, n_local, p, kernel_ms, kernel_ms_isolated, nstreams, cus):
+    """Roofline of the dominant kernel, per launch, from HIP events on the launch stream; the
+    instruction count from the rocprofv3 PMC passes (profiles/r2_pmc_c3.json) of that same kernel."""
+    kern_s, iso_s = kernel_ms * 1e-3, kernel_ms_isolated * 1e-3
+    pmc = load_json(PMC_FILE) or {}
+    if mode == "sequential":
+        kname = seq_kernel_label(n_local)
+        entry = pmc.get("kernels", {}).get("sequential", {})
+        return {"bound": "latency", "achieved": kernel_ms * 1e3 / p, "peak": None, "unit": "us/pod (serial)",
+                "frac": None, "kernel": kname, "kernel_ms": kernel_ms,
+                "traffic": entry.get("hbm_bytes_per_launch") if entry.get("kernel") == kname else None,
+                "note": "one pod at a time: scan (5 VALU per 32 nodes per lane) + DPP min + commit per pod"}
+    kname = bits_kernel_label(n_local, p, cus, shard=mode == "nodeshard")
+    evals = float(n_local) * p
+    entry = pmc.get("kernels", {}).get("batch", {})
+    pmc_ok = entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
+    model_ops = LANE_OPS_PER_EVAL * evals
+    valu_instr = entry.get("SQ_INSTS_VALU") if pmc_ok else None
+    lane_ops = valu_instr * 64 if valu_instr else model_ops
+    ceiling = measured_bitop3_ceiling()
+    uniq_bytes = 0.75 * n_local + 18.0 * p         # bit planes + pod records + outputs, once
+    survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts L1/L2 re-reads)
+    return {
+        "bound": "valu",
+        "achieved": lane_ops / kern_s / 1e9,
+        "peak": VALU_PEAK_LANE_OPS / 1e9,
+        "unit": "Glane-op/s",
+        "frac": lane_ops / kern_s / VALU_PEAK_LANE_OPS,
+        "traffic": entry.get("hbm_bytes_per_launch") if pmc_ok else None,
+        "kernel": kname,
+        "kernel_ms": kernel_ms,
+        "kernel_ms_note": (f"interval at which launches complete with {nstreams} streams in flight; "
+                           "kernel_ms_isolated = the same launches back to back on one stream "
+                           "(= rocprofv3's per-kernel average)") if nstreams > 1 else "one stream",
+        "kernel_ms_isolated": kernel_ms_isolated,
+        "frac_isolated": lane_ops / iso_s / VALU_PEAK_LANE_OPS,
+        "lane_ops_source": "rocprofv3 SQ_INSTS_VALU x 64 per launch (profiles/r2_pmc_c3.json)" if valu_instr
+                           else "instruction model (no matching PMC file)",
+        "valu_lane_ops_per_eval_measured": valu_instr * 64 / evals if valu_instr else None,
+        "valu_lane_ops_per_eval_model": LANE_OPS_PER_EVAL,
+        "scan_share_of_valu": model_ops / lane_ops if valu_instr else None,
+        "measured_bitop3_ceiling": ceiling / 1e9 if ceiling else None,
+        "frac_vs_measured_bitop3_ceiling": (lane_ops / kern_s / ceiling) if ceiling else None,
+        "hbm": {"bound": "hbm", "achieved": uniq_bytes / kern_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": uniq_bytes / kern_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
+                "survey_8d_bytes_per_launch": survey_bytes,
+                "survey_8d_frac": survey_bytes / kern_s / HBM_PEAK,
+                "survey_8d_note": "2 B per pair counts every L1/L2/SGPR re-read of the node table as HBM "
+                                  "traffic; the 4 KB table is read from HBM once per launch"},
+    }
+
+
+def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
+    """Secondary BASELINE configs and the host-buffer path, each timed and checked bit-exact."""
+    out = {}
+
+    def dbufs(pd, pt):
+        p = len(pd)
+        return [torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev), torch.empty(p, dtype=torch.int32, device=dev),
+                torch.empty(p, dtype=torch.int64, device=dev), torch.empty(p, dtype=torch.int32, device=dev)]
+
+    def got(b):
+        return tuple(t.cpu().numpy() for t in b[2:])
+
+    def same(a, b):
+        return all((x == y).all() for x, y in zip(a, b))
+
+    S2 = Streams(torch, dev, 2)
+
+    def batch_rate(ctx, n, pairs, k, norm=0, weight=1):
+        """ms per batch of k launches over 2 streams (2 independent pod batches)."""
+        bs = [dbufs(*pp) for pp in pairs]
+        p = len(pairs[0][0])
+        launch = lambda i, sh: ctx.schedule_batch_device(p, *[t.data_ptr() for t in bs[i % 2]], sh)
+        S2.time(launch, 4)
+        ms = S2.time(launch, k)
+        ok = all(same(got(b), closed_form_modes(*ctx_nodes[ctx], pp[0], pp[1], weight, norm)) for b, pp in zip(bs, pairs))
+        return ms, ok
+
+    ctx_nodes = {}
+    # ---- C3 (5k x 100k): weight 3 + DefaultNormalizeScore, and min-max (north_star stage 3) ----
+    n, p = 5000, 100_000
+    u, nd = synth.make_nodes(n)[1:]
+    pd_all, pt_all = synth._make_pods_fast(2 * p, synth.SEED)[1:]
+    pairs = [(np.ascontiguousarray(pd_all[:p]), np.ascontiguousarray(pt_all[:p])),
+             (np.ascontiguousarray(pd_all[p:]), np.ascontiguousarray(pt_all[p:]))]
+    ctx = msh.DeviceContext(dev.index or 0)
+    ctx.upload_nodes(u, nd)
+    ctx_nodes[ctx] = (u, nd)
+    variants = {}
+    for name, weight, norm in (("weight3_default_normalize", 3, 1), ("minmax_normalize", 1, 3),
+                               ("reverse_normalize", 1, 2)):
+        ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                        [msh.ScorePluginConfig(msh.NODE_NUMBER, weight, msh.Normalize(norm))])
+        ms, ok = batch_rate(ctx, n, pairs, 100, norm, weight)
+        variants[name] = {"kernel": bits_kernel_label(n, p, cus, kx=norm in (2, 3)), "ms_per_step": ms,
+                          "evals_per_s": n * p / (ms * 1e-3), "streams": 2,
+                          "check": "bit-exact vs closed form" if ok else "MISMATCH"}
+    out["c3_normalize_variants"] = variants
+    ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+
+    # ---- e2e: the host-buffer C-ABI call (msh_schedule_batch), PCIe in and out ----
+    pd, pt = pairs[0]
+    want = closed_form_modes(u, nd, pd, pt)
+    hpd, hpt = msh.pinned_empty(p, np.int8), msh.pinned_empty(p, np.uint8)
+    hpd[:], hpt[:] = pd, pt
+    e2e = {}
+    for name, args, outs in (("pinned", (hpd, hpt), (msh.pinned_empty(p, np.int32), msh.pinned_empty(p, np.int64),
+                                                       msh.pinned_empty(p, np.int32))),
+                             ("pageable", (pd, pt), (np.empty(p, np.int32), np.empty(p, np.int64), np.empty(p, np.int32)))):
+        for _ in range(5):
+            ctx.schedule_batch(*args, out=outs)
+        ts = []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            ctx.schedule_batch(*args, out=outs)
+            ts.append(time.perf_counter() - t0)
+        us = float(np.median(ts)) * 1e6
+        e2e[name] = {"us_per_batch": us, "pods_per_s": p / (us * 1e-6), "evals_per_s": n * p / (us * 1e-6),
+                     "check": "bit-exact vs closed form" if same(outs, want) else "MISMATCH"}
+    e2e["note"] = ("msh_schedule_batch from host buffers, synchronous, median of 50 calls (C3): the kernel "
+                   "reads the pod columns from and writes the outputs into page-locked host memory over PCIe; "
+                   "'pinned' = buffers from msh_host_alloc (no host copy), 'pageable' = numpy arrays (staged "
+                   "through the ctx's page-locked buffer, copies split over host threads)")
+    out["e2e"] = e2e
+
+    # ---- C5: 5k x 100k sequential commit (one launch = the whole 100k-pod batch) ----
+    b = dbufs(pd, pt)
+    s1 = Streams(torch, dev, 1)
+    seq = lambda i, sh: ctx.schedule_sequential_device(p, b[0].data_ptr(), b[1].data_ptr(), 0, *[t.data_ptr() for t in b[2:]], sh)
+    s1.time(seq, 1)
+    ctx.reset_node_pod_counts()
+    ms = s1.time(seq, 3)
+    counts = ctx.node_pod_counts()
+    g = got(b)
+    placed = g[2] == 0
+    ok = same(g, want) and (counts == 3 * np.bincount(g[0][placed], minlength=n)).all()
+    out["c5_sequential"] = {"kernel": seq_kernel_label(n), "ms_per_step": ms, "us_per_pod": ms * 1e3 / p,
+                            "pods_per_s": p / (ms * 1e-3), "evals_per_s": n * p / (ms * 1e-3),
+                            "check": ("seq == batch (closed form), node counts == 3 x placements" if ok else "MISMATCH")}
+    ctx.close()
+
+    # ---- C2: 1k x 10k ----
+    n2, p2 = 1000, 10_000
+    u2, nd2 = synth.make_nodes(n2)[1:]
+    pd2, pt2 = synth._make_pods_fast(2 * p2, synth.SEED)[1:]
+    ctx = msh.DeviceContext(dev.index or 0)
+    ctx.upload_nodes(u2, nd2)
+    ctx_nodes[ctx] = (u2, nd2)
+    ms, ok = batch_rate(ctx, n2, [(np.ascontiguousarray(pd2[:p2]), np.ascontiguousarray(pt2[:p2])),
+                                  (np.ascontiguousarray(pd2[p2:]), np.ascontiguousarray(pt2[p2:]))], 100)
+    out["c2"] = {"kernel": bits_kernel_label(n2, p2, cus), "ms_per_step": ms, "evals_per_s": n2 * p2 / (ms * 1e-3),
+                 "streams": 2, "check": "bit-exact vs closed form" if ok else "MISMATCH"}
+    ctx.close()
+
+    # ---- C4 on one GPU: 100k nodes x 1M pods, whole table, and one-rank node-shard keys + decode ----
+    n4, p4 = 100_000, 1_000_000
+    u4, nd4 = synth.make_nodes(n4)[1:]
+    pd4, pt4 = synth._make_pods_fast(p4, synth.SEED)[1:]
+    want4 = closed_form_modes(u4, nd4, pd4, pt4)
+    ctx = msh.DeviceContext(dev.index or 0)
+    ctx.upload_nodes(u4, nd4)
+    b4 = dbufs(pd4, pt4)
+    launch = lambda i, sh: ctx.schedule_batch_device(p4, *[t.data_ptr() for t in b4], sh)
+    s1.time(launch, 1)
+    ms_b = s1.time(launch, 5)
+    ok_b = same(got(b4), want4)
+    keys = torch.empty(ctx.shard_keys_len(p4), dtype=torch.int32, device=dev)
+
+    def shard_step(i, sh):
+        ctx.shard_keys_device(p4, b4[0].data_ptr(), b4[1].data_ptr(), 0, keys.data_ptr(), sh)
+        D.merge_shard_keys_(keys)  # world 1: no collective
+        ctx.decode_keys_device(p4, b4[0].data_ptr(), b4[1].data_ptr(), keys.data_ptr(), *[t.data_ptr() for t in b4[2:]], sh)
+
+    for t in b4[2:]:
+        t.fill_(-7)
+    s1.time(shard_step, 1)
+    ms_s = s1.time(shard_step, 5)
+    ok_s = same(got(b4), want4)
+    out["c4_one_gpu"] = {
+        "batch": {"kernel": bits_kernel_label(n4, p4, cus), "ms_per_step": ms_b, "evals_per_s": n4 * p4 / (ms_b * 1e-3),
+                  "check": "bit-exact vs closed form" if ok_b else "MISMATCH"},
+        "node_shard_keys_plus_decode": {"kernel": bits_kernel_label(n4, p4, cus, shard=True), "ms_per_step": ms_s,
+                                        "evals_per_s": n4 * p4 / (ms_s * 1e-3),
+                                        "check": "bit-exact vs closed form" if ok_s else "MISMATCH"},
+        "note": "one GPU holds the whole 100k-node table (75 KB of bit planes); the 8-GPU C4 run splits it "
+                "(bench.py --mode nodeshard)"}
+    ctx.close()
+    return out
+
+
+def host_cpu_share() -> int:
+    """Host threads this process may use: its CPU affinity, capped by OMP_NUM_THREADS when the
+    machine sets it (the GPU pool gives a one-GPU job a share of the host: 16 CPUs)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(env))) if env.isdigit() else n
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode: str, threads: int = 1):
@@ -377,9 +596,9 @@ def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode:
     evals = float(n) * done
     return {"value": evals / t, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
             "sample": f"{done} pods (cycling over the {p}-pod batch) x {n} nodes, C restatement "
-                      f"({'scalar' if threads == 1 else f'OpenMP {threads} threads'}), {t:.2f} s; "
-                      f"{os.cpu_count()} host CPUs visible",
-            "pods_per_s": done / t}
+                      f"({'scalar' if threads == 1 else f'OpenMP {threads} threads'}), {t:.2f} s",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "host_cpu_share": host_cpu_share(), "pods_per_s": done / t}
 
 
 if __name__ == "__main__":

@@ -7,11 +7,13 @@
 // device is an error (MSH_ERR_NO_DEVICE).
 //
 // Host-buffer entry points (msh_schedule_batch / msh_schedule_sequential), the path a cgo caller
-// takes: the pod columns go to device scratch by DMA; the kernel writes idx / score / status
-// straight into page-locked host memory (zero-copy over PCIe, no copy after the kernel). When the
-// caller's buffers are page-locked (msh_host_alloc, or registered with HIP) they are used as they
-// are; otherwise the ctx stages through its own page-locked buffer, and the copies between the
-// caller's memory and the stage are split over a small pool of host threads.
+// takes: the kernel reads the pod columns from and writes idx / score / status into page-locked
+// host memory over PCIe (zero-copy: no DMA command and no copy after the kernel; measured at C3,
+// 56.6 us per 100k-pod call against 73 us with the columns DMA'd and 97 us with everything DMA'd,
+// profiles/ab/r2_e2e_host2.jsonl). When the caller's buffers are page-locked (msh_host_alloc, or
+// registered with HIP) they are used as they are; otherwise the ctx stages through its own
+// page-locked buffer, and the copies between the caller's memory and the stage are split over a
+// small pool of host threads.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -152,6 +154,7 @@ struct msh_ctx {
   size_t stage_cap = 0;
   unsigned char* h_stage = nullptr;  // page-locked: digit p | tol p | idx 4p | score 8p | status 4p
   CopyPool* pool = nullptr;
+  hipEvent_t done_ev = nullptr;  // MSH_HOST_SYNC=poll
   size_t patch_cap = 0;
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
   int32_t patch_pending = 0;              // entries in d_patch the next prepare() applies
@@ -314,10 +317,9 @@ struct DeviceGuard {
   explicit DeviceGuard(int d) { (void)hipSetDevice(d); }
 };
 
-// Host-buffer I/O of one synchronous call: pod columns DMA'd into device scratch; the outputs
-// written by the kernel straight into page-locked host memory (default), or (MSH_HOST_IO=dma at
-// msh_create, A/B) into device scratch and copied there by DMA; then, for a pageable caller,
-// copied from the stage into the caller's arrays.
+// Host-buffer I/O of one synchronous call: pod columns and outputs in page-locked host memory,
+// read and written by the kernel (default; the A/B modes of DeviceInfo DMA them through device
+// scratch); then, for a pageable caller, outputs copied from the stage into the caller's arrays.
 struct HostIO {
   int8_t* d_pd = nullptr;
   uint8_t* d_pt = nullptr;
@@ -345,14 +347,21 @@ int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t*
     if ((rc = ensure_stage(c, p)) != MSH_OK) return rc;
   }
   const StageLayout L((size_t)p);
-  if (in_pinned) {  // DMA straight from the caller's page-locked columns
-    MSH_HIP(c, hipMemcpyAsync(c->d_pd, pod_digit, (size_t)p, hipMemcpyHostToDevice, c->stream));
-    MSH_HIP(c, hipMemcpyAsync(c->d_pt, pod_tol, (size_t)p, hipMemcpyHostToDevice, c->stream));
-  } else {  // through the stage
+  const int8_t* src_pd = pod_digit;
+  const uint8_t* src_pt = pod_tol;
+  if (!in_pinned) {  // through the stage
     const CopyJob jobs[2] = {{c->h_stage + L.pd, pod_digit, (size_t)p}, {c->h_stage + L.pt, pod_tol, (size_t)p}};
     par_copy(c->pool, jobs, 2);
-    MSH_HIP(c, hipMemcpyAsync(c->d_pd, c->h_stage + L.pd, (size_t)p, hipMemcpyHostToDevice, c->stream));
-    MSH_HIP(c, hipMemcpyAsync(c->d_pt, c->h_stage + L.pt, (size_t)p, hipMemcpyHostToDevice, c->stream));
+    src_pd = reinterpret_cast<const int8_t*>(c->h_stage + L.pd);
+    src_pt = c->h_stage + L.pt;
+  }
+  if (c->dev.host_io_zc_in) {  // the kernel reads the page-locked columns itself
+    io.d_pd = static_cast<int8_t*>(pinned_device_ptr(src_pd));
+    io.d_pt = static_cast<uint8_t*>(pinned_device_ptr(src_pt));
+    if (!io.d_pd || !io.d_pt) return fail(c, MSH_ERR_HIP, "page-locked pod columns without a device address");
+  } else {  // DMA into device scratch
+    MSH_HIP(c, hipMemcpyAsync(c->d_pd, src_pd, (size_t)p, hipMemcpyHostToDevice, c->stream));
+    MSH_HIP(c, hipMemcpyAsync(c->d_pt, src_pt, (size_t)p, hipMemcpyHostToDevice, c->stream));
   }
   if (io.staged) {
     io.h_idx = reinterpret_cast<int32_t*>(c->h_stage + L.idx);
@@ -384,7 +393,15 @@ int host_io_end(msh_ctx* c, int32_t p, int32_t* out_idx, int64_t* out_score, int
     MSH_HIP(c, hipMemcpyAsync(io.h_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     MSH_HIP(c, hipMemcpyAsync(io.h_status, c->d_ost, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   }
-  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  if (c->dev.host_sync_poll) {
+    if (!c->done_ev) MSH_HIP(c, hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming));
+    MSH_HIP(c, hipEventRecord(c->done_ev, c->stream));
+    hipError_t q;
+    while ((q = hipEventQuery(c->done_ev)) == hipErrorNotReady) std::this_thread::yield();
+    if (q != hipSuccess) return hip_fail(c, q, "hipEventQuery");
+  } else {
+    MSH_HIP(c, hipStreamSynchronize(c->stream));
+  }
   if (io.staged) {
     const CopyJob jobs[3] = {{out_idx, io.h_idx, (size_t)p * sizeof(int32_t)},
                              {out_score, io.h_score, (size_t)p * sizeof(int64_t)},
@@ -440,7 +457,11 @@ int msh_create(int device, msh_ctx** out_ctx) {
   // test / A-B switches, read once here (never on a launch path)
   if (const char* e = getenv("MSH_BITS_SLICES")) c->dev.bits_slices = atoi(e);
   if (const char* e = getenv("MSH_SEQ_WAVES")) c->dev.seq_waves = atoi(e);
-  if (const char* e = getenv("MSH_HOST_IO")) c->dev.host_io_dma = strcmp(e, "dma") == 0;
+  if (const char* e = getenv("MSH_HOST_IO")) {
+    c->dev.host_io_dma = strcmp(e, "dma") == 0;
+    c->dev.host_io_zc_in = strcmp(e, "dma") != 0 && strcmp(e, "zc") != 0;
+  }
+  if (const char* e = getenv("MSH_HOST_SYNC")) c->dev.host_sync_poll = strcmp(e, "poll") == 0;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return MSH_ERR_HIP;
@@ -469,6 +490,7 @@ void msh_destroy(msh_ctx* c) {
   // launches queued on caller streams (the *_device entry points) may still read the tables
   (void)hipDeviceSynchronize();
   delete c->pool;
+  if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   free_nodes(c);
   free_pods(c);
   (void)hipHostFree(c->h_stage);

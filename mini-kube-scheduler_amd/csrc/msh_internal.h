@@ -38,7 +38,12 @@ struct DeviceInfo {
   int cus = 256;
   int bits_slices = 0;   // tests / A-B only (MSH_BITS_SLICES at msh_create): slice waves per pod block, 0 = auto
   int seq_waves = 0;     // tests / A-B only (MSH_SEQ_WAVES at msh_create): sequential scanning waves, 0 = auto
-  int host_io_dma = 0;   // A/B only (MSH_HOST_IO=dma at msh_create): host-buffer outputs by DMA, not zero-copy
+  // Host-buffer calls (msh_schedule_batch / _sequential): the kernel reads the pod columns from and
+  // writes the outputs to page-locked host memory (default). A/B only, MSH_HOST_IO at msh_create:
+  // "dma" = columns and outputs DMA'd through device scratch, "zc" = columns DMA'd, outputs zero-copy.
+  int host_io_dma = 0;
+  int host_io_zc_in = 1;
+  int host_sync_poll = 0;  // A/B only (MSH_HOST_SYNC=poll): poll an event instead of hipStreamSynchronize
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit

@@ -35,29 +35,6 @@ namespace msh {
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
-template <bool IS_MIN, int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp_step(uint32_t v) {
-  // Lanes whose row is masked off keep `old`: the identity of the reduction.
-  const int ident = IS_MIN ? -1 : 0;
-  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(ident, (int)v, CTRL, ROW_MASK, 0xF, false);
-  return IS_MIN ? umin(v, t) : umax(v, t);
-}
-
-// Wave-wide unsigned max (IS_MIN=false) / min (IS_MIN=true); result is wave-uniform.
-template <bool IS_MIN>
-__device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
-  v = dpp_step<IS_MIN, 0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
-  v = dpp_step<IS_MIN, 0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
-  v = dpp_step<IS_MIN, 0x141, 0xF>(v);  // row_half_mirror
-  v = dpp_step<IS_MIN, 0x140, 0xF>(v);  // row_mirror   -> each 16-lane row holds its result
-  v = dpp_step<IS_MIN, 0x142, 0xA>(v);  // row_bcast:15 -> rows 1,3 fold in rows 0,2
-  v = dpp_step<IS_MIN, 0x143, 0xC>(v);  // row_bcast:31 -> rows 2,3 fold in row 1 (= rows 0..1)
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return wave_reduce<false>(v); }
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return wave_reduce<true>(v); }
-
 // ---------------------------------------------------------------------------------------
 // Stage 1: node table preparation + feasibility bitmask (once per upload / plugin change).
 // For the only filter, NodeUnschedulable (upstream v1.22.0), feasibility depends on the pod
@@ -232,6 +209,13 @@ __device__ __forceinline__ uint32_t or_xor_s(uint32_t t, uint32_t d, uint32_t p)
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xf6" : "=v"(r) : "v"(t), "s"(d), "v"(p));
   return r;
 }
+// x & m in one v_and_b32, x wave-uniform (SGPR), m a per-lane mask: left to itself the backend
+// rewrites `x & (tol ? 0 : ~0)` as v_mov + v_cndmask on the lane condition, two VALU per word.
+__device__ __forceinline__ uint32_t and_s(uint32_t x, uint32_t m) {
+  uint32_t r;
+  asm("v_and_b32_e32 %0, %1, %2" : "=v"(r) : "s"(x), "v"(m));
+  return r;
+}
 // ~dm | xi | ~v (truth table over S0 = dm, S1 = xi, S2 = v), v wave-uniform
 __device__ __forceinline__ uint32_t nmiss_s(uint32_t dm, uint32_t xi, uint32_t v) {
   uint32_t r;
@@ -288,7 +272,25 @@ __device__ __forceinline__ uint32_t group_first(const uint32_t* __restrict__ pla
   return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
 }
 
-template <int S, bool KX, bool SHARD>
+// The first node with a zero bit among the 8 kept miss words of group g (words ascend in List
+// order, and bits within a word): descending selects, then the lowest zero bit.
+__device__ __forceinline__ uint32_t kept_first(const uint32_t (&k)[PLANE_GW], uint32_t g) {
+  uint32_t bw = 0;
+  int32_t bj = 0;
+#pragma unroll
+  for (int c = PLANE_GW - 1; c >= 0; --c) {
+    const uint32_t hit = ~k[c];
+    bj = hit ? c : bj;
+    bw = hit ? hit : bw;
+  }
+  return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
+}
+
+// KEEP (short slices): the miss words of the first group with a hit are kept in registers as the
+// scan passes (8 v_cndmask per group), instead of re-reading that group's planes afterwards
+// (group_first: ten 16-byte loads per lane and ~100 VALU, a memory round trip at the end of every
+// wave, where little else is left to overlap it).
+template <int S, bool KX, bool SHARD, bool KEEP>
 __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
   __shared__ uint32_t s_res[S][KX ? 2 : 1][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -306,6 +308,9 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
   const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
   const int32_t g_lo = min(s * a.gps, a.n_groups), g_hi = min(g_lo + a.gps, a.n_groups);
   uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group with a feasible match / non-match
+  uint32_t km[PLANE_GW], kx[PLANE_GW];     // KEEP: that group's miss words
+#pragma unroll
+  for (int c = 0; c < PLANE_GW; ++c) km[c] = kx[c] = 0xFFFFFFFFu;
   constexpr int NPL = KX ? PLANE_N : PLANE_V;  // planes the scan reads
   for (int32_t g = g_hi - 1; g >= g_lo; --g) {
     // the group's planes, wave-uniform: one s_load_dwordx8 per plane, all in flight together,
@@ -319,13 +324,14 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
 #pragma unroll
       for (int c = 0; c < PLANE_GW; ++c) pg[k * PLANE_GW + c] = pl[k][c];
     uint32_t am = 0xFFFFFFFFu, ax = 0xFFFFFFFFu;
+    uint32_t gm[PLANE_GW], gx[PLANE_GW];
 #pragma unroll
     for (int w = 0; w < PLANE_GW; w += 2) {
       uint32_t mm[2], mx[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int c = w + q;
-        const uint32_t xi = pg[PLANE_X * PLANE_GW + c] & nT;
+        const uint32_t xi = and_s(pg[PLANE_X * PLANE_GW + c], nT);
         if constexpr (KX) {
           uint32_t dm = pg[c] ^ P0;
           dm = or_xor_s(dm, pg[PLANE_GW + c], P1);
@@ -342,13 +348,30 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
       }
       am &= mm[0] & mm[1];
       if constexpr (KX) ax &= mx[0] & mx[1];
+      gm[w] = mm[0];
+      gm[w + 1] = mm[1];
+      gx[w] = mx[0];
+      gx[w + 1] = mx[1];
     }
-    fm = am != 0xFFFFFFFFu ? (uint32_t)g : fm;
-    if constexpr (KX) fx = ax != 0xFFFFFFFFu ? (uint32_t)g : fx;
+    const bool hm = am != 0xFFFFFFFFu, hx = KX && ax != 0xFFFFFFFFu;
+    fm = hm ? (uint32_t)g : fm;
+    if constexpr (KX) fx = hx ? (uint32_t)g : fx;
+    if constexpr (KEEP) {
+#pragma unroll
+      for (int c = 0; c < PLANE_GW; ++c) {
+        km[c] = hm ? gm[c] : km[c];
+        if constexpr (KX) kx[c] = hx ? gx[c] : kx[c];
+      }
+    }
   }
   uint32_t rm = NOFIT, rx = NOFIT;  // node index of the first feasible match / non-match
-  if (fm != NO_GROUP) rm = group_first<false>(a.planes, fm, P0, P1, P2, P3, nT);
-  if (KX && fx != NO_GROUP) rx = group_first<true>(a.planes, fx, P0, P1, P2, P3, nT);
+  if constexpr (KEEP) {
+    if (fm != NO_GROUP) rm = kept_first(km, fm);
+    if (KX && fx != NO_GROUP) rx = kept_first(kx, fx);
+  } else {
+    if (fm != NO_GROUP) rm = group_first<false>(a.planes, fm, P0, P1, P2, P3, nT);
+    if (KX && fx != NO_GROUP) rx = group_first<true>(a.planes, fx, P0, P1, P2, P3, nT);
+  }
   if constexpr (S > 1) {
     s_res[s][0][lane] = rm;
     if constexpr (KX) s_res[s][1][lane] = rx;
@@ -402,11 +425,12 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
 // ---------------------------------------------------------------------------------------
 // Sequential-commit kernel (BASELINE C5) on the bit-sliced table: ONE workgroup walks the pods
 // in order, one pod at a time, and commits each placement before the next pod is decided.
-// Word w of the table lives in registers: lane w % 64 of wave (w / 64) % NW, slot (w / 64) / NW
-// (RS slots per lane), all six planes, plus a FULL plane with a capacity. Per pod (its code bits
-// and class are wave-uniform here), every lane evaluates its words (5 VALU per 32 pairs), turns
-// its first hit into a node index (v_ffbl_b32: the lowest set bit, all-ones when there is none),
-// and the wave takes the minimum with DPP. NW > 1 waves meet in a triple-buffered LDS slot
+// Word w of the table lives in registers: q = w / RS, lane q % 64 of wave q / 64, slot w % RS (RS
+// consecutive words per lane, lanes and waves in List order), all six planes, plus a FULL plane
+// with a capacity. Per pod (its code bits and class are wave-uniform here), every lane evaluates
+// its words (5 VALU per 32 pairs), turns its first hit into a node index (v_ffbl_b32: the lowest
+// set bit, all-ones when there is none), and the wave's first is its first lane with a hit
+// (wave_first). NW > 1 waves meet in a triple-buffered LDS slot
 // (atomic min) behind one LDS-only barrier. Then decode, output and commit: the node's pod count
 // (an LDS table when it fits, device memory otherwise) and, with max_pods_per_node, the owning
 // lane sets the node's FULL bit once the count reaches it, so later pods see it infeasible.
@@ -422,6 +446,14 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// The wave's smallest value when lanes hold ascending, disjoint ranges (lane l's candidates all
+// precede lane l + 1's): the first lane that has one. One ballot, s_ff1 and a readlane instead of a
+// 6-step DPP reduction on the per-pod critical path.
+__device__ __forceinline__ uint32_t wave_first(uint32_t v) {
+  const unsigned long long m = __ballot(v != 0xFFFFFFFFu);
+  return m ? (uint32_t)__builtin_amdgcn_readlane((int)v, __builtin_ctzll(m)) : 0xFFFFFFFFu;
 }
 
 // Lowest set bit (v_ffbl_b32): 0xFFFFFFFF when x == 0, so (base | ffbl(x)) is "no node" then.
@@ -447,7 +479,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   uint32_t D0[RS], D1[RS], D2[RS], D3[RS], XX[RS], VV[RS], FULL[RS];
 #pragma unroll
   for (int r = 0; r < RS; ++r) {
-    const int32_t w = (r * NW + wv) * WAVE + lane;
+    const int32_t w = (wv * WAVE + lane) * RS + r;
     D0[r] = D1[r] = D2[r] = D3[r] = 0xFFFFFFFFu;  // code 15: never a match
     XX[r] = 0u;
     VV[r] = 0u;
@@ -499,7 +531,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   const uint32_t ball1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.ball[1]);
   int32_t* counts = a.counts;
   const IdentDecode idec = make_ident_decode(pp);
-  const uint32_t lane_base = (uint32_t)(wv * WAVE + lane) << 5;  // node index of bit 0 of slot 0's word
+  const uint32_t lane_base = (uint32_t)((wv * WAVE + lane) * RS) << 5;  // node index of bit 0 of slot 0's word
   uint32_t pcv = CODE_NONE_POD, tolv = 0;
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
@@ -529,17 +561,17 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     uint32_t cm = NONE, ca = NONE, cx = NONE;  // this lane's first match / feasible / non-match
     if (scanner) {
 #pragma unroll
-      for (int r = RS - 1; r >= 0; --r) {  // slots ascend in List order per lane: the last hit is the first
+      for (int r = RS - 1; r >= 0; --r) {  // slots ascend in List order per lane
         const uint32_t dm = (D0[r] ^ p0) | (D1[r] ^ p1) | (D2[r] ^ p2) | (D3[r] ^ p3);
         const uint32_t bad = (XX[r] & nT) | (CAP ? FULL[r] : 0u);
-        const uint32_t base = lane_base + (uint32_t)(r * NW * WAVE * 32);
+        const uint32_t base = lane_base + (uint32_t)(r * 32);
         cm = umin(cm, base | ffbl(~(dm | bad)));
         if (CAP) ca = umin(ca, base | ffbl(VV[r] & ~bad));
         if (KX) cx = umin(cx, base | ffbl(VV[r] & ~bad & dm));
       }
-      cm = wave_min_u32(cm);
-      if (CAP) ca = wave_min_u32(ca);
-      if (KX) cx = wave_min_u32(cx);
+      cm = wave_first(cm);
+      if (CAP) ca = wave_first(ca);
+      if (KX) cx = wave_first(cx);
     }
     if constexpr (NW > 1) {
       // lane 0 of every scanning wave folds its wave's result into this pod's slot; after the
@@ -586,16 +618,16 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
           else atomicAdd(&counts[sel], 1);
         }
       } else {
-        const uint32_t w = (uint32_t)sel >> 5;
-        if ((int)((w / WAVE) % NW) == wv) {  // the owning wave
+        const uint32_t w = (uint32_t)sel >> 5, q = w / RS;
+        if ((int)(q / WAVE) == wv) {  // the owning wave
           int32_t old = 0;
           if (lane == 0) old = lds_counts ? atomicAdd(&lcnt[sel], 1) : atomicAdd(&counts[sel], 1);
           const bool full = __builtin_amdgcn_readfirstlane(old) + 1 >= max_pods;
           if (full) {
             // the owning lane: the register by a wave-uniform index (scalar branches), the lane by
             // a compare
-            const int rs = (int)((w / WAVE) / NW);
-            const uint32_t bit = (lane == (int)(w % WAVE)) ? (1u << (sel & 31)) : 0u;
+            const int rs = (int)(w % RS);
+            const uint32_t bit = (lane == (int)(q % WAVE)) ? (1u << (sel & 31)) : 0u;
 #pragma unroll
             for (int r = 0; r < RS; ++r)
               if (r == rs) FULL[r] |= bit;
@@ -728,12 +760,17 @@ int bits_slices(int64_t n_pods, int32_t n_groups, const DeviceInfo& dev) {
   return sl;
 }
 
+constexpr int KEEP_MAX_GROUPS = 8;  // slices of at most this many groups keep the words (KEEP)
+
 template <int S, bool KX, bool SHARD>
 hipError_t launch_bits_s(const BatchArgs& a, hipStream_t s) {
   BatchArgs ka = a;
   ka.gps = (a.n_groups + S - 1) / S;
   const int64_t blocks = ((int64_t)a.n_pods + WAVE - 1) / WAVE;
-  hipLaunchKernelGGL((bits_kernel<S, KX, SHARD>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  if (ka.gps <= KEEP_MAX_GROUPS)
+    hipLaunchKernelGGL((bits_kernel<S, KX, SHARD, true>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  else
+    hipLaunchKernelGGL((bits_kernel<S, KX, SHARD, false>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
   return hipGetLastError();
 }
 

@@ -23,8 +23,9 @@ hpd, hpt = msh.pinned_empty(p, np.int8), msh.pinned_empty(p, np.uint8)
 hpd[:], hpt[:] = pd, pt
 pin_out = (msh.pinned_empty(p, np.int32), msh.pinned_empty(p, np.int64), msh.pinned_empty(p, np.int32))
 page_out = (np.empty(p, np.int32), np.empty(p, np.int64), np.empty(p, np.int32))
-for io in ("zc", "dma"):
+for io, sync in (("zc", "stream"), ("zc2", "stream"), ("zc", "poll"), ("zc2", "poll"), ("dma", "stream")):
     os.environ["MSH_HOST_IO"] = io
+    os.environ["MSH_HOST_SYNC"] = sync
     ctx = msh.DeviceContext(0)
     ctx.upload_nodes(u, nd)
     for name, args, out in (("pageable", (pd, pt), page_out), ("pinned", (hpd, hpt), pin_out)):
@@ -36,13 +37,14 @@ for io in ("zc", "dma"):
             ctx.schedule_batch(*args, out=out)
             ts.append(time.perf_counter() - t0)
         med = float(np.median(ts))
-        print(json.dumps({"path": name, "outputs": io, "nodes": n, "pods": p, "us_per_batch_median": med * 1e6,
+        print(json.dumps({"path": name, "io": io, "sync": sync, "nodes": n, "pods": p, "us_per_batch_median": med * 1e6,
                           "us_per_batch_min": min(ts) * 1e6, "pods_per_s": p / med, "evals_per_s": n * p / med}),
               flush=True)
     ctx.close()
 
 # submission cost of the device-resident entry point from Python (ctypes) vs device time
 os.environ.pop("MSH_HOST_IO", None)
+os.environ.pop("MSH_HOST_SYNC", None)
 ctx = msh.DeviceContext(0)
 ctx.upload_nodes(u, nd)
 dev = torch.device("cuda:0")

@@ -15,6 +15,8 @@ p = int(os.environ.get("PODS", 100000))
 k = int(os.environ.get("LAUNCHES", 20))
 mode = os.environ.get("MODE", "batch")
 ctx = msh.DeviceContext(0)
+norm = int(os.environ.get("NORM", 0))  # msh_normalize (3 = MINMAX: the KX kernel)
+ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm))])
 u, nd, pd, pt = synth.make_soa(n, p)
 ctx.upload_nodes(u, nd)
 dev = torch.device("cuda:0")

@@ -42,3 +42,44 @@ def closed_form(unsched, node_digit, pod_digit, pod_tol, weight: int = 1):
             else:
                 idx[sel] = first_feas
     return idx, score, status
+
+
+def closed_form_modes(unsched, node_digit, pod_digit, pod_tol, weight: int = 1, mode: int = 0):
+    """The same, for every NormalizeScore mode of the C-ABI (msh_normalize) with the reference
+    filter / prescore / score lists and weight w. Per (tolerates, digit) class: the first feasible
+    node, the first feasible digit match (raw 10) and the first feasible non-match (raw 0); over a
+    2-level raw list the normalised winner and its score are (build extensions):
+      NONE     match ? (match, 10w) : (first feasible, 0)
+      DEFAULT  match ? (match, 100w) : (first feasible, 0)          DefaultNormalizeScore
+      REVERSE  non-match ? (non-match, 100w) : (first feasible, 0)  DefaultNormalizeScore reverse
+      MINMAX   match ? (match, non-match ? 100w : 0) : (first feasible, 0)"""
+    unsched = np.asarray(unsched, bool)
+    node_digit = np.asarray(node_digit, np.int16)
+    pod_digit, pod_tol = np.asarray(pod_digit), np.asarray(pod_tol)
+    p, n = len(pod_digit), len(unsched)
+    idx = np.full(p, -1, np.int32)
+    score = np.zeros(p, np.int64)
+    status = np.zeros(p, np.int32)
+    first = lambda m: int(np.argmax(m)) if m.any() else -1
+    for tol in (0, 1):
+        feas = np.ones(n, bool) if tol else ~unsched
+        ia = first(feas)
+        for d in range(-1, 10):
+            sel = (pod_tol == tol) & (pod_digit == d)
+            if not sel.any():
+                continue
+            if ia < 0:
+                status[sel] = 1
+                continue
+            if d < 0:
+                status[sel] = 2
+                continue
+            im = first(feas & (node_digit == d))
+            ix = first(feas & (node_digit != d))
+            if mode in (0, 1):
+                idx[sel], score[sel] = (im, (10 if mode == 0 else 100) * weight) if im >= 0 else (ia, 0)
+            elif mode == 2:
+                idx[sel], score[sel] = (ix, 100 * weight) if ix >= 0 else (ia, 0)
+            else:
+                idx[sel], score[sel] = (im, 100 * weight if ix >= 0 else 0) if im >= 0 else (ia, 0)
+    return idx, score, status

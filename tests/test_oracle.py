@@ -92,3 +92,20 @@ def test_norm_in_loop_quirk_is_identity_for_nodenumber(oracle, synth):
     b = oracle.c_schedule_batch(u, nd, pd, pt, norm_in_loop=True)
     for x, y in zip(a[:3], b[:3]):
         assert (x == y).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("weight", [1, 3])
+def test_closed_form_modes_matches_oracle(oracle, mode, weight):
+    """The per-class closed form bench.py checks its extra configs with (tests/closed_form.py)
+    agrees with the oracle's real normalizers on random tables, empty ones included."""
+    from closed_form import closed_form_modes
+    rng = np.random.default_rng(10 * mode + weight)
+    for n in (0, 1, 37, 300):
+        u = (rng.random(n) < 0.4).astype(np.uint8)
+        nd = rng.integers(-1, 10, n).astype(np.int8)
+        pd = rng.integers(-1, 10, 400).astype(np.int8)
+        pt = (rng.random(400) < 0.3).astype(np.uint8)
+        want = oracle.c_schedule_batch(u, nd, pd, pt, oracle.PluginSet(weights=[weight], normalize=[mode]))
+        got = closed_form_modes(u, nd, pd, pt, weight, mode)
+        assert all((a == b).all() for a, b in zip(got, want[:3]))
