@@ -575,9 +575,8 @@ def cpu_model() -> str:
 def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode: str, threads: int = 1):
     """The C restatement (oracle/msh_oracle.c) on this host's cores, on a bounded sample of the
     same workload: pods in chunks against the full node table until the budget is spent."""
+    importlib.import_module("oracle.build").build_oracle()
     O = importlib.import_module("oracle.oracle")
-    build = importlib.import_module("mini-kube-scheduler_amd.build")
-    build.build_oracle()
     n = len(unsched)
     p = len(pod_digit)
     chunk = min(2000 * threads, p)

@@ -1,7 +1,8 @@
 """Build recipe for libminisched_hip.so (gfx950) — in-tree, no JIT cache.
 
 `python -m` is not needed: `build()` is called by `__graft_entry__.build()` and by the tests'
-session fixture when the library is missing or stale. Objects go to `build/` next to this
+session fixture when the library is missing or stale. The oracle (test infrastructure) is built
+by oracle/build.py, not from here. Objects go to `build/` next to this
 file; the shared library lands in the package directory so it travels with the repo
 snapshot to the GPU box.
 """
@@ -89,53 +90,6 @@ def build_demo(verbose: bool = False) -> Path:
     return DEMO
 
 
-def build_diagnostic(verbose: bool = False) -> Path:
-    """Diagnostic variant with per-wave phase stamps (-DMSH_STAMPS): libminisched_hip_stamps.so.
-    Used only by scripts/stamps.py; never loaded by the product path."""
-    return build_variant(["-DMSH_STAMPS"], "stamps", verbose)
-
-
-def build_variant(defines: list[str], tag: str, verbose: bool = False) -> Path:
-    """A/B build of the library with extra -D flags: libminisched_hip_<tag>.so (tuning only)."""
-    out = PKG_DIR / f"libminisched_hip_{tag}.so"
-    if not _stale(out, [CSRC / src for src, _, _ in SOURCES] + HEADERS):
-        return out
-    OBJ.mkdir(exist_ok=True)
-    objs = []
-    for src, cc, extra in SOURCES:
-        s = CSRC / src
-        o = OBJ / (s.stem + f".{tag}.o")
-        objs.append(o)
-        if not _stale(o, [s, *HEADERS]):
-            continue
-        if cc == "hipcc":
-            cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *defines,
-                   "-Wno-unused-result", "-Wno-unused-value", *extra, "-c", str(s), "-o", str(o)]
-        else:
-            cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-c", str(s), "-o", str(o)]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-    if _stale(out, objs):
-        subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(out)],
-                       check=True)
-    return out
-
-
-def build_oracle(verbose: bool = False) -> Path:
-    """Compile the C oracle (test infrastructure) into oracle/build/libmsh_oracle.so."""
-    odir = REPO / "oracle"
-    out = odir / "build" / "libmsh_oracle.so"
-    srcs = [odir / "msh_oracle.c", odir / "msh_oracle_omp.c", odir / "msh_oracle.h"]
-    if _stale(out, srcs):
-        cmd = ["make", "-C", str(odir)]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True, stdout=None if verbose else subprocess.DEVNULL)
-    return out
-
-
 if __name__ == "__main__":
     print(build(verbose=True))
     print(build_demo(verbose=True))
-    print(build_oracle(verbose=True))

@@ -1,4 +1,6 @@
-"""Per-pod latency of the sequential-commit kernel for MSH_SEQ_WAVES in {4, 8, 16}."""
+"""Per-pod latency of the sequential-commit kernel for MSH_SEQ_WAVES (scanning waves, read by
+msh_create: one ctx per setting) in {0 = the launcher's choice, 1, 4, 16}, with and without a
+capacity (CAPS)."""
 import importlib
 import json
 import os
@@ -14,9 +16,13 @@ msh = importlib.import_module("mini-kube-scheduler_amd")
 synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
 n = int(os.environ.get("NODES", 5000))
 p = int(os.environ.get("PODS", 20000))
-ctx = msh.DeviceContext(0)
 u, nd, pd, pt = synth.make_soa(n, p)
-ctx.upload_nodes(u, nd)
+WAVES = os.environ.get("WAVES", "0,1,4,16").split(",")
+ctxs = {}
+for w in WAVES:
+    os.environ["MSH_SEQ_WAVES"] = w
+    ctxs[w] = msh.DeviceContext(0)
+    ctxs[w].upload_nodes(u, nd)
 dev = torch.device("cuda:0")
 d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
 oi = torch.empty(p, dtype=torch.int32, device=dev)
@@ -27,8 +33,8 @@ res = {}
 caps = [int(c) for c in os.environ.get("CAPS", "0").split(",")]  # max_pods_per_node (0 = reference)
 for rnd in range(4):
     for cap in caps:
-        for w in ("4", "8", "16"):
-            os.environ["MSH_SEQ_WAVES"] = w
+        for w in WAVES:
+            ctx = ctxs[w]
             ctx.reset_node_pod_counts()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)

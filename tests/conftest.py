@@ -17,9 +17,8 @@ def pytest_configure(config):
 
 
 def _build():
-    build = importlib.import_module("mini-kube-scheduler_amd.build")
-    build.build()
-    build.build_oracle()
+    importlib.import_module("mini-kube-scheduler_amd.build").build()
+    importlib.import_module("oracle.build").build_oracle()
 
 
 @pytest.fixture(scope="session")

@@ -55,7 +55,7 @@ def test_product_package_does_not_import_oracle():
     for f in list(pkg.glob("*.py")) + list((pkg / "csrc").glob("*")):
         if f.is_file():
             assert not pat.search(f.read_text(errors="ignore")), f
-    assert "oracle" not in (pkg / "build.py").read_text().split("def build_oracle")[0].split("SOURCES")[1]
+    assert "oracle" not in (pkg / "build.py").read_text().split("SOURCES")[1]
 
 
 def _run_demo(msh):
