@@ -68,9 +68,10 @@ def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
     rs = lambda nw: -(-words // (nw * 64))
     nw = 1 if rs(1) <= 4 else 4 if rs(4) <= 4 else (16 if cap else 15)
     r = rs(nw)
-    rsv = {1: [1, 2, 4], 4: [2, 4]}.get(nw, [4, 8] if cap else [4, 8, 12])
+    rsv = {1: [1, 2, 3, 4], 4: [2, 4]}.get(nw, [4, 8] if cap else [4, 8, 12])
     r = next(v for v in rsv if r <= v)
-    return f"void msh::seq_kernel<{r}, {nw}, {str(kx).lower()}, {str(cap).lower()}>"
+    u = 4 if nw == 1 and not cap else 1  # SEQ_AHEAD
+    return f"void msh::seq_kernel<{r}, {nw}, {str(kx).lower()}, {str(cap).lower()}, {u}>"
 
 
 def parse():

@@ -117,7 +117,6 @@ struct SeqArgs {
   PluginParams pp;
   int32_t max_pods;
   int32_t* counts;           // [n_pad] per-node assigned pods (read at start, updated)
-  int32_t lds_counts;        // 1: the kernel keeps the counts in LDS and writes them back at the end
   int32_t* out_idx;
   int64_t* out_score;
   int32_t* out_status;

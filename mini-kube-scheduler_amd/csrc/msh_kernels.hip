@@ -451,9 +451,22 @@ __device__ __forceinline__ void lds_barrier() {
 // The wave's smallest value when lanes hold ascending, disjoint ranges (lane l's candidates all
 // precede lane l + 1's): the first lane that has one. One ballot, s_ff1 and a readlane instead of a
 // 6-step DPP reduction on the per-pod critical path.
+// Branch-free: with no lane holding a value the first lane of (m | lane 63) is lane 63, whose
+// value is then "none" too.
 __device__ __forceinline__ uint32_t wave_first(uint32_t v) {
-  const unsigned long long m = __ballot(v != 0xFFFFFFFFu);
-  return m ? (uint32_t)__builtin_amdgcn_readlane((int)v, __builtin_ctzll(m)) : 0xFFFFFFFFu;
+  const unsigned long long m = __ballot(v != 0xFFFFFFFFu) | (1ull << 63);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, __builtin_ctzll(m));
+}
+
+// One commit of a pod count (no return value waited for): a plain ds_add_u32 from the calling
+// lane. Written as asm: the backend's atomic optimizer turns a single-lane atomicAdd into an
+// mbcnt / bcnt sequence and two more exec-mask branches per pod.
+__device__ __forceinline__ void lds_add(uint32_t lds_addr, uint32_t v) {
+  asm volatile("ds_add_u32 %0, %1" ::"v"(lds_addr), "v"(v) : "memory");
+}
+// 32-bit LDS address of a __shared__ object (its offset in the workgroup's LDS)
+__device__ __forceinline__ uint32_t lds_addr(const int32_t* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int32_t*)p;
 }
 
 // Lowest set bit (v_ffbl_b32): 0xFFFFFFFF when x == 0, so (base | ffbl(x)) is "no node" then.
@@ -463,18 +476,23 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
   return r;
 }
 
-template <int RS, int NW, bool KX, bool CAP>
+// U: pods decided per step (U > 1 only for one wave without a capacity; U divides 64).
+template <int RS, int NW, bool KX, bool CAP, int U>
 __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_kernel(SeqArgs a) {
+  static_assert(U == 1 || (NW == 1 && !CAP), "pods are decided ahead of commits only when no commit feeds a decision");
   constexpr bool FIN = !CAP && NW > 1;  // a finalizer wave decodes, keeps the outputs and commits
   constexpr int FINW = FIN ? NW : 0;    // the wave that keeps the outputs
+  constexpr bool LDSC = NW <= 4;        // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32
+                                        // nodes = 32,768 nodes, 128 KB), else in device memory
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-pod exchange slots (NW > 1), triple-buffered: [slot][first match, first feasible, first
   // feasible non-match]
   __shared__ uint32_t xs[3][3];
-  extern __shared__ int32_t lcnt[];  // [n_pad] per-node pod counts when a.lds_counts
+  extern __shared__ int32_t lcnt[];  // [n_pad] per-node pod counts (LDSC)
+  __shared__ int32_t ldummy[WAVE];    // branch-free commits: the other lanes add 0 here
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool scanner = wv < NW;
+  const bool scanner = !FIN || wv < NW;
 
   uint32_t D0[RS], D1[RS], D2[RS], D3[RS], XX[RS], VV[RS], FULL[RS];
 #pragma unroll
@@ -498,7 +516,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
       }
     }
   }
-  if (a.lds_counts)  // ordered before the first commit by the first pod's exchange / barrier
+  if (LDSC)  // ordered before the first commit by the first pod's exchange / barrier
     for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) lcnt[i] = a.counts[i];
   if (threadIdx.x < 9) xs[threadIdx.x / 3][threadIdx.x % 3] = NONE;
   __syncthreads();
@@ -525,8 +543,8 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   PluginParams pp = a.pp;
   asm volatile("" : "+s"(pp.has_nu_filter), "+s"(pp.has_nn_score), "+s"(pp.nn_prescore), "+s"(pp.mode),
                "+s"(pp.weight));
-  int32_t max_pods = a.max_pods, lds_counts = a.lds_counts;
-  asm volatile("" : "+s"(max_pods), "+s"(lds_counts));
+  int32_t max_pods = a.max_pods;
+  asm volatile("" : "+s"(max_pods));
   const uint32_t ball0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.ball[0]);
   const uint32_t ball1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.ball[1]);
   int32_t* counts = a.counts;
@@ -544,93 +562,114 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
       a.out_status[j0 + lane] = o_st;
     }
   };
-  for (int32_t j = 0; j < a.n_pods; ++j) {
-    const int jl = j & (WAVE - 1);
-    if (jl == 0) {
+  for (int32_t j = 0; j < a.n_pods; j += U) {
+    if ((j & (WAVE - 1)) == 0) {
       // order matters for vmcnt (in-order): the conversion waits only for the loads issued one
       // block ago, then the previous block's results leave, then the next block is requested
       convert(j, dn, tn, pcv, tolv);
       if (wv == FINW && j > 0) store_block(j - WAVE, WAVE);
       load_raw(j + WAVE, dn, tn);
     }
-    const uint32_t pc = (uint32_t)__builtin_amdgcn_readlane((int)pcv, jl);
-    const uint32_t tol = (uint32_t)__builtin_amdgcn_readlane((int)tolv, jl);
-    // the pod's code bits as all-ones / all-zero masks, and ~tolerates: wave-uniform (SGPRs)
-    const uint32_t p0 = 0u - (pc & 1u), p1 = 0u - ((pc >> 1) & 1u), p2 = 0u - ((pc >> 2) & 1u), p3 = 0u - (pc >> 3);
-    const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
-    uint32_t cm = NONE, ca = NONE, cx = NONE;  // this lane's first match / feasible / non-match
-    if (scanner) {
+    // ---- decide: the U pods' scans (U > 1 only without a capacity, where no commit feeds a
+    // later decision: independent chains, the same reordering as round 1's finalizer wave) ----
+    uint32_t pcu[U], tolu[U], cmu[U], cau[U], cxu[U];
 #pragma unroll
-      for (int r = RS - 1; r >= 0; --r) {  // slots ascend in List order per lane
-        const uint32_t dm = (D0[r] ^ p0) | (D1[r] ^ p1) | (D2[r] ^ p2) | (D3[r] ^ p3);
-        const uint32_t bad = (XX[r] & nT) | (CAP ? FULL[r] : 0u);
-        const uint32_t base = lane_base + (uint32_t)(r * 32);
-        cm = umin(cm, base | ffbl(~(dm | bad)));
-        if (CAP) ca = umin(ca, base | ffbl(VV[r] & ~bad));
-        if (KX) cx = umin(cx, base | ffbl(VV[r] & ~bad & dm));
-      }
-      cm = wave_first(cm);
-      if (CAP) ca = wave_first(ca);
-      if (KX) cx = wave_first(cx);
-    }
-    if constexpr (NW > 1) {
-      // lane 0 of every scanning wave folds its wave's result into this pod's slot; after the
-      // barrier the pod's result is ONE broadcast read
-      if (scanner && lane == 0) {
-        atomicMin(&xs[sl][0], cm);
-        if (CAP) atomicMin(&xs[sl][1], ca);
-        if (KX) atomicMin(&xs[sl][2], cx);
-      }
-      lds_barrier();
-      const int sl_now = sl;
-      sl = sl == 2 ? 0 : sl + 1;
-      if (!CAP && wv != FINW) continue;  // without a capacity only the finalizer finishes a pod
-      cm = xs[sl_now][0];
-      if (CAP) ca = xs[sl_now][1];
-      if (KX) cx = xs[sl_now][2];
-      // the slot read one pod ago is free now (every reader passed this pod's barrier) and is
-      // next folded into two pods ahead (after the next barrier): wave FINW resets it in between
-      if (wv == FINW && lane == 0) {
-        const int sr = sl_now == 0 ? 2 : sl_now - 1;
-        xs[sr][0] = NONE;
-        xs[sr][1] = NONE;
-        xs[sr][2] = NONE;
-      }
-    }
-    const int64_t im = cm != NONE ? (int64_t)cm : -1;
-    const int64_t ia = CAP ? (ca != NONE ? (int64_t)ca : -1) : key_to_idx(tol ? ball1 : ball0);
-    int32_t sel, st;
-    int64_t sc;
-    if (KX)
-      decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pc != CODE_NONE_POD, pp, &sel, &sc, &st);
-    else
-      decode_ident(im, ia, pc != CODE_NONE_POD, idec, &sel, &sc, &st);
-    if (wv == FINW) {
-      const bool mine = lane == jl;
-      o_idx = mine ? sel : o_idx;
-      o_sc = mine ? sc : o_sc;
-      o_st = mine ? st : o_st;
-    }
-    if (st == 0) {  // commit (NodeInfo.AddPod analogue)
-      if (!CAP) {
-        if (lane == 0) {  // no return value waited for
-          if (lds_counts) atomicAdd(&lcnt[sel], 1);
-          else atomicAdd(&counts[sel], 1);
+    for (int u = 0; u < U; ++u) {
+      const int jl = (j + u) & (WAVE - 1);
+      pcu[u] = (uint32_t)__builtin_amdgcn_readlane((int)pcv, jl);
+      tolu[u] = (uint32_t)__builtin_amdgcn_readlane((int)tolv, jl);
+      const uint32_t pc = pcu[u];
+      // the pod's code bits as all-ones / all-zero masks, and ~tolerates: wave-uniform (SGPRs)
+      const uint32_t p0 = 0u - (pc & 1u), p1 = 0u - ((pc >> 1) & 1u), p2 = 0u - ((pc >> 2) & 1u), p3 = 0u - (pc >> 3);
+      const uint32_t nT = tolu[u] ? 0u : 0xFFFFFFFFu;
+      uint32_t cm = NONE, ca = NONE, cx = NONE;  // this lane's first match / feasible / non-match
+      if (scanner) {
+#pragma unroll
+        for (int r = RS - 1; r >= 0; --r) {  // slots ascend in List order per lane
+          const uint32_t dm = (D0[r] ^ p0) | (D1[r] ^ p1) | (D2[r] ^ p2) | (D3[r] ^ p3);
+          const uint32_t bad = (XX[r] & nT) | (CAP ? FULL[r] : 0u);
+          const uint32_t base = lane_base + (uint32_t)(r * 32);
+          cm = umin(cm, base | ffbl(~(dm | bad)));
+          if (CAP) ca = umin(ca, base | ffbl(VV[r] & ~bad));
+          if (KX) cx = umin(cx, base | ffbl(VV[r] & ~bad & dm));
         }
-      } else {
-        const uint32_t w = (uint32_t)sel >> 5, q = w / RS;
-        if ((int)(q / WAVE) == wv) {  // the owning wave
-          int32_t old = 0;
-          if (lane == 0) old = lds_counts ? atomicAdd(&lcnt[sel], 1) : atomicAdd(&counts[sel], 1);
-          const bool full = __builtin_amdgcn_readfirstlane(old) + 1 >= max_pods;
-          if (full) {
-            // the owning lane: the register by a wave-uniform index (scalar branches), the lane by
-            // a compare
-            const int rs = (int)(w % RS);
-            const uint32_t bit = (lane == (int)(q % WAVE)) ? (1u << (sel & 31)) : 0u;
+        cm = wave_first(cm);
+        if (CAP) ca = wave_first(ca);
+        if (KX) cx = wave_first(cx);
+      }
+      cmu[u] = cm;
+      cau[u] = ca;
+      cxu[u] = cx;
+    }
+    // ---- then, in pod order: exchange (NW > 1), decode, output, commit ----
 #pragma unroll
-            for (int r = 0; r < RS; ++r)
-              if (r == rs) FULL[r] |= bit;
+    for (int u = 0; u < U; ++u) {
+      const bool valid = U == 1 || j + u < a.n_pods;  // wave-uniform: the tail step's pods past the batch
+      const int jl = (j + u) & (WAVE - 1);
+      const uint32_t pc = pcu[u], tol = tolu[u];
+      uint32_t cm = cmu[u], ca = cau[u], cx = cxu[u];
+      if constexpr (NW > 1) {
+        // lane 0 of every scanning wave folds its wave's result into this pod's slot; after the
+        // barrier the pod's result is ONE broadcast read
+        if (scanner && lane == 0) {
+          atomicMin(&xs[sl][0], cm);
+          if (CAP) atomicMin(&xs[sl][1], ca);
+          if (KX) atomicMin(&xs[sl][2], cx);
+        }
+        lds_barrier();
+        const int sl_now = sl;
+        sl = sl == 2 ? 0 : sl + 1;
+        if (!CAP && wv != FINW) continue;  // without a capacity only the finalizer finishes a pod
+        cm = xs[sl_now][0];
+        if (CAP) ca = xs[sl_now][1];
+        if (KX) cx = xs[sl_now][2];
+        // the slot read one pod ago is free now (every reader passed this pod's barrier) and is
+        // next folded into two pods ahead (after the next barrier): wave FINW resets it in between
+        if (wv == FINW && lane == 0) {
+          const int sr = sl_now == 0 ? 2 : sl_now - 1;
+          xs[sr][0] = NONE;
+          xs[sr][1] = NONE;
+          xs[sr][2] = NONE;
+        }
+      }
+      const int64_t im = cm != NONE ? (int64_t)cm : -1;
+      const int64_t ia = CAP ? (ca != NONE ? (int64_t)ca : -1) : key_to_idx(tol ? ball1 : ball0);
+      int32_t sel, st;
+      int64_t sc;
+      if (KX)
+        decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pc != CODE_NONE_POD, pp, &sel, &sc, &st);
+      else
+        decode_ident(im, ia, pc != CODE_NONE_POD, idec, &sel, &sc, &st);
+      if (wv == FINW) {
+        const bool mine = lane == jl;
+        o_idx = mine ? sel : o_idx;
+        o_sc = mine ? sc : o_sc;
+        o_st = mine ? st : o_st;
+      }
+      if (!CAP && LDSC) {
+        // commit (NodeInfo.AddPod analogue), branch-free: lane 0 adds 1 to the node's count (0 to
+        // node 0 when the pod is not placed), the other lanes add 0 to slots of their own
+        const bool placed = valid && st == 0;
+        const uint32_t node = lds_addr(lcnt) + 4u * (uint32_t)(placed ? sel : 0);
+        lds_add(lane == 0 ? node : lds_addr(ldummy) + 4u * (uint32_t)lane, (lane == 0 && placed) ? 1u : 0u);
+      } else if (valid && st == 0) {  // commit
+        if (!CAP) {
+          if (lane == 0) atomicAdd(&counts[sel], 1);  // no return value waited for
+        } else {
+          const uint32_t w = (uint32_t)sel >> 5, q = w / RS;
+          if ((int)(q / WAVE) == wv) {  // the owning wave
+            int32_t old = 0;
+            if (lane == 0) old = LDSC ? atomicAdd(&lcnt[sel], 1) : atomicAdd(&counts[sel], 1);
+            const bool full = __builtin_amdgcn_readfirstlane(old) + 1 >= max_pods;
+            if (full) {
+              // the owning lane: the register by a wave-uniform index (scalar branches), the lane
+              // by a compare
+              const int rs = (int)(w % RS);
+              const uint32_t bit = (lane == (int)(q % WAVE)) ? (1u << (sel & 31)) : 0u;
+#pragma unroll
+              for (int r = 0; r < RS; ++r)
+                if (r == rs) FULL[r] |= bit;
+            }
           }
         }
       }
@@ -641,7 +680,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     const int32_t j0 = (a.n_pods - 1) & ~(WAVE - 1);
     store_block(j0, a.n_pods - j0);
   }
-  if (a.lds_counts) {
+  if (LDSC) {
     __syncthreads();
     for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) a.counts[i] = lcnt[i];
   }
@@ -804,14 +843,15 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
 }
 
 namespace {
-constexpr size_t SEQ_LDS_COUNTS_MAX = 128 * 1024;  // per-node counts kept in LDS up to 32,768 nodes
+constexpr int SEQ_AHEAD = 4;  // pods decided per step by one wave without a capacity
 
 template <int RS, int NW, bool CAP>
 hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
   const dim3 blk((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64);  // + the finalizer wave without a capacity
-  const size_t lds = a.lds_counts ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;
-  auto kx = seq_kernel<RS, NW, true, CAP>;
-  auto id = seq_kernel<RS, NW, false, CAP>;
+  const size_t lds = NW <= 4 ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;  // seq_kernel's LDSC
+  constexpr int U = (NW == 1 && !CAP) ? SEQ_AHEAD : 1;
+  auto kx = seq_kernel<RS, NW, true, CAP, U>;
+  auto id = seq_kernel<RS, NW, false, CAP, U>;
   const void* k = needs_kx(a.pp) ? reinterpret_cast<const void*>(kx) : reinterpret_cast<const void*>(id);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -827,6 +867,7 @@ hipError_t launch_seq_nw(const SeqArgs& a, int rs, hipStream_t s) {
   if constexpr (NW == 1) {
     if (rs <= 1) return launch_seq_rs<1, NW, CAP>(a, s);
     if (rs <= 2) return launch_seq_rs<2, NW, CAP>(a, s);
+    if (rs <= 3) return launch_seq_rs<3, NW, CAP>(a, s);
     return launch_seq_rs<4, NW, CAP>(a, s);
   } else if constexpr (NW == 4) {
     if (rs <= 2) return launch_seq_rs<2, NW, CAP>(a, s);
@@ -860,8 +901,7 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
              std::to_string(nw_big * WAVE * rs_max * 32) + " nodes per device" + (cap ? " with a capacity" : "");
     return hipErrorInvalidValue;
   }
-  SeqArgs ka = a;
-  ka.lds_counts = (size_t)a.n_words * 32 * sizeof(int32_t) <= SEQ_LDS_COUNTS_MAX ? 1 : 0;
+  const SeqArgs& ka = a;
   if (cap) {
     if (nw == 1) return launch_seq_nw<1, true>(ka, rs, s);
     if (nw == 4) return launch_seq_nw<4, true>(ka, rs, s);

@@ -262,7 +262,7 @@ def test_sequential(msh, oracle, n, max_pods, seq_waves, monkeypatch):
     monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)
     rng = np.random.default_rng(n + max_pods)
     ps = oracle.PluginSet()
-    u, nd, pd, pt = _rand_case(rng, n, 3000)
+    u, nd, pd, pt = _rand_case(rng, n, 3001)  # not a multiple of the 4 pods one wave decides per step
     with msh.DeviceContext(0) as ctx:
         _set(ctx, msh, ps)
         ctx.upload_nodes(u, nd)
