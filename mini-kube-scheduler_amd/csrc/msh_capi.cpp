@@ -313,8 +313,16 @@ msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t
   return a;
 }
 
+// The ctx's device current for the call, the caller's restored after it (no switch at all in the
+// common case of a caller already on that device).
 struct DeviceGuard {
-  explicit DeviceGuard(int d) { (void)hipSetDevice(d); }
+  int prev = -1, want;
+  explicit DeviceGuard(int d) : want(d) {
+    if (hipGetDevice(&prev) != hipSuccess || prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
+  }
 };
 
 // Host-buffer I/O of one synchronous call: pod columns and outputs in page-locked host memory,
@@ -447,7 +455,9 @@ int msh_create(int device, msh_ctx** out_ctx) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MSH_ERR_NO_DEVICE;
   if (device < 0 || device >= n) return MSH_ERR_NO_DEVICE;
-  if (hipSetDevice(device) != hipSuccess) return MSH_ERR_NO_DEVICE;
+  DeviceGuard g(device);
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != device) return MSH_ERR_NO_DEVICE;
   msh_ctx* c = new (std::nothrow) msh_ctx();
   if (!c) return MSH_ERR_NOMEM;
   c->device = device;
@@ -486,7 +496,7 @@ int msh_create(int device, msh_ctx** out_ctx) {
 
 void msh_destroy(msh_ctx* c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  DeviceGuard g(c->device);
   // launches queued on caller streams (the *_device entry points) may still read the tables
   (void)hipDeviceSynchronize();
   delete c->pool;

@@ -189,8 +189,8 @@ __device__ __forceinline__ int64_t key_to_idx(uint32_t k) {
 // chain, 5 VALU per 32 x 64 pairs. Padding slots carry code 15, pods without a digit code 14: they
 // never match. Pairs of words AND into a per-group accumulator (v_bitop3, 3 inputs); a group of
 // PLANE_GW words with a zero bit is remembered (groups are walked in DESCENDING List order, so the
-// last one remembered is the first); afterwards the lane re-reads its own first group (vector
-// loads) and finds the exact node: first word with a zero bit, then its lowest zero bit. No
+// last one remembered is the first); the exact node is the first word of that group with a zero
+// bit, then its lowest zero bit (see below for where the words come from). No
 // cross-lane reduction at all: the first maximum of selectHost (minisched.go:304-325) falls out of
 // the List order of words and bits.
 //
@@ -286,11 +286,13 @@ __device__ __forceinline__ uint32_t kept_first(const uint32_t (&k)[PLANE_GW], ui
   return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
 }
 
-// KEEP (short slices): the miss words of the first group with a hit are kept in registers as the
-// scan passes (8 v_cndmask per group), instead of re-reading that group's planes afterwards
-// (group_first: ten 16-byte loads per lane and ~100 VALU, a memory round trip at the end of every
-// wave, where little else is left to overlap it).
-template <int S, bool KX, bool SHARD, bool KEEP>
+// The lowest group of a slice is scanned last (groups descend) and its miss words are still in
+// registers: a lane whose first hit lies there (nearly every lane: a 256-node group almost always
+// holds a feasible node of each digit) reads it off them (kept_first). Only a lane whose first hit
+// lies in a higher group re-reads that group's planes (group_first, vector loads), behind an
+// exec-mask branch the wave skips when no lane needs it. The groups above the lowest only track
+// the first group with a hit: 5 VALU per word, the pair ANDs and one select per group.
+template <int S, bool KX, bool SHARD>
 __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
   __shared__ uint32_t s_res[S][KX ? 2 : 1][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -307,12 +309,9 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
                  P3 = 0u - (code >> 3);
   const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
   const int32_t g_lo = min(s * a.gps, a.n_groups), g_hi = min(g_lo + a.gps, a.n_groups);
-  uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group with a feasible match / non-match
-  uint32_t km[PLANE_GW], kx[PLANE_GW];     // KEEP: that group's miss words
-#pragma unroll
-  for (int c = 0; c < PLANE_GW; ++c) km[c] = kx[c] = 0xFFFFFFFFu;
   constexpr int NPL = KX ? PLANE_N : PLANE_V;  // planes the scan reads
-  for (int32_t g = g_hi - 1; g >= g_lo; --g) {
+  // One group: the miss words (gm; KX: gx, the non-match miss words) and whether any has a zero bit.
+  auto scan_group = [&](int32_t g, uint32_t (&gm)[PLANE_GW], uint32_t (&gx)[PLANE_GW], bool& hm, bool& hx) {
     // the group's planes, wave-uniform: one s_load_dwordx8 per plane, all in flight together,
     // one wait (left to itself the backend interleaves single-dword scalar loads with the
     // bitop3 chain, one lgkmcnt wait every few instructions)
@@ -324,10 +323,8 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
 #pragma unroll
       for (int c = 0; c < PLANE_GW; ++c) pg[k * PLANE_GW + c] = pl[k][c];
     uint32_t am = 0xFFFFFFFFu, ax = 0xFFFFFFFFu;
-    uint32_t gm[PLANE_GW], gx[PLANE_GW];
 #pragma unroll
     for (int w = 0; w < PLANE_GW; w += 2) {
-      uint32_t mm[2], mx[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int c = w + q;
@@ -337,40 +334,36 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
           dm = or_xor_s(dm, pg[PLANE_GW + c], P1);
           dm = or_xor_s(dm, pg[2 * PLANE_GW + c], P2);
           dm = or_xor_s(dm, pg[3 * PLANE_GW + c], P3);
-          mm[q] = dm | xi;
-          mx[q] = nmiss_s(dm, xi, pg[PLANE_V * PLANE_GW + c]);
+          gm[c] = dm | xi;
+          gx[c] = nmiss_s(dm, xi, pg[PLANE_V * PLANE_GW + c]);
         } else {
           uint32_t t = or_xor_s(xi, pg[c], P0);
           t = or_xor_s(t, pg[PLANE_GW + c], P1);
           t = or_xor_s(t, pg[2 * PLANE_GW + c], P2);
-          mm[q] = or_xor_s(t, pg[3 * PLANE_GW + c], P3);
+          gm[c] = or_xor_s(t, pg[3 * PLANE_GW + c], P3);
         }
       }
-      am &= mm[0] & mm[1];
-      if constexpr (KX) ax &= mx[0] & mx[1];
-      gm[w] = mm[0];
-      gm[w + 1] = mm[1];
-      gx[w] = mx[0];
-      gx[w + 1] = mx[1];
+      am &= gm[w] & gm[w + 1];
+      if constexpr (KX) ax &= gx[w] & gx[w + 1];
     }
-    const bool hm = am != 0xFFFFFFFFu, hx = KX && ax != 0xFFFFFFFFu;
+    hm = am != 0xFFFFFFFFu;
+    hx = KX && ax != 0xFFFFFFFFu;
+  };
+  uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group above the lowest with a feasible match / non-match
+  uint32_t gm[PLANE_GW], gx[PLANE_GW];
+  bool hm = false, hx = false;
+  for (int32_t g = g_hi - 1; g > g_lo; --g) {
+    scan_group(g, gm, gx, hm, hx);
     fm = hm ? (uint32_t)g : fm;
     if constexpr (KX) fx = hx ? (uint32_t)g : fx;
-    if constexpr (KEEP) {
-#pragma unroll
-      for (int c = 0; c < PLANE_GW; ++c) {
-        km[c] = hm ? gm[c] : km[c];
-        if constexpr (KX) kx[c] = hx ? gx[c] : kx[c];
-      }
-    }
   }
   uint32_t rm = NOFIT, rx = NOFIT;  // node index of the first feasible match / non-match
-  if constexpr (KEEP) {
-    if (fm != NO_GROUP) rm = kept_first(km, fm);
-    if (KX && fx != NO_GROUP) rx = kept_first(kx, fx);
-  } else {
-    if (fm != NO_GROUP) rm = group_first<false>(a.planes, fm, P0, P1, P2, P3, nT);
-    if (KX && fx != NO_GROUP) rx = group_first<true>(a.planes, fx, P0, P1, P2, P3, nT);
+  if (g_lo < g_hi) {
+    scan_group(g_lo, gm, gx, hm, hx);
+    if (hm) rm = kept_first(gm, (uint32_t)g_lo);
+    if (KX && hx) rx = kept_first(gx, (uint32_t)g_lo);
+    if (!hm && fm != NO_GROUP) rm = group_first<false>(a.planes, fm, P0, P1, P2, P3, nT);
+    if (KX && !hx && fx != NO_GROUP) rx = group_first<true>(a.planes, fx, P0, P1, P2, P3, nT);
   }
   if constexpr (S > 1) {
     s_res[s][0][lane] = rm;
@@ -788,8 +781,8 @@ hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_
 
 namespace {
 // Slice waves per 64-pod block of the bit-sliced kernel: enough waves for ~6 per SIMD, each
-// slice at least two groups (512 nodes) so the per-wave fixed cost (pod bytes, the first-group
-// re-read, the LDS merge) stays small next to the scan.
+// slice at least two groups (512 nodes) so the per-wave fixed cost (pod bytes, the first-node
+// decode, the LDS merge) stays small next to the scan.
 int bits_slices(int64_t n_pods, int32_t n_groups, const DeviceInfo& dev) {
   if (dev.bits_slices > 0) return dev.bits_slices;
   const int64_t blocks = (n_pods + WAVE - 1) / WAVE;
@@ -799,17 +792,12 @@ int bits_slices(int64_t n_pods, int32_t n_groups, const DeviceInfo& dev) {
   return sl;
 }
 
-constexpr int KEEP_MAX_GROUPS = 8;  // slices of at most this many groups keep the words (KEEP)
-
 template <int S, bool KX, bool SHARD>
 hipError_t launch_bits_s(const BatchArgs& a, hipStream_t s) {
   BatchArgs ka = a;
   ka.gps = (a.n_groups + S - 1) / S;
   const int64_t blocks = ((int64_t)a.n_pods + WAVE - 1) / WAVE;
-  if (ka.gps <= KEEP_MAX_GROUPS)
-    hipLaunchKernelGGL((bits_kernel<S, KX, SHARD, true>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
-  else
-    hipLaunchKernelGGL((bits_kernel<S, KX, SHARD, false>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  hipLaunchKernelGGL((bits_kernel<S, KX, SHARD>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
   return hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ def counters(tag, prefix):
 
 res = {"source": str(src), "nodes": N, "pods": P, "kernels": {}}
 for mode, prefix, tags in (("batch", "void msh::bits_kernel", ("b_sq", "b_sq2", "b_grbm", "b_fetch", "b_write")),
+                           ("batch_minmax", "void msh::bits_kernel", ("k_sq",)),
                            ("sequential", "void msh::seq_kernel", ("s_sq", "s_fetch", "s_write"))):
     e = {"nodes": N, "pods": P, "launches_per_counter": {}}
     for t in tags:
@@ -44,7 +45,7 @@ for mode, prefix, tags in (("batch", "void msh::bits_kernel", ("b_sq", "b_sq2", 
         e["hbm_bytes_per_launch_fetch_x2"] = 2 * e["fetch_bytes_raw"] + e["write_bytes"]
     if "SQ_INSTS_VALU" in e:
         e["valu_lane_ops_per_eval"] = e["SQ_INSTS_VALU"] * 64 / (N * P)
-        if mode == "batch":
+        if mode.startswith("batch"):
             e["scan_model_share"] = (46 / 8) * (P / 64) * (N / 32) / e["SQ_INSTS_VALU"]
     if "SQ_WAVE_CYCLES" in e:
         for k in ("SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):

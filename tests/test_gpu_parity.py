@@ -103,8 +103,8 @@ def test_plugin_sets_random(msh, gpu_ctx, oracle, combo, norm, weight):
 @pytest.mark.parametrize("n", [0, 1, 5, 63, 64, 65, 1023, 1024, 1025, 5000, 16384, 16385, 21504, 21505, 40000,
                                64512, 64513, 70000, 140000])
 def test_node_sizes(msh, gpu_ctx, oracle, n):
-    """Empty / ragged / tile-boundary / multi-stage node tables (IDENT: LDS stage 21,504 nodes,
-    compute tile 64,512 nodes; compare/select kernel: LDS tile 16,384 nodes)."""
+    """Empty / ragged / boundary node tables: 32-node words, 256-node groups, 1,024-node prep
+    blocks, and slice splits of the group range (bits_slices) at several table sizes."""
     rng = np.random.default_rng(n)
     ps = oracle.PluginSet()
     _set(gpu_ctx, msh, ps)
@@ -507,6 +507,10 @@ def test_host_buffer_paths(msh, gpu_ctx, oracle, synth, norm):
     for o in outs:
         o.fill(-7)
     _assert_same(gpu_ctx.schedule_batch(pd, pt, out=outs), want, "pageable in / pinned out")
+    # ragged batch sizes through the staged and the zero-copy input paths
+    for q in (2 * 16384 + 7, 3 * 16384 + 100, 99_937):
+        _assert_same(gpu_ctx.schedule_batch(pd[:q], pt[:q]), tuple(w[:q] for w in want[:3]), f"pageable {q}")
+        _assert_same(gpu_ctx.schedule_batch(hpd[:q], hpt[:q]), tuple(w[:q] for w in want[:3]), f"pinned in {q}")
     gpu_ctx.reset_node_pod_counts()
     for o in outs:
         o.fill(-7)
