@@ -424,16 +424,20 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
 // its words (5 VALU per 32 pairs), turns its first hit into a node index (v_ffbl_b32: the lowest
 // set bit, all-ones when there is none), and the wave's first is its first lane with a hit
 // (wave_first). NW > 1 waves meet in a triple-buffered LDS slot
-// (atomic min) behind one LDS-only barrier. Then decode, output and commit: the node's pod count
-// (an LDS table when it fits, device memory otherwise) and, with max_pods_per_node, the owning
-// lane sets the node's FULL bit once the count reaches it, so later pods see it infeasible.
-// Without a capacity a commit changes nothing a later pod reads, so with NW > 1 a dedicated
-// FINALIZER wave decodes, keeps the outputs and commits while the scanners go on; the barrier per
-// pod still orders every commit before the next pod is decided.
+// (atomic min) behind one LDS-only barrier. Then decode, output and commit. With
+// max_pods_per_node the commit is per pod: the node's pod count (an LDS table when it fits, device
+// memory otherwise) and the owning lane sets the node's FULL bit once the count reaches it, so
+// later pods see it infeasible. Without a capacity a commit changes nothing a later pod reads:
+// one wave decides U = 4 pods per step (independent scan chains, interleaved word by word), with
+// NW > 1 a dedicated FINALIZER wave decodes and keeps the outputs while the scanners go on, and
+// the counts of a block of 64 placements are committed together when the block's outputs leave.
 // Nothing inside the per-pod loop waits on memory: the barrier fences LDS only (a plain
 // __syncthreads() is a workgroup fence over global memory too, `s_waitcnt vmcnt(0)`); outputs
-// collect in lanes (lane jl holds pod j0 + jl) and leave as one coalesced store per 64 pods; the
-// next 64 pods' bytes are requested one block ahead.
+// collect in lanes (lane jl holds pod j0 + jl, two v_writelane_b32 per pod) and leave as one
+// coalesced store per 64 pods; the next 64 pods' bytes are requested one block ahead.
+// Issue cost: a wave alone on its SIMD issues one instruction per ~4 cycles of any kind, so the
+// per-pod instruction count (VALU and SALU alike) is the latency: 55 per pod at RS = 3 without a
+// capacity (profiles/r2_pmc_c3.json, SQ_INSTS_* of the C5 launch).
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -451,16 +455,34 @@ __device__ __forceinline__ uint32_t wave_first(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, __builtin_ctzll(m));
 }
 
-// One commit of a pod count (no return value waited for): a plain ds_add_u32 from the calling
-// lane. Written as asm: the backend's atomic optimizer turns a single-lane atomicAdd into an
-// mbcnt / bcnt sequence and two more exec-mask branches per pod.
-__device__ __forceinline__ void lds_add(uint32_t lds_addr, uint32_t v) {
-  asm volatile("ds_add_u32 %0, %1" ::"v"(lds_addr), "v"(v) : "memory");
+// t | (d ^ p) and ~(t | (x & m)) in one v_bitop3_b32 each, with the pod's mask p / m wave-uniform
+// (SGPR) and the node planes in VGPRs: the sequential kernel's form of or_xor_s.
+__device__ __forceinline__ uint32_t or_xor_vs(uint32_t t, uint32_t d, uint32_t p) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xf6" : "=v"(r) : "v"(t), "v"(d), "s"(p));
+  return r;
 }
-// 32-bit LDS address of a __shared__ object (its offset in the workgroup's LDS)
-__device__ __forceinline__ uint32_t lds_addr(const int32_t* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int32_t*)p;
+__device__ __forceinline__ uint32_t nor_and_vs(uint32_t t, uint32_t x, uint32_t m) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x07" : "=v"(r) : "v"(t), "v"(x), "s"(m));
+  return r;
 }
+
+// a[lane] = va and b[lane] = vb for ONE lane (wave-uniform values and lane): two v_writelane_b32.
+// No builtin for it in this compiler. The lane select goes through M0 (a second SGPR operand
+// would break the constant-bus limit), and the s_nop covers the SALU-written select (a hazard the
+// backend does not see through inline asm).
+// (M0 is reserved: the backend never allocates it, and nothing else in this file uses it; the
+// clobber stays so that a later M0 user is not silently overwritten.)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void write_lane2(int32_t& a, int32_t& b, int32_t va, int32_t vb, int32_t lane) {
+  asm volatile("s_mov_b32 m0, %4\n\ts_nop 3\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
+               : "+v"(a), "+v"(b)
+               : "s"(va), "s"(vb), "s"(lane)
+               : "m0");
+}
+#pragma clang diagnostic pop
 
 // Lowest set bit (v_ffbl_b32): 0xFFFFFFFF when x == 0, so (base | ffbl(x)) is "no node" then.
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
@@ -482,9 +504,8 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   // feasible non-match]
   __shared__ uint32_t xs[3][3];
   extern __shared__ int32_t lcnt[];  // [n_pad] per-node pod counts (LDSC)
-  __shared__ int32_t ldummy[WAVE];    // branch-free commits: the other lanes add 0 here
   const int lane = threadIdx.x & (WAVE - 1);
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wv = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool scanner = !FIN || wv < NW;
 
   uint32_t D0[RS], D1[RS], D2[RS], D3[RS], XX[RS], VV[RS], FULL[RS];
@@ -525,11 +546,6 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     dr = a.pod_digit[jj];
     tr = a.pod_tol[jj];
   };
-  auto convert = [&](int32_t j0, int32_t dr, int32_t tr, uint32_t& pcl, uint32_t& tll) {
-    const bool ok = j0 + lane < a.n_pods;
-    pcl = (ok && dr >= 0 && dr <= 9) ? (uint32_t)dr : CODE_NONE_POD;
-    tll = (ok && tr != 0) ? 1u : 0u;
-  };
   // Loop-invariant arguments pinned in SGPRs: otherwise the backend re-loads them from the
   // kernel-argument segment inside the loop, and each reload's lgkmcnt wait lands in front of the
   // LDS exchange.
@@ -542,64 +558,98 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   const uint32_t ball1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.ball[1]);
   int32_t* counts = a.counts;
   const IdentDecode idec = make_ident_decode(pp);
+  // first feasible node of each pod class (no capacity: constant over the launch), -1 = none
+  const int32_t ia0 = ball0 ? (int32_t)(KMAX - ball0) : -1, ia1 = ball1 ? (int32_t)(KMAX - ball1) : -1;
+  // A pod's lane word: code | tolerates << 4 | class status << 5, where the class status is
+  // decode_ident's status, which without a capacity depends on the pod's class alone (FitError when
+  // the class has no feasible node, the NodeNumber score error for a pod without a digit): worked
+  // out here once per 64 pods by the lanes, not per pod by the scalar unit.
+  auto convert = [&](int32_t j0, int32_t dr, int32_t tr, uint32_t& pk) {
+    const bool ok = j0 + lane < a.n_pods;
+    const bool dig = ok && dr >= 0 && dr <= 9, tl = ok && tr != 0;
+    const bool fit = (tl ? ia1 : ia0) < 0;
+    const bool serr = !fit && (idec.err_all || (idec.err_nodigit && !dig));
+    const uint32_t st = fit ? 1u : (serr ? 2u : 0u);
+    pk = (dig ? (uint32_t)dr : CODE_NONE_POD) | (tl ? 16u : 0u) | (st << 5);
+  };
   const uint32_t lane_base = (uint32_t)((wv * WAVE + lane) * RS) << 5;  // node index of bit 0 of slot 0's word
-  uint32_t pcv = CODE_NONE_POD, tolv = 0;
+  // the one non-zero score a decode can give (decode_ident: weight x 10 or 100; decode_pod: x 100)
+  const int64_t sm = KX ? 100 * pp.weight : idec.sm;
+  uint32_t pkv = CODE_NONE_POD;  // lane jl: pod j0 + jl's code | tolerates << 4
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
-  int32_t o_idx = -1, o_st = 0;  // wave FINW: lane jl holds pod j0 + jl of the current block
-  int64_t o_sc = 0;
+  // wave FINW: lane jl holds pod j0 + jl's node and status | scored << 2 (one v_writelane each per
+  // pod); the score and status arrays are expanded from them once per 64 pods
+  int32_t o_idx = -1;
+  int32_t o_code = 0;
   auto store_block = [&](int32_t j0, int32_t cnt) {  // wave FINW: one coalesced store per array
     if (lane < cnt) {
+      const int32_t st = o_code & 3;
       a.out_idx[j0 + lane] = o_idx;
-      a.out_score[j0 + lane] = o_sc;
-      a.out_status[j0 + lane] = o_st;
+      a.out_score[j0 + lane] = (o_code & 4) ? sm : 0;
+      a.out_status[j0 + lane] = st;
+      // Without a capacity no decision reads a count, so the block's placements are committed
+      // here, one atomic per lane (NodeInfo.AddPod analogue), instead of one per pod.
+      if (!CAP && st == 0) {
+        if (LDSC) atomicAdd(&lcnt[o_idx], 1);
+        else atomicAdd(&counts[o_idx], 1);
+      }
     }
   };
   for (int32_t j = 0; j < a.n_pods; j += U) {
     if ((j & (WAVE - 1)) == 0) {
       // order matters for vmcnt (in-order): the conversion waits only for the loads issued one
       // block ago, then the previous block's results leave, then the next block is requested
-      convert(j, dn, tn, pcv, tolv);
+      convert(j, dn, tn, pkv);
       if (wv == FINW && j > 0) store_block(j - WAVE, WAVE);
       load_raw(j + WAVE, dn, tn);
     }
     // ---- decide: the U pods' scans (U > 1 only without a capacity, where no commit feeds a
-    // later decision: independent chains, the same reordering as round 1's finalizer wave) ----
-    uint32_t pcu[U], tolu[U], cmu[U], cau[U], cxu[U];
+    // later decision: independent chains, interleaved word by word) ----
+    uint32_t pku[U], p0[U], p1[U], p2[U], p3[U], ntu[U], cmu[U], cau[U], cxu[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int jl = (j + u) & (WAVE - 1);
-      pcu[u] = (uint32_t)__builtin_amdgcn_readlane((int)pcv, jl);
-      tolu[u] = (uint32_t)__builtin_amdgcn_readlane((int)tolv, jl);
-      const uint32_t pc = pcu[u];
+      pku[u] = (uint32_t)__builtin_amdgcn_readlane((int)pkv, (j + u) & (WAVE - 1));
       // the pod's code bits as all-ones / all-zero masks, and ~tolerates: wave-uniform (SGPRs)
-      const uint32_t p0 = 0u - (pc & 1u), p1 = 0u - ((pc >> 1) & 1u), p2 = 0u - ((pc >> 2) & 1u), p3 = 0u - (pc >> 3);
-      const uint32_t nT = tolu[u] ? 0u : 0xFFFFFFFFu;
-      uint32_t cm = NONE, ca = NONE, cx = NONE;  // this lane's first match / feasible / non-match
-      if (scanner) {
+      p0[u] = 0u - (pku[u] & 1u);
+      p1[u] = 0u - ((pku[u] >> 1) & 1u);
+      p2[u] = 0u - ((pku[u] >> 2) & 1u);
+      p3[u] = 0u - ((pku[u] >> 3) & 1u);
+      ntu[u] = ((pku[u] >> 4) & 1u) - 1u;
+      cmu[u] = cau[u] = cxu[u] = NONE;  // this lane's first match / feasible / non-match
+    }
+    if (scanner) {
 #pragma unroll
-        for (int r = RS - 1; r >= 0; --r) {  // slots ascend in List order per lane
-          const uint32_t dm = (D0[r] ^ p0) | (D1[r] ^ p1) | (D2[r] ^ p2) | (D3[r] ^ p3);
-          const uint32_t bad = (XX[r] & nT) | (CAP ? FULL[r] : 0u);
-          const uint32_t base = lane_base + (uint32_t)(r * 32);
-          cm = umin(cm, base | ffbl(~(dm | bad)));
-          if (CAP) ca = umin(ca, base | ffbl(VV[r] & ~bad));
-          if (KX) cx = umin(cx, base | ffbl(VV[r] & ~bad & dm));
+      for (int r = RS - 1; r >= 0; --r) {  // slots ascend in List order per lane
+        const uint32_t base = lane_base + (uint32_t)(r * 32);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          uint32_t dm = D0[r] ^ p0[u];
+          dm = or_xor_vs(dm, D1[r], p1[u]);
+          dm = or_xor_vs(dm, D2[r], p2[u]);
+          dm = or_xor_vs(dm, D3[r], p3[u]);
+          if constexpr (!CAP && !KX) {
+            cmu[u] = umin(cmu[u], base | ffbl(nor_and_vs(dm, XX[r], ntu[u])));
+          } else {
+            const uint32_t bad = (XX[r] & ntu[u]) | (CAP ? FULL[r] : 0u);
+            cmu[u] = umin(cmu[u], base | ffbl(~(dm | bad)));
+            if (CAP) cau[u] = umin(cau[u], base | ffbl(VV[r] & ~bad));
+            if (KX) cxu[u] = umin(cxu[u], base | ffbl(VV[r] & ~bad & dm));
+          }
         }
-        cm = wave_first(cm);
-        if (CAP) ca = wave_first(ca);
-        if (KX) cx = wave_first(cx);
       }
-      cmu[u] = cm;
-      cau[u] = ca;
-      cxu[u] = cx;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        cmu[u] = wave_first(cmu[u]);
+        if (CAP) cau[u] = wave_first(cau[u]);
+        if (KX) cxu[u] = wave_first(cxu[u]);
+      }
     }
     // ---- then, in pod order: exchange (NW > 1), decode, output, commit ----
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool valid = U == 1 || j + u < a.n_pods;  // wave-uniform: the tail step's pods past the batch
       const int jl = (j + u) & (WAVE - 1);
-      const uint32_t pc = pcu[u], tol = tolu[u];
+      const uint32_t pc = pku[u] & 15u, tol = pku[u] >> 4;
       uint32_t cm = cmu[u], ca = cau[u], cx = cxu[u];
       if constexpr (NW > 1) {
         // lane 0 of every scanning wave folds its wave's result into this pod's slot; after the
@@ -625,44 +675,37 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
           xs[sr][2] = NONE;
         }
       }
-      const int64_t im = cm != NONE ? (int64_t)cm : -1;
-      const int64_t ia = CAP ? (ca != NONE ? (int64_t)ca : -1) : key_to_idx(tol ? ball1 : ball0);
-      int32_t sel, st;
-      int64_t sc;
-      if (KX)
-        decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pc != CODE_NONE_POD, pp, &sel, &sc, &st);
-      else
-        decode_ident(im, ia, pc != CODE_NONE_POD, idec, &sel, &sc, &st);
-      if (wv == FINW) {
-        const bool mine = lane == jl;
-        o_idx = mine ? sel : o_idx;
-        o_sc = mine ? sc : o_sc;
-        o_st = mine ? st : o_st;
+      int32_t sel, st, code;
+      if constexpr (!CAP && !KX) {  // decode_ident with the class status from the lane word
+        st = (int32_t)((pku[u] >> 5) & 3u);
+        const bool hit = idec.use_im && cm != NONE;
+        sel = st ? -1 : (hit ? (int32_t)cm : (tol ? ia1 : ia0));
+        code = st | ((hit && st == 0) ? 4 : 0);
+      } else {
+        const int64_t im = cm != NONE ? (int64_t)cm : -1;
+        const int64_t ia = CAP ? (ca != NONE ? (int64_t)ca : -1) : (int64_t)(tol ? ia1 : ia0);
+        int64_t sc;
+        if (KX)
+          decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pc != CODE_NONE_POD, pp, &sel, &sc, &st);
+        else
+          decode_ident(im, ia, pc != CODE_NONE_POD, idec, &sel, &sc, &st);
+        code = st | (sc != 0 ? 4 : 0);
       }
-      if (!CAP && LDSC) {
-        // commit (NodeInfo.AddPod analogue), branch-free: lane 0 adds 1 to the node's count (0 to
-        // node 0 when the pod is not placed), the other lanes add 0 to slots of their own
-        const bool placed = valid && st == 0;
-        const uint32_t node = lds_addr(lcnt) + 4u * (uint32_t)(placed ? sel : 0);
-        lds_add(lane == 0 ? node : lds_addr(ldummy) + 4u * (uint32_t)lane, (lane == 0 && placed) ? 1u : 0u);
-      } else if (valid && st == 0) {  // commit
-        if (!CAP) {
-          if (lane == 0) atomicAdd(&counts[sel], 1);  // no return value waited for
-        } else {
-          const uint32_t w = (uint32_t)sel >> 5, q = w / RS;
-          if ((int)(q / WAVE) == wv) {  // the owning wave
-            int32_t old = 0;
-            if (lane == 0) old = LDSC ? atomicAdd(&lcnt[sel], 1) : atomicAdd(&counts[sel], 1);
-            const bool full = __builtin_amdgcn_readfirstlane(old) + 1 >= max_pods;
-            if (full) {
-              // the owning lane: the register by a wave-uniform index (scalar branches), the lane
-              // by a compare
-              const int rs = (int)(w % RS);
-              const uint32_t bit = (lane == (int)(q % WAVE)) ? (1u << (sel & 31)) : 0u;
+      if (wv == FINW) write_lane2(o_idx, o_code, sel, code, jl);
+      if (CAP && st == 0) {  // commit, seen by the next pod's decision
+        const uint32_t w = (uint32_t)sel >> 5, q = w / RS;
+        if ((int)(q / WAVE) == wv) {  // the owning wave
+          int32_t old = 0;
+          if (lane == 0) old = LDSC ? atomicAdd(&lcnt[sel], 1) : atomicAdd(&counts[sel], 1);
+          const bool full = __builtin_amdgcn_readfirstlane(old) + 1 >= max_pods;
+          if (full) {
+            // the owning lane: the register by a wave-uniform index (scalar branches), the lane
+            // by a compare
+            const int rs = (int)(w % RS);
+            const uint32_t bit = (lane == (int)(q % WAVE)) ? (1u << (sel & 31)) : 0u;
 #pragma unroll
-              for (int r = 0; r < RS; ++r)
-                if (r == rs) FULL[r] |= bit;
-            }
+            for (int r = 0; r < RS; ++r)
+              if (r == rs) FULL[r] |= bit;
           }
         }
       }
