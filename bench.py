@@ -379,43 +379,62 @@ def make_roofline(mode, n_local, p, kernel_ms, kernel_ms_isolated, nstreams, cus
     kern_s, iso_s = kernel_ms * 1e-3, kernel_ms_isolated * 1e-3
     pmc = load_json(PMC_FILE) or {}
     if mode == "sequential":
+        # One wave decides the pods in order; alone on its SIMD it issues about one instruction per
+        # 4 cycles of any kind (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so the floor
+        # of the per-pod latency is its instruction count (VALU + SALU, counted by rocprofv3 for
+        # this kernel at C5) x 4 cycles at 2.4 GHz.
         kname = seq_kernel_label(n_local)
         entry = pmc.get("kernels", {}).get("sequential", {})
-        return {"bound": "latency", "achieved": kernel_ms * 1e3 / p, "peak": None, "unit": "us/pod (serial)",
-                "frac": None, "kernel": kname, "kernel_ms": kernel_ms,
-                "traffic": entry.get("hbm_bytes_per_launch") if entry.get("kernel") == kname else None,
-                "note": "one pod at a time: scan (5 VALU per 32 nodes per lane) + DPP min + commit per pod"}
+        ok = entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
+        instr = (entry.get("SQ_INSTS_VALU", 0) + entry.get("SQ_INSTS_SALU", 0)) / p if ok else None
+        floor_us = instr * 4 / 2.4e3 if instr else None
+        achieved = kernel_ms * 1e3 / p
+        return {"bound": "issue latency (one wave)", "achieved": achieved, "peak": floor_us,
+                "unit": "us/pod (serial)", "frac": floor_us / achieved if floor_us else None,
+                "kernel": kname, "kernel_ms": kernel_ms,
+                "traffic": entry.get("hbm_bytes_per_launch") if ok else None,
+                "instructions_per_pod": instr,
+                "note": "peak = instructions per pod (rocprofv3 SQ_INSTS_VALU + SQ_INSTS_SALU / pods, "
+                        "profiles/r2_pmc_c3.json) x 4 cycles / 2.4 GHz; frac = that floor / measured us per pod"}
     kname = bits_kernel_label(n_local, p, cus, shard=mode == "nodeshard")
     evals = float(n_local) * p
     entry = pmc.get("kernels", {}).get("batch", {})
     pmc_ok = entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
+    # achieved = ALGORITHMIC lane-ops (the scan's instruction model: 46 VALU per 8 words per 64
+    # pods) / launch interval; next to it the counter-derived figure (SQ_INSTS_VALU x 64 of the
+    # same kernel at the same size, profiles/r2_pmc_c3.json), which adds the per-wave prologue,
+    # first-node decode, slice merge and epilogue
     model_ops = LANE_OPS_PER_EVAL * evals
     valu_instr = entry.get("SQ_INSTS_VALU") if pmc_ok else None
-    lane_ops = valu_instr * 64 if valu_instr else model_ops
+    counter_ops = valu_instr * 64 if valu_instr else None
     ceiling = measured_bitop3_ceiling()
     uniq_bytes = 0.75 * n_local + 18.0 * p         # bit planes + pod records + outputs, once
     survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts L1/L2 re-reads)
     return {
         "bound": "valu",
-        "achieved": lane_ops / kern_s / 1e9,
+        "achieved": model_ops / kern_s / 1e9,
         "peak": VALU_PEAK_LANE_OPS / 1e9,
         "unit": "Glane-op/s",
-        "frac": lane_ops / kern_s / VALU_PEAK_LANE_OPS,
+        "frac": model_ops / kern_s / VALU_PEAK_LANE_OPS,
         "traffic": entry.get("hbm_bytes_per_launch") if pmc_ok else None,
+        "traffic_note": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024), same kernel and size",
         "kernel": kname,
         "kernel_ms": kernel_ms,
         "kernel_ms_note": (f"interval at which launches complete with {nstreams} streams in flight; "
                            "kernel_ms_isolated = the same launches back to back on one stream "
                            "(= rocprofv3's per-kernel average)") if nstreams > 1 else "one stream",
         "kernel_ms_isolated": kernel_ms_isolated,
-        "frac_isolated": lane_ops / iso_s / VALU_PEAK_LANE_OPS,
-        "lane_ops_source": "rocprofv3 SQ_INSTS_VALU x 64 per launch (profiles/r2_pmc_c3.json)" if valu_instr
-                           else "instruction model (no matching PMC file)",
-        "valu_lane_ops_per_eval_measured": valu_instr * 64 / evals if valu_instr else None,
+        "frac_isolated": model_ops / iso_s / VALU_PEAK_LANE_OPS,
         "valu_lane_ops_per_eval_model": LANE_OPS_PER_EVAL,
-        "scan_share_of_valu": model_ops / lane_ops if valu_instr else None,
+        "valu_lane_ops_per_eval_measured": valu_instr * 64 / evals if valu_instr else None,
+        "frac_counter": counter_ops / kern_s / VALU_PEAK_LANE_OPS if counter_ops else None,
+        "counter_source": ("rocprofv3 SQ_INSTS_VALU x 64 per launch (profiles/r2_pmc_c3.json)" if valu_instr
+                           else "no PMC entry for this kernel and size"),
+        "scan_share_of_valu": model_ops / counter_ops if counter_ops else None,
         "measured_bitop3_ceiling": ceiling / 1e9 if ceiling else None,
-        "frac_vs_measured_bitop3_ceiling": (lane_ops / kern_s / ceiling) if ceiling else None,
+        "frac_counter_vs_measured_bitop3_ceiling": (counter_ops / kern_s / ceiling) if (ceiling and counter_ops) else None,
+        "peak_note": "peak = FP32 vector 157.3 TF / 2 (one lane-op per lane per 2-cycle wave64 issue); the scan's "
+                     "v_bitop3 with an SGPR plane issues every ~4 cycles (measured_bitop3_ceiling)",
         "hbm": {"bound": "hbm", "achieved": uniq_bytes / kern_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": uniq_bytes / kern_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
                 "survey_8d_bytes_per_launch": survey_bytes,
@@ -512,7 +531,8 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     ok = same(g, want) and (counts == 3 * np.bincount(g[0][placed], minlength=n)).all()
     out["c5_sequential"] = {"kernel": seq_kernel_label(n), "ms_per_step": ms, "us_per_pod": ms * 1e3 / p,
                             "pods_per_s": p / (ms * 1e-3), "evals_per_s": n * p / (ms * 1e-3),
-                            "check": ("seq == batch (closed form), node counts == 3 x placements" if ok else "MISMATCH")}
+                            "check": ("seq == batch (closed form), node counts == 3 x placements" if ok else "MISMATCH"),
+                            "roofline": make_roofline("sequential", n, p, ms, ms, 1, cus)}
     ctx.close()
 
     # ---- C2: 1k x 10k ----
