@@ -118,16 +118,21 @@ class Streams:
         self.torch = torch
         self.main = torch.cuda.current_stream(dev)
         self.all = [self.main] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+        # fork / join events made once and reused: a torch Event creates its HIP event on its first
+        # record, a few microseconds that would otherwise land inside every timed region
+        self.fork_ev = torch.cuda.Event()
+        self.join_evs = [torch.cuda.Event() for _ in self.all[1:]]
+        self.fork()
+        self.join()
+        torch.cuda.synchronize()
 
     def fork(self):
-        ev = self.torch.cuda.Event()
-        ev.record(self.main)
+        self.fork_ev.record(self.main)
         for st in self.all[1:]:
-            st.wait_event(ev)
+            st.wait_event(self.fork_ev)
 
     def join(self):
-        for st in self.all[1:]:
-            ev = self.torch.cuda.Event()
+        for st, ev in zip(self.all[1:], self.join_evs):
             ev.record(st)
             self.main.wait_event(ev)
 
@@ -206,11 +211,12 @@ def main():
     klen = ctx.shard_keys_len(p) if mode == "nodeshard" else 0  # int32 keys one step all-reduces
     S = Streams(torch, dev, nstreams)
 
-    # Batch steps call the C entry point with each buffer's pointers taken once (a Python method
-    # wrapper and five data_ptr() calls per step cost ~1 us next to a ~3 us launch).
-    batch_fn, handle = ctx._lib.msh_schedule_batch_device, ctx.handle
+    # Batch steps call the C entry point through the fast-call module (csrc/msh_pyfast.c) with each
+    # buffer's pointers taken once: a Python method wrapper, five data_ptr() calls and ctypes
+    # conversions cost ~1-2 us per step next to a ~2.6 us launch.
+    batch_fn, handle = ctx._fast.schedule_batch_device, ctx._hv()
     batch_args = [(handle, p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["idx"].data_ptr(), b["score"].data_ptr(),
-                   b["status"].data_ptr(), st.cuda_stream) for b, st in zip(bufs, S.all)]
+                   b["status"].data_ptr(), st.cuda_stream or None) for b, st in zip(bufs, S.all)]
 
     def step(k, ev0=None, ev1=None, single=False):
         b = bufs[0] if single else bufs[k % nstreams]
@@ -221,7 +227,7 @@ def main():
         if mode == "batch":
             ba = batch_args[0] if single else batch_args[k % nstreams]
             if single:
-                ba = ba[:7] + (sh,)
+                ba = ba[:7] + (sh or None,)
             rc = batch_fn(*ba)
             if rc:
                 ctx._check(rc)
@@ -254,6 +260,10 @@ def main():
     per_step = mode == "nodeshard"
     evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
            if per_step else [(None, None)] * args.steps)
+    for e0, e1 in evs:  # create the HIP events before the timed region
+        if e0 is not None:
+            e0.record(S.main)
+            e1.record(S.main)
     # Graph launch (batch mode, A/B): the K steps -- the same K launches over the same streams --
     # captured once, untimed, and replayed once in the timed region.
     graph = None
@@ -273,6 +283,12 @@ def main():
             S.main, S.all = saved
         torch.cuda.synchronize()
     r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    r0.record(S.main)  # create both HIP events before the timed region
+    r1.record(S.main)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     r0.record(S.main)
     if graph is not None:

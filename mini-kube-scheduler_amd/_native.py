@@ -149,6 +149,26 @@ def lib() -> C.CDLL:
     return _LIB
 
 
+_FAST = None
+
+
+def fast():
+    """The CPython fast-call module (csrc/msh_pyfast.c) for the per-batch device entry points;
+    it links this package's libminisched_hip.so. Raises if it is missing: no fallback path."""
+    global _FAST
+    if _FAST is None:
+        lib()  # the HIP runtime shared with torch, and the library, loaded first
+        import importlib.util
+        path = next(LIB_PATH.parent.glob("_msh_fast*.so"), None)
+        if path is None:
+            raise RuntimeError(f"_msh_fast*.so is missing next to {LIB_PATH}: build it with __graft_entry__.build()")
+        spec = importlib.util.spec_from_file_location("_msh_fast", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _FAST = mod
+    return _FAST
+
+
 def ptr(a: np.ndarray | None):
     """Host numpy array -> void* (None for an absent optional array)."""
     if a is None:

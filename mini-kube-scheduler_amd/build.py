@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 import shutil
 import subprocess
+import sysconfig
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -45,9 +46,16 @@ def _stale(target: Path, deps: list[Path]) -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile the kernels + C-ABI for gfx950 and link libminisched_hip.so."""
+    """Compile the kernels + C-ABI for gfx950, link libminisched_hip.so, and the CPython
+    fast-call module on top of it."""
+    _build_lib(force, verbose)
+    build_fast(force, verbose)
+    return LIB
+
+
+def _build_lib(force: bool, verbose: bool) -> None:
     if not force and not _stale(LIB, [CSRC / src for src, _, _ in SOURCES] + HEADERS):
-        return LIB  # up to date (objects need not be present, e.g. on the GPU box)
+        return  # up to date (objects need not be present, e.g. on the GPU box)
     OBJ.mkdir(exist_ok=True)
     objs = []
     for src, cc, extra in SOURCES:
@@ -70,7 +78,23 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-    return LIB
+
+
+FAST_SRC = CSRC / "msh_pyfast.c"
+FAST = PKG_DIR / ("_msh_fast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+
+
+def build_fast(force: bool = False, verbose: bool = False) -> Path:
+    """The CPython fast-call module for the per-batch device entry points (msh_pyfast.c)."""
+    if not force and not _stale(FAST, [FAST_SRC, LIB, INCLUDE / "minisched_hip.h"]):
+        return FAST
+    cmd = ["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-Wextra",
+           f"-I{sysconfig.get_paths()['include']}", f"-I{INCLUDE}", str(FAST_SRC),
+           f"-L{PKG_DIR}", "-lminisched_hip", "-Wl,-rpath,$ORIGIN", "-o", str(FAST)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return FAST
 
 
 DEMO = PKG_DIR / "abi_demo"

@@ -1,0 +1,116 @@
+/* msh_pyfast.c — CPython fast-call bindings for the per-batch device entry points of
+ * include/minisched_hip.h, for the Python host mirror (scheduler.DeviceContext) and bench.py.
+ *
+ * A device entry point costs ~2.6 us of host time (a HIP kernel launch, profiles/ab/
+ * r2_submit_cost.jsonl); through ctypes the Python side added ~0.9 us per call on top (argument
+ * conversion of eight parameters). These METH_FASTCALL wrappers take plain ints (the ctx handle,
+ * device pointers, the stream handle) and call the C ABI directly. They do not replace the ABI:
+ * everything else goes through ctypes (_native.py), and a cgo caller binds the C functions.
+ * Build (mini-kube-scheduler_amd/build.py): gcc -shared against libminisched_hip.so. */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include "../../include/minisched_hip.h"
+
+/* int (or None) -> pointer; -1 with a Python error set on failure */
+static int as_ptr(PyObject* o, void** out) {
+  if (o == Py_None) {
+    *out = NULL;
+    return 0;
+  }
+  *out = PyLong_AsVoidPtr(o);
+  return PyErr_Occurred() ? -1 : 0;
+}
+
+static int as_i64(PyObject* o, long long* out) {
+  *out = PyLong_AsLongLong(o);
+  return PyErr_Occurred() ? -1 : 0;
+}
+
+static int want_args(Py_ssize_t n, Py_ssize_t want, const char* name) {
+  if (n == want) return 0;
+  PyErr_Format(PyExc_TypeError, "%s takes %zd arguments (%zd given)", name, want, n);
+  return -1;
+}
+
+/* schedule_batch_device(ctx, p, d_pod_digit, d_pod_tol, d_out_idx, d_out_score, d_out_status,
+ * stream) -> rc */
+static PyObject* py_schedule_batch_device(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  void *ctx, *pd, *pt, *oi, *os, *ost, *st;
+  long long p;
+  if (want_args(n, 8, "schedule_batch_device") || as_ptr(a[0], &ctx) || as_i64(a[1], &p) ||
+      as_ptr(a[2], &pd) || as_ptr(a[3], &pt) || as_ptr(a[4], &oi) || as_ptr(a[5], &os) ||
+      as_ptr(a[6], &ost) || as_ptr(a[7], &st))
+    return NULL;
+  if (p < INT32_MIN || p > INT32_MAX) return PyErr_Format(PyExc_OverflowError, "pod count out of range");
+  const int rc = msh_schedule_batch_device((msh_ctx*)ctx, (int32_t)p, (const int8_t*)pd, (const uint8_t*)pt,
+                                           (int32_t*)oi, (int64_t*)os, (int32_t*)ost, st);
+  return PyLong_FromLong(rc);
+}
+
+/* schedule_sequential_device(ctx, p, d_pod_digit, d_pod_tol, max_pods_per_node, d_out_idx,
+ * d_out_score, d_out_status, stream) -> rc */
+static PyObject* py_schedule_sequential_device(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  void *ctx, *pd, *pt, *oi, *os, *ost, *st;
+  long long p, cap;
+  if (want_args(n, 9, "schedule_sequential_device") || as_ptr(a[0], &ctx) || as_i64(a[1], &p) ||
+      as_ptr(a[2], &pd) || as_ptr(a[3], &pt) || as_i64(a[4], &cap) || as_ptr(a[5], &oi) ||
+      as_ptr(a[6], &os) || as_ptr(a[7], &ost) || as_ptr(a[8], &st))
+    return NULL;
+  if (p < INT32_MIN || p > INT32_MAX || cap < INT32_MIN || cap > INT32_MAX)
+    return PyErr_Format(PyExc_OverflowError, "argument out of range");
+  const int rc = msh_schedule_sequential_device((msh_ctx*)ctx, (int32_t)p, (const int8_t*)pd, (const uint8_t*)pt,
+                                                (int32_t)cap, (int32_t*)oi, (int64_t*)os, (int32_t*)ost, st);
+  return PyLong_FromLong(rc);
+}
+
+/* shard_keys_device(ctx, p, d_pod_digit, d_pod_tol, node_base, d_keys, stream) -> rc */
+static PyObject* py_shard_keys_device(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  void *ctx, *pd, *pt, *keys, *st;
+  long long p, base;
+  if (want_args(n, 7, "shard_keys_device") || as_ptr(a[0], &ctx) || as_i64(a[1], &p) || as_ptr(a[2], &pd) ||
+      as_ptr(a[3], &pt) || as_i64(a[4], &base) || as_ptr(a[5], &keys) || as_ptr(a[6], &st))
+    return NULL;
+  if (p < INT32_MIN || p > INT32_MAX) return PyErr_Format(PyExc_OverflowError, "pod count out of range");
+  const int rc = msh_shard_keys_device((msh_ctx*)ctx, (int32_t)p, (const int8_t*)pd, (const uint8_t*)pt,
+                                       (int64_t)base, (int32_t*)keys, st);
+  return PyLong_FromLong(rc);
+}
+
+/* decode_keys_device(ctx, p, d_pod_digit, d_pod_tol, d_keys, d_out_idx, d_out_score,
+ * d_out_status, stream) -> rc */
+static PyObject* py_decode_keys_device(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  void *ctx, *pd, *pt, *keys, *oi, *os, *ost, *st;
+  long long p;
+  if (want_args(n, 9, "decode_keys_device") || as_ptr(a[0], &ctx) || as_i64(a[1], &p) || as_ptr(a[2], &pd) ||
+      as_ptr(a[3], &pt) || as_ptr(a[4], &keys) || as_ptr(a[5], &oi) || as_ptr(a[6], &os) || as_ptr(a[7], &ost) ||
+      as_ptr(a[8], &st))
+    return NULL;
+  if (p < INT32_MIN || p > INT32_MAX) return PyErr_Format(PyExc_OverflowError, "pod count out of range");
+  const int rc = msh_decode_keys_device((msh_ctx*)ctx, (int32_t)p, (const int8_t*)pd, (const uint8_t*)pt,
+                                        (const int32_t*)keys, (int32_t*)oi, (int64_t*)os, (int32_t*)ost, st);
+  return PyLong_FromLong(rc);
+}
+
+static PyMethodDef methods[] = {
+    {"schedule_batch_device", (PyCFunction)(void (*)(void))py_schedule_batch_device, METH_FASTCALL,
+     "msh_schedule_batch_device(ctx, p, pod_digit, pod_tol, out_idx, out_score, out_status, stream) -> rc"},
+    {"schedule_sequential_device", (PyCFunction)(void (*)(void))py_schedule_sequential_device, METH_FASTCALL,
+     "msh_schedule_sequential_device(ctx, p, pod_digit, pod_tol, max_pods_per_node, out_idx, out_score, "
+     "out_status, stream) -> rc"},
+    {"shard_keys_device", (PyCFunction)(void (*)(void))py_shard_keys_device, METH_FASTCALL,
+     "msh_shard_keys_device(ctx, p, pod_digit, pod_tol, node_base, keys, stream) -> rc"},
+    {"decode_keys_device", (PyCFunction)(void (*)(void))py_decode_keys_device, METH_FASTCALL,
+     "msh_decode_keys_device(ctx, p, pod_digit, pod_tol, keys, out_idx, out_score, out_status, stream) -> rc"},
+    {NULL, NULL, 0, NULL},
+};
+
+static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_msh_fast",
+                                    "Fast-call bindings of the per-batch device entry points", -1, methods,
+                                    NULL, NULL, NULL, NULL};
+
+PyMODINIT_FUNC PyInit__msh_fast(void) { return PyModule_Create(&module); }

@@ -26,6 +26,24 @@ def test_library_exports_every_declared_symbol(msh):
         assert hasattr(lib, name), name
 
 
+def test_fast_call_module(msh):
+    """The CPython fast-call module (csrc/msh_pyfast.c) loads against the same library, exposes
+    the four per-batch device entry points, and passes a NULL ctx through to the ABI's own check
+    (MSH_ERR_INVALID, no device call)."""
+    fast = msh._native.fast()
+    names = ["schedule_batch_device", "schedule_sequential_device", "shard_keys_device", "decode_keys_device"]
+    assert all(callable(getattr(fast, n)) for n in names)
+    inv = msh._native.MSH_ERR_INVALID
+    assert fast.schedule_batch_device(None, 0, None, None, None, None, None, None) == inv
+    assert fast.schedule_sequential_device(None, 0, None, None, 0, None, None, None, None) == inv
+    assert fast.shard_keys_device(None, 0, None, None, 0, None, None) == inv
+    assert fast.decode_keys_device(None, 0, None, None, None, None, None, None, None) == inv
+    with pytest.raises(TypeError):
+        fast.schedule_batch_device(None, 0)
+    with pytest.raises(OverflowError):
+        fast.schedule_batch_device(None, 1 << 40, None, None, None, None, None, None)
+
+
 def test_abi_version(msh):
     header = (ROOT / "include" / "minisched_hip.h").read_text()
     assert f"#define MSH_ABI_VERSION {msh._native.lib().msh_abi_version()}" in header

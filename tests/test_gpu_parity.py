@@ -381,10 +381,9 @@ def test_determinism_device_entry(msh, gpu_ctx, oracle, synth):
 
 @pytest.mark.parametrize("n,norm", [(5000, 0), (100_000, 0), (100_000, 3), (20_000, 2)])
 def test_pipelined_streams(msh, gpu_ctx, oracle, n, norm):
-    """Independent batches in flight on several HIP streams of ONE ctx, as bench.py pipelines them:
-    the multi-tile work-queue kernel (100k nodes) and the compare/select kernel whose running
-    results live in per-ctx scratch (REVERSE / MINMAX above 16,384 nodes) must give every batch
-    the oracle's answer."""
+    """Independent batches in flight on several HIP streams of ONE ctx, as bench.py pipelines them,
+    in the identity and the KX modes, at several slice counts: every batch gets the oracle's
+    answer (no per-ctx scratch is shared between launches)."""
     torch = pytest.importorskip("torch")
     rng = np.random.default_rng(n + norm)
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, norm)
@@ -409,6 +408,44 @@ def test_pipelined_streams(msh, gpu_ctx, oracle, n, norm):
     for (pd, pt), (_, (oi, osc, ost)) in zip(batches, outs):
         want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
         _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"n={n} norm={norm}")
+
+
+@pytest.mark.parametrize("change", ["patch", "upload"])
+def test_table_change_while_batches_in_flight(msh, gpu_ctx, oracle, change):
+    """msh_patch_nodes / msh_upload_nodes while batches queued on other streams still read the
+    planes: the table is rebuilt only after the device has drained (prepare() and the upload /
+    patch calls wait for it), so the queued batches see the old table and later ones the new."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(77)
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    n = 20_000
+    u, nd, _, _ = _rand_case(rng, n, 1, p_unsched=0.2)
+    gpu_ctx.upload_nodes(u, nd)
+    dev = torch.device("cuda:0")
+    side = torch.cuda.Stream(dev)
+    _, _, pd, pt = _rand_case(rng, 1, 200_000, p_tol=0.3)
+    d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+    old = [(torch.empty(len(pd), dtype=torch.int32, device=dev), torch.empty(len(pd), dtype=torch.int64, device=dev),
+            torch.empty(len(pd), dtype=torch.int32, device=dev)) for _ in range(4)]
+    torch.cuda.synchronize()
+    for oi, osc, ost in old:  # queued, not waited for
+        gpu_ctx.schedule_batch_device(len(pd), d_pd.data_ptr(), d_pt.data_ptr(), oi.data_ptr(), osc.data_ptr(),
+                                      ost.data_ptr(), side.cuda_stream)
+    u2, nd2 = u.copy(), nd.copy()
+    idx = rng.choice(n, 6000, replace=False).astype(np.int32)
+    u2[idx] ^= 1
+    nd2[idx[:3000]] = rng.integers(-1, 10, 3000).astype(np.int8)
+    if change == "patch":
+        gpu_ctx.patch_nodes(idx, u2[idx], nd2[idx])
+    else:
+        gpu_ctx.upload_nodes(u2, nd2)
+    new = gpu_ctx.schedule_batch(pd, pt)
+    torch.cuda.synchronize()
+    want_old = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+    for oi, osc, ost in old:
+        _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want_old, f"{change}: queued batch")
+    _assert_same(new, oracle.c_schedule_batch(u2, nd2, pd, pt, ps, threads=8), f"{change}: after the change")
 
 
 def test_maximum_node_table(msh, gpu_ctx, synth):
