@@ -282,9 +282,14 @@ def main():
                 S.join()
             S.main, S.all = saved
         torch.cuda.synchronize()
-    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    r0.record(S.main)  # create both HIP events before the timed region
-    r1.record(S.main)
+    # r0 opens the region on the main stream and is the side streams' fork point; each stream
+    # closes with its own end event (the final synchronize waits for all of them): four event
+    # operations around the K launches, created before the region (a torch Event creates its HIP
+    # event on its first record)
+    r0 = torch.cuda.Event(enable_timing=True)
+    ends = [torch.cuda.Event(enable_timing=True) for _ in S.all]
+    for e in [r0] + ends:
+        e.record(S.main)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -294,12 +299,15 @@ def main():
     if graph is not None:
         with torch.cuda.stream(S.main):
             graph.replay()
+        ends[0].record(S.main)
+        ends = ends[:1]
     else:
-        S.fork()
+        for st in S.all[1:]:
+            st.wait_event(r0)
         for k, (e0, e1) in enumerate(evs):
             step(k, e0, e1)
-        S.join()
-    r1.record(S.main)
+        for st, e in zip(S.all, ends):
+            e.record(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -308,7 +316,7 @@ def main():
     if per_step:
         kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     else:
-        kernel_ms = r0.elapsed_time(r1) / args.steps
+        kernel_ms = max(r0.elapsed_time(e) for e in ends) / args.steps
 
     # Isolated launch time (outside the timed region): the same launches back to back on ONE
     # stream, which is what rocprofv3's per-kernel average measures.

@@ -13,6 +13,12 @@ import torch
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
+if os.environ.get("SPIN"):  # A/B: completion waits spin instead of yielding / sleeping
+    import ctypes
+    import importlib.util as _u
+    _hip = ctypes.CDLL(str(Path(_u.find_spec("torch").submodule_search_locations[0]) / "lib" / "libamdhip64.so"),
+                       mode=ctypes.RTLD_GLOBAL)
+    print(json.dumps({"hipSetDeviceFlags(spin)": _hip.hipSetDeviceFlags(int(os.environ["SPIN"]))}), flush=True)
 msh = importlib.import_module("mini-kube-scheduler_amd")
 synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
 K = int(os.environ.get("K", 20))
@@ -32,16 +38,20 @@ for i in range(NS):
          torch.empty(p, dtype=torch.int32, device=dev), torch.empty(p, dtype=torch.int64, device=dev),
          torch.empty(p, dtype=torch.int32, device=dev)]
     bufs.append(b)
-fn, h = ctx._lib.msh_schedule_batch_device, ctx.handle
-args = [(h, p, *[t.data_ptr() for t in b], st.cuda_stream) for b, st in zip(bufs, streams)]
+fn, h = ctx._fast.schedule_batch_device, ctx._hv()
+args = [(h, p, *[t.data_ptr() for t in b], st.cuda_stream or None) for b, st in zip(bufs, streams)]
+
+
+r0, r1, ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), torch.cuda.Event()
+jevs = [torch.cuda.Event() for _ in streams[1:]]
+for e in [r0, r1, ev] + jevs:
+    e.record(main)
 
 
 def region(k):
     torch.cuda.synchronize()
-    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t = [time.perf_counter()]
     r0.record(main)
-    ev = torch.cuda.Event()
     ev.record(main)
     for st in streams[1:]:
         st.wait_event(ev)
@@ -49,8 +59,7 @@ def region(k):
     for i in range(k):
         fn(*args[i % NS])
         t.append(time.perf_counter())
-    for st in streams[1:]:
-        e = torch.cuda.Event()
+    for st, e in zip(streams[1:], jevs):
         e.record(st)
         main.wait_event(e)
     r1.record(main)
