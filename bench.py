@@ -352,7 +352,7 @@ def main():
         extras = measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus)
 
     cpu = cpu_omp = None
-    if rank == 0 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:  # the contract: rank 0 at N=1 only
         pod_digit, pod_tol = batches[0]
         cpu = cpu_baseline(unsched, node_digit, pod_digit, pod_tol, args.cpu_seconds, mode)
         if mode != "sequential":
