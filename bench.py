@@ -158,11 +158,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MSH_BENCH_REHEARSE=1 (one-GPU rehearsal of the N>1 path only): every rank on device 0 and the
+    # process group on gloo, since RCCL refuses two ranks on one GPU. Never set for measurements.
+    rehearse = os.environ.get("MSH_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     # the rank's device first, so the process group (RCCL) binds its communicator to it
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
 
     build = importlib.import_module("mini-kube-scheduler_amd.build")
     if not build.LIB.exists():
@@ -383,7 +388,8 @@ def main():
             "config": {"workload": wl, "nodes": n_total, "pods_per_step": int(p if mode != "nodeshard" else p_total),
                        "plugins": "filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber w=1]",
                        "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}",
-                       "streams": nstreams, "launch": launch},
+                       "streams": nstreams, "launch": launch,
+                       **({"rehearsal": "all ranks on cuda:0, gloo (not a measurement)"} if rehearse else {})},
             "pods_per_s": pods_total / elapsed,
             "check": check,
             "roofline": roofline,
