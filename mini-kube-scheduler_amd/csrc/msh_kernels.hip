@@ -494,15 +494,15 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
 // U: pods decided per step (U > 1 only for one wave without a capacity; U divides 64).
 template <int RS, int NW, bool KX, bool CAP, int U>
 __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_kernel(SeqArgs a) {
-  static_assert(U == 1 || (NW == 1 && !CAP), "pods are decided ahead of commits only when no commit feeds a decision");
+  static_assert(U == 1 || !CAP, "pods are decided ahead of commits only when no commit feeds a decision");
   constexpr bool FIN = !CAP && NW > 1;  // a finalizer wave decodes, keeps the outputs and commits
   constexpr int FINW = FIN ? NW : 0;    // the wave that keeps the outputs
   constexpr bool LDSC = NW <= 4;        // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32
                                         // nodes = 32,768 nodes, 128 KB), else in device memory
   constexpr uint32_t NONE = 0xFFFFFFFFu;
-  // per-pod exchange slots (NW > 1), triple-buffered: [slot][first match, first feasible, first
-  // feasible non-match]
-  __shared__ uint32_t xs[3][3];
+  // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first
+  // feasible, first feasible non-match]
+  __shared__ uint32_t xs[3][U][3];
   extern __shared__ int32_t lcnt[];  // [n_pad] per-node pod counts (LDSC)
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -532,7 +532,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   }
   if (LDSC)  // ordered before the first commit by the first pod's exchange / barrier
     for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) lcnt[i] = a.counts[i];
-  if (threadIdx.x < 9) xs[threadIdx.x / 3][threadIdx.x % 3] = NONE;
+  if (threadIdx.x < 9 * U) (&xs[0][0][0])[threadIdx.x] = NONE;
   __syncthreads();
   int sl = 0;
   // Drain the node-state loads here: otherwise the waitcnt pass, unsure they have landed on every
@@ -645,36 +645,37 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
         if (KX) cxu[u] = wave_first(cxu[u]);
       }
     }
-    // ---- then, in pod order: exchange (NW > 1), decode, output, commit ----
+    // ---- exchange (NW > 1): lane 0 of every scanning wave folds its wave's results for the step's
+    // U pods into their slots; after ONE barrier each pod's result is one broadcast read ----
+    if constexpr (NW > 1) {
+      if (scanner && lane == 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          atomicMin(&xs[sl][u][0], cmu[u]);
+          if (CAP) atomicMin(&xs[sl][u][1], cau[u]);
+          if (KX) atomicMin(&xs[sl][u][2], cxu[u]);
+        }
+      }
+      lds_barrier();
+      const int sl_now = sl;
+      sl = sl == 2 ? 0 : sl + 1;
+      if (!CAP && wv != FINW) continue;  // without a capacity only the finalizer finishes a pod
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        cmu[u] = xs[sl_now][u][0];
+        if (CAP) cau[u] = xs[sl_now][u][1];
+        if (KX) cxu[u] = xs[sl_now][u][2];
+      }
+      // the slot read one step ago is free now (every reader passed this step's barrier) and is
+      // next folded into two steps ahead (after the next barrier): wave FINW resets it in between
+      if (wv == FINW && lane < 3 * U) (&xs[sl_now == 0 ? 2 : sl_now - 1][0][0])[lane] = NONE;
+    }
+    // ---- then, in pod order: decode, output, commit ----
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int jl = (j + u) & (WAVE - 1);
-      const uint32_t pc = pku[u] & 15u, tol = pku[u] >> 4;
-      uint32_t cm = cmu[u], ca = cau[u], cx = cxu[u];
-      if constexpr (NW > 1) {
-        // lane 0 of every scanning wave folds its wave's result into this pod's slot; after the
-        // barrier the pod's result is ONE broadcast read
-        if (scanner && lane == 0) {
-          atomicMin(&xs[sl][0], cm);
-          if (CAP) atomicMin(&xs[sl][1], ca);
-          if (KX) atomicMin(&xs[sl][2], cx);
-        }
-        lds_barrier();
-        const int sl_now = sl;
-        sl = sl == 2 ? 0 : sl + 1;
-        if (!CAP && wv != FINW) continue;  // without a capacity only the finalizer finishes a pod
-        cm = xs[sl_now][0];
-        if (CAP) ca = xs[sl_now][1];
-        if (KX) cx = xs[sl_now][2];
-        // the slot read one pod ago is free now (every reader passed this pod's barrier) and is
-        // next folded into two pods ahead (after the next barrier): wave FINW resets it in between
-        if (wv == FINW && lane == 0) {
-          const int sr = sl_now == 0 ? 2 : sl_now - 1;
-          xs[sr][0] = NONE;
-          xs[sr][1] = NONE;
-          xs[sr][2] = NONE;
-        }
-      }
+      const uint32_t pc = pku[u] & 15u, tol = (pku[u] >> 4) & 1u;
+      const uint32_t cm = cmu[u], ca = cau[u], cx = cxu[u];
       int32_t sel, st, code;
       if constexpr (!CAP && !KX) {  // decode_ident with the class status from the lane word
         st = (int32_t)((pku[u] >> 5) & 3u);
@@ -874,13 +875,13 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
 }
 
 namespace {
-constexpr int SEQ_AHEAD = 4;  // pods decided per step by one wave without a capacity
+constexpr int SEQ_AHEAD = 4;  // pods decided per step without a capacity
 
 template <int RS, int NW, bool CAP>
 hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
   const dim3 blk((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64);  // + the finalizer wave without a capacity
   const size_t lds = NW <= 4 ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;  // seq_kernel's LDSC
-  constexpr int U = (NW == 1 && !CAP) ? SEQ_AHEAD : 1;
+  constexpr int U = !CAP ? SEQ_AHEAD : 1;
   auto kx = seq_kernel<RS, NW, true, CAP, U>;
   auto id = seq_kernel<RS, NW, false, CAP, U>;
   const void* k = needs_kx(a.pp) ? reinterpret_cast<const void*>(kx) : reinterpret_cast<const void*>(id);

@@ -275,6 +275,31 @@ def test_sequential(msh, oracle, n, max_pods, seq_waves, monkeypatch):
             _assert_same(got, ctx.schedule_batch(pd, pt), "seq == batch")
 
 
+@pytest.mark.parametrize("seq_waves", ["1", "4", "16"])
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+@pytest.mark.parametrize("combo", range(len(PLUGIN_COMBOS)))
+def test_sequential_plugin_sets(msh, oracle, combo, norm, seq_waves, monkeypatch):
+    """Sequential commit for every plugin-list combination and normalize mode (the KX decode
+    included), at 1, 4 and 16 scanning waves, with and without a capacity, on tables where whole
+    pod classes have no feasible node (FitError) and pods without a digit (score error)."""
+    monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)
+    rng = np.random.default_rng(500 + 10 * combo + norm)
+    f, pre, sc = PLUGIN_COMBOS[combo]
+    ps = _plugins(oracle, f, pre, sc, 3, norm)
+    with msh.DeviceContext(0) as ctx:
+        _set(ctx, msh, ps)
+        for n, p_unsched in ((300, 1.0), (300, 0.0), (2000, 0.5)):
+            u, nd, pd, pt = _rand_case(rng, n, 1001, p_unsched=p_unsched, p_tol=0.3)
+            ctx.upload_nodes(u, nd)
+            for cap in (0, 2):
+                ctx.reset_node_pod_counts()
+                got = ctx.schedule_sequential(pd, pt, cap)
+                want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, cap)
+                what = f"combo={combo} norm={norm} waves={seq_waves} n={n} unsched={p_unsched} cap={cap}"
+                _assert_same(got, (want_i, want_s, want_st), what)
+                assert (ctx.node_pod_counts() == want_counts).all(), what
+
+
 @pytest.mark.parametrize("norm", [0, 3])
 def test_sequential_large_tables(msh, gpu_ctx, oracle, norm):
     """Tables far past the round-1 cap of 12,288 nodes: 300,000 nodes (15 scanning waves x 10 words
