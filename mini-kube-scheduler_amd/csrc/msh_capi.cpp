@@ -20,9 +20,11 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <iterator>
 #include <mutex>
 #include <new>
 #include <string>
@@ -252,10 +254,24 @@ int ensure_stage(msh_ctx* c, int32_t p) {
   return MSH_OK;
 }
 
-// Device-visible address of page-locked host memory (hipHostMalloc'd or hipHostRegister'ed),
-// or nullptr for pageable memory. A failed query is not an error of the call: it is cleared so
-// that the next launch's hipGetLastError does not report it.
+// Buffers from msh_host_alloc, [start, end) by start: a host-buffer call finds its page-locked
+// arrays here without asking HIP (five hipPointerGetAttributes per call otherwise).
+std::mutex g_host_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_host_allocs;
+
+bool in_host_allocs(const void* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> g(g_host_mu);
+  auto it = std::upper_bound(g_host_allocs.begin(), g_host_allocs.end(), std::make_pair(a, UINTPTR_MAX));
+  return it != g_host_allocs.begin() && a < std::prev(it)->second;
+}
+
+// Device-visible address of page-locked host memory (msh_host_alloc'd: the same address, as for
+// any hipHostMalloc memory; otherwise hipHostRegister'ed, asked of HIP), or nullptr for pageable
+// memory. A failed query is not an error of the call: it is cleared so that the next launch's
+// hipGetLastError does not report it.
 void* pinned_device_ptr(const void* p) {
+  if (in_host_allocs(p)) return const_cast<void*>(p);
   hipPointerAttribute_t at;
   if (hipPointerGetAttributes(&at, p) != hipSuccess) {
     (void)hipGetLastError();
@@ -438,15 +454,27 @@ int msh_host_alloc(size_t bytes, void** out_ptr) {
   *out_ptr = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MSH_ERR_NO_DEVICE;
-  if (hipHostMalloc(out_ptr, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+  const size_t n_bytes = std::max<size_t>(bytes, 1);
+  if (hipHostMalloc(out_ptr, n_bytes, hipHostMallocDefault) != hipSuccess) {
     *out_ptr = nullptr;
     return MSH_ERR_NOMEM;
   }
+  const uintptr_t a = reinterpret_cast<uintptr_t>(*out_ptr);
+  std::lock_guard<std::mutex> g(g_host_mu);
+  g_host_allocs.insert(std::upper_bound(g_host_allocs.begin(), g_host_allocs.end(), std::make_pair(a, a)),
+                       std::make_pair(a, a + n_bytes));
   return MSH_OK;
 }
 
 void msh_host_free(void* ptr) {
-  if (ptr) (void)hipHostFree(ptr);
+  if (!ptr) return;
+  {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    std::lock_guard<std::mutex> g(g_host_mu);
+    auto it = std::lower_bound(g_host_allocs.begin(), g_host_allocs.end(), std::make_pair(a, (uintptr_t)0));
+    if (it != g_host_allocs.end() && it->first == a) g_host_allocs.erase(it);
+  }
+  (void)hipHostFree(ptr);
 }
 
 int msh_create(int device, msh_ctx** out_ctx) {

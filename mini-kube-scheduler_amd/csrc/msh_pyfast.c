@@ -6,6 +6,8 @@
  * conversion of eight parameters). These METH_FASTCALL wrappers take plain ints (the ctx handle,
  * device pointers, the stream handle) and call the C ABI directly. They do not replace the ABI:
  * everything else goes through ctypes (_native.py), and a cgo caller binds the C functions.
+ * schedule_batch_host does the same for the host-buffer msh_schedule_batch, taking arrays by the
+ * buffer protocol.
  * Build (mini-kube-scheduler_amd/build.py): gcc -shared against libminisched_hip.so. */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -96,7 +98,72 @@ static PyObject* py_decode_keys_device(PyObject* self, PyObject* const* a, Py_ss
   return PyLong_FromLong(rc);
 }
 
+/* ---- host-buffer calls: numpy arrays (or any C-contiguous buffer) by the buffer protocol ----
+ * Taking an array's address through numpy's ctypes interface costs ~3 us per array in Python,
+ * five per call; PyObject_GetBuffer costs ~0.1 us. The GIL is released during the call. */
+static int get_buf(PyObject* o, Py_buffer* b, int writable, Py_ssize_t itemsize, const char* what) {
+  if (PyObject_GetBuffer(o, b, PyBUF_C_CONTIGUOUS | (writable ? PyBUF_WRITABLE : 0)) < 0) return -1;
+  if (b->itemsize != itemsize) {
+    PyBuffer_Release(b);
+    PyErr_Format(PyExc_ValueError, "%s: item size %zd, expected %zd", what, b->itemsize, itemsize);
+    return -1;
+  }
+  return 0;
+}
+
+/* The pod columns and the three output arrays of a host-buffer call; outputs may be longer. */
+typedef struct {
+  Py_buffer pd, pt, oi, os, ost;
+  int n;
+} HostBufs;
+
+static void release_bufs(HostBufs* h) {
+  Py_buffer* all[5] = {&h->pd, &h->pt, &h->oi, &h->os, &h->ost};
+  for (int i = 0; i < h->n; ++i) PyBuffer_Release(all[i]);
+}
+
+static int get_host_bufs(PyObject* const* a, HostBufs* h, Py_ssize_t* p) {
+  h->n = 0;
+  if (get_buf(a[0], &h->pd, 0, 1, "pod_digit")) return -1;
+  h->n = 1;
+  if (get_buf(a[1], &h->pt, 0, 1, "pod_tol")) goto fail;
+  h->n = 2;
+  if (get_buf(a[2], &h->oi, 1, 4, "out_idx")) goto fail;
+  h->n = 3;
+  if (get_buf(a[3], &h->os, 1, 8, "out_score")) goto fail;
+  h->n = 4;
+  if (get_buf(a[4], &h->ost, 1, 4, "out_status")) goto fail;
+  h->n = 5;
+  *p = h->pd.len;
+  if (h->pt.len != *p || h->oi.len < 4 * *p || h->os.len < 8 * *p || h->ost.len < 4 * *p || *p > INT32_MAX) {
+    PyErr_SetString(PyExc_ValueError, "pod_digit / pod_tol lengths differ, or an output array is too short");
+    goto fail;
+  }
+  return 0;
+fail:
+  release_bufs(h);
+  return -1;
+}
+
+/* schedule_batch_host(ctx, pod_digit, pod_tol, out_idx, out_score, out_status) -> rc */
+static PyObject* py_schedule_batch_host(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  void* ctx;
+  HostBufs h;
+  Py_ssize_t p;
+  if (want_args(n, 6, "schedule_batch_host") || as_ptr(a[0], &ctx) || get_host_bufs(a + 1, &h, &p)) return NULL;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = msh_schedule_batch((msh_ctx*)ctx, (int32_t)p, (const int8_t*)h.pd.buf, (const uint8_t*)h.pt.buf,
+                          (int32_t*)h.oi.buf, (int64_t*)h.os.buf, (int32_t*)h.ost.buf);
+  Py_END_ALLOW_THREADS
+  release_bufs(&h);
+  return PyLong_FromLong(rc);
+}
+
 static PyMethodDef methods[] = {
+    {"schedule_batch_host", (PyCFunction)(void (*)(void))py_schedule_batch_host, METH_FASTCALL,
+     "msh_schedule_batch(ctx, pod_digit, pod_tol, out_idx, out_score, out_status) -> rc (buffer protocol)"},
     {"schedule_batch_device", (PyCFunction)(void (*)(void))py_schedule_batch_device, METH_FASTCALL,
      "msh_schedule_batch_device(ctx, p, pod_digit, pod_tol, out_idx, out_score, out_status, stream) -> rc"},
     {"schedule_sequential_device", (PyCFunction)(void (*)(void))py_schedule_sequential_device, METH_FASTCALL,

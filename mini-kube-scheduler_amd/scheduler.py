@@ -162,8 +162,9 @@ class DeviceContext:
         pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
         p = _same_len("schedule_batch", pod_digit, pod_tol)
         idx, score, status = self._outputs(p, out)
-        self._check(self._lib.msh_schedule_batch(self.handle, p, N.ptr(pod_digit), N.ptr(pod_tol),
-                                                 N.ptr(idx), N.ptr(score), N.ptr(status)))
+        rc = self._fast.schedule_batch_host(self._hv(), pod_digit, pod_tol, idx, score, status)
+        if rc:
+            self._check(rc)
         return idx, score, status
 
     def schedule_sequential(self, pod_digit: np.ndarray, pod_tol: np.ndarray, max_pods_per_node: int = 0,

@@ -5,6 +5,7 @@ import ctypes as C
 import re
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -38,6 +39,15 @@ def test_fast_call_module(msh):
     assert fast.schedule_sequential_device(None, 0, None, None, 0, None, None, None, None) == inv
     assert fast.shard_keys_device(None, 0, None, None, 0, None, None) == inv
     assert fast.decode_keys_device(None, 0, None, None, None, None, None, None, None) == inv
+    pd, pt = np.zeros(10, np.int8), np.zeros(10, np.uint8)
+    oi, os_, ost = np.zeros(10, np.int32), np.zeros(10, np.int64), np.zeros(10, np.int32)
+    assert fast.schedule_batch_host(None, pd, pt, oi, os_, ost) == inv
+    with pytest.raises(ValueError):  # lengths differ
+        fast.schedule_batch_host(None, pd, pt[:9], oi, os_, ost)
+    with pytest.raises(ValueError):  # score must be 8-byte items
+        fast.schedule_batch_host(None, pd, pt, oi, ost, ost)
+    with pytest.raises((ValueError, BufferError)):  # outputs must be writable, C-contiguous
+        fast.schedule_batch_host(None, pd, pt, oi[::2].repeat(2), os_[::-1], ost)
     with pytest.raises(TypeError):
         fast.schedule_batch_device(None, 0)
     with pytest.raises(OverflowError):
