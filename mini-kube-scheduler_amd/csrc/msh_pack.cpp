@@ -26,8 +26,9 @@ constexpr std::string_view kTaintValue = "";
 
 std::string_view sv(const char* s) { return s ? std::string_view(s) : std::string_view(); }
 
-int8_t suffix_digit(const char* name, int64_t len) {
-  const unsigned char c = static_cast<unsigned char>(name[len - 1]);
+// the digit of the name ending at byte `end` (exclusive) of its blob
+int8_t suffix_digit(const char* blob, int64_t end) {
+  const unsigned char c = static_cast<unsigned char>(blob[end - 1]);
   return (c >= '0' && c <= '9') ? static_cast<int8_t>(c - '0') : static_cast<int8_t>(-1);
 }
 
@@ -74,7 +75,7 @@ int msh_pack_nodes(int32_t n, const char* names, const int64_t* name_off,
     const int32_t i = order[k];
     out_order[k] = i;
     out_unsched[k] = unschedulable[i] ? 1 : 0;
-    out_digit[k] = suffix_digit(nm[i].data(), static_cast<int64_t>(nm[i].size()));
+    out_digit[k] = suffix_digit(nm[i].data(), static_cast<int64_t>(nm[i].size()));  // name's own end
   }
   return MSH_OK;
 }
@@ -85,14 +86,18 @@ int msh_pack_pods(int32_t p, const char* names, const int64_t* name_off,
   if (p < 0) return MSH_ERR_INVALID;
   if (p == 0) return MSH_OK;
   if (!names || !name_off || !tol_off || !out_digit || !out_tol) return MSH_ERR_INVALID;
+  // Offsets are validated in their own pass (monotone, names non-empty), so the packing pass
+  // below has no early exits: one name byte and two offsets per pod, tolerations only for pods
+  // that carry any.
+  if (name_off[0] < 0 || tol_off[0] < 0) return MSH_ERR_INVALID;
+  bool bad = false;
+  for (int32_t j = 0; j < p; j++) bad |= (name_off[j + 1] <= name_off[j]) | (tol_off[j + 1] < tol_off[j]);
+  if (bad || (tol_off[p] > tol_off[0] && !tols)) return MSH_ERR_INVALID;
   for (int32_t j = 0; j < p; j++) {
-    const int64_t a = name_off[j], b = name_off[j + 1];
-    if (a < 0 || b <= a) return MSH_ERR_INVALID;
-    out_digit[j] = suffix_digit(names + a, b - a);
-    const int64_t t0 = tol_off[j], t1 = tol_off[j + 1];
-    if (t0 < 0 || t1 < t0 || (t1 > t0 && !tols)) return MSH_ERR_INVALID;
+    out_digit[j] = suffix_digit(names, name_off[j + 1]);
     uint8_t tol = 0;
-    for (int64_t k = t0; k < t1 && !tol; k++) tol = tolerates(tols[k]) ? 1 : 0;  // any toleration
+    for (int64_t k = tol_off[j], t1 = tol_off[j + 1]; k < t1 && !tol; k++)
+      tol = tolerates(tols[k]) ? 1 : 0;  // any toleration
     out_tol[j] = tol;
   }
   return MSH_OK;
