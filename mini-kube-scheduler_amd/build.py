@@ -28,7 +28,7 @@ SOURCES = [
     ("msh_capi.cpp", "hipcc", []),
     ("msh_pack.cpp", "g++", []),
 ]
-HEADERS = [CSRC / "msh_internal.h", INCLUDE / "minisched_hip.h"]
+HEADERS = [CSRC / "msh_internal.h", CSRC / "msh_pool.h", INCLUDE / "minisched_hip.h"]
 
 
 def _hipcc() -> str:
@@ -69,7 +69,7 @@ def _build_lib(force: bool, verbose: bool) -> None:
                    "-Wall", "-Wno-unused-result", "-Wno-unused-value", *extra,
                    "-c", str(s), "-o", str(o)]
         else:
-            cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-c", str(s), "-o", str(o)]
+            cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wextra", "-c", str(s), "-o", str(o)]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -33,68 +33,12 @@
 
 #include "../../include/minisched_hip.h"
 #include "msh_internal.h"
+#include "msh_pool.h"
 
+using msh::HostPool;
 using msh::PluginParams;
 
 namespace {
-
-// Persistent host threads for the staged copies of the pageable path: run(f) calls f(0..n-1),
-// part 0 on the calling thread, the rest on the workers, and returns when all are done. A worker
-// spins on the job counter for a while after each job before it blocks, so back-to-back batches
-// do not pay a futex wake-up per call (tens of microseconds on a busy host).
-class CopyPool {
- public:
-  explicit CopyPool(int workers) {
-    for (int w = 0; w < workers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      stop_.store(true);
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  int parts() const { return (int)th_.size() + 1; }
-  void run(const std::function<void(int)>& f) {
-    job_ = &f;
-    pending_.store((int)th_.size(), std::memory_order_relaxed);
-    gen_.fetch_add(1, std::memory_order_release);
-    { std::lock_guard<std::mutex> g(m_); }  // a worker between its check and its wait sees the new job
-    cv_.notify_all();
-    f(0);
-    while (pending_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-    job_ = nullptr;
-  }
-
- private:
-  void loop(int part) {
-    uint64_t seen = 0;
-    for (;;) {
-      uint64_t g = gen_.load(std::memory_order_acquire);
-      for (int spin = 0; g == seen && !stop_.load(std::memory_order_relaxed) && spin < (1 << 16); ++spin) {
-        std::this_thread::yield();
-        g = gen_.load(std::memory_order_acquire);
-      }
-      if (g == seen) {
-        std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [&] { return stop_.load() || gen_.load(std::memory_order_acquire) != seen; });
-        g = gen_.load(std::memory_order_acquire);
-      }
-      if (stop_.load()) return;
-      seen = g;
-      (*job_)(part);
-      pending_.fetch_sub(1, std::memory_order_release);
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex m_;
-  std::condition_variable cv_;
-  const std::function<void(int)>* job_ = nullptr;
-  std::atomic<int> pending_{0};
-  std::atomic<uint64_t> gen_{0};
-  std::atomic<bool> stop_{false};
-};
 
 struct CopyJob {
   void* dst;
@@ -104,7 +48,7 @@ struct CopyJob {
 
 // The copies, each split into pool.parts() contiguous pieces (64-byte aligned cuts), in ONE pool
 // run; small totals on the calling thread alone.
-void par_copy(CopyPool* pool, const CopyJob* jobs, int n_jobs) {
+void par_copy(HostPool* pool, const CopyJob* jobs, int n_jobs) {
   size_t total = 0;
   for (int i = 0; i < n_jobs; ++i) total += jobs[i].bytes;
   if (!pool || total < (256u << 10)) {
@@ -155,7 +99,7 @@ struct msh_ctx {
   int32_t* d_ost = nullptr;
   size_t stage_cap = 0;
   unsigned char* h_stage = nullptr;  // page-locked: digit p | tol p | idx 4p | score 8p | status 4p
-  CopyPool* pool = nullptr;
+  HostPool* pool = nullptr;
   hipEvent_t done_ev = nullptr;  // MSH_HOST_SYNC=poll
   size_t patch_cap = 0;
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
@@ -247,9 +191,8 @@ int ensure_stage(msh_ctx* c, int32_t p) {
     c->stage_cap = cap;
   }
   if (!c->pool && (size_t)p >= 16384) {
-    const unsigned hw = std::thread::hardware_concurrency();
-    const int workers = (int)std::min<unsigned>(7u, hw > 2 ? hw / 2 - 1 : 0u);
-    if (workers > 0) c->pool = new (std::nothrow) CopyPool(workers);
+    const int workers = msh::host_pool_workers();
+    if (workers > 0) c->pool = new (std::nothrow) HostPool(workers);
   }
   return MSH_OK;
 }

@@ -12,17 +12,20 @@
 //     NodeUnschedulable.Filter (upstream node_unschedulable.go, v1.22.0).
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <numeric>
 #include <string_view>
 #include <vector>
 
 #include "../../include/minisched_hip.h"
+#include "msh_pool.h"
 
 namespace {
 
 constexpr std::string_view kTaintKey = "node.kubernetes.io/unschedulable";
 constexpr std::string_view kTaintEffect = "NoSchedule";
 constexpr std::string_view kTaintValue = "";
+constexpr int32_t kParallelPods = 16384;  // msh_pack_pods splits batches of at least this many
 
 std::string_view sv(const char* s) { return s ? std::string_view(s) : std::string_view(); }
 
@@ -86,21 +89,38 @@ int msh_pack_pods(int32_t p, const char* names, const int64_t* name_off,
   if (p < 0) return MSH_ERR_INVALID;
   if (p == 0) return MSH_OK;
   if (!names || !name_off || !tol_off || !out_digit || !out_tol) return MSH_ERR_INVALID;
-  // Offsets are validated in their own pass (monotone, names non-empty), so the packing pass
-  // below has no early exits: one name byte and two offsets per pod, tolerations only for pods
-  // that carry any.
   if (name_off[0] < 0 || tol_off[0] < 0) return MSH_ERR_INVALID;
-  bool bad = false;
-  for (int32_t j = 0; j < p; j++) bad |= (name_off[j + 1] <= name_off[j]) | (tol_off[j + 1] < tol_off[j]);
-  if (bad || (tol_off[p] > tol_off[0] && !tols)) return MSH_ERR_INVALID;
-  for (int32_t j = 0; j < p; j++) {
-    out_digit[j] = suffix_digit(names, name_off[j + 1]);
-    uint8_t tol = 0;
-    for (int64_t k = tol_off[j], t1 = tol_off[j + 1]; k < t1 && !tol; k++)
-      tol = tolerates(tols[k]) ? 1 : 0;  // any toleration
-    out_tol[j] = tol;
+  if (tol_off[p] > tol_off[0] && !tols) return MSH_ERR_INVALID;
+  // Pods [lo, hi): offsets checked without early exits (monotone, names non-empty), one name
+  // byte and two offsets per pod, tolerations only for pods that carry any.
+  auto pack_range = [&](int32_t lo, int32_t hi) {
+    bool bad = false;
+    for (int32_t j = lo; j < hi; j++) {
+      bad |= (name_off[j + 1] <= name_off[j]) | (tol_off[j + 1] < tol_off[j]);
+      out_digit[j] = suffix_digit(names, name_off[j + 1]);
+      uint8_t tol = 0;
+      for (int64_t k = tol_off[j], t1 = tol_off[j + 1]; k < t1 && !tol; k++)
+        tol = tolerates(tols[k]) ? 1 : 0;  // any toleration
+      out_tol[j] = tol;
+    }
+    return bad;
+  };
+  // Large batches are split over a persistent pool of host threads (one caller at a time uses it;
+  // a concurrent caller packs on its own thread).
+  static msh::HostPool* pool = msh::host_pool_workers() > 0 ? new msh::HostPool(msh::host_pool_workers()) : nullptr;
+  static std::mutex pool_mu;
+  std::unique_lock<std::mutex> lk(pool_mu, std::defer_lock);
+  if (p >= kParallelPods && pool && lk.try_lock()) {
+    const int n = pool->parts();
+    std::vector<char> bad(static_cast<size_t>(n), 0);
+    pool->run([&](int k) {
+      bad[k] = pack_range((int32_t)((int64_t)p * k / n), (int32_t)((int64_t)p * (k + 1) / n)) ? 1 : 0;
+    });
+    for (char b : bad)
+      if (b) return MSH_ERR_INVALID;
+    return MSH_OK;
   }
-  return MSH_OK;
+  return pack_range(0, p) ? MSH_ERR_INVALID : MSH_OK;
 }
 
 }  // extern "C"

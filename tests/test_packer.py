@@ -78,3 +78,30 @@ def test_random_names_vs_object_oracle(msh, oracle):
     objs = oracle.list_order([oracle.Node(n, i % 3 == 0) for i, n in enumerate(names)])
     assert nt.names == [o.name for o in objs]
     assert nt.unsched.tolist() == [int(o.unschedulable) for o in objs]
+
+
+def test_large_pod_batch_split_over_threads(msh, oracle):
+    """msh_pack_pods splits batches of 16,384+ pods over host threads: a 50,003-pod batch with
+    random suffixes and every toleration shape, against the object oracle pod by pod; an invalid
+    offset in the last part is still rejected."""
+    rng = np.random.default_rng(11)
+    alphabet = list("abz09-.+Z7")
+    shapes = [{"key": "node.kubernetes.io/unschedulable", "operator": "Exists", "effect": "NoSchedule"},
+              {"key": "node.kubernetes.io/unschedulable", "operator": "Equal", "value": "true"},
+              {"operator": "Exists"}, {"key": "x", "operator": "Exists"},
+              {"key": "node.kubernetes.io/unschedulable", "effect": "NoExecute"}]
+    pods, want_d, want_t = [], [], []
+    for j in range(50_003):
+        name = f"p{j}" + "".join(rng.choice(alphabet, int(rng.integers(0, 3))))
+        tols = [shapes[int(k)] for k in rng.integers(0, len(shapes), int(rng.integers(0, 3)))]
+        pods.append({"metadata": {"name": name}, "spec": {"tolerations": tols}})
+        want_d.append(oracle.atoi_last_byte(name))
+        want_t.append(int(any(oracle.tolerates_taint(oracle.Toleration(t.get("key", ""), t.get("operator", ""),
+                                                                        t.get("value", ""), t.get("effect", "")))
+                              for t in tols)))
+    pt = msh.pack_pods(pods)
+    assert pt.digit.tolist() == want_d
+    assert pt.tolerates.tolist() == want_t
+    pods[-1]["metadata"]["name"] = ""
+    with pytest.raises(msh.MshError):
+        msh.pack_pods(pods)
