@@ -71,11 +71,14 @@ class HostPool {
   std::atomic<bool> stop_{false};
 };
 
-// Workers for a pool on this host: half the hardware threads less one, at most 7 (the caller
-// runs a part too: at most 8 parts).
+// Workers for a pool on this host: half the hardware threads less one, at most MSH_POOL_MAX - 1
+// (the caller runs a part too). A one-GPU job on the MI355X pool gets a 16-CPU share.
+#ifndef MSH_POOL_MAX
+#define MSH_POOL_MAX 16
+#endif
 inline int host_pool_workers() {
   const unsigned hw = std::thread::hardware_concurrency();
-  return (int)std::min<unsigned>(7u, hw > 2 ? hw / 2 - 1 : 0u);
+  return (int)std::min<unsigned>(MSH_POOL_MAX - 1, hw > 2 ? hw / 2 - 1 : 0u);
 }
 
 }  // namespace msh
