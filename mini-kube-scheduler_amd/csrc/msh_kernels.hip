@@ -428,9 +428,10 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
 // max_pods_per_node the commit is per pod: the node's pod count (an LDS table when it fits, device
 // memory otherwise) and the owning lane sets the node's FULL bit once the count reaches it, so
 // later pods see it infeasible. Without a capacity a commit changes nothing a later pod reads:
-// one wave decides U = 4 pods per step (independent scan chains, interleaved word by word), with
-// NW > 1 a dedicated FINALIZER wave decodes and keeps the outputs while the scanners go on, and
-// the counts of a block of 64 placements are committed together when the block's outputs leave.
+// the waves decide U = 4 pods per step (independent scan chains, interleaved word by word; with
+// NW > 1 one barrier per step), a dedicated FINALIZER wave (NW > 1) decodes and keeps the outputs
+// while the scanners go on, and the counts of a block of 64 placements are committed together
+// when the block's outputs leave.
 // Nothing inside the per-pod loop waits on memory: the barrier fences LDS only (a plain
 // __syncthreads() is a workgroup fence over global memory too, `s_waitcnt vmcnt(0)`); outputs
 // collect in lanes (lane jl holds pod j0 + jl, two v_writelane_b32 per pod) and leave as one
