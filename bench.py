@@ -103,7 +103,7 @@ def load_json(path: Path):
 
 def measured_bitop3_ceiling():
     """Lane-ops/s of the scan's own instruction forms (v_bitop3_b32 / v_and_b32 with an SGPR
-    source, 8 waves per SIMD), measured by scripts/ubench_valu3.hip."""
+    source, 8 waves per SIMD), measured by scripts/ubench_bitop3.hip (profiles/r2_ubench_bitop3.jsonl)."""
     try:
         rows = [json.loads(l) for l in UBENCH.read_text().splitlines() if l.startswith("{")]
         ipc = max(r["wave_instr_per_simd_cycle@2.4GHz"] for r in rows if r.get("op") == "bits scan mix")
