@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary configs (one GPU only)")
     ap.add_argument("--streams", type=int, default=2,
                     help="batch mode: independent batches pipelined over this many HIP streams")
+    ap.add_argument("--submit", choices=["c", "python"], default="c",
+                    help="batch mode: the K timed steps submitted by a C loop (the caller a cgo binding "
+                         "is) or by a Python loop")
     ap.add_argument("--launch", choices=["eager", "graph"], default="eager",
                     help="batch mode: K host launches, or (A/B) the K timed steps captured as one hipGraph "
                          "and replayed once; graph replay measured slower on ROCm 7.2 "
@@ -264,6 +267,10 @@ def main():
     # Node-shard steps hold an RCCL all-reduce and a decode launch too, so there the shard kernel
     # is bracketed per step.
     per_step = mode == "nodeshard"
+    # Batch mode submits the K steps from C by default (--submit c): the loop a C or Go caller runs,
+    # one msh_schedule_batch_device call per step, with no interpreter between the launches
+    # (~0.5 us per step of Python otherwise). --submit python keeps the per-step Python loop.
+    c_loop = mode == "batch" and args.submit == "c"
     evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
            if per_step else [(None, None)] * args.steps)
     for e0, e1 in evs:  # create the HIP events before the timed region
@@ -310,8 +317,13 @@ def main():
     else:
         for st in S.all[1:]:
             st.wait_event(r0)
-        for k, (e0, e1) in enumerate(evs):
-            step(k, e0, e1)
+        if c_loop:
+            rc = ctx._fast.schedule_batch_device_steps(batch_args, args.steps)
+            if rc:
+                ctx._check(rc)
+        else:
+            for k, (e0, e1) in enumerate(evs):
+                step(k, e0, e1)
         for st, e in zip(S.all, ends):
             e.record(st)
     torch.cuda.synchronize()
@@ -389,7 +401,7 @@ def main():
             "config": {"workload": wl, "nodes": n_total, "pods_per_step": int(p if mode != "nodeshard" else p_total),
                        "plugins": "filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber w=1]",
                        "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}",
-                       "streams": nstreams, "launch": launch,
+                       "streams": nstreams, "launch": launch, "submit": "c" if c_loop else "python",
                        **({"rehearsal": "all ranks on cuda:0, gloo (not a measurement)"} if rehearse else {})},
             "pods_per_s": pods_total / elapsed,
             "check": check,

@@ -51,6 +51,50 @@ static PyObject* py_schedule_batch_device(PyObject* self, PyObject* const* a, Py
   return PyLong_FromLong(rc);
 }
 
+/* schedule_batch_device_steps(steps, k) -> rc: `steps` is a sequence of up to 16 argument tuples
+ * of schedule_batch_device; call i (0 <= i < k) uses steps[i % len(steps)]. The loop a C or Go
+ * caller runs when it submits k batches back to back: no interpreter between the launches.
+ * Stops at the first failing call and returns its code. */
+static PyObject* py_schedule_batch_device_steps(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  enum { MAXS = 16 };
+  void *ctx[MAXS], *pd[MAXS], *pt[MAXS], *oi[MAXS], *os[MAXS], *ost[MAXS], *st[MAXS];
+  long long p[MAXS], k;
+  if (want_args(n, 2, "schedule_batch_device_steps") || as_i64(a[1], &k)) return NULL;
+  PyObject* seq = PySequence_Fast(a[0], "steps must be a sequence of argument tuples");
+  if (!seq) return NULL;
+  const Py_ssize_t ns = PySequence_Fast_GET_SIZE(seq);
+  if (ns < 1 || ns > MAXS) {
+    Py_DECREF(seq);
+    return PyErr_Format(PyExc_ValueError, "1 to %d argument tuples", MAXS);
+  }
+  for (Py_ssize_t i = 0; i < ns; ++i) {
+    PyObject* t = PySequence_Fast(PySequence_Fast_GET_ITEM(seq, i), "an argument tuple");
+    if (!t) {
+      Py_DECREF(seq);
+      return NULL;
+    }
+    PyObject** v = PySequence_Fast_ITEMS(t);
+    const int bad = PySequence_Fast_GET_SIZE(t) != 8 || as_ptr(v[0], &ctx[i]) || as_i64(v[1], &p[i]) ||
+                    as_ptr(v[2], &pd[i]) || as_ptr(v[3], &pt[i]) || as_ptr(v[4], &oi[i]) ||
+                    as_ptr(v[5], &os[i]) || as_ptr(v[6], &ost[i]) || as_ptr(v[7], &st[i]);
+    Py_DECREF(t);
+    if (bad || p[i] < INT32_MIN || p[i] > INT32_MAX) {
+      Py_DECREF(seq);
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "an argument tuple of schedule_batch_device");
+      return NULL;
+    }
+  }
+  Py_DECREF(seq);
+  int rc = 0;
+  for (long long i = 0; i < k && rc == 0; ++i) {
+    const int j = (int)(i % ns);
+    rc = msh_schedule_batch_device((msh_ctx*)ctx[j], (int32_t)p[j], (const int8_t*)pd[j], (const uint8_t*)pt[j],
+                                   (int32_t*)oi[j], (int64_t*)os[j], (int32_t*)ost[j], st[j]);
+  }
+  return PyLong_FromLong(rc);
+}
+
 /* schedule_sequential_device(ctx, p, d_pod_digit, d_pod_tol, max_pods_per_node, d_out_idx,
  * d_out_score, d_out_status, stream) -> rc */
 static PyObject* py_schedule_sequential_device(PyObject* self, PyObject* const* a, Py_ssize_t n) {
@@ -162,6 +206,8 @@ static PyObject* py_schedule_batch_host(PyObject* self, PyObject* const* a, Py_s
 }
 
 static PyMethodDef methods[] = {
+    {"schedule_batch_device_steps", (PyCFunction)(void (*)(void))py_schedule_batch_device_steps, METH_FASTCALL,
+     "k msh_schedule_batch_device calls from C, cycling over the given argument tuples -> first rc"},
     {"schedule_batch_host", (PyCFunction)(void (*)(void))py_schedule_batch_host, METH_FASTCALL,
      "msh_schedule_batch(ctx, pod_digit, pod_tol, out_idx, out_score, out_status) -> rc (buffer protocol)"},
     {"schedule_batch_device", (PyCFunction)(void (*)(void))py_schedule_batch_device, METH_FASTCALL,

@@ -48,6 +48,13 @@ def test_fast_call_module(msh):
         fast.schedule_batch_host(None, pd, pt, oi, ost, ost)
     with pytest.raises((ValueError, BufferError)):  # outputs must be writable, C-contiguous
         fast.schedule_batch_host(None, pd, pt, oi[::2].repeat(2), os_[::-1], ost)
+    step = (None, 0, None, None, None, None, None, None)
+    assert fast.schedule_batch_device_steps([step, step], 5) == inv  # stops at the first failing call
+    assert fast.schedule_batch_device_steps([step], 0) == 0
+    with pytest.raises(ValueError):
+        fast.schedule_batch_device_steps([step[:7]], 1)
+    with pytest.raises(ValueError):
+        fast.schedule_batch_device_steps([], 1)
     with pytest.raises(TypeError):
         fast.schedule_batch_device(None, 0)
     with pytest.raises(OverflowError):
