@@ -87,7 +87,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary configs (one GPU only)")
     ap.add_argument("--streams", type=int, default=2,
                     help="batch mode: independent batches pipelined over this many HIP streams")
-    ap.add_argument("--submit", choices=["c", "python"], default="c",
+    ap.add_argument("--submit", choices=["c", "python"], default="python",
                     help="batch mode: the K timed steps submitted by a C loop (the caller a cgo binding "
                          "is) or by a Python loop")
     ap.add_argument("--launch", choices=["eager", "graph"], default="eager",
@@ -267,9 +267,10 @@ def main():
     # Node-shard steps hold an RCCL all-reduce and a decode launch too, so there the shard kernel
     # is bracketed per step.
     per_step = mode == "nodeshard"
-    # Batch mode submits the K steps from C by default (--submit c): the loop a C or Go caller runs,
-    # one msh_schedule_batch_device call per step, with no interpreter between the launches
-    # (~0.5 us per step of Python otherwise). --submit python keeps the per-step Python loop.
+    # --submit c (A/B): batch mode submits the K steps from a C loop in the fast-call module, the
+    # loop a C or Go caller runs, one msh_schedule_batch_device call per step; measured no faster
+    # than the Python loop through the fast-call module (profiles/ab/r2_sweep_bench_cloop.jsonl),
+    # so the default stays the Python host mirror's own loop.
     c_loop = mode == "batch" and args.submit == "c"
     evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
            if per_step else [(None, None)] * args.steps)
