@@ -477,7 +477,15 @@ __device__ __forceinline__ uint32_t nor_and_vs(uint32_t t, uint32_t x, uint32_t 
 // clobber stays so that a later M0 user is not silently overwritten.)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
+// (The values are wave-uniform; readfirstlane puts them in SGPRs where the backend holds them in
+// VGPRs, e.g. after a broadcast LDS read.)
+__device__ __forceinline__ void write_lane1(int32_t& a, int32_t va, int32_t lane) {
+  va = __builtin_amdgcn_readfirstlane(va);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 3\n\tv_writelane_b32 %0, %1, m0" : "+v"(a) : "s"(va), "s"(lane) : "m0");
+}
 __device__ __forceinline__ void write_lane2(int32_t& a, int32_t& b, int32_t va, int32_t vb, int32_t lane) {
+  va = __builtin_amdgcn_readfirstlane(va);
+  vb = __builtin_amdgcn_readfirstlane(vb);
   asm volatile("s_mov_b32 m0, %4\n\ts_nop 3\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
                : "+v"(a), "+v"(b)
                : "s"(va), "s"(vb), "s"(lane)
@@ -579,21 +587,40 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   uint32_t pkv = CODE_NONE_POD;  // lane jl: pod j0 + jl's code | tolerates << 4
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
-  // wave FINW: lane jl holds pod j0 + jl's node and status | scored << 2 (one v_writelane each per
-  // pod); the score and status arrays are expanded from them once per 64 pods
-  int32_t o_idx = -1;
-  int32_t o_code = 0;
-  auto store_block = [&](int32_t j0, int32_t cnt) {  // wave FINW: one coalesced store per array
+  // wave FINW: lane jl holds pod j0 + jl's result, written by v_writelane_b32 as the pod is decided:
+  // without a capacity only what the scan found (first match o_a; first non-match o_b in the KX
+  // modes), decoded by the lanes together once per 64 pods; with a capacity the decoded node (o_a)
+  // and status | scored << 2 (o_b), since every commit needs them at once
+  int32_t o_a = -1, o_b = -1;
+  auto store_block = [&](int32_t j0, int32_t cnt, uint32_t pk) {  // wave FINW: one coalesced store per array
     if (lane < cnt) {
-      const int32_t st = o_code & 3;
-      a.out_idx[j0 + lane] = o_idx;
-      a.out_score[j0 + lane] = (o_code & 4) ? sm : 0;
+      int32_t sel, st;
+      int64_t sc;
+      if constexpr (CAP) {
+        sel = o_a;
+        st = o_b & 3;
+        sc = (o_b & 4) ? sm : 0;
+      } else {
+        const uint32_t cm = (uint32_t)o_a, tol = (pk >> 4) & 1u;
+        const int32_t ia = tol ? ia1 : ia0;
+        if constexpr (KX) {
+          decode_pod(cm != NONE ? (int64_t)cm : -1, (uint32_t)o_b != NONE ? (int64_t)(uint32_t)o_b : -1, ia,
+                     (pk & 15u) != CODE_NONE_POD, pp, &sel, &sc, &st);
+        } else {  // decode_ident with the class status from the lane word
+          st = (int32_t)((pk >> 5) & 3u);
+          const bool hit = idec.use_im && cm != NONE;
+          sel = st ? -1 : (hit ? (int32_t)cm : ia);
+          sc = (hit && st == 0) ? idec.sm : 0;
+        }
+      }
+      a.out_idx[j0 + lane] = sel;
+      a.out_score[j0 + lane] = sc;
       a.out_status[j0 + lane] = st;
       // Without a capacity no decision reads a count, so the block's placements are committed
       // here, one atomic per lane (NodeInfo.AddPod analogue), instead of one per pod.
       if (!CAP && st == 0) {
-        if (LDSC) atomicAdd(&lcnt[o_idx], 1);
-        else atomicAdd(&counts[o_idx], 1);
+        if (LDSC) atomicAdd(&lcnt[sel], 1);
+        else atomicAdd(&counts[sel], 1);
       }
     }
   };
@@ -601,8 +628,9 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     if ((j & (WAVE - 1)) == 0) {
       // order matters for vmcnt (in-order): the conversion waits only for the loads issued one
       // block ago, then the previous block's results leave, then the next block is requested
+      const uint32_t pk_done = pkv;  // the previous block's lane words, for its decode
       convert(j, dn, tn, pkv);
-      if (wv == FINW && j > 0) store_block(j - WAVE, WAVE);
+      if (wv == FINW && j > 0) store_block(j - WAVE, WAVE, pk_done);
       load_raw(j + WAVE, dn, tn);
     }
     // ---- decide: the U pods' scans (U > 1 only without a capacity, where no commit feeds a
@@ -671,30 +699,30 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
       // next folded into two steps ahead (after the next barrier): wave FINW resets it in between
       if (wv == FINW && lane < 3 * U) (&xs[sl_now == 0 ? 2 : sl_now - 1][0][0])[lane] = NONE;
     }
-    // ---- then, in pod order: decode, output, commit ----
+    // ---- then, in pod order: keep the result in its lane (decoded per 64 pods) or, with a
+    // capacity, decode, keep and commit ----
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int jl = (j + u) & (WAVE - 1);
-      const uint32_t pc = pku[u] & 15u, tol = (pku[u] >> 4) & 1u;
-      const uint32_t cm = cmu[u], ca = cau[u], cx = cxu[u];
-      int32_t sel, st, code;
-      if constexpr (!CAP && !KX) {  // decode_ident with the class status from the lane word
-        st = (int32_t)((pku[u] >> 5) & 3u);
-        const bool hit = idec.use_im && cm != NONE;
-        sel = st ? -1 : (hit ? (int32_t)cm : (tol ? ia1 : ia0));
-        code = st | ((hit && st == 0) ? 4 : 0);
-      } else {
-        const int64_t im = cm != NONE ? (int64_t)cm : -1;
-        const int64_t ia = CAP ? (ca != NONE ? (int64_t)ca : -1) : (int64_t)(tol ? ia1 : ia0);
-        int64_t sc;
-        if (KX)
-          decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pc != CODE_NONE_POD, pp, &sel, &sc, &st);
-        else
-          decode_ident(im, ia, pc != CODE_NONE_POD, idec, &sel, &sc, &st);
-        code = st | (sc != 0 ? 4 : 0);
+      if constexpr (!CAP) {
+        if (wv == FINW) {
+          if (KX) write_lane2(o_a, o_b, (int32_t)cmu[u], (int32_t)cxu[u], jl);
+          else write_lane1(o_a, (int32_t)cmu[u], jl);
+        }
+        continue;
       }
-      if (wv == FINW) write_lane2(o_idx, o_code, sel, code, jl);
-      if (CAP && st == 0) {  // commit, seen by the next pod's decision
+      const uint32_t pc = pku[u] & 15u;
+      const uint32_t cm = cmu[u], ca = cau[u], cx = cxu[u];
+      const int64_t im = cm != NONE ? (int64_t)cm : -1;
+      const int64_t ia = ca != NONE ? (int64_t)ca : -1;
+      int32_t sel, st;
+      int64_t sc;
+      if (KX)
+        decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pc != CODE_NONE_POD, pp, &sel, &sc, &st);
+      else
+        decode_ident(im, ia, pc != CODE_NONE_POD, idec, &sel, &sc, &st);
+      if (wv == FINW) write_lane2(o_a, o_b, sel, st | (sc != 0 ? 4 : 0), jl);
+      if (st == 0) {  // commit, seen by the next pod's decision
         const uint32_t w = (uint32_t)sel >> 5, q = w / RS;
         if ((int)(q / WAVE) == wv) {  // the owning wave
           int32_t old = 0;
@@ -716,7 +744,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
 
   if (wv == FINW && a.n_pods > 0) {
     const int32_t j0 = (a.n_pods - 1) & ~(WAVE - 1);
-    store_block(j0, a.n_pods - j0);
+    store_block(j0, a.n_pods - j0, pkv);
   }
   if (LDSC) {
     __syncthreads();
