@@ -471,8 +471,8 @@ __device__ __forceinline__ uint32_t nor_and_vs(uint32_t t, uint32_t x, uint32_t 
 
 // a[lane] = va and b[lane] = vb for ONE lane (wave-uniform values and lane): two v_writelane_b32.
 // No builtin for it in this compiler. The lane select goes through M0 (a second SGPR operand
-// would break the constant-bus limit), and the s_nop covers the SALU-written select (a hazard the
-// backend does not see through inline asm).
+// would break the constant-bus limit); M0 is written by the SALU, and only a VALU-written lane
+// select needs wait states before v_writelane.
 // (M0 is reserved: the backend never allocates it, and nothing else in this file uses it; the
 // clobber stays so that a later M0 user is not silently overwritten.)
 #pragma clang diagnostic push
@@ -481,12 +481,12 @@ __device__ __forceinline__ uint32_t nor_and_vs(uint32_t t, uint32_t x, uint32_t 
 // VGPRs, e.g. after a broadcast LDS read.)
 __device__ __forceinline__ void write_lane1(int32_t& a, int32_t va, int32_t lane) {
   va = __builtin_amdgcn_readfirstlane(va);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 3\n\tv_writelane_b32 %0, %1, m0" : "+v"(a) : "s"(va), "s"(lane) : "m0");
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(a) : "s"(va), "s"(lane) : "m0");
 }
 __device__ __forceinline__ void write_lane2(int32_t& a, int32_t& b, int32_t va, int32_t vb, int32_t lane) {
   va = __builtin_amdgcn_readfirstlane(va);
   vb = __builtin_amdgcn_readfirstlane(vb);
-  asm volatile("s_mov_b32 m0, %4\n\ts_nop 3\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
+  asm volatile("s_mov_b32 m0, %4\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
                : "+v"(a), "+v"(b)
                : "s"(va), "s"(vb), "s"(lane)
                : "m0");
