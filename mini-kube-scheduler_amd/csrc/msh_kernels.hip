@@ -30,6 +30,8 @@
 // See DESIGN.md for the roofline / instruction budget of each kernel.
 #include "msh_internal.h"
 
+#include <type_traits>
+
 namespace msh {
 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
@@ -477,6 +479,34 @@ __device__ __forceinline__ uint32_t nor_and_vs(uint32_t t, uint32_t x, uint32_t 
 // clobber stays so that a later M0 user is not silently overwritten.)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
+// Compile-time loop: f(integral_constant<int, i>) for i in [B, E) while f returns true.
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    if (f(std::integral_constant<int, B>{})) static_for<B + 1, E>(f);
+  }
+}
+// a lane index plus a compile-time offset, kept compile-time when the index is
+template <int D, int L>
+__device__ __forceinline__ std::integral_constant<int, L + D> lane_plus(std::integral_constant<int, L>) { return {}; }
+template <int D>
+__device__ __forceinline__ int32_t lane_plus(int32_t l) { return l + D; }
+
+// v_writelane_b32 with the lane as an inline constant
+template <int L>
+__device__ __forceinline__ void write_lane1(int32_t& a, int32_t va, std::integral_constant<int, L>) {
+  va = __builtin_amdgcn_readfirstlane(va);
+  asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(a) : "s"(va), "n"(L));
+}
+template <int L>
+__device__ __forceinline__ void write_lane2(int32_t& a, int32_t& b, int32_t va, int32_t vb,
+                                            std::integral_constant<int, L>) {
+  va = __builtin_amdgcn_readfirstlane(va);
+  vb = __builtin_amdgcn_readfirstlane(vb);
+  asm volatile("v_writelane_b32 %0, %2, %4\n\tv_writelane_b32 %1, %3, %4" : "+v"(a), "+v"(b)
+               : "s"(va), "s"(vb), "n"(L));
+}
+
 // (The values are wave-uniform; readfirstlane puts them in SGPRs where the backend holds them in
 // VGPRs, e.g. after a broadcast LDS read.)
 __device__ __forceinline__ void write_lane1(int32_t& a, int32_t va, int32_t lane) {
@@ -624,121 +654,141 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
       }
     }
   };
-  for (int32_t j = 0; j < a.n_pods; j += U) {
-    if ((j & (WAVE - 1)) == 0) {
-      // order matters for vmcnt (in-order): the conversion waits only for the loads issued one
-      // block ago, then the previous block's results leave, then the next block is requested
-      const uint32_t pk_done = pkv;  // the previous block's lane words, for its decode
-      convert(j, dn, tn, pkv);
-      if (wv == FINW && j > 0) store_block(j - WAVE, WAVE, pk_done);
-      load_raw(j + WAVE, dn, tn);
-    }
-    // ---- decide: the U pods' scans (U > 1 only without a capacity, where no commit feeds a
-    // later decision: independent chains, interleaved word by word) ----
-    uint32_t pku[U], p0[U], p1[U], p2[U], p3[U], ntu[U], cmu[U], cau[U], cxu[U];
+  // One step: the U pods from pod j on, whose lanes start at jl0 (an int, or without a capacity a
+  // compile-time constant: a block's 64 / U steps are unrolled, so readlane and v_writelane take
+  // the lane as an inline constant, with no lane arithmetic and no M0). Returns false to end the
+  // block early (never; the caller checks the pod count).
+  auto step = [&](int32_t j, auto jl0) -> bool {
+      // ---- decide: the U pods' scans (U > 1 only without a capacity, where no commit feeds a
+      // later decision: independent chains, interleaved word by word) ----
+      uint32_t pku[U], p0[U], p1[U], p2[U], p3[U], ntu[U], cmu[U], cau[U], cxu[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      pku[u] = (uint32_t)__builtin_amdgcn_readlane((int)pkv, (j + u) & (WAVE - 1));
-      // the pod's code bits as all-ones / all-zero masks, and ~tolerates: wave-uniform (SGPRs)
-      p0[u] = 0u - (pku[u] & 1u);
-      p1[u] = 0u - ((pku[u] >> 1) & 1u);
-      p2[u] = 0u - ((pku[u] >> 2) & 1u);
-      p3[u] = 0u - ((pku[u] >> 3) & 1u);
-      ntu[u] = ((pku[u] >> 4) & 1u) - 1u;
-      cmu[u] = cau[u] = cxu[u] = NONE;  // this lane's first match / feasible / non-match
-    }
-    if (scanner) {
+      for (int u = 0; u < U; ++u) {
+        pku[u] = (uint32_t)__builtin_amdgcn_readlane((int)pkv, (int32_t)jl0 + u);
+        // the pod's code bits as all-ones / all-zero masks, and ~tolerates: wave-uniform (SGPRs)
+        p0[u] = 0u - (pku[u] & 1u);
+        p1[u] = 0u - ((pku[u] >> 1) & 1u);
+        p2[u] = 0u - ((pku[u] >> 2) & 1u);
+        p3[u] = 0u - ((pku[u] >> 3) & 1u);
+        ntu[u] = ((pku[u] >> 4) & 1u) - 1u;
+        cmu[u] = cau[u] = cxu[u] = NONE;  // this lane's first match / feasible / non-match
+      }
+      if (scanner) {
 #pragma unroll
-      for (int r = RS - 1; r >= 0; --r) {  // slots ascend in List order per lane
-        const uint32_t base = lane_base + (uint32_t)(r * 32);
+        for (int r = RS - 1; r >= 0; --r) {  // slots ascend in List order per lane
+          const uint32_t base = lane_base + (uint32_t)(r * 32);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          uint32_t dm = D0[r] ^ p0[u];
-          dm = or_xor_vs(dm, D1[r], p1[u]);
-          dm = or_xor_vs(dm, D2[r], p2[u]);
-          dm = or_xor_vs(dm, D3[r], p3[u]);
-          if constexpr (!CAP && !KX) {
-            cmu[u] = umin(cmu[u], base | ffbl(nor_and_vs(dm, XX[r], ntu[u])));
-          } else {
-            const uint32_t bad = (XX[r] & ntu[u]) | (CAP ? FULL[r] : 0u);
-            cmu[u] = umin(cmu[u], base | ffbl(~(dm | bad)));
-            if (CAP) cau[u] = umin(cau[u], base | ffbl(VV[r] & ~bad));
-            if (KX) cxu[u] = umin(cxu[u], base | ffbl(VV[r] & ~bad & dm));
+          for (int u = 0; u < U; ++u) {
+            uint32_t dm = D0[r] ^ p0[u];
+            dm = or_xor_vs(dm, D1[r], p1[u]);
+            dm = or_xor_vs(dm, D2[r], p2[u]);
+            dm = or_xor_vs(dm, D3[r], p3[u]);
+            if constexpr (!CAP && !KX) {
+              cmu[u] = umin(cmu[u], base | ffbl(nor_and_vs(dm, XX[r], ntu[u])));
+            } else {
+              const uint32_t bad = (XX[r] & ntu[u]) | (CAP ? FULL[r] : 0u);
+              cmu[u] = umin(cmu[u], base | ffbl(~(dm | bad)));
+              if (CAP) cau[u] = umin(cau[u], base | ffbl(VV[r] & ~bad));
+              if (KX) cxu[u] = umin(cxu[u], base | ffbl(VV[r] & ~bad & dm));
+            }
           }
         }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        cmu[u] = wave_first(cmu[u]);
-        if (CAP) cau[u] = wave_first(cau[u]);
-        if (KX) cxu[u] = wave_first(cxu[u]);
-      }
-    }
-    // ---- exchange (NW > 1): lane 0 of every scanning wave folds its wave's results for the step's
-    // U pods into their slots; after ONE barrier each pod's result is one broadcast read ----
-    if constexpr (NW > 1) {
-      if (scanner && lane == 0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          atomicMin(&xs[sl][u][0], cmu[u]);
-          if (CAP) atomicMin(&xs[sl][u][1], cau[u]);
-          if (KX) atomicMin(&xs[sl][u][2], cxu[u]);
+          cmu[u] = wave_first(cmu[u]);
+          if (CAP) cau[u] = wave_first(cau[u]);
+          if (KX) cxu[u] = wave_first(cxu[u]);
         }
       }
-      lds_barrier();
-      const int sl_now = sl;
-      sl = sl == 2 ? 0 : sl + 1;
-      if (!CAP && wv != FINW) continue;  // without a capacity only the finalizer finishes a pod
+      // ---- exchange (NW > 1): lane 0 of every scanning wave folds its wave's results for the step's
+      // U pods into their slots; after ONE barrier each pod's result is one broadcast read ----
+      if constexpr (NW > 1) {
+        if (scanner && lane == 0) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        cmu[u] = xs[sl_now][u][0];
-        if (CAP) cau[u] = xs[sl_now][u][1];
-        if (KX) cxu[u] = xs[sl_now][u][2];
+          for (int u = 0; u < U; ++u) {
+            atomicMin(&xs[sl][u][0], cmu[u]);
+            if (CAP) atomicMin(&xs[sl][u][1], cau[u]);
+            if (KX) atomicMin(&xs[sl][u][2], cxu[u]);
+          }
+        }
+        lds_barrier();
+        const int sl_now = sl;
+        sl = sl == 2 ? 0 : sl + 1;
+        if (!CAP && wv != FINW) return true;  // without a capacity only the finalizer finishes a pod
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cmu[u] = xs[sl_now][u][0];
+          if (CAP) cau[u] = xs[sl_now][u][1];
+          if (KX) cxu[u] = xs[sl_now][u][2];
+        }
+        // the slot read one step ago is free now (every reader passed this step's barrier) and is
+        // next folded into two steps ahead (after the next barrier): wave FINW resets it in between
+        if (wv == FINW && lane < 3 * U) (&xs[sl_now == 0 ? 2 : sl_now - 1][0][0])[lane] = NONE;
       }
-      // the slot read one step ago is free now (every reader passed this step's barrier) and is
-      // next folded into two steps ahead (after the next barrier): wave FINW resets it in between
-      if (wv == FINW && lane < 3 * U) (&xs[sl_now == 0 ? 2 : sl_now - 1][0][0])[lane] = NONE;
-    }
-    // ---- then, in pod order: keep the result in its lane (decoded per 64 pods) or, with a
-    // capacity, decode, keep and commit ----
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int jl = (j + u) & (WAVE - 1);
+      // ---- then, in pod order: keep the result in its lane (decoded per 64 pods) or, with a
+      // capacity, decode, keep and commit ----
       if constexpr (!CAP) {
         if (wv == FINW) {
-          if (KX) write_lane2(o_a, o_b, (int32_t)cmu[u], (int32_t)cxu[u], jl);
-          else write_lane1(o_a, (int32_t)cmu[u], jl);
+          static_for<0, U>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            const auto jl = lane_plus<u>(jl0);
+            if (KX) write_lane2(o_a, o_b, (int32_t)cmu[u], (int32_t)cxu[u], jl);
+            else write_lane1(o_a, (int32_t)cmu[u], jl);
+            return true;
+          });
         }
-        continue;
+        return true;
       }
-      const uint32_t pc = pku[u] & 15u;
-      const uint32_t cm = cmu[u], ca = cau[u], cx = cxu[u];
-      const int64_t im = cm != NONE ? (int64_t)cm : -1;
-      const int64_t ia = ca != NONE ? (int64_t)ca : -1;
-      int32_t sel, st;
-      int64_t sc;
-      if (KX)
-        decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pc != CODE_NONE_POD, pp, &sel, &sc, &st);
-      else
-        decode_ident(im, ia, pc != CODE_NONE_POD, idec, &sel, &sc, &st);
-      if (wv == FINW) write_lane2(o_a, o_b, sel, st | (sc != 0 ? 4 : 0), jl);
-      if (st == 0) {  // commit, seen by the next pod's decision
-        const uint32_t w = (uint32_t)sel >> 5, q = w / RS;
-        if ((int)(q / WAVE) == wv) {  // the owning wave
-          int32_t old = 0;
-          if (lane == 0) old = LDSC ? atomicAdd(&lcnt[sel], 1) : atomicAdd(&counts[sel], 1);
-          const bool full = __builtin_amdgcn_readfirstlane(old) + 1 >= max_pods;
-          if (full) {
-            // the owning lane: the register by a wave-uniform index (scalar branches), the lane
-            // by a compare
-            const int rs = (int)(w % RS);
-            const uint32_t bit = (lane == (int)(q % WAVE)) ? (1u << (sel & 31)) : 0u;
 #pragma unroll
-            for (int r = 0; r < RS; ++r)
-              if (r == rs) FULL[r] |= bit;
+      for (int u = 0; u < U; ++u) {
+        const int32_t jl = (int32_t)jl0 + u;
+        const uint32_t pc = pku[u] & 15u;
+        const uint32_t cm = cmu[u], ca = cau[u], cx = cxu[u];
+        const int64_t im = cm != NONE ? (int64_t)cm : -1;
+        const int64_t ia = ca != NONE ? (int64_t)ca : -1;
+        int32_t sel, st;
+        int64_t sc;
+        if (KX)
+          decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pc != CODE_NONE_POD, pp, &sel, &sc, &st);
+        else
+          decode_ident(im, ia, pc != CODE_NONE_POD, idec, &sel, &sc, &st);
+        if (wv == FINW) write_lane2(o_a, o_b, sel, st | (sc != 0 ? 4 : 0), jl);
+        if (st == 0) {  // commit, seen by the next pod's decision
+          const uint32_t w = (uint32_t)sel >> 5, q = w / RS;
+          if ((int)(q / WAVE) == wv) {  // the owning wave
+            int32_t old = 0;
+            if (lane == 0) old = LDSC ? atomicAdd(&lcnt[sel], 1) : atomicAdd(&counts[sel], 1);
+            const bool full = __builtin_amdgcn_readfirstlane(old) + 1 >= max_pods;
+            if (full) {
+              // the owning lane: the register by a wave-uniform index (scalar branches), the lane
+              // by a compare
+              const int rs = (int)(w % RS);
+              const uint32_t bit = (lane == (int)(q % WAVE)) ? (1u << (sel & 31)) : 0u;
+#pragma unroll
+              for (int r = 0; r < RS; ++r)
+                if (r == rs) FULL[r] |= bit;
+            }
           }
         }
       }
+      return true;
+  };
+  for (int32_t jb = 0; jb < a.n_pods; jb += WAVE) {
+    // order matters for vmcnt (in-order): the conversion waits only for the loads issued one
+    // block ago, then the previous block's results leave, then the next block is requested
+    const uint32_t pk_done = pkv;  // the previous block's lane words, for its decode
+    convert(jb, dn, tn, pkv);
+    if (wv == FINW && jb > 0) store_block(jb - WAVE, WAVE, pk_done);
+    load_raw(jb + WAVE, dn, tn);
+    if constexpr (!CAP) {
+      static_for<0, WAVE / U>([&](auto sc) {
+        constexpr int JL = decltype(sc)::value * U;
+        if (jb + JL >= a.n_pods) return false;
+        return step(jb + JL, std::integral_constant<int, JL>{});
+      });
+    } else {
+      const int32_t je = min(jb + WAVE, a.n_pods);
+      for (int32_t j = jb; j < je; j += U) step(j, (int32_t)(j - jb));
     }
   }
 
