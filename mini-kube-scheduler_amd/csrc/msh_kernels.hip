@@ -599,7 +599,8 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   const IdentDecode idec = make_ident_decode(pp);
   // first feasible node of each pod class (no capacity: constant over the launch), -1 = none
   const int32_t ia0 = ball0 ? (int32_t)(KMAX - ball0) : -1, ia1 = ball1 ? (int32_t)(KMAX - ball1) : -1;
-  // A pod's lane word: code | tolerates << 4 | class status << 5, where the class status is
+  // A pod's lane word: code | does-not-tolerate << 4 | class status << 5 (bit 4 set for pods that
+  // do not tolerate, so one sign-extending bit extract gives the ~tolerates mask), where the class status is
   // decode_ident's status, which without a capacity depends on the pod's class alone (FitError when
   // the class has no feasible node, the NodeNumber score error for a pod without a digit): worked
   // out here once per 64 pods by the lanes, not per pod by the scalar unit.
@@ -609,12 +610,12 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     const bool fit = (tl ? ia1 : ia0) < 0;
     const bool serr = !fit && (idec.err_all || (idec.err_nodigit && !dig));
     const uint32_t st = fit ? 1u : (serr ? 2u : 0u);
-    pk = (dig ? (uint32_t)dr : CODE_NONE_POD) | (tl ? 16u : 0u) | (st << 5);
+    pk = (dig ? (uint32_t)dr : CODE_NONE_POD) | (tl ? 0u : 16u) | (st << 5);
   };
   const uint32_t lane_base = (uint32_t)((wv * WAVE + lane) * RS) << 5;  // node index of bit 0 of slot 0's word
   // the one non-zero score a decode can give (decode_ident: weight x 10 or 100; decode_pod: x 100)
   const int64_t sm = KX ? 100 * pp.weight : idec.sm;
-  uint32_t pkv = CODE_NONE_POD;  // lane jl: pod j0 + jl's code | tolerates << 4
+  uint32_t pkv = CODE_NONE_POD;  // lane jl: pod j0 + jl's lane word
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
   // wave FINW: lane jl holds pod j0 + jl's result, written by v_writelane_b32 as the pod is decided:
@@ -631,7 +632,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
         st = o_b & 3;
         sc = (o_b & 4) ? sm : 0;
       } else {
-        const uint32_t cm = (uint32_t)o_a, tol = (pk >> 4) & 1u;
+        const uint32_t cm = (uint32_t)o_a, tol = ((pk >> 4) & 1u) ^ 1u;
         const int32_t ia = tol ? ia1 : ia0;
         if constexpr (KX) {
           decode_pod(cm != NONE ? (int64_t)cm : -1, (uint32_t)o_b != NONE ? (int64_t)(uint32_t)o_b : -1, ia,
@@ -670,7 +671,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
         p1[u] = 0u - ((pku[u] >> 1) & 1u);
         p2[u] = 0u - ((pku[u] >> 2) & 1u);
         p3[u] = 0u - ((pku[u] >> 3) & 1u);
-        ntu[u] = ((pku[u] >> 4) & 1u) - 1u;
+        ntu[u] = 0u - ((pku[u] >> 4) & 1u);
         cmu[u] = cau[u] = cxu[u] = NONE;  // this lane's first match / feasible / non-match
       }
       if (scanner) {
