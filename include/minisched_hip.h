@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSH_ABI_VERSION 3
+#define MSH_ABI_VERSION 4
 
 /* ---- error codes (return values) ---- */
 typedef enum msh_err {
@@ -154,7 +154,10 @@ int msh_patch_nodes(msh_ctx* ctx, int32_t count, const int32_t* idx, const uint8
  * pod_tol[j]   = pod tolerates taint {node.kubernetes.io/unschedulable, NoSchedule} (0/1).
  * Outputs per pod: out_idx (node index, -1 unless PLACED), out_score (total int64 score of
  * the selected node, 0 unless PLACED), out_status (msh_status). Synchronous. Host buffers:
- * page-locked ones (msh_host_alloc) take the zero-copy path, pageable ones are staged. */
+ * page-locked ones (msh_host_alloc) take the zero-copy path, pageable ones are staged.
+ * out_score may be NULL, here and in every entry point below that takes one (ABI v4): the scores
+ * are then not written, 8 of the 16 output bytes per pod (a binding that only places pods, as
+ * scheduleOne does after selectHost, needs the node and the status). */
 int msh_schedule_batch(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
                        int32_t* out_idx, int64_t* out_score, int32_t* out_status);
 

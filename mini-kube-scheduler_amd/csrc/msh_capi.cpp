@@ -305,11 +305,13 @@ int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t*
   if (rc != MSH_OK) return rc;
   io.d_pd = c->d_pd;
   io.d_pt = c->d_pt;
+  // out_score is optional (NULL: scores not written, 8 B per pod less over PCIe)
   void* di = pinned_device_ptr(out_idx);
-  void* ds = di ? pinned_device_ptr(out_score) : nullptr;
-  void* dt = ds ? pinned_device_ptr(out_status) : nullptr;
+  void* ds = (di && out_score) ? pinned_device_ptr(out_score) : nullptr;
+  const bool score_ok = !out_score || ds;
+  void* dt = (di && score_ok) ? pinned_device_ptr(out_status) : nullptr;
   const bool in_pinned = pinned_device_ptr(pod_digit) && pinned_device_ptr(pod_tol);
-  io.staged = !(di && ds && dt);
+  io.staged = !(di && score_ok && dt);
   if (io.staged || !in_pinned) {
     if ((rc = ensure_stage(c, p)) != MSH_OK) return rc;
   }
@@ -332,7 +334,7 @@ int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t*
   }
   if (io.staged) {
     io.h_idx = reinterpret_cast<int32_t*>(c->h_stage + L.idx);
-    io.h_score = reinterpret_cast<int64_t*>(c->h_stage + L.score);
+    io.h_score = out_score ? reinterpret_cast<int64_t*>(c->h_stage + L.score) : nullptr;
     io.h_status = reinterpret_cast<int32_t*>(c->h_stage + L.status);
     io.o_idx = io.h_idx;  // hipHostMalloc memory: the host pointer is valid on the device too
     io.o_score = io.h_score;
@@ -347,7 +349,7 @@ int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t*
   }
   if (c->dev.host_io_dma) {
     io.o_idx = c->d_oi;
-    io.o_score = c->d_os;
+    io.o_score = out_score ? c->d_os : nullptr;
     io.o_status = c->d_ost;
   }
   return MSH_OK;
@@ -357,7 +359,8 @@ int host_io_end(msh_ctx* c, int32_t p, int32_t* out_idx, int64_t* out_score, int
                 const HostIO& io) {
   if (c->dev.host_io_dma) {
     MSH_HIP(c, hipMemcpyAsync(io.h_idx, c->d_oi, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    MSH_HIP(c, hipMemcpyAsync(io.h_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    if (out_score)
+      MSH_HIP(c, hipMemcpyAsync(io.h_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     MSH_HIP(c, hipMemcpyAsync(io.h_status, c->d_ost, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   }
   if (c->dev.host_sync_poll) {
@@ -371,9 +374,9 @@ int host_io_end(msh_ctx* c, int32_t p, int32_t* out_idx, int64_t* out_score, int
   }
   if (io.staged) {
     const CopyJob jobs[3] = {{out_idx, io.h_idx, (size_t)p * sizeof(int32_t)},
-                             {out_score, io.h_score, (size_t)p * sizeof(int64_t)},
-                             {out_status, io.h_status, (size_t)p * sizeof(int32_t)}};
-    par_copy(c->pool, jobs, 3);
+                             {out_status, io.h_status, (size_t)p * sizeof(int32_t)},
+                             {out_score, io.h_score, (size_t)p * sizeof(int64_t)}};
+    par_copy(c->pool, jobs, out_score ? 3 : 2);
   }
   return MSH_OK;
 }
@@ -660,7 +663,7 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   if (!c) return MSH_ERR_INVALID;
   c->err.clear();
   if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
-  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_out_idx || !d_out_score || !d_out_status))
+  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_out_idx || !d_out_status))  // d_out_score optional
     return fail(c, MSH_ERR_INVALID, "null device pointer");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -680,7 +683,7 @@ int msh_schedule_batch(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   if (!c) return MSH_ERR_INVALID;
   c->err.clear();
   if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
-  if (p > 0 && (!pod_digit || !pod_tol || !out_idx || !out_score || !out_status))
+  if (p > 0 && (!pod_digit || !pod_tol || !out_idx || !out_status))  // out_score optional
     return fail(c, MSH_ERR_INVALID, "null host pointer");
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (p == 0) return MSH_OK;
@@ -701,7 +704,7 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   if (!c) return MSH_ERR_INVALID;
   c->err.clear();
   if (p < 0 || max_pods_per_node < 0) return fail(c, MSH_ERR_INVALID, "negative argument");
-  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_out_idx || !d_out_score || !d_out_status))
+  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_out_idx || !d_out_status))  // d_out_score optional
     return fail(c, MSH_ERR_INVALID, "null device pointer");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -736,7 +739,7 @@ int msh_schedule_sequential(msh_ctx* c, int32_t p, const int8_t* pod_digit, cons
   if (!c) return MSH_ERR_INVALID;
   c->err.clear();
   if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
-  if (p > 0 && (!pod_digit || !pod_tol || !out_idx || !out_score || !out_status))
+  if (p > 0 && (!pod_digit || !pod_tol || !out_idx || !out_status))  // out_score optional
     return fail(c, MSH_ERR_INVALID, "null host pointer");
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (p == 0) return MSH_OK;
@@ -751,7 +754,7 @@ int msh_schedule_sequential(msh_ctx* c, int32_t p, const int8_t* pod_digit, cons
   if ((rc = host_io_end(c, p, out_idx, out_score, out_status, io)) != MSH_OK) return rc;
   if (commit_cb)
     for (int32_t j = 0; j < p; j++)
-      if (out_status[j] == MSH_PLACED) commit_cb(user, j, out_idx[j], out_score[j]);
+      if (out_status[j] == MSH_PLACED) commit_cb(user, j, out_idx[j], out_score ? out_score[j] : 0);
   return MSH_OK;
 }
 
@@ -818,7 +821,7 @@ int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   if (!c) return MSH_ERR_INVALID;
   c->err.clear();
   if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
-  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_keys || !d_out_idx || !d_out_score || !d_out_status))
+  if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_keys || !d_out_idx || !d_out_status))  // d_out_score optional
     return fail(c, MSH_ERR_INVALID, "null device pointer");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

@@ -388,12 +388,15 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
   } else {
     const int64_t ia = key_to_idx(a.ball[tol]);
     const int64_t im = rm != NOFIT ? (int64_t)rm : -1;
+    int32_t oi, ost;
+    int64_t osc;
     if constexpr (KX)
-      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, a.pp, &a.out_idx[j],
-                 &a.out_score[j], &a.out_status[j]);
+      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
     else
-      decode_ident(im, ia, code != CODE_NONE_POD, make_ident_decode(a.pp), &a.out_idx[j], &a.out_score[j],
-                   &a.out_status[j]);
+      decode_ident(im, ia, code != CODE_NONE_POD, make_ident_decode(a.pp), &oi, &osc, &ost);
+    a.out_idx[j] = oi;
+    if (a.out_score) a.out_score[j] = osc;  // optional output (NULL: not written)
+    a.out_status[j] = ost;
   }
 }
 
@@ -413,8 +416,12 @@ __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restri
   const int32_t ka = slot1_any ? k1 : (k0 > k1 ? k0 : k1);
   auto idx_of = [](int32_t k) -> int64_t { return k ? (int64_t)(GKEY_MAX - k) : -1; };
   const int d = pod_digit[j];
-  decode_pod(idx_of(k0), idx_of(k1), idx_of(ka), d >= 0 && d <= 9, pp, &out_idx[j],
-             &out_score[j], &out_status[j]);
+  int32_t oi, ost;
+  int64_t osc;
+  decode_pod(idx_of(k0), idx_of(k1), idx_of(ka), d >= 0 && d <= 9, pp, &oi, &osc, &ost);
+  out_idx[j] = oi;
+  if (out_score) out_score[j] = osc;  // optional output
+  out_status[j] = ost;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -645,7 +652,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
         }
       }
       a.out_idx[j0 + lane] = sel;
-      a.out_score[j0 + lane] = sc;
+      if (a.out_score) a.out_score[j0 + lane] = sc;  // optional output
       a.out_status[j0 + lane] = st;
       // Without a capacity no decision reads a count, so the block's placements are committed
       // here, one atomic per lane (NodeInfo.AddPod analogue), instead of one per pod.

@@ -163,7 +163,8 @@ typedef struct {
 
 static void release_bufs(HostBufs* h) {
   Py_buffer* all[5] = {&h->pd, &h->pt, &h->oi, &h->os, &h->ost};
-  for (int i = 0; i < h->n; ++i) PyBuffer_Release(all[i]);
+  for (int i = 0; i < h->n; ++i)
+    if (all[i]->obj) PyBuffer_Release(all[i]);  // (an absent out_score holds no buffer)
 }
 
 static int get_host_bufs(PyObject* const* a, HostBufs* h, Py_ssize_t* p) {
@@ -174,12 +175,19 @@ static int get_host_bufs(PyObject* const* a, HostBufs* h, Py_ssize_t* p) {
   h->n = 2;
   if (get_buf(a[2], &h->oi, 1, 4, "out_idx")) goto fail;
   h->n = 3;
-  if (get_buf(a[3], &h->os, 1, 8, "out_score")) goto fail;
+  if (a[3] == Py_None) {  // optional: scores not written
+    h->os.buf = NULL;
+    h->os.len = 0;
+    h->os.obj = NULL;
+  } else if (get_buf(a[3], &h->os, 1, 8, "out_score")) {
+    goto fail;
+  }
   h->n = 4;
   if (get_buf(a[4], &h->ost, 1, 4, "out_status")) goto fail;
   h->n = 5;
   *p = h->pd.len;
-  if (h->pt.len != *p || h->oi.len < 4 * *p || h->os.len < 8 * *p || h->ost.len < 4 * *p || *p > INT32_MAX) {
+  if (h->pt.len != *p || h->oi.len < 4 * *p || (h->os.buf && h->os.len < 8 * *p) || h->ost.len < 4 * *p ||
+      *p > INT32_MAX) {
     PyErr_SetString(PyExc_ValueError, "pod_digit / pod_tol lengths differ, or an output array is too short");
     goto fail;
   }
@@ -189,7 +197,7 @@ fail:
   return -1;
 }
 
-/* schedule_batch_host(ctx, pod_digit, pod_tol, out_idx, out_score, out_status) -> rc */
+/* schedule_batch_host(ctx, pod_digit, pod_tol, out_idx, out_score or None, out_status) -> rc */
 static PyObject* py_schedule_batch_host(PyObject* self, PyObject* const* a, Py_ssize_t n) {
   (void)self;
   void* ctx;

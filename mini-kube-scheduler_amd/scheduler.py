@@ -146,22 +146,27 @@ class DeviceContext:
 
     # -- host-buffer entry points --
     @staticmethod
-    def _outputs(p: int, out):
+    def _outputs(p: int, out, scores: bool = True):
         if out is None:
-            return np.empty(p, np.int32), np.empty(p, np.int64), np.empty(p, np.int32)
+            return np.empty(p, np.int32), (np.empty(p, np.int64) if scores else None), np.empty(p, np.int32)
         idx, score, status = out
+        if not scores:
+            score = None
         for a, dt in ((idx, np.int32), (score, np.int64), (status, np.int32)):
+            if a is None and dt is np.int64:
+                continue
             if a.dtype != dt or len(a) < p or not a.flags["C_CONTIGUOUS"]:
-                raise ValueError("out: (int32 idx, int64 score, int32 status), C-contiguous, >= p entries")
+                raise ValueError("out: (int32 idx, int64 score or None, int32 status), C-contiguous, >= p entries")
         return idx, score, status
 
-    def schedule_batch(self, pod_digit: np.ndarray, pod_tol: np.ndarray, out=None):
+    def schedule_batch(self, pod_digit: np.ndarray, pod_tol: np.ndarray, out=None, scores: bool = True):
         """msh_schedule_batch. `out` = (idx, score, status) arrays to fill (e.g. pinned_empty ones:
-        with page-locked columns and outputs the call copies nothing on the host)."""
+        with page-locked columns and outputs the call copies nothing on the host). scores=False
+        (or out with score None): scores are not written and (idx, None, status) comes back."""
         pod_digit = np.ascontiguousarray(pod_digit, np.int8)
         pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
         p = _same_len("schedule_batch", pod_digit, pod_tol)
-        idx, score, status = self._outputs(p, out)
+        idx, score, status = self._outputs(p, out, scores)
         rc = self._fast.schedule_batch_host(self._hv(), pod_digit, pod_tol, idx, score, status)
         if rc:
             self._check(rc)

@@ -435,6 +435,47 @@ def test_pipelined_streams(msh, gpu_ctx, oracle, n, norm):
         _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want, f"n={n} norm={norm}")
 
 
+@pytest.mark.parametrize("norm", [0, 3])
+def test_scores_optional(msh, gpu_ctx, oracle, synth, norm):
+    """out_score = NULL (ABI v4) through every entry point that takes it: idx and status as with
+    scores, nothing written where the scores would go (device entry points keep a sentinel-filled
+    buffer untouched)."""
+    torch = pytest.importorskip("torch")
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
+    _set(gpu_ctx, msh, ps)
+    u, nd, pd, pt = synth.make_soa(5000, 50_000)
+    gpu_ctx.upload_nodes(u, nd)
+    want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+    p = len(pd)
+
+    def same2(got, what):
+        assert got[1] is None
+        assert (got[0] == want[0]).all() and (got[2] == want[2]).all(), what
+
+    same2(gpu_ctx.schedule_batch(pd, pt, scores=False), "pageable")
+    hpd, hpt = msh.pinned_empty(p, np.int8), msh.pinned_empty(p, np.uint8)
+    hpd[:], hpt[:] = pd, pt
+    outs = (msh.pinned_empty(p, np.int32), None, msh.pinned_empty(p, np.int32))
+    same2(gpu_ctx.schedule_batch(hpd, hpt, out=outs, scores=False), "pinned")
+    dev = torch.device("cuda:0")
+    d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+    oi, ost = torch.empty(p, dtype=torch.int32, device=dev), torch.empty(p, dtype=torch.int32, device=dev)
+    gpu_ctx.schedule_batch_device(p, d_pd.data_ptr(), d_pt.data_ptr(), oi.data_ptr(), 0, ost.data_ptr())
+    torch.cuda.synchronize()
+    same2((oi.cpu().numpy(), None, ost.cpu().numpy()), "device batch")
+    gpu_ctx.reset_node_pod_counts()
+    gpu_ctx.schedule_sequential_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, oi.data_ptr(), 0, ost.data_ptr())
+    torch.cuda.synchronize()
+    same2((oi.cpu().numpy(), None, ost.cpu().numpy()), "device sequential")
+    klen = gpu_ctx.shard_keys_len(p)
+    keys = torch.zeros(klen, dtype=torch.int32, device=dev)
+    gpu_ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr())
+    gpu_ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), keys.data_ptr(), oi.data_ptr(), 0,
+                               ost.data_ptr())
+    torch.cuda.synchronize()
+    same2((oi.cpu().numpy(), None, ost.cpu().numpy()), "shard keys + decode")
+
+
 @pytest.mark.parametrize("change", ["patch", "upload"])
 def test_table_change_while_batches_in_flight(msh, gpu_ctx, oracle, change):
     """msh_patch_nodes / msh_upload_nodes while batches queued on other streams still read the
