@@ -85,11 +85,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary configs (one GPU only)")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="batch mode: independent batches pipelined over this many HIP streams")
-    ap.add_argument("--submit", choices=["c", "python"], default="python",
-                    help="batch mode: the K timed steps submitted by a C loop (the caller a cgo binding "
-                         "is) or by a Python loop")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="batch mode: independent batches pipelined over this many HIP streams "
+                         "(default 3 with --submit mt, else 2)")
+    ap.add_argument("--submit", choices=["mt", "c", "python"], default="mt",
+                    help="batch mode: the K timed steps submitted from one host thread per stream, each "
+                         "with its own ctx (mt, csrc/msh_pyfast.c Submitter: one HIP launch costs more host "
+                         "time than a C3 batch takes on the device), or (A/B) by one C loop or one Python "
+                         "loop over the streams")
     ap.add_argument("--launch", choices=["eager", "graph"], default="eager",
                     help="batch mode: K host launches, or (A/B) the K timed steps captured as one hipGraph "
                          "and replayed once; graph replay measured slower on ROCm 7.2 "
@@ -194,7 +197,8 @@ def main():
     # its own pod and output buffers), so that one launch's ramp and tail overlap the next one's.
     # Sequential mode carries node state from batch to batch and node-shard mode has a collective
     # per step: both stay on one stream.
-    nstreams = args.streams if mode == "batch" else 1
+    mt = mode == "batch" and args.submit == "mt" and args.launch == "eager"
+    nstreams = (args.streams or (3 if mt else 2)) if mode == "batch" else 1
     if mode == "nodeshard":
         sharded = D.NodeShardedScheduler(ctx, unsched, node_digit, world, rank)
         node_base = sharded.shard.lo
@@ -252,10 +256,28 @@ def main():
             ctx.decode_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["keys"].data_ptr(), b["idx"].data_ptr(),
                                    b["score"].data_ptr(), b["status"].data_ptr(), sh)
 
-    S.fork()
-    for k in range(args.warmup):
-        step(k)
-    S.join()
+    # --submit mt: lane i (ctx, stream, buffers of its own) submits steps i, i + L, ... from its own
+    # host thread; lane 0 is the main ctx with its own stream too, so the lanes share nothing
+    sub, lane_ctxs = None, []
+    if mt:
+        lane_streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+        lane_ctxs = [ctx] + [msh.DeviceContext(local) for _ in range(nstreams - 1)]
+        for c in lane_ctxs[1:]:
+            c.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+            c.upload_nodes(unsched, node_digit)
+        sub = ctx._fast.Submitter(local, [
+            (c._hv(), p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["idx"].data_ptr(), b["score"].data_ptr(),
+             b["status"].data_ptr(), st.cuda_stream) for c, b, st in zip(lane_ctxs, bufs, lane_streams)])
+        torch.cuda.synchronize()
+
+    if sub is not None:
+        if sub.run(args.warmup):
+            raise RuntimeError("warmup launch failed")
+    else:
+        S.fork()
+        for k in range(args.warmup):
+            step(k)
+        S.join()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -307,10 +329,17 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    if sub is not None:
+        sub.run(0)  # no launches: re-arms the lane threads' spin window after a long barrier
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r0.record(S.main)
-    if graph is not None:
+    if sub is None:
+        r0.record(S.main)
+    if sub is not None:
+        rc = sub.run(args.steps)
+        if rc:
+            ctx._check(rc)
+    elif graph is not None:
         with torch.cuda.stream(S.main):
             graph.replay()
         ends[0].record(S.main)
@@ -334,6 +363,9 @@ def main():
     elapsed = time.perf_counter() - t0
     if per_step:
         kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    elif sub is not None:  # each lane's start / end events on its stream: latest end - earliest start
+        kernel_ms = sub.span_ms() / args.steps
+        sub.close()  # the lane threads stop spinning before anything else runs on the host
     else:
         kernel_ms = max(r0.elapsed_time(e) for e in ends) / args.steps
 
@@ -402,7 +434,7 @@ def main():
             "config": {"workload": wl, "nodes": n_total, "pods_per_step": int(p if mode != "nodeshard" else p_total),
                        "plugins": "filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber w=1]",
                        "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}",
-                       "streams": nstreams, "launch": launch, "submit": "c" if c_loop else "python",
+                       "streams": nstreams, "launch": launch, "submit": ("mt (one host thread + ctx per stream)" if mt else "c" if c_loop else "python"),
                        **({"rehearsal": "all ranks on cuda:0, gloo (not a measurement)"} if rehearse else {})},
             "pods_per_s": pods_total / elapsed,
             "check": check,
@@ -412,6 +444,8 @@ def main():
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
+    for c in lane_ctxs[1:]:
+        c.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -55,6 +55,15 @@ def test_fast_call_module(msh):
         fast.schedule_batch_device_steps([step[:7]], 1)
     with pytest.raises(ValueError):
         fast.schedule_batch_device_steps([], 1)
+    # the multi-thread Submitter checks its lanes before it touches the device
+    with pytest.raises(ValueError):
+        fast.Submitter(0, [])
+    with pytest.raises(ValueError):  # every lane its own ctx (the ABI's one-ctx-per-thread rule)
+        fast.Submitter(0, [(1, 10, 1, 1, 1, 1, 1, 2), (1, 10, 1, 1, 1, 1, 1, 3)])
+    with pytest.raises(ValueError):  # and its own stream
+        fast.Submitter(0, [(1, 10, 1, 1, 1, 1, 1, 2), (4, 10, 1, 1, 1, 1, 1, 2)])
+    with pytest.raises(ValueError):
+        fast.Submitter(0, [step[:7]])
     with pytest.raises(TypeError):
         fast.schedule_batch_device(None, 0)
     with pytest.raises(OverflowError):

@@ -620,3 +620,44 @@ def test_host_buffer_paths(msh, gpu_ctx, oracle, synth, norm):
     got = gpu_ctx.schedule_sequential(hpd[:20_000], hpt[:20_000], 0, out=outs)
     _assert_same(tuple(g[:20_000] for g in got), tuple(w[:20_000] for w in want[:3]), "sequential pinned")
     assert (outs[0][20_000:] == -7).all()  # nothing written past p
+
+
+@pytest.mark.parametrize("lanes,k", [(3, 20), (2, 7), (4, 3)])
+def test_submitter_lanes_bit_exact(msh, oracle, lanes, k):
+    """bench.py's default submission (csrc/msh_pyfast.c Submitter): one host thread per lane, each
+    with its own ctx, stream and pod batch, batch i by lane i % lanes; every lane's last outputs
+    are bit-exact vs the oracle, and the event span covers the run."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(4242 + lanes)
+    u, nd, _, _ = _rand_case(rng, 5000, 1)
+    dev = torch.device("cuda:0")
+    ctxs = [msh.DeviceContext(0) for _ in range(lanes)]
+    try:
+        cases, args = [], []
+        for c in ctxs:
+            c.upload_nodes(u, nd)
+            _, _, pd, pt = _rand_case(rng, 1, 100_000 + int(rng.integers(0, 64)))
+            t = [torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev),
+                 torch.full((len(pd),), -7, dtype=torch.int32, device=dev),
+                 torch.zeros(len(pd), dtype=torch.int64, device=dev),
+                 torch.full((len(pd),), -7, dtype=torch.int32, device=dev)]
+            st = torch.cuda.Stream(dev)
+            cases.append((pd, pt, t))
+            args.append((c._hv(), len(pd), *[x.data_ptr() for x in t], st.cuda_stream))
+        torch.cuda.synchronize()
+        sub = ctxs[0]._fast.Submitter(0, args)
+        try:
+            assert sub.run(k) == 0
+            torch.cuda.synchronize()
+            assert sub.span_ms() > 0
+        finally:
+            sub.close()
+        for j, (pd, pt, t) in enumerate(cases):
+            got = [x.cpu().numpy() for x in t[2:]]
+            if j >= k:  # lane never ran: outputs untouched
+                assert (got[0] == -7).all() and (got[2] == -7).all()
+                continue
+            _assert_same(got, oracle.c_schedule_batch(u, nd, pd, pt), f"lane {j}")
+    finally:
+        for c in ctxs:
+            c.close()
