@@ -86,6 +86,7 @@ struct msh_ctx {
   uint8_t* d_unsched = nullptr;
   int8_t* d_digit = nullptr;
   uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout)
+  uint32_t* d_erows = nullptr;   // digit rows (msh_internal.h ER_* layout)
   uint32_t* d_ball = nullptr;    // [0..1] first feasible node per pod class, as keys
   int32_t* d_counts = nullptr;
   size_t node_cap = 0;
@@ -129,10 +130,12 @@ void free_nodes(msh_ctx* c) {
   (void)hipFree(c->d_unsched);
   (void)hipFree(c->d_digit);
   (void)hipFree(c->d_planes);
+  (void)hipFree(c->d_erows);
   (void)hipFree(c->d_counts);
   c->d_unsched = nullptr;
   c->d_digit = nullptr;
   c->d_planes = nullptr;
+  c->d_erows = nullptr;
   c->d_counts = nullptr;
   c->node_cap = 0;
 }
@@ -252,7 +255,7 @@ int prepare(msh_ctx* c, hipStream_t s) {
   if (!c->dirty) return MSH_OK;
   MSH_HIP(c, hipDeviceSynchronize());
   hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad, c->pp.has_nu_filter,
-                                       c->d_ball, c->d_planes, s, c->d_patch, c->patch_pending);
+                                       c->d_ball, c->d_planes, c->d_erows, s, c->d_patch, c->patch_pending);
   c->patch_pending = 0;
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
   MSH_HIP(c, hipStreamSynchronize(s));
@@ -263,6 +266,7 @@ int prepare(msh_ctx* c, hipStream_t s) {
 msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t* pt) {
   msh::BatchArgs a{};
   a.planes = c->d_planes;
+  a.erows = c->d_erows;
   a.n_groups = c->n_pad / msh::GROUP_NODES;
   a.pod_digit = pd;
   a.pod_tol = pt;
@@ -556,6 +560,7 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
     MSH_HIP(c, hipMalloc(&c->d_digit, cap));
     MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
     MSH_HIP(c, hipMalloc(&c->d_planes, cap / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
+    MSH_HIP(c, hipMalloc(&c->d_erows, cap / msh::GROUP_NODES * msh::ER_GD * sizeof(uint32_t)));
     c->node_cap = cap;
   }
   if (n > 0) {

@@ -70,11 +70,22 @@ constexpr int GROUP_NODES = PLANE_GW * 32;
 constexpr int GROUP_DWORDS = PLANE_GW * PLANE_N;
 constexpr int32_t NODE_PAD = 1024;  // tables are padded to whole 1,024-node prep blocks (4 groups)
 
+// Digit rows (a bitmap index on NodeNumber's node digit; the input of the identity-mode batch
+// kernel): for every word, ER_ROWS row words, row r = the word's real nodes whose suffix digit is
+// r (r = 0..9); row 10 stays zero (the row of pods without a digit suffix). Per group, two chunks
+// of 4 consecutive words, each chunk row-major with a row's 4 words contiguous:
+//   erows[g * ER_GD + (c * ER_ROWS + r) * 4 + k] = row r of word g * PLANE_GW + 4 c + k
+// so a pod's row words of one chunk are one 16-byte read, and the 11 rows of a chunk (44 dwords)
+// sit in distinct LDS banks. 1.375 B per node.
+constexpr int ER_ROWS = 11;
+constexpr int ER_Q = 2 * ER_ROWS;      // 16-byte row chunks per group
+constexpr int ER_GD = ER_Q * 4;        // dwords per group
+
 // ---- launchers (msh_kernels.hip) ----
 // Applies `patch_count` pending msh_patch_nodes entries (idx | unsched << 32 | (uint8)digit << 40)
 // to the raw columns, then rebuilds the planes and the first feasible node per class (ball).
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n, int32_t n_pad,
-                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, hipStream_t s,
+                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows, hipStream_t s,
                             const unsigned long long* d_patch = nullptr, int32_t patch_count = 0);
 
 constexpr int64_t EXPORT_NONE = INT64_MIN;  // msh_export_results: no score recorded
@@ -85,6 +96,7 @@ hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_
 
 struct BatchArgs {
   const uint32_t* planes;    // bit-sliced node table, n_groups groups
+  const uint32_t* erows;     // digit rows (ER_* layout), n_groups groups
   int32_t n_groups;          // n_pad / GROUP_NODES
   int32_t gps;               // groups per slice wave (set by the launcher)
   const int8_t* pod_digit;

@@ -51,7 +51,8 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
                                                                  const int8_t* __restrict__ digit,
                                                                  int32_t n, int32_t has_nu,
                                                                  uint32_t* __restrict__ ball,
-                                                                 uint32_t* __restrict__ planes) {
+                                                                 uint32_t* __restrict__ planes,
+                                                                 uint32_t* __restrict__ erows) {
   constexpr int NWV = PREP_THREADS / WAVE;
   __shared__ uint32_t s_k0[NWV], s_k1[NWV];
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -74,6 +75,20 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
     for (int q = 1; q < PLANE_N; ++q) m = (k == q) ? pm[q] : m;
     const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;  // i - lane: the wave's first node
     planes[((word / PLANE_GW) * PLANE_N + k) * PLANE_GW + word % PLANE_GW] = (uint32_t)(m >> (32 * half));
+  }
+  // the digit rows of the same two words (ER_* layout): row r = real nodes with digit r; lanes
+  // 0..21 write rows 0..10 (row 10, pods without a digit, stays zero)
+  unsigned long long em[ER_ROWS - 1];
+#pragma unroll
+  for (int r = 0; r < ER_ROWS - 1; ++r) em[r] = __ballot(code == (uint32_t)r);  // padding: code 15
+  if (lane < 2 * ER_ROWS) {
+    const int r = lane >> 1, half = lane & 1;
+    unsigned long long m = 0;
+#pragma unroll
+    for (int q = 0; q < ER_ROWS - 1; ++q) m = (r == q) ? em[q] : m;
+    const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
+    const uint32_t g = word / PLANE_GW, c = (word / 4) & 1u, k = word & 3u;
+    erows[(size_t)g * ER_GD + (c * ER_ROWS + (uint32_t)r) * 4 + k] = (uint32_t)(m >> (32 * half));
   }
   const unsigned long long m0 = pm[PLANE_V] & ~pm[PLANE_X], m1 = pm[PLANE_V];
   if (lane == 0) {
@@ -394,6 +409,184 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
       decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
     else
       decode_ident(im, ia, code != CODE_NONE_POD, make_ident_decode(a.pp), &oi, &osc, &ost);
+    a.out_idx[j] = oi;
+    if (a.out_score) a.out_score[j] = osc;  // optional output (NULL: not written)
+    a.out_status[j] = ost;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Digit-row batched kernel: stages 1-4 for the identity-like modes (NONE, DEFAULT: everything
+// that needs only the first feasible match per pod), the default batch path.
+//
+// Lanes = pods as in bits_kernel, but the node side is the digit-row bitmap index (ER_* layout,
+// msh_internal.h): for a word of 32 nodes, row r holds the nodes whose suffix digit is r, so a pod
+// reads the ONE row of its own digit instead of combining four code planes. Per lane and word:
+//   hit = E[row] & ~(X & nT)          one v_bitop3_b32 (X wave-uniform, SGPR)
+// is set exactly at the nodes that pass NodeUnschedulable for this pod AND score 10 for it
+// (NodeNumber.Score, digit equal): 32 (pod, node) pairs per lane-op. The row words come from LDS:
+// each wave stages its slice's rows in tiles of ER_TG groups (16-byte copies, wave-private, no
+// barrier), and a lane reads its row of a chunk of 4 words with one ds_read_b128 (lanes of one
+// digit share the address and broadcast; the 11 rows of a chunk occupy distinct banks). The
+// group's hits are ORed (v_or3) and a group with one is remembered; groups are walked in
+// DESCENDING List order, so the last remembered is the first, and the lowest group of the slice,
+// scanned last, keeps its hit words in registers for the exact node (first word with a hit, its
+// lowest set bit). A lane whose first hit lies in a higher group re-reads that group's row and X
+// words from memory behind an exec-mask branch (rare: 256 nodes almost always hold a match).
+// 1.75 VALU per 32 x 64 pairs (bits_kernel: 5.75): the scan is bound by VALU issue at ~1.75
+// clock per wave-word per CU, with LDS reads (one b128 per 4 words, 1 clock per wave-word per CU)
+// beside it. Slices and the LDS merge of their firsts as in bits_kernel.
+// ---------------------------------------------------------------------------------------
+constexpr int ER_TG = 8;  // groups per LDS tile (2,816 B per wave)
+
+// e & ~(x & m) in one v_bitop3_b32 (truth table 0x70 over S0 = e, S1 = x, S2 = m), x wave-uniform
+__device__ __forceinline__ uint32_t hit_s(uint32_t e, uint32_t x, uint32_t m) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x70" : "=v"(r) : "v"(e), "s"(x), "v"(m));
+  return r;
+}
+
+// The first node among 8 hit words of group g (words ascend in List order, bits within a word).
+__device__ __forceinline__ uint32_t hits_first(const uint32_t (&h)[PLANE_GW], uint32_t g) {
+  uint32_t bw = 0;
+  int32_t bj = 0;
+#pragma unroll
+  for (int c = PLANE_GW - 1; c >= 0; --c) {
+    bj = h[c] ? c : bj;
+    bw = h[c] ? h[c] : bw;
+  }
+  return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
+}
+
+// The lane's first feasible match in group g, from memory (its row words and the X plane).
+__device__ __forceinline__ uint32_t rows_group_first(const BatchArgs& a, uint32_t g, uint32_t row, uint32_t nT) {
+  const uint4* er = reinterpret_cast<const uint4*>(a.erows) + (size_t)g * ER_Q;
+  const uint4* xp = reinterpret_cast<const uint4*>(a.planes + (size_t)g * GROUP_DWORDS + PLANE_X * PLANE_GW);
+  const uint4 e0 = er[row], e1 = er[ER_ROWS + row], x0 = xp[0], x1 = xp[1];
+  const uint32_t e[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+  const uint32_t x[PLANE_GW] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  uint32_t h[PLANE_GW];
+#pragma unroll
+  for (int k = 0; k < PLANE_GW; ++k) h[k] = e[k] & ~(x[k] & nT);
+  return hits_first(h, g);
+}
+
+// The X words of group g (wave-uniform) into SGPRs: one s_load_dwordx8, waited for by sx_wait.
+__device__ __forceinline__ void sx_load(u32x8& x, const uint32_t* xg) {
+  asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(x) : "s"(xg));
+}
+// One wait for the outstanding scalar (and LDS) loads, tied to the loaded registers so that no
+// use of them is scheduled in front of it (the backend does not count asm-issued scalar loads).
+__device__ __forceinline__ void sx_wait(u32x8& x0, u32x8& x1) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(x0), "+s"(x1));
+}
+__device__ __forceinline__ void sx_wait(u32x8& x0) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(x0)); }
+
+// One group's hits: the lane's row words of both chunks (two ds_read_b128, issued by the caller)
+// against the group's X words; returns whether any word has a hit.
+__device__ __forceinline__ bool rows_hits(const uint4& e0, const uint4& e1, const u32x8& x, uint32_t nT,
+                                          uint32_t (&h)[PLANE_GW]) {
+  const uint32_t e[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+  for (int k = 0; k < PLANE_GW; ++k) h[k] = hit_s(e[k], x[k], nT);
+  return ((h[0] | h[1] | h[2]) | (h[3] | h[4] | h[5]) | (h[6] | h[7])) != 0u;
+}
+
+template <int S, bool SHARD>
+__global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
+  __shared__ uint4 s_tile[S][ER_TG * ER_Q];
+  __shared__ uint32_t s_res[S][WAVE];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int32_t j = (int32_t)blockIdx.x * WAVE + lane;
+  const bool act = j < a.n_pods;
+  // Prologue: the pod bytes (clamped index: no branch, so nothing waits for them yet), the class
+  // firsts and the top tile's row words are all requested before the first use of any of them.
+  const int32_t jc = act ? j : a.n_pods - 1;  // n_pods >= 1 (the launcher skips empty batches)
+  const int d = a.pod_digit[jc];
+  const uint8_t tb = a.pod_tol[jc];
+  const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
+  const int32_t g_lo = min(s * a.gps, a.n_groups), g_hi = min(g_lo + a.gps, a.n_groups);
+  const int32_t ng = g_hi - g_lo;
+  const uint4* __restrict__ er = reinterpret_cast<const uint4*>(a.erows);
+  uint4* tile = s_tile[s];
+  // this wave's tile, read only by this wave: a whole ER_TG-group tile is copied (sources clamped
+  // to the table, so all loads issue before any wait; rows past the slice are never read)
+  const int32_t q_last = a.n_groups * ER_Q - 1;
+  static_assert(ER_TG * ER_Q > 2 * WAVE && ER_TG * ER_Q <= 3 * WAVE, "fill: three 16-byte copies per lane");
+  auto fill = [&](int32_t t_lo) {
+    const int32_t q0 = t_lo * ER_Q + lane;
+    const uint4 v0 = er[min(q0, q_last)], v1 = er[min(q0 + WAVE, q_last)], v2 = er[min(q0 + 2 * WAVE, q_last)];
+    tile[lane] = v0;
+    tile[lane + WAVE] = v1;
+    if (lane + 2 * WAVE < ER_TG * ER_Q) tile[lane + 2 * WAVE] = v2;
+    __builtin_amdgcn_wave_barrier();
+  };
+  const int32_t t_top = ng > 0 ? (ng - 1) / ER_TG : -1;
+  if (t_top >= 0) fill(g_lo + t_top * ER_TG);
+  const uint32_t code = (act && d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
+  const uint32_t tol = (act && tb) ? 1u : 0u;
+  const uint32_t row = code <= 9u ? code : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
+  const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
+  const uint32_t* xplane = a.planes + PLANE_X * PLANE_GW;
+  const uint4* lrow = tile + row;  // the lane's row in chunk 0 of a tile's first group
+  uint32_t h[PLANE_GW];
+  uint32_t fm = NO_GROUP;  // first group above the lowest with a feasible match
+  // Tiles from the top down, each one's groups descending; the lowest group of the slice last.
+  for (int32_t t = t_top; t >= 0; --t) {
+    const int32_t t_lo = g_lo + t * ER_TG, t_hi = min(t_lo + ER_TG, g_hi);
+    if (t != t_top) fill(t_lo);
+    const int32_t g_end = t == 0 ? g_lo + 1 : t_lo;  // tile 0: all but the lowest group
+    int32_t g = t_hi - 1;
+    for (; g - 1 >= g_end; g -= 2) {  // two groups per step: all their loads before one wait
+      u32x8 x0, x1;
+      sx_load(x0, xplane + (size_t)g * GROUP_DWORDS);
+      sx_load(x1, xplane + (size_t)(g - 1) * GROUP_DWORDS);
+      const uint4* r0 = lrow + (g - t_lo) * ER_Q;
+      const uint4 e00 = r0[0], e01 = r0[ER_ROWS], e10 = r0[-ER_Q], e11 = r0[ER_ROWS - ER_Q];
+      sx_wait(x0, x1);
+      uint32_t h2[PLANE_GW];
+      const bool a0 = rows_hits(e00, e01, x0, nT, h);
+      const bool a1 = rows_hits(e10, e11, x1, nT, h2);
+      fm = a0 ? (uint32_t)g : fm;
+      fm = a1 ? (uint32_t)(g - 1) : fm;
+    }
+    if (g >= g_end) {
+      u32x8 x0;
+      sx_load(x0, xplane + (size_t)g * GROUP_DWORDS);
+      const uint4* r0 = lrow + (g - t_lo) * ER_Q;
+      const uint4 e00 = r0[0], e01 = r0[ER_ROWS];
+      sx_wait(x0);
+      fm = rows_hits(e00, e01, x0, nT, h) ? (uint32_t)g : fm;
+    }
+    if (t == 0) {  // the lowest group: its hit words stay in registers for the exact node
+      u32x8 x0;
+      sx_load(x0, xplane + (size_t)g_lo * GROUP_DWORDS);
+      const uint4 e00 = lrow[0], e01 = lrow[ER_ROWS];
+      sx_wait(x0);
+      fm = rows_hits(e00, e01, x0, nT, h) ? NO_GROUP - 1 : fm;  // marker: the first hit is in h
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  uint32_t rm = NOFIT;  // node index of the first feasible match
+  if (fm == NO_GROUP - 1) rm = hits_first(h, (uint32_t)g_lo);
+  else if (fm != NO_GROUP) rm = rows_group_first(a, fm, row, nT);
+  if constexpr (S > 1) {
+    s_res[s][lane] = rm;
+    __syncthreads();
+    if (s != 0) return;
+#pragma unroll
+    for (int k = 1; k < S; ++k) rm = umin(rm, s_res[k][lane]);
+  }
+  if (SHARD) write_class_keys(a);
+  if (!act) return;
+  if constexpr (SHARD) {
+    a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
+  } else {
+    int32_t oi, ost;
+    int64_t osc;
+    decode_ident(rm != NOFIT ? (int64_t)rm : -1, key_to_idx(tol ? ball1 : ball0), code != CODE_NONE_POD,
+                 make_ident_decode(a.pp), &oi, &osc, &ost);
     a.out_idx[j] = oi;
     if (a.out_score) a.out_score[j] = osc;  // optional output (NULL: not written)
     a.out_status[j] = ost;
@@ -831,7 +1024,7 @@ __global__ __launch_bounds__(256) void prep_reset_kernel(uint32_t* __restrict__ 
 }
 
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n, int32_t n_pad,
-                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, hipStream_t s,
+                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows, hipStream_t s,
                             const unsigned long long* d_patch, int32_t patch_count) {
   hipLaunchKernelGGL(prep_reset_kernel, dim3(patch_count > 0 ? (patch_count + 255) / 256 : 1), dim3(256), 0, s,
                      d_ball, d_patch, patch_count, const_cast<uint8_t*>(d_unsched), const_cast<int8_t*>(d_digit));
@@ -839,7 +1032,7 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
   if (e != hipSuccess) return e;
   if (n_pad == 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel, dim3(n_pad / PREP_THREADS), dim3(PREP_THREADS), 0, s, d_unsched, d_digit, n,
-                     has_nu, d_ball, d_planes);
+                     has_nu, d_ball, d_planes, d_erows);
   return hipGetLastError();
 }
 
@@ -932,6 +1125,26 @@ hipError_t launch_bits_s(const BatchArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int S, bool SHARD>
+hipError_t launch_rows_s(const BatchArgs& a, hipStream_t s) {
+  BatchArgs ka = a;
+  ka.gps = (a.n_groups + S - 1) / S;
+  const int64_t blocks = ((int64_t)a.n_pods + WAVE - 1) / WAVE;
+  hipLaunchKernelGGL((rows_kernel<S, SHARD>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  return hipGetLastError();
+}
+
+template <bool SHARD>
+hipError_t launch_rows_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
+  switch (bits_slices(a.n_pods, a.n_groups, dev)) {
+    case 1: return launch_rows_s<1, SHARD>(a, s);
+    case 2: return launch_rows_s<2, SHARD>(a, s);
+    case 4: return launch_rows_s<4, SHARD>(a, s);
+    case 8: return launch_rows_s<8, SHARD>(a, s);
+    default: return launch_rows_s<16, SHARD>(a, s);
+  }
+}
+
 template <bool KX, bool SHARD>
 hipError_t launch_bits_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
   switch (bits_slices(a.n_pods, a.n_groups, dev)) {
@@ -947,8 +1160,10 @@ hipError_t launch_bits_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t 
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s) {
   if (a.n_pods == 0) return hipSuccess;
   const bool kx = needs_kx(a.pp);
-  if (shard) return kx ? launch_bits_t<true, true>(a, dev, s) : launch_bits_t<false, true>(a, dev, s);
-  return kx ? launch_bits_t<true, false>(a, dev, s) : launch_bits_t<false, false>(a, dev, s);
+  // identity-like modes on the digit rows; REVERSE / MINMAX (first feasible non-match too) on the
+  // code planes
+  if (shard) return kx ? launch_bits_t<true, true>(a, dev, s) : launch_rows_t<true>(a, dev, s);
+  return kx ? launch_bits_t<true, false>(a, dev, s) : launch_rows_t<false>(a, dev, s);
 }
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-2 profile of the hot kernels (bits_kernel at C3, seq_kernel at C5), run on the GPU box:
+# Round-2 profile of the hot kernels (rows_kernel at C3, bits_kernel for MIN-MAX, seq_kernel at C5),
+# run on the GPU box:
 #  1. the scan-mix issue-rate microbenchmark (the VALU ceiling bench.py quotes);
 #  2. rocprofv3 --kernel-trace --stats over the headline bench.py command;
 #  3. one --pmc pass per counter set (never combined with tracing), each under its own limit.
@@ -25,6 +26,7 @@ pass() {
 }
 pass b_sq batch SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU || exit 1
 pass b_sq2 batch SQ_INSTS_VMEM SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS || exit 1
+pass b_lds batch SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE || exit 1
 pass b_grbm batch GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
 pass b_fetch batch FETCH_SIZE || exit 1
 pass b_write batch WRITE_SIZE || exit 1

@@ -1,7 +1,9 @@
 // submit_mt.hip — does the HIP launch path scale over host threads? C3 batches submitted through
 // msh_schedule_batch_device from T host threads at once, each thread with its own ctx (the ABI's
 // one-ctx-per-thread rule), its own stream and its own pod/output buffers; and, for scale, an empty
-// kernel launched the same way. One JSON line per (what, T): wall time per launch over all threads
+// kernel launched the same way (one workgroup, and the C3 batch's grid: 1,563 workgroups of 256
+// threads), and the batch entry point on a 64-pod batch. One JSON line per (what, T): wall time per
+// launch over all threads
 // (submit phase, and up to the device synchronize), every thread's launches counted.
 // Build: hipcc --offload-arch=gfx950 -O2 -Iinclude scripts/submit_mt.hip -Lmini-kube-scheduler_amd
 //        -lminisched_hip -Wl,-rpath,'$ORIGIN/../mini-kube-scheduler_amd' -pthread -o scripts/submit_mt
@@ -76,7 +78,9 @@ int main() {
     CHECK(hipMemcpy(l.pd, pd.data(), P, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(l.pt, pt.data(), P, hipMemcpyHostToDevice));
   }
-  for (int what = 0; what < 2; ++what) {
+  const char* names[4] = {"empty kernel hipLaunchKernelGGL", "msh_schedule_batch_device C3",
+                          "empty kernel, C3 grid (1563 x 256)", "msh_schedule_batch_device 64 pods"};
+  for (int what = 0; what < 4; ++what) {
     for (int T = 1; T <= TMAX; ++T) {
       for (int rep = 0; rep < 2; ++rep) {
         std::atomic<int> ready{0}, go{0}, bad{0};
@@ -84,22 +88,20 @@ int main() {
         auto body = [&](int t) {
           Lane& l = lanes[t];
           const int k = K / T;
-          for (int i = 0; i < 20; ++i) {  // warm the thread's own launch path
+          auto launch = [&]() {
             if (what == 0)
               hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, l.st, nullptr);
-            else if (msh_schedule_batch_device(l.ctx, P, l.pd, l.pt, l.oi, l.sc, l.os, l.st))
+            else if (what == 2)
+              hipLaunchKernelGGL(empty_kernel, dim3((P + 63) / 64), dim3(256), 0, l.st, nullptr);
+            else if (msh_schedule_batch_device(l.ctx, what == 1 ? P : 64, l.pd, l.pt, l.oi, l.sc, l.os, l.st))
               bad = 1;
-          }
+          };
+          for (int i = 0; i < 20; ++i) launch();  // warm the thread's own launch path
           if (hipStreamSynchronize(l.st)) bad = 1;
           ready.fetch_add(1);
           while (!go.load(std::memory_order_acquire)) {
           }
-          for (int i = 0; i < k; ++i) {
-            if (what == 0)
-              hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, l.st, nullptr);
-            else if (msh_schedule_batch_device(l.ctx, P, l.pd, l.pt, l.oi, l.sc, l.os, l.st))
-              bad = 1;
-          }
+          for (int i = 0; i < k; ++i) launch();
           t_end[t] = now_us();
         };
         std::vector<std::thread> th;
@@ -120,7 +122,7 @@ int main() {
         const double launches = (double)(K / T) * T;
         printf("{\"what\": \"%s\", \"threads\": %d, \"rep\": %d, \"submit_us_per_launch\": %.3f, "
                "\"wall_us_per_launch\": %.3f}\n",
-               what == 0 ? "empty kernel hipLaunchKernelGGL" : "msh_schedule_batch_device C3", T, rep,
+               names[what], T, rep,
                (t1 - t0) / launches, (t2 - t0) / launches);
         fflush(stdout);
       }
