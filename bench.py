@@ -338,7 +338,8 @@ def main():
     if sub is None:
         r0.record(S.main)
     if sub is not None:
-        rc = sub.run(args.steps)
+        # MSH_BENCH_LANESYNC (A/B): each lane also waits for its own stream before run() returns
+        rc = sub.run(args.steps, 1 if os.environ.get("MSH_BENCH_LANESYNC") else 0)
         if rc:
             ctx._check(rc)
     elif graph is not None:
@@ -358,11 +359,18 @@ def main():
                 step(k, e0, e1)
         for st, e in zip(S.all, ends):
             e.record(st)
+    t_sub = time.perf_counter()
     torch.cuda.synchronize()
-    if world > 1:
+    if world > 1:  # the barrier and a second synchronize only where there is a barrier
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if os.environ.get("MSH_BENCH_PROBE"):  # A/B: where the host time of the region goes
+        t_idle = time.perf_counter()
+        torch.cuda.synchronize()
+        t_idle = time.perf_counter() - t_idle
+        print(json.dumps({"probe": {"submit_us": (t_sub - t0) * 1e6, "sync_us": (elapsed - (t_sub - t0)) * 1e6,
+                                    "idle_sync_us": t_idle * 1e6, "steps": args.steps}}), file=sys.stderr, flush=True)
     if per_step:
         kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     elif sub is not None:  # each lane's start / end events on its stream: latest end - earliest start

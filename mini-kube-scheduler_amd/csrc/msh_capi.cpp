@@ -445,6 +445,7 @@ int msh_create(int device, msh_ctx** out_ctx) {
   // test / A-B switches, read once here (never on a launch path)
   if (const char* e = getenv("MSH_BITS_SLICES")) c->dev.bits_slices = atoi(e);
   if (const char* e = getenv("MSH_SEQ_WAVES")) c->dev.seq_waves = atoi(e);
+  if (const char* e = getenv("MSH_ROWS_PPL")) c->dev.rows_ppl = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("MSH_HOST_IO")) {
     c->dev.host_io_dma = strcmp(e, "dma") == 0;
     c->dev.host_io_zc_in = strcmp(e, "dma") != 0 && strcmp(e, "zc") != 0;

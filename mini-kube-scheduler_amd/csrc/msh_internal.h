@@ -38,6 +38,7 @@ struct DeviceInfo {
   int cus = 256;
   int bits_slices = 0;   // tests / A-B only (MSH_BITS_SLICES at msh_create): slice waves per pod block, 0 = auto
   int seq_waves = 0;     // tests / A-B only (MSH_SEQ_WAVES at msh_create): sequential scanning waves, 0 = auto
+  int rows_ppl = 1;      // pods per lane of the digit-row kernel (1 or 2; MSH_ROWS_PPL at msh_create, A/B)
   // Host-buffer calls (msh_schedule_batch / _sequential): the kernel reads the pod columns from and
   // writes the outputs to page-locked host memory (default). A/B only, MSH_HOST_IO at msh_create:
   // "dma" = columns and outputs DMA'd through device scratch, "zc" = columns DMA'd, outputs zero-copy.
@@ -73,13 +74,16 @@ constexpr int32_t NODE_PAD = 1024;  // tables are padded to whole 1,024-node pre
 // Digit rows (a bitmap index on NodeNumber's node digit; the input of the identity-mode batch
 // kernel): for every word, ER_ROWS row words, row r = the word's real nodes whose suffix digit is
 // r (r = 0..9); row 10 stays zero (the row of pods without a digit suffix). Per group, two chunks
-// of 4 consecutive words, each chunk row-major with a row's 4 words contiguous:
+// of 4 consecutive words, each chunk row-major with a row's 4 words contiguous, then the group's 8
+// X words (the PLANE_X plane again, so that one copy brings a group's whole input):
 //   erows[g * ER_GD + (c * ER_ROWS + r) * 4 + k] = row r of word g * PLANE_GW + 4 c + k
+//   erows[g * ER_GD + ER_Q * 4 + j]              = X of word g * PLANE_GW + j
 // so a pod's row words of one chunk are one 16-byte read, and the 11 rows of a chunk (44 dwords)
-// sit in distinct LDS banks. 1.375 B per node.
+// sit in distinct LDS banks. 1.5 B per node.
 constexpr int ER_ROWS = 11;
 constexpr int ER_Q = 2 * ER_ROWS;      // 16-byte row chunks per group
-constexpr int ER_GD = ER_Q * 4;        // dwords per group
+constexpr int ER_GQ = ER_Q + 2;        // 16-byte chunks per group: the rows, then X
+constexpr int ER_GD = ER_GQ * 4;       // dwords per group
 
 // ---- launchers (msh_kernels.hip) ----
 // Applies `patch_count` pending msh_patch_nodes entries (idx | unsched << 32 | (uint8)digit << 40)

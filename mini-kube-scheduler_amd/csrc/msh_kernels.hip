@@ -89,6 +89,10 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
     const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
     const uint32_t g = word / PLANE_GW, c = (word / 4) & 1u, k = word & 3u;
     erows[(size_t)g * ER_GD + (c * ER_ROWS + (uint32_t)r) * 4 + k] = (uint32_t)(m >> (32 * half));
+  } else if (lane < 2 * ER_ROWS + 2) {  // lanes 22, 23: the X words behind the rows
+    const int half = lane & 1;
+    const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
+    erows[(size_t)(word / PLANE_GW) * ER_GD + ER_Q * 4 + word % PLANE_GW] = (uint32_t)(pm[PLANE_X] >> (32 * half));
   }
   const unsigned long long m0 = pm[PLANE_V] & ~pm[PLANE_X], m1 = pm[PLANE_V];
   if (lane == 0) {
@@ -437,7 +441,7 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
 // clock per wave-word per CU, with LDS reads (one b128 per 4 words, 1 clock per wave-word per CU)
 // beside it. Slices and the LDS merge of their firsts as in bits_kernel.
 // ---------------------------------------------------------------------------------------
-constexpr int ER_TG = 8;  // groups per LDS tile (2,816 B per wave)
+constexpr int ER_TG = 8;  // groups per LDS tile (3,072 B per wave)
 
 // e & ~(x & m) in one v_bitop3_b32 (truth table 0x70 over S0 = e, S1 = x, S2 = m), x wave-uniform
 __device__ __forceinline__ uint32_t hit_s(uint32_t e, uint32_t x, uint32_t m) {
@@ -460,9 +464,8 @@ __device__ __forceinline__ uint32_t hits_first(const uint32_t (&h)[PLANE_GW], ui
 
 // The lane's first feasible match in group g, from memory (its row words and the X plane).
 __device__ __forceinline__ uint32_t rows_group_first(const BatchArgs& a, uint32_t g, uint32_t row, uint32_t nT) {
-  const uint4* er = reinterpret_cast<const uint4*>(a.erows) + (size_t)g * ER_Q;
-  const uint4* xp = reinterpret_cast<const uint4*>(a.planes + (size_t)g * GROUP_DWORDS + PLANE_X * PLANE_GW);
-  const uint4 e0 = er[row], e1 = er[ER_ROWS + row], x0 = xp[0], x1 = xp[1];
+  const uint4* er = reinterpret_cast<const uint4*>(a.erows) + (size_t)g * ER_GQ;
+  const uint4 e0 = er[row], e1 = er[ER_ROWS + row], x0 = er[ER_Q], x1 = er[ER_Q + 1];
   const uint32_t e[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
   const uint32_t x[PLANE_GW] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
   uint32_t h[PLANE_GW];
@@ -471,40 +474,44 @@ __device__ __forceinline__ uint32_t rows_group_first(const BatchArgs& a, uint32_
   return hits_first(h, g);
 }
 
-// The X words of group g (wave-uniform) into SGPRs: one s_load_dwordx8, waited for by sx_wait.
-__device__ __forceinline__ void sx_load(u32x8& x, const uint32_t* xg) {
-  asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(x) : "s"(xg));
+// e & ~(x & m) in one v_bitop3_b32, all three in VGPRs (x: the same in every lane)
+__device__ __forceinline__ uint32_t hit_v(uint32_t e, uint32_t x, uint32_t m) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x70" : "=v"(r) : "v"(e), "v"(x), "v"(m));
+  return r;
 }
-// One wait for the outstanding scalar (and LDS) loads, tied to the loaded registers so that no
-// use of them is scheduled in front of it (the backend does not count asm-issued scalar loads).
-__device__ __forceinline__ void sx_wait(u32x8& x0, u32x8& x1) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(x0), "+s"(x1));
-}
-__device__ __forceinline__ void sx_wait(u32x8& x0) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(x0)); }
 
-// One group's hits: the lane's row words of both chunks (two ds_read_b128, issued by the caller)
-// against the group's X words; returns whether any word has a hit.
-__device__ __forceinline__ bool rows_hits(const uint4& e0, const uint4& e1, const u32x8& x, uint32_t nT,
-                                          uint32_t (&h)[PLANE_GW]) {
+// One group's hits: the lane's row words of both chunks and the group's X words (four
+// ds_read_b128 of the staged tile, the X reads at one address for all lanes); returns whether any
+// word has a hit.
+__device__ __forceinline__ bool rows_hits(const uint4& e0, const uint4& e1, const uint4& x0, const uint4& x1,
+                                          uint32_t nT, uint32_t (&h)[PLANE_GW]) {
   const uint32_t e[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+  const uint32_t x[PLANE_GW] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-  for (int k = 0; k < PLANE_GW; ++k) h[k] = hit_s(e[k], x[k], nT);
+  for (int k = 0; k < PLANE_GW; ++k) h[k] = hit_v(e[k], x[k], nT);
   return ((h[0] | h[1] | h[2]) | (h[3] | h[4] | h[5]) | (h[6] | h[7])) != 0u;
 }
 
-template <int S, bool SHARD>
+template <int S, bool SHARD, int PPL>
 __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
-  __shared__ uint4 s_tile[S][ER_TG * ER_Q];
-  __shared__ uint32_t s_res[S][WAVE];
+  __shared__ uint4 s_tile[S][ER_TG * ER_GQ];
+  __shared__ uint32_t s_res[S][PPL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int32_t j = (int32_t)blockIdx.x * WAVE + lane;
-  const bool act = j < a.n_pods;
+  // PPL pods per lane: lane l holds pods base + q * 64 + l (q < PPL); the group's X words and the
+  // staged row tile serve all of them
+  const int32_t base = (int32_t)blockIdx.x * (PPL * WAVE) + lane;
   // Prologue: the pod bytes (clamped index: no branch, so nothing waits for them yet), the class
   // firsts and the top tile's row words are all requested before the first use of any of them.
-  const int32_t jc = act ? j : a.n_pods - 1;  // n_pods >= 1 (the launcher skips empty batches)
-  const int d = a.pod_digit[jc];
-  const uint8_t tb = a.pod_tol[jc];
+  int dq[PPL];
+  uint8_t tq[PPL];
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    const int32_t jc = min(base + q * WAVE, a.n_pods - 1);  // n_pods >= 1 (empty batches never launch)
+    dq[q] = a.pod_digit[jc];
+    tq[q] = a.pod_tol[jc];
+  }
   const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
   const int32_t g_lo = min(s * a.gps, a.n_groups), g_hi = min(g_lo + a.gps, a.n_groups);
   const int32_t ng = g_hi - g_lo;
@@ -512,84 +519,111 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
   uint4* tile = s_tile[s];
   // this wave's tile, read only by this wave: a whole ER_TG-group tile is copied (sources clamped
   // to the table, so all loads issue before any wait; rows past the slice are never read)
-  const int32_t q_last = a.n_groups * ER_Q - 1;
-  static_assert(ER_TG * ER_Q > 2 * WAVE && ER_TG * ER_Q <= 3 * WAVE, "fill: three 16-byte copies per lane");
+  const int32_t q_last = a.n_groups * ER_GQ - 1;
+  static_assert(ER_TG * ER_GQ == 3 * WAVE, "fill: three 16-byte copies per lane");
   auto fill = [&](int32_t t_lo) {
-    const int32_t q0 = t_lo * ER_Q + lane;
+    const int32_t q0 = t_lo * ER_GQ + lane;
     const uint4 v0 = er[min(q0, q_last)], v1 = er[min(q0 + WAVE, q_last)], v2 = er[min(q0 + 2 * WAVE, q_last)];
     tile[lane] = v0;
     tile[lane + WAVE] = v1;
-    if (lane + 2 * WAVE < ER_TG * ER_Q) tile[lane + 2 * WAVE] = v2;
+    tile[lane + 2 * WAVE] = v2;
     __builtin_amdgcn_wave_barrier();
   };
   const int32_t t_top = ng > 0 ? (ng - 1) / ER_TG : -1;
   if (t_top >= 0) fill(g_lo + t_top * ER_TG);
-  const uint32_t code = (act && d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
-  const uint32_t tol = (act && tb) ? 1u : 0u;
-  const uint32_t row = code <= 9u ? code : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
-  const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
-  const uint32_t* xplane = a.planes + PLANE_X * PLANE_GW;
-  const uint4* lrow = tile + row;  // the lane's row in chunk 0 of a tile's first group
-  uint32_t h[PLANE_GW];
-  uint32_t fm = NO_GROUP;  // first group above the lowest with a feasible match
+  bool act[PPL];
+  uint32_t code[PPL], tol[PPL], nT[PPL];
+  const uint4* lrow[PPL];  // the lane's row in chunk 0 of a tile's first group
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    act[q] = base + q * WAVE < a.n_pods;
+    code[q] = (act[q] && dq[q] >= 0 && dq[q] <= 9) ? (uint32_t)dq[q] : CODE_NONE_POD;
+    tol[q] = (act[q] && tq[q]) ? 1u : 0u;
+    nT[q] = tol[q] ? 0u : 0xFFFFFFFFu;
+    lrow[q] = tile + (code[q] <= 9u ? code[q] : (uint32_t)(ER_ROWS - 1));  // no digit: the zero row
+  }
+  uint32_t h[PPL][PLANE_GW];
+  uint32_t fm[PPL];  // first group above the lowest with a feasible match (NO_GROUP - 1: in h)
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) fm[q] = NO_GROUP;
   // Tiles from the top down, each one's groups descending; the lowest group of the slice last.
   for (int32_t t = t_top; t >= 0; --t) {
     const int32_t t_lo = g_lo + t * ER_TG, t_hi = min(t_lo + ER_TG, g_hi);
     if (t != t_top) fill(t_lo);
     const int32_t g_end = t == 0 ? g_lo + 1 : t_lo;  // tile 0: all but the lowest group
     int32_t g = t_hi - 1;
-    for (; g - 1 >= g_end; g -= 2) {  // two groups per step: all their loads before one wait
-      u32x8 x0, x1;
-      sx_load(x0, xplane + (size_t)g * GROUP_DWORDS);
-      sx_load(x1, xplane + (size_t)(g - 1) * GROUP_DWORDS);
-      const uint4* r0 = lrow + (g - t_lo) * ER_Q;
-      const uint4 e00 = r0[0], e01 = r0[ER_ROWS], e10 = r0[-ER_Q], e11 = r0[ER_ROWS - ER_Q];
-      sx_wait(x0, x1);
-      uint32_t h2[PLANE_GW];
-      const bool a0 = rows_hits(e00, e01, x0, nT, h);
-      const bool a1 = rows_hits(e10, e11, x1, nT, h2);
-      fm = a0 ? (uint32_t)g : fm;
-      fm = a1 ? (uint32_t)(g - 1) : fm;
+    for (; g - 1 >= g_end; g -= 2) {  // two groups per step: all their LDS reads before the first use
+      const uint4* tg0 = tile + (g - t_lo) * ER_GQ;
+      const uint4 x00 = tg0[ER_Q], x01 = tg0[ER_Q + 1], x10 = tg0[ER_Q - ER_GQ], x11 = tg0[ER_Q + 1 - ER_GQ];
+      uint4 e[PPL][4];
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) {
+        const uint4* r0 = lrow[q] + (g - t_lo) * ER_GQ;
+        e[q][0] = r0[0];
+        e[q][1] = r0[ER_ROWS];
+        e[q][2] = r0[-ER_GQ];
+        e[q][3] = r0[ER_ROWS - ER_GQ];
+      }
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) {
+        uint32_t h2[PLANE_GW];
+        const bool a0 = rows_hits(e[q][0], e[q][1], x00, x01, nT[q], h[q]);
+        const bool a1 = rows_hits(e[q][2], e[q][3], x10, x11, nT[q], h2);
+        fm[q] = a0 ? (uint32_t)g : fm[q];
+        fm[q] = a1 ? (uint32_t)(g - 1) : fm[q];
+      }
     }
     if (g >= g_end) {
-      u32x8 x0;
-      sx_load(x0, xplane + (size_t)g * GROUP_DWORDS);
-      const uint4* r0 = lrow + (g - t_lo) * ER_Q;
-      const uint4 e00 = r0[0], e01 = r0[ER_ROWS];
-      sx_wait(x0);
-      fm = rows_hits(e00, e01, x0, nT, h) ? (uint32_t)g : fm;
+      const uint4* tg0 = tile + (g - t_lo) * ER_GQ;
+      const uint4 x00 = tg0[ER_Q], x01 = tg0[ER_Q + 1];
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) {
+        const uint4* r0 = lrow[q] + (g - t_lo) * ER_GQ;
+        fm[q] = rows_hits(r0[0], r0[ER_ROWS], x00, x01, nT[q], h[q]) ? (uint32_t)g : fm[q];
+      }
     }
     if (t == 0) {  // the lowest group: its hit words stay in registers for the exact node
-      u32x8 x0;
-      sx_load(x0, xplane + (size_t)g_lo * GROUP_DWORDS);
-      const uint4 e00 = lrow[0], e01 = lrow[ER_ROWS];
-      sx_wait(x0);
-      fm = rows_hits(e00, e01, x0, nT, h) ? NO_GROUP - 1 : fm;  // marker: the first hit is in h
+      const uint4 x00 = tile[ER_Q], x01 = tile[ER_Q + 1];
+#pragma unroll
+      for (int q = 0; q < PPL; ++q)
+        fm[q] = rows_hits(lrow[q][0], lrow[q][ER_ROWS], x00, x01, nT[q], h[q]) ? NO_GROUP - 1 : fm[q];
     }
     __builtin_amdgcn_wave_barrier();
   }
-  uint32_t rm = NOFIT;  // node index of the first feasible match
-  if (fm == NO_GROUP - 1) rm = hits_first(h, (uint32_t)g_lo);
-  else if (fm != NO_GROUP) rm = rows_group_first(a, fm, row, nT);
+  uint32_t rm[PPL];  // node index of the first feasible match
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    rm[q] = NOFIT;
+    if (fm[q] == NO_GROUP - 1) rm[q] = hits_first(h[q], (uint32_t)g_lo);
+    else if (fm[q] != NO_GROUP)
+      rm[q] = rows_group_first(a, fm[q], code[q] <= 9u ? code[q] : (uint32_t)(ER_ROWS - 1), nT[q]);
+  }
   if constexpr (S > 1) {
-    s_res[s][lane] = rm;
+#pragma unroll
+    for (int q = 0; q < PPL; ++q) s_res[s][q][lane] = rm[q];
     __syncthreads();
     if (s != 0) return;
 #pragma unroll
-    for (int k = 1; k < S; ++k) rm = umin(rm, s_res[k][lane]);
+    for (int k = 1; k < S; ++k)
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) rm[q] = umin(rm[q], s_res[k][q][lane]);
   }
   if (SHARD) write_class_keys(a);
-  if (!act) return;
-  if constexpr (SHARD) {
-    a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
-  } else {
-    int32_t oi, ost;
-    int64_t osc;
-    decode_ident(rm != NOFIT ? (int64_t)rm : -1, key_to_idx(tol ? ball1 : ball0), code != CODE_NONE_POD,
-                 make_ident_decode(a.pp), &oi, &osc, &ost);
-    a.out_idx[j] = oi;
-    if (a.out_score) a.out_score[j] = osc;  // optional output (NULL: not written)
-    a.out_status[j] = ost;
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    if (!act[q]) continue;
+    const int32_t j = base + q * WAVE;
+    if constexpr (SHARD) {
+      a.keys[j] = rm[q] != NOFIT ? shard_key(a.node_base, rm[q]) : 0;
+    } else {
+      int32_t oi, ost;
+      int64_t osc;
+      decode_ident(rm[q] != NOFIT ? (int64_t)rm[q] : -1, key_to_idx(tol[q] ? ball1 : ball0),
+                   code[q] != CODE_NONE_POD, make_ident_decode(a.pp), &oi, &osc, &ost);
+      a.out_idx[j] = oi;
+      if (a.out_score) a.out_score[j] = osc;  // optional output (NULL: not written)
+      a.out_status[j] = ost;
+    }
   }
 }
 
@@ -1125,24 +1159,30 @@ hipError_t launch_bits_s(const BatchArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int S, bool SHARD>
+template <int S, bool SHARD, int PPL>
 hipError_t launch_rows_s(const BatchArgs& a, hipStream_t s) {
   BatchArgs ka = a;
   ka.gps = (a.n_groups + S - 1) / S;
-  const int64_t blocks = ((int64_t)a.n_pods + WAVE - 1) / WAVE;
-  hipLaunchKernelGGL((rows_kernel<S, SHARD>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  const int64_t blocks = ((int64_t)a.n_pods + PPL * WAVE - 1) / (PPL * WAVE);
+  hipLaunchKernelGGL((rows_kernel<S, SHARD, PPL>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
   return hipGetLastError();
+}
+
+template <bool SHARD, int PPL>
+hipError_t launch_rows_p(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
+  // slices for the launch's pod blocks of PPL * 64 pods
+  switch (bits_slices((a.n_pods + PPL - 1) / PPL, a.n_groups, dev)) {
+    case 1: return launch_rows_s<1, SHARD, PPL>(a, s);
+    case 2: return launch_rows_s<2, SHARD, PPL>(a, s);
+    case 4: return launch_rows_s<4, SHARD, PPL>(a, s);
+    case 8: return launch_rows_s<8, SHARD, PPL>(a, s);
+    default: return launch_rows_s<16, SHARD, PPL>(a, s);
+  }
 }
 
 template <bool SHARD>
 hipError_t launch_rows_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
-  switch (bits_slices(a.n_pods, a.n_groups, dev)) {
-    case 1: return launch_rows_s<1, SHARD>(a, s);
-    case 2: return launch_rows_s<2, SHARD>(a, s);
-    case 4: return launch_rows_s<4, SHARD>(a, s);
-    case 8: return launch_rows_s<8, SHARD>(a, s);
-    default: return launch_rows_s<16, SHARD>(a, s);
-  }
+  return dev.rows_ppl == 1 ? launch_rows_p<SHARD, 1>(a, dev, s) : launch_rows_p<SHARD, 2>(a, dev, s);
 }
 
 template <bool KX, bool SHARD>

@@ -117,6 +117,7 @@ extern int hipEventCreate(hipEvent_t*);
 extern int hipEventDestroy(hipEvent_t);
 extern int hipEventRecord(hipEvent_t, void*);
 extern int hipEventElapsedTime(float*, hipEvent_t, hipEvent_t);
+extern int hipStreamSynchronize(void*);
 
 enum { SUB_MAXT = 8 };
 static const long long SUB_SPIN_NS = 2000000000LL;  // spin up to 2 s after a run, then sleep
@@ -141,6 +142,7 @@ typedef struct Submitter {
   pthread_cond_t cv;
   atomic_int gen, done, stop, rc;
   long long k;
+  int sync;  // the lanes wait for their own stream before reporting done
 } Submitter;
 
 static long long mono_ns(void) {
@@ -178,6 +180,7 @@ static void* sub_thread(void* v) {
         rc = msh_schedule_batch_device((msh_ctx*)l->ctx, (int32_t)l->p, (const int8_t*)l->pd, (const uint8_t*)l->pt,
                                        (int32_t*)l->oi, (int64_t*)l->os, (int32_t*)l->ost, l->st);
       if (rc == 0 && hipEventRecord(l->e1, l->st)) rc = MSH_ERR_HIP;
+      if (rc == 0 && s->sync && hipStreamSynchronize(l->st)) rc = MSH_ERR_HIP;
       if (rc) {
         int zero = 0;
         atomic_compare_exchange_strong(&s->rc, &zero, rc);
@@ -272,14 +275,17 @@ fail:
   return NULL;
 }
 
-/* run(k) -> rc: k batches over the lanes; returns once all are submitted */
+/* run(k[, sync]) -> rc: k batches over the lanes; returns once all are submitted (sync: once every
+ * lane has also waited for its own stream) */
 static PyObject* sub_run(Submitter* s, PyObject* const* a, Py_ssize_t n) {
-  long long k;
-  if (want_args(n, 1, "run") || as_i64(a[0], &k)) return NULL;
+  long long k, sync = 0;
+  if (n == 2 && as_i64(a[1], &sync)) return NULL;
+  if ((n != 2 && want_args(n, 1, "run")) || as_i64(a[0], &k)) return NULL;
   if (k < 0) return PyErr_Format(PyExc_ValueError, "negative step count");
   if (!s->started) return PyErr_Format(PyExc_RuntimeError, "submitter closed");
   Py_BEGIN_ALLOW_THREADS
   s->k = k;
+  s->sync = sync != 0;
   atomic_store(&s->done, 0);
   atomic_store(&s->rc, 0);
   pthread_mutex_lock(&s->mu);
@@ -315,7 +321,8 @@ static PyObject* sub_close(Submitter* s, PyObject* unused) {
 }
 
 static PyMethodDef sub_methods[] = {
-    {"run", (PyCFunction)(void (*)(void))sub_run, METH_FASTCALL, "run(k) -> rc: submit k batches over the lanes"},
+    {"run", (PyCFunction)(void (*)(void))sub_run, METH_FASTCALL,
+     "run(k[, sync]) -> rc: submit k batches over the lanes (sync: each lane then waits for its stream)"},
     {"span_ms", (PyCFunction)sub_span_ms, METH_NOARGS, "device span of the last run in ms (synchronize first)"},
     {"close", (PyCFunction)sub_close, METH_NOARGS, "stop the lane threads"},
     {NULL, NULL, 0, NULL},

@@ -21,6 +21,10 @@ SUBMIT = {
     "submit:mt4": ["--submit", "mt", "--streams", "4"],
     "submit:mt6": ["--submit", "mt", "--streams", "6"],
 }
+# hardware queues per process (HIP's default 4) x lanes: (env, bench.py flags)
+for hq in (4, 8, 16):
+    for ln in (3, 4, 6):
+        SUBMIT[f"hwq{hq}:mt{ln}"] = ({"GPU_MAX_HW_QUEUES": str(hq)}, ["--submit", "mt", "--streams", str(ln)])
 VARIANTS = {
     "base": {},
     "dev_kernarg_0": {"HIP_FORCE_DEV_KERNARG": "0"},
@@ -39,8 +43,11 @@ for name, env in list(VARIANTS.items()) + list(SUBMIT.items()):
         continue
     for k, reps in ((20, REPS), (200, 1)):
         for rep in range(reps):
-            extra = env if isinstance(env, list) else []
-            e = dict(os.environ, **(env if isinstance(env, dict) else {}))
+            if isinstance(env, tuple):
+                ev, extra = env
+            else:
+                ev, extra = (env, []) if isinstance(env, dict) else ({}, env)
+            e = dict(os.environ, **ev)
             cmd = [sys.executable, str(ROOT / "bench.py"), "--steps", str(k), "--warmup", "5",
                    "--no-extras", "--cpu-seconds", "0", *extra]
             try:
@@ -52,7 +59,7 @@ for name, env in list(VARIANTS.items()) + list(SUBMIT.items()):
                 print(json.dumps({"variant": name, "k": k, "rc": r.returncode, "err": r.stderr[-400:]}), flush=True)
                 sys.exit(1)
             line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-            print(json.dumps({"variant": name, "env": env, "k": k, "rep": rep,
+            print(json.dumps({"variant": name, "env": ev, "args": extra, "k": k, "rep": rep,
                               "ms_per_step": line["ms_per_step"], "value": line["value"],
                               "kernel_ms": line["roofline"]["kernel_ms"],
                               "kernel_ms_isolated": line["roofline"]["kernel_ms_isolated"],

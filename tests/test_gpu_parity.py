@@ -539,15 +539,17 @@ def test_maximum_node_table(msh, gpu_ctx, synth):
 
 @pytest.mark.parametrize("slices", ["1", "2", "4", "8", "16"])
 @pytest.mark.parametrize("n", [20_000, 70_000])
-def test_bits_slices(msh, oracle, n, slices, monkeypatch):
+@pytest.mark.parametrize("ppl", ["1", "2"])
+def test_bits_slices(msh, oracle, n, slices, ppl, monkeypatch):
     """Few pods against a large table: SLICES waves share each 64-pod block, each scanning a range
     of 256-node groups, firsts merged by min in LDS. Every slice count (MSH_BITS_SLICES, read once
     by msh_create) against the oracle, for the batch and the shard-key entry points, in the
     identity-like and the non-match (MINMAX) modes."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("MSH_BITS_SLICES", slices)
+    monkeypatch.setenv("MSH_ROWS_PPL", ppl)  # pods per lane of the digit-row kernel
     rng = np.random.default_rng(n + int(slices))
-    u, nd, pd, pt = _rand_case(rng, n, 1500, p_unsched=0.2, p_tol=0.3)
+    u, nd, pd, pt = _rand_case(rng, n, 1500 + int(ppl) * 37, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4  # digit 3 only in the second half: late first matches
     dev = torch.device("cuda:0")
     d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
@@ -558,7 +560,7 @@ def test_bits_slices(msh, oracle, n, slices, monkeypatch):
             _set(ctx, msh, ps)
             ctx.upload_nodes(u, nd)
             want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
-            _assert_same(ctx.schedule_batch(pd, pt), want, f"slices={slices} n={n} norm={norm}")
+            _assert_same(ctx.schedule_batch(pd, pt), want, f"slices={slices} ppl={ppl} n={n} norm={norm}")
             keys = torch.empty(ctx.shard_keys_len(p), dtype=torch.int32, device=dev)
             ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream)
