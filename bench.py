@@ -42,14 +42,14 @@ sys.path.insert(0, str(ROOT))
 METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
 VALU_PEAK_LANE_OPS = 157.3e12 / 2  # MI355X_MICROARCH.md: FP32 vector peak 157.3 TFLOPS = 2 x lane-ops/s
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-N_SIMD = 256 * 4
-# Instruction model of bits_kernel's scan (msh_kernels.hip): per pod (lane) and 32-node word,
-# 1 v_and + 4 v_bitop3 (5 VALU), plus one v_bitop3 per two words (the group AND) and a compare +
-# select per 8-word group: 46 VALU per 8 words -> 5.75 wave-instr per 32 x 64 pairs.
-VALU_PER_WORD = 46 / 8
-LANE_OPS_PER_EVAL = VALU_PER_WORD / 32
+# The digit-row kernel (rows_kernel, the identity-like modes): per 8-word group and 64-pod wave,
+# four ds_read_b128 (the lane's row words of both chunks, and the group's X words at one address)
+# = 4 KiB through the LDS array (4 LDS cycles each, MI355X_MICROARCH.md LDS table), and 8 v_bitop3
+# + 4 ORs + compare + select + the running-first move = 15 VALU.
+LDS_PEAK = 150e12                  # MI355X_MICROARCH.md: ~150 TB/s aggregate for ds_read_b64/b128
+ROWS_LDS_BYTES_PER_GROUP_WAVE = 4 * 1024
+ROWS_VALU_PER_GROUP = 15
 PMC_FILE = ROOT / "profiles" / "r2_pmc_c3.json"
-UBENCH = ROOT / "profiles" / "r2_ubench_bitop3.jsonl"
 
 
 def bits_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False) -> str:
@@ -61,7 +61,7 @@ def bits_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sha
     while sl < 16 and blocks * sl < cus * 4 * 6 and groups // (2 * sl) >= 2:
         sl *= 2
     if not kx:  # identity-like modes: the digit-row kernel
-        return f"void msh::rows_kernel<{sl}, {str(shard).lower()}>"
+        return f"void msh::rows_kernel<{sl}, {str(shard).lower()}, 1>"  # 1 pod per lane (rows_ppl)
     return f"void msh::bits_kernel<{sl}, {str(kx).lower()}, {str(shard).lower()}>"
 
 
@@ -105,17 +105,6 @@ def parse():
 def load_json(path: Path):
     try:
         return json.loads(path.read_text())
-    except Exception:
-        return None
-
-
-def measured_bitop3_ceiling():
-    """Lane-ops/s of the scan's own instruction forms (v_bitop3_b32 / v_and_b32 with an SGPR
-    source, 8 waves per SIMD), measured by scripts/ubench_bitop3.hip (profiles/r2_ubench_bitop3.jsonl)."""
-    try:
-        rows = [json.loads(l) for l in UBENCH.read_text().splitlines() if l.startswith("{")]
-        ipc = max(r["wave_instr_per_simd_cycle@2.4GHz"] for r in rows if r.get("op") == "bits scan mix")
-        return ipc * 2.4e9 * N_SIMD * 64
     except Exception:
         return None
 
@@ -488,22 +477,27 @@ def make_roofline(mode, n_local, p, kernel_ms, kernel_ms_isolated, nstreams, cus
     evals = float(n_local) * p
     entry = pmc.get("kernels", {}).get("batch", {})
     pmc_ok = entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
-    # achieved = ALGORITHMIC lane-ops (the scan's instruction model: 46 VALU per 8 words per 64
-    # pods) / launch interval; next to it the counter-derived figure (SQ_INSTS_VALU x 64 of the
-    # same kernel at the same size, profiles/r2_pmc_c3.json), which adds the per-wave prologue,
-    # first-node decode, slice merge and epilogue
-    model_ops = LANE_OPS_PER_EVAL * evals
+    n_groups = max(-(-n_local // 1024) * 1024, 1024) // 256
+    group_waves = float(n_groups) * -(-p // 64)  # every 64-pod block meets every 256-node group once
+    # achieved = ALGORITHMIC LDS-array bytes of the scan per launch (4 KiB per group and 64-pod wave:
+    # 0.25 B per pod-node pair) / launch interval; next to it the counters of the same kernel at the
+    # same size (profiles/r2_pmc_c3.json): SQ_LDS_IDX_ACTIVE (LDS-array cycles, all CUs) and
+    # SQ_INSTS_VALU x 64 (the scan plus the per-wave prologue, tile copy, first-node decode, slice
+    # merge and epilogue)
+    lds_bytes = group_waves * ROWS_LDS_BYTES_PER_GROUP_WAVE
+    lds_cycles = entry.get("SQ_LDS_IDX_ACTIVE") if pmc_ok else None
+    model_ops = group_waves * ROWS_VALU_PER_GROUP * 64
     valu_instr = entry.get("SQ_INSTS_VALU") if pmc_ok else None
     counter_ops = valu_instr * 64 if valu_instr else None
-    ceiling = measured_bitop3_ceiling()
-    uniq_bytes = 0.75 * n_local + 18.0 * p         # bit planes + pod records + outputs, once
-    survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts L1/L2 re-reads)
+    uniq_bytes = 1.5 * n_local + 18.0 * p           # digit rows + X words, pod records + outputs, once
+    survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts L1/L2/LDS re-reads)
+    lds_clk = LDS_PEAK / (256 * 256)                 # the guide's aggregate as LDS-array cycles per CU
     return {
-        "bound": "valu",
-        "achieved": model_ops / kern_s / 1e9,
-        "peak": VALU_PEAK_LANE_OPS / 1e9,
-        "unit": "Glane-op/s",
-        "frac": model_ops / kern_s / VALU_PEAK_LANE_OPS,
+        "bound": "lds",
+        "achieved": lds_bytes / kern_s / 1e9,
+        "peak": LDS_PEAK / 1e9,
+        "unit": "GB/s",
+        "frac": lds_bytes / kern_s / LDS_PEAK,
         "traffic": entry.get("hbm_bytes_per_launch") if pmc_ok else None,
         "traffic_note": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024), same kernel and size",
         "kernel": kname,
@@ -512,23 +506,27 @@ def make_roofline(mode, n_local, p, kernel_ms, kernel_ms_isolated, nstreams, cus
                            "kernel_ms_isolated = the same launches back to back on one stream "
                            "(= rocprofv3's per-kernel average)") if nstreams > 1 else "one stream",
         "kernel_ms_isolated": kernel_ms_isolated,
-        "frac_isolated": model_ops / iso_s / VALU_PEAK_LANE_OPS,
-        "valu_lane_ops_per_eval_model": LANE_OPS_PER_EVAL,
-        "valu_lane_ops_per_eval_measured": valu_instr * 64 / evals if valu_instr else None,
-        "frac_counter": counter_ops / kern_s / VALU_PEAK_LANE_OPS if counter_ops else None,
-        "counter_source": ("rocprofv3 SQ_INSTS_VALU x 64 per launch (profiles/r2_pmc_c3.json)" if valu_instr
+        "frac_isolated": lds_bytes / iso_s / LDS_PEAK,
+        "lds_bytes_per_launch": lds_bytes,
+        "lds_bytes_per_eval": lds_bytes / evals,
+        "frac_counter": (lds_cycles / (cus * kern_s * lds_clk)) if lds_cycles else None,
+        "counter_source": ("rocprofv3 SQ_LDS_IDX_ACTIVE per launch (profiles/r2_pmc_c3.json)" if lds_cycles
                            else "no PMC entry for this kernel and size"),
-        "scan_share_of_valu": model_ops / counter_ops if counter_ops else None,
-        "measured_bitop3_ceiling": ceiling / 1e9 if ceiling else None,
-        "frac_counter_vs_measured_bitop3_ceiling": (counter_ops / kern_s / ceiling) if (ceiling and counter_ops) else None,
-        "peak_note": "peak = FP32 vector 157.3 TF / 2 (one lane-op per lane per 2-cycle wave64 issue); the scan's "
-                     "v_bitop3 with an SGPR plane issues every ~4 cycles (measured_bitop3_ceiling)",
+        "peak_note": "peak = MI355X_MICROARCH.md LDS aggregate for ds_read_b128 (256 B/clk/CU); the scan moves "
+                     "4 KiB through the LDS array per 256-node group and 64-pod wave (rows + broadcast X words)",
+        "valu": {"bound": "valu", "unit": "Glane-op/s", "peak": VALU_PEAK_LANE_OPS / 1e9,
+                 "achieved_model": model_ops / kern_s / 1e9, "frac_model": model_ops / kern_s / VALU_PEAK_LANE_OPS,
+                 "lane_ops_per_eval_model": model_ops / evals,
+                 "lane_ops_per_eval_measured": counter_ops / evals if counter_ops else None,
+                 "frac_counter": counter_ops / kern_s / VALU_PEAK_LANE_OPS if counter_ops else None,
+                 "scan_share_of_valu": model_ops / counter_ops if counter_ops else None,
+                 "note": "peak = FP32 vector 157.3 TF / 2 (one lane-op per lane per 2-cycle wave64 issue)"},
         "hbm": {"bound": "hbm", "achieved": uniq_bytes / kern_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": uniq_bytes / kern_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
                 "survey_8d_bytes_per_launch": survey_bytes,
                 "survey_8d_frac": survey_bytes / kern_s / HBM_PEAK,
-                "survey_8d_note": "2 B per pair counts every L1/L2/SGPR re-read of the node table as HBM "
-                                  "traffic; the 4 KB table is read from HBM once per launch"},
+                "survey_8d_note": "2 B per pair counts every L1/L2/LDS re-read of the node table as HBM "
+                                  "traffic; the 7.5 KB table is read from HBM once per launch"},
     }
 
 
