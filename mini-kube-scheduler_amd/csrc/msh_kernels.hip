@@ -450,16 +450,21 @@ __device__ __forceinline__ uint32_t hit_s(uint32_t e, uint32_t x, uint32_t m) {
   return r;
 }
 
-// The first node among 8 hit words of group g (words ascend in List order, bits within a word).
+// The first node among 8 hit words of group g (words ascend in List order, bits within a word):
+// v_ffbl_b32 gives each word's lowest set bit, all-ones for an empty word, which ORed with the
+// word's offset (32 c) stays all-ones; the unsigned minimum over the words is the first hit.
+// 19 VALU (selects per word: ~30). The group must hold a hit.
+__device__ __forceinline__ uint32_t lowbit(uint32_t x) {  // v_ffbl_b32: all-ones for 0 (ctz's 0 is UB)
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 __device__ __forceinline__ uint32_t hits_first(const uint32_t (&h)[PLANE_GW], uint32_t g) {
-  uint32_t bw = 0;
-  int32_t bj = 0;
+  uint32_t t[PLANE_GW];
 #pragma unroll
-  for (int c = PLANE_GW - 1; c >= 0; --c) {
-    bj = h[c] ? c : bj;
-    bw = h[c] ? h[c] : bw;
-  }
-  return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
+  for (int c = 0; c < PLANE_GW; ++c) t[c] = lowbit(h[c]) | (uint32_t)(32 * c);
+  const uint32_t m = umin(umin(umin(t[0], t[1]), umin(t[2], t[3])), umin(umin(t[4], t[5]), umin(t[6], t[7])));
+  return g * GROUP_NODES + m;
 }
 
 // The lane's first feasible match in group g, from memory (its row words and the X plane).
