@@ -498,8 +498,25 @@ __device__ __forceinline__ bool rows_hits(const uint4& e0, const uint4& e1, cons
   return ((h[0] | h[1] | h[2]) | (h[3] | h[4] | h[5]) | (h[6] | h[7])) != 0u;
 }
 
+#ifdef MSH_STAMPS
+// Timeline A/B build only (scripts/stamps.sh; never in libminisched_hip.so): per wave, the
+// 100 MHz wall clock at entry, after the prologue's loads, after the scan and before the stores.
+__device__ unsigned long long* g_stamps;
+#define MSH_STAMP(i) (__builtin_amdgcn_s_waitcnt(0), stamp_t[i] = wall_clock64())
+#else
+#define MSH_STAMP(i) ((void)0)
+#endif
+
 template <int S, bool SHARD, int PPL>
 __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
+#ifdef MSH_STAMPS
+  unsigned long long stamp_t[4] = {0, 0, 0, 0};
+  MSH_STAMP(0);
+  auto stamps_out = [&]() {
+    if ((threadIdx.x & (WAVE - 1)) == 0)
+      for (int i = 0; i < 4; ++i) g_stamps[((size_t)blockIdx.x * S + (threadIdx.x >> 6)) * 4 + i] = stamp_t[i];
+  };
+#endif
   __shared__ uint4 s_tile[S][ER_TG * ER_GQ];
   __shared__ uint32_t s_res[S][PPL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -547,6 +564,7 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
     nT[q] = tol[q] ? 0u : 0xFFFFFFFFu;
     lrow[q] = tile + (code[q] <= 9u ? code[q] : (uint32_t)(ER_ROWS - 1));  // no digit: the zero row
   }
+  MSH_STAMP(1);
   uint32_t h[PPL][PLANE_GW];
   uint32_t fm[PPL];  // first group above the lowest with a feasible match (NO_GROUP - 1: in h)
 #pragma unroll
@@ -596,6 +614,7 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
     __builtin_amdgcn_wave_barrier();
   }
   uint32_t rm[PPL];  // node index of the first feasible match
+  MSH_STAMP(2);
 #pragma unroll
   for (int q = 0; q < PPL; ++q) {
     rm[q] = NOFIT;
@@ -607,13 +626,24 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
 #pragma unroll
     for (int q = 0; q < PPL; ++q) s_res[s][q][lane] = rm[q];
     __syncthreads();
+#ifdef MSH_STAMPS
+    if (s != 0) {
+      stamps_out();
+      return;
+    }
+#else
     if (s != 0) return;
+#endif
 #pragma unroll
     for (int k = 1; k < S; ++k)
 #pragma unroll
       for (int q = 0; q < PPL; ++q) rm[q] = umin(rm[q], s_res[k][q][lane]);
   }
   if (SHARD) write_class_keys(a);
+#ifdef MSH_STAMPS
+  MSH_STAMP(3);
+  stamps_out();
+#endif
 #pragma unroll
   for (int q = 0; q < PPL; ++q) {
     if (!act[q]) continue;
@@ -1290,5 +1320,9 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
   if (nw == 4) return launch_seq_nw<4, false>(ka, rs, s);
   return launch_seq_nw<15, false>(ka, rs, s);
 }
+
+#ifdef MSH_STAMPS
+extern "C" int msh_stamps_set(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
+#endif
 
 }  // namespace msh
