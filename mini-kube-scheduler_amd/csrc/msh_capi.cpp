@@ -561,7 +561,8 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
     MSH_HIP(c, hipMalloc(&c->d_digit, cap));
     MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
     MSH_HIP(c, hipMalloc(&c->d_planes, cap / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
-    MSH_HIP(c, hipMalloc(&c->d_erows, cap / msh::GROUP_NODES * msh::ER_GD * sizeof(uint32_t)));
+    // + ER_TG groups: the batch kernel copies whole tiles without clamping (never read as rows)
+    MSH_HIP(c, hipMalloc(&c->d_erows, (cap / msh::GROUP_NODES + msh::ER_TG) * msh::ER_GD * sizeof(uint32_t)));
     c->node_cap = cap;
   }
   if (n > 0) {

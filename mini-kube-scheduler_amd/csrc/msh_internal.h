@@ -84,6 +84,8 @@ constexpr int ER_ROWS = 11;
 constexpr int ER_Q = 2 * ER_ROWS;      // 16-byte row chunks per group
 constexpr int ER_GQ = ER_Q + 2;        // 16-byte chunks per group: the rows, then X
 constexpr int ER_GD = ER_GQ * 4;       // dwords per group
+constexpr int ER_TG = 8;               // groups per LDS tile of the batch kernel (3,072 B per wave);
+                                       // the table is allocated with ER_TG groups of padding
 
 // ---- launchers (msh_kernels.hip) ----
 // Applies `patch_count` pending msh_patch_nodes entries (idx | unsched << 32 | (uint8)digit << 40)

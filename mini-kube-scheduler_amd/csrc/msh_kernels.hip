@@ -441,7 +441,6 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
 // clock per wave-word per CU, with LDS reads (one b128 per 4 words, 1 clock per wave-word per CU)
 // beside it. Slices and the LDS merge of their firsts as in bits_kernel.
 // ---------------------------------------------------------------------------------------
-constexpr int ER_TG = 8;  // groups per LDS tile (3,072 B per wave)
 
 // e & ~(x & m) in one v_bitop3_b32 (truth table 0x70 over S0 = e, S1 = x, S2 = m), x wave-uniform
 __device__ __forceinline__ uint32_t hit_s(uint32_t e, uint32_t x, uint32_t m) {
@@ -523,36 +522,47 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
   const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   // PPL pods per lane: lane l holds pods base + q * 64 + l (q < PPL); the group's X words and the
   // staged row tile serve all of them
-  const int32_t base = (int32_t)blockIdx.x * (PPL * WAVE) + lane;
-  // Prologue: the pod bytes (clamped index: no branch, so nothing waits for them yet), the class
-  // firsts and the top tile's row words are all requested before the first use of any of them.
-  int dq[PPL];
-  uint8_t tq[PPL];
-#pragma unroll
-  for (int q = 0; q < PPL; ++q) {
-    const int32_t jc = min(base + q * WAVE, a.n_pods - 1);  // n_pods >= 1 (empty batches never launch)
-    dq[q] = a.pod_digit[jc];
-    tq[q] = a.pod_tol[jc];
-  }
-  const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
+  const int32_t block0 = (int32_t)blockIdx.x * (PPL * WAVE);
+  const int32_t base = block0 + lane;
   const int32_t g_lo = min(s * a.gps, a.n_groups), g_hi = min(g_lo + a.gps, a.n_groups);
   const int32_t ng = g_hi - g_lo;
   const uint4* __restrict__ er = reinterpret_cast<const uint4*>(a.erows);
   uint4* tile = s_tile[s];
-  // this wave's tile, read only by this wave: a whole ER_TG-group tile is copied (sources clamped
-  // to the table, so all loads issue before any wait; rows past the slice are never read)
-  const int32_t q_last = a.n_groups * ER_GQ - 1;
+  // This wave's tile, read only by this wave: a whole ER_TG-group tile is copied, three 16-byte
+  // copies per lane (the table carries ER_TG groups of padding, so no copy needs a clamp; rows past
+  // the slice are never read). Loads and stores are separate so that the prologue can put the
+  // pod-byte loads between them.
   static_assert(ER_TG * ER_GQ == 3 * WAVE, "fill: three 16-byte copies per lane");
-  auto fill = [&](int32_t t_lo) {
-    const int32_t q0 = t_lo * ER_GQ + lane;
-    const uint4 v0 = er[min(q0, q_last)], v1 = er[min(q0 + WAVE, q_last)], v2 = er[min(q0 + 2 * WAVE, q_last)];
-    tile[lane] = v0;
-    tile[lane + WAVE] = v1;
-    tile[lane + 2 * WAVE] = v2;
+  uint4 f0, f1, f2;
+  auto fill_load = [&](int32_t t_lo) {
+    const uint4* src = er + (uint32_t)(t_lo * ER_GQ);  // wave-uniform base, 32-bit lane offsets
+    f0 = src[(uint32_t)lane];
+    f1 = src[(uint32_t)(lane + WAVE)];
+    f2 = src[(uint32_t)(lane + 2 * WAVE)];
+  };
+  auto fill_store = [&]() {
+    tile[lane] = f0;
+    tile[lane + WAVE] = f1;
+    tile[lane + 2 * WAVE] = f2;
     __builtin_amdgcn_wave_barrier();
   };
+  // Prologue: the top tile's row words, the pod bytes (clamped offset: no branch, so nothing waits
+  // for them yet) and the class firsts are all requested before the first use of any of them.
   const int32_t t_top = ng > 0 ? (ng - 1) / ER_TG : -1;
-  if (t_top >= 0) fill(g_lo + t_top * ER_TG);
+  fill_load(g_lo + max(t_top, 0) * ER_TG);  // (an empty slice copies a padding tile it never reads)
+  int dq[PPL];
+  uint8_t tq[PPL];
+  const uint32_t last = (uint32_t)(a.n_pods - 1 - block0);  // n_pods > block0 (empty batches never launch)
+  const int8_t* pdb = a.pod_digit + block0;                   // wave-uniform bases, 32-bit lane offsets
+  const uint8_t* ptb = a.pod_tol + block0;
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    const uint32_t off = min((uint32_t)(lane + q * WAVE), last);
+    dq[q] = pdb[off];
+    tq[q] = ptb[off];
+  }
+  const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
+  fill_store();
   bool act[PPL];
   uint32_t code[PPL], tol[PPL], nT[PPL];
   const uint4* lrow[PPL];  // the lane's row in chunk 0 of a tile's first group
@@ -572,7 +582,10 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
   // Tiles from the top down, each one's groups descending; the lowest group of the slice last.
   for (int32_t t = t_top; t >= 0; --t) {
     const int32_t t_lo = g_lo + t * ER_TG, t_hi = min(t_lo + ER_TG, g_hi);
-    if (t != t_top) fill(t_lo);
+    if (t != t_top) {
+      fill_load(t_lo);
+      fill_store();
+    }
     const int32_t g_end = t == 0 ? g_lo + 1 : t_lo;  // tile 0: all but the lowest group
     int32_t g = t_hi - 1;
     for (; g - 1 >= g_end; g -= 2) {  // two groups per step: all their LDS reads before the first use
