@@ -8,7 +8,10 @@ inputs already resident in HBM.
 
 Modes (the headline line)
   batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per GPU. With N GPUs the pods
-              are sharded (each rank its own 100k batch; no data-path collective) -> weak scaling.
+              are sharded (each rank its own 100k batches; no data-path collective) -> weak
+              scaling. The K steps are submitted from three host threads, each with its own ctx,
+              HIP stream and pod batch (the fast-call module's Submitter): one HIP launch costs
+              more host time than a batch takes on the device.
   sequential  BASELINE C5: same sizes, one pod at a time with node-state commits.
   nodeshard   BASELINE C4 shape: the node table split over the ranks, per-shard first keys
               merged with an RCCL all-reduce(MAX), then decoded (--nodes 100000 --pods 1000000).
