@@ -92,7 +92,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary configs (one GPU only)")
     ap.add_argument("--streams", type=int, default=None,
                     help="batch mode: independent batches pipelined over this many HIP streams "
-                         "(default 3 with --submit mt, else 2)")
+                         "(default with --submit mt: 4 for K <= 64 steps, else 3; otherwise 2)")
     ap.add_argument("--submit", choices=["mt", "c", "python"], default="mt",
                     help="batch mode: the K timed steps submitted from one host thread per stream, each "
                          "with its own ctx (mt, csrc/msh_pyfast.c Submitter: one HIP launch costs more host "
@@ -192,7 +192,11 @@ def main():
     # Sequential mode carries node state from batch to batch and node-shard mode has a collective
     # per step: both stay on one stream.
     mt = mode == "batch" and args.submit == "mt" and args.launch == "eager"
-    nstreams = (args.streams or (3 if mt else 2)) if mode == "batch" else 1
+    # Lanes for --submit mt: a lane's kernels run back to back on its stream at the one-stream
+    # latency (~4 us at C3), so a short burst of K batches ends sooner spread over 4 lanes; in a
+    # long run 4 lanes contend and 3 complete batches faster (profiles/ab/r2_lanes_k20_k200.jsonl:
+    # K = 20 4.5 vs 4.9 us per step, K = 200 2.20 vs 1.97)
+    nstreams = (args.streams or ((4 if args.steps <= 64 else 3) if mt else 2)) if mode == "batch" else 1
     if mode == "nodeshard":
         sharded = D.NodeShardedScheduler(ctx, unsched, node_digit, world, rank)
         node_base = sharded.shard.lo
