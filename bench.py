@@ -366,7 +366,11 @@ def main():
         torch.cuda.synchronize()
         t_idle = time.perf_counter() - t_idle
         print(json.dumps({"probe": {"submit_us": (t_sub - t0) * 1e6, "sync_us": (elapsed - (t_sub - t0)) * 1e6,
-                                    "idle_sync_us": t_idle * 1e6, "steps": args.steps}}), file=sys.stderr, flush=True)
+                                    "idle_sync_us": t_idle * 1e6, "steps": args.steps,
+                                    "lanes_host_us": ([[round(x, 2) for x in r] for r in sub.host_us()]
+                                                      if sub is not None else None),
+                                    "lanes_event_us": ([[round(x * 1e3, 2) for x in r] for r in sub.events_ms()]
+                                                       if sub is not None else None)}}), file=sys.stderr, flush=True)
     if per_step:
         kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     elif sub is not None:  # each lane's start / end events on its stream: latest end - earliest start

@@ -602,8 +602,8 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
       }
 #pragma unroll
       for (int q = 0; q < PPL; ++q) {
-        uint32_t h2[PLANE_GW];
-        const bool a0 = rows_hits(e[q][0], e[q][1], x00, x01, nT[q], h[q]);
+        uint32_t h1[PLANE_GW], h2[PLANE_GW];  // (only the lowest group's words are kept, in h)
+        const bool a0 = rows_hits(e[q][0], e[q][1], x00, x01, nT[q], h1);
         const bool a1 = rows_hits(e[q][2], e[q][3], x10, x11, nT[q], h2);
         fm[q] = a0 ? (uint32_t)g : fm[q];
         fm[q] = a1 ? (uint32_t)(g - 1) : fm[q];
@@ -615,7 +615,8 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
 #pragma unroll
       for (int q = 0; q < PPL; ++q) {
         const uint4* r0 = lrow[q] + (g - t_lo) * ER_GQ;
-        fm[q] = rows_hits(r0[0], r0[ER_ROWS], x00, x01, nT[q], h[q]) ? (uint32_t)g : fm[q];
+        uint32_t h1[PLANE_GW];
+        fm[q] = rows_hits(r0[0], r0[ER_ROWS], x00, x01, nT[q], h1) ? (uint32_t)g : fm[q];
       }
     }
     if (t == 0) {  // the lowest group: its hit words stay in registers for the exact node

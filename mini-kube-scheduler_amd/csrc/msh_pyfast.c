@@ -122,11 +122,14 @@ extern int hipStreamSynchronize(void*);
 enum { SUB_MAXT = 8 };
 static const long long SUB_SPIN_NS = 2000000000LL;  // spin up to 2 s after a run, then sleep
 
+enum { SUB_NT = 24 };  // host timestamps kept per lane and run (A/B probe)
 typedef struct {
   void *ctx, *pd, *pt, *oi, *os, *ost, *st;
   long long p;
   hipEvent_t e0, e1;
   int ran;
+  int nt;                 // timestamps taken in the last run
+  long long ts[SUB_NT];   // wake, after the start event, after each launch..., after the end event
 } SubLane;
 
 typedef struct Submitter {
@@ -142,6 +145,7 @@ typedef struct Submitter {
   pthread_cond_t cv;
   atomic_int gen, done, stop, rc;
   long long k;
+  long long t_go;  // CLOCK_MONOTONIC ns at the signal of the last run
   int sync;  // the lanes wait for their own stream before reporting done
 } Submitter;
 
@@ -174,12 +178,20 @@ static void* sub_thread(void* v) {
     seen = atomic_load_explicit(&s->gen, memory_order_acquire);
     const long long k = s->k;
     l->ran = t < k;
+    l->nt = 0;
+#define SUB_TS() \
+  if (l->nt < SUB_NT) l->ts[l->nt++] = mono_ns()
+    SUB_TS();
     if (l->ran) {
       int rc = hipEventRecord(l->e0, l->st) ? MSH_ERR_HIP : 0;
-      for (long long i = t; i < k && rc == 0; i += s->nt)
+      SUB_TS();
+      for (long long i = t; i < k && rc == 0; i += s->nt) {
         rc = msh_schedule_batch_device((msh_ctx*)l->ctx, (int32_t)l->p, (const int8_t*)l->pd, (const uint8_t*)l->pt,
                                        (int32_t*)l->oi, (int64_t*)l->os, (int32_t*)l->ost, l->st);
+        SUB_TS();
+      }
       if (rc == 0 && hipEventRecord(l->e1, l->st)) rc = MSH_ERR_HIP;
+      SUB_TS();
       if (rc == 0 && s->sync && hipStreamSynchronize(l->st)) rc = MSH_ERR_HIP;
       if (rc) {
         int zero = 0;
@@ -286,6 +298,7 @@ static PyObject* sub_run(Submitter* s, PyObject* const* a, Py_ssize_t n) {
   Py_BEGIN_ALLOW_THREADS
   s->k = k;
   s->sync = sync != 0;
+  s->t_go = mono_ns();
   atomic_store(&s->done, 0);
   atomic_store(&s->rc, 0);
   pthread_mutex_lock(&s->mu);
@@ -314,6 +327,48 @@ static PyObject* sub_span_ms(Submitter* s, PyObject* unused) {
   return PyFloat_FromDouble(best);
 }
 
+/* host_us() -> [[us, ...] per lane]: the lanes' host timestamps of the last run, relative to the
+ * run's signal: wake, after the start event, after each launch, after the end event (A/B probe) */
+static PyObject* sub_host_us(Submitter* s, PyObject* unused) {
+  (void)unused;
+  PyObject* out = PyList_New(s->nt);
+  if (!out) return NULL;
+  for (int t = 0; t < s->nt; ++t) {
+    PyObject* row = PyList_New(s->lane[t].nt);
+    if (!row) {
+      Py_DECREF(out);
+      return NULL;
+    }
+    for (int i = 0; i < s->lane[t].nt; ++i)
+      PyList_SET_ITEM(row, i, PyFloat_FromDouble((double)(s->lane[t].ts[i] - s->t_go) * 1e-3));
+    PyList_SET_ITEM(out, t, row);
+  }
+  return out;
+}
+
+/* events_ms() -> [(start, end) per lane] in ms relative to lane 0's start event (synchronize first) */
+static PyObject* sub_events_ms(Submitter* s, PyObject* unused) {
+  (void)unused;
+  PyObject* out = PyList_New(0);
+  if (!out || !s->lane[0].ran) return out;
+  for (int t = 0; t < s->nt; ++t) {
+    if (!s->lane[t].ran) continue;
+    float a = 0, b = 0;
+    if (hipEventElapsedTime(&a, s->lane[0].e0, s->lane[t].e0) || hipEventElapsedTime(&b, s->lane[0].e0, s->lane[t].e1)) {
+      Py_DECREF(out);
+      return PyErr_Format(PyExc_RuntimeError, "hipEventElapsedTime failed (synchronize first)");
+    }
+    PyObject* pr = Py_BuildValue("(dd)", (double)a, (double)b);
+    if (!pr || PyList_Append(out, pr)) {
+      Py_XDECREF(pr);
+      Py_DECREF(out);
+      return NULL;
+    }
+    Py_DECREF(pr);
+  }
+  return out;
+}
+
 static PyObject* sub_close(Submitter* s, PyObject* unused) {
   (void)unused;
   sub_stop(s);
@@ -324,6 +379,8 @@ static PyMethodDef sub_methods[] = {
     {"run", (PyCFunction)(void (*)(void))sub_run, METH_FASTCALL,
      "run(k[, sync]) -> rc: submit k batches over the lanes (sync: each lane then waits for its stream)"},
     {"span_ms", (PyCFunction)sub_span_ms, METH_NOARGS, "device span of the last run in ms (synchronize first)"},
+    {"host_us", (PyCFunction)sub_host_us, METH_NOARGS, "the lanes' host timestamps of the last run (A/B probe)"},
+    {"events_ms", (PyCFunction)sub_events_ms, METH_NOARGS, "per lane (start, end) event times vs lane 0's start"},
     {"close", (PyCFunction)sub_close, METH_NOARGS, "stop the lane threads"},
     {NULL, NULL, 0, NULL},
 };
