@@ -334,8 +334,7 @@ def main():
     if sub is None:
         r0.record(S.main)
     if sub is not None:
-        # MSH_BENCH_LANESYNC (A/B): each lane also waits for its own stream before run() returns
-        rc = sub.run(args.steps, 1 if os.environ.get("MSH_BENCH_LANESYNC") else 0)
+        rc = sub.run(args.steps)
         if rc:
             ctx._check(rc)
     elif graph is not None:

@@ -117,7 +117,6 @@ extern int hipEventCreate(hipEvent_t*);
 extern int hipEventDestroy(hipEvent_t);
 extern int hipEventRecord(hipEvent_t, void*);
 extern int hipEventElapsedTime(float*, hipEvent_t, hipEvent_t);
-extern int hipStreamSynchronize(void*);
 
 enum { SUB_MAXT = 8 };
 static const long long SUB_SPIN_NS = 2000000000LL;  // spin up to 2 s after a run, then sleep
@@ -146,7 +145,6 @@ typedef struct Submitter {
   atomic_int gen, done, stop, rc;
   long long k;
   long long t_go;  // CLOCK_MONOTONIC ns at the signal of the last run
-  int sync;  // the lanes wait for their own stream before reporting done
 } Submitter;
 
 static long long mono_ns(void) {
@@ -192,7 +190,6 @@ static void* sub_thread(void* v) {
       }
       if (rc == 0 && hipEventRecord(l->e1, l->st)) rc = MSH_ERR_HIP;
       SUB_TS();
-      if (rc == 0 && s->sync && hipStreamSynchronize(l->st)) rc = MSH_ERR_HIP;
       if (rc) {
         int zero = 0;
         atomic_compare_exchange_strong(&s->rc, &zero, rc);
@@ -287,17 +284,14 @@ fail:
   return NULL;
 }
 
-/* run(k[, sync]) -> rc: k batches over the lanes; returns once all are submitted (sync: once every
- * lane has also waited for its own stream) */
+/* run(k) -> rc: k batches over the lanes; returns once all are submitted */
 static PyObject* sub_run(Submitter* s, PyObject* const* a, Py_ssize_t n) {
-  long long k, sync = 0;
-  if (n == 2 && as_i64(a[1], &sync)) return NULL;
-  if ((n != 2 && want_args(n, 1, "run")) || as_i64(a[0], &k)) return NULL;
+  long long k;
+  if (want_args(n, 1, "run") || as_i64(a[0], &k)) return NULL;
   if (k < 0) return PyErr_Format(PyExc_ValueError, "negative step count");
   if (!s->started) return PyErr_Format(PyExc_RuntimeError, "submitter closed");
   Py_BEGIN_ALLOW_THREADS
   s->k = k;
-  s->sync = sync != 0;
   s->t_go = mono_ns();
   atomic_store(&s->done, 0);
   atomic_store(&s->rc, 0);
@@ -376,8 +370,7 @@ static PyObject* sub_close(Submitter* s, PyObject* unused) {
 }
 
 static PyMethodDef sub_methods[] = {
-    {"run", (PyCFunction)(void (*)(void))sub_run, METH_FASTCALL,
-     "run(k[, sync]) -> rc: submit k batches over the lanes (sync: each lane then waits for its stream)"},
+    {"run", (PyCFunction)(void (*)(void))sub_run, METH_FASTCALL, "run(k) -> rc: submit k batches over the lanes"},
     {"span_ms", (PyCFunction)sub_span_ms, METH_NOARGS, "device span of the last run in ms (synchronize first)"},
     {"host_us", (PyCFunction)sub_host_us, METH_NOARGS, "the lanes' host timestamps of the last run (A/B probe)"},
     {"events_ms", (PyCFunction)sub_events_ms, METH_NOARGS, "per lane (start, end) event times vs lane 0's start"},
