@@ -652,6 +652,11 @@ def test_submitter_lanes_bit_exact(msh, oracle, lanes, k):
             assert sub.run(k) == 0
             torch.cuda.synchronize()
             assert sub.span_ms() > 0
+            ran = min(lanes, k)
+            host = sub.host_us()  # per lane: wake, start event, each launch, end event
+            assert [len(h) for h in host] == [(3 + len(range(j, k, lanes))) if j < k else 1 for j in range(lanes)]
+            ev = sub.events_ms()
+            assert len(ev) == ran and ev[0][0] == 0.0 and all(b > a for a, b in ev)
         finally:
             sub.close()
         for j, (pd, pt, t) in enumerate(cases):
