@@ -21,6 +21,13 @@
 __global__ void empty_kernel(int* p) {
   if (p && threadIdx.x == 1024) p[0] = 0;
 }
+struct Args120 {  // the size of the batch kernel's argument block (msh::BatchArgs)
+  int* p;
+  uint64_t pad[14];
+};
+__global__ void empty_kernel_120(Args120 a) {
+  if (a.p && threadIdx.x == 1024) a.p[0] = (int)a.pad[3];
+}
 
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -78,9 +85,10 @@ int main() {
     CHECK(hipMemcpy(l.pd, pd.data(), P, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(l.pt, pt.data(), P, hipMemcpyHostToDevice));
   }
-  const char* names[4] = {"empty kernel hipLaunchKernelGGL", "msh_schedule_batch_device C3",
-                          "empty kernel, C3 grid (1563 x 256)", "msh_schedule_batch_device 64 pods"};
-  for (int what = 0; what < 4; ++what) {
+  const char* names[5] = {"empty kernel hipLaunchKernelGGL", "msh_schedule_batch_device C3",
+                          "empty kernel, C3 grid (1563 x 256)", "msh_schedule_batch_device 64 pods",
+                          "empty kernel, 120-byte arguments"};
+  for (int what = 0; what < 5; ++what) {
     for (int T = 1; T <= TMAX; ++T) {
       for (int rep = 0; rep < 2; ++rep) {
         std::atomic<int> ready{0}, go{0}, bad{0};
@@ -93,6 +101,8 @@ int main() {
               hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, l.st, nullptr);
             else if (what == 2)
               hipLaunchKernelGGL(empty_kernel, dim3((P + 63) / 64), dim3(256), 0, l.st, nullptr);
+            else if (what == 4)
+              hipLaunchKernelGGL(empty_kernel_120, dim3(1), dim3(64), 0, l.st, Args120{});
             else if (msh_schedule_batch_device(l.ctx, what == 1 ? P : 64, l.pd, l.pt, l.oi, l.sc, l.os, l.st))
               bad = 1;
           };
