@@ -63,9 +63,8 @@ def bits_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sha
     sl = 1
     while sl < 16 and blocks * sl < cus * 4 * 6 and groups // (2 * sl) >= 2:
         sl *= 2
-    if not kx:  # identity-like modes: the digit-row kernel
-        return f"void msh::rows_kernel<{sl}, {str(shard).lower()}, 1>"  # 1 pod per lane (rows_ppl)
-    return f"void msh::bits_kernel<{sl}, {str(kx).lower()}, {str(shard).lower()}>"
+    # the digit-row kernel in every mode, 1 pod per lane (rows_ppl)
+    return f"void msh::rows_kernel<{sl}, {str(kx).lower()}, {str(shard).lower()}, 1>"
 
 
 def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:

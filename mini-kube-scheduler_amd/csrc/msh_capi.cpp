@@ -446,6 +446,7 @@ int msh_create(int device, msh_ctx** out_ctx) {
   if (const char* e = getenv("MSH_BITS_SLICES")) c->dev.bits_slices = atoi(e);
   if (const char* e = getenv("MSH_SEQ_WAVES")) c->dev.seq_waves = atoi(e);
   if (const char* e = getenv("MSH_ROWS_PPL")) c->dev.rows_ppl = atoi(e) == 1 ? 1 : 2;
+  if (const char* e = getenv("MSH_KX_BITS")) c->dev.kx_bits = atoi(e) == 1;
   if (const char* e = getenv("MSH_HOST_IO")) {
     c->dev.host_io_dma = strcmp(e, "dma") == 0;
     c->dev.host_io_zc_in = strcmp(e, "dma") != 0 && strcmp(e, "zc") != 0;
@@ -561,8 +562,8 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
     MSH_HIP(c, hipMalloc(&c->d_digit, cap));
     MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
     MSH_HIP(c, hipMalloc(&c->d_planes, cap / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
-    // + ER_TG groups: the batch kernel copies whole tiles without clamping (never read as rows)
-    MSH_HIP(c, hipMalloc(&c->d_erows, (cap / msh::GROUP_NODES + msh::ER_TG) * msh::ER_GD * sizeof(uint32_t)));
+    // + ER_PAD groups: the batch kernel copies whole tiles without clamping (never read as rows)
+    MSH_HIP(c, hipMalloc(&c->d_erows, (cap / msh::GROUP_NODES + msh::ER_PAD) * msh::ER_GD * sizeof(uint32_t)));
     c->node_cap = cap;
   }
   if (n > 0) {

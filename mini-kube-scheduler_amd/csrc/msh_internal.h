@@ -39,6 +39,7 @@ struct DeviceInfo {
   int bits_slices = 0;   // tests / A-B only (MSH_BITS_SLICES at msh_create): slice waves per pod block, 0 = auto
   int seq_waves = 0;     // tests / A-B only (MSH_SEQ_WAVES at msh_create): sequential scanning waves, 0 = auto
   int rows_ppl = 1;      // pods per lane of the digit-row kernel (1 or 2; MSH_ROWS_PPL at msh_create, A/B)
+  int kx_bits = 0;       // A/B only (MSH_KX_BITS=1 at msh_create): REVERSE / MINMAX on the code-plane kernel
   // Host-buffer calls (msh_schedule_batch / _sequential): the kernel reads the pod columns from and
   // writes the outputs to page-locked host memory (default). A/B only, MSH_HOST_IO at msh_create:
   // "dma" = columns and outputs DMA'd through device scratch, "zc" = columns DMA'd, outputs zero-copy.
@@ -75,17 +76,19 @@ constexpr int32_t NODE_PAD = 1024;  // tables are padded to whole 1,024-node pre
 // kernel): for every word, ER_ROWS row words, row r = the word's real nodes whose suffix digit is
 // r (r = 0..9); row 10 stays zero (the row of pods without a digit suffix). Per group, two chunks
 // of 4 consecutive words, each chunk row-major with a row's 4 words contiguous, then the group's 8
-// X words (the PLANE_X plane again, so that one copy brings a group's whole input):
+// X words and its 8 V words (the PLANE_X / PLANE_V planes again, so that one copy brings a group's
+// whole input):
 //   erows[g * ER_GD + (c * ER_ROWS + r) * 4 + k] = row r of word g * PLANE_GW + 4 c + k
 //   erows[g * ER_GD + ER_Q * 4 + j]              = X of word g * PLANE_GW + j
+//   erows[g * ER_GD + ER_Q * 4 + 8 + j]          = V of word g * PLANE_GW + j
 // so a pod's row words of one chunk are one 16-byte read, and the 11 rows of a chunk (44 dwords)
-// sit in distinct LDS banks. 1.5 B per node.
+// sit in distinct LDS banks. 1.625 B per node.
 constexpr int ER_ROWS = 11;
 constexpr int ER_Q = 2 * ER_ROWS;      // 16-byte row chunks per group
-constexpr int ER_GQ = ER_Q + 2;        // 16-byte chunks per group: the rows, then X
+constexpr int ER_GQ = ER_Q + 4;        // 16-byte chunks per group: the rows, then X, then V
 constexpr int ER_GD = ER_GQ * 4;       // dwords per group
-constexpr int ER_TG = 8;               // groups per LDS tile of the batch kernel (3,072 B per wave);
-                                       // the table is allocated with ER_TG groups of padding
+constexpr int ER_TG = 8;               // groups per LDS tile of the batch kernel (3,328 B per wave)
+constexpr int ER_PAD = 2 * ER_TG;      // groups of padding: whole-tile copies need no clamp
 
 // ---- launchers (msh_kernels.hip) ----
 // Applies `patch_count` pending msh_patch_nodes entries (idx | unsched << 32 | (uint8)digit << 40)

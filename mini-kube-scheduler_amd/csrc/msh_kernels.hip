@@ -89,10 +89,11 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
     const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
     const uint32_t g = word / PLANE_GW, c = (word / 4) & 1u, k = word & 3u;
     erows[(size_t)g * ER_GD + (c * ER_ROWS + (uint32_t)r) * 4 + k] = (uint32_t)(m >> (32 * half));
-  } else if (lane < 2 * ER_ROWS + 2) {  // lanes 22, 23: the X words behind the rows
-    const int half = lane & 1;
+  } else if (lane < 2 * ER_ROWS + 4) {  // lanes 22..25: the X, then the V words behind the rows
+    const int half = lane & 1, v = (lane - 2 * ER_ROWS) >> 1;
     const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
-    erows[(size_t)(word / PLANE_GW) * ER_GD + ER_Q * 4 + word % PLANE_GW] = (uint32_t)(pm[PLANE_X] >> (32 * half));
+    erows[(size_t)(word / PLANE_GW) * ER_GD + (ER_Q + 2 * v) * 4 + word % PLANE_GW] =
+        (uint32_t)(pm[v ? PLANE_V : PLANE_X] >> (32 * half));
   }
   const unsigned long long m0 = pm[PLANE_V] & ~pm[PLANE_X], m1 = pm[PLANE_V];
   if (lane == 0) {
@@ -506,7 +507,32 @@ __device__ unsigned long long* g_stamps;
 #define MSH_STAMP(i) ((void)0)
 #endif
 
-template <int S, bool SHARD, int PPL>
+// One group's feasible non-matches (KX modes): nm = V & ~E & ~(X & nT), two VALU per word
+// (xm = X & nT, then one v_bitop3 with truth table 0x10 = S0 & ~S1 & ~S2).
+__device__ __forceinline__ uint32_t nonmatch_v(uint32_t v, uint32_t e, uint32_t xm) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x10" : "=v"(r) : "v"(v), "v"(e), "v"(xm));
+  return r;
+}
+__device__ __forceinline__ bool rows_nonmatch(const uint4& e0, const uint4& e1, const uint4& x0, const uint4& x1,
+                                              const uint4& v0, const uint4& v1, uint32_t nT,
+                                              uint32_t (&n)[PLANE_GW]) {
+  const uint32_t e[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+  const uint32_t x[PLANE_GW] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  const uint32_t v[PLANE_GW] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+  for (int k = 0; k < PLANE_GW; ++k) n[k] = nonmatch_v(v[k], e[k], x[k] & nT);
+  return ((n[0] | n[1] | n[2]) | (n[3] | n[4] | n[5]) | (n[6] | n[7])) != 0u;
+}
+// The lane's first feasible non-match in group g, from memory (rare path of the KX modes).
+__device__ __forceinline__ uint32_t rows_group_first_nm(const BatchArgs& a, uint32_t g, uint32_t row, uint32_t nT) {
+  const uint4* er = reinterpret_cast<const uint4*>(a.erows) + (size_t)g * ER_GQ;
+  uint32_t n[PLANE_GW];
+  rows_nonmatch(er[row], er[ER_ROWS + row], er[ER_Q], er[ER_Q + 1], er[ER_Q + 2], er[ER_Q + 3], nT, n);
+  return hits_first(n, g);
+}
+
+template <int S, bool KX, bool SHARD, int PPL>
 __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
 #ifdef MSH_STAMPS
   unsigned long long stamp_t[4] = {0, 0, 0, 0};
@@ -516,8 +542,9 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
       for (int i = 0; i < 4; ++i) g_stamps[((size_t)blockIdx.x * S + (threadIdx.x >> 6)) * 4 + i] = stamp_t[i];
   };
 #endif
+  constexpr int NR = KX ? 2 : 1;  // results per pod: first feasible match (+ first feasible non-match)
   __shared__ uint4 s_tile[S][ER_TG * ER_GQ];
-  __shared__ uint32_t s_res[S][PPL][WAVE];
+  __shared__ uint32_t s_res[S][NR][PPL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   // PPL pods per lane: lane l holds pods base + q * 64 + l (q < PPL); the group's X words and the
@@ -528,22 +555,25 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
   const int32_t ng = g_hi - g_lo;
   const uint4* __restrict__ er = reinterpret_cast<const uint4*>(a.erows);
   uint4* tile = s_tile[s];
-  // This wave's tile, read only by this wave: a whole ER_TG-group tile is copied, three 16-byte
-  // copies per lane (the table carries ER_TG groups of padding, so no copy needs a clamp; rows past
-  // the slice are never read). Loads and stores are separate so that the prologue can put the
-  // pod-byte loads between them.
-  static_assert(ER_TG * ER_GQ == 3 * WAVE, "fill: three 16-byte copies per lane");
-  uint4 f0, f1, f2;
+  // This wave's tile, read only by this wave: a whole ER_TG-group tile is copied, four 16-byte
+  // copies per lane (the table carries padding, so no copy needs a clamp; rows past the slice are
+  // never read). Loads and stores are separate so that the prologue can put the pod-byte loads
+  // between them.
+  constexpr int TQ = ER_TG * ER_GQ;
+  static_assert(TQ > 3 * WAVE && TQ <= 4 * WAVE, "fill: four 16-byte copies per lane");
+  uint4 f0, f1, f2, f3;
   auto fill_load = [&](int32_t t_lo) {
     const uint4* src = er + (uint32_t)(t_lo * ER_GQ);  // wave-uniform base, 32-bit lane offsets
     f0 = src[(uint32_t)lane];
     f1 = src[(uint32_t)(lane + WAVE)];
     f2 = src[(uint32_t)(lane + 2 * WAVE)];
+    f3 = src[(uint32_t)(lane + 3 * WAVE)];
   };
   auto fill_store = [&]() {
     tile[lane] = f0;
     tile[lane + WAVE] = f1;
     tile[lane + 2 * WAVE] = f2;
+    if (lane + 3 * WAVE < TQ) tile[lane + 3 * WAVE] = f3;
     __builtin_amdgcn_wave_barrier();
   };
   // Prologue: the top tile's row words, the pod bytes (clamped offset: no branch, so nothing waits
@@ -564,7 +594,7 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
   const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
   fill_store();
   bool act[PPL];
-  uint32_t code[PPL], tol[PPL], nT[PPL];
+  uint32_t code[PPL], tol[PPL], nT[PPL], row[PPL];
   const uint4* lrow[PPL];  // the lane's row in chunk 0 of a tile's first group
 #pragma unroll
   for (int q = 0; q < PPL; ++q) {
@@ -572,13 +602,24 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
     code[q] = (act[q] && dq[q] >= 0 && dq[q] <= 9) ? (uint32_t)dq[q] : CODE_NONE_POD;
     tol[q] = (act[q] && tq[q]) ? 1u : 0u;
     nT[q] = tol[q] ? 0u : 0xFFFFFFFFu;
-    lrow[q] = tile + (code[q] <= 9u ? code[q] : (uint32_t)(ER_ROWS - 1));  // no digit: the zero row
+    row[q] = code[q] <= 9u ? code[q] : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
+    lrow[q] = tile + row[q];
   }
   MSH_STAMP(1);
-  uint32_t h[PPL][PLANE_GW];
-  uint32_t fm[PPL];  // first group above the lowest with a feasible match (NO_GROUP - 1: in h)
+  uint32_t h[PPL][PLANE_GW], hn[PPL][PLANE_GW];
+  // first group above the lowest with a feasible match / non-match (NO_GROUP - 1: in h / hn)
+  uint32_t fm[PPL], fx[PPL];
 #pragma unroll
-  for (int q = 0; q < PPL; ++q) fm[q] = NO_GROUP;
+  for (int q = 0; q < PPL; ++q) fm[q] = fx[q] = NO_GROUP;
+  // One group g of the tile for pod q: hits into hq (and non-matches into nq); returns the flags.
+  auto group = [&](int32_t g, int32_t t_lo, int q, uint32_t (&hq)[PLANE_GW], uint32_t (&nq)[PLANE_GW], bool& am,
+                   bool& ax) {
+    const uint4* tg = tile + (g - t_lo) * ER_GQ;
+    const uint4* r0 = lrow[q] + (g - t_lo) * ER_GQ;
+    const uint4 e0 = r0[0], e1 = r0[ER_ROWS], x0 = tg[ER_Q], x1 = tg[ER_Q + 1];
+    am = rows_hits(e0, e1, x0, x1, nT[q], hq);
+    if constexpr (KX) ax = rows_nonmatch(e0, e1, x0, x1, tg[ER_Q + 2], tg[ER_Q + 3], nT[q], nq);
+  };
   // Tiles from the top down, each one's groups descending; the lowest group of the slice last.
   for (int32_t t = t_top; t >= 0; --t) {
     const int32_t t_lo = g_lo + t * ER_TG, t_hi = min(t_lo + ER_TG, g_hi);
@@ -588,57 +629,60 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
     }
     const int32_t g_end = t == 0 ? g_lo + 1 : t_lo;  // tile 0: all but the lowest group
     int32_t g = t_hi - 1;
-    for (; g - 1 >= g_end; g -= 2) {  // two groups per step: all their LDS reads before the first use
-      const uint4* tg0 = tile + (g - t_lo) * ER_GQ;
-      const uint4 x00 = tg0[ER_Q], x01 = tg0[ER_Q + 1], x10 = tg0[ER_Q - ER_GQ], x11 = tg0[ER_Q + 1 - ER_GQ];
-      uint4 e[PPL][4];
+    for (; g - 1 >= g_end; g -= 2) {  // two groups per step
 #pragma unroll
       for (int q = 0; q < PPL; ++q) {
-        const uint4* r0 = lrow[q] + (g - t_lo) * ER_GQ;
-        e[q][0] = r0[0];
-        e[q][1] = r0[ER_ROWS];
-        e[q][2] = r0[-ER_GQ];
-        e[q][3] = r0[ER_ROWS - ER_GQ];
-      }
-#pragma unroll
-      for (int q = 0; q < PPL; ++q) {
-        uint32_t h1[PLANE_GW], h2[PLANE_GW];  // (only the lowest group's words are kept, in h)
-        const bool a0 = rows_hits(e[q][0], e[q][1], x00, x01, nT[q], h1);
-        const bool a1 = rows_hits(e[q][2], e[q][3], x10, x11, nT[q], h2);
-        fm[q] = a0 ? (uint32_t)g : fm[q];
-        fm[q] = a1 ? (uint32_t)(g - 1) : fm[q];
+        uint32_t h1[PLANE_GW], h2[PLANE_GW], n1[PLANE_GW], n2[PLANE_GW];  // (only the lowest group's are kept)
+        bool m1, m2, x1 = false, x2 = false;
+        group(g, t_lo, q, h1, n1, m1, x1);
+        group(g - 1, t_lo, q, h2, n2, m2, x2);
+        fm[q] = m1 ? (uint32_t)g : fm[q];
+        fm[q] = m2 ? (uint32_t)(g - 1) : fm[q];
+        if constexpr (KX) {
+          fx[q] = x1 ? (uint32_t)g : fx[q];
+          fx[q] = x2 ? (uint32_t)(g - 1) : fx[q];
+        }
       }
     }
     if (g >= g_end) {
-      const uint4* tg0 = tile + (g - t_lo) * ER_GQ;
-      const uint4 x00 = tg0[ER_Q], x01 = tg0[ER_Q + 1];
 #pragma unroll
       for (int q = 0; q < PPL; ++q) {
-        const uint4* r0 = lrow[q] + (g - t_lo) * ER_GQ;
-        uint32_t h1[PLANE_GW];
-        fm[q] = rows_hits(r0[0], r0[ER_ROWS], x00, x01, nT[q], h1) ? (uint32_t)g : fm[q];
+        uint32_t h1[PLANE_GW], n1[PLANE_GW];
+        bool m1, x1 = false;
+        group(g, t_lo, q, h1, n1, m1, x1);
+        fm[q] = m1 ? (uint32_t)g : fm[q];
+        if constexpr (KX) fx[q] = x1 ? (uint32_t)g : fx[q];
       }
     }
-    if (t == 0) {  // the lowest group: its hit words stay in registers for the exact node
-      const uint4 x00 = tile[ER_Q], x01 = tile[ER_Q + 1];
+    if (t == 0) {  // the lowest group: its hit (and non-match) words stay in registers
 #pragma unroll
-      for (int q = 0; q < PPL; ++q)
-        fm[q] = rows_hits(lrow[q][0], lrow[q][ER_ROWS], x00, x01, nT[q], h[q]) ? NO_GROUP - 1 : fm[q];
+      for (int q = 0; q < PPL; ++q) {
+        bool m1, x1 = false;
+        group(g_lo, t_lo, q, h[q], hn[q], m1, x1);
+        fm[q] = m1 ? NO_GROUP - 1 : fm[q];
+        if constexpr (KX) fx[q] = x1 ? NO_GROUP - 1 : fx[q];
+      }
     }
     __builtin_amdgcn_wave_barrier();
   }
-  uint32_t rm[PPL];  // node index of the first feasible match
+  uint32_t rm[PPL], rx[PPL];  // node index of the first feasible match / non-match
   MSH_STAMP(2);
 #pragma unroll
   for (int q = 0; q < PPL; ++q) {
-    rm[q] = NOFIT;
+    rm[q] = rx[q] = NOFIT;
     if (fm[q] == NO_GROUP - 1) rm[q] = hits_first(h[q], (uint32_t)g_lo);
-    else if (fm[q] != NO_GROUP)
-      rm[q] = rows_group_first(a, fm[q], code[q] <= 9u ? code[q] : (uint32_t)(ER_ROWS - 1), nT[q]);
+    else if (fm[q] != NO_GROUP) rm[q] = rows_group_first(a, fm[q], row[q], nT[q]);
+    if constexpr (KX) {
+      if (fx[q] == NO_GROUP - 1) rx[q] = hits_first(hn[q], (uint32_t)g_lo);
+      else if (fx[q] != NO_GROUP) rx[q] = rows_group_first_nm(a, fx[q], row[q], nT[q]);
+    }
   }
   if constexpr (S > 1) {
 #pragma unroll
-    for (int q = 0; q < PPL; ++q) s_res[s][q][lane] = rm[q];
+    for (int q = 0; q < PPL; ++q) {
+      s_res[s][0][q][lane] = rm[q];
+      if constexpr (KX) s_res[s][NR - 1][q][lane] = rx[q];
+    }
     __syncthreads();
 #ifdef MSH_STAMPS
     if (s != 0) {
@@ -651,9 +695,12 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
 #pragma unroll
     for (int k = 1; k < S; ++k)
 #pragma unroll
-      for (int q = 0; q < PPL; ++q) rm[q] = umin(rm[q], s_res[k][q][lane]);
+      for (int q = 0; q < PPL; ++q) {
+        rm[q] = umin(rm[q], s_res[k][0][q][lane]);
+        if constexpr (KX) rx[q] = umin(rx[q], s_res[k][NR - 1][q][lane]);
+      }
   }
-  if (SHARD) write_class_keys(a);
+  if (SHARD && !KX) write_class_keys(a);
 #ifdef MSH_STAMPS
   MSH_STAMP(3);
   stamps_out();
@@ -664,11 +711,15 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
     const int32_t j = base + q * WAVE;
     if constexpr (SHARD) {
       a.keys[j] = rm[q] != NOFIT ? shard_key(a.node_base, rm[q]) : 0;
+      if constexpr (KX) a.keys[(size_t)a.n_pods + j] = rx[q] != NOFIT ? shard_key(a.node_base, rx[q]) : 0;
     } else {
       int32_t oi, ost;
       int64_t osc;
-      decode_ident(rm[q] != NOFIT ? (int64_t)rm[q] : -1, key_to_idx(tol[q] ? ball1 : ball0),
-                   code[q] != CODE_NONE_POD, make_ident_decode(a.pp), &oi, &osc, &ost);
+      const int64_t im = rm[q] != NOFIT ? (int64_t)rm[q] : -1, ia = key_to_idx(tol[q] ? ball1 : ball0);
+      if constexpr (KX)
+        decode_pod(im, rx[q] != NOFIT ? (int64_t)rx[q] : -1, ia, code[q] != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
+      else
+        decode_ident(im, ia, code[q] != CODE_NONE_POD, make_ident_decode(a.pp), &oi, &osc, &ost);
       a.out_idx[j] = oi;
       if (a.out_score) a.out_score[j] = osc;  // optional output (NULL: not written)
       a.out_status[j] = ost;
@@ -1208,30 +1259,30 @@ hipError_t launch_bits_s(const BatchArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int S, bool SHARD, int PPL>
+template <int S, bool KX, bool SHARD, int PPL>
 hipError_t launch_rows_s(const BatchArgs& a, hipStream_t s) {
   BatchArgs ka = a;
   ka.gps = (a.n_groups + S - 1) / S;
   const int64_t blocks = ((int64_t)a.n_pods + PPL * WAVE - 1) / (PPL * WAVE);
-  hipLaunchKernelGGL((rows_kernel<S, SHARD, PPL>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  hipLaunchKernelGGL((rows_kernel<S, KX, SHARD, PPL>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
   return hipGetLastError();
 }
 
-template <bool SHARD, int PPL>
+template <bool KX, bool SHARD, int PPL>
 hipError_t launch_rows_p(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
   // slices for the launch's pod blocks of PPL * 64 pods
   switch (bits_slices((a.n_pods + PPL - 1) / PPL, a.n_groups, dev)) {
-    case 1: return launch_rows_s<1, SHARD, PPL>(a, s);
-    case 2: return launch_rows_s<2, SHARD, PPL>(a, s);
-    case 4: return launch_rows_s<4, SHARD, PPL>(a, s);
-    case 8: return launch_rows_s<8, SHARD, PPL>(a, s);
-    default: return launch_rows_s<16, SHARD, PPL>(a, s);
+    case 1: return launch_rows_s<1, KX, SHARD, PPL>(a, s);
+    case 2: return launch_rows_s<2, KX, SHARD, PPL>(a, s);
+    case 4: return launch_rows_s<4, KX, SHARD, PPL>(a, s);
+    case 8: return launch_rows_s<8, KX, SHARD, PPL>(a, s);
+    default: return launch_rows_s<16, KX, SHARD, PPL>(a, s);
   }
 }
 
-template <bool SHARD>
+template <bool KX, bool SHARD>
 hipError_t launch_rows_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
-  return dev.rows_ppl == 1 ? launch_rows_p<SHARD, 1>(a, dev, s) : launch_rows_p<SHARD, 2>(a, dev, s);
+  return dev.rows_ppl == 1 ? launch_rows_p<KX, SHARD, 1>(a, dev, s) : launch_rows_p<KX, SHARD, 2>(a, dev, s);
 }
 
 template <bool KX, bool SHARD>
@@ -1249,10 +1300,11 @@ hipError_t launch_bits_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t 
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s) {
   if (a.n_pods == 0) return hipSuccess;
   const bool kx = needs_kx(a.pp);
-  // identity-like modes on the digit rows; REVERSE / MINMAX (first feasible non-match too) on the
-  // code planes
-  if (shard) return kx ? launch_bits_t<true, true>(a, dev, s) : launch_rows_t<true>(a, dev, s);
-  return kx ? launch_bits_t<true, false>(a, dev, s) : launch_rows_t<false>(a, dev, s);
+  // every mode on the digit rows (REVERSE / MINMAX also track the first feasible non-match)
+  if (kx && dev.kx_bits)  // A/B: the code-plane kernel for REVERSE / MINMAX
+    return shard ? launch_bits_t<true, true>(a, dev, s) : launch_bits_t<true, false>(a, dev, s);
+  if (shard) return kx ? launch_rows_t<true, true>(a, dev, s) : launch_rows_t<false, true>(a, dev, s);
+  return kx ? launch_rows_t<true, false>(a, dev, s) : launch_rows_t<false, false>(a, dev, s);
 }
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,

@@ -1,5 +1,5 @@
 """Summarise scripts/profile_r2.sh (gpurun_out/prof_r2) into profiles/r2_pmc_c3.json: per-launch
-counters of the hot kernels at C3 (rows_kernel; bits_kernel for MIN-MAX) and C5 (seq_kernel), with the derived figures
+counters of the hot kernels at C3 (rows_kernel, identity and MIN-MAX) and C5 (seq_kernel), with the derived figures
 bench.py's roofline quotes. FETCH_SIZE / WRITE_SIZE are KiB (x 1024); WRITE_SIZE reads exact bytes
 for coalesced stores (MI355X_MICROARCH.md, HBM section); FETCH_SIZE is reported raw and with the
 guide's x2 correction for wide streaming reads (an upper bound here: the pod bytes are read 64 B
@@ -29,7 +29,7 @@ def counters(tag, prefix):
 
 res = {"source": str(src), "nodes": N, "pods": P, "kernels": {}}
 for mode, prefix, tags in (("batch", "void msh::rows_kernel", ("b_sq", "b_sq2", "b_lds", "b_grbm", "b_fetch", "b_write")),
-                           ("batch_minmax", "void msh::bits_kernel", ("k_sq",)),
+                           ("batch_minmax", "void msh::rows_kernel", ("k_sq",)),
                            ("sequential", "void msh::seq_kernel", ("s_sq", "s_fetch", "s_write"))):
     e = {"nodes": N, "pods": P, "launches_per_counter": {}}
     for t in tags:
@@ -45,9 +45,9 @@ for mode, prefix, tags in (("batch", "void msh::rows_kernel", ("b_sq", "b_sq2", 
         e["hbm_bytes_per_launch_fetch_x2"] = 2 * e["fetch_bytes_raw"] + e["write_bytes"]
     if "SQ_INSTS_VALU" in e:
         e["valu_lane_ops_per_eval"] = e["SQ_INSTS_VALU"] * 64 / (N * P)
-        # the scan's modelled VALU per 8-word group: rows_kernel 8 v_bitop3 + 4 ORs + compare +
-        # select (14), bits_kernel KX 68
-        per_group = {"batch": 14, "batch_minmax": 68}.get(mode)
+        # the scan's modelled VALU per 8-word group and wave: rows_kernel 8 v_bitop3 + 4 ORs +
+        # compare + select + move (15); with the non-match too (MIN-MAX) 38
+        per_group = {"batch": 15, "batch_minmax": 38}.get(mode)
         if per_group:
             e["scan_model_share"] = (per_group / 8) * (P / 64) * (N / 32) / e["SQ_INSTS_VALU"]
     if "SQ_WAVE_CYCLES" in e:

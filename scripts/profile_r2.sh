@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 profile of the hot kernels (rows_kernel at C3, bits_kernel for MIN-MAX, seq_kernel at C5),
+# Round-2 profile of the hot kernels (rows_kernel at C3, also with MIN-MAX, seq_kernel at C5),
 # run on the GPU box:
 #  1. the scan-mix issue-rate microbenchmark (the VALU ceiling bench.py quotes);
 #  2. rocprofv3 --kernel-trace --stats over the headline bench.py command;

@@ -539,8 +539,8 @@ def test_maximum_node_table(msh, gpu_ctx, synth):
 
 @pytest.mark.parametrize("slices", ["1", "2", "4", "8", "16"])
 @pytest.mark.parametrize("n", [20_000, 70_000])
-@pytest.mark.parametrize("ppl", ["1", "2"])
-def test_bits_slices(msh, oracle, n, slices, ppl, monkeypatch):
+@pytest.mark.parametrize("ppl,kx_bits", [("1", "0"), ("2", "0"), ("1", "1")])
+def test_bits_slices(msh, oracle, n, slices, ppl, kx_bits, monkeypatch):
     """Few pods against a large table: SLICES waves share each 64-pod block, each scanning a range
     of 256-node groups, firsts merged by min in LDS. Every slice count (MSH_BITS_SLICES, read once
     by msh_create) against the oracle, for the batch and the shard-key entry points, in the
@@ -548,6 +548,7 @@ def test_bits_slices(msh, oracle, n, slices, ppl, monkeypatch):
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("MSH_BITS_SLICES", slices)
     monkeypatch.setenv("MSH_ROWS_PPL", ppl)  # pods per lane of the digit-row kernel
+    monkeypatch.setenv("MSH_KX_BITS", kx_bits)  # MINMAX on the code-plane kernel (A/B) or the rows
     rng = np.random.default_rng(n + int(slices))
     u, nd, pd, pt = _rand_case(rng, n, 1500 + int(ppl) * 37, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4  # digit 3 only in the second half: late first matches
