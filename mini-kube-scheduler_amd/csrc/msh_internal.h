@@ -76,18 +76,17 @@ constexpr int32_t NODE_PAD = 1024;  // tables are padded to whole 1,024-node pre
 // kernel): for every word, ER_ROWS row words, row r = the word's real nodes whose suffix digit is
 // r (r = 0..9); row 10 stays zero (the row of pods without a digit suffix). Per group, two chunks
 // of 4 consecutive words, each chunk row-major with a row's 4 words contiguous, then the group's 8
-// X words and its 8 V words (the PLANE_X / PLANE_V planes again, so that one copy brings a group's
-// whole input):
+// X words (the PLANE_X plane again, so that one copy brings a group's whole input):
 //   erows[g * ER_GD + (c * ER_ROWS + r) * 4 + k] = row r of word g * PLANE_GW + 4 c + k
 //   erows[g * ER_GD + ER_Q * 4 + j]              = X of word g * PLANE_GW + j
-//   erows[g * ER_GD + ER_Q * 4 + 8 + j]          = V of word g * PLANE_GW + j
 // so a pod's row words of one chunk are one 16-byte read, and the 11 rows of a chunk (44 dwords)
-// sit in distinct LDS banks. 1.625 B per node.
+// sit in distinct LDS banks. 1.5 B per node. (The REVERSE / MINMAX modes also read the V plane,
+// from the code planes.)
 constexpr int ER_ROWS = 11;
 constexpr int ER_Q = 2 * ER_ROWS;      // 16-byte row chunks per group
-constexpr int ER_GQ = ER_Q + 4;        // 16-byte chunks per group: the rows, then X, then V
+constexpr int ER_GQ = ER_Q + 2;        // 16-byte chunks per group: the rows, then X
 constexpr int ER_GD = ER_GQ * 4;       // dwords per group
-constexpr int ER_TG = 8;               // groups per LDS tile of the batch kernel (3,328 B per wave)
+constexpr int ER_TG = 8;               // groups per LDS tile of the batch kernel (3,072 B per wave)
 constexpr int ER_PAD = 2 * ER_TG;      // groups of padding: whole-tile copies need no clamp
 
 // ---- launchers (msh_kernels.hip) ----

@@ -89,11 +89,10 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
     const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
     const uint32_t g = word / PLANE_GW, c = (word / 4) & 1u, k = word & 3u;
     erows[(size_t)g * ER_GD + (c * ER_ROWS + (uint32_t)r) * 4 + k] = (uint32_t)(m >> (32 * half));
-  } else if (lane < 2 * ER_ROWS + 4) {  // lanes 22..25: the X, then the V words behind the rows
-    const int half = lane & 1, v = (lane - 2 * ER_ROWS) >> 1;
+  } else if (lane < 2 * ER_ROWS + 2) {  // lanes 22, 23: the X words behind the rows
+    const int half = lane & 1;
     const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
-    erows[(size_t)(word / PLANE_GW) * ER_GD + (ER_Q + 2 * v) * 4 + word % PLANE_GW] =
-        (uint32_t)(pm[v ? PLANE_V : PLANE_X] >> (32 * half));
+    erows[(size_t)(word / PLANE_GW) * ER_GD + ER_Q * 4 + word % PLANE_GW] = (uint32_t)(pm[PLANE_X] >> (32 * half));
   }
   const unsigned long long m0 = pm[PLANE_V] & ~pm[PLANE_X], m1 = pm[PLANE_V];
   if (lane == 0) {
@@ -524,11 +523,13 @@ __device__ __forceinline__ bool rows_nonmatch(const uint4& e0, const uint4& e1, 
   for (int k = 0; k < PLANE_GW; ++k) n[k] = nonmatch_v(v[k], e[k], x[k] & nT);
   return ((n[0] | n[1] | n[2]) | (n[3] | n[4] | n[5]) | (n[6] | n[7])) != 0u;
 }
-// The lane's first feasible non-match in group g, from memory (rare path of the KX modes).
+// The lane's first feasible non-match in group g, from memory (rare path of the KX modes): the
+// rows and X from the digit rows, V from the code planes.
 __device__ __forceinline__ uint32_t rows_group_first_nm(const BatchArgs& a, uint32_t g, uint32_t row, uint32_t nT) {
   const uint4* er = reinterpret_cast<const uint4*>(a.erows) + (size_t)g * ER_GQ;
+  const uint4* vp = reinterpret_cast<const uint4*>(a.planes + (size_t)g * GROUP_DWORDS + PLANE_V * PLANE_GW);
   uint32_t n[PLANE_GW];
-  rows_nonmatch(er[row], er[ER_ROWS + row], er[ER_Q], er[ER_Q + 1], er[ER_Q + 2], er[ER_Q + 3], nT, n);
+  rows_nonmatch(er[row], er[ER_ROWS + row], er[ER_Q], er[ER_Q + 1], vp[0], vp[1], nT, n);
   return hits_first(n, g);
 }
 
@@ -544,6 +545,7 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
 #endif
   constexpr int NR = KX ? 2 : 1;  // results per pod: first feasible match (+ first feasible non-match)
   __shared__ uint4 s_tile[S][ER_TG * ER_GQ];
+  __shared__ uint4 s_vw[KX ? S : 1][KX ? 2 * ER_TG : 1];  // KX: the tile's V words (from the code planes)
   __shared__ uint32_t s_res[S][NR][PPL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -555,25 +557,29 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
   const int32_t ng = g_hi - g_lo;
   const uint4* __restrict__ er = reinterpret_cast<const uint4*>(a.erows);
   uint4* tile = s_tile[s];
-  // This wave's tile, read only by this wave: a whole ER_TG-group tile is copied, four 16-byte
+  // This wave's tile, read only by this wave: a whole ER_TG-group tile is copied, three 16-byte
   // copies per lane (the table carries padding, so no copy needs a clamp; rows past the slice are
-  // never read). Loads and stores are separate so that the prologue can put the pod-byte loads
-  // between them.
-  constexpr int TQ = ER_TG * ER_GQ;
-  static_assert(TQ > 3 * WAVE && TQ <= 4 * WAVE, "fill: four 16-byte copies per lane");
-  uint4 f0, f1, f2, f3;
+  // never read), and in the KX modes the tile's V words from the code planes (16 lanes, one group
+  // half each, clamped to the table). Loads and stores are separate so that the prologue can put
+  // the pod-byte loads between them.
+  static_assert(ER_TG * ER_GQ == 3 * WAVE, "fill: three 16-byte copies per lane");
+  uint4 f0, f1, f2, fv;
+  uint4* vtile = s_vw[KX ? s : 0];
   auto fill_load = [&](int32_t t_lo) {
     const uint4* src = er + (uint32_t)(t_lo * ER_GQ);  // wave-uniform base, 32-bit lane offsets
     f0 = src[(uint32_t)lane];
     f1 = src[(uint32_t)(lane + WAVE)];
     f2 = src[(uint32_t)(lane + 2 * WAVE)];
-    f3 = src[(uint32_t)(lane + 3 * WAVE)];
+    if constexpr (KX) {
+      const int32_t gv = min(t_lo + (lane >> 1) % ER_TG, a.n_groups - 1);
+      fv = reinterpret_cast<const uint4*>(a.planes + (size_t)gv * GROUP_DWORDS + PLANE_V * PLANE_GW)[lane & 1];
+    }
   };
   auto fill_store = [&]() {
     tile[lane] = f0;
     tile[lane + WAVE] = f1;
     tile[lane + 2 * WAVE] = f2;
-    if (lane + 3 * WAVE < TQ) tile[lane + 3 * WAVE] = f3;
+    if (KX && lane < 2 * ER_TG) vtile[lane] = fv;
     __builtin_amdgcn_wave_barrier();
   };
   // Prologue: the top tile's row words, the pod bytes (clamped offset: no branch, so nothing waits
@@ -618,7 +624,10 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
     const uint4* r0 = lrow[q] + (g - t_lo) * ER_GQ;
     const uint4 e0 = r0[0], e1 = r0[ER_ROWS], x0 = tg[ER_Q], x1 = tg[ER_Q + 1];
     am = rows_hits(e0, e1, x0, x1, nT[q], hq);
-    if constexpr (KX) ax = rows_nonmatch(e0, e1, x0, x1, tg[ER_Q + 2], tg[ER_Q + 3], nT[q], nq);
+    if constexpr (KX) {
+      const uint4* vg = vtile + 2 * (g - t_lo);
+      ax = rows_nonmatch(e0, e1, x0, x1, vg[0], vg[1], nT[q], nq);
+    }
   };
   // Tiles from the top down, each one's groups descending; the lowest group of the slice last.
   for (int32_t t = t_top; t >= 0; --t) {
@@ -1282,7 +1291,10 @@ hipError_t launch_rows_p(const BatchArgs& a, const DeviceInfo& dev, hipStream_t 
 
 template <bool KX, bool SHARD>
 hipError_t launch_rows_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
-  return dev.rows_ppl == 1 ? launch_rows_p<KX, SHARD, 1>(a, dev, s) : launch_rows_p<KX, SHARD, 2>(a, dev, s);
+  if constexpr (KX)  // (two pods per lane, an A/B of the identity modes, would spill here)
+    return launch_rows_p<KX, SHARD, 1>(a, dev, s);
+  else
+    return dev.rows_ppl == 1 ? launch_rows_p<KX, SHARD, 1>(a, dev, s) : launch_rows_p<KX, SHARD, 2>(a, dev, s);
 }
 
 template <bool KX, bool SHARD>
