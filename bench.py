@@ -55,7 +55,7 @@ ROWS_VALU_PER_GROUP = 15
 PMC_FILE = ROOT / "profiles" / "r2_pmc_c3.json"
 
 
-def bits_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False) -> str:
+def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False) -> str:
     """The kernel msh_kernels.hip launch_batch dispatches (bits_slices' choice of S)."""
     n_pad = max(-(-n_nodes // 1024) * 1024, 1024)
     groups = n_pad // 256
@@ -482,7 +482,7 @@ def make_roofline(mode, n_local, p, kernel_ms, kernel_ms_isolated, nstreams, cus
                 "instructions_per_pod": instr,
                 "note": "peak = instructions per pod (rocprofv3 SQ_INSTS_VALU + SQ_INSTS_SALU / pods, "
                         "profiles/r2_pmc_c3.json) x 4 cycles / 2.4 GHz; frac = that floor / measured us per pod"}
-    kname = bits_kernel_label(n_local, p, cus, shard=mode == "nodeshard")
+    kname = batch_kernel_label(n_local, p, cus, shard=mode == "nodeshard")
     evals = float(n_local) * p
     entry = pmc.get("kernels", {}).get("batch", {})
     pmc_ok = entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
@@ -582,7 +582,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                         [msh.ScorePluginConfig(msh.NODE_NUMBER, weight, msh.Normalize(norm))])
         ms, ok = batch_rate(ctx, n, pairs, 100, norm, weight)
-        variants[name] = {"kernel": bits_kernel_label(n, p, cus, kx=norm in (2, 3)), "ms_per_step": ms,
+        variants[name] = {"kernel": batch_kernel_label(n, p, cus, kx=norm in (2, 3)), "ms_per_step": ms,
                           "evals_per_s": n * p / (ms * 1e-3), "streams": 2,
                           "check": "bit-exact vs closed form" if ok else "MISMATCH"}
     out["c3_normalize_variants"] = variants
@@ -678,7 +678,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     ctx_nodes[ctx] = (u2, nd2)
     ms, ok = batch_rate(ctx, n2, [(np.ascontiguousarray(pd2[:p2]), np.ascontiguousarray(pt2[:p2])),
                                   (np.ascontiguousarray(pd2[p2:]), np.ascontiguousarray(pt2[p2:]))], 100)
-    out["c2"] = {"kernel": bits_kernel_label(n2, p2, cus), "ms_per_step": ms, "evals_per_s": n2 * p2 / (ms * 1e-3),
+    out["c2"] = {"kernel": batch_kernel_label(n2, p2, cus), "ms_per_step": ms, "evals_per_s": n2 * p2 / (ms * 1e-3),
                  "streams": 2, "check": "bit-exact vs closed form" if ok else "MISMATCH"}
     ctx.close()
 
@@ -707,9 +707,9 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     ms_s = s1.time(shard_step, 5)
     ok_s = same(got(b4), want4)
     out["c4_one_gpu"] = {
-        "batch": {"kernel": bits_kernel_label(n4, p4, cus), "ms_per_step": ms_b, "evals_per_s": n4 * p4 / (ms_b * 1e-3),
+        "batch": {"kernel": batch_kernel_label(n4, p4, cus), "ms_per_step": ms_b, "evals_per_s": n4 * p4 / (ms_b * 1e-3),
                   "check": "bit-exact vs closed form" if ok_b else "MISMATCH"},
-        "node_shard_keys_plus_decode": {"kernel": bits_kernel_label(n4, p4, cus, shard=True), "ms_per_step": ms_s,
+        "node_shard_keys_plus_decode": {"kernel": batch_kernel_label(n4, p4, cus, shard=True), "ms_per_step": ms_s,
                                         "evals_per_s": n4 * p4 / (ms_s * 1e-3),
                                         "check": "bit-exact vs closed form" if ok_s else "MISMATCH"},
         "note": "one GPU holds the whole 100k-node table (75 KB of bit planes); the 8-GPU C4 run splits it "
