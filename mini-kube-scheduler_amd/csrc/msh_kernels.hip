@@ -420,34 +420,28 @@ __global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Digit-row batched kernel: stages 1-4 for the identity-like modes (NONE, DEFAULT: everything
-// that needs only the first feasible match per pod), the default batch path.
+// Digit-row batched kernel: stages 1-4 for every normalize mode, the default batch path.
 //
 // Lanes = pods as in bits_kernel, but the node side is the digit-row bitmap index (ER_* layout,
 // msh_internal.h): for a word of 32 nodes, row r holds the nodes whose suffix digit is r, so a pod
 // reads the ONE row of its own digit instead of combining four code planes. Per lane and word:
-//   hit = E[row] & ~(X & nT)          one v_bitop3_b32 (X wave-uniform, SGPR)
+//   hit = E[row] & ~(X & nT)          one v_bitop3_b32
 // is set exactly at the nodes that pass NodeUnschedulable for this pod AND score 10 for it
-// (NodeNumber.Score, digit equal): 32 (pod, node) pairs per lane-op. The row words come from LDS:
-// each wave stages its slice's rows in tiles of ER_TG groups (16-byte copies, wave-private, no
-// barrier), and a lane reads its row of a chunk of 4 words with one ds_read_b128 (lanes of one
-// digit share the address and broadcast; the 11 rows of a chunk occupy distinct banks). The
-// group's hits are ORed (v_or3) and a group with one is remembered; groups are walked in
+// (NodeNumber.Score, digit equal): 32 (pod, node) pairs per lane-op. The KX modes (REVERSE,
+// MINMAX) also need the first feasible non-match, nm = V & ~E[row] & ~(X & nT), two more VALU.
+// Each wave stages its slice's rows and X words in LDS tiles of ER_TG groups (16-byte copies,
+// wave-private, no barrier; KX: the V words too, from the code planes), and per group a lane reads
+// its row of each 4-word chunk with one ds_read_b128 (lanes of one digit share the address and
+// broadcast; the 11 rows of a chunk occupy distinct banks) and the group's X words at one address.
+// The group's hits are ORed (v_or3) and a group with one is remembered; groups are walked in
 // DESCENDING List order, so the last remembered is the first, and the lowest group of the slice,
 // scanned last, keeps its hit words in registers for the exact node (first word with a hit, its
-// lowest set bit). A lane whose first hit lies in a higher group re-reads that group's row and X
-// words from memory behind an exec-mask branch (rare: 256 nodes almost always hold a match).
-// 1.75 VALU per 32 x 64 pairs (bits_kernel: 5.75): the scan is bound by VALU issue at ~1.75
-// clock per wave-word per CU, with LDS reads (one b128 per 4 words, 1 clock per wave-word per CU)
-// beside it. Slices and the LDS merge of their firsts as in bits_kernel.
+// lowest set bit). A lane whose first hit lies in a higher group re-reads that group from memory
+// behind an exec-mask branch (rare: 256 nodes almost always hold a match). ~2 VALU and two
+// ds_read_b128 per 32 x 64 pairs (bits_kernel: 5.75 VALU); at C3 the launches are bound by VALU
+// issue with the LDS array about half busy. Slices and the LDS merge of their
+// firsts as in bits_kernel.
 // ---------------------------------------------------------------------------------------
-
-// e & ~(x & m) in one v_bitop3_b32 (truth table 0x70 over S0 = e, S1 = x, S2 = m), x wave-uniform
-__device__ __forceinline__ uint32_t hit_s(uint32_t e, uint32_t x, uint32_t m) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x70" : "=v"(r) : "v"(e), "s"(x), "v"(m));
-  return r;
-}
 
 // The first node among 8 hit words of group g (words ascend in List order, bits within a word):
 // v_ffbl_b32 gives each word's lowest set bit, all-ones for an empty word, which ORed with the
