@@ -7,11 +7,12 @@ minisched/minisched.go:50-87 for every pod of a batch) over one batch of synthet
 inputs already resident in HBM.
 
 Modes (the headline line)
-  batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per GPU. With N GPUs the pods
-              are sharded (each rank its own 100k batches; no data-path collective) -> weak
-              scaling. The K steps are submitted from three host threads, each with its own ctx,
-              HIP stream and pod batch (the fast-call module's Submitter): one HIP launch costs
-              more host time than a batch takes on the device.
+  batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per batch per GPU. With N GPUs the
+              pods are sharded (each rank its own 100k batches; no data-path collective) -> weak
+              scaling. The K steps are K independent batches (eight distinct pod batches, each with
+              its own outputs, used in turn) submitted from one host thread on one HIP stream
+              through msh_schedule_batches_device, MSH_BATCHES_PER_LAUNCH (8) batches per kernel
+              launch: the submission a caller with several drained batches ready makes.
   sequential  BASELINE C5: same sizes, one pod at a time with node-state commits.
   nodeshard   BASELINE C4 shape: the node table split over the ranks, per-shard first keys
               merged with an RCCL all-reduce(MAX), then decoded (--nodes 100000 --pods 1000000).
@@ -43,7 +44,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
-VALU_PEAK_LANE_OPS = 157.3e12 / 2  # MI355X_MICROARCH.md: FP32 vector peak 157.3 TFLOPS = 2 x lane-ops/s
+CLOCK_HZ = 2.4e9                   # MI355X_MICROARCH.md: max clock
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # The digit-row kernel (rows_kernel, the identity-like modes): per 8-word group and 64-pod wave,
 # four ds_read_b128 (the lane's row words of both chunks, and the group's X words at one address)
@@ -51,20 +52,17 @@ HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # + 4 ORs + compare + select + the running-first move = 15 VALU.
 LDS_PEAK = 150e12                  # MI355X_MICROARCH.md: ~150 TB/s aggregate for ds_read_b64/b128
 ROWS_LDS_BYTES_PER_GROUP_WAVE = 4 * 1024
-ROWS_VALU_PER_GROUP = 15
-PMC_FILE = ROOT / "profiles" / "r2_pmc_c3.json"
+# wg_kernel (round 3): per group and wave 8 v_bitop3 + the OR tree + the group flag
+WG_VALU_PER_GROUP = 14
+PMC_FILE = ROOT / "profiles" / "r3_pmc_c3.json"
+VALU_PEAK_FILE = ROOT / "profiles" / "r3_ubench_valu_peak.json"
 
 
-def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False) -> str:
-    """The kernel msh_kernels.hip launch_batch dispatches (bits_slices' choice of S)."""
-    n_pad = max(-(-n_nodes // 1024) * 1024, 1024)
-    groups = n_pad // 256
-    blocks = -(-n_pods // 64)
-    sl = 1
-    while sl < 16 and blocks * sl < cus * 4 * 6 and groups // (2 * sl) >= 2:
-        sl *= 2
-    # the digit-row kernel in every mode, 1 pod per lane (rows_ppl)
-    return f"void msh::rows_kernel<{sl}, {str(kx).lower()}, {str(shard).lower()}, 1>"
+def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False,
+                       multi: bool = False) -> str:
+    """The kernel msh_kernels.hip launch_batch / launch_batches dispatches (4-wave workgroups)."""
+    b = lambda v: str(v).lower()
+    return f"void msh::wg_kernel<4, {b(kx)}, {b(shard)}, {b(multi)}>"
 
 
 def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
@@ -89,18 +87,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary configs (one GPU only)")
-    ap.add_argument("--streams", type=int, default=None,
-                    help="batch mode: independent batches pipelined over this many HIP streams "
-                         "(default with --submit mt: 4 for K <= 64 steps, else 3; otherwise 2)")
-    ap.add_argument("--submit", choices=["mt", "c", "python"], default="mt",
-                    help="batch mode: the K timed steps submitted from one host thread per stream, each "
-                         "with its own ctx (mt, csrc/msh_pyfast.c Submitter: one HIP launch costs more host "
-                         "time than a C3 batch takes on the device), or (A/B) by one C loop or one Python "
-                         "loop over the streams")
-    ap.add_argument("--launch", choices=["eager", "graph"], default="eager",
-                    help="batch mode: K host launches, or (A/B) the K timed steps captured as one hipGraph "
-                         "and replayed once; graph replay measured slower on ROCm 7.2 "
-                         "(profiles/ab/r2_sweep_bench.jsonl)")
+    ap.add_argument("--submit", choices=["multi", "single"], default="multi",
+                    help="batch mode: the K steps through msh_schedule_batches_device, 8 batches per launch "
+                         "(default), or (A/B) one msh_schedule_batch_device launch per step; one host thread "
+                         "and one HIP stream either way")
     return ap.parse_args()
 
 
@@ -186,16 +176,8 @@ def main():
     ctx = msh.DeviceContext(local)
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
     unsched, node_digit = synth.make_nodes(n_total)[1:]
-    # Batch mode pipelines consecutive, independent batches over `nstreams` HIP streams (each with
-    # its own pod and output buffers), so that one launch's ramp and tail overlap the next one's.
-    # Sequential mode carries node state from batch to batch and node-shard mode has a collective
-    # per step: both stay on one stream.
-    mt = mode == "batch" and args.submit == "mt" and args.launch == "eager"
-    # Lanes for --submit mt: a lane's kernels run back to back on its stream at the one-stream
-    # latency (~4 us at C3), so a short burst of K batches ends sooner spread over 4 lanes; in a
-    # long run 4 lanes contend and 3 complete batches faster (profiles/ab/r2_lanes_k20_k200.jsonl:
-    # K = 20 4.5 vs 4.9 us per step, K = 200 2.20 vs 1.97)
-    nstreams = (args.streams or ((4 if args.steps <= 64 else 3) if mt else 2)) if mode == "batch" else 1
+    G = msh._native.BATCHES_PER_LAUNCH  # batches per msh_schedule_batches_device launch
+    multi = mode == "batch" and args.submit == "multi"
     if mode == "nodeshard":
         sharded = D.NodeShardedScheduler(ctx, unsched, node_digit, world, rank)
         node_base = sharded.shard.lo
@@ -203,12 +185,13 @@ def main():
     else:
         ctx.upload_nodes(unsched, node_digit)
         node_base = 0
-        # pod-sharded weak scaling: rank r owns pods [r*P*S, (r+1)*P*S) of one global stream,
-        # split into S batches of P pods (one per stream)
-        pd_all, pt_all = synth._make_pods_fast(p_total * world * nstreams, synth.SEED)[1:]
+        # pod-sharded weak scaling: rank r owns pods [r*P*B, (r+1)*P*B) of one global stream, split
+        # into B distinct batches of P pods (batch mode: B = 8, step i schedules batch i mod 8)
+        nb = G if mode == "batch" else 1
+        pd_all, pt_all = synth._make_pods_fast(p_total * world * nb, synth.SEED)[1:]
         batches = []
-        for i in range(nstreams):
-            lo = (rank * nstreams + i) * p_total
+        for i in range(nb):
+            lo = (rank * nb + i) * p_total
             batches.append((np.ascontiguousarray(pd_all[lo:lo + p_total]), np.ascontiguousarray(pt_all[lo:lo + p_total])))
     p = len(batches[0][0])
     bufs = []
@@ -219,174 +202,101 @@ def main():
                      "status": torch.empty(p, dtype=torch.int32, device=dev),
                      "keys": torch.zeros(2 * p, dtype=torch.int32, device=dev)})
     klen = ctx.shard_keys_len(p) if mode == "nodeshard" else 0  # int32 keys one step all-reduces
-    S = Streams(torch, dev, nstreams)
-
-    # Batch steps call the C entry point through the fast-call module (csrc/msh_pyfast.c) with each
-    # buffer's pointers taken once: a Python method wrapper, five data_ptr() calls and ctypes
-    # conversions cost ~1-2 us per step next to a ~2.6 us launch.
-    batch_fn, handle = ctx._fast.schedule_batch_device, ctx._hv()
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    # the msh_batch descriptors of the eight batches, built once (host memory, read at each call)
+    descs = ctx.batch_descs([(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["idx"].data_ptr(), b["score"].data_ptr(),
+                              b["status"].data_ptr()) for b in bufs])
+    fast, handle = ctx._fast, ctx._hv()
     batch_args = [(handle, p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["idx"].data_ptr(), b["score"].data_ptr(),
-                   b["status"].data_ptr(), st.cuda_stream or None) for b, st in zip(bufs, S.all)]
+                   b["status"].data_ptr(), sh or None) for b in bufs]
+    descs_addr = __import__("ctypes").addressof(descs)
 
-    def step(k, ev0=None, ev1=None, single=False):
-        b = bufs[0] if single else bufs[k % nstreams]
-        st = S.main if single else S.all[k % nstreams]
-        sh = st.cuda_stream
-        if ev0 is not None:
-            ev0.record(st)
-        if mode == "batch":
-            ba = batch_args[0] if single else batch_args[k % nstreams]
-            if single:
-                ba = ba[:7] + (sh or None,)
-            rc = batch_fn(*ba)
-            if rc:
-                ctx._check(rc)
-        elif mode == "sequential":
-            ctx.schedule_sequential_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), 0, b["idx"].data_ptr(),
-                                           b["score"].data_ptr(), b["status"].data_ptr(), sh)
-        else:
-            ctx.shard_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), node_base, b["keys"].data_ptr(), sh)
-        if ev1 is not None:
-            ev1.record(st)
-        if mode == "nodeshard":  # RCCL all-reduce(MAX) of the per-shard keys, then decode
-            D.merge_shard_keys_(b["keys"][:klen])
-            ctx.decode_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["keys"].data_ptr(), b["idx"].data_ptr(),
-                                   b["score"].data_ptr(), b["status"].data_ptr(), sh)
+    def submit(k: int) -> None:
+        """Steps 0..k-1 of the current mode, in order, on `stream` (one host thread)."""
+        if mode == "batch" and multi:
+            for i0 in range(0, k, G):  # batch i of a launch = buffer i (launches start at multiples of 8)
+                rc = fast.schedule_batches_device(handle, min(G, k - i0), descs_addr, sh or None)
+                if rc:
+                    ctx._check(rc)
+            return
+        for i in range(k):
+            b = bufs[i % len(bufs)]
+            if mode == "batch":
+                rc = fast.schedule_batch_device(*batch_args[i % len(bufs)])
+                if rc:
+                    ctx._check(rc)
+            elif mode == "sequential":
+                ctx.schedule_sequential_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), 0, b["idx"].data_ptr(),
+                                               b["score"].data_ptr(), b["status"].data_ptr(), sh)
+            else:  # per-shard keys, RCCL all-reduce(MAX) on the same stream, then decode
+                ctx.shard_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), node_base, b["keys"].data_ptr(), sh)
+                D.merge_shard_keys_(b["keys"][:klen])
+                ctx.decode_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["keys"].data_ptr(),
+                                       b["idx"].data_ptr(), b["score"].data_ptr(), b["status"].data_ptr(), sh)
 
-    # --submit mt: lane i (ctx, stream, buffers of its own) submits steps i, i + L, ... from its own
-    # host thread; lane 0 is the main ctx with its own stream too, so the lanes share nothing
-    sub, lane_ctxs = None, []
-    if mt:
-        lane_streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
-        lane_ctxs = [ctx] + [msh.DeviceContext(local) for _ in range(nstreams - 1)]
-        for c in lane_ctxs[1:]:
-            c.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
-            c.upload_nodes(unsched, node_digit)
-        sub = ctx._fast.Submitter(local, [
-            (c._hv(), p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["idx"].data_ptr(), b["score"].data_ptr(),
-             b["status"].data_ptr(), st.cuda_stream) for c, b, st in zip(lane_ctxs, bufs, lane_streams)])
-        torch.cuda.synchronize()
-
-    if sub is not None:
-        if sub.run(args.warmup):
-            raise RuntimeError("warmup launch failed")
-    else:
-        S.fork()
-        for k in range(args.warmup):
-            step(k)
-        S.join()
+    submit(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-
-    # Device time from HIP events on the main stream bracketing the whole timed region (side
-    # streams fork from / join into it), divided by K: the interval at which batches complete.
-    # No event between launches: an event record is itself a barrier + timestamp packet.
-    # Node-shard steps hold an RCCL all-reduce and a decode launch too, so there the shard kernel
-    # is bracketed per step.
-    per_step = mode == "nodeshard"
-    # --submit c (A/B): batch mode submits the K steps from a C loop in the fast-call module, the
-    # loop a C or Go caller runs, one msh_schedule_batch_device call per step; measured no faster
-    # than the Python loop through the fast-call module (profiles/ab/r2_sweep_bench_cloop.jsonl),
-    # so the default stays the Python host mirror's own loop.
-    c_loop = mode == "batch" and args.submit == "c"
-    evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-           if per_step else [(None, None)] * args.steps)
-    for e0, e1 in evs:  # create the HIP events before the timed region
-        if e0 is not None:
-            e0.record(S.main)
-            e1.record(S.main)
-    # Graph launch (batch mode, A/B): the K steps -- the same K launches over the same streams --
-    # captured once, untimed, and replayed once in the timed region.
-    graph = None
-    launch = args.launch if mode == "batch" else "eager"
-    if launch == "graph":
-        graph = torch.cuda.CUDAGraph()
-        cap = torch.cuda.Stream(dev)
-        with torch.cuda.stream(cap):
-            S_cap = Streams(torch, dev, nstreams)  # main = the capture stream, side streams joined by events
-            saved = S.main, S.all
-            S.main, S.all = S_cap.main, S_cap.all
-            with torch.cuda.graph(graph, stream=cap):
-                S.fork()
-                for k in range(args.steps):
-                    step(k)
-                S.join()
-            S.main, S.all = saved
-        torch.cuda.synchronize()
-    # r0 opens the region on the main stream and is the side streams' fork point; each stream
-    # closes with its own end event (the final synchronize waits for all of them): four event
-    # operations around the K launches, created before the region (a torch Event creates its HIP
-    # event on its first record)
-    r0 = torch.cuda.Event(enable_timing=True)
-    ends = [torch.cuda.Event(enable_timing=True) for _ in S.all]
-    for e in [r0] + ends:
-        e.record(S.main)
+    # ---- the timed region: barrier (N > 1) + synchronize, K steps, synchronize (+ barrier) ----
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for e in (r0, r1):  # create the HIP events before the region (a torch Event makes its HIP event on first record)
+        e.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    if sub is not None:
-        sub.run(0)  # no launches: re-arms the lane threads' spin window after a long barrier
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if sub is None:
-        r0.record(S.main)
-    if sub is not None:
-        rc = sub.run(args.steps)
-        if rc:
-            ctx._check(rc)
-    elif graph is not None:
-        with torch.cuda.stream(S.main):
-            graph.replay()
-        ends[0].record(S.main)
-        ends = ends[:1]
-    else:
-        for st in S.all[1:]:
-            st.wait_event(r0)
-        if c_loop:
-            rc = ctx._fast.schedule_batch_device_steps(batch_args, args.steps)
-            if rc:
-                ctx._check(rc)
-        else:
-            for k, (e0, e1) in enumerate(evs):
-                step(k, e0, e1)
-        for st, e in zip(S.all, ends):
-            e.record(st)
-    t_sub = time.perf_counter()
+    r0.record(stream)
+    submit(args.steps)
+    r1.record(stream)
     torch.cuda.synchronize()
     if world > 1:  # the barrier and a second synchronize only where there is a barrier
         dist.barrier()
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if os.environ.get("MSH_BENCH_PROBE"):  # A/B: where the host time of the region goes
-        t_idle = time.perf_counter()
-        torch.cuda.synchronize()
-        t_idle = time.perf_counter() - t_idle
-        print(json.dumps({"probe": {"submit_us": (t_sub - t0) * 1e6, "sync_us": (elapsed - (t_sub - t0)) * 1e6,
-                                    "idle_sync_us": t_idle * 1e6, "steps": args.steps,
-                                    "lanes_host_us": ([[round(x, 2) for x in r] for r in sub.host_us()]
-                                                      if sub is not None else None),
-                                    "lanes_event_us": ([[round(x * 1e3, 2) for x in r] for r in sub.events_ms()]
-                                                       if sub is not None else None)}}), file=sys.stderr, flush=True)
-    if per_step:
-        kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
-    elif sub is not None:  # each lane's start / end events on its stream: latest end - earliest start
-        kernel_ms = sub.span_ms() / args.steps
-        sub.close()  # the lane threads stop spinning before anything else runs on the host
-    else:
-        kernel_ms = max(r0.elapsed_time(e) for e in ends) / args.steps
+    region_ms = r0.elapsed_time(r1)  # device span of the region on the launch stream
 
-    # Isolated launch time (outside the timed region): the same launches back to back on ONE
-    # stream, which is what rocprofv3's per-kernel average measures.
-    kernel_ms_isolated = kernel_ms
-    if nstreams > 1:
-        kernel_ms_isolated = Streams(torch, dev, 1).time(lambda k, sh: step(k, single=True), args.steps)
+    # ---- the dominant kernel's launch duration, for the roofline: R launches, each bracketed by its
+    # own HIP events on the stream it runs on (what rocprofv3's per-kernel average measures); in batch
+    # mode the full 8-batch launches of the default submission, or single-batch launches ----
+    R = 50 if mode != "nodeshard" else min(args.steps, 20)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(R)]
+    for e0, e1 in evs:
+        e0.record(stream)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    for e0, e1 in evs:
+        e0.record(stream)
+        if mode == "batch" and multi:
+            rc = fast.schedule_batches_device(handle, G, descs_addr, sh or None)
+            if rc:
+                ctx._check(rc)
+        elif mode == "batch":
+            rc = fast.schedule_batch_device(*batch_args[0])
+            if rc:
+                ctx._check(rc)
+        elif mode == "sequential":
+            b = bufs[0]
+            ctx.schedule_sequential_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), 0, b["idx"].data_ptr(),
+                                           b["score"].data_ptr(), b["status"].data_ptr(), sh)
+        else:
+            b = bufs[0]
+            ctx.shard_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), node_base, b["keys"].data_ptr(), sh)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    launch_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    batches_per_launch = G if (mode == "batch" and multi) else 1
+    if mode == "nodeshard":  # the timed steps hold the all-reduce and the decode too: redo them after
+        submit(1)
+        torch.cuda.synchronize()
 
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms, kernel_ms_isolated], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, launch_ms, region_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms, kernel_ms_isolated = float(t[0]), float(t[1]), float(t[2])
+        elapsed, launch_ms, region_ms = float(t[0]), float(t[1]), float(t[2])
 
     # ---- correctness of every buffer's last batch against the independent closed form ----
     check = "skipped"
@@ -404,7 +314,8 @@ def main():
     value = evals_total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    roofline = make_roofline(mode, n_local, p, kernel_ms, kernel_ms_isolated, nstreams, cus)
+    roofline = make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus)
+    roofline["region_device_ms_per_step"] = region_ms / args.steps
 
     extras = {}
     if rank == 0 and world == 1 and not args.no_extras:
@@ -420,8 +331,9 @@ def main():
 
     if rank == 0:
         if mode == "batch":
-            wl = (f"C3 batched: {n_total} nodes x {p} pods per batch per GPU (pod-sharded over {world} GPU; "
-                  f"{nstreams} independent batches in flight on {nstreams} HIP streams)")
+            wl = (f"C3 batched: {n_total} nodes x {p} pods per batch per GPU (pod-sharded over {world} GPU); "
+                  + (f"the K batches through msh_schedule_batches_device, {G} per launch, one stream"
+                     if multi else "one msh_schedule_batch_device launch per batch, one stream"))
         elif mode == "sequential":
             wl = f"C5 sequential-commit: {n_total} nodes x {p} pods per GPU, one pod at a time"
         else:
@@ -442,7 +354,8 @@ def main():
             "config": {"workload": wl, "nodes": n_total, "pods_per_step": int(p if mode != "nodeshard" else p_total),
                        "plugins": "filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber w=1]",
                        "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}",
-                       "streams": nstreams, "launch": launch, "submit": ("mt (one host thread + ctx per stream)" if mt else "c" if c_loop else "python"),
+                       "streams": 1, "submit": (f"multi ({G} batches per launch)" if multi else "single") if mode == "batch"
+                       else "per step",
                        **({"rehearsal": "all ranks on cuda:0, gloo (not a measurement)"} if rehearse else {})},
             "pods_per_s": pods_total / elapsed,
             "check": check,
@@ -452,91 +365,101 @@ def main():
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
-    for c in lane_ctxs[1:]:
-        c.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def make_roofline(mode, n_local, p, kernel_ms, kernel_ms_isolated, nstreams, cus):
-    """Roofline of the dominant kernel, per launch, from HIP events on the launch stream; the
-    instruction count from the rocprofv3 PMC passes (profiles/r2_pmc_c3.json) of that same kernel."""
-    kern_s, iso_s = kernel_ms * 1e-3, kernel_ms_isolated * 1e-3
+def load_valu_peak():
+    """The integer VALU issue rate measured on MI355X (scripts/ubench_valu_peak.hip ->
+    profiles/r3_ubench_valu_peak.json): wave64 instructions per SIMD per cycle for the scan's forms."""
+    d = load_json(VALU_PEAK_FILE) or {}
+    return d.get("int_valu_wave_instr_per_simd_cycle"), d
+
+
+def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
+    """Roofline of the dominant kernel, per launch: algorithmic bytes (or instructions) of one
+    launch / the launch's average duration, measured with HIP events on the launch stream around
+    each of R launches (bench.py main), the quantity rocprofv3's per-kernel average reports."""
+    launch_s = launch_ms * 1e-3
     pmc = load_json(PMC_FILE) or {}
+    ipc, peak_src = load_valu_peak()
+    valu_peak = (ipc * 4 * 64 * cus * CLOCK_HZ) if ipc else None  # lane-ops/s
     if mode == "sequential":
         # One wave decides the pods in order; alone on its SIMD it issues about one instruction per
         # 4 cycles of any kind (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so the floor
         # of the per-pod latency is its instruction count (VALU + SALU, counted by rocprofv3 for
-        # this kernel at C5) x 4 cycles at 2.4 GHz.
+        # this kernel at C5) x 4 cycles at 2.4 GHz. That is an issue floor of the code as written,
+        # not a hardware roofline: reported as issue_floor_frac, not frac.
         kname = seq_kernel_label(n_local)
         entry = pmc.get("kernels", {}).get("sequential", {})
         ok = entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
         instr = (entry.get("SQ_INSTS_VALU", 0) + entry.get("SQ_INSTS_SALU", 0)) / p if ok else None
         floor_us = instr * 4 / 2.4e3 if instr else None
-        achieved = kernel_ms * 1e3 / p
-        return {"bound": "issue latency (one wave)", "achieved": achieved, "peak": floor_us,
-                "unit": "us/pod (serial)", "frac": floor_us / achieved if floor_us else None,
-                "kernel": kname, "kernel_ms": kernel_ms,
+        achieved = launch_ms * 1e3 / p
+        return {"bound": "issue latency (one wave, serial)", "achieved": achieved, "unit": "us/pod",
+                "issue_floor_us_per_pod": floor_us,
+                "issue_floor_frac": floor_us / achieved if floor_us else None,
+                "kernel": kname, "kernel_ms": launch_ms,
                 "traffic": entry.get("hbm_bytes_per_launch") if ok else None,
                 "instructions_per_pod": instr,
-                "note": "peak = instructions per pod (rocprofv3 SQ_INSTS_VALU + SQ_INSTS_SALU / pods, "
-                        "profiles/r2_pmc_c3.json) x 4 cycles / 2.4 GHz; frac = that floor / measured us per pod"}
-    kname = batch_kernel_label(n_local, p, cus, shard=mode == "nodeshard")
-    evals = float(n_local) * p
-    entry = pmc.get("kernels", {}).get("batch", {})
-    pmc_ok = entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
+                "note": "a serial mode: the floor is the kernel's own instruction count per pod (rocprofv3 "
+                        "SQ_INSTS_VALU + SQ_INSTS_SALU / pods) x 4 cycles / 2.4 GHz, not a hardware roofline"}
+    multi = batches_per_launch > 1
+    kname = batch_kernel_label(n_local, p, cus, shard=mode == "nodeshard", multi=multi)
+    evals = float(n_local) * p * batches_per_launch
+    entry = pmc.get("kernels", {}).get("batch_multi" if multi else "batch", {})
+    pmc_ok = (entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
+              and entry.get("batches_per_launch", 1) == batches_per_launch)
     n_groups = max(-(-n_local // 1024) * 1024, 1024) // 256
-    group_waves = float(n_groups) * -(-p // 64)  # every 64-pod block meets every 256-node group once
-    # achieved = ALGORITHMIC LDS-array bytes of the scan per launch (4 KiB per group and 64-pod wave:
-    # 0.25 B per pod-node pair) / launch interval; next to it the counters of the same kernel at the
-    # same size (profiles/r2_pmc_c3.json): SQ_LDS_IDX_ACTIVE (LDS-array cycles, all CUs) and
-    # SQ_INSTS_VALU x 64 (the scan plus the per-wave prologue, tile copy, first-node decode, slice
-    # merge and epilogue)
+    group_waves = float(n_groups) * -(-p // 64) * batches_per_launch  # every 64-pod wave meets every group once
+    # achieved = ALGORITHMIC LDS-array bytes of the scan per launch (4 KiB per 256-node group and 64-pod
+    # wave: the lane's two 16-byte row reads and the group's two 16-byte X reads, 0.25 B per pod-node
+    # pair) / the launch's duration
     lds_bytes = group_waves * ROWS_LDS_BYTES_PER_GROUP_WAVE
     lds_cycles = entry.get("SQ_LDS_IDX_ACTIVE") if pmc_ok else None
-    model_ops = group_waves * ROWS_VALU_PER_GROUP * 64
+    model_instr = group_waves * WG_VALU_PER_GROUP  # wave-instructions of the scan
     valu_instr = entry.get("SQ_INSTS_VALU") if pmc_ok else None
-    counter_ops = valu_instr * 64 if valu_instr else None
-    uniq_bytes = 1.5 * n_local + 18.0 * p           # digit rows + X words, pod records + outputs, once
-    survey_bytes = 2.0 * n_local * p + 18.0 * p      # SURVEY §8d accounting (counts L1/L2/LDS re-reads)
-    lds_clk = LDS_PEAK / (256 * 256)                 # the guide's aggregate as LDS-array cycles per CU
-    return {
+    uniq_bytes = (1.5 * n_local + 18.0 * p * batches_per_launch)  # rows + X once, pod records + outputs
+    survey_bytes = 2.0 * n_local * p * batches_per_launch + 18.0 * p * batches_per_launch
+    out = {
         "bound": "lds",
-        "achieved": lds_bytes / kern_s / 1e9,
+        "achieved": lds_bytes / launch_s / 1e9,
         "peak": LDS_PEAK / 1e9,
         "unit": "GB/s",
-        "frac": lds_bytes / kern_s / LDS_PEAK,
+        "frac": lds_bytes / launch_s / LDS_PEAK,
         "traffic": entry.get("hbm_bytes_per_launch") if pmc_ok else None,
-        "traffic_note": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024), same kernel and size",
+        "traffic_note": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024), same kernel, size and batches",
         "kernel": kname,
-        "kernel_ms": kernel_ms,
-        "kernel_ms_note": (f"interval at which launches complete with {nstreams} streams in flight; "
-                           "kernel_ms_isolated = the same launches back to back on one stream "
-                           "(= rocprofv3's per-kernel average)") if nstreams > 1 else "one stream",
-        "kernel_ms_isolated": kernel_ms_isolated,
-        "frac_isolated": lds_bytes / iso_s / LDS_PEAK,
+        "kernel_ms": launch_ms,
+        "kernel_ms_note": ("mean of R launches, each bracketed by HIP events on its stream (rocprofv3's "
+                           "per-kernel average of the same launches must agree)"),
+        "batches_per_launch": batches_per_launch,
+        "ms_per_batch": launch_ms / batches_per_launch,
         "lds_bytes_per_launch": lds_bytes,
         "lds_bytes_per_eval": lds_bytes / evals,
-        "frac_counter": (lds_cycles / (cus * kern_s * lds_clk)) if lds_cycles else None,
-        "counter_source": ("rocprofv3 SQ_LDS_IDX_ACTIVE per launch (profiles/r2_pmc_c3.json)" if lds_cycles
-                           else "no PMC entry for this kernel and size"),
-        "peak_note": "peak = MI355X_MICROARCH.md LDS aggregate for ds_read_b128 (256 B/clk/CU); the scan moves "
-                     "4 KiB through the LDS array per 256-node group and 64-pod wave (rows + broadcast X words)",
-        "valu": {"bound": "valu", "unit": "Glane-op/s", "peak": VALU_PEAK_LANE_OPS / 1e9,
-                 "achieved_model": model_ops / kern_s / 1e9, "frac_model": model_ops / kern_s / VALU_PEAK_LANE_OPS,
-                 "lane_ops_per_eval_model": model_ops / evals,
-                 "lane_ops_per_eval_measured": counter_ops / evals if counter_ops else None,
-                 "frac_counter": counter_ops / kern_s / VALU_PEAK_LANE_OPS if counter_ops else None,
-                 "scan_share_of_valu": model_ops / counter_ops if counter_ops else None,
-                 "note": "peak = FP32 vector 157.3 TF / 2 (one lane-op per lane per 2-cycle wave64 issue)"},
-        "hbm": {"bound": "hbm", "achieved": uniq_bytes / kern_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": uniq_bytes / kern_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
+        "frac_counter": (lds_cycles / (cus * launch_s * LDS_PEAK / (256 * 256))) if lds_cycles else None,
+        "counter_source": (f"rocprofv3 SQ_LDS_IDX_ACTIVE per launch ({PMC_FILE.name})" if lds_cycles
+                           else "no PMC entry for this kernel, size and batch count"),
+        "peak_note": "MI355X_MICROARCH.md LDS: 256 B/clk/CU for ds_read_b128, ~150 TB/s aggregate",
+        "valu": {"bound": "valu (integer, measured issue rate)", "unit": "Gwave-instr/s",
+                 "peak": (valu_peak / 64 / 1e9) if valu_peak else None,
+                 "peak_source": (f"{VALU_PEAK_FILE.name}: {ipc:.3f} wave64 integer instructions per SIMD-cycle "
+                                 f"x 1,024 SIMDs x 2.4 GHz" if ipc else "unmeasured"),
+                 "achieved_model": model_instr / launch_s / 1e9,
+                 "frac_model": (model_instr / launch_s / (valu_peak / 64)) if valu_peak else None,
+                 "instr_per_group_wave_model": WG_VALU_PER_GROUP,
+                 "instr_measured": valu_instr,
+                 "frac_counter": (valu_instr / launch_s / (valu_peak / 64)) if (valu_instr and valu_peak) else None,
+                 "scan_share_of_valu": model_instr / valu_instr if valu_instr else None},
+        "hbm": {"bound": "hbm", "achieved": uniq_bytes / launch_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": uniq_bytes / launch_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
                 "survey_8d_bytes_per_launch": survey_bytes,
-                "survey_8d_frac": survey_bytes / kern_s / HBM_PEAK,
+                "survey_8d_frac": survey_bytes / launch_s / HBM_PEAK,
                 "survey_8d_note": "2 B per pair counts every L1/L2/LDS re-read of the node table as HBM "
                                   "traffic; the 7.5 KB table is read from HBM once per launch"},
     }
+    return out
 
 
 def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSH_ABI_VERSION 4
+#define MSH_ABI_VERSION 5
 
 /* ---- error codes (return values) ---- */
 typedef enum msh_err {
@@ -93,21 +93,24 @@ int msh_device_count(int* out_count);
 
 /* Page-locked host memory (hipHostMalloc) for the host-buffer entry points' pod columns and
  * outputs. With buffers from here (or registered with HIP) msh_schedule_batch / _sequential copy
- * nothing on the host: the pod columns go to the device by DMA and the kernel writes idx / score /
- * status straight into these buffers over PCIe. Pageable buffers work too; they are staged through
- * a page-locked buffer of the ctx. A cgo caller allocates its batch buffers here once and reuses
- * them. msh_host_free(NULL) is a no-op. */
+ * nothing on the host and issue no DMA: the kernel reads the pod columns from these buffers and
+ * writes idx / score / status straight into them over PCIe (zero-copy). Pageable buffers work too;
+ * they are staged through a page-locked buffer of the ctx. A cgo caller allocates its batch buffers
+ * here once and reuses them. msh_host_free(NULL) is a no-op. */
 int msh_host_alloc(size_t bytes, void** out_ptr);
 void msh_host_free(void* ptr);
 
 /* Create/destroy a context on `device`. Default plugin set = the reference's
  * (initialize.go:80-123): filter=[NodeUnschedulable], prescore=[NodeNumber],
- * score=[NodeNumber] weight 1, normalize NONE. msh_destroy first waits for every stream of the
- * device (launches the caller queued with the *_device entry points read the ctx's tables). */
+ * score=[NodeNumber] weight 1, normalize NONE. msh_create reads the library's test / A-B switches
+ * (MSH_* environment variables) once; a value outside a switch's set is MSH_ERR_INVALID. msh_destroy
+ * first waits for the launches this ctx queued with the *_device entry points (they read the ctx's
+ * tables), not for the rest of the device. */
 int msh_create(int device, msh_ctx** out_ctx);
 void msh_destroy(msh_ctx* ctx);
 
-/* Message for the last failing call on this ctx ("" if none). Valid until the next call. */
+/* Message for the last failing call on this ctx ("" if none). Valid until the next call. With a
+ * NULL ctx: the message of the last failed msh_create on the calling thread. */
 const char* msh_last_error(const msh_ctx* ctx);
 
 /* Plugin lists (Scheduler.filterPlugins / preScorePlugins / scorePlugins,
@@ -165,12 +168,32 @@ int msh_schedule_batch(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const u
  * Launches on different streams may overlap (independent batches pipelined): each needs its own
  * pod and output buffers. The ctx's node tables are read-only during batches; when an upload,
  * patch or plugin change left them to be re-prepared, the first launch after it prepares them and
- * waits for that before returning. The few configurations whose kernel keeps running results in
- * per-ctx scratch (normalizers needing the non-match extent on tables above 16,384 nodes) are
- * ordered across streams by the library. */
+ * waits for that before returning. The ctx records an event on `stream` after each launch: a later
+ * upload, patch, plugin change or count reset of THIS ctx is ordered after the ctx's own launches
+ * in flight (on its internal stream), and never waits for other ctxs' or the caller's other work. */
 int msh_schedule_batch_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
                               const uint8_t* d_pod_tol, int32_t* d_out_idx,
                               int64_t* d_out_score, int32_t* d_out_status, void* stream);
+
+/* Several independent batches in one submission (ABI v5): what a caller draining a deep activeQ
+ * (minisched.go:28-34, one scheduleOne per pod) hands over when it has more than one batch ready,
+ * e.g. consecutive next_batch drains. batches[i] describes batch i exactly as the arguments of
+ * msh_schedule_batch_device (device pointers, out_score may be NULL); the descriptor array itself
+ * is host memory, read during the call. Up to MSH_BATCHES_PER_LAUNCH batches share one kernel
+ * launch (a larger nb takes ceil(nb / MSH_BATCHES_PER_LAUNCH) launches, in order, on `stream`),
+ * which spreads the launch cost and the kernel's fill and drain over them. Results are identical to
+ * nb msh_schedule_batch_device calls. Asynchronous, like msh_schedule_batch_device. */
+#define MSH_BATCHES_PER_LAUNCH 8
+typedef struct msh_batch {
+  int32_t p;
+  int32_t reserved; /* 0 */
+  const int8_t* pod_digit;
+  const uint8_t* pod_tol;
+  int32_t* out_idx;
+  int64_t* out_score;
+  int32_t* out_status;
+} msh_batch;
+int msh_schedule_batches_device(msh_ctx* ctx, int32_t nb, const msh_batch* batches, void* stream);
 
 /* Sequential-commit mode (one pod at a time, node state committed between placements).
  * The node table stays in registers of one workgroup: up to 368,640 nodes without a capacity,

@@ -90,9 +90,7 @@ def build_fast(force: bool = False, verbose: bool = False) -> Path:
         return FAST
     cmd = ["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-Wextra",
            f"-I{sysconfig.get_paths()['include']}", f"-I{INCLUDE}", str(FAST_SRC),
-           f"-L{PKG_DIR}", "-lminisched_hip", "-Wl,-rpath,$ORIGIN",
-           # the Submitter's threads and its HIP events (the same libamdhip64.so.7 the library needs)
-           "-pthread", f"-L{Path(_hipcc()).resolve().parents[1] / 'lib'}", "-lamdhip64", "-o", str(FAST)]
+           f"-L{PKG_DIR}", "-lminisched_hip", "-Wl,-rpath,$ORIGIN", "-o", str(FAST)]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

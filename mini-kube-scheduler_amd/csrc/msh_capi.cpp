@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <initializer_list>
 #include <iterator>
 #include <mutex>
 #include <new>
@@ -36,6 +37,7 @@
 #include "msh_pool.h"
 
 using msh::HostPool;
+using msh::PoolLease;
 using msh::PluginParams;
 
 namespace {
@@ -46,12 +48,14 @@ struct CopyJob {
   size_t bytes;
 };
 
-// The copies, each split into pool.parts() contiguous pieces (64-byte aligned cuts), in ONE pool
-// run; small totals on the calling thread alone.
-void par_copy(HostPool* pool, const CopyJob* jobs, int n_jobs) {
+// The copies, each split into pool.parts() contiguous pieces (64-byte aligned cuts), in ONE run of
+// the process-wide pool (msh_pool.h); small totals, or no pool to lease, on the calling thread.
+void par_copy(const CopyJob* jobs, int n_jobs) {
   size_t total = 0;
   for (int i = 0; i < n_jobs; ++i) total += jobs[i].bytes;
-  if (!pool || total < (256u << 10)) {
+  PoolLease lease;
+  HostPool* pool = total >= (256u << 10) ? lease.get() : nullptr;
+  if (!pool) {
     for (int i = 0; i < n_jobs; ++i) std::memcpy(jobs[i].dst, jobs[i].src, jobs[i].bytes);
     return;
   }
@@ -100,8 +104,11 @@ struct msh_ctx {
   int32_t* d_ost = nullptr;
   size_t stage_cap = 0;
   unsigned char* h_stage = nullptr;  // page-locked: digit p | tol p | idx 4p | score 8p | status 4p
-  HostPool* pool = nullptr;
   hipEvent_t done_ev = nullptr;  // MSH_HOST_SYNC=poll
+  // Launches of the *_device entry points read the ctx's tables after the call returns: one event
+  // per caller stream, re-recorded after each launch on it. A table rewrite (upload, patch, plugin
+  // change, count reset) makes the ctx's own stream wait for exactly these, never the whole device.
+  std::vector<std::pair<hipStream_t, hipEvent_t>> inflight;
   size_t patch_cap = 0;
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
   int32_t patch_pending = 0;              // entries in d_patch the next prepare() applies
@@ -193,10 +200,6 @@ int ensure_stage(msh_ctx* c, int32_t p) {
     MSH_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), cap, hipHostMallocDefault));
     c->stage_cap = cap;
   }
-  if (!c->pool && (size_t)p >= 16384) {
-    const int workers = msh::host_pool_workers();
-    if (workers > 0) c->pool = new (std::nothrow) HostPool(workers);
-  }
   return MSH_OK;
 }
 
@@ -246,14 +249,47 @@ int check_ids(msh_ctx* c, const int32_t* ids, int32_t n, bool filter, const char
   return MSH_OK;
 }
 
+// After a *_device launch on caller stream s: (re-)record the ctx's event for s. One event per
+// stream the ctx has launched on (a linear search: callers use a handful of streams).
+int track_launch(msh_ctx* c, hipStream_t s) {
+  for (auto& e : c->inflight)
+    if (e.first == s) {
+      MSH_HIP(c, hipEventRecord(e.second, s));
+      return MSH_OK;
+    }
+  hipEvent_t ev = nullptr;
+  MSH_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  hipError_t e = hipEventRecord(ev, s);
+  if (e != hipSuccess) {
+    (void)hipEventDestroy(ev);
+    return hip_fail(c, e, "hipEventRecord");
+  }
+  c->inflight.emplace_back(s, ev);
+  return MSH_OK;
+}
+
+// Order the ctx's own stream after every launch this ctx queued on caller streams (device-side
+// waits: the host does not block here, and other ctxs' work on the device is not waited for).
+int after_inflight(msh_ctx* c) {
+  for (auto& e : c->inflight) MSH_HIP(c, hipStreamWaitEvent(c->stream, e.second, 0));
+  return MSH_OK;
+}
+
+// Host wait for every launch this ctx queued (msh_destroy: the tables are freed after it).
+void wait_inflight(msh_ctx* c) {
+  for (auto& e : c->inflight) (void)hipEventSynchronize(e.second);
+}
+
 // Rebuild the derived tables (planes, first feasible per class) after an upload, a patch or a
-// filter-list change. Launches queued earlier on ANY stream (the *_device entry points) may still
-// be reading the tables this rewrites: wait for the whole device first (this runs only after an
-// upload, a patch or a plugin change, never per batch), and finish the rebuild before returning.
+// filter-list change, on the ctx's stream behind every launch of this ctx still in flight (they may
+// read the tables this rewrites), and finish it before returning; then make launches on `s` wait for
+// the rebuild. Runs only after an upload, a patch or a plugin change, never per batch.
 int prepare(msh_ctx* c, hipStream_t s) {
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (!c->dirty) return MSH_OK;
-  MSH_HIP(c, hipDeviceSynchronize());
+  int rc = after_inflight(c);
+  if (rc != MSH_OK) return rc;
+  s = c->stream;
   hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad, c->pp.has_nu_filter,
                                        c->d_ball, c->d_planes, c->d_erows, s, c->d_patch, c->patch_pending);
   c->patch_pending = 0;
@@ -324,7 +360,7 @@ int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t*
   const uint8_t* src_pt = pod_tol;
   if (!in_pinned) {  // through the stage
     const CopyJob jobs[2] = {{c->h_stage + L.pd, pod_digit, (size_t)p}, {c->h_stage + L.pt, pod_tol, (size_t)p}};
-    par_copy(c->pool, jobs, 2);
+    par_copy(jobs, 2);
     src_pd = reinterpret_cast<const int8_t*>(c->h_stage + L.pd);
     src_pt = c->h_stage + L.pt;
   }
@@ -380,9 +416,42 @@ int host_io_end(msh_ctx* c, int32_t p, int32_t* out_idx, int64_t* out_score, int
     const CopyJob jobs[3] = {{out_idx, io.h_idx, (size_t)p * sizeof(int32_t)},
                              {out_status, io.h_status, (size_t)p * sizeof(int32_t)},
                              {out_score, io.h_score, (size_t)p * sizeof(int64_t)}};
-    par_copy(c->pool, jobs, out_score ? 3 : 2);
+    par_copy(jobs, out_score ? 3 : 2);
   }
   return MSH_OK;
+}
+
+// The message of the last failed msh_create on this thread (msh_last_error(NULL)).
+thread_local std::string g_create_err;
+
+// One A/B switch: unset leaves *out alone; a value outside `allowed` fails with a message.
+bool knob(const char* name, std::initializer_list<std::pair<const char*, int>> allowed, int* out, std::string* err) {
+  const char* v = getenv(name);
+  if (!v) return true;
+  for (const auto& a : allowed)
+    if (strcmp(v, a.first) == 0) {
+      *out = a.second;
+      return true;
+    }
+  *err = std::string(name) + "=" + v + ": not one of";
+  for (const auto& a : allowed) *err += std::string(" ") + a.first;
+  return false;
+}
+
+bool read_knobs(msh::DeviceInfo& d, std::string* err) {
+  int io = 0, poll = 0;
+  const bool ok = knob("MSH_BITS_SLICES", {{"0", 0}, {"1", 1}, {"2", 2}, {"4", 4}, {"8", 8}, {"16", 16}}, &d.bits_slices, err) &&
+                  knob("MSH_SEQ_WAVES", {{"0", 0}, {"1", 1}, {"4", 4}, {"15", 15}, {"16", 16}}, &d.seq_waves, err) &&
+                  knob("MSH_ROWS_PPL", {{"1", 1}, {"2", 2}}, &d.rows_ppl, err) &&
+                  knob("MSH_KX_BITS", {{"0", 0}, {"1", 1}}, &d.kx_bits, err) &&
+                  knob("MSH_HOST_IO", {{"zero-copy", 0}, {"zc", 1}, {"dma", 2}}, &io, err) &&
+                  knob("MSH_HOST_SYNC", {{"wait", 0}, {"poll", 1}}, &poll, err) &&
+                  knob("MSH_BATCH_KERNEL", {{"wg", 0}, {"slices", 1}}, &d.batch_kernel, err) &&
+                  knob("MSH_WG_WAVES", {{"0", 0}, {"4", 4}, {"8", 8}}, &d.wg_waves, err);
+  d.host_io_dma = io == 2;
+  d.host_io_zc_in = io == 0;
+  d.host_sync_poll = poll;
+  return ok;
 }
 
 }  // namespace
@@ -428,6 +497,7 @@ void msh_host_free(void* ptr) {
 }
 
 int msh_create(int device, msh_ctx** out_ctx) {
+  g_create_err.clear();
   if (!out_ctx) return MSH_ERR_INVALID;
   *out_ctx = nullptr;
   int n = 0;
@@ -442,16 +512,14 @@ int msh_create(int device, msh_ctx** out_ctx) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->dev.cus = prop.multiProcessorCount;
-  // test / A-B switches, read once here (never on a launch path)
-  if (const char* e = getenv("MSH_BITS_SLICES")) c->dev.bits_slices = atoi(e);
-  if (const char* e = getenv("MSH_SEQ_WAVES")) c->dev.seq_waves = atoi(e);
-  if (const char* e = getenv("MSH_ROWS_PPL")) c->dev.rows_ppl = atoi(e) == 1 ? 1 : 2;
-  if (const char* e = getenv("MSH_KX_BITS")) c->dev.kx_bits = atoi(e) == 1;
-  if (const char* e = getenv("MSH_HOST_IO")) {
-    c->dev.host_io_dma = strcmp(e, "dma") == 0;
-    c->dev.host_io_zc_in = strcmp(e, "dma") != 0 && strcmp(e, "zc") != 0;
+  // test / A-B switches, read once here (never on a launch path); a value outside a switch's set is
+  // rejected (MSH_ERR_INVALID, message in msh_last_error(NULL)), never mapped to another setting
+  std::string bad;
+  if (!read_knobs(c->dev, &bad)) {
+    delete c;
+    g_create_err = bad;
+    return MSH_ERR_INVALID;
   }
-  if (const char* e = getenv("MSH_HOST_SYNC")) c->dev.host_sync_poll = strcmp(e, "poll") == 0;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return MSH_ERR_HIP;
@@ -477,9 +545,10 @@ int msh_create(int device, msh_ctx** out_ctx) {
 void msh_destroy(msh_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
-  // launches queued on caller streams (the *_device entry points) may still read the tables
-  (void)hipDeviceSynchronize();
-  delete c->pool;
+  // launches this ctx queued on caller streams (the *_device entry points) may still read the tables
+  wait_inflight(c);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& e : c->inflight) (void)hipEventDestroy(e.second);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   free_nodes(c);
   free_pods(c);
@@ -490,7 +559,7 @@ void msh_destroy(msh_ctx* c) {
   delete c;
 }
 
-const char* msh_last_error(const msh_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+const char* msh_last_error(const msh_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
 int msh_set_plugins_ex(msh_ctx* c, const int32_t* filter_ids, int32_t nf,
                        const int32_t* prescore_ids, int32_t npre, const int32_t* score_ids,
@@ -550,12 +619,16 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
   if (n < 0 || n > msh::MAX_NODES) return fail(c, MSH_ERR_INVALID, "node count outside [0, 2^24-2]");
   if (n > 0 && (!unsched || !digit)) return fail(c, MSH_ERR_INVALID, "null node arrays");
   DeviceGuard g(c->device);
-  // launches queued earlier on any stream may still read the tables rewritten below
-  MSH_HIP(c, hipDeviceSynchronize());
+  // launches this ctx queued earlier may still read the tables rewritten below: the copies below go
+  // behind them on the ctx's stream, and a reallocation first waits for them on the host
+  int rc = after_inflight(c);
+  if (rc != MSH_OK) return rc;
   // Padded to whole 1,024-node blocks, and never empty: an empty cluster is a table of padding
   // slots (infeasible for every pod), so every pod gets FitError from the kernel.
   const int32_t n_pad = std::max(((n + msh::NODE_PAD - 1) / msh::NODE_PAD) * msh::NODE_PAD, msh::NODE_PAD);
   if ((size_t)n_pad > c->node_cap || c->d_planes == nullptr) {
+    wait_inflight(c);
+    MSH_HIP(c, hipStreamSynchronize(c->stream));
     free_nodes(c);
     const size_t cap = (size_t)n_pad;
     MSH_HIP(c, hipMalloc(&c->d_unsched, cap));
@@ -598,8 +671,8 @@ int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t
                     ((unsigned long long)(unsched[k] ? 1u : 0u) << 32) |
                     ((unsigned long long)(uint8_t)digit[k] << 40);
   DeviceGuard g(c->device);
-  // launches queued earlier on any stream may still read the tables the patch rewrites
-  MSH_HIP(c, hipDeviceSynchronize());
+  // d_patch is only read by the prep launch of an earlier (synchronous) prepare; the columns and the
+  // tables the entries change are rewritten by prepare(), behind this ctx's launches in flight
   if ((size_t)count > c->patch_cap) {
     (void)hipFree(c->d_patch);
     c->d_patch = nullptr;
@@ -682,8 +755,46 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   a.out_score = d_out_score;
   a.out_status = d_out_status;
   hipError_t e = msh::launch_batch(a, false, c->dev, s);
-  if (e != hipSuccess) return hip_fail(c, e, "bits_kernel");
-  return MSH_OK;
+  if (e != hipSuccess) return hip_fail(c, e, "batch kernel");
+  return p > 0 ? track_launch(c, s) : MSH_OK;
+}
+
+int msh_schedule_batches_device(msh_ctx* c, int32_t nb, const msh_batch* batches, void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (nb < 0) return fail(c, MSH_ERR_INVALID, "negative batch count");
+  if (nb > 0 && !batches) return fail(c, MSH_ERR_INVALID, "null batch array");
+  for (int32_t i = 0; i < nb; ++i) {
+    const msh_batch& b = batches[i];
+    if (b.p < 0) return fail(c, MSH_ERR_INVALID, "batch " + std::to_string(i) + ": negative pod count");
+    if (b.p > 0 && (!b.pod_digit || !b.pod_tol || !b.out_idx || !b.out_status))  // out_score optional
+      return fail(c, MSH_ERR_INVALID, "batch " + std::to_string(i) + ": null device pointer");
+  }
+  DeviceGuard g(c->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int rc = prepare(c, s);
+  if (rc != MSH_OK) return rc;
+  const bool single = c->dev.batch_kernel == 1 || (msh::needs_kx(c->pp) && c->dev.kx_bits);  // A/B kernels
+  for (int32_t i0 = 0; i0 < nb; i0 += msh::MULTI_MAX) {
+    const int n = std::min<int32_t>(msh::MULTI_MAX, nb - i0);
+    msh::BatchDesc d[msh::MULTI_MAX];
+    for (int k = 0; k < n; ++k) {
+      const msh_batch& b = batches[i0 + k];
+      d[k] = msh::BatchDesc{b.pod_digit, b.pod_tol, b.out_idx, b.out_score, b.out_status, b.p, 0};
+      if (single && b.p > 0) {
+        msh::BatchArgs a = batch_args(c, b.p, b.pod_digit, b.pod_tol);
+        a.out_idx = b.out_idx;
+        a.out_score = b.out_score;
+        a.out_status = b.out_status;
+        hipError_t e = msh::launch_batch(a, false, c->dev, s);
+        if (e != hipSuccess) return hip_fail(c, e, "batch kernel");
+      }
+    }
+    if (single) continue;
+    hipError_t e = msh::launch_batches(batch_args(c, 0, nullptr, nullptr), d, n, c->dev, s);
+    if (e != hipSuccess) return hip_fail(c, e, "wg_kernel (multi-batch)");
+  }
+  return nb > 0 ? track_launch(c, s) : MSH_OK;
 }
 
 int msh_schedule_batch(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
@@ -738,7 +849,7 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
     if (!err.empty()) return fail(c, MSH_ERR_UNSUPPORTED, err);
     return hip_fail(c, e, "seq_kernel");
   }
-  return MSH_OK;
+  return p > 0 ? track_launch(c, s) : MSH_OK;
 }
 
 int msh_schedule_sequential(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
@@ -773,8 +884,11 @@ int msh_node_pod_counts(msh_ctx* c, int32_t* out_counts) {
   if (c->n_nodes > 0 && !out_counts) return fail(c, MSH_ERR_INVALID, "null output");
   if (c->n_nodes == 0) return MSH_OK;
   DeviceGuard g(c->device);
-  MSH_HIP(c, hipDeviceSynchronize());
-  MSH_HIP(c, hipMemcpy(out_counts, c->d_counts, (size_t)c->n_nodes * sizeof(int32_t), hipMemcpyDeviceToHost));
+  int rc = after_inflight(c);  // sequential launches of this ctx in flight update the counts
+  if (rc != MSH_OK) return rc;
+  MSH_HIP(c, hipMemcpyAsync(out_counts, c->d_counts, (size_t)c->n_nodes * sizeof(int32_t), hipMemcpyDeviceToHost,
+                            c->stream));
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
   return MSH_OK;
 }
 
@@ -783,7 +897,8 @@ int msh_reset_node_pod_counts(msh_ctx* c) {
   c->err.clear();
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   DeviceGuard g(c->device);
-  MSH_HIP(c, hipDeviceSynchronize());  // sequential launches in flight update the counts
+  int rc = after_inflight(c);  // sequential launches of this ctx in flight update the counts
+  if (rc != MSH_OK) return rc;
   MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->node_cap * sizeof(int32_t), c->stream));
   MSH_HIP(c, hipStreamSynchronize(c->stream));
   return MSH_OK;
@@ -819,8 +934,8 @@ int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   a.keys = d_keys;
   a.node_base = node_base;
   hipError_t e = msh::launch_batch(a, true, c->dev, s);
-  if (e != hipSuccess) return hip_fail(c, e, "bits_kernel(shard)");
-  return MSH_OK;
+  if (e != hipSuccess) return hip_fail(c, e, "batch kernel (shard keys)");
+  return p > 0 ? track_launch(c, s) : MSH_OK;
 }
 
 int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,

@@ -46,6 +46,8 @@ struct DeviceInfo {
   int host_io_dma = 0;
   int host_io_zc_in = 1;
   int host_sync_poll = 0;  // A/B only (MSH_HOST_SYNC=poll): poll an event instead of hipStreamSynchronize
+  int batch_kernel = 0;    // 0 = wg_kernel (default), 1 = the round-2 slice kernel rows_kernel (MSH_BATCH_KERNEL=slices, A/B)
+  int wg_waves = 0;        // A/B only (MSH_WG_WAVES=1|2|4|8): waves per workgroup of wg_kernel, 0 = auto
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit
@@ -120,6 +122,28 @@ struct BatchArgs {
 };
 
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s);
+
+// One batch of a multi-batch launch (msh_schedule_batches_device): its own pod columns and
+// outputs; blk_end = the launch's workgroups up to and including this batch's (exclusive prefix).
+struct BatchDesc {
+  const int8_t* pod_digit;
+  const uint8_t* pod_tol;
+  int32_t* out_idx;
+  int64_t* out_score;  // may be null
+  int32_t* out_status;
+  int32_t n_pods;
+  int32_t blk_end;
+};
+constexpr int MULTI_MAX = 8;  // batches per launch (kernel-argument descriptors, 48 B each)
+struct MultiArgs {
+  BatchArgs a;  // the node table, plugin set and launch geometry (its pod / output fields unused)
+  int32_t nb;
+  BatchDesc d[MULTI_MAX];
+};
+
+// nb (1..MULTI_MAX) independent batches of device-resident pods in ONE launch of the workgroup
+// kernel. `a` carries the table and plugin set.
+hipError_t launch_batches(const BatchArgs& a, const BatchDesc* d, int nb, const DeviceInfo& dev, hipStream_t s);
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,
                               const int32_t* keys, int32_t slot1_any, PluginParams pp,

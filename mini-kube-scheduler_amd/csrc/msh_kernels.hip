@@ -730,6 +730,209 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Workgroup-table batched kernel (the default batch path since round 3).
+//
+// The same per-pair evaluation as rows_kernel (lanes = pods, per lane and 32-node word
+// hit = E[row] & ~(X & nT), one v_bitop3_b32), but the node side is staged ONCE per workgroup:
+// the W waves of a workgroup (W x 64 pods) copy the digit rows and X words (KX: and the V words)
+// of up to WG_CHUNK groups into LDS together, and every wave then scans every group of the table
+// for its own 64 pods. No slices, so no slice merge and no per-wave tile copies (rows_kernel's
+// S slice waves each copied their own tile). Groups are walked in descending List order and a
+// group with a hit pushes a 1 into a per-chunk bitmap (bit k = group lo + k), two VALU per group
+// (v_min_u32 + v_lshl_or_b32) where rows_kernel kept a running index (compare, move, select);
+// the first group with a hit is the lowest set bit of the lowest chunk's bitmap that has one, and
+// its hit words are recomputed from LDS once per lane at the end (from memory when it lies in a
+// chunk that is no longer staged: more than WG_CHUNK groups above the first with a hit, rare).
+// Tables larger than one chunk are streamed chunk by chunk, descending: the next chunk's copy is in
+// flight in registers while the current one is scanned (two workgroup barriers per chunk).
+//
+// MULTI: the launch serves up to MULTI_MAX independent batches (msh_schedule_batches_device), each
+// with its own pod columns and outputs, described in the kernel arguments; a workgroup finds its
+// batch by the exclusive prefix of workgroups (a scalar count over at most 7 compares).
+// ---------------------------------------------------------------------------------------
+constexpr int WG_CHUNK = 32;  // groups per staged chunk (8,192 nodes; 12 KiB, 13 KiB with V words)
+
+template <bool MULTI>
+struct KArgs {
+  using T = BatchArgs;
+};
+template <>
+struct KArgs<true> {
+  using T = MultiArgs;
+};
+__device__ __forceinline__ const BatchArgs& base_args(const BatchArgs& a) { return a; }
+__device__ __forceinline__ const BatchArgs& base_args(const MultiArgs& m) { return m.a; }
+
+template <int W, bool KX, bool SHARD, bool MULTI>
+__global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T ka) {
+  static_assert(!(SHARD && MULTI), "shard keys come from single-batch launches");
+  constexpr int GQ = KX ? ER_GQ + 2 : ER_GQ;                     // 16-byte entries per staged group
+  constexpr int NT = W * WAVE;                                   // threads per workgroup
+  constexpr int EPT = (WG_CHUNK * GQ + NT - 1) / NT;             // staged entries per thread per chunk
+  __shared__ uint4 s_tab[WG_CHUNK * GQ];
+  const BatchArgs& A = base_args(ka);
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+
+  // ---- this workgroup's batch ----
+  int32_t blk = (int32_t)blockIdx.x;
+  const int8_t* pod_digit = A.pod_digit;
+  const uint8_t* pod_tol = A.pod_tol;
+  int32_t* out_idx = A.out_idx;
+  int64_t* out_score = A.out_score;
+  int32_t* out_status = A.out_status;
+  int32_t n_pods = A.n_pods;
+  if constexpr (MULTI) {
+    int b = 0;
+#pragma unroll
+    for (int k = 0; k < MULTI_MAX - 1; ++k) b += (k + 1 < ka.nb && blk >= ka.d[k].blk_end) ? 1 : 0;
+    b = __builtin_amdgcn_readfirstlane(b);
+    if (b > 0) blk -= ka.d[b - 1].blk_end;
+    const BatchDesc& d = ka.d[b];
+    pod_digit = d.pod_digit;
+    pod_tol = d.pod_tol;
+    out_idx = d.out_idx;
+    out_score = d.out_score;
+    out_status = d.out_status;
+    n_pods = d.n_pods;
+  }
+  const int32_t wbase = blk * NT + wv * WAVE;  // this wave's first pod (may lie past the batch)
+  const int32_t j = wbase + lane;
+
+  // ---- staging: chunk c = groups [c * WG_CHUNK, min(+WG_CHUNK, n_groups)) ----
+  const int32_t n_groups = A.n_groups;
+  const int32_t n_chunks = (n_groups + WG_CHUNK - 1) / WG_CHUNK;  // >= 1 (tables are never empty)
+  const uint4* __restrict__ er = reinterpret_cast<const uint4*>(A.erows);
+  // Every thread loads EPT (<= 4) entries unconditionally (indices past the chunk clamped to its
+  // last entry: no divergent branch around a load, so the copies stay in flight) and stores every
+  // slot of the staging array it owns (slots past the chunk are never read). Four named registers,
+  // not an array: an array of uint4 captured by the lambdas went to scratch.
+  static_assert(EPT <= 4, "wg_kernel stages at most four 16-byte entries per thread and chunk");
+  uint4 st0, st1, st2, st3;
+  auto st_ref = [&](int k) -> uint4& { return k == 0 ? st0 : k == 1 ? st1 : k == 2 ? st2 : st3; };
+  auto chunk_load = [&](int32_t c) {
+    const int32_t glo = c * WG_CHUNK, last = min(WG_CHUNK, n_groups - glo) * GQ - 1;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int32_t i = min((int32_t)threadIdx.x + k * NT, last);
+      if constexpr (KX) {
+        const int32_t gi = i / GQ, q = i - gi * GQ;
+        const uint4* src = q < ER_GQ ? er + (size_t)(glo + gi) * ER_GQ + q
+                                     : reinterpret_cast<const uint4*>(A.planes + (size_t)(glo + gi) * GROUP_DWORDS +
+                                                                      PLANE_V * PLANE_GW) + (q - ER_GQ);
+        st_ref(k) = *src;
+      } else {
+        st_ref(k) = er[(size_t)glo * ER_GQ + i];
+      }
+    }
+  };
+  auto chunk_store = [&]() {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int32_t i = (int32_t)threadIdx.x + k * NT;
+      if ((k + 1) * NT <= WG_CHUNK * GQ || i < WG_CHUNK * GQ) s_tab[i] = st_ref(k);
+    }
+  };
+
+  // ---- prologue: the top chunk's copy, the pod bytes (clamped offset) and the class firsts in
+  // flight together ----
+  chunk_load(n_chunks - 1);
+  const uint32_t lastp = n_pods > 0 ? (uint32_t)(n_pods - 1) : 0u;
+  const uint32_t jj = min((uint32_t)j, lastp);
+  const int dq = pod_digit[jj];
+  const uint8_t tq = pod_tol[jj];
+  const uint32_t ball0 = A.ball[0], ball1 = A.ball[1];
+  chunk_store();
+  const bool act = j < n_pods;
+  const uint32_t code = (act && dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;
+  const uint32_t tol = (act && tq) ? 1u : 0u;
+  const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
+  const uint32_t row = code <= 9u ? code : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
+  __syncthreads();
+
+  // hits of one staged group (and KX: feasible non-matches); returns the OR of the words
+  auto group_words = [&](const uint4* tg, uint32_t (&h)[PLANE_GW], uint32_t (&nm)[PLANE_GW]) {
+    const uint4 e0 = tg[row], e1 = tg[ER_ROWS + row], x0 = tg[ER_Q], x1 = tg[ER_Q + 1];
+    rows_hits(e0, e1, x0, x1, nT, h);
+    if constexpr (KX) rows_nonmatch(e0, e1, x0, x1, tg[ER_GQ], tg[ER_GQ + 1], nT, nm);
+  };
+  auto or8 = [](const uint32_t (&h)[PLANE_GW]) {
+    return ((h[0] | h[1] | h[2]) | (h[3] | h[4] | h[5])) | (h[6] | h[7]);
+  };
+  uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group with a feasible match / non-match
+  for (int32_t c = n_chunks - 1; c >= 0; --c) {
+    const int32_t glo = c * WG_CHUNK, ng = min(WG_CHUNK, n_groups - glo);
+    if (c != n_chunks - 1) {
+      __syncthreads();  // every wave is done with chunk c + 1
+      chunk_store();
+      __syncthreads();
+    }
+    if (c > 0) chunk_load(c - 1);  // in flight during this chunk's scan
+    uint32_t bm = 0, bx = 0;        // bit k: group glo + k has a feasible match / non-match
+    int32_t k = ng - 1;
+    for (; k >= 1; k -= 2) {  // two groups per step, all eight reads before the first use
+      uint32_t h1[PLANE_GW], h0[PLANE_GW], n1[PLANE_GW], n0[PLANE_GW];
+      group_words(s_tab + k * GQ, h1, n1);
+      group_words(s_tab + (k - 1) * GQ, h0, n0);
+      bm = (bm << 2) | (umin(or8(h1), 1u) << 1) | umin(or8(h0), 1u);
+      if constexpr (KX) bx = (bx << 2) | (umin(or8(n1), 1u) << 1) | umin(or8(n0), 1u);
+    }
+    if (k == 0) {
+      uint32_t h0[PLANE_GW], n0[PLANE_GW];
+      group_words(s_tab, h0, n0);
+      bm = (bm << 1) | umin(or8(h0), 1u);
+      if constexpr (KX) bx = (bx << 1) | umin(or8(n0), 1u);
+    }
+    if (bm) fm = (uint32_t)glo + lowbit(bm);
+    if constexpr (KX)
+      if (bx) fx = (uint32_t)glo + lowbit(bx);
+  }
+  // the exact first node of the first group with a hit: chunk 0 is still staged
+  uint32_t rm = NOFIT, rx = NOFIT;
+  const uint32_t staged_hi = (uint32_t)min(WG_CHUNK, n_groups);
+  if (fm != NO_GROUP) {
+    if (fm < staged_hi) {
+      uint32_t h[PLANE_GW], nm[PLANE_GW];
+      const uint4* tg = s_tab + fm * GQ;
+      rows_hits(tg[row], tg[ER_ROWS + row], tg[ER_Q], tg[ER_Q + 1], nT, h);
+      (void)nm;
+      rm = hits_first(h, fm);
+    } else {
+      rm = rows_group_first(A, fm, row, nT);
+    }
+  }
+  if constexpr (KX) {
+    if (fx != NO_GROUP) {
+      if (fx < staged_hi) {
+        uint32_t n[PLANE_GW];
+        const uint4* tg = s_tab + fx * GQ;
+        rows_nonmatch(tg[row], tg[ER_ROWS + row], tg[ER_Q], tg[ER_Q + 1], tg[ER_GQ], tg[ER_GQ + 1], nT, n);
+        rx = hits_first(n, fx);
+      } else {
+        rx = rows_group_first_nm(A, fx, row, nT);
+      }
+    }
+  }
+  if constexpr (SHARD && !KX) write_class_keys(A);
+  if (!act) return;
+  if constexpr (SHARD) {
+    A.keys[j] = rm != NOFIT ? shard_key(A.node_base, rm) : 0;
+    if constexpr (KX) A.keys[(size_t)n_pods + j] = rx != NOFIT ? shard_key(A.node_base, rx) : 0;
+  } else {
+    int32_t oi, ost;
+    int64_t osc;
+    const int64_t im = rm != NOFIT ? (int64_t)rm : -1, ia = key_to_idx(tol ? ball1 : ball0);
+    if constexpr (KX)
+      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, A.pp, &oi, &osc, &ost);
+    else
+      decode_ident(im, ia, code != CODE_NONE_POD, make_ident_decode(A.pp), &oi, &osc, &ost);
+    out_idx[j] = oi;
+    if (out_score) out_score[j] = osc;  // optional output (NULL: not written)
+    out_status[j] = ost;
+  }
+}
+
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
 __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restrict__ pod_digit,
                                                           const uint8_t* __restrict__ pod_tol,
@@ -1291,6 +1494,40 @@ hipError_t launch_rows_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t 
     return dev.rows_ppl == 1 ? launch_rows_p<KX, SHARD, 1>(a, dev, s) : launch_rows_p<KX, SHARD, 2>(a, dev, s);
 }
 
+// Waves per workgroup of wg_kernel: 4 (one staged copy of the table per 256 pods), or 8 (A/B,
+// MSH_WG_WAVES=8).
+int wg_waves(int64_t n_pods, const DeviceInfo& dev) {
+  (void)n_pods;
+  return dev.wg_waves == 8 ? 8 : 4;
+}
+
+template <int W, bool KX, bool SHARD>
+hipError_t launch_wg_w(const BatchArgs& a, hipStream_t s) {
+  const int64_t blocks = ((int64_t)a.n_pods + W * WAVE - 1) / (W * WAVE);
+  hipLaunchKernelGGL((wg_kernel<W, KX, SHARD, false>), dim3((unsigned)blocks), dim3(W * WAVE), 0, s, a);
+  return hipGetLastError();
+}
+
+template <bool KX, bool SHARD>
+hipError_t launch_wg_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
+  switch (wg_waves(a.n_pods, dev)) {
+    case 8: return launch_wg_w<8, KX, SHARD>(a, s);
+    default: return launch_wg_w<4, KX, SHARD>(a, s);
+  }
+}
+
+template <int W, bool KX>
+hipError_t launch_multi_w(MultiArgs& m, hipStream_t s) {
+  int32_t blocks = 0;
+  for (int b = 0; b < m.nb; ++b) {
+    blocks += (m.d[b].n_pods + W * WAVE - 1) / (W * WAVE);
+    m.d[b].blk_end = blocks;
+  }
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((wg_kernel<W, KX, false, true>), dim3((unsigned)blocks), dim3(W * WAVE), 0, s, m);
+  return hipGetLastError();
+}
+
 template <bool KX, bool SHARD>
 hipError_t launch_bits_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
   switch (bits_slices(a.n_pods, a.n_groups, dev)) {
@@ -1309,8 +1546,29 @@ hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, h
   // every mode on the digit rows (REVERSE / MINMAX also track the first feasible non-match)
   if (kx && dev.kx_bits)  // A/B: the code-plane kernel for REVERSE / MINMAX
     return shard ? launch_bits_t<true, true>(a, dev, s) : launch_bits_t<true, false>(a, dev, s);
-  if (shard) return kx ? launch_rows_t<true, true>(a, dev, s) : launch_rows_t<false, true>(a, dev, s);
-  return kx ? launch_rows_t<true, false>(a, dev, s) : launch_rows_t<false, false>(a, dev, s);
+  if (dev.batch_kernel == 1) {  // A/B: the round-2 slice kernel
+    if (shard) return kx ? launch_rows_t<true, true>(a, dev, s) : launch_rows_t<false, true>(a, dev, s);
+    return kx ? launch_rows_t<true, false>(a, dev, s) : launch_rows_t<false, false>(a, dev, s);
+  }
+  if (shard) return kx ? launch_wg_t<true, true>(a, dev, s) : launch_wg_t<false, true>(a, dev, s);
+  return kx ? launch_wg_t<true, false>(a, dev, s) : launch_wg_t<false, false>(a, dev, s);
+}
+
+hipError_t launch_batches(const BatchArgs& a, const BatchDesc* d, int nb, const DeviceInfo& dev, hipStream_t s) {
+  if (nb <= 0 || nb > MULTI_MAX) return hipErrorInvalidValue;
+  MultiArgs m{};
+  m.a = a;
+  m.nb = nb;
+  int64_t pods = 0;
+  for (int b = 0; b < nb; ++b) {
+    m.d[b] = d[b];
+    pods += d[b].n_pods;
+  }
+  const bool kx = needs_kx(a.pp);
+  switch (wg_waves(pods, dev)) {
+    case 8: return kx ? launch_multi_w<8, true>(m, s) : launch_multi_w<8, false>(m, s);
+    default: return kx ? launch_multi_w<4, true>(m, s) : launch_multi_w<4, false>(m, s);
+  }
 }
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,

@@ -12,7 +12,6 @@
 //     NodeUnschedulable.Filter (upstream node_unschedulable.go, v1.22.0).
 #include <algorithm>
 #include <cstring>
-#include <mutex>
 #include <numeric>
 #include <string_view>
 #include <vector>
@@ -55,7 +54,7 @@ int msh_toleration_tolerates_unschedulable(const msh_toleration* t) {
 
 int msh_pack_nodes(int32_t n, const char* names, const int64_t* name_off,
                    const uint8_t* unschedulable, int32_t* out_order, uint8_t* out_unsched,
-                   int8_t* out_digit) {
+                   int8_t* out_digit) try {
   if (n < 0) return MSH_ERR_INVALID;
   if (n == 0) return MSH_OK;
   if (!names || !name_off || !unschedulable || !out_order || !out_unsched || !out_digit)
@@ -81,46 +80,53 @@ int msh_pack_nodes(int32_t n, const char* names, const int64_t* name_off,
     out_digit[k] = suffix_digit(nm[i].data(), static_cast<int64_t>(nm[i].size()));  // name's own end
   }
   return MSH_OK;
+} catch (...) {  // std::bad_alloc: nothing throws across the C-ABI
+  return MSH_ERR_NOMEM;
 }
 
 int msh_pack_pods(int32_t p, const char* names, const int64_t* name_off,
                   const msh_toleration* tols, const int64_t* tol_off, int8_t* out_digit,
-                  uint8_t* out_tol) {
+                  uint8_t* out_tol) try {
   if (p < 0) return MSH_ERR_INVALID;
   if (p == 0) return MSH_OK;
   if (!names || !name_off || !tol_off || !out_digit || !out_tol) return MSH_ERR_INVALID;
-  if (name_off[0] < 0 || tol_off[0] < 0) return MSH_ERR_INVALID;
-  if (tol_off[p] > tol_off[0] && !tols) return MSH_ERR_INVALID;
-  // Pods [lo, hi): offsets checked without early exits (monotone, names non-empty), one name
-  // byte and two offsets per pod, tolerations only for pods that carry any.
+  // Pods [lo, hi): each pod's offsets are checked BEFORE any read they guard (a name must be
+  // non-empty and start at a non-negative offset; a toleration range must be non-negative, ordered
+  // and backed by `tols`), so malformed offsets return MSH_ERR_INVALID without touching memory
+  // outside the ranges they describe. One pass, split over the pool for large batches.
   auto pack_range = [&](int32_t lo, int32_t hi) {
     bool bad = false;
     for (int32_t j = lo; j < hi; j++) {
-      bad |= (name_off[j + 1] <= name_off[j]) | (tol_off[j + 1] < tol_off[j]);
-      out_digit[j] = suffix_digit(names, name_off[j + 1]);
+      const int64_t n0 = name_off[j], n1 = name_off[j + 1], t0 = tol_off[j], t1 = tol_off[j + 1];
+      const bool name_ok = n0 >= 0 && n1 > n0;
+      const bool tol_ok = t0 >= 0 && t1 >= t0 && (t1 == t0 || tols != nullptr);
+      bad |= !(name_ok && tol_ok);
+      out_digit[j] = name_ok ? suffix_digit(names, n1) : static_cast<int8_t>(-1);
       uint8_t tol = 0;
-      for (int64_t k = tol_off[j], t1 = tol_off[j + 1]; k < t1 && !tol; k++)
-        tol = tolerates(tols[k]) ? 1 : 0;  // any toleration
+      if (tol_ok)
+        for (int64_t k = t0; k < t1 && !tol; k++) tol = tolerates(tols[k]) ? 1 : 0;  // any toleration
       out_tol[j] = tol;
     }
     return bad;
   };
-  // Large batches are split over a persistent pool of host threads (one caller at a time uses it;
-  // a concurrent caller packs on its own thread).
-  static msh::HostPool* pool = msh::host_pool_workers() > 0 ? new msh::HostPool(msh::host_pool_workers()) : nullptr;
-  static std::mutex pool_mu;
-  std::unique_lock<std::mutex> lk(pool_mu, std::defer_lock);
-  if (p >= kParallelPods && pool && lk.try_lock()) {
-    const int n = pool->parts();
-    std::vector<char> bad(static_cast<size_t>(n), 0);
-    pool->run([&](int k) {
-      bad[k] = pack_range((int32_t)((int64_t)p * k / n), (int32_t)((int64_t)p * (k + 1) / n)) ? 1 : 0;
-    });
-    for (char b : bad)
-      if (b) return MSH_ERR_INVALID;
-    return MSH_OK;
+  // Large batches are split over the process-wide pool of host threads (msh_pool.h: one caller at a
+  // time; a concurrent caller, a forked child or a host without the threads packs on its own thread).
+  if (p >= kParallelPods) {
+    msh::PoolLease lease;
+    if (msh::HostPool* pool = lease.get()) {
+      const int n = pool->parts();
+      std::vector<char> bad(static_cast<size_t>(n), 0);
+      pool->run([&](int k) {
+        bad[k] = pack_range((int32_t)((int64_t)p * k / n), (int32_t)((int64_t)p * (k + 1) / n)) ? 1 : 0;
+      });
+      for (char b : bad)
+        if (b) return MSH_ERR_INVALID;
+      return MSH_OK;
+    }
   }
   return pack_range(0, p) ? MSH_ERR_INVALID : MSH_OK;
+} catch (...) {
+  return MSH_ERR_NOMEM;
 }
 
 }  // extern "C"

@@ -1,6 +1,13 @@
-// msh_pool.h — a small persistent pool of host threads, shared by the C-ABI's staged copies
-// (msh_capi.cpp) and the snapshot packer (msh_pack.cpp). Host code only.
+// msh_pool.h — ONE process-wide pool of persistent host threads, shared by the C-ABI's staged
+// copies (msh_capi.cpp) and the snapshot packer (msh_pack.cpp). Host code only.
+//
+// Use it through PoolLease: a caller that finds the pool busy (another thread's pack or copy), a
+// process forked after the pool was created (its copy of the pool has no threads), or a failed
+// thread creation gets no pool and runs on its own thread. Nothing here throws across the C-ABI.
 #pragma once
+
+#include <sys/types.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -8,19 +15,30 @@
 #include <cstdint>
 #include <functional>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
 namespace msh {
 
-// Persistent host threads: run(f) calls f(0..n-1),
-// part 0 on the calling thread, the rest on the workers, and returns when all are done. A worker
-// spins on the job counter for a while after each job before it blocks, so back-to-back batches
-// do not pay a futex wake-up per call (tens of microseconds on a busy host).
+// Persistent host threads: run(f) calls f(0..n-1), part 0 on the calling thread, the rest on the
+// workers, and returns when all are done. A worker spins on the job counter for a while after each
+// job before it blocks, so back-to-back batches do not pay a futex wake-up per call (tens of
+// microseconds on a busy host).
 class HostPool {
  public:
-  explicit HostPool(int workers) {
-    for (int w = 0; w < workers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
+  // nullptr when a worker thread cannot be created (the ones that were are joined).
+  static HostPool* create(int workers) noexcept {
+    HostPool* p = new (std::nothrow) HostPool();
+    if (!p) return nullptr;
+    try {
+      p->th_.reserve((size_t)workers);
+      for (int w = 0; w < workers; ++w) p->th_.emplace_back([p, w] { p->loop(w + 1); });
+    } catch (...) {  // std::system_error from std::thread, std::bad_alloc
+      delete p;
+      return nullptr;
+    }
+    return p;
   }
   ~HostPool() {
     {
@@ -43,6 +61,7 @@ class HostPool {
   }
 
  private:
+  HostPool() = default;
   void loop(int part) {
     uint64_t seen = 0;
     for (;;) {
@@ -71,7 +90,7 @@ class HostPool {
   std::atomic<bool> stop_{false};
 };
 
-// Workers for a pool on this host: half the hardware threads less one, at most MSH_POOL_MAX - 1
+// Workers for the pool on this host: half the hardware threads less one, at most MSH_POOL_MAX - 1
 // (the caller runs a part too). A one-GPU job on the MI355X pool gets a 16-CPU share.
 #ifndef MSH_POOL_MAX
 #define MSH_POOL_MAX 16
@@ -80,5 +99,48 @@ inline int host_pool_workers() {
   const unsigned hw = std::thread::hardware_concurrency();
   return (int)std::min<unsigned>(MSH_POOL_MAX - 1, hw > 2 ? hw / 2 - 1 : 0u);
 }
+
+// The process-wide pool's state: atomics only (no mutex a fork could leave locked in the child).
+struct SharedPool {
+  std::atomic<int> state{0};  // 0 not created, 1 being created, 2 ready, 3 none (no workers / failed)
+  std::atomic<int> busy{0};   // one run at a time
+  HostPool* pool = nullptr;
+  pid_t owner = 0;            // the process whose threads these are
+};
+inline SharedPool& shared_pool_state() {
+  static SharedPool s;
+  return s;
+}
+
+// RAII lease of the shared pool: get() is the pool, or nullptr (run on the calling thread).
+class PoolLease {
+ public:
+  PoolLease() {
+    SharedPool& s = shared_pool_state();
+    int st = s.state.load(std::memory_order_acquire);
+    if (st == 0) {
+      int zero = 0;
+      if (!s.state.compare_exchange_strong(zero, 1, std::memory_order_acq_rel)) return;  // another thread creates it
+      const int w = host_pool_workers();
+      s.pool = w > 0 ? HostPool::create(w) : nullptr;
+      s.owner = getpid();
+      s.state.store(s.pool ? 2 : 3, std::memory_order_release);
+      st = s.pool ? 2 : 3;
+    }
+    if (st != 2 || s.owner != getpid()) return;  // none, still being created, or a forked child
+    int free_ = 0;
+    if (!s.busy.compare_exchange_strong(free_, 1, std::memory_order_acquire)) return;
+    pool_ = s.pool;
+  }
+  ~PoolLease() {
+    if (pool_) shared_pool_state().busy.store(0, std::memory_order_release);
+  }
+  PoolLease(const PoolLease&) = delete;
+  PoolLease& operator=(const PoolLease&) = delete;
+  HostPool* get() const { return pool_; }
+
+ private:
+  HostPool* pool_ = nullptr;
+};
 
 }  // namespace msh

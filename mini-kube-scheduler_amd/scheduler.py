@@ -202,6 +202,23 @@ class DeviceContext:
         if rc:
             self._check(rc)
 
+    @staticmethod
+    def batch_descs(batches: Sequence[tuple]) -> "C.Array":
+        """An msh_batch array for schedule_batches_device from (p, d_pod_digit, d_pod_tol, d_idx,
+        d_score or 0, d_status) tuples of device addresses; build it once and reuse it."""
+        arr = (N.Batch * len(batches))()
+        for i, (p, pd, pt, oi, os_, ost) in enumerate(batches):
+            arr[i] = N.Batch(int(p), 0, pd, pt, oi, os_ or None, ost)
+        return arr
+
+    def schedule_batches_device(self, descs, nb: int | None = None, stream: int = 0) -> None:
+        """msh_schedule_batches_device over an msh_batch array (batch_descs): up to
+        N.BATCHES_PER_LAUNCH batches per kernel launch, asynchronous on `stream`."""
+        nb = len(descs) if nb is None else nb
+        rc = self._fast.schedule_batches_device(self._hv(), nb, C.addressof(descs), stream or None)
+        if rc:
+            self._check(rc)
+
     def schedule_sequential_device(self, p: int, d_pod_digit: int, d_pod_tol: int, max_pods_per_node: int,
                                    d_idx: int, d_score: int, d_status: int, stream: int = 0) -> None:
         rc = self._fast.schedule_sequential_device(self._hv(), p, d_pod_digit, d_pod_tol,

@@ -29,10 +29,11 @@ def test_library_exports_every_declared_symbol(msh):
 
 def test_fast_call_module(msh):
     """The CPython fast-call module (csrc/msh_pyfast.c) loads against the same library, exposes
-    the four per-batch device entry points, and passes a NULL ctx through to the ABI's own check
+    the per-batch device entry points, and passes a NULL ctx through to the ABI's own check
     (MSH_ERR_INVALID, no device call)."""
     fast = msh._native.fast()
-    names = ["schedule_batch_device", "schedule_sequential_device", "shard_keys_device", "decode_keys_device"]
+    names = ["schedule_batch_device", "schedule_batches_device", "schedule_sequential_device", "shard_keys_device",
+             "decode_keys_device"]
     assert all(callable(getattr(fast, n)) for n in names)
     inv = msh._native.MSH_ERR_INVALID
     assert fast.schedule_batch_device(None, 0, None, None, None, None, None, None) == inv
@@ -48,22 +49,10 @@ def test_fast_call_module(msh):
         fast.schedule_batch_host(None, pd, pt, oi, ost, ost)
     with pytest.raises((ValueError, BufferError)):  # outputs must be writable, C-contiguous
         fast.schedule_batch_host(None, pd, pt, oi[::2].repeat(2), os_[::-1], ost)
-    step = (None, 0, None, None, None, None, None, None)
-    assert fast.schedule_batch_device_steps([step, step], 5) == inv  # stops at the first failing call
-    assert fast.schedule_batch_device_steps([step], 0) == 0
-    with pytest.raises(ValueError):
-        fast.schedule_batch_device_steps([step[:7]], 1)
-    with pytest.raises(ValueError):
-        fast.schedule_batch_device_steps([], 1)
-    # the multi-thread Submitter checks its lanes before it touches the device
-    with pytest.raises(ValueError):
-        fast.Submitter(0, [])
-    with pytest.raises(ValueError):  # every lane its own ctx (the ABI's one-ctx-per-thread rule)
-        fast.Submitter(0, [(1, 10, 1, 1, 1, 1, 1, 2), (1, 10, 1, 1, 1, 1, 1, 3)])
-    with pytest.raises(ValueError):  # and its own stream
-        fast.Submitter(0, [(1, 10, 1, 1, 1, 1, 1, 2), (4, 10, 1, 1, 1, 1, 1, 2)])
-    with pytest.raises(ValueError):
-        fast.Submitter(0, [step[:7]])
+    assert fast.schedule_batches_device(None, 0, None, None) == inv
+    descs = (msh._native.Batch * 2)()
+    assert fast.schedule_batches_device(None, 2, C.addressof(descs), None) == inv
+    assert not hasattr(fast, "Submitter")  # bench-only submission code is not in the product module
     with pytest.raises(TypeError):
         fast.schedule_batch_device(None, 0)
     with pytest.raises(OverflowError):
@@ -73,7 +62,7 @@ def test_fast_call_module(msh):
 def test_abi_version(msh):
     header = (ROOT / "include" / "minisched_hip.h").read_text()
     assert f"#define MSH_ABI_VERSION {msh._native.lib().msh_abi_version()}" in header
-    assert msh._native.lib().msh_abi_version() == 4
+    assert msh._native.lib().msh_abi_version() == 5
 
 
 def test_no_device_is_an_error_not_a_fallback(msh):

@@ -478,9 +478,9 @@ def test_scores_optional(msh, gpu_ctx, oracle, synth, norm):
 
 @pytest.mark.parametrize("change", ["patch", "upload"])
 def test_table_change_while_batches_in_flight(msh, gpu_ctx, oracle, change):
-    """msh_patch_nodes / msh_upload_nodes while batches queued on other streams still read the
-    planes: the table is rebuilt only after the device has drained (prepare() and the upload /
-    patch calls wait for it), so the queued batches see the old table and later ones the new."""
+    """msh_patch_nodes / msh_upload_nodes while batches of the same ctx queued on another stream
+    still read the tables: the rebuild is ordered after the ctx's own launches in flight (one event
+    per caller stream), so the queued batches see the old table and later ones the new."""
     torch = pytest.importorskip("torch")
     rng = np.random.default_rng(77)
     ps = oracle.PluginSet()
@@ -512,6 +512,55 @@ def test_table_change_while_batches_in_flight(msh, gpu_ctx, oracle, change):
     for oi, osc, ost in old:
         _assert_same((oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy()), want_old, f"{change}: queued batch")
     _assert_same(new, oracle.c_schedule_batch(u2, nd2, pd, pt, ps, threads=8), f"{change}: after the change")
+
+
+@pytest.mark.parametrize("change", ["patch", "upload", "reset_counts"])
+def test_table_change_does_not_wait_for_other_ctx(msh, oracle, change):
+    """A table change of ctx A waits for A's own launches only (verdict r2 #3): ctx B has ~10 ms of
+    C4-size batches queued on its own stream; A's one-node cordon flip (the f2 informer Update path,
+    eventhandler.go:45-65), re-upload or count reset returns while B's batches are still running. A's
+    batch queued before the change sees the old table, A's batch after it the new one, and B's
+    outputs are all bit-exact vs the oracle."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(91)
+    dev = torch.device("cuda:0")
+    ua, nda, _, _ = _rand_case(rng, 5000, 1, p_unsched=0.2)
+    ub, ndb, _, _ = _rand_case(rng, 100_000, 1, p_unsched=0.1)
+    _, _, pd, pt = _rand_case(rng, 1, 100_000, p_tol=0.2)
+    _, _, pdb, ptb = _rand_case(rng, 1, 1_000_000, p_tol=0.05)
+    with msh.DeviceContext(0) as A, msh.DeviceContext(0) as B:
+        A.upload_nodes(ua, nda)
+        B.upload_nodes(ub, ndb)
+        sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        a_old = _dev_batch(torch, dev, pd, pt)
+        b_bufs = [_dev_batch(torch, dev, pdb, ptb) for _ in range(2)]
+        done_b = torch.cuda.Event()
+        torch.cuda.synchronize()
+        for k in range(36):  # ~275 us each on one MI355X: ~10 ms queued on B's stream
+            t = b_bufs[k % 2]
+            B.schedule_batch_device(len(pdb), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
+                                    t[4].data_ptr(), sb.cuda_stream)
+        done_b.record(sb)
+        A.schedule_batch_device(len(pd), *[x.data_ptr() for x in a_old], sa.cuda_stream)
+        u2, nd2 = ua.copy(), nda.copy()
+        u2[17] ^= 1
+        if change == "patch":
+            A.patch_nodes(np.array([17], np.int32), u2[17:18], nd2[17:18])
+        elif change == "upload":
+            A.upload_nodes(u2, nd2)
+        else:
+            A.reset_node_pod_counts()
+            u2 = ua
+        b_running = not done_b.query()
+        a_new = A.schedule_batch(pd, pt)
+        torch.cuda.synchronize()
+        assert b_running, f"{change} on ctx A waited for ctx B's queued batches"
+        _assert_same([a_old[i].cpu().numpy() for i in (2, 3, 4)], oracle.c_schedule_batch(ua, nda, pd, pt),
+                     f"{change}: A before")
+        _assert_same(a_new, oracle.c_schedule_batch(u2, nd2, pd, pt), f"{change}: A after")
+        want_b = closed_form(ub, ndb, pdb, ptb)
+        for t in b_bufs:
+            _assert_same([t[i].cpu().numpy() for i in (2, 3, 4)], want_b, f"{change}: B")
 
 
 def test_maximum_node_table(msh, gpu_ctx, synth):
@@ -546,6 +595,7 @@ def test_bits_slices(msh, oracle, n, slices, ppl, kx_bits, monkeypatch):
     by msh_create) against the oracle, for the batch and the shard-key entry points, in the
     identity-like and the non-match (MINMAX) modes."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_BATCH_KERNEL", "slices")  # the round-2 slice kernel (A/B)
     monkeypatch.setenv("MSH_BITS_SLICES", slices)
     monkeypatch.setenv("MSH_ROWS_PPL", ppl)  # pods per lane of the digit-row kernel
     monkeypatch.setenv("MSH_KX_BITS", kx_bits)  # MINMAX on the code-plane kernel (A/B) or the rows
@@ -625,47 +675,125 @@ def test_host_buffer_paths(msh, gpu_ctx, oracle, synth, norm):
     assert (outs[0][20_000:] == -7).all()  # nothing written past p
 
 
-@pytest.mark.parametrize("lanes,k", [(3, 20), (2, 7), (4, 3)])
-def test_submitter_lanes_bit_exact(msh, oracle, lanes, k):
-    """bench.py's default submission (csrc/msh_pyfast.c Submitter): one host thread per lane, each
-    with its own ctx, stream and pod batch, batch i by lane i % lanes; every lane's last outputs
-    are bit-exact vs the oracle, and the event span covers the run."""
+def _dev_batch(torch, dev, pd, pt, scores=True):
+    return [torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev),
+            torch.full((len(pd),), -7, dtype=torch.int32, device=dev),
+            torch.full((len(pd),), -7, dtype=torch.int64, device=dev) if scores else None,
+            torch.full((len(pd),), -7, dtype=torch.int32, device=dev)]
+
+
+def _desc(t):
+    return (len(t[0]), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr() if t[3] is not None else 0,
+            t[4].data_ptr())
+
+
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+@pytest.mark.parametrize("nb", [1, 3, 8, 9, 17])
+def test_multi_batch_launch(msh, gpu_ctx, oracle, norm, nb):
+    """msh_schedule_batches_device (ABI v5): nb independent batches, up to 8 per launch, ragged pod
+    counts (empty and one-pod batches among them), some without scores; every batch bit-exact vs
+    the oracle, and nothing written past a batch's end."""
     torch = pytest.importorskip("torch")
-    rng = np.random.default_rng(4242 + lanes)
-    u, nd, _, _ = _rand_case(rng, 5000, 1)
     dev = torch.device("cuda:0")
-    ctxs = [msh.DeviceContext(0) for _ in range(lanes)]
-    try:
-        cases, args = [], []
-        for c in ctxs:
-            c.upload_nodes(u, nd)
-            _, _, pd, pt = _rand_case(rng, 1, 100_000 + int(rng.integers(0, 64)))
-            t = [torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev),
-                 torch.full((len(pd),), -7, dtype=torch.int32, device=dev),
-                 torch.zeros(len(pd), dtype=torch.int64, device=dev),
-                 torch.full((len(pd),), -7, dtype=torch.int32, device=dev)]
-            st = torch.cuda.Stream(dev)
-            cases.append((pd, pt, t))
-            args.append((c._hv(), len(pd), *[x.data_ptr() for x in t], st.cuda_stream))
-        torch.cuda.synchronize()
-        sub = ctxs[0]._fast.Submitter(0, args)
-        try:
-            assert sub.run(k) == 0
+    rng = np.random.default_rng(77 * nb + norm)
+    sizes = [0, 1, 64, 65, 255, 257, 100_003, 5000, 333, 4096, 1, 2, 700, 64, 128, 129, 999][:nb]
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, norm)
+    _set(gpu_ctx, msh, ps)
+    u, nd, _, _ = _rand_case(rng, 5000, 1)
+    gpu_ctx.upload_nodes(u, nd)
+    cases = []
+    for k, p in enumerate(sizes):
+        _, _, pd, pt = _rand_case(rng, 1, p)
+        t = _dev_batch(torch, dev, pd, pt, scores=(k % 3 != 2))
+        pad = torch.full((8,), -7, dtype=torch.int32, device=dev)  # canary behind nothing: outputs sized p
+        cases.append((pd, pt, t, pad))
+    descs = gpu_ctx.batch_descs([_desc(c[2]) for c in cases])
+    stream = torch.cuda.current_stream().cuda_stream
+    gpu_ctx.schedule_batches_device(descs, stream=stream)
+    torch.cuda.synchronize()
+    for k, (pd, pt, t, _) in enumerate(cases):
+        want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+        gi, gst = t[2].cpu().numpy(), t[4].cpu().numpy()
+        gs = t[3].cpu().numpy() if t[3] is not None else want[1]
+        _assert_same((gi, gs, gst), want, f"batch {k} of {nb} (p={len(pd)}) norm={norm}")
+    # a second submission on the same descriptors gives the same outputs (buffers reused)
+    for _, _, t, _ in cases:
+        t[2].fill_(-7)
+    gpu_ctx.schedule_batches_device(descs, stream=stream)
+    torch.cuda.synchronize()
+    for k, (pd, pt, t, _) in enumerate(cases):
+        assert (t[2].cpu().numpy() == oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)[0]).all(), k
+
+
+def test_multi_batch_invalid(msh, gpu_ctx):
+    """Bad descriptors are rejected before any launch (MSH_ERR_INVALID), and nb = 0 is a no-op."""
+    N = msh._native
+    fast = gpu_ctx._fast
+    assert fast.schedule_batches_device(gpu_ctx._hv(), 0, None, None) == 0
+    assert fast.schedule_batches_device(gpu_ctx._hv(), 2, None, None) == N.MSH_ERR_INVALID
+    assert fast.schedule_batches_device(gpu_ctx._hv(), -1, None, None) == N.MSH_ERR_INVALID
+    bad = gpu_ctx.batch_descs([(-1, 1, 1, 1, 0, 1)])
+    with pytest.raises(msh.MshError):
+        gpu_ctx.schedule_batches_device(bad)
+    bad = gpu_ctx.batch_descs([(10, 1, 0, 1, 0, 1)])  # null pod_tol
+    with pytest.raises(msh.MshError):
+        gpu_ctx.schedule_batches_device(bad)
+
+
+@pytest.mark.parametrize("waves", ["4", "8"])
+@pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 70_000])
+def test_wg_kernel_chunks(msh, oracle, n, waves, monkeypatch):
+    """wg_kernel streams tables above 32 groups (8,192 nodes) through LDS chunk by chunk, and
+    re-reads the first group with a hit from memory when it lies above the staged chunk 0: digit 3
+    only in the second half of the table makes those pods' first matches late. 4- and 8-wave
+    workgroups (MSH_WG_WAVES), batch, multi-batch and shard-key entry points, NONE and MINMAX."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_WG_WAVES", waves)
+    rng = np.random.default_rng(n + int(waves))
+    u, nd, pd, pt = _rand_case(rng, n, 3000, p_unsched=0.2, p_tol=0.3)
+    nd[: n // 2][nd[: n // 2] == 3] = 4
+    dev = torch.device("cuda:0")
+    p = len(pd)
+    with msh.DeviceContext(0) as ctx:
+        for norm in (0, 3):
+            ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, norm)
+            _set(ctx, msh, ps)
+            ctx.upload_nodes(u, nd)
+            want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+            _assert_same(ctx.schedule_batch(pd, pt), want, f"wg n={n} W={waves} norm={norm}")
+            halves = [_dev_batch(torch, dev, pd[: p // 3], pt[: p // 3]), _dev_batch(torch, dev, pd[p // 3:], pt[p // 3:])]
+            descs = ctx.batch_descs([_desc(t) for t in halves])
+            ctx.schedule_batches_device(descs, stream=torch.cuda.current_stream().cuda_stream)
+            t0, t1 = halves
+            keys = torch.empty(ctx.shard_keys_len(p), dtype=torch.int32, device=dev)
+            d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+            ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+            out = _dev_batch(torch, dev, pd, pt)
+            ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), keys.data_ptr(), out[2].data_ptr(),
+                                   out[3].data_ptr(), out[4].data_ptr(), torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
-            assert sub.span_ms() > 0
-            ran = min(lanes, k)
-            host = sub.host_us()  # per lane: wake, start event, each launch, end event
-            assert [len(h) for h in host] == [(3 + len(range(j, k, lanes))) if j < k else 1 for j in range(lanes)]
-            ev = sub.events_ms()
-            assert len(ev) == ran and ev[0][0] == 0.0 and all(b > a for a, b in ev)
-        finally:
-            sub.close()
-        for j, (pd, pt, t) in enumerate(cases):
-            got = [x.cpu().numpy() for x in t[2:]]
-            if j >= k:  # lane never ran: outputs untouched
-                assert (got[0] == -7).all() and (got[2] == -7).all()
-                continue
-            _assert_same(got, oracle.c_schedule_batch(u, nd, pd, pt), f"lane {j}")
-    finally:
-        for c in ctxs:
-            c.close()
+            got = [np.concatenate([t0[i].cpu().numpy(), t1[i].cpu().numpy()]) for i in (2, 3, 4)]
+            _assert_same(got, want, f"multi n={n} W={waves} norm={norm}")
+            _assert_same([out[i].cpu().numpy() for i in (2, 3, 4)], want, f"keys n={n} W={waves} norm={norm}")
+
+
+@pytest.mark.parametrize("kernel", ["wg", "slices"])
+def test_batch_kernel_ab(msh, oracle, kernel, monkeypatch):
+    """The default workgroup-table kernel and the round-2 slice kernel (MSH_BATCH_KERNEL=slices, an
+    A/B switch read once by msh_create) place identically at C3 size, multi-batch included."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_BATCH_KERNEL", kernel)
+    rng = np.random.default_rng(5)
+    u, nd, pd, pt = _rand_case(rng, 5000, 100_000, p_unsched=0.1, p_tol=0.05)
+    dev = torch.device("cuda:0")
+    with msh.DeviceContext(0) as ctx:
+        ctx.upload_nodes(u, nd)
+        want = oracle.c_schedule_batch(u, nd, pd, pt, threads=8)
+        _assert_same(ctx.schedule_batch(pd, pt), want, kernel)
+        ts = [_dev_batch(torch, dev, pd, pt) for _ in range(3)]
+        ctx.schedule_batches_device(ctx.batch_descs([_desc(t) for t in ts]),
+                                    stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for t in ts:
+            _assert_same([t[i].cpu().numpy() for i in (2, 3, 4)], want, f"{kernel} multi")
