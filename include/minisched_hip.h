@@ -164,6 +164,21 @@ int msh_patch_nodes(msh_ctx* ctx, int32_t count, const int32_t* idx, const uint8
 int msh_schedule_batch(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
                        int32_t* out_idx, int64_t* out_score, int32_t* out_status);
 
+/* Asynchronous host-buffer batch (ABI v5): msh_schedule_batch for page-locked buffers (msh_host_alloc
+ * or registered with HIP; pageable ones are MSH_ERR_INVALID) that returns once the batch is launched.
+ * The kernel reads the pod columns and writes the outputs over PCIe as in the synchronous call; they
+ * are valid once msh_wait(ctx, ticket) returns MSH_OK. A caller packs batch i + 1 (msh_pack_pods)
+ * while batch i runs, the pipeline a cgo caller draining activeQ batch after batch (minisched.go:28-34)
+ * runs. Batches of one ctx complete in submission order; at most MSH_ASYNC_DEPTH are in flight (a
+ * further submission first waits for the oldest). The caller must not touch a batch's buffers before
+ * its msh_wait. Tickets are positive and increase by one per call. */
+#define MSH_ASYNC_DEPTH 4
+int msh_schedule_batch_async(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                             int32_t* out_idx, int64_t* out_score, int32_t* out_status, uint64_t* out_ticket);
+/* Wait for batch `ticket` (and every earlier one) of msh_schedule_batch_async. A ticket the ctx
+ * never handed out is MSH_ERR_INVALID; an already completed one returns at once. */
+int msh_wait(msh_ctx* ctx, uint64_t ticket);
+
 /* Same, device-resident inputs/outputs, asynchronous on `stream` (hipStream_t).
  * Launches on different streams may overlap (independent batches pipelined): each needs its own
  * pod and output buffers. The ctx's node tables are read-only during batches; when an upload,

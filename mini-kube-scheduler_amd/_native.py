@@ -51,7 +51,8 @@ EXPORTED = (
     "msh_abi_version", "msh_device_count", "msh_host_alloc", "msh_host_free", "msh_create", "msh_destroy", "msh_last_error",
     "msh_set_plugins", "msh_set_plugins_ex", "msh_upload_nodes", "msh_num_nodes",
     "msh_patch_nodes", "msh_export_results",
-    "msh_schedule_batch", "msh_schedule_batch_device", "msh_schedule_batches_device", "msh_schedule_sequential",
+    "msh_schedule_batch", "msh_schedule_batch_async", "msh_wait", "msh_schedule_batch_device",
+    "msh_schedule_batches_device", "msh_schedule_sequential",
     "msh_schedule_sequential_device", "msh_node_pod_counts", "msh_reset_node_pod_counts",
     "msh_shard_keys_len", "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
     "msh_pack_nodes", "msh_pack_pods", "msh_toleration_tolerates_unschedulable",
@@ -76,6 +77,7 @@ class Batch(C.Structure):
 
 
 BATCHES_PER_LAUNCH = 8  # MSH_BATCHES_PER_LAUNCH
+ASYNC_DEPTH = 4  # MSH_ASYNC_DEPTH
 
 COMMIT_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.c_int64)
 
@@ -100,6 +102,8 @@ _SIGS = {
     "msh_schedule_batch": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P]),
     "msh_schedule_batch_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P]),
     "msh_schedule_batches_device": (C.c_int, [_P, _I32, _P, _P]),
+    "msh_schedule_batch_async": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, C.POINTER(C.c_uint64)]),
+    "msh_wait": (C.c_int, [_P, C.c_uint64]),
     "msh_schedule_sequential": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, COMMIT_CB, _P]),
     "msh_schedule_sequential_device": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, _P]),
     "msh_node_pod_counts": (C.c_int, [_P, _P]),

@@ -109,6 +109,10 @@ struct msh_ctx {
   // per caller stream, re-recorded after each launch on it. A table rewrite (upload, patch, plugin
   // change, count reset) makes the ctx's own stream wait for exactly these, never the whole device.
   std::vector<std::pair<hipStream_t, hipEvent_t>> inflight;
+  // msh_schedule_batch_async: a ring of MSH_ASYNC_DEPTH events on the ctx's stream; ticket t's event
+  // is async_ev[t % MSH_ASYNC_DEPTH]; every ticket <= async_done has completed
+  hipEvent_t async_ev[MSH_ASYNC_DEPTH] = {};
+  uint64_t async_issued = 0, async_done = 0;
   size_t patch_cap = 0;
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
   int32_t patch_pending = 0;              // entries in d_patch the next prepare() applies
@@ -412,6 +416,7 @@ int host_io_end(msh_ctx* c, int32_t p, int32_t* out_idx, int64_t* out_score, int
   } else {
     MSH_HIP(c, hipStreamSynchronize(c->stream));
   }
+  c->async_done = c->async_issued;  // the ctx's stream is drained: every async batch is done too
   if (io.staged) {
     const CopyJob jobs[3] = {{out_idx, io.h_idx, (size_t)p * sizeof(int32_t)},
                              {out_status, io.h_status, (size_t)p * sizeof(int32_t)},
@@ -549,6 +554,8 @@ void msh_destroy(msh_ctx* c) {
   wait_inflight(c);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& e : c->inflight) (void)hipEventDestroy(e.second);
+  for (hipEvent_t e : c->async_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   free_nodes(c);
   free_pods(c);
@@ -814,6 +821,57 @@ int msh_schedule_batch(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   rc = msh_schedule_batch_device(c, p, io.d_pd, io.d_pt, io.o_idx, io.o_score, io.o_status, c->stream);
   if (rc != MSH_OK) return rc;
   return host_io_end(c, p, out_idx, out_score, out_status, io);
+}
+
+int msh_schedule_batch_async(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                             int32_t* out_idx, int64_t* out_score, int32_t* out_status, uint64_t* out_ticket) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (!out_ticket) return fail(c, MSH_ERR_INVALID, "null ticket");
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  if (p > 0 && (!pod_digit || !pod_tol || !out_idx || !out_status))  // out_score optional
+    return fail(c, MSH_ERR_INVALID, "null host pointer");
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  DeviceGuard g(c->device);
+  void *dpd = nullptr, *dpt = nullptr, *doi = nullptr, *dos = nullptr, *dost = nullptr;
+  if (p > 0) {
+    dpd = pinned_device_ptr(pod_digit);
+    dpt = pinned_device_ptr(pod_tol);
+    doi = pinned_device_ptr(out_idx);
+    dos = out_score ? pinned_device_ptr(out_score) : nullptr;
+    dost = pinned_device_ptr(out_status);
+    if (!dpd || !dpt || !doi || !dost || (out_score && !dos))
+      return fail(c, MSH_ERR_INVALID, "msh_schedule_batch_async needs page-locked buffers (msh_host_alloc)");
+  }
+  int rc = prepare(c, c->stream);
+  if (rc != MSH_OK) return rc;
+  if (c->async_issued - c->async_done >= MSH_ASYNC_DEPTH) {  // the ring is full: wait for the oldest
+    const uint64_t t = c->async_done + 1;
+    MSH_HIP(c, hipEventSynchronize(c->async_ev[t % MSH_ASYNC_DEPTH]));
+    c->async_done = t;
+  }
+  hipEvent_t& ev = c->async_ev[(c->async_issued + 1) % MSH_ASYNC_DEPTH];
+  if (!ev) MSH_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  if (p > 0) {
+    rc = msh_schedule_batch_device(c, p, static_cast<const int8_t*>(dpd), static_cast<const uint8_t*>(dpt),
+                                   static_cast<int32_t*>(doi), static_cast<int64_t*>(dos), static_cast<int32_t*>(dost),
+                                   c->stream);
+    if (rc != MSH_OK) return rc;
+  }
+  MSH_HIP(c, hipEventRecord(ev, c->stream));
+  *out_ticket = ++c->async_issued;
+  return MSH_OK;
+}
+
+int msh_wait(msh_ctx* c, uint64_t ticket) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (ticket == 0 || ticket > c->async_issued) return fail(c, MSH_ERR_INVALID, "unknown ticket");
+  if (ticket <= c->async_done) return MSH_OK;
+  DeviceGuard g(c->device);
+  MSH_HIP(c, hipEventSynchronize(c->async_ev[ticket % MSH_ASYNC_DEPTH]));
+  c->async_done = ticket;  // in-order completion on the ctx's stream
+  return MSH_OK;
 }
 
 int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,

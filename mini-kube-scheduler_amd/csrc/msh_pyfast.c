@@ -183,7 +183,41 @@ static PyObject* py_schedule_batch_host(PyObject* self, PyObject* const* a, Py_s
   return PyLong_FromLong(rc);
 }
 
+/* schedule_batch_host_async(ctx, pod_digit, pod_tol, out_idx, out_score or None, out_status)
+ * -> (rc, ticket): msh_schedule_batch_async; the arrays must stay alive (and untouched) until
+ * wait(ctx, ticket) returns 0. */
+static PyObject* py_schedule_batch_host_async(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  void* ctx;
+  HostBufs h;
+  Py_ssize_t p;
+  if (want_args(n, 6, "schedule_batch_host_async") || as_ptr(a[0], &ctx) || get_host_bufs(a + 1, &h, &p))
+    return NULL;
+  uint64_t ticket = 0;
+  const int rc = msh_schedule_batch_async((msh_ctx*)ctx, (int32_t)p, (const int8_t*)h.pd.buf, (const uint8_t*)h.pt.buf,
+                                          (int32_t*)h.oi.buf, (int64_t*)h.os.buf, (int32_t*)h.ost.buf, &ticket);
+  release_bufs(&h);
+  return Py_BuildValue("(iK)", rc, (unsigned long long)ticket);
+}
+
+/* wait(ctx, ticket) -> rc: msh_wait, with the GIL released */
+static PyObject* py_wait(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  void* ctx;
+  if (want_args(n, 2, "wait") || as_ptr(a[0], &ctx)) return NULL;
+  const unsigned long long t = PyLong_AsUnsignedLongLong(a[1]);
+  if (PyErr_Occurred()) return NULL;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = msh_wait((msh_ctx*)ctx, (uint64_t)t);
+  Py_END_ALLOW_THREADS
+  return PyLong_FromLong(rc);
+}
+
 static PyMethodDef methods[] = {
+    {"schedule_batch_host_async", (PyCFunction)(void (*)(void))py_schedule_batch_host_async, METH_FASTCALL,
+     "msh_schedule_batch_async(ctx, pod_digit, pod_tol, out_idx, out_score, out_status) -> (rc, ticket)"},
+    {"wait", (PyCFunction)(void (*)(void))py_wait, METH_FASTCALL, "msh_wait(ctx, ticket) -> rc"},
     {"schedule_batches_device", (PyCFunction)(void (*)(void))py_schedule_batches_device, METH_FASTCALL,
      "msh_schedule_batches_device(ctx, nb, batches, stream) -> rc (batches: address of an msh_batch array)"},
     {"schedule_batch_host", (PyCFunction)(void (*)(void))py_schedule_batch_host, METH_FASTCALL,

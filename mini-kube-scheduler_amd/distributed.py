@@ -46,11 +46,33 @@ def decode_key(key: np.ndarray) -> np.ndarray:
     return np.where(k > 0, GKEY_MAX - k, -1).astype(np.int64)
 
 
-def merge_shard_keys_(keys, group=None):
-    """In-place element-wise MAX of per-shard keys over the process group (RCCL on GPU
-    tensors, gloo on CPU tensors). `keys` is the int32 tensor of msh_shard_keys_len entries."""
+def as_torch_stream(stream, device):
+    """A torch stream for `stream`: None -> the device's current stream, a torch.cuda.Stream as is,
+    an int (a hipStream_t handle, e.g. `Stream.cuda_stream`) wrapped as an ExternalStream."""
+    import torch
+    if stream is None or (isinstance(stream, int) and stream == 0):
+        return torch.cuda.current_stream(device)
+    if isinstance(stream, int):
+        return torch.cuda.ExternalStream(stream, device=device)
+    return stream
+
+
+def merge_shard_keys_(keys, group=None, stream=None):
+    """In-place element-wise MAX of per-shard keys over the process group (RCCL on GPU tensors,
+    gloo on CPU or GPU tensors). `keys` is the int32 tensor of msh_shard_keys_len entries.
+
+    For a GPU tensor the collective is issued with `stream` (the stream the keys were produced on and
+    the decode will run on; default: the current stream) as torch's current stream, so the process
+    group orders it after the keys kernel and the decode after it (ProcessGroupNCCL: its stream waits
+    on the current one, and the current one on the collective)."""
+    import torch
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        return keys
+    if keys.is_cuda:
+        with torch.cuda.stream(as_torch_stream(stream, keys.device)):
+            dist.all_reduce(keys, op=dist.ReduceOp.MAX, group=group)
+    else:
         dist.all_reduce(keys, op=dist.ReduceOp.MAX, group=group)
     return keys
 
@@ -79,16 +101,20 @@ class NodeShardedScheduler:
         self.group = group
         ctx.upload_nodes(np.ascontiguousarray(unsched[lo:hi]), np.ascontiguousarray(digit[lo:hi]))
 
-    def schedule(self, d_pod_digit, d_pod_tol, d_keys, d_idx, d_score, d_status, stream: int = 0) -> None:
+    def schedule(self, d_pod_digit, d_pod_tol, d_keys, d_idx, d_score, d_status, stream=None) -> None:
         """All tensors on this rank's GPU (d_keys: int32, >= ctx.shard_keys_len(p) entries);
-        every rank ends with the global decisions."""
+        every rank ends with the global decisions. `stream`: a torch.cuda.Stream or a hipStream_t
+        handle (default: the current stream); the keys kernel, the all-reduce and the decode are
+        ordered on it (the cross-shard selectHost, minisched.go:304-325)."""
         p = d_pod_digit.numel()
         klen = self.ctx.shard_keys_len(p)
+        s = as_torch_stream(stream, d_keys.device)
+        h = s.cuda_stream
         self.ctx.shard_keys_device(p, d_pod_digit.data_ptr(), d_pod_tol.data_ptr(), self.shard.lo,
-                                   d_keys.data_ptr(), stream)
-        merge_shard_keys_(d_keys[:klen], self.group)
+                                   d_keys.data_ptr(), h)
+        merge_shard_keys_(d_keys[:klen], self.group, s)
         self.ctx.decode_keys_device(p, d_pod_digit.data_ptr(), d_pod_tol.data_ptr(), d_keys.data_ptr(),
-                                    d_idx.data_ptr(), d_score.data_ptr(), d_status.data_ptr(), stream)
+                                    d_idx.data_ptr(), d_score.data_ptr(), d_status.data_ptr(), h)
 
 
 class PodShardedScheduler:

@@ -172,6 +172,23 @@ class DeviceContext:
             self._check(rc)
         return idx, score, status
 
+    def schedule_batch_async(self, pod_digit: np.ndarray, pod_tol: np.ndarray, out, scores: bool = True) -> int:
+        """msh_schedule_batch_async: page-locked columns and outputs (pinned_empty arrays) only; returns
+        the ticket. The outputs are valid after wait(ticket); keep every array alive and untouched
+        until then."""
+        p = _same_len("schedule_batch_async", pod_digit, pod_tol)
+        idx, score, status = self._outputs(p, out, scores)
+        rc, ticket = self._fast.schedule_batch_host_async(self._hv(), pod_digit, pod_tol, idx, score, status)
+        if rc:
+            self._check(rc)
+        return ticket
+
+    def wait(self, ticket: int) -> None:
+        """msh_wait: batch `ticket` of schedule_batch_async (and every earlier one) has completed."""
+        rc = self._fast.wait(self._hv(), int(ticket))
+        if rc:
+            self._check(rc)
+
     def schedule_sequential(self, pod_digit: np.ndarray, pod_tol: np.ndarray, max_pods_per_node: int = 0,
                             on_commit: Callable[[int, int, int], None] | None = None, out=None):
         pod_digit = np.ascontiguousarray(pod_digit, np.int8)

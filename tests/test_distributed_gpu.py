@@ -8,6 +8,9 @@ minisched/minisched.go:304-325), then msh_decode_keys_device decodes them on eve
 decisions must equal the oracle's over the whole table, in the identity (NONE) and the
 non-match (MINMAX) key layouts.
 
+The same again through NodeShardedScheduler.schedule on a busy non-default stream with the keys
+on the GPU (the stream-ordering of keys kernel -> all-reduce -> decode, as bench.py runs it).
+
 Pod sharding of sequential mode: each rank schedules its pod range one pod at a time against
 the full table, and PodShardedScheduler.merge_node_counts sums the per-node commit counts; with
 no capacity (the reference semantics) they must equal the oracle's serial loop over all pods.
@@ -77,6 +80,22 @@ def _worker(rank, world, port, seed, n, p, norm, out_q):
                                ost.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         node_sharded = (oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy())
+        # ---- the same through NodeShardedScheduler.schedule on a NON-default stream that is busy
+        # first (a long matmul queued on it), with the keys zeroed on the default stream: the keys
+        # kernel, the GPU-tensor all-reduce (gloo here, RCCL in bench.py) and the decode must all be
+        # ordered on `side`, or the merge reads the zeros / the decode reads unmerged keys
+        side = torch.cuda.Stream(dev)
+        keys2 = torch.zeros(klen, dtype=torch.int32, device=dev)
+        out2 = [torch.full((p,), -7, dtype=dt, device=dev) for dt in (torch.int32, torch.int64, torch.int32)]
+        a = torch.randn(3000, 3000, device=dev)
+        torch.cuda.synchronize()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(8):
+                a = a @ a / 3000.0
+        sched.schedule(d_pd, d_pt, keys2, *out2, stream=side)
+        torch.cuda.synchronize()
+        on_side = tuple(t.cpu().numpy() for t in out2)
         # ---- pod sharding of sequential mode: per-rank commits, counts summed over the ranks
         pod = D.PodShardedScheduler(ctx, u, nd, world, rank)
         lo, hi = pod.pod_range(p)
@@ -87,7 +106,7 @@ def _worker(rank, world, port, seed, n, p, norm, out_q):
         parts = [None] * world
         dist.all_gather_object(parts, (lo, [a.tolist() for a in seq]))
         if rank == 0:
-            out_q.put((node_sharded, counts.numpy(), sorted(parts, key=lambda x: x[0])))
+            out_q.put((node_sharded, on_side, counts.numpy(), sorted(parts, key=lambda x: x[0])))
         ctx.close()
     finally:
         dist.destroy_process_group()
@@ -104,7 +123,7 @@ def test_sharded_paths_across_processes(oracle, world, norm):
     for pr in procs:
         pr.start()
     try:
-        node_sharded, counts, parts = q.get(timeout=180)
+        node_sharded, on_side, counts, parts = q.get(timeout=180)
     finally:
         for pr in procs:
             pr.join(timeout=60)
@@ -112,8 +131,8 @@ def test_sharded_paths_across_processes(oracle, world, norm):
     u, nd, pd, pt = _case(seed, n, p)
     ps = oracle.PluginSet(weights=[2], normalize=[norm])
     wi, ws, wst, _ = oracle.c_schedule_batch(u, nd, pd, pt, ps)
-    gi, gs, gst = node_sharded
-    assert (gi == wi).all() and (gs == ws).all() and (gst == wst).all()
+    for gi, gs, gst in (node_sharded, on_side):
+        assert (gi == wi).all() and (gs == ws).all() and (gst == wst).all()
     # the pod-sharded sequential runs reassemble to the serial loop over all pods
     si, ss, sst, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, 0)
     seq_idx = np.concatenate([np.array(x[1][0], np.int64) for x in parts])

@@ -675,6 +675,49 @@ def test_host_buffer_paths(msh, gpu_ctx, oracle, synth, norm):
     assert (outs[0][20_000:] == -7).all()  # nothing written past p
 
 
+def test_async_host_batches(msh, gpu_ctx, oracle):
+    """msh_schedule_batch_async + msh_wait (ABI v5): six batches in page-locked buffers submitted
+    back to back (the fifth and sixth wait for the ring's oldest: MSH_ASYNC_DEPTH = 4), waited
+    out of order; every batch bit-exact vs the oracle. Pageable buffers are rejected, an unknown
+    ticket is MSH_ERR_INVALID, an empty batch gets a ticket, and a synchronous call completes all."""
+    rng = np.random.default_rng(606)
+    ps = oracle.PluginSet()
+    _set(gpu_ctx, msh, ps)
+    u, nd, _, _ = _rand_case(rng, 5000, 1, p_unsched=0.2)
+    gpu_ctx.upload_nodes(u, nd)
+    sets = []
+    for k in range(6):
+        _, _, pd, pt = _rand_case(rng, 1, [100_000, 1, 64, 4097, 99_999, 0][k], p_tol=0.1)
+        hpd, hpt = msh.pinned_empty(len(pd), np.int8), msh.pinned_empty(len(pd), np.uint8)
+        hpd[:], hpt[:] = pd, pt
+        outs = (msh.pinned_empty(len(pd), np.int32), msh.pinned_empty(len(pd), np.int64),
+                msh.pinned_empty(len(pd), np.int32))
+        for o in outs:
+            o.fill(-7)
+        sets.append((pd, pt, hpd, hpt, outs))
+    tickets = [gpu_ctx.schedule_batch_async(hpd, hpt, outs) for _, _, hpd, hpt, outs in sets]
+    assert tickets == list(range(tickets[0], tickets[0] + 6))
+    for k in (3, 0, 5, 1, 4, 2):
+        gpu_ctx.wait(tickets[k])
+        pd, pt, _, _, outs = sets[k]
+        _assert_same(outs, oracle.c_schedule_batch(u, nd, pd, pt, ps), f"async batch {k}")
+    with pytest.raises(msh.MshError):
+        gpu_ctx.wait(tickets[-1] + 1)
+    with pytest.raises(msh.MshError):
+        gpu_ctx.wait(0)
+    pd, pt = sets[0][0], sets[0][1]
+    with pytest.raises(msh.MshError):  # pageable buffers
+        gpu_ctx.schedule_batch_async(pd, pt, (np.empty(len(pd), np.int32), np.empty(len(pd), np.int64),
+                                              np.empty(len(pd), np.int32)))
+    _, _, hpd, hpt, outs = sets[3]
+    t = gpu_ctx.schedule_batch_async(hpd, hpt, outs, scores=False)  # out_score = NULL
+    gpu_ctx.schedule_batch(sets[0][0], sets[0][1])  # a synchronous call drains the ctx's stream
+    gpu_ctx.wait(t)  # already complete
+    pd3, pt3 = sets[3][0], sets[3][1]
+    want = oracle.c_schedule_batch(u, nd, pd3, pt3, ps)
+    assert (outs[0] == want[0]).all() and (outs[2] == want[2]).all()
+
+
 def _dev_batch(torch, dev, pd, pt, scores=True):
     return [torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev),
             torch.full((len(pd),), -7, dtype=torch.int32, device=dev),
