@@ -66,7 +66,16 @@ typedef enum msh_status {
 /* ---- device plugin ids (framework.Plugin.Name() -> id) ---- */
 typedef enum msh_plugin_id {
   MSH_PLUGIN_NODE_UNSCHEDULABLE = 1, /* "NodeUnschedulable" (Filter) */
-  MSH_PLUGIN_NODE_NUMBER = 2         /* "NodeNumber" (PreScore, Score) */
+  MSH_PLUGIN_NODE_NUMBER = 2,        /* "NodeNumber" (PreScore, Score) */
+  /* Score-column plugins (ABI v5, build extension): a score plugin whose Score(pod, node) is an
+   * int64 the host computed per node (msh_upload_score_column), e.g. a node-only scorer evaluated
+   * once per snapshot. Score lists with one of these run on the generic pipeline (an explicit
+   * int64 score per pair, per-plugin NormalizeScore over the feasible list, weights, first max);
+   * the batch entry points only (shard keys, sequential mode and the export: MSH_ERR_UNSUPPORTED). */
+  MSH_PLUGIN_SCORE_COLUMN0 = 16,
+  MSH_PLUGIN_SCORE_COLUMN1 = 17,
+  MSH_PLUGIN_SCORE_COLUMN2 = 18,
+  MSH_PLUGIN_SCORE_COLUMN3 = 19
 } msh_plugin_id;
 
 /* ---- per-score-plugin normalize stage ----
@@ -130,6 +139,12 @@ int msh_set_plugins_ex(msh_ctx* ctx, const int32_t* filter_ids, int32_t nf,
  * 0 <= n < 2^24. Replaces the per-cycle Nodes().List (minisched.go:40). */
 int msh_upload_nodes(msh_ctx* ctx, int32_t n, const uint8_t* unsched, const int8_t* digit);
 int msh_num_nodes(const msh_ctx* ctx, int32_t* out_n);
+
+/* The per-node scores of score-column plugin `plugin_id` (MSH_PLUGIN_SCORE_COLUMN0..3), n = the
+ * uploaded node count, List order, each in [-2^31, 2^31]. An msh_upload_nodes drops every column
+ * (its nodes are gone); a batch whose score list names a column not uploaded since is
+ * MSH_ERR_STATE. Totals are Go int64 arithmetic: weight x normalized score summed with wrap-around. */
+int msh_upload_score_column(msh_ctx* ctx, int32_t plugin_id, int32_t n, const int64_t* scores);
 
 /* Per-pair plugin results for a small batch: the matrices the simulator's result store
  * turns into pod annotations (scheduler/plugin/resultstore/store.go:170-234, recorded by the

@@ -9,7 +9,7 @@ a Python identifier).
 """
 from . import _native
 from ._native import MshError, device_count
-from .framework import (MAX_NODE_SCORE, NODE_NUMBER, NODE_UNSCHEDULABLE, Code, NodeScore, Normalize,
+from .framework import (MAX_NODE_SCORE, NODE_NUMBER, NODE_UNSCHEDULABLE, SCORE_COLUMNS, Code, NodeScore, Normalize,
                         Outcome, ScheduleResult)
 from .scheduler import DeviceContext, Scheduler, ScorePluginConfig, pinned_empty
 from .snapshot import NodeTable, PodTable, pack_nodes, pack_pods

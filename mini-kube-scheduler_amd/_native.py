@@ -38,6 +38,7 @@ MSH_SCORE_ERROR = 2
 
 MSH_PLUGIN_NODE_UNSCHEDULABLE = 1
 MSH_PLUGIN_NODE_NUMBER = 2
+MSH_PLUGIN_SCORE_COLUMN0 = 16  # .. 19: score-column plugins (generic pipeline)
 
 MSH_EXPORT_NONE = -(1 << 63)  # msh_export_results: no score recorded
 
@@ -49,7 +50,7 @@ MSH_NORMALIZE_MINMAX = 3
 # Every symbol include/minisched_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "msh_abi_version", "msh_device_count", "msh_host_alloc", "msh_host_free", "msh_create", "msh_destroy", "msh_last_error",
-    "msh_set_plugins", "msh_set_plugins_ex", "msh_upload_nodes", "msh_num_nodes",
+    "msh_set_plugins", "msh_set_plugins_ex", "msh_upload_nodes", "msh_upload_score_column", "msh_num_nodes",
     "msh_patch_nodes", "msh_export_results",
     "msh_schedule_batch", "msh_schedule_batch_async", "msh_wait", "msh_schedule_batch_device",
     "msh_schedule_batches_device", "msh_schedule_sequential",
@@ -97,6 +98,7 @@ _SIGS = {
     "msh_set_plugins_ex": (C.c_int, [_P, _P, _I32, _P, _I32, _P, _P, _P, _I32]),
     "msh_upload_nodes": (C.c_int, [_P, _I32, _P, _P]),
     "msh_num_nodes": (C.c_int, [_P, C.POINTER(_I32)]),
+    "msh_upload_score_column": (C.c_int, [_P, _I32, _I32, _P]),
     "msh_patch_nodes": (C.c_int, [_P, _I32, _P, _P, _P]),
     "msh_export_results": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P]),
     "msh_schedule_batch": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P]),

@@ -94,6 +94,10 @@ struct msh_ctx {
   uint32_t* d_ball = nullptr;    // [0..1] first feasible node per pod class, as keys
   int32_t* d_counts = nullptr;
   size_t node_cap = 0;
+  // score-column plugins (generic pipeline): GEN_COLS x node_cap int64, column k valid when col_ok[k]
+  int64_t* d_cols = nullptr;
+  bool col_ok[msh::GEN_COLS] = {};
+  bool generic = false;  // the score list names a score-column plugin
 
   // host-path buffers
   size_t pod_cap = 0;
@@ -138,6 +142,9 @@ int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
   } while (0)
 
 void free_nodes(msh_ctx* c) {
+  (void)hipFree(c->d_cols);
+  c->d_cols = nullptr;
+  for (bool& ok : c->col_ok) ok = false;
   (void)hipFree(c->d_unsched);
   (void)hipFree(c->d_digit);
   (void)hipFree(c->d_planes);
@@ -238,12 +245,16 @@ bool contains(const std::vector<int32_t>& v, int32_t id) {
   return std::find(v.begin(), v.end(), id) != v.end();
 }
 
-int check_ids(msh_ctx* c, const int32_t* ids, int32_t n, bool filter, const char* what) {
+bool is_column(int32_t id) { return id >= MSH_PLUGIN_SCORE_COLUMN0 && id < MSH_PLUGIN_SCORE_COLUMN0 + msh::GEN_COLS; }
+
+// kind: 0 filter list, 1 prescore list, 2 score list
+int check_ids(msh_ctx* c, const int32_t* ids, int32_t n, int kind, const char* what) {
   if (n < 0 || n > 8) return fail(c, MSH_ERR_INVALID, std::string(what) + ": bad list length");
   if (n > 0 && !ids) return fail(c, MSH_ERR_INVALID, std::string(what) + ": null list");
   for (int32_t i = 0; i < n; i++) {
     const int32_t id = ids[i];
-    const bool ok = filter ? id == MSH_PLUGIN_NODE_UNSCHEDULABLE : id == MSH_PLUGIN_NODE_NUMBER;
+    const bool ok = kind == 0 ? id == MSH_PLUGIN_NODE_UNSCHEDULABLE
+                              : (id == MSH_PLUGIN_NODE_NUMBER || (kind == 2 && is_column(id)));
     if (!ok)
       return fail(c, MSH_ERR_UNSUPPORTED,
                   std::string(what) + ": plugin id " + std::to_string(id) + " has no device implementation");
@@ -314,6 +325,49 @@ msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t
   a.ball = c->d_ball;
   a.pp = c->pp;
   return a;
+}
+
+// The generic pipeline runs the batch entry points when the score list names a score column (or
+// for every list with MSH_BATCH_KERNEL=generic, an A/B switch).
+bool use_generic(const msh_ctx* c) { return c->generic || c->dev.batch_kernel == 2; }
+
+int generic_args(msh_ctx* c, msh::GenericArgs& g) {
+  g = msh::GenericArgs{};
+  g.unsched = c->d_unsched;
+  g.digit = c->d_digit;
+  g.cols = c->d_cols;
+  g.col_stride = (int64_t)c->node_cap;
+  g.n_nodes = c->n_nodes;
+  g.has_nu = c->pp.has_nu_filter;
+  g.nn_prescore = c->pp.nn_prescore;
+  g.nn_score = c->pp.has_nn_score;
+  g.ns = (int32_t)c->score_ids.size();
+  for (int32_t k = 0; k < g.ns; ++k) {
+    const int32_t id = c->score_ids[k];
+    g.kind[k] = id == MSH_PLUGIN_NODE_NUMBER ? 0 : 1 + (id - MSH_PLUGIN_SCORE_COLUMN0);
+    if (g.kind[k] > 0 && !c->col_ok[g.kind[k] - 1])
+      return fail(c, MSH_ERR_STATE, "score column " + std::to_string(id) + " not uploaded since the last node upload");
+    g.mode[k] = c->normalize[k];
+    g.weight[k] = c->weights[k];
+    g.need_ext = g.need_ext || g.mode[k] != MSH_NORMALIZE_NONE;
+  }
+  return MSH_OK;
+}
+
+int launch_generic_batch(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t* pt, int32_t* oi, int64_t* os,
+                         int32_t* ost, hipStream_t s) {
+  msh::GenericArgs g;
+  int rc = generic_args(c, g);
+  if (rc != MSH_OK) return rc;
+  g.pod_digit = pd;
+  g.pod_tol = pt;
+  g.n_pods = p;
+  g.out_idx = oi;
+  g.out_score = os;
+  g.out_status = ost;
+  hipError_t e = msh::launch_generic(g, s);
+  if (e != hipSuccess) return hip_fail(c, e, "generic_kernel");
+  return MSH_OK;
 }
 
 // The ctx's device current for the call, the caller's restored after it (no switch at all in the
@@ -574,9 +628,9 @@ int msh_set_plugins_ex(msh_ctx* c, const int32_t* filter_ids, int32_t nf,
   if (!c) return MSH_ERR_INVALID;
   c->err.clear();
   int rc;
-  if ((rc = check_ids(c, filter_ids, nf, true, "filter")) != MSH_OK) return rc;
-  if ((rc = check_ids(c, prescore_ids, npre, false, "prescore")) != MSH_OK) return rc;
-  if ((rc = check_ids(c, score_ids, ns, false, "score")) != MSH_OK) return rc;
+  if ((rc = check_ids(c, filter_ids, nf, 0, "filter")) != MSH_OK) return rc;
+  if ((rc = check_ids(c, prescore_ids, npre, 1, "prescore")) != MSH_OK) return rc;
+  if ((rc = check_ids(c, score_ids, ns, 2, "score")) != MSH_OK) return rc;
   for (int32_t i = 0; i < ns; i++) {
     const int64_t w = weights ? weights[i] : 1;
     if (w < 1 || w > (int64_t(1) << 32)) return fail(c, MSH_ERR_INVALID, "score weight outside [1, 2^32]");
@@ -607,6 +661,8 @@ int msh_set_plugins_ex(msh_ctx* c, const int32_t* filter_ids, int32_t nf,
   }
   if (pp.has_nu_filter != c->pp.has_nu_filter) c->dirty = true;
   c->pp = pp;
+  c->generic = false;
+  for (int32_t i = 0; i < ns; i++) c->generic = c->generic || is_column(c->score_ids[i]);
   return MSH_OK;
 }
 
@@ -651,6 +707,7 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
     MSH_HIP(c, hipMemcpyAsync(c->d_digit, digit, (size_t)n, hipMemcpyHostToDevice, c->stream));
   }
   MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->node_cap * sizeof(int32_t), c->stream));
+  for (bool& ok : c->col_ok) ok = false;  // score columns belong to the previous table's nodes
   c->n_nodes = n;
   c->n_pad = n_pad;
   c->have_nodes = true;
@@ -704,6 +761,7 @@ int msh_export_results(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
   const size_t pairs = (size_t)p * (size_t)c->n_nodes;
   if (pairs > ((size_t)1 << 28)) return fail(c, MSH_ERR_UNSUPPORTED, "export limited to p*n <= 2^28 pairs");
+  if (c->generic) return fail(c, MSH_ERR_UNSUPPORTED, "score-column plugins run on the batch entry points only");
   if (pairs == 0) return MSH_OK;
   if (!pod_digit || !pod_tol || !out_filter || !out_score || !out_final)
     return fail(c, MSH_ERR_INVALID, "null pointer");
@@ -739,6 +797,29 @@ int msh_export_results(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   return rc;
 }
 
+int msh_upload_score_column(msh_ctx* c, int32_t plugin_id, int32_t n, const int64_t* scores) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (!is_column(plugin_id)) return fail(c, MSH_ERR_INVALID, "not a score-column plugin id");
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
+  if (n != c->n_nodes) return fail(c, MSH_ERR_INVALID, "a score column has one entry per uploaded node");
+  if (n > 0 && !scores) return fail(c, MSH_ERR_INVALID, "null scores");
+  for (int32_t i = 0; i < n; ++i)
+    if (scores[i] < -(int64_t(1) << 31) || scores[i] > (int64_t(1) << 31))
+      return fail(c, MSH_ERR_INVALID, "score column value outside [-2^31, 2^31] at node " + std::to_string(i));
+  DeviceGuard g(c->device);
+  int rc = after_inflight(c);  // generic launches of this ctx in flight may read the column
+  if (rc != MSH_OK) return rc;
+  if (!c->d_cols) MSH_HIP(c, hipMalloc(&c->d_cols, (size_t)msh::GEN_COLS * c->node_cap * sizeof(int64_t)));
+  const int k = plugin_id - MSH_PLUGIN_SCORE_COLUMN0;
+  if (n > 0)
+    MSH_HIP(c, hipMemcpyAsync(c->d_cols + (size_t)k * c->node_cap, scores, (size_t)n * sizeof(int64_t),
+                              hipMemcpyHostToDevice, c->stream));
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  c->col_ok[k] = true;
+  return MSH_OK;
+}
+
 int msh_num_nodes(const msh_ctx* c, int32_t* out_n) {
   if (!c || !out_n) return MSH_ERR_INVALID;
   *out_n = c->have_nodes ? c->n_nodes : 0;
@@ -757,6 +838,12 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = prepare(c, s);
   if (rc != MSH_OK) return rc;
+  if (use_generic(c)) {
+    if (p == 0) return MSH_OK;
+    if ((rc = launch_generic_batch(c, p, d_pod_digit, d_pod_tol, d_out_idx, d_out_score, d_out_status, s)) != MSH_OK)
+      return rc;
+    return track_launch(c, s);
+  }
   msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
   a.out_idx = d_out_idx;
   a.out_score = d_out_score;
@@ -781,6 +868,15 @@ int msh_schedule_batches_device(msh_ctx* c, int32_t nb, const msh_batch* batches
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = prepare(c, s);
   if (rc != MSH_OK) return rc;
+  if (use_generic(c)) {  // one generic launch per batch
+    for (int32_t i = 0; i < nb; ++i) {
+      const msh_batch& b = batches[i];
+      if (b.p > 0 &&
+          (rc = launch_generic_batch(c, b.p, b.pod_digit, b.pod_tol, b.out_idx, b.out_score, b.out_status, s)) != MSH_OK)
+        return rc;
+    }
+    return nb > 0 ? track_launch(c, s) : MSH_OK;
+  }
   const bool single = c->dev.batch_kernel == 1 || (msh::needs_kx(c->pp) && c->dev.kx_bits);  // A/B kernels
   for (int32_t i0 = 0; i0 < nb; i0 += msh::MULTI_MAX) {
     const int n = std::min<int32_t>(msh::MULTI_MAX, nb - i0);
@@ -883,6 +979,7 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   if (p < 0 || max_pods_per_node < 0) return fail(c, MSH_ERR_INVALID, "negative argument");
   if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_out_idx || !d_out_status))  // d_out_score optional
     return fail(c, MSH_ERR_INVALID, "null device pointer");
+  if (c->generic) return fail(c, MSH_ERR_UNSUPPORTED, "score-column plugins run on the batch entry points only");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = prepare(c, s);
@@ -984,6 +1081,7 @@ int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   if (p < 0 || node_base < 0) return fail(c, MSH_ERR_INVALID, "negative argument");
   if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_keys)) return fail(c, MSH_ERR_INVALID, "null device pointer");
   if (node_base + (int64_t)c->n_nodes >= msh::GKEY_MAX) return fail(c, MSH_ERR_INVALID, "global node index overflows the key");
+  if (c->generic) return fail(c, MSH_ERR_UNSUPPORTED, "score-column plugins run on the batch entry points only");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = prepare(c, s);

@@ -46,7 +46,8 @@ struct DeviceInfo {
   int host_io_dma = 0;
   int host_io_zc_in = 1;
   int host_sync_poll = 0;  // A/B only (MSH_HOST_SYNC=poll): poll an event instead of hipStreamSynchronize
-  int batch_kernel = 0;    // 0 = wg_kernel (default), 1 = the round-2 slice kernel rows_kernel (MSH_BATCH_KERNEL=slices, A/B)
+  int batch_kernel = 0;    // 0 = wg_kernel (default), 1 = the round-2 slice kernel rows_kernel (MSH_BATCH_KERNEL=slices,
+                           // A/B), 2 = generic_kernel for every plugin list (MSH_BATCH_KERNEL=generic, A/B)
   int wg_waves = 0;        // A/B only (MSH_WG_WAVES=1|2|4|8): waves per workgroup of wg_kernel, 0 = auto
 };
 
@@ -149,6 +150,32 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
                               const int32_t* keys, int32_t slot1_any, PluginParams pp,
                               int32_t* out_idx, int64_t* out_score, int32_t* out_status,
                               hipStream_t s);
+
+// ---- generic score pipeline (any score plugin list; generic_kernel) ----
+constexpr int GEN_MAX_SCORE = 5;  // score plugins per list: NodeNumber + up to four score columns
+constexpr int GEN_COLS = 4;       // score-column plugins MSH_PLUGIN_SCORE_COLUMN0..3
+struct GenericArgs {
+  const uint8_t* unsched;  // the uploaded columns, List order
+  const int8_t* digit;
+  const int64_t* cols;     // GEN_COLS x col_stride int64: column k at cols + k * col_stride
+  int64_t col_stride;
+  int32_t n_nodes;
+  int32_t has_nu;          // NodeUnschedulable in the filter list
+  int32_t nn_prescore;     // NodeNumber in the prescore list
+  int32_t nn_score;        // NodeNumber in the score list
+  int32_t ns;              // score plugins
+  int32_t need_ext;        // some plugin normalizes: the extent pass runs
+  int32_t kind[GEN_MAX_SCORE];   // 0 = NodeNumber, 1 + k = score column k
+  int32_t mode[GEN_MAX_SCORE];   // msh_normalize
+  int64_t weight[GEN_MAX_SCORE];
+  const int8_t* pod_digit;
+  const uint8_t* pod_tol;
+  int32_t n_pods;
+  int32_t* out_idx;
+  int64_t* out_score;      // may be null
+  int32_t* out_status;
+};
+hipError_t launch_generic(const GenericArgs& a, hipStream_t s);
 
 struct SeqArgs {
   const uint32_t* planes;    // bit-sliced node table (PLANE_* layout)

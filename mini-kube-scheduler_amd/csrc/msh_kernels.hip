@@ -933,6 +933,220 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Generic score pipeline: any score plugin list (NodeNumber and up to four score-column plugins,
+// MSH_PLUGIN_SCORE_COLUMN0..3), with the int64 score of every (pod, node) pair computed
+// explicitly. The bitmap kernels above are exact only because NodeNumber's raw score takes two
+// values; this kernel is the general form of RunScorePlugins (minisched.go:164-199), north_star's
+// stages one to one:
+//   5. node-table tiles: GEN_TILE nodes (the raw columns and the score columns in use) staged in
+//      LDS once per workgroup and reused by its GEN_PB pods;
+//   1. feasibility: one node per lane, NodeUnschedulable per pair; the wave's ballot is the
+//      feasibility bitmask of its 64 nodes (the feasible count comes from its popcount);
+//   3. per-pod extent of every score plugin over the feasible nodes (a pass of its own, only
+//      when some plugin normalizes): per-lane max / min, a wave-shuffle reduction, then an LDS
+//      reduction across the waves (64-bit LDS atomics);
+//   2. the int64 total of each pair: sum over plugins of weight x NormalizeScore(raw) (upstream
+//      helper.DefaultNormalizeScore, reverse, or min-max), in Go int64 arithmetic (wrapping);
+//   4. selectHost: per lane the first maximum of its nodes (they ascend), then a wave-shuffle
+//      argmax on (total desc, index asc) and a cross-wave merge in LDS.
+// One workgroup of GEN_THREADS lanes per GEN_PB pods; lanes take nodes i = tid + k * GEN_THREADS
+// of each tile. Status as the reference routes it: FitError when no node is feasible, the
+// NodeNumber score error (no PreScore state) when some node is.
+// ---------------------------------------------------------------------------------------
+constexpr int GEN_PB = 8;           // pods per workgroup
+constexpr int GEN_TILE = 1024;      // nodes per staged tile (2 KiB + 8 KiB per score column in use)
+constexpr int GEN_THREADS = 256;
+constexpr int GEN_WAVES = GEN_THREADS / WAVE;
+constexpr uint8_t GEN_PAD = 2;      // s_un value of a slot past the table
+
+__device__ __forceinline__ int64_t shfl_xor64(int64_t v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)(uint64_t)v, m), hi = __shfl_xor((int)((uint64_t)v >> 32), m);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+
+// NormalizeScore of one raw score given the pod's extent of that plugin over its feasible nodes
+// (mx, mn): upstream helper.DefaultNormalizeScore(MaxNodeScore = 100, reverse) — maxCount starts at
+// 0, an all-zero list is left alone (reverse: all 100) — or min-max (0 when max == min).
+__device__ __forceinline__ int64_t gen_normalize(int64_t raw, int32_t mode, int64_t mx, int64_t mn) {
+  switch (mode) {
+    case 1: {
+      const int64_t m = mx > 0 ? mx : 0;
+      return m == 0 ? raw : 100 * raw / m;
+    }
+    case 2: {
+      const int64_t m = mx > 0 ? mx : 0;
+      return m == 0 ? 100 : 100 - 100 * raw / m;
+    }
+    case 3: return mx == mn ? 0 : (raw - mn) * 100 / (mx - mn);
+    default: return raw;
+  }
+}
+
+__global__ __launch_bounds__(GEN_THREADS) void generic_kernel(GenericArgs a) {
+  __shared__ uint8_t s_un[GEN_TILE];
+  __shared__ int8_t s_dg[GEN_TILE];
+  __shared__ int64_t s_col[GEN_COLS][GEN_TILE];
+  __shared__ int64_t s_max[GEN_PB][GEN_MAX_SCORE], s_min[GEN_PB][GEN_MAX_SCORE];
+  __shared__ int64_t s_btot[GEN_PB][GEN_WAVES];
+  __shared__ int32_t s_bidx[GEN_PB][GEN_WAVES];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int32_t j0 = (int32_t)blockIdx.x * GEN_PB;
+  const int npb = min(GEN_PB, a.n_pods - j0);
+  // the score columns the plugin list reads (a mask over GEN_COLS)
+  int colmask = 0;
+  for (int s = 0; s < a.ns; ++s)
+    if (a.kind[s] > 0) colmask |= 1 << (a.kind[s] - 1);
+  if (tid < GEN_PB * GEN_MAX_SCORE) {
+    (&s_max[0][0])[tid] = INT64_MIN;
+    (&s_min[0][0])[tid] = INT64_MAX;
+  }
+  if (tid < GEN_PB * GEN_WAVES) {
+    (&s_btot[0][0])[tid] = 0;
+    (&s_bidx[0][0])[tid] = -1;
+  }
+  const int32_t n_tiles = (a.n_nodes + GEN_TILE - 1) / GEN_TILE;
+  constexpr int NPT = GEN_TILE / GEN_THREADS;  // nodes per lane and tile
+  for (int sweep = a.need_ext ? 0 : 1; sweep < 2; ++sweep) {
+    for (int32_t t = 0; t < n_tiles; ++t) {
+      __syncthreads();  // the previous tile (or sweep) is done with the staged columns
+      const int32_t base = t * GEN_TILE;
+      for (int i = tid; i < GEN_TILE; i += GEN_THREADS) {  // coalesced copies of the tile
+        const int32_t node = base + i;
+        const bool v = node < a.n_nodes;
+        s_un[i] = v ? (a.unsched[node] ? 1 : 0) : GEN_PAD;
+        s_dg[i] = v ? a.digit[node] : (int8_t)-1;
+#pragma unroll
+        for (int k = 0; k < GEN_COLS; ++k)
+          if (colmask & (1 << k)) s_col[k][i] = v ? a.cols[k * a.col_stride + node] : 0;
+      }
+      __syncthreads();
+      for (int q = 0; q < npb; ++q) {
+        const int pd = a.pod_digit[j0 + q];
+        const bool tol = a.pod_tol[j0 + q] != 0;
+        const bool pd_ok = pd >= 0 && pd <= 9;
+        // raw score of plugin s at staged node i (NodeNumber: 10 on a suffix-digit match)
+        auto raw = [&](int s, int i) -> int64_t {
+          const int kd = a.kind[s];
+          if (kd == 0) return (pd_ok && s_dg[i] == pd) ? 10 : 0;
+          return s_col[kd - 1][i];
+        };
+        if (sweep == 0) {  // ---- stage 3: the extent of every score plugin over the feasible nodes
+          int64_t lmx[GEN_MAX_SCORE], lmn[GEN_MAX_SCORE];
+#pragma unroll
+          for (int s = 0; s < GEN_MAX_SCORE; ++s) {
+            lmx[s] = INT64_MIN;
+            lmn[s] = INT64_MAX;
+          }
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) {
+            const int i = tid + k * GEN_THREADS;
+            const uint8_t u = s_un[i];
+            const bool feas = u != GEN_PAD && !(a.has_nu && u && !tol);  // stage 1: NodeUnschedulable
+            if (feas)
+#pragma unroll
+              for (int s = 0; s < GEN_MAX_SCORE; ++s)
+                if (s < a.ns) {
+                  const int64_t r = raw(s, i);
+                  lmx[s] = r > lmx[s] ? r : lmx[s];
+                  lmn[s] = r < lmn[s] ? r : lmn[s];
+                }
+          }
+#pragma unroll
+          for (int s = 0; s < GEN_MAX_SCORE; ++s) {
+            if (s >= a.ns) break;
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) {  // wave-shuffle reduction
+              const int64_t ox = shfl_xor64(lmx[s], m), on = shfl_xor64(lmn[s], m);
+              lmx[s] = ox > lmx[s] ? ox : lmx[s];
+              lmn[s] = on < lmn[s] ? on : lmn[s];
+            }
+            if (lane == 0 && lmx[s] != INT64_MIN) {  // LDS reduction across the waves
+              atomicMax((long long*)&s_max[q][s], (long long)lmx[s]);
+              atomicMin((long long*)&s_min[q][s], (long long)lmn[s]);
+            }
+          }
+        } else {  // ---- stages 1, 2, 4: feasibility, the weighted int64 total, the first maximum
+          int64_t mx[GEN_MAX_SCORE], mn[GEN_MAX_SCORE];
+#pragma unroll
+          for (int s = 0; s < GEN_MAX_SCORE; ++s) {
+            mx[s] = s_max[q][s];
+            mn[s] = s_min[q][s];
+          }
+          int64_t btot = 0;
+          int32_t bidx = -1;
+          uint64_t fmask = 0;  // this wave's feasibility bitmask (stage 1), one tile slice at a time
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) {
+            const int i = tid + k * GEN_THREADS;
+            const uint8_t u = s_un[i];
+            const bool feas = u != GEN_PAD && !(a.has_nu && u && !tol);
+            fmask |= __ballot(feas);
+            if (feas) {
+              uint64_t tot = 0;  // Go int64: wrapping
+#pragma unroll
+              for (int s = 0; s < GEN_MAX_SCORE; ++s)
+                if (s < a.ns) tot += (uint64_t)gen_normalize(raw(s, i), a.mode[s], mx[s], mn[s]) * (uint64_t)a.weight[s];
+              const int64_t ts = (int64_t)tot;
+              if (bidx < 0 || ts > btot) {  // nodes ascend per lane: the first maximum
+                btot = ts;
+                bidx = base + i;
+              }
+            }
+          }
+          if (fmask) {  // some node of this wave's slice is feasible for pod q
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) {  // wave-shuffle argmax: total desc, index asc
+              const int64_t ot = shfl_xor64(btot, m);
+              const int32_t oi = __shfl_xor(bidx, m);
+              const bool take = oi >= 0 && (bidx < 0 || ot > btot || (ot == btot && oi < bidx));
+              btot = take ? ot : btot;
+              bidx = take ? oi : bidx;
+            }
+            if (lane == 0) {  // this wave's running best across tiles (tiles ascend)
+              const int32_t ci = s_bidx[q][wv];
+              if (ci < 0 || btot > s_btot[q][wv]) {
+                s_btot[q][wv] = btot;
+                s_bidx[q][wv] = bidx;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < npb) {  // merge the waves' bests (LDS), decode, write
+    const int q = tid, j = j0 + q;
+    int64_t bt = 0;
+    int32_t bi = -1;
+#pragma unroll
+    for (int w = 0; w < GEN_WAVES; ++w) {
+      const int32_t oi = s_bidx[q][w];
+      const int64_t ot = s_btot[q][w];
+      if (oi >= 0 && (bi < 0 || ot > bt || (ot == bt && oi < bi))) {
+        bt = ot;
+        bi = oi;
+      }
+    }
+    const int pd = a.pod_digit[j];
+    const bool pd_ok = pd >= 0 && pd <= 9;
+    int32_t st = 0;
+    if (bi < 0) st = 1;                                           // FitError (minisched.go:143-148)
+    else if (a.nn_score && (!a.nn_prescore || !pd_ok)) st = 2;    // NodeNumber.Score error (nodenumber.go:74-77)
+    a.out_idx[j] = st ? -1 : bi;
+    if (a.out_score) a.out_score[j] = st ? 0 : bt;
+    a.out_status[j] = st;
+  }
+}
+
+hipError_t launch_generic(const GenericArgs& a, hipStream_t s) {
+  if (a.n_pods <= 0) return hipSuccess;
+  hipLaunchKernelGGL(generic_kernel, dim3((unsigned)((a.n_pods + GEN_PB - 1) / GEN_PB)), dim3(GEN_THREADS), 0, s, a);
+  return hipGetLastError();
+}
+
 // Decode globally merged shard keys (after an element-wise MAX across node shards).
 __global__ __launch_bounds__(256) void decode_keys_kernel(const int8_t* __restrict__ pod_digit,
                                                           const uint8_t* __restrict__ pod_tol,

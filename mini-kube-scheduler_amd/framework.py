@@ -15,6 +15,9 @@ MAX_NODE_SCORE = 100  # framework.MaxNodeScore
 # Plugin names (framework.Plugin.Name()) the device path implements.
 NODE_UNSCHEDULABLE = "NodeUnschedulable"  # upstream nodeunschedulable.Name
 NODE_NUMBER = "NodeNumber"                # minisched/plugins/score/nodenumber/nodenumber.go:31
+# Score-column plugins (build extension, generic pipeline): Score(pod, node) = a per-node int64 the
+# host computed (DeviceContext.upload_score_column); names "ScoreColumn0" .. "ScoreColumn3"
+SCORE_COLUMNS = tuple(f"ScoreColumn{k}" for k in range(4))
 
 # The taint NodeUnschedulable.Filter tolerates against (upstream v1.22.0).
 TAINT_NODE_UNSCHEDULABLE = "node.kubernetes.io/unschedulable"

@@ -22,12 +22,14 @@ from typing import Any, Callable, Iterable, Sequence
 import numpy as np
 
 from . import _native as N
-from .framework import (NODE_NUMBER, NODE_UNSCHEDULABLE, Normalize, Outcome, ScheduleResult)
+from .framework import (NODE_NUMBER, NODE_UNSCHEDULABLE, SCORE_COLUMNS, Normalize, Outcome, ScheduleResult)
 from .snapshot import NodeTable, PodTable, pack_nodes, pack_pods
 
 FILTER_IDS = {NODE_UNSCHEDULABLE: N.MSH_PLUGIN_NODE_UNSCHEDULABLE}
-SCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER}
-PRESCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER}
+SCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER,
+             **{name: N.MSH_PLUGIN_SCORE_COLUMN0 + k for k, name in enumerate(SCORE_COLUMNS)}}
+PRESCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER,
+             **{name: N.MSH_PLUGIN_SCORE_COLUMN0 + k for k, name in enumerate(SCORE_COLUMNS)}}
 
 
 @dataclass(frozen=True)
@@ -121,6 +123,14 @@ class DeviceContext:
         n = _same_len("upload_nodes", unsched, digit)
         self._check(self._lib.msh_upload_nodes(self.handle, n, N.ptr(unsched), N.ptr(digit)))
         self.n_nodes = len(unsched)
+
+    def upload_score_column(self, name: str, scores: np.ndarray) -> None:
+        """msh_upload_score_column: the per-node int64 scores (List order) of score-column plugin
+        `name` ("ScoreColumn0".."ScoreColumn3")."""
+        if name not in SCORE_COLUMNS:
+            raise ValueError(f"{name!r} is not a score-column plugin")
+        scores = np.ascontiguousarray(scores, np.int64)
+        self._check(self._lib.msh_upload_score_column(self.handle, SCORE_IDS[name], len(scores), N.ptr(scores)))
 
     def patch_nodes(self, idx: np.ndarray, unsched: np.ndarray, digit: np.ndarray) -> None:
         """In-place update of table entries (List order unchanged): msh_patch_nodes."""

@@ -13,6 +13,10 @@ extern "C" {
 
 enum { ORACLE_PLACED = 0, ORACLE_FIT_ERROR = 1, ORACLE_SCORE_ERROR = 2 };
 enum { ORACLE_PLUGIN_NODE_UNSCHEDULABLE = 1, ORACLE_PLUGIN_NODE_NUMBER = 2 };
+/* Score-column plugins (build extension, MSH_PLUGIN_SCORE_COLUMN0..3 of the C-ABI): Score(pod, node)
+ * = a host-computed int64 per node, column k of oracle_nodes.cols. */
+#define ORACLE_PLUGIN_SCORE_COLUMN0 16
+#define ORACLE_MAX_COLUMNS 4
 enum {
   ORACLE_NORM_NONE = 0,
   ORACLE_NORM_DEFAULT = 1,
@@ -24,6 +28,7 @@ typedef struct {
   int32_t n;
   const uint8_t* unsched; /* node.Spec.Unschedulable, List order */
   const int8_t* digit;    /* Atoi(last byte of node.Name) or -1 */
+  const int64_t* cols;    /* ORACLE_MAX_COLUMNS x n score columns (column k at cols + k*n), or NULL */
 } oracle_nodes;
 
 typedef struct {
@@ -58,8 +63,15 @@ int oracle_schedule_soa_impl(int32_t n, const uint8_t* unsched, const int8_t* no
                              const int32_t* filter_ids, int32_t nf, const int32_t* prescore_ids,
                              int32_t npre, const int32_t* score_ids, const int64_t* weights,
                              const int32_t* norm, int32_t ns, int norm_in_loop, int sequential,
-                             int32_t max_pods, int32_t* counts, int32_t* out_idx,
+                             int32_t max_pods, int32_t* counts, const int64_t* cols, int32_t* out_idx,
                              int64_t* out_score, int32_t* out_status, uint32_t* out_diag);
+/* oracle_schedule_batch_soa with score columns (ORACLE_MAX_COLUMNS x n int64, column k at cols + k*n). */
+int oracle_schedule_batch_soa_cols(int32_t n, const uint8_t* unsched, const int8_t* node_digit,
+                                   int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                                   const int32_t* filter_ids, int32_t nf, const int32_t* prescore_ids,
+                                   int32_t npre, const int32_t* score_ids, const int64_t* weights,
+                                   const int32_t* norm, int32_t ns, const int64_t* cols,
+                                   int32_t* out_idx, int64_t* out_score, int32_t* out_status);
 int oracle_schedule_batch_soa(int32_t n, const uint8_t* unsched, const int8_t* node_digit,
                               int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
                               const int32_t* filter_ids, int32_t nf, const int32_t* prescore_ids,

@@ -28,7 +28,7 @@ int oracle_schedule_batch_soa_omp(int32_t n, const uint8_t* unsched, const int8_
     if (hi > lo) {
       rc_all |= oracle_schedule_soa_impl(n, unsched, node_digit, hi - lo, pod_digit + lo,
                                          pod_tol + lo, filter_ids, nf, prescore_ids, npre,
-                                         score_ids, weights, norm, ns, 0, 0, 0, NULL,
+                                         score_ids, weights, norm, ns, 0, 0, 0, NULL, NULL,
                                          out_idx + lo, out_score + lo, out_status + lo, NULL);
     }
   }

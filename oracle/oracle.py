@@ -15,6 +15,8 @@ Two restatements of the reference hot path (shopetan/mini-kube-scheduler, Go):
      - RunPreScorePlugins minisched/minisched.go:153-162; NodeNumber.PreScore nodenumber.go:50-64
      - RunScorePlugins   minisched/minisched.go:164-199; NodeNumber.Score nodenumber.go:73-95
      - selectHost        minisched/minisched.go:304-325 with the first-max tie-break
+     - score-column plugins (build extension, no reference plugin): Score = a host-given int64
+       per node, normalized and weighted like any score plugin; totals in Go int64 (wrapping)
    Used for small cases and to generate / pin the golden fixtures.
 
 2. `c_schedule_batch` / `c_schedule_sequential` — ctypes entry to oracle/msh_oracle.c, the
@@ -39,7 +41,9 @@ ORACLE_LIB = ORACLE_DIR / "build" / "libmsh_oracle.so"
 PLACED, FIT_ERROR, SCORE_ERROR = 0, 1, 2
 NODE_UNSCHEDULABLE, NODE_NUMBER = 1, 2
 NORM_NONE, NORM_DEFAULT, NORM_DEFAULT_REVERSE, NORM_MINMAX = 0, 1, 2, 3
-PLUGIN_IDS = {"NodeUnschedulable": NODE_UNSCHEDULABLE, "NodeNumber": NODE_NUMBER}
+SCORE_COLUMN0, MAX_COLUMNS = 16, 4  # score-column plugins (build extension): Score = a per-node int64
+PLUGIN_IDS = {"NodeUnschedulable": NODE_UNSCHEDULABLE, "NodeNumber": NODE_NUMBER,
+              **{f"ScoreColumn{k}": SCORE_COLUMN0 + k for k in range(MAX_COLUMNS)}}
 PLUGIN_NAMES = {v: k for k, v in PLUGIN_IDS.items()}
 MAX_NODE_SCORE = 100
 TAINT_KEY = "node.kubernetes.io/unschedulable"
@@ -112,6 +116,12 @@ def list_order(nodes: list[Node]) -> list[Node]:
     return sorted(nodes, key=lambda n: n.name.encode("utf-8"))
 
 
+def _wrap64(v: int) -> int:
+    """Go int64 arithmetic: two's complement wrap."""
+    v &= (1 << 64) - 1
+    return v - (1 << 64) if v >> 63 else v
+
+
 def go_div(a: int, b: int) -> int:
     """Go int64 division truncates toward zero."""
     q = abs(a) // abs(b)
@@ -164,8 +174,9 @@ class ObjectResult:
 class ObjectOracle:
     """scheduleOne's selection part over objects (minisched/minisched.go:32-87)."""
 
-    def __init__(self, plugins: PluginSet | None = None):
+    def __init__(self, plugins: PluginSet | None = None, columns: dict | None = None):
         self.plugins = plugins or PluginSet()
+        self.columns = columns or {}  # score-column plugin name -> {node name: int64 score}
 
     def run_filter_plugins(self, pod: Pod, nodes: list[Node]):
         feasible, diag = [], set()
@@ -201,10 +212,12 @@ class ObjectOracle:
                         return ObjectResult(pod.name, SCORE_ERROR)
                     nd = atoi_last_byte(nodes[i].name)
                     lst.append(0 if nd < 0 else (10 if nd == state["PreScoreNodeNumber"] else 0))
+                elif name in self.columns:
+                    lst.append(int(self.columns[name][nodes[i].name]))
                 else:
                     raise ValueError(f"unknown score plugin {name}")
             per_plugin.append(normalize(self.plugins.normalize[k], lst))
-        total = [sum(per_plugin[k][f] * self.plugins.weights[k] for k in range(len(per_plugin)))
+        total = [_wrap64(sum(per_plugin[k][f] * self.plugins.weights[k] for k in range(len(per_plugin))))
                  for f in range(len(feasible))]
         best = 0
         for f in range(1, len(feasible)):  # selectHost, first max
@@ -247,9 +260,12 @@ def _plugin_arrays(plugins: PluginSet):
 
 
 def c_schedule_batch(unsched, node_digit, pod_digit, pod_tol, plugins: PluginSet | None = None,
-                     norm_in_loop: bool = False, threads: int = 1):
-    """Batched oracle over SoA columns -> (idx int32, score int64, status int32, diag uint32)."""
+                     norm_in_loop: bool = False, threads: int = 1, cols=None):
+    """Batched oracle over SoA columns -> (idx int32, score int64, status int32, diag uint32).
+    cols: {k: int64 array of n} for the ScoreColumn<k> plugins (List order)."""
     plugins = plugins or PluginSet()
+    if any(x.startswith("ScoreColumn") for x in plugins.score):
+        return _c_schedule_batch_cols(unsched, node_digit, pod_digit, pod_tol, plugins, cols or {})
     unsched = np.ascontiguousarray(unsched, np.uint8)
     node_digit = np.ascontiguousarray(node_digit, np.int8)
     pod_digit = np.ascontiguousarray(pod_digit, np.int8)
@@ -296,3 +312,26 @@ def c_schedule_sequential(unsched, node_digit, pod_digit, pod_tol, plugins: Plug
     if rc != 0:
         raise RuntimeError(f"oracle failed rc={rc}")
     return idx, score, status, counts[:n]
+
+
+def _c_schedule_batch_cols(unsched, node_digit, pod_digit, pod_tol, plugins: PluginSet, cols: dict):
+    unsched = np.ascontiguousarray(unsched, np.uint8)
+    node_digit = np.ascontiguousarray(node_digit, np.int8)
+    pod_digit = np.ascontiguousarray(pod_digit, np.int8)
+    pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
+    n, p = len(unsched), len(pod_digit)
+    allc = np.zeros((MAX_COLUMNS, max(n, 1)), np.int64)
+    for k, v in cols.items():
+        allc[k, :n] = np.asarray(v, np.int64)
+    allc = np.ascontiguousarray(allc[:, :n]) if n else allc
+    f, pre, s, w, nm = _plugin_arrays(plugins)
+    idx = np.empty(p, np.int32)
+    score = np.empty(p, np.int64)
+    status = np.empty(p, np.int32)
+    rc = clib().oracle_schedule_batch_soa_cols(
+        C.c_int32(n), _p(unsched), _p(node_digit), C.c_int32(p), _p(pod_digit), _p(pod_tol),
+        _p(f), C.c_int32(len(f)), _p(pre), C.c_int32(len(pre)), _p(s), _p(w), _p(nm),
+        C.c_int32(len(s)), _p(allc), _p(idx), _p(score), _p(status))
+    if rc != 0:
+        raise RuntimeError(f"oracle failed rc={rc}")
+    return idx, score, status, np.zeros(p, np.uint32)

@@ -840,3 +840,113 @@ def test_batch_kernel_ab(msh, oracle, kernel, monkeypatch):
         torch.cuda.synchronize()
         for t in ts:
             _assert_same([t[i].cpu().numpy() for i in (2, 3, 4)], want, f"{kernel} multi")
+
+
+# ---- the generic score pipeline (score-column plugins; north_star stages 1-5 with explicit int64 scores)
+
+GENERIC_LISTS = [
+    ["ScoreColumn0"],
+    ["NodeNumber", "ScoreColumn0"],
+    ["ScoreColumn1", "NodeNumber", "ScoreColumn0"],
+    ["ScoreColumn0", "ScoreColumn1", "ScoreColumn2", "ScoreColumn3", "NodeNumber"],
+]
+
+
+def _cols(rng, n):
+    return {0: rng.integers(-(1 << 31), (1 << 31) + 1, n), 1: rng.integers(0, 5, n) * 11,
+            2: np.full(n, 7), 3: rng.integers(-3, 3, n)}
+
+
+@pytest.mark.parametrize("lst", range(len(GENERIC_LISTS)))
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+def test_generic_pipeline_score_columns(msh, gpu_ctx, oracle, lst, norm):
+    """Score lists with score-column plugins run on generic_kernel: per pair an explicit int64
+    total (weight x NormalizeScore(raw) summed, Go int64 wrap), per-plugin extents by shuffle + LDS
+    reduction, wave-shuffle argmax; bit-exact vs the oracle's RunScorePlugins restatement for
+    tables across tile boundaries, ragged pod blocks, weights up to 2^32, tied / negative columns."""
+    rng = np.random.default_rng(31 * lst + norm)
+    names = GENERIC_LISTS[lst]
+    weights = [int(w) for w in rng.choice([1, 3, 1 << 32], len(names))]
+    modes = [norm if k % 2 == 0 else (norm + k) % 4 for k in range(len(names))]
+    pre = ["NodeNumber"] if "NodeNumber" in names else []
+    ps = oracle.PluginSet(filters=["NodeUnschedulable"], prescore=pre, score=names, weights=weights, normalize=modes)
+    gpu_ctx.set_plugins(ps.filters, ps.prescore, [msh.ScorePluginConfig(s, w, msh.Normalize(m))
+                                                  for s, w, m in zip(names, weights, modes)])
+    for n, p in [(1, 7), (70, 300), (1025, 1000), (5000, 4097), (20_000, 513)]:
+        u, nd, pd, pt = _rand_case(rng, n, p, p_unsched=0.3, p_tol=0.2)
+        cols = _cols(rng, n)
+        gpu_ctx.upload_nodes(u, nd)
+        for k in range(4):
+            gpu_ctx.upload_score_column(f"ScoreColumn{k}", cols[k])
+        got = gpu_ctx.schedule_batch(pd, pt)
+        want = oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols)
+        _assert_same(got, want, f"generic {names} modes={modes} n={n} p={p}")
+
+
+def test_generic_pipeline_entry_points_and_errors(msh, oracle):
+    """The generic pipeline through the multi-batch and async entry points; a column not uploaded
+    since the last node upload is MSH_ERR_STATE; bad column uploads are MSH_ERR_INVALID; shard keys,
+    sequential mode and the export reject score-column lists (MSH_ERR_UNSUPPORTED)."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(12)
+    u, nd, pd, pt = _rand_case(rng, 3000, 2000)
+    cols = _cols(rng, 3000)
+    ps = oracle.PluginSet(score=["NodeNumber", "ScoreColumn2", "ScoreColumn0"], weights=[5, 1, 2], normalize=[1, 0, 3])
+    with msh.DeviceContext(0) as ctx:
+        ctx.set_plugins(ps.filters, ps.prescore, [msh.ScorePluginConfig(s, w, msh.Normalize(m))
+                                                  for s, w, m in zip(ps.score, ps.weights, ps.normalize)])
+        ctx.upload_nodes(u, nd)
+        ctx.upload_score_column("ScoreColumn0", cols[0])
+        with pytest.raises(msh.MshError, match="MSH_ERR_STATE"):  # ScoreColumn2 missing
+            ctx.schedule_batch(pd, pt)
+        ctx.upload_score_column("ScoreColumn2", cols[2])
+        want = oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols)
+        _assert_same(ctx.schedule_batch(pd, pt), want, "generic host path")
+        ts = [_dev_batch(torch, dev, pd, pt) for _ in range(3)]
+        ctx.schedule_batches_device(ctx.batch_descs([_desc(t) for t in ts]),
+                                    stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for t in ts:
+            _assert_same([t[i].cpu().numpy() for i in (2, 3, 4)], want, "generic multi-batch")
+        hpd, hpt = msh.pinned_empty(len(pd), np.int8), msh.pinned_empty(len(pd), np.uint8)
+        hpd[:], hpt[:] = pd, pt
+        outs = (msh.pinned_empty(len(pd), np.int32), msh.pinned_empty(len(pd), np.int64),
+                msh.pinned_empty(len(pd), np.int32))
+        ctx.wait(ctx.schedule_batch_async(hpd, hpt, outs))
+        _assert_same(outs, want, "generic async")
+        with pytest.raises(msh.MshError, match="MSH_ERR_INVALID"):
+            ctx.upload_score_column("ScoreColumn1", np.zeros(2999, np.int64))
+        bad = np.zeros(3000, np.int64)
+        bad[5] = (1 << 31) + 1
+        with pytest.raises(msh.MshError, match="MSH_ERR_INVALID"):
+            ctx.upload_score_column("ScoreColumn1", bad)
+        with pytest.raises(msh.MshError, match="MSH_ERR_UNSUPPORTED"):
+            ctx.schedule_sequential(pd, pt)
+        with pytest.raises(msh.MshError, match="MSH_ERR_UNSUPPORTED"):
+            ctx.export_results(pd[:5], pt[:5])
+        d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+        keys = torch.empty(2 * len(pd), dtype=torch.int32, device=dev)
+        with pytest.raises(msh.MshError, match="MSH_ERR_UNSUPPORTED"):
+            ctx.shard_keys_device(len(pd), d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr(), 0)
+        ctx.upload_nodes(u, nd)  # drops the columns
+        with pytest.raises(msh.MshError, match="MSH_ERR_STATE"):
+            ctx.schedule_batch(pd, pt)
+
+
+@pytest.mark.parametrize("combo", range(len(PLUGIN_COMBOS)))
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+def test_generic_kernel_cross_checks_bitmap_kernel(msh, oracle, combo, norm, monkeypatch):
+    """MSH_BATCH_KERNEL=generic runs the reference plugin lists on generic_kernel too (explicit
+    int64 scores, real NormalizeScore over the feasible list) instead of the bitmap kernel's closed
+    forms: both place identically, and both equal the oracle (BASELINE C2 size, weight 3)."""
+    monkeypatch.setenv("MSH_BATCH_KERNEL", "generic")
+    rng = np.random.default_rng(500 + 10 * combo + norm)
+    f, pre, s = PLUGIN_COMBOS[combo]
+    ps = _plugins(oracle, f, pre, s, 3, norm)
+    u, nd, pd, pt = _rand_case(rng, 1000, 10_000, p_unsched=0.3, p_tol=0.1)
+    with msh.DeviceContext(0) as ctx:
+        _set(ctx, msh, ps)
+        ctx.upload_nodes(u, nd)
+        _assert_same(ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8),
+                     f"generic combo={combo} norm={norm}")

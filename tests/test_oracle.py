@@ -109,3 +109,34 @@ def test_closed_form_modes_matches_oracle(oracle, mode, weight):
         want = oracle.c_schedule_batch(u, nd, pd, pt, oracle.PluginSet(weights=[weight], normalize=[mode]))
         got = closed_form_modes(u, nd, pd, pt, weight, mode)
         assert all((a == b).all() for a, b in zip(got, want[:3]))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_score_columns_both_restatements(oracle, seed):
+    """Score-column plugins (the generic pipeline's build extension: Score = a host-given int64 per
+    node): the C restatement and the object restatement agree for NodeNumber + two columns, every
+    normalize mode, weights up to 2^32 (Go int64 totals wrap), negative and tied column values."""
+    rng = np.random.default_rng(seed)
+    n, p = int(rng.integers(1, 60)), 40
+    names = [f"node{i}" for i in range(n)]
+    nodes = oracle.list_order([oracle.Node(x, bool(rng.random() < 0.3)) for x in names])
+    unsched = np.array([nd.unschedulable for nd in nodes], np.uint8)
+    digit = np.array([oracle.atoi_last_byte(nd.name) for nd in nodes], np.int8)
+    cols = {0: rng.integers(-(1 << 31), 1 << 31, n), 1: rng.integers(0, 4, n) * 7}  # List order
+    T = oracle.Toleration
+    pods = [oracle.Pod(f"pod{j}" + ("x" if rng.random() < 0.1 else ""),
+                       (T("node.kubernetes.io/unschedulable", "Exists", "", "NoSchedule"),) if rng.random() < 0.2 else ())
+            for j in range(p)]
+    pd = np.array([oracle.atoi_last_byte(x.name) for x in pods], np.int8)
+    pt = np.array([oracle.pod_tolerates_unschedulable(x) for x in pods], np.uint8)
+    for modes in ([0, 0, 0], [1, 2, 3], [3, 3, 1], [2, 0, 3]):
+        for weights in ([1, 1, 1], [3, 1 << 32, 7]):
+            ps = oracle.PluginSet(score=["NodeNumber", "ScoreColumn0", "ScoreColumn1"], weights=weights,
+                                  normalize=modes)
+            ci, cs, cst, _ = oracle.c_schedule_batch(unsched, digit, pd, pt, ps, cols=cols)
+            oo = oracle.ObjectOracle(ps, columns={f"ScoreColumn{k}": {nd.name: int(v[i]) for i, nd in enumerate(nodes)}
+                                                  for k, v in cols.items()})
+            res = oo.schedule(pods, nodes)
+            assert [r.index for r in res] == ci.tolist(), (modes, weights)
+            assert [r.score for r in res] == cs.tolist(), (modes, weights)
+            assert [r.status for r in res] == cst.tolist(), (modes, weights)
