@@ -624,7 +624,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     out["c5_sequential"] = {"kernel": seq_kernel_label(n), "ms_per_step": ms, "us_per_pod": ms * 1e3 / p,
                             "pods_per_s": p / (ms * 1e-3), "evals_per_s": n * p / (ms * 1e-3),
                             "check": ("seq == batch (closed form), node counts == 3 x placements" if ok else "MISMATCH"),
-                            "roofline": make_roofline("sequential", n, p, ms, ms, 1, cus)}
+                            "roofline": make_roofline("sequential", n, p, ms, 1, cus)}
     ctx.close()
 
     # ---- C2: 1k x 10k ----

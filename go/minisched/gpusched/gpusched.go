@@ -1,0 +1,391 @@
+// Package gpusched is the Go side of the MI355X scheduling core: it packs the informer snapshot of
+// v1.Node and v1.Pod objects into the SoA columns libminisched_hip.so reads and calls its C-ABI
+// (include/minisched_hip.h) through cgo.
+//
+// It replaces the selection part of Scheduler.scheduleOne (minisched/minisched.go:40-87: the node
+// LIST, RunFilterPlugins, RunPreScorePlugins, RunScorePlugins and selectHost) for a batch of pods
+// drained from activeQ. Permit, Bind, the queue and the event handlers stay in Go, unchanged.
+//
+// The framework.*Plugin values stay the source of truth: New maps their Name()s to device plugin
+// ids and reports ErrUnsupported for a plugin list the device path does not implement, in which
+// case the caller keeps the reference's per-pod Go loop (minisched.go:115-199).
+//
+// Not compiled in the repository that ships this file (its build image has no Go toolchain): copy
+// the go/minisched tree into the reference's minisched/ and build it with the module's own go.mod
+// (k8s.io/kubernetes v1.22.0). See go/README.md.
+package gpusched
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../../mini-kube-scheduler_amd -lminisched_hip -Wl,-rpath,${SRCDIR}/../../../mini-kube-scheduler_amd
+#include <stdlib.h>
+#include "minisched_hip.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"runtime"
+	"sort"
+	"unsafe"
+
+	v1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/util/sets"
+	"k8s.io/kubernetes/pkg/scheduler/framework"
+)
+
+// ErrUnsupported: the plugin list names a plugin with no device implementation. The caller keeps
+// the reference's Go loop for it.
+var ErrUnsupported = errors.New("gpusched: plugin list not implemented on the device")
+
+// Device ids of the framework.Plugin names the device path implements (initialize.go:80-123).
+var (
+	filterIDs   = map[string]C.int32_t{"NodeUnschedulable": C.MSH_PLUGIN_NODE_UNSCHEDULABLE}
+	preScoreIDs = map[string]C.int32_t{"NodeNumber": C.MSH_PLUGIN_NODE_NUMBER}
+	scoreIDs    = map[string]C.int32_t{"NodeNumber": C.MSH_PLUGIN_NODE_NUMBER}
+)
+
+// Normalize is the NormalizeScore stage of one score plugin (msh_normalize). NodeNumber has no
+// ScoreExtensions (nodenumber.go:98-100): NormalizeNone reproduces the reference.
+type Normalize int32
+
+const (
+	NormalizeNone           Normalize = C.MSH_NORMALIZE_NONE
+	NormalizeDefault        Normalize = C.MSH_NORMALIZE_DEFAULT         // helper.DefaultNormalizeScore(100, false)
+	NormalizeDefaultReverse Normalize = C.MSH_NORMALIZE_DEFAULT_REVERSE // helper.DefaultNormalizeScore(100, true)
+	NormalizeMinMax         Normalize = C.MSH_NORMALIZE_MINMAX
+)
+
+// ScoreConfig is one entry of the score list. The reference has no weights ("TODO: plugin weight",
+// minisched.go:187): Weight 1 reproduces it.
+type ScoreConfig struct {
+	Plugin    framework.ScorePlugin
+	Weight    int64
+	Normalize Normalize
+}
+
+// Scores is the reference's score list as device entries: weight 1, no normalize (minisched.go:164-199).
+func Scores(plugins []framework.ScorePlugin) []ScoreConfig {
+	out := make([]ScoreConfig, len(plugins))
+	for i, p := range plugins {
+		out[i] = ScoreConfig{Plugin: p, Weight: 1, Normalize: NormalizeNone}
+	}
+	return out
+}
+
+// Ctx is one device context (one per GPU; not safe for concurrent use: give each goroutine that
+// submits its own Ctx, locked to its OS thread or not — every entry point sets the device).
+type Ctx struct {
+	c        *C.msh_ctx
+	byIndex  []*v1.Node // device node index -> node (List order)
+	hasNodes bool
+}
+
+func (x *Ctx) lastErr(what string, rc C.int) error {
+	return fmt.Errorf("%s: %d: %s", what, int(rc), C.GoString(C.msh_last_error(x.c)))
+}
+
+// New creates a device context for `device` and installs the plugin lists (Scheduler.filterPlugins,
+// preScorePlugins, scorePlugins; initialize.go:25-27).
+func New(device int, filters []framework.FilterPlugin, preScores []framework.PreScorePlugin, scores []ScoreConfig) (*Ctx, error) {
+	fids := make([]C.int32_t, 0, len(filters))
+	for _, p := range filters {
+		id, ok := filterIDs[p.Name()]
+		if !ok {
+			return nil, fmt.Errorf("%w: filter %q", ErrUnsupported, p.Name())
+		}
+		fids = append(fids, id)
+	}
+	pids := make([]C.int32_t, 0, len(preScores))
+	for _, p := range preScores {
+		id, ok := preScoreIDs[p.Name()]
+		if !ok {
+			return nil, fmt.Errorf("%w: pre-score %q", ErrUnsupported, p.Name())
+		}
+		pids = append(pids, id)
+	}
+	sids := make([]C.int32_t, 0, len(scores))
+	ws := make([]C.int64_t, 0, len(scores))
+	norms := make([]C.int32_t, 0, len(scores))
+	for _, s := range scores {
+		id, ok := scoreIDs[s.Plugin.Name()]
+		if !ok {
+			return nil, fmt.Errorf("%w: score %q", ErrUnsupported, s.Plugin.Name())
+		}
+		w := s.Weight
+		if w == 0 {
+			w = 1
+		}
+		sids = append(sids, id)
+		ws = append(ws, C.int64_t(w))
+		norms = append(norms, C.int32_t(s.Normalize))
+	}
+	var c *C.msh_ctx
+	if rc := C.msh_create(C.int(device), &c); rc != C.MSH_OK {
+		return nil, fmt.Errorf("msh_create(%d): %d: %s", device, int(rc), C.GoString(C.msh_last_error(nil)))
+	}
+	x := &Ctx{c: c}
+	if rc := C.msh_set_plugins_ex(c, ptrI32(fids), C.int32_t(len(fids)), ptrI32(pids), C.int32_t(len(pids)),
+		ptrI32(sids), ptrI64(ws), ptrI32(norms), C.int32_t(len(sids))); rc != C.MSH_OK {
+		err := x.lastErr("msh_set_plugins_ex", rc)
+		C.msh_destroy(c)
+		return nil, err
+	}
+	runtime.SetFinalizer(x, (*Ctx).Close)
+	return x, nil
+}
+
+// Close releases the device context. Batches in flight are waited for.
+func (x *Ctx) Close() {
+	if x.c != nil {
+		C.msh_destroy(x.c)
+		x.c = nil
+	}
+	runtime.SetFinalizer(x, nil)
+}
+
+// UploadNodes replaces the per-cycle Nodes().List (minisched.go:40): the nodes are put in List
+// order (byte-sorted names, the apiserver's etcd key order) and their two columns uploaded.
+// It returns the device-index -> node mapping, also kept for ScheduleBatch.
+func (x *Ctx) UploadNodes(nodes []v1.Node) ([]*v1.Node, error) {
+	sorted := make([]*v1.Node, len(nodes))
+	for i := range nodes {
+		sorted[i] = &nodes[i]
+	}
+	sort.Slice(sorted, func(a, b int) bool { return sorted[a].Name < sorted[b].Name }) // Go string order == bytes
+	uns := make([]C.uint8_t, len(sorted))
+	dig := make([]C.int8_t, len(sorted))
+	for i, n := range sorted {
+		if n.Spec.Unschedulable {
+			uns[i] = 1
+		}
+		dig[i] = C.int8_t(suffixDigit(n.Name))
+	}
+	if rc := C.msh_upload_nodes(x.c, C.int32_t(len(sorted)), ptrU8(uns), ptrI8(dig)); rc != C.MSH_OK {
+		return nil, x.lastErr("msh_upload_nodes", rc)
+	}
+	x.byIndex, x.hasNodes = sorted, true
+	return sorted, nil
+}
+
+// UpdateNode applies an informer Update that keeps the node's name (eventhandler.go:45-50, e.g. a
+// cordon flipping Spec.Unschedulable) in O(1) host->device traffic. Adds, deletes and renames
+// change List positions: call UploadNodes for those.
+func (x *Ctx) UpdateNode(n *v1.Node) error {
+	i := sort.Search(len(x.byIndex), func(k int) bool { return x.byIndex[k].Name >= n.Name })
+	if i == len(x.byIndex) || x.byIndex[i].Name != n.Name {
+		return fmt.Errorf("gpusched: node %q is not in the uploaded snapshot", n.Name)
+	}
+	idx := []C.int32_t{C.int32_t(i)}
+	uns := []C.uint8_t{0}
+	if n.Spec.Unschedulable {
+		uns[0] = 1
+	}
+	dig := []C.int8_t{C.int8_t(suffixDigit(n.Name))}
+	if rc := C.msh_patch_nodes(x.c, 1, ptrI32(idx), ptrU8(uns), ptrI8(dig)); rc != C.MSH_OK {
+		return x.lastErr("msh_patch_nodes", rc)
+	}
+	x.byIndex[i] = n
+	return nil
+}
+
+// Result of scheduleOne's selection part (minisched.go:50-87) for one pod.
+type Result struct {
+	Node   *v1.Node            // set when placed (selectHost's choice: the first maximum in List order)
+	Score  int64               // the selected node's total score
+	FitErr *framework.FitError // RunFilterPlugins found no feasible node (minisched.go:143-148)
+	Err    error               // a Score plugin failed (minisched.go:70-75); ErrorFunc gets the nil filter error
+}
+
+// HostBatch holds one batch's pod columns and outputs in page-locked C memory (msh_host_alloc), so
+// msh_schedule_batch copies nothing on the host: the kernel reads the columns and writes the outputs
+// over PCIe. It is C memory, so the cgo pointer rules do not apply to it. Allocate once, reuse.
+type HostBatch struct {
+	cap         int
+	mem         unsafe.Pointer
+	pd          []C.int8_t
+	pt          []C.uint8_t
+	idx, status []C.int32_t
+	score       []C.int64_t
+	ticket      C.uint64_t // the pending msh_schedule_batch_async ticket, 0 = none
+	pods        []*v1.Pod
+}
+
+// NewHostBatch allocates a HostBatch for up to `cap` pods (18 B per pod).
+func NewHostBatch(cap int) (*HostBatch, error) {
+	var mem unsafe.Pointer
+	// score | idx | status | digit | tol: 8-byte aligned sections
+	if rc := C.msh_host_alloc(C.size_t(18*cap+16), &mem); rc != C.MSH_OK {
+		return nil, fmt.Errorf("msh_host_alloc(%d pods): %d", cap, int(rc))
+	}
+	b := &HostBatch{cap: cap, mem: mem}
+	base := uintptr(mem)
+	b.score = unsafe.Slice((*C.int64_t)(unsafe.Pointer(base)), cap)
+	b.idx = unsafe.Slice((*C.int32_t)(unsafe.Pointer(base+uintptr(8*cap))), cap)
+	b.status = unsafe.Slice((*C.int32_t)(unsafe.Pointer(base+uintptr(12*cap))), cap)
+	b.pd = unsafe.Slice((*C.int8_t)(unsafe.Pointer(base+uintptr(16*cap))), cap)
+	b.pt = unsafe.Slice((*C.uint8_t)(unsafe.Pointer(base+uintptr(17*cap))), cap)
+	runtime.SetFinalizer(b, func(b *HostBatch) { C.msh_host_free(b.mem) })
+	return b, nil
+}
+
+// pack writes the pods' PreScore / Filter inputs: the name suffix digit (NodeNumber.PreScore,
+// nodenumber.go:50-64) and whether the tolerations tolerate the unschedulable taint
+// (NodeUnschedulable.Filter, upstream v1.22.0).
+func (b *HostBatch) pack(pods []*v1.Pod) error {
+	if len(pods) > b.cap {
+		return fmt.Errorf("gpusched: batch of %d pods exceeds the HostBatch capacity %d", len(pods), b.cap)
+	}
+	for j, pod := range pods {
+		b.pd[j] = C.int8_t(suffixDigit(pod.Name))
+		b.pt[j] = 0
+		if tolerates(pod.Spec.Tolerations) {
+			b.pt[j] = 1
+		}
+	}
+	b.pods = pods
+	return nil
+}
+
+// results decodes the outputs with the reference's error routing (minisched.go:50-75,
+// ErrorFunc :283-298).
+func (x *Ctx) results(b *HostBatch) []Result {
+	out := make([]Result, len(b.pods))
+	for j, pod := range b.pods {
+		switch b.status[j] {
+		case C.MSH_PLACED:
+			out[j] = Result{Node: x.byIndex[b.idx[j]], Score: int64(b.score[j])}
+		case C.MSH_FIT_ERROR:
+			diag := framework.Diagnosis{NodeToStatusMap: framework.NodeToStatusMap{}, UnschedulablePlugins: sets.NewString()}
+			if len(x.byIndex) > 0 { // some node failed NodeUnschedulable
+				diag.UnschedulablePlugins.Insert("NodeUnschedulable")
+			}
+			out[j] = Result{FitErr: &framework.FitError{Pod: pod, Diagnosis: diag}} // as minisched.go:143-148
+		default:
+			out[j] = Result{Err: framework.AsStatus(framework.ErrNotFound).AsError()}
+		}
+	}
+	return out
+}
+
+// ScheduleBatch runs minisched.go:50-87 for every pod against the uploaded snapshot, synchronously.
+func (x *Ctx) ScheduleBatch(pods []*v1.Pod, b *HostBatch) ([]Result, error) {
+	if !x.hasNodes {
+		return nil, errors.New("gpusched: UploadNodes has not been called")
+	}
+	if err := b.pack(pods); err != nil {
+		return nil, err
+	}
+	p := len(pods)
+	if rc := C.msh_schedule_batch(x.c, C.int32_t(p), ptrI8(b.pd[:p]), ptrU8(b.pt[:p]), ptrI32(b.idx[:p]),
+		ptrI64(b.score[:p]), ptrI32(b.status[:p])); rc != C.MSH_OK {
+		return nil, x.lastErr("msh_schedule_batch", rc)
+	}
+	return x.results(b), nil
+}
+
+// Submit launches a batch asynchronously (msh_schedule_batch_async) and returns at once: the caller
+// packs and submits the next drained batch into another HostBatch while this one runs. Collect it
+// with Wait. Batches of one Ctx complete in submission order.
+func (x *Ctx) Submit(pods []*v1.Pod, b *HostBatch) error {
+	if !x.hasNodes {
+		return errors.New("gpusched: UploadNodes has not been called")
+	}
+	if b.ticket != 0 {
+		return errors.New("gpusched: HostBatch has a batch in flight; Wait for it first")
+	}
+	if err := b.pack(pods); err != nil {
+		return err
+	}
+	p := len(pods)
+	if rc := C.msh_schedule_batch_async(x.c, C.int32_t(p), ptrI8(b.pd[:p]), ptrU8(b.pt[:p]), ptrI32(b.idx[:p]),
+		ptrI64(b.score[:p]), ptrI32(b.status[:p]), &b.ticket); rc != C.MSH_OK {
+		b.ticket = 0
+		return x.lastErr("msh_schedule_batch_async", rc)
+	}
+	return nil
+}
+
+// Wait returns the results of the batch last submitted into b.
+func (x *Ctx) Wait(b *HostBatch) ([]Result, error) {
+	if b.ticket == 0 {
+		return nil, errors.New("gpusched: no batch in flight in this HostBatch")
+	}
+	t := b.ticket
+	b.ticket = 0
+	if rc := C.msh_wait(x.c, t); rc != C.MSH_OK {
+		return nil, x.lastErr("msh_wait", rc)
+	}
+	return x.results(b), nil
+}
+
+// ScheduleSequential places the pods one at a time with a node-state commit between placements
+// (the reference's serial Run loop, minisched.go:28-30, on the device). maxPodsPerNode > 0 makes a
+// node infeasible once it holds that many pods (build extension); 0 = reference semantics.
+func (x *Ctx) ScheduleSequential(pods []*v1.Pod, b *HostBatch, maxPodsPerNode int32) ([]Result, error) {
+	if !x.hasNodes {
+		return nil, errors.New("gpusched: UploadNodes has not been called")
+	}
+	if err := b.pack(pods); err != nil {
+		return nil, err
+	}
+	p := len(pods)
+	if rc := C.msh_schedule_sequential(x.c, C.int32_t(p), ptrI8(b.pd[:p]), ptrU8(b.pt[:p]), C.int32_t(maxPodsPerNode),
+		ptrI32(b.idx[:p]), ptrI64(b.score[:p]), ptrI32(b.status[:p]), nil, nil); rc != C.MSH_OK {
+		return nil, x.lastErr("msh_schedule_sequential", rc)
+	}
+	return x.results(b), nil
+}
+
+// suffixDigit is strconv.Atoi(name[len(name)-1:]) (nodenumber.go:51-56, :81-87): only '0'..'9' parse.
+func suffixDigit(name string) int {
+	if name == "" {
+		return -1
+	}
+	c := name[len(name)-1]
+	if c >= '0' && c <= '9' {
+		return int(c - '0')
+	}
+	return -1
+}
+
+// tolerates is v1helper.TolerationsTolerateTaint(tolerations, unschedulable taint), what upstream
+// NodeUnschedulable.Filter (k8s.io/kubernetes v1.22.0) asks.
+func tolerates(ts []v1.Toleration) bool {
+	taint := &v1.Taint{Key: v1.TaintNodeUnschedulable, Effect: v1.TaintEffectNoSchedule}
+	for i := range ts {
+		if ts[i].ToleratesTaint(taint) {
+			return true
+		}
+	}
+	return false
+}
+
+func ptrI32(s []C.int32_t) *C.int32_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return &s[0]
+}
+
+func ptrI64(s []C.int64_t) *C.int64_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return &s[0]
+}
+
+func ptrU8(s []C.uint8_t) *C.uint8_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return &s[0]
+}
+
+func ptrI8(s []C.int8_t) *C.int8_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return &s[0]
+}

@@ -121,6 +121,10 @@ struct msh_ctx {
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
   int32_t patch_pending = 0;              // entries in d_patch the next prepare() applies
   std::vector<unsigned long long> h_patch;
+  // page-locked staging of node columns / patch entries (uploads copy from it, never from pageable
+  // memory: a pageable copy may wait for more than this ctx's stream)
+  size_t nstage_cap = 0;
+  unsigned char* h_nstage = nullptr;
 };
 
 namespace {
@@ -287,6 +291,19 @@ int track_launch(msh_ctx* c, hipStream_t s) {
 // waits: the host does not block here, and other ctxs' work on the device is not waited for).
 int after_inflight(msh_ctx* c) {
   for (auto& e : c->inflight) MSH_HIP(c, hipStreamWaitEvent(c->stream, e.second, 0));
+  return MSH_OK;
+}
+
+// The page-locked node staging buffer, at least `bytes` long. Every upload / patch finishes its copies
+// before returning (prepare() synchronizes the ctx stream), so the buffer is free on entry.
+int node_stage(msh_ctx* c, size_t bytes) {
+  if (bytes <= c->nstage_cap) return MSH_OK;
+  (void)hipHostFree(c->h_nstage);
+  c->h_nstage = nullptr;
+  c->nstage_cap = 0;
+  const size_t cap = std::max<size_t>(bytes, 4096);
+  MSH_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_nstage), cap, hipHostMallocDefault));
+  c->nstage_cap = cap;
   return MSH_OK;
 }
 
@@ -505,7 +522,7 @@ bool read_knobs(msh::DeviceInfo& d, std::string* err) {
                   knob("MSH_KX_BITS", {{"0", 0}, {"1", 1}}, &d.kx_bits, err) &&
                   knob("MSH_HOST_IO", {{"zero-copy", 0}, {"zc", 1}, {"dma", 2}}, &io, err) &&
                   knob("MSH_HOST_SYNC", {{"wait", 0}, {"poll", 1}}, &poll, err) &&
-                  knob("MSH_BATCH_KERNEL", {{"wg", 0}, {"slices", 1}}, &d.batch_kernel, err) &&
+                  knob("MSH_BATCH_KERNEL", {{"wg", 0}, {"slices", 1}, {"generic", 2}}, &d.batch_kernel, err) &&
                   knob("MSH_WG_WAVES", {{"0", 0}, {"4", 4}, {"8", 8}}, &d.wg_waves, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;
@@ -614,6 +631,7 @@ void msh_destroy(msh_ctx* c) {
   free_nodes(c);
   free_pods(c);
   (void)hipHostFree(c->h_stage);
+  (void)hipHostFree(c->h_nstage);
   (void)hipFree(c->d_patch);
   (void)hipFree(c->d_ball);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -703,8 +721,11 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
     c->node_cap = cap;
   }
   if (n > 0) {
-    MSH_HIP(c, hipMemcpyAsync(c->d_unsched, unsched, (size_t)n, hipMemcpyHostToDevice, c->stream));
-    MSH_HIP(c, hipMemcpyAsync(c->d_digit, digit, (size_t)n, hipMemcpyHostToDevice, c->stream));
+    if ((rc = node_stage(c, 2 * (size_t)n)) != MSH_OK) return rc;
+    std::memcpy(c->h_nstage, unsched, (size_t)n);
+    std::memcpy(c->h_nstage + n, digit, (size_t)n);
+    MSH_HIP(c, hipMemcpyAsync(c->d_unsched, c->h_nstage, (size_t)n, hipMemcpyHostToDevice, c->stream));
+    MSH_HIP(c, hipMemcpyAsync(c->d_digit, c->h_nstage + n, (size_t)n, hipMemcpyHostToDevice, c->stream));
   }
   MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->node_cap * sizeof(int32_t), c->stream));
   for (bool& ok : c->col_ok) ok = false;  // score columns belong to the previous table's nodes
@@ -745,8 +766,11 @@ int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t
     MSH_HIP(c, hipMalloc(&c->d_patch, cap * sizeof(unsigned long long)));
     c->patch_cap = cap;
   }
-  MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_patch.data(), (size_t)count * sizeof(unsigned long long),
-                            hipMemcpyHostToDevice, c->stream));
+  const size_t pbytes = (size_t)count * sizeof(unsigned long long);
+  int rc = node_stage(c, pbytes);
+  if (rc != MSH_OK) return rc;
+  std::memcpy(c->h_nstage, c->h_patch.data(), pbytes);
+  MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_nstage, pbytes, hipMemcpyHostToDevice, c->stream));
   // the entries are applied by the prep's reset launch, then the derived tables are rebuilt
   c->patch_pending = count;
   c->dirty = true;
@@ -812,9 +836,13 @@ int msh_upload_score_column(msh_ctx* c, int32_t plugin_id, int32_t n, const int6
   if (rc != MSH_OK) return rc;
   if (!c->d_cols) MSH_HIP(c, hipMalloc(&c->d_cols, (size_t)msh::GEN_COLS * c->node_cap * sizeof(int64_t)));
   const int k = plugin_id - MSH_PLUGIN_SCORE_COLUMN0;
-  if (n > 0)
-    MSH_HIP(c, hipMemcpyAsync(c->d_cols + (size_t)k * c->node_cap, scores, (size_t)n * sizeof(int64_t),
-                              hipMemcpyHostToDevice, c->stream));
+  if (n > 0) {
+    const size_t bytes = (size_t)n * sizeof(int64_t);
+    if ((rc = node_stage(c, bytes)) != MSH_OK) return rc;
+    std::memcpy(c->h_nstage, scores, bytes);
+    MSH_HIP(c, hipMemcpyAsync(c->d_cols + (size_t)k * c->node_cap, c->h_nstage, bytes, hipMemcpyHostToDevice,
+                              c->stream));
+  }
   MSH_HIP(c, hipStreamSynchronize(c->stream));
   c->col_ok[k] = true;
   return MSH_OK;

@@ -6,24 +6,29 @@
 //   RunScorePlugins    minisched/minisched.go:164-199  (NodeNumber.Score, nodenumber.go:73-95)
 //   selectHost         minisched/minisched.go:304-325  (argmax; ties -> lowest index here)
 //
-// Layout: the node table is bit-sliced (msh_internal.h, PLANE_*): one 32-bit word per plane
-// covers 32 consecutive nodes of the List order; planes are the 4 bits of the node's NodeNumber
-// code, the NodeUnschedulable verdict for non-tolerating pods (X) and "real node" (V). The
-// batched kernel puts one POD per lane and streams the planes through SGPRs, so every VALU
-// bit operation evaluates 32 (pod, node) pairs per lane.
+// Layout (msh_internal.h): per group of 256 List-order nodes, the digit rows ER[r] (bit i of row r:
+// node i is feasible-relevant and scores 10 for a digit-r pod; row 10 all zero), the X words
+// (NodeUnschedulable verdict for non-tolerating pods) and, for REVERSE / MINMAX, the V words (real
+// node), plus the bit planes of the node codes the sequential / A/B kernels read. The batched kernels
+// put one POD per lane: a lane's hit word for 32 nodes is ER[row] & ~(X & nT), one v_bitop3, so every
+// VALU operation evaluates 32 (pod, node) pairs.
 // Stages (north_star):
-//   1. feasibility bitmask with wavefront __ballot (the X / V planes)         -> node_prep_kernel
-//   2. int64 score with the plugin weight fused                              -> decode_pod / decode_ident
-//   3. per-pod normalisation (DEFAULT / REVERSE / MINMAX need the extent of the raw scores
-//      over the feasible list: first feasible match / non-match)            -> bits_kernel<KX> + decode
-//   4. argmax with a fixed lowest-index tie-break: the first zero bit in List order (groups,
-//      words, bits), slice results merged by min in LDS                      -> bits_kernel
-//   5. node-table tiles: each group of 256 nodes is loaded once per wave into SGPRs (scalar
-//      loads through the scalar cache) and reused by all 64 pods of the wave   -> bits_kernel
+//   1. feasibility bitmask with wavefront __ballot (X / V words, first feasible per class) -> node_prep_kernel
+//   2. int64 score with the plugin weight fused                    -> decode_pod / decode_ident
+//   3. per-pod normalisation (DEFAULT / REVERSE / MINMAX need the extent of the raw scores over the
+//      feasible list: first feasible match / non-match)             -> wg_kernel<KX> + decode
+//   4. argmax with a fixed lowest-index tie-break: the lowest group with a hit, then its first set
+//      bit (v_ffbl) in List order                                   -> wg_kernel
+//   5. node-table tiles staged in LDS once per 4-wave workgroup and reused by its 256 pods -> wg_kernel
+//   generic_kernel does stages 1-5 with an explicit int64 score per pair, for any score-plugin list
+//   (score-column plugins; a real LDS min/max reduction and a wave-shuffle argmax).
 //
 // Kernels, by entry point:
 //   node_prep_kernel (+ prep_reset_kernel)  every upload / patch / plugin change
-//   bits_kernel          msh_schedule_batch*, msh_shard_keys_device (every normalize mode)
+//   wg_kernel            msh_schedule_batch*, msh_schedule_batches_device (MULTI), msh_shard_keys_device
+//   generic_kernel       the batch entry points when the score list names a score-column plugin
+//   rows_kernel          A/B (MSH_BATCH_KERNEL=slices): the round-2 slice kernel
+//   bits_kernel          A/B (MSH_KX_BITS=1): REVERSE / MINMAX on the code planes
 //   decode_keys_kernel   node-sharded mode: decode the merged int32 shard keys
 //   seq_kernel           sequential commit, one pod at a time, one workgroup
 //   export_kernel        per-pair result export (simulator result store)
