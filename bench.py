@@ -11,7 +11,7 @@ Modes (the headline line)
               pods are sharded (each rank its own 100k batches; no data-path collective) -> weak
               scaling. The K steps are K independent batches (eight distinct pod batches, each with
               its own outputs, used in turn) submitted from one host thread on one HIP stream
-              through msh_schedule_batches_device, MSH_BATCHES_PER_LAUNCH (8) batches per kernel
+              through msh_schedule_batches_device, MSH_BATCHES_PER_LAUNCH (32) batches per kernel
               launch: the submission a caller with several drained batches ready makes.
   sequential  BASELINE C5: same sizes, one pod at a time with node-state commits.
   nodeshard   BASELINE C4 shape: the node table split over the ranks, per-shard first keys
@@ -259,17 +259,13 @@ def main():
     elapsed = time.perf_counter() - t0
     region_ms = r0.elapsed_time(r1)  # device span of the region on the launch stream
 
-    # ---- the dominant kernel's launch duration, for the roofline: R launches, each bracketed by its
-    # own HIP events on the stream it runs on (what rocprofv3's per-kernel average measures); in batch
-    # mode the full 8-batch launches of the default submission, or single-batch launches ----
+    # ---- the dominant kernel's launch duration, for the roofline: R launches back to back on the
+    # stream the kernels run on, each timed by its own start / stop events recorded at the kernel's
+    # start and completion (msh_timing_begin: hipExtLaunchKernelGGL events, the interval rocprofv3's
+    # kernel trace averages); in batch mode the full 8-batch launches of the default submission ----
     R = 50 if mode != "nodeshard" else min(args.steps, 20)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(R)]
-    for e0, e1 in evs:
-        e0.record(stream)
-        e1.record(stream)
-    torch.cuda.synchronize()
-    for e0, e1 in evs:
-        e0.record(stream)
+    ctx.timing_begin(R)
+    for _ in range(R):
         if mode == "batch" and multi:
             rc = fast.schedule_batches_device(handle, G, descs_addr, sh or None)
             if rc:
@@ -285,9 +281,8 @@ def main():
         else:
             b = bufs[0]
             ctx.shard_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), node_base, b["keys"].data_ptr(), sh)
-        e1.record(stream)
-    torch.cuda.synchronize()
-    launch_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    n_timed, tot_ms, max_ms = ctx.timing_end()
+    launch_ms = tot_ms / max(n_timed, 1)
     batches_per_launch = G if (mode == "batch" and multi) else 1
     if mode == "nodeshard":  # the timed steps hold the all-reduce and the decode too: redo them after
         submit(1)
@@ -374,7 +369,7 @@ def load_valu_peak():
     """The integer VALU issue rate measured on MI355X (scripts/ubench_valu_peak.hip ->
     profiles/r3_ubench_valu_peak.json): wave64 instructions per SIMD per cycle for the scan's forms."""
     d = load_json(VALU_PEAK_FILE) or {}
-    return d.get("int_valu_wave_instr_per_simd_cycle"), d
+    return d.get("scan_forms_wave_instr_per_simd_cycle") or d.get("int_valu_wave_instr_per_simd_cycle"), d
 
 
 def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
@@ -432,8 +427,9 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
         "traffic_note": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024), same kernel, size and batches",
         "kernel": kname,
         "kernel_ms": launch_ms,
-        "kernel_ms_note": ("mean of R launches, each bracketed by HIP events on its stream (rocprofv3's "
-                           "per-kernel average of the same launches must agree)"),
+        "kernel_ms_note": ("mean duration of R back-to-back launches, each timed from the kernel's own start "
+                           "to its completion (msh_timing_begin / _end: hipExtLaunchKernelGGL events), the "
+                           "interval rocprofv3's kernel trace averages"),
         "batches_per_launch": batches_per_launch,
         "ms_per_batch": launch_ms / batches_per_launch,
         "lds_bytes_per_launch": lds_bytes,

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSH_ABI_VERSION 5
+#define MSH_ABI_VERSION 6
 
 /* ---- error codes (return values) ---- */
 typedef enum msh_err {
@@ -213,7 +213,7 @@ int msh_schedule_batch_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit
  * launch (a larger nb takes ceil(nb / MSH_BATCHES_PER_LAUNCH) launches, in order, on `stream`),
  * which spreads the launch cost and the kernel's fill and drain over them. Results are identical to
  * nb msh_schedule_batch_device calls. Asynchronous, like msh_schedule_batch_device. */
-#define MSH_BATCHES_PER_LAUNCH 8
+#define MSH_BATCHES_PER_LAUNCH 32
 typedef struct msh_batch {
   int32_t p;
   int32_t reserved; /* 0 */
@@ -272,6 +272,16 @@ int msh_decode_keys_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
 /* Whether keys[1] holds "first feasible of any class" (1, per class) or "first feasible
  * non-match" (0, per pod) under the ctx's current plugin set. */
 int msh_keys_slot1_is_any(const msh_ctx* ctx, int32_t* out_flag);
+
+/* ---- kernel timing (measurement hook) ----
+ * msh_timing_begin arms up to max_launches (1..4096) event pairs: each following hot-kernel launch of
+ * this ctx made from this thread (the batch, multi-batch, generic and sequential kernels) records its
+ * pair at the kernel's own start and completion (hipExtLaunchKernelGGL), the interval a kernel trace
+ * (rocprofv3) reports, without the stream gaps around it. msh_timing_end waits for the recorded
+ * launches and returns their count, summed and longest duration (ms), and disarms. Launches past
+ * max_launches are not timed. Not needed by a scheduler; used by bench.py's roofline. */
+int msh_timing_begin(msh_ctx* ctx, int32_t max_launches);
+int msh_timing_end(msh_ctx* ctx, int32_t* out_launches, double* out_total_ms, double* out_max_ms);
 
 /* ---- snapshot packer (host, no device needed) ----
  * Names are given as one byte blob + n+1 offsets (name i = blob[off[i]:off[i+1]]).

@@ -56,6 +56,7 @@ EXPORTED = (
     "msh_schedule_batches_device", "msh_schedule_sequential",
     "msh_schedule_sequential_device", "msh_node_pod_counts", "msh_reset_node_pod_counts",
     "msh_shard_keys_len", "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
+    "msh_timing_begin", "msh_timing_end",
     "msh_pack_nodes", "msh_pack_pods", "msh_toleration_tolerates_unschedulable",
 )
 
@@ -77,7 +78,7 @@ class Batch(C.Structure):
                 ("out_idx", C.c_void_p), ("out_score", C.c_void_p), ("out_status", C.c_void_p)]
 
 
-BATCHES_PER_LAUNCH = 8  # MSH_BATCHES_PER_LAUNCH
+BATCHES_PER_LAUNCH = 32  # MSH_BATCHES_PER_LAUNCH
 ASYNC_DEPTH = 4  # MSH_ASYNC_DEPTH
 
 COMMIT_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.c_int64)
@@ -106,6 +107,8 @@ _SIGS = {
     "msh_schedule_batches_device": (C.c_int, [_P, _I32, _P, _P]),
     "msh_schedule_batch_async": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, C.POINTER(C.c_uint64)]),
     "msh_wait": (C.c_int, [_P, C.c_uint64]),
+    "msh_timing_begin": (C.c_int, [_P, _I32]),
+    "msh_timing_end": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "msh_schedule_sequential": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, COMMIT_CB, _P]),
     "msh_schedule_sequential_device": (C.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P, _P]),
     "msh_node_pod_counts": (C.c_int, [_P, _P]),

@@ -72,6 +72,21 @@ void par_copy(const CopyJob* jobs, int n_jobs) {
 
 }  // namespace
 
+// One version of the node-side device tables (List order, padded to cap nodes).
+struct NodeTable {
+  size_t cap = 0;
+  uint8_t* d_unsched = nullptr;  // the uploaded columns
+  int8_t* d_digit = nullptr;
+  uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout)
+  uint32_t* d_erows = nullptr;   // digit rows (msh_internal.h ER_* layout)
+  uint32_t* d_ball = nullptr;    // [0..1] first feasible node per pod class, as keys
+  // score-column plugins (generic pipeline): GEN_COLS x cap int64, column k valid when col_ok[k]
+  int64_t* d_cols = nullptr;
+  bool col_ok[msh::GEN_COLS] = {};
+  // launches that read this version: one event per caller stream, re-recorded after each launch
+  std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
+};
+
 struct msh_ctx {
   int device = 0;
   std::string err;
@@ -83,20 +98,23 @@ struct msh_ctx {
   std::vector<int64_t> weights;
   PluginParams pp{1, 1, 1, 0, 1};
 
-  // node table
+  // node table: two versions. Launches read tab[cur]; a rewrite (upload, patch, plugin change,
+  // score column) builds the other version on prep_stream and then publishes it, so it never waits
+  // for launches in flight on the version they read (only for those of two rewrites ago, on the
+  // version it overwrites, long done in practice).
   bool have_nodes = false;
-  bool dirty = true;
   int32_t n_nodes = 0, n_pad = 0;
-  uint8_t* d_unsched = nullptr;
-  int8_t* d_digit = nullptr;
-  uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout)
-  uint32_t* d_erows = nullptr;   // digit rows (msh_internal.h ER_* layout)
-  uint32_t* d_ball = nullptr;    // [0..1] first feasible node per pod class, as keys
+  NodeTable tab[2];
+  int cur = 0;
+  // sequential-mode state (not versioned: carried from call to call): pods committed per node, and
+  // the sequential launches in flight that update it
   int32_t* d_counts = nullptr;
-  size_t node_cap = 0;
-  // score-column plugins (generic pipeline): GEN_COLS x node_cap int64, column k valid when col_ok[k]
-  int64_t* d_cols = nullptr;
-  bool col_ok[msh::GEN_COLS] = {};
+  size_t counts_cap = 0;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> seq_inflight;
+  // the rewrites' own stream, created with the device's highest priority: HIP gives each priority
+  // its own hardware queues, so a rewrite never queues behind other streams' kernels that happen to
+  // share a hardware queue with it (GPU_MAX_HW_QUEUES per priority)
+  hipStream_t prep_stream = nullptr;
   bool generic = false;  // the score list names a score-column plugin
 
   // host-path buffers
@@ -109,22 +127,21 @@ struct msh_ctx {
   size_t stage_cap = 0;
   unsigned char* h_stage = nullptr;  // page-locked: digit p | tol p | idx 4p | score 8p | status 4p
   hipEvent_t done_ev = nullptr;  // MSH_HOST_SYNC=poll
-  // Launches of the *_device entry points read the ctx's tables after the call returns: one event
-  // per caller stream, re-recorded after each launch on it. A table rewrite (upload, patch, plugin
-  // change, count reset) makes the ctx's own stream wait for exactly these, never the whole device.
-  std::vector<std::pair<hipStream_t, hipEvent_t>> inflight;
   // msh_schedule_batch_async: a ring of MSH_ASYNC_DEPTH events on the ctx's stream; ticket t's event
   // is async_ev[t % MSH_ASYNC_DEPTH]; every ticket <= async_done has completed
   hipEvent_t async_ev[MSH_ASYNC_DEPTH] = {};
   uint64_t async_issued = 0, async_done = 0;
   size_t patch_cap = 0;
   unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
-  int32_t patch_pending = 0;              // entries in d_patch the next prepare() applies
   std::vector<unsigned long long> h_patch;
   // page-locked staging of node columns / patch entries (uploads copy from it, never from pageable
   // memory: a pageable copy may wait for more than this ctx's stream)
   size_t nstage_cap = 0;
   unsigned char* h_nstage = nullptr;
+  // msh_timing_begin / _end: kernel start / stop event pairs for the next hot-kernel launches
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+  size_t t_next = 0;
 };
 
 namespace {
@@ -145,21 +162,33 @@ int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
   } while (0)
 
-void free_nodes(msh_ctx* c) {
-  (void)hipFree(c->d_cols);
-  c->d_cols = nullptr;
-  for (bool& ok : c->col_ok) ok = false;
-  (void)hipFree(c->d_unsched);
-  (void)hipFree(c->d_digit);
-  (void)hipFree(c->d_planes);
-  (void)hipFree(c->d_erows);
-  (void)hipFree(c->d_counts);
-  c->d_unsched = nullptr;
-  c->d_digit = nullptr;
-  c->d_planes = nullptr;
-  c->d_erows = nullptr;
-  c->d_counts = nullptr;
-  c->node_cap = 0;
+NodeTable& cur_table(msh_ctx* c) { return c->tab[c->cur]; }
+
+void free_table(NodeTable& t) {
+  (void)hipFree(t.d_cols);
+  (void)hipFree(t.d_unsched);
+  (void)hipFree(t.d_digit);
+  (void)hipFree(t.d_planes);
+  (void)hipFree(t.d_erows);
+  (void)hipFree(t.d_ball);
+  t.d_cols = nullptr;
+  t.d_unsched = nullptr;
+  t.d_digit = nullptr;
+  t.d_planes = nullptr;
+  t.d_erows = nullptr;
+  t.d_ball = nullptr;
+  for (bool& ok : t.col_ok) ok = false;
+  t.cap = 0;
+}
+
+// Host wait for the launches recorded in `evs` (their events are kept for reuse).
+void wait_events(const std::vector<std::pair<hipStream_t, hipEvent_t>>& evs) {
+  for (auto& e : evs) (void)hipEventSynchronize(e.second);
+}
+
+void destroy_events(std::vector<std::pair<hipStream_t, hipEvent_t>>& evs) {
+  for (auto& e : evs) (void)hipEventDestroy(e.second);
+  evs.clear();
 }
 
 void free_pods(msh_ctx* c) {
@@ -270,8 +299,8 @@ int check_ids(msh_ctx* c, const int32_t* ids, int32_t n, int kind, const char* w
 
 // After a *_device launch on caller stream s: (re-)record the ctx's event for s. One event per
 // stream the ctx has launched on (a linear search: callers use a handful of streams).
-int track_launch(msh_ctx* c, hipStream_t s) {
-  for (auto& e : c->inflight)
+int record_on(msh_ctx* c, std::vector<std::pair<hipStream_t, hipEvent_t>>& evs, hipStream_t s) {
+  for (auto& e : evs)
     if (e.first == s) {
       MSH_HIP(c, hipEventRecord(e.second, s));
       return MSH_OK;
@@ -283,19 +312,27 @@ int track_launch(msh_ctx* c, hipStream_t s) {
     (void)hipEventDestroy(ev);
     return hip_fail(c, e, "hipEventRecord");
   }
-  c->inflight.emplace_back(s, ev);
+  evs.emplace_back(s, ev);
   return MSH_OK;
 }
 
-// Order the ctx's own stream after every launch this ctx queued on caller streams (device-side
-// waits: the host does not block here, and other ctxs' work on the device is not waited for).
-int after_inflight(msh_ctx* c) {
-  for (auto& e : c->inflight) MSH_HIP(c, hipStreamWaitEvent(c->stream, e.second, 0));
+// After a launch on caller stream s that reads the current table version (seq: and updates the
+// sequential-mode counts).
+int track_launch(msh_ctx* c, hipStream_t s, bool seq = false) {
+  int rc = record_on(c, cur_table(c).readers, s);
+  if (rc == MSH_OK && seq) rc = record_on(c, c->seq_inflight, s);
+  return rc;
+}
+
+// Order prep_stream after the sequential launches in flight (device-side waits): they update the
+// counts that a count read, reset or re-upload touches next.
+int after_seq(msh_ctx* c) {
+  for (auto& e : c->seq_inflight) MSH_HIP(c, hipStreamWaitEvent(c->prep_stream, e.second, 0));
   return MSH_OK;
 }
 
-// The page-locked node staging buffer, at least `bytes` long. Every upload / patch finishes its copies
-// before returning (prepare() synchronizes the ctx stream), so the buffer is free on entry.
+// The page-locked node staging buffer, at least `bytes` long. Every rewrite finishes its copies
+// before returning (it synchronizes prep_stream), so the buffer is free on entry.
 int node_stage(msh_ctx* c, size_t bytes) {
   if (bytes <= c->nstage_cap) return MSH_OK;
   (void)hipHostFree(c->h_nstage);
@@ -307,39 +344,158 @@ int node_stage(msh_ctx* c, size_t bytes) {
   return MSH_OK;
 }
 
-// Host wait for every launch this ctx queued (msh_destroy: the tables are freed after it).
-void wait_inflight(msh_ctx* c) {
-  for (auto& e : c->inflight) (void)hipEventSynchronize(e.second);
+// A node table version with room for n_pad nodes (a reallocation first waits for its readers).
+int ensure_table(msh_ctx* c, NodeTable& t, size_t n_pad) {
+  if (t.cap >= n_pad && t.d_planes) return MSH_OK;
+  wait_events(t.readers);
+  free_table(t);
+  MSH_HIP(c, hipMalloc(&t.d_unsched, n_pad));
+  MSH_HIP(c, hipMalloc(&t.d_digit, n_pad));
+  MSH_HIP(c, hipMalloc(&t.d_planes, n_pad / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
+  // + ER_PAD groups: the batch kernel copies whole tiles without clamping (never read as rows)
+  MSH_HIP(c, hipMalloc(&t.d_erows, (n_pad / msh::GROUP_NODES + msh::ER_PAD) * msh::ER_GD * sizeof(uint32_t)));
+  MSH_HIP(c, hipMalloc(&t.d_ball, 2 * sizeof(uint32_t)));
+  t.cap = n_pad;
+  return MSH_OK;
 }
 
-// Rebuild the derived tables (planes, first feasible per class) after an upload, a patch or a
-// filter-list change, on the ctx's stream behind every launch of this ctx still in flight (they may
-// read the tables this rewrites), and finish it before returning; then make launches on `s` wait for
-// the rebuild. Runs only after an upload, a patch or a plugin change, never per batch.
-int prepare(msh_ctx* c, hipStream_t s) {
-  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
-  if (!c->dirty) return MSH_OK;
-  int rc = after_inflight(c);
+int ensure_cols(msh_ctx* c, NodeTable& t) {
+  if (!t.d_cols) MSH_HIP(c, hipMalloc(&t.d_cols, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t)));
+  return MSH_OK;
+}
+
+// What a rewrite changes relative to the published version.
+struct Rewrite {
+  enum Kind { UPLOAD, PATCH, REPREP, COLUMN } kind;
+  int32_t n = 0;                    // UPLOAD: the new node count and columns
+  const uint8_t* unsched = nullptr;
+  const int8_t* digit = nullptr;
+  int32_t patch_count = 0;          // PATCH: entries in c->h_patch
+  int col = -1;                     // COLUMN: column k and its n scores
+  const int64_t* scores = nullptr;
+};
+
+// Build the unpublished table version from the published one (or from the upload) on prep_stream,
+// wait for that work alone, and publish it. Launches in flight keep reading the old version.
+int rewrite(msh_ctx* c, const Rewrite& w) {
+  const int s = 1 - c->cur;
+  NodeTable& src = c->tab[c->cur];
+  NodeTable& dst = c->tab[s];
+  hipStream_t ps = c->prep_stream;
+  const bool up = w.kind == Rewrite::UPLOAD;
+  const int32_t n = up ? w.n : c->n_nodes;
+  // Padded to whole 1,024-node blocks, and never empty: an empty cluster is a table of padding
+  // slots (infeasible for every pod), so every pod gets FitError from the kernel.
+  const int32_t n_pad = std::max(((n + msh::NODE_PAD - 1) / msh::NODE_PAD) * msh::NODE_PAD, msh::NODE_PAD);
+  // the version overwritten here was last read by launches of two rewrites ago
+  wait_events(dst.readers);
+  int rc = ensure_table(c, dst, (size_t)n_pad);
   if (rc != MSH_OK) return rc;
-  s = c->stream;
-  hipError_t e = msh::launch_node_prep(c->d_unsched, c->d_digit, c->n_nodes, c->n_pad, c->pp.has_nu_filter,
-                                       c->d_ball, c->d_planes, c->d_erows, s, c->d_patch, c->patch_pending);
-  c->patch_pending = 0;
+  // the raw columns: uploaded, or the published ones
+  if (up && n > 0) {
+    if ((rc = node_stage(c, 2 * (size_t)n)) != MSH_OK) return rc;
+    std::memcpy(c->h_nstage, w.unsched, (size_t)n);
+    std::memcpy(c->h_nstage + n, w.digit, (size_t)n);
+    MSH_HIP(c, hipMemcpyAsync(dst.d_unsched, c->h_nstage, (size_t)n, hipMemcpyHostToDevice, ps));
+    MSH_HIP(c, hipMemcpyAsync(dst.d_digit, c->h_nstage + n, (size_t)n, hipMemcpyHostToDevice, ps));
+  } else if (!up && n > 0) {
+    MSH_HIP(c, hipMemcpyAsync(dst.d_unsched, src.d_unsched, (size_t)n, hipMemcpyDeviceToDevice, ps));
+    MSH_HIP(c, hipMemcpyAsync(dst.d_digit, src.d_digit, (size_t)n, hipMemcpyDeviceToDevice, ps));
+  }
+  // score columns: an upload drops them (they belong to the previous table's nodes)
+  for (int k = 0; k < msh::GEN_COLS; ++k) {
+    dst.col_ok[k] = !up && src.col_ok[k];
+    if (w.kind == Rewrite::COLUMN && k == w.col) continue;
+    if (dst.col_ok[k] && n > 0) {
+      if ((rc = ensure_cols(c, dst)) != MSH_OK) return rc;
+      MSH_HIP(c, hipMemcpyAsync(dst.d_cols + (size_t)k * dst.cap, src.d_cols + (size_t)k * src.cap,
+                                (size_t)n * sizeof(int64_t), hipMemcpyDeviceToDevice, ps));
+    }
+  }
+  if (w.kind == Rewrite::COLUMN) {
+    if ((rc = ensure_cols(c, dst)) != MSH_OK) return rc;
+    if (n > 0) {
+      const size_t bytes = (size_t)n * sizeof(int64_t);
+      if ((rc = node_stage(c, bytes)) != MSH_OK) return rc;
+      std::memcpy(c->h_nstage, w.scores, bytes);
+      MSH_HIP(c, hipMemcpyAsync(dst.d_cols + (size_t)w.col * dst.cap, c->h_nstage, bytes, hipMemcpyHostToDevice, ps));
+    }
+    dst.col_ok[w.col] = true;
+  }
+  // patch entries, applied to the copied columns by the prep's reset launch
+  if (w.kind == Rewrite::PATCH) {
+    const size_t pbytes = (size_t)w.patch_count * sizeof(unsigned long long);
+    if ((size_t)w.patch_count > c->patch_cap) {
+      (void)hipFree(c->d_patch);  // last read by a rewrite that has completed
+      c->d_patch = nullptr;
+      c->patch_cap = 0;
+      const size_t cap = std::max<size_t>((size_t)w.patch_count, 256);
+      MSH_HIP(c, hipMalloc(&c->d_patch, cap * sizeof(unsigned long long)));
+      c->patch_cap = cap;
+    }
+    if ((rc = node_stage(c, pbytes)) != MSH_OK) return rc;
+    std::memcpy(c->h_nstage, c->h_patch.data(), pbytes);
+    MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_nstage, pbytes, hipMemcpyHostToDevice, ps));
+  }
+  hipError_t e = msh::launch_node_prep(dst.d_unsched, dst.d_digit, n, n_pad, c->pp.has_nu_filter, dst.d_ball,
+                                       dst.d_planes, dst.d_erows, ps, c->d_patch,
+                                       w.kind == Rewrite::PATCH ? w.patch_count : 0);
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
-  MSH_HIP(c, hipStreamSynchronize(s));
-  c->dirty = false;
+  // an upload zeroes the sequential-mode counts (after the sequential launches in flight)
+  if (up) {
+    if ((size_t)n_pad > c->counts_cap) {
+      wait_events(c->seq_inflight);
+      (void)hipFree(c->d_counts);
+      c->d_counts = nullptr;
+      c->counts_cap = 0;
+      MSH_HIP(c, hipMalloc(&c->d_counts, (size_t)n_pad * sizeof(int32_t)));
+      c->counts_cap = (size_t)n_pad;
+    }
+    if ((rc = after_seq(c)) != MSH_OK) return rc;
+    MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->counts_cap * sizeof(int32_t), ps));
+  }
+  MSH_HIP(c, hipStreamSynchronize(ps));
+  c->cur = s;
+  c->n_nodes = n;
+  c->n_pad = n_pad;
+  c->have_nodes = true;
+  return MSH_OK;
+}
+
+// One hot-kernel launch under msh_timing_begin: arms the next event pair for the launcher on this
+// thread; a launcher that launched nothing leaves it unused.
+struct TimedLaunch {
+  msh_ctx* c;
+  bool armed = false;
+  explicit TimedLaunch(msh_ctx* ctx) : c(ctx) {
+    if (c->timing && c->t_next < c->tev.size()) {
+      msh::set_launch_events(c->tev[c->t_next].first, c->tev[c->t_next].second);
+      armed = true;
+    }
+  }
+  ~TimedLaunch() {
+    if (!armed) return;
+    if (msh::launch_events_pending()) msh::set_launch_events(nullptr, nullptr);
+    else ++c->t_next;
+  }
+};
+
+// Launch-path check: the tables are always published ready (rewrites are synchronous).
+int ready(msh_ctx* c) {
+  if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   return MSH_OK;
 }
 
 msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t* pt) {
   msh::BatchArgs a{};
-  a.planes = c->d_planes;
-  a.erows = c->d_erows;
+  const NodeTable& t = cur_table(c);
+  a.planes = t.d_planes;
+  a.erows = t.d_erows;
   a.n_groups = c->n_pad / msh::GROUP_NODES;
   a.pod_digit = pd;
   a.pod_tol = pt;
   a.n_pods = p;
-  a.ball = c->d_ball;
+  a.ball = t.d_ball;
   a.pp = c->pp;
   return a;
 }
@@ -350,10 +506,11 @@ bool use_generic(const msh_ctx* c) { return c->generic || c->dev.batch_kernel ==
 
 int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   g = msh::GenericArgs{};
-  g.unsched = c->d_unsched;
-  g.digit = c->d_digit;
-  g.cols = c->d_cols;
-  g.col_stride = (int64_t)c->node_cap;
+  const NodeTable& t = cur_table(c);
+  g.unsched = t.d_unsched;
+  g.digit = t.d_digit;
+  g.cols = t.d_cols;
+  g.col_stride = (int64_t)t.cap;
   g.n_nodes = c->n_nodes;
   g.has_nu = c->pp.has_nu_filter;
   g.nn_prescore = c->pp.nn_prescore;
@@ -362,7 +519,7 @@ int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   for (int32_t k = 0; k < g.ns; ++k) {
     const int32_t id = c->score_ids[k];
     g.kind[k] = id == MSH_PLUGIN_NODE_NUMBER ? 0 : 1 + (id - MSH_PLUGIN_SCORE_COLUMN0);
-    if (g.kind[k] > 0 && !c->col_ok[g.kind[k] - 1])
+    if (g.kind[k] > 0 && !t.col_ok[g.kind[k] - 1])
       return fail(c, MSH_ERR_STATE, "score column " + std::to_string(id) + " not uploaded since the last node upload");
     g.mode[k] = c->normalize[k];
     g.weight[k] = c->weights[k];
@@ -382,6 +539,7 @@ int launch_generic_batch(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t*
   g.out_idx = oi;
   g.out_score = os;
   g.out_status = ost;
+  TimedLaunch tl(c);
   hipError_t e = msh::launch_generic(g, s);
   if (e != hipSuccess) return hip_fail(c, e, "generic_kernel");
   return MSH_OK;
@@ -596,14 +754,11 @@ int msh_create(int device, msh_ctx** out_ctx) {
     g_create_err = bad;
     return MSH_ERR_INVALID;
   }
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
-    return MSH_ERR_HIP;
-  }
-  if (hipMalloc(&c->d_ball, 2 * sizeof(uint32_t)) != hipSuccess ||
-      hipMemset(c->d_ball, 0, 2 * sizeof(uint32_t)) != hipSuccess) {
-    (void)hipFree(c->d_ball);
-    (void)hipStreamDestroy(c->stream);
+  int lo_prio = 0, hi_prio = 0;  // numerically lower = higher priority
+  if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) hi_prio = 0;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->prep_stream, hipStreamNonBlocking, hi_prio) != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return MSH_ERR_HIP;
   }
@@ -622,19 +777,29 @@ void msh_destroy(msh_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
   // launches this ctx queued on caller streams (the *_device entry points) may still read the tables
-  wait_inflight(c);
+  for (NodeTable& t : c->tab) wait_events(t.readers);
+  wait_events(c->seq_inflight);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (auto& e : c->inflight) (void)hipEventDestroy(e.second);
+  if (c->prep_stream) (void)hipStreamSynchronize(c->prep_stream);
+  for (NodeTable& t : c->tab) {
+    destroy_events(t.readers);
+    free_table(t);
+  }
+  destroy_events(c->seq_inflight);
+  (void)hipFree(c->d_counts);
   for (hipEvent_t e : c->async_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
-  free_nodes(c);
+  for (auto& e : c->tev) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
   free_pods(c);
   (void)hipHostFree(c->h_stage);
   (void)hipHostFree(c->h_nstage);
   (void)hipFree(c->d_patch);
-  (void)hipFree(c->d_ball);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->prep_stream) (void)hipStreamDestroy(c->prep_stream);
   delete c;
 }
 
@@ -677,10 +842,15 @@ int msh_set_plugins_ex(msh_ctx* c, const int32_t* filter_ids, int32_t nf,
       pp.weight = c->weights[i];
     }
   }
-  if (pp.has_nu_filter != c->pp.has_nu_filter) c->dirty = true;
+  const bool reprep = pp.has_nu_filter != c->pp.has_nu_filter;  // the X words depend on the filter list
   c->pp = pp;
   c->generic = false;
   for (int32_t i = 0; i < ns; i++) c->generic = c->generic || is_column(c->score_ids[i]);
+  if (reprep && c->have_nodes) {
+    DeviceGuard g(c->device);
+    Rewrite w{Rewrite::REPREP};
+    return rewrite(c, w);
+  }
   return MSH_OK;
 }
 
@@ -700,40 +870,11 @@ int msh_upload_nodes(msh_ctx* c, int32_t n, const uint8_t* unsched, const int8_t
   if (n < 0 || n > msh::MAX_NODES) return fail(c, MSH_ERR_INVALID, "node count outside [0, 2^24-2]");
   if (n > 0 && (!unsched || !digit)) return fail(c, MSH_ERR_INVALID, "null node arrays");
   DeviceGuard g(c->device);
-  // launches this ctx queued earlier may still read the tables rewritten below: the copies below go
-  // behind them on the ctx's stream, and a reallocation first waits for them on the host
-  int rc = after_inflight(c);
-  if (rc != MSH_OK) return rc;
-  // Padded to whole 1,024-node blocks, and never empty: an empty cluster is a table of padding
-  // slots (infeasible for every pod), so every pod gets FitError from the kernel.
-  const int32_t n_pad = std::max(((n + msh::NODE_PAD - 1) / msh::NODE_PAD) * msh::NODE_PAD, msh::NODE_PAD);
-  if ((size_t)n_pad > c->node_cap || c->d_planes == nullptr) {
-    wait_inflight(c);
-    MSH_HIP(c, hipStreamSynchronize(c->stream));
-    free_nodes(c);
-    const size_t cap = (size_t)n_pad;
-    MSH_HIP(c, hipMalloc(&c->d_unsched, cap));
-    MSH_HIP(c, hipMalloc(&c->d_digit, cap));
-    MSH_HIP(c, hipMalloc(&c->d_counts, cap * sizeof(int32_t)));
-    MSH_HIP(c, hipMalloc(&c->d_planes, cap / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
-    // + ER_PAD groups: the batch kernel copies whole tiles without clamping (never read as rows)
-    MSH_HIP(c, hipMalloc(&c->d_erows, (cap / msh::GROUP_NODES + msh::ER_PAD) * msh::ER_GD * sizeof(uint32_t)));
-    c->node_cap = cap;
-  }
-  if (n > 0) {
-    if ((rc = node_stage(c, 2 * (size_t)n)) != MSH_OK) return rc;
-    std::memcpy(c->h_nstage, unsched, (size_t)n);
-    std::memcpy(c->h_nstage + n, digit, (size_t)n);
-    MSH_HIP(c, hipMemcpyAsync(c->d_unsched, c->h_nstage, (size_t)n, hipMemcpyHostToDevice, c->stream));
-    MSH_HIP(c, hipMemcpyAsync(c->d_digit, c->h_nstage + n, (size_t)n, hipMemcpyHostToDevice, c->stream));
-  }
-  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->node_cap * sizeof(int32_t), c->stream));
-  for (bool& ok : c->col_ok) ok = false;  // score columns belong to the previous table's nodes
-  c->n_nodes = n;
-  c->n_pad = n_pad;
-  c->have_nodes = true;
-  c->dirty = true;
-  return prepare(c, c->stream);  // synchronous
+  Rewrite w{Rewrite::UPLOAD};
+  w.n = n;
+  w.unsched = unsched;
+  w.digit = digit;
+  return rewrite(c, w);  // synchronous; launches in flight keep the previous version
 }
 
 int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t* unsched,
@@ -756,25 +897,9 @@ int msh_patch_nodes(msh_ctx* c, int32_t count, const int32_t* idx, const uint8_t
                     ((unsigned long long)(unsched[k] ? 1u : 0u) << 32) |
                     ((unsigned long long)(uint8_t)digit[k] << 40);
   DeviceGuard g(c->device);
-  // d_patch is only read by the prep launch of an earlier (synchronous) prepare; the columns and the
-  // tables the entries change are rewritten by prepare(), behind this ctx's launches in flight
-  if ((size_t)count > c->patch_cap) {
-    (void)hipFree(c->d_patch);
-    c->d_patch = nullptr;
-    c->patch_cap = 0;
-    const size_t cap = std::max<size_t>((size_t)count, 256);
-    MSH_HIP(c, hipMalloc(&c->d_patch, cap * sizeof(unsigned long long)));
-    c->patch_cap = cap;
-  }
-  const size_t pbytes = (size_t)count * sizeof(unsigned long long);
-  int rc = node_stage(c, pbytes);
-  if (rc != MSH_OK) return rc;
-  std::memcpy(c->h_nstage, c->h_patch.data(), pbytes);
-  MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_nstage, pbytes, hipMemcpyHostToDevice, c->stream));
-  // the entries are applied by the prep's reset launch, then the derived tables are rebuilt
-  c->patch_pending = count;
-  c->dirty = true;
-  return prepare(c, c->stream);  // synchronous
+  Rewrite w{Rewrite::PATCH};
+  w.patch_count = count;
+  return rewrite(c, w);  // synchronous; launches in flight keep the previous version
 }
 
 int msh_export_results(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
@@ -790,8 +915,8 @@ int msh_export_results(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   if (!pod_digit || !pod_tol || !out_filter || !out_score || !out_final)
     return fail(c, MSH_ERR_INVALID, "null pointer");
   DeviceGuard g(c->device);
-  int rc = prepare(c, c->stream);
-  if (rc != MSH_OK) return rc;
+  int rc = MSH_OK;
+  const NodeTable& t = cur_table(c);
   int8_t* d_pd = nullptr;
   uint8_t* d_pt = nullptr;
   uint8_t* d_f = nullptr;
@@ -808,7 +933,7 @@ int msh_export_results(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   if (rc == MSH_OK) {
     step(hipMemcpyAsync(d_pd, pod_digit, (size_t)p, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync");
     step(hipMemcpyAsync(d_pt, pod_tol, (size_t)p, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync");
-    step(msh::launch_export(c->d_unsched, c->d_digit, c->n_nodes, d_pd, d_pt, p, c->pp, d_f, d_r, d_o,
+    step(msh::launch_export(t.d_unsched, t.d_digit, c->n_nodes, d_pd, d_pt, p, c->pp, d_f, d_r, d_o,
                             c->stream), "export_kernel");
     step(hipMemcpyAsync(out_filter, d_f, pairs, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync");
     step(hipMemcpyAsync(out_score, d_r, pairs * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream),
@@ -832,20 +957,10 @@ int msh_upload_score_column(msh_ctx* c, int32_t plugin_id, int32_t n, const int6
     if (scores[i] < -(int64_t(1) << 31) || scores[i] > (int64_t(1) << 31))
       return fail(c, MSH_ERR_INVALID, "score column value outside [-2^31, 2^31] at node " + std::to_string(i));
   DeviceGuard g(c->device);
-  int rc = after_inflight(c);  // generic launches of this ctx in flight may read the column
-  if (rc != MSH_OK) return rc;
-  if (!c->d_cols) MSH_HIP(c, hipMalloc(&c->d_cols, (size_t)msh::GEN_COLS * c->node_cap * sizeof(int64_t)));
-  const int k = plugin_id - MSH_PLUGIN_SCORE_COLUMN0;
-  if (n > 0) {
-    const size_t bytes = (size_t)n * sizeof(int64_t);
-    if ((rc = node_stage(c, bytes)) != MSH_OK) return rc;
-    std::memcpy(c->h_nstage, scores, bytes);
-    MSH_HIP(c, hipMemcpyAsync(c->d_cols + (size_t)k * c->node_cap, c->h_nstage, bytes, hipMemcpyHostToDevice,
-                              c->stream));
-  }
-  MSH_HIP(c, hipStreamSynchronize(c->stream));
-  c->col_ok[k] = true;
-  return MSH_OK;
+  Rewrite w{Rewrite::COLUMN};
+  w.col = plugin_id - MSH_PLUGIN_SCORE_COLUMN0;
+  w.scores = scores;
+  return rewrite(c, w);  // generic launches in flight keep reading the previous version
 }
 
 int msh_num_nodes(const msh_ctx* c, int32_t* out_n) {
@@ -864,7 +979,7 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
     return fail(c, MSH_ERR_INVALID, "null device pointer");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int rc = prepare(c, s);
+  int rc = ready(c);
   if (rc != MSH_OK) return rc;
   if (use_generic(c)) {
     if (p == 0) return MSH_OK;
@@ -876,7 +991,11 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   a.out_idx = d_out_idx;
   a.out_score = d_out_score;
   a.out_status = d_out_status;
-  hipError_t e = msh::launch_batch(a, false, c->dev, s);
+  hipError_t e;
+  {
+    TimedLaunch tl(c);
+    e = msh::launch_batch(a, false, c->dev, s);
+  }
   if (e != hipSuccess) return hip_fail(c, e, "batch kernel");
   return p > 0 ? track_launch(c, s) : MSH_OK;
 }
@@ -894,7 +1013,7 @@ int msh_schedule_batches_device(msh_ctx* c, int32_t nb, const msh_batch* batches
   }
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int rc = prepare(c, s);
+  int rc = ready(c);
   if (rc != MSH_OK) return rc;
   if (use_generic(c)) {  // one generic launch per batch
     for (int32_t i = 0; i < nb; ++i) {
@@ -917,11 +1036,13 @@ int msh_schedule_batches_device(msh_ctx* c, int32_t nb, const msh_batch* batches
         a.out_idx = b.out_idx;
         a.out_score = b.out_score;
         a.out_status = b.out_status;
+        TimedLaunch tl(c);
         hipError_t e = msh::launch_batch(a, false, c->dev, s);
         if (e != hipSuccess) return hip_fail(c, e, "batch kernel");
       }
     }
     if (single) continue;
+    TimedLaunch tl(c);
     hipError_t e = msh::launch_batches(batch_args(c, 0, nullptr, nullptr), d, n, c->dev, s);
     if (e != hipSuccess) return hip_fail(c, e, "wg_kernel (multi-batch)");
   }
@@ -938,7 +1059,7 @@ int msh_schedule_batch(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uin
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (p == 0) return MSH_OK;
   DeviceGuard g(c->device);
-  int rc = prepare(c, c->stream);
+  int rc = ready(c);
   if (rc != MSH_OK) return rc;
   HostIO io;
   if ((rc = host_io_begin(c, p, pod_digit, pod_tol, out_idx, out_score, out_status, io)) != MSH_OK) return rc;
@@ -967,7 +1088,7 @@ int msh_schedule_batch_async(msh_ctx* c, int32_t p, const int8_t* pod_digit, con
     if (!dpd || !dpt || !doi || !dost || (out_score && !dos))
       return fail(c, MSH_ERR_INVALID, "msh_schedule_batch_async needs page-locked buffers (msh_host_alloc)");
   }
-  int rc = prepare(c, c->stream);
+  int rc = ready(c);
   if (rc != MSH_OK) return rc;
   if (c->async_issued - c->async_done >= MSH_ASYNC_DEPTH) {  // the ring is full: wait for the oldest
     const uint64_t t = c->async_done + 1;
@@ -1010,12 +1131,13 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   if (c->generic) return fail(c, MSH_ERR_UNSUPPORTED, "score-column plugins run on the batch entry points only");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int rc = prepare(c, s);
+  int rc = ready(c);
   if (rc != MSH_OK) return rc;
   msh::SeqArgs a{};
-  a.planes = c->d_planes;
+  const NodeTable& t = cur_table(c);
+  a.planes = t.d_planes;
   a.n_words = c->n_pad / 32;
-  a.ball = c->d_ball;
+  a.ball = t.d_ball;
   a.n_nodes = c->n_nodes;
   a.pod_digit = d_pod_digit;
   a.pod_tol = d_pod_tol;
@@ -1027,12 +1149,16 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   a.out_score = d_out_score;
   a.out_status = d_out_status;
   std::string err;
-  hipError_t e = msh::launch_sequential(a, c->dev, s, &err);
+  hipError_t e;
+  {
+    TimedLaunch tl(c);
+    e = msh::launch_sequential(a, c->dev, s, &err);
+  }
   if (e != hipSuccess) {
     if (!err.empty()) return fail(c, MSH_ERR_UNSUPPORTED, err);
     return hip_fail(c, e, "seq_kernel");
   }
-  return p > 0 ? track_launch(c, s) : MSH_OK;
+  return p > 0 ? track_launch(c, s, true) : MSH_OK;
 }
 
 int msh_schedule_sequential(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
@@ -1046,7 +1172,7 @@ int msh_schedule_sequential(msh_ctx* c, int32_t p, const int8_t* pod_digit, cons
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   if (p == 0) return MSH_OK;
   DeviceGuard g(c->device);
-  int rc = prepare(c, c->stream);
+  int rc = ready(c);
   if (rc != MSH_OK) return rc;
   HostIO io;
   if ((rc = host_io_begin(c, p, pod_digit, pod_tol, out_idx, out_score, out_status, io)) != MSH_OK) return rc;
@@ -1067,11 +1193,11 @@ int msh_node_pod_counts(msh_ctx* c, int32_t* out_counts) {
   if (c->n_nodes > 0 && !out_counts) return fail(c, MSH_ERR_INVALID, "null output");
   if (c->n_nodes == 0) return MSH_OK;
   DeviceGuard g(c->device);
-  int rc = after_inflight(c);  // sequential launches of this ctx in flight update the counts
+  int rc = after_seq(c);  // sequential launches of this ctx in flight update the counts
   if (rc != MSH_OK) return rc;
   MSH_HIP(c, hipMemcpyAsync(out_counts, c->d_counts, (size_t)c->n_nodes * sizeof(int32_t), hipMemcpyDeviceToHost,
-                            c->stream));
-  MSH_HIP(c, hipStreamSynchronize(c->stream));
+                            c->prep_stream));
+  MSH_HIP(c, hipStreamSynchronize(c->prep_stream));
   return MSH_OK;
 }
 
@@ -1080,10 +1206,10 @@ int msh_reset_node_pod_counts(msh_ctx* c) {
   c->err.clear();
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   DeviceGuard g(c->device);
-  int rc = after_inflight(c);  // sequential launches of this ctx in flight update the counts
+  int rc = after_seq(c);  // sequential launches of this ctx in flight update the counts
   if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->node_cap * sizeof(int32_t), c->stream));
-  MSH_HIP(c, hipStreamSynchronize(c->stream));
+  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->counts_cap * sizeof(int32_t), c->prep_stream));
+  MSH_HIP(c, hipStreamSynchronize(c->prep_stream));
   return MSH_OK;
 }
 
@@ -1112,7 +1238,7 @@ int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   if (c->generic) return fail(c, MSH_ERR_UNSUPPORTED, "score-column plugins run on the batch entry points only");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int rc = prepare(c, s);
+  int rc = ready(c);
   if (rc != MSH_OK) return rc;
   msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
   a.keys = d_keys;
@@ -1136,6 +1262,46 @@ int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   hipError_t e = msh::launch_decode_keys(d_pod_digit, d_pod_tol, p, d_keys, slot1_any, c->pp,
                                          d_out_idx, d_out_score, d_out_status, s);
   if (e != hipSuccess) return hip_fail(c, e, "decode_keys_kernel");
+  return MSH_OK;
+}
+
+int msh_timing_begin(msh_ctx* c, int32_t max_launches) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (max_launches < 1 || max_launches > 4096) return fail(c, MSH_ERR_INVALID, "max_launches outside [1, 4096]");
+  DeviceGuard g(c->device);
+  while (c->tev.size() < (size_t)max_launches) {
+    hipEvent_t a = nullptr, b = nullptr;
+    MSH_HIP(c, hipEventCreate(&a));
+    if (hipEventCreate(&b) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      return fail(c, MSH_ERR_HIP, "hipEventCreate");
+    }
+    c->tev.emplace_back(a, b);
+  }
+  c->timing = true;
+  c->t_next = 0;
+  return MSH_OK;
+}
+
+int msh_timing_end(msh_ctx* c, int32_t* out_launches, double* out_total_ms, double* out_max_ms) {
+  if (!c || !out_launches || !out_total_ms) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (!c->timing) return fail(c, MSH_ERR_STATE, "msh_timing_begin has not been called");
+  DeviceGuard g(c->device);
+  c->timing = false;
+  double total = 0, mx = 0;
+  for (size_t i = 0; i < c->t_next; ++i) {
+    MSH_HIP(c, hipEventSynchronize(c->tev[i].second));
+    float ms = 0;
+    MSH_HIP(c, hipEventElapsedTime(&ms, c->tev[i].first, c->tev[i].second));
+    total += ms;
+    mx = std::max(mx, (double)ms);
+  }
+  *out_launches = (int32_t)c->t_next;
+  *out_total_ms = total;
+  if (out_max_ms) *out_max_ms = mx;
+  c->t_next = 0;
   return MSH_OK;
 }
 

@@ -125,7 +125,8 @@ struct BatchArgs {
 hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s);
 
 // One batch of a multi-batch launch (msh_schedule_batches_device): its own pod columns and
-// outputs; blk_end = the launch's workgroups up to and including this batch's (exclusive prefix).
+// outputs. The launch grid is 2-D: blockIdx.y = the batch, blockIdx.x = the pod block within it
+// (the x extent is the largest batch's; a workgroup past its batch's end exits at once).
 struct BatchDesc {
   const int8_t* pod_digit;
   const uint8_t* pod_tol;
@@ -133,9 +134,9 @@ struct BatchDesc {
   int64_t* out_score;  // may be null
   int32_t* out_status;
   int32_t n_pods;
-  int32_t blk_end;
+  int32_t reserved;
 };
-constexpr int MULTI_MAX = 8;  // batches per launch (kernel-argument descriptors, 48 B each)
+constexpr int MULTI_MAX = 32;  // batches per launch (kernel-argument descriptors, 48 B each: ~1.7 KB)
 struct MultiArgs {
   BatchArgs a;  // the node table, plugin set and launch geometry (its pod / output fields unused)
   int32_t nb;
@@ -194,5 +195,10 @@ struct SeqArgs {
 };
 
 hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err);
+
+// Launch timing (msh_timing_begin / _end): the next hot-kernel launch on this thread (batch, multi-
+// batch, generic, sequential kernels) records `start` / `stop` at the kernel's own start and end.
+void set_launch_events(hipEvent_t start, hipEvent_t stop);
+bool launch_events_pending();
 
 }  // namespace msh

@@ -35,9 +35,32 @@
 // See DESIGN.md for the roofline / instruction budget of each kernel.
 #include "msh_internal.h"
 
+#include <hip/hip_ext.h>
+
 #include <type_traits>
 
 namespace msh {
+
+// Kernel start / stop events for the next hot-kernel launch on this thread (msh_timing_begin):
+// hipExtLaunchKernelGGL records them at the kernel's own start and completion, the interval
+// rocprofv3's kernel trace reports, not around the launch like events recorded on the stream.
+namespace {
+thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+}
+void set_launch_events(hipEvent_t start, hipEvent_t stop) {
+  t_ev_start = start;
+  t_ev_stop = stop;
+}
+bool launch_events_pending() { return t_ev_start != nullptr; }
+#define MSH_TIMED_LAUNCH(kern, grid, block, lds, stream, ...)                                                   \
+  do {                                                                                                          \
+    if (t_ev_start) {                                                                                           \
+      hipExtLaunchKernelGGL(kern, grid, block, lds, stream, t_ev_start, t_ev_stop, 0, __VA_ARGS__);             \
+      t_ev_start = t_ev_stop = nullptr;                                                                         \
+    } else {                                                                                                    \
+      hipLaunchKernelGGL(kern, grid, block, lds, stream, __VA_ARGS__);                                          \
+    }                                                                                                           \
+  } while (0)
 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
@@ -738,25 +761,42 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
 // ---------------------------------------------------------------------------------------
 // Workgroup-table batched kernel (the default batch path since round 3).
 //
-// The same per-pair evaluation as rows_kernel (lanes = pods, per lane and 32-node word
-// hit = E[row] & ~(X & nT), one v_bitop3_b32), but the node side is staged ONCE per workgroup:
-// the W waves of a workgroup (W x 64 pods) copy the digit rows and X words (KX: and the V words)
-// of up to WG_CHUNK groups into LDS together, and every wave then scans every group of the table
-// for its own 64 pods. No slices, so no slice merge and no per-wave tile copies (rows_kernel's
-// S slice waves each copied their own tile). Groups are walked in descending List order and a
-// group with a hit pushes a 1 into a per-chunk bitmap (bit k = group lo + k), two VALU per group
-// (v_min_u32 + v_lshl_or_b32) where rows_kernel kept a running index (compare, move, select);
-// the first group with a hit is the lowest set bit of the lowest chunk's bitmap that has one, and
-// its hit words are recomputed from LDS once per lane at the end (from memory when it lies in a
-// chunk that is no longer staged: more than WG_CHUNK groups above the first with a hit, rare).
-// Tables larger than one chunk are streamed chunk by chunk, descending: the next chunk's copy is in
-// flight in registers while the current one is scanned (two workgroup barriers per chunk).
+// Lanes = pods, as in rows_kernel, but the node side is staged ONCE per workgroup: the W waves of a
+// workgroup (W x 64 pods) copy the digit rows and X words (KX: and the V words) of up to WG_CHUNK
+// groups into LDS together, and every wave then scans every group of the table for its own 64 pods.
+// No slices, so no slice merge and no per-wave tile copies. Per lane and 256-node group the scan
+// folds the pair evaluation and the group's OR into one v_bitop3 per 32-node word:
+//   acc = acc | (E[row] & ~X')        truth table 0xF4 (the first word: E & ~X', 0x44)
+// where X' is the group's X words for a pod that does not tolerate the unschedulable taint and a
+// zero block staged next to them for one that does (NodeUnschedulable per pair: a tolerating pod
+// passes every real node); the lane picks its block once, by address. A group whose acc is non-zero
+// holds a feasible digit match: it pushes a 1 into a per-chunk bitmap (bit k = group lo + k; v_min +
+// v_lshl_or per group). 11 VALU per group and lane (8 bitop3, the flag, the addresses) against
+// rows_kernel's 16; KX also accumulates the feasible non-matches, acc' |= V & ~(E | X') (v_or +
+// v_bitop3 per word). Groups are walked in descending List order; the first group with a hit is the
+// lowest set bit of the lowest chunk's bitmap that has one, and its hit words are recomputed once per
+// lane at the end (from LDS, or from memory when it lies in a chunk no longer staged: more than
+// WG_CHUNK groups above the first with a hit, rare). Tables larger than one chunk are streamed chunk
+// by chunk, descending: the next chunk's copy is in flight in registers while the current one is
+// scanned (two workgroup barriers per chunk).
 //
 // MULTI: the launch serves up to MULTI_MAX independent batches (msh_schedule_batches_device), each
-// with its own pod columns and outputs, described in the kernel arguments; a workgroup finds its
-// batch by the exclusive prefix of workgroups (a scalar count over at most 7 compares).
+// with its own pod columns and outputs, described in the kernel arguments; the grid is 2-D, batch =
+// blockIdx.y (one scalar load of its descriptor).
 // ---------------------------------------------------------------------------------------
-constexpr int WG_CHUNK = 32;  // groups per staged chunk (8,192 nodes; 12 KiB, 13 KiB with V words)
+// Phase experiments of the stamps build only (scripts/wg_expt.sh; never the product library):
+// bit 0 skips the scan loop, bit 1 the output stores, bit 2 the table copy into LDS. MSH_WG_FLAG
+// selects the form of the per-group flag (A/B of the same build).
+#ifndef MSH_WG_EXPT
+#define MSH_WG_EXPT 0
+#endif
+#ifndef MSH_WG_FLAG
+#define MSH_WG_FLAG 0
+#endif
+constexpr int WG_CHUNK = 32;  // groups per staged chunk (8,192 nodes; 13 KiB, 14 KiB with V words)
+// LDS layout of a staged group, in 16-byte entries: the 22 row chunks, X (2), a zero block Z (2) that
+// tolerating pods read instead of X, and (KX) V (2)
+constexpr int LQ_X = ER_Q, LQ_Z = ER_GQ, LQ_V = ER_GQ + 2;
 
 template <bool MULTI>
 struct KArgs {
@@ -769,13 +809,63 @@ struct KArgs<true> {
 __device__ __forceinline__ const BatchArgs& base_args(const BatchArgs& a) { return a; }
 __device__ __forceinline__ const BatchArgs& base_args(const MultiArgs& m) { return m.a; }
 
+// acc | (e & ~x), one v_bitop3_b32 (S0 = acc, S1 = e, S2 = x). The builtin, not inline asm: the
+// compiler then knows the instruction's hazards (inline asm got a conservative s_nop after each pair).
+__device__ __forceinline__ uint32_t acc_andn(uint32_t acc, uint32_t e, uint32_t x) {
+  return __builtin_amdgcn_bitop3_b32(acc, e, x, 0xf4);
+}
+// e & ~x (the first word of a group: S0 is a don't-care)
+__device__ __forceinline__ uint32_t andn(uint32_t e, uint32_t x) { return __builtin_amdgcn_bitop3_b32(e, e, x, 0x44); }
+__device__ __forceinline__ uint32_t min1(uint32_t x) {  // x != 0 as 0 / 1 in one v_min_u32
+  uint32_t r;
+  asm("v_min_u32 %0, 1, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t sh, uint32_t b) {  // (a << sh) | b
+  uint32_t r;
+  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(sh), "v"(b));
+  return r;
+}
+
+// One staged group for one lane: the OR over its 8 words of the feasible digit matches (hit) and, KX,
+// of the feasible non-matches (nm). tr: the lane's row entry, tx: the lane's X or Z entry, tv: V.
+template <bool KX>
+__device__ __forceinline__ void group_acc(const uint4* tr, const uint4* tx, const uint4* tv, uint32_t& hit,
+                                          uint32_t& nm) {
+  const uint4 e0 = tr[0], e1 = tr[ER_ROWS], x0 = tx[0], x1 = tx[1];
+  hit = andn(e0.x, x0.x);
+  hit = acc_andn(hit, e0.y, x0.y);
+  hit = acc_andn(hit, e0.z, x0.z);
+  hit = acc_andn(hit, e0.w, x0.w);
+  hit = acc_andn(hit, e1.x, x1.x);
+  hit = acc_andn(hit, e1.y, x1.y);
+  hit = acc_andn(hit, e1.z, x1.z);
+  hit = acc_andn(hit, e1.w, x1.w);
+  if constexpr (KX) {
+    const uint4 v0 = tv[0], v1 = tv[1];
+    nm = andn(v0.x, e0.x | x0.x);
+    nm = acc_andn(nm, v0.y, e0.y | x0.y);
+    nm = acc_andn(nm, v0.z, e0.z | x0.z);
+    nm = acc_andn(nm, v0.w, e0.w | x0.w);
+    nm = acc_andn(nm, v1.x, e1.x | x1.x);
+    nm = acc_andn(nm, v1.y, e1.y | x1.y);
+    nm = acc_andn(nm, v1.z, e1.z | x1.z);
+    nm = acc_andn(nm, v1.w, e1.w | x1.w);
+  }
+}
+
 template <int W, bool KX, bool SHARD, bool MULTI>
 __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T ka) {
   static_assert(!(SHARD && MULTI), "shard keys come from single-batch launches");
-  constexpr int GQ = KX ? ER_GQ + 2 : ER_GQ;                     // 16-byte entries per staged group
+  constexpr int GQ = KX ? ER_GQ + 2 : ER_GQ;                     // 16-byte entries per group in memory
+  constexpr int GQL = KX ? LQ_V + 2 : LQ_Z + 2;                  // ... per staged group in LDS
   constexpr int NT = W * WAVE;                                   // threads per workgroup
   constexpr int EPT = (WG_CHUNK * GQ + NT - 1) / NT;             // staged entries per thread per chunk
-  __shared__ uint4 s_tab[WG_CHUNK * GQ];
+  __shared__ uint4 s_tab[WG_CHUNK * GQL];
+#ifdef MSH_STAMPS
+  unsigned long long stamp_t[4] = {0, 0, 0, 0};
+  MSH_STAMP(0);
+#endif
   const BatchArgs& A = base_args(ka);
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -789,12 +879,8 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
   int32_t* out_status = A.out_status;
   int32_t n_pods = A.n_pods;
   if constexpr (MULTI) {
-    int b = 0;
-#pragma unroll
-    for (int k = 0; k < MULTI_MAX - 1; ++k) b += (k + 1 < ka.nb && blk >= ka.d[k].blk_end) ? 1 : 0;
-    b = __builtin_amdgcn_readfirstlane(b);
-    if (b > 0) blk -= ka.d[b - 1].blk_end;
-    const BatchDesc& d = ka.d[b];
+    const BatchDesc& d = ka.d[blockIdx.y];
+    if (blk * NT >= d.n_pods) return;  // past this batch's end (the grid's x extent is the largest batch's)
     pod_digit = d.pod_digit;
     pod_tol = d.pod_tol;
     out_idx = d.out_idx;
@@ -817,6 +903,7 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
   uint4 st0, st1, st2, st3;
   auto st_ref = [&](int k) -> uint4& { return k == 0 ? st0 : k == 1 ? st1 : k == 2 ? st2 : st3; };
   auto chunk_load = [&](int32_t c) {
+    if constexpr ((MSH_WG_EXPT & 4) != 0) return;
     const int32_t glo = c * WG_CHUNK, last = min(WG_CHUNK, n_groups - glo) * GQ - 1;
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
@@ -832,39 +919,35 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
       }
     }
   };
-  auto chunk_store = [&]() {
+  auto chunk_store = [&]() {  // memory entry i of group gi -> LDS entry gi * GQL + q (V past Z)
+    if constexpr ((MSH_WG_EXPT & 4) != 0) return;
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int32_t i = (int32_t)threadIdx.x + k * NT;
-      if ((k + 1) * NT <= WG_CHUNK * GQ || i < WG_CHUNK * GQ) s_tab[i] = st_ref(k);
+      const int32_t gi = i / GQ, q = i - gi * GQ;
+      if ((k + 1) * NT <= WG_CHUNK * GQ || i < WG_CHUNK * GQ) s_tab[gi * GQL + q + (q >= ER_GQ ? 2 : 0)] = st_ref(k);
     }
   };
 
   // ---- prologue: the top chunk's copy, the pod bytes (clamped offset) and the class firsts in
-  // flight together ----
+  // flight together; the zero blocks written once ----
   chunk_load(n_chunks - 1);
   const uint32_t lastp = n_pods > 0 ? (uint32_t)(n_pods - 1) : 0u;
   const uint32_t jj = min((uint32_t)j, lastp);
   const int dq = pod_digit[jj];
   const uint8_t tq = pod_tol[jj];
   const uint32_t ball0 = A.ball[0], ball1 = A.ball[1];
+  if (threadIdx.x < 2 * WG_CHUNK) s_tab[(threadIdx.x >> 1) * GQL + LQ_Z + (threadIdx.x & 1)] = make_uint4(0, 0, 0, 0);
   chunk_store();
   const bool act = j < n_pods;
   const uint32_t code = (act && dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;
   const uint32_t tol = (act && tq) ? 1u : 0u;
   const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
   const uint32_t row = code <= 9u ? code : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
+  const uint32_t xq = tol ? (uint32_t)LQ_Z : (uint32_t)LQ_X;           // X, or the zero block
   __syncthreads();
+  MSH_STAMP(1);
 
-  // hits of one staged group (and KX: feasible non-matches); returns the OR of the words
-  auto group_words = [&](const uint4* tg, uint32_t (&h)[PLANE_GW], uint32_t (&nm)[PLANE_GW]) {
-    const uint4 e0 = tg[row], e1 = tg[ER_ROWS + row], x0 = tg[ER_Q], x1 = tg[ER_Q + 1];
-    rows_hits(e0, e1, x0, x1, nT, h);
-    if constexpr (KX) rows_nonmatch(e0, e1, x0, x1, tg[ER_GQ], tg[ER_GQ + 1], nT, nm);
-  };
-  auto or8 = [](const uint32_t (&h)[PLANE_GW]) {
-    return ((h[0] | h[1] | h[2]) | (h[3] | h[4] | h[5])) | (h[6] | h[7]);
-  };
   uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group with a feasible match / non-match
   for (int32_t c = n_chunks - 1; c >= 0; --c) {
     const int32_t glo = c * WG_CHUNK, ng = min(WG_CHUNK, n_groups - glo);
@@ -875,33 +958,40 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
     }
     if (c > 0) chunk_load(c - 1);  // in flight during this chunk's scan
     uint32_t bm = 0, bx = 0;        // bit k: group glo + k has a feasible match / non-match
-    int32_t k = ng - 1;
-    for (; k >= 1; k -= 2) {  // two groups per step, all eight reads before the first use
-      uint32_t h1[PLANE_GW], h0[PLANE_GW], n1[PLANE_GW], n0[PLANE_GW];
-      group_words(s_tab + k * GQ, h1, n1);
-      group_words(s_tab + (k - 1) * GQ, h0, n0);
-      bm = (bm << 2) | (umin(or8(h1), 1u) << 1) | umin(or8(h0), 1u);
-      if constexpr (KX) bx = (bx << 2) | (umin(or8(n1), 1u) << 1) | umin(or8(n0), 1u);
+    int32_t k = (MSH_WG_EXPT & 1) ? -1 : ng - 1;
+    for (; k >= 1; k -= 2) {  // two groups per step
+      const uint4* t1 = s_tab + k * GQL;
+      const uint4* t0 = t1 - GQL;
+      uint32_t h1, h0, n1 = 0, n0 = 0;
+      group_acc<KX>(t1 + row, t1 + xq, t1 + LQ_V, h1, n1);
+      group_acc<KX>(t0 + row, t0 + xq, t0 + LQ_V, h0, n0);
+#if MSH_WG_FLAG == 1
+      bm = (bm << 2) + (h1 != 0 ? 2u : 0u) + (h0 != 0 ? 1u : 0u);
+      if constexpr (KX) bx = (bx << 2) + (n1 != 0 ? 2u : 0u) + (n0 != 0 ? 1u : 0u);
+#else
+      bm = lshl_or(bm, 2, lshl_or(min1(h1), 1, min1(h0)));
+      if constexpr (KX) bx = lshl_or(bx, 2, lshl_or(min1(n1), 1, min1(n0)));
+#endif
     }
     if (k == 0) {
-      uint32_t h0[PLANE_GW], n0[PLANE_GW];
-      group_words(s_tab, h0, n0);
-      bm = (bm << 1) | umin(or8(h0), 1u);
-      if constexpr (KX) bx = (bx << 1) | umin(or8(n0), 1u);
+      uint32_t h0, n0 = 0;
+      group_acc<KX>(s_tab + row, s_tab + xq, s_tab + LQ_V, h0, n0);
+      bm = lshl_or(bm, 1, min1(h0));
+      if constexpr (KX) bx = lshl_or(bx, 1, min1(n0));
     }
     if (bm) fm = (uint32_t)glo + lowbit(bm);
     if constexpr (KX)
       if (bx) fx = (uint32_t)glo + lowbit(bx);
   }
+  MSH_STAMP(2);
   // the exact first node of the first group with a hit: chunk 0 is still staged
   uint32_t rm = NOFIT, rx = NOFIT;
   const uint32_t staged_hi = (uint32_t)min(WG_CHUNK, n_groups);
   if (fm != NO_GROUP) {
     if (fm < staged_hi) {
-      uint32_t h[PLANE_GW], nm[PLANE_GW];
-      const uint4* tg = s_tab + fm * GQ;
-      rows_hits(tg[row], tg[ER_ROWS + row], tg[ER_Q], tg[ER_Q + 1], nT, h);
-      (void)nm;
+      uint32_t h[PLANE_GW];
+      const uint4* tg = s_tab + fm * GQL;
+      rows_hits(tg[row], tg[ER_ROWS + row], tg[LQ_X], tg[LQ_X + 1], nT, h);
       rm = hits_first(h, fm);
     } else {
       rm = rows_group_first(A, fm, row, nT);
@@ -911,8 +1001,8 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
     if (fx != NO_GROUP) {
       if (fx < staged_hi) {
         uint32_t n[PLANE_GW];
-        const uint4* tg = s_tab + fx * GQ;
-        rows_nonmatch(tg[row], tg[ER_ROWS + row], tg[ER_Q], tg[ER_Q + 1], tg[ER_GQ], tg[ER_GQ + 1], nT, n);
+        const uint4* tg = s_tab + fx * GQL;
+        rows_nonmatch(tg[row], tg[ER_ROWS + row], tg[LQ_X], tg[LQ_X + 1], tg[LQ_V], tg[LQ_V + 1], nT, n);
         rx = hits_first(n, fx);
       } else {
         rx = rows_group_first_nm(A, fx, row, nT);
@@ -932,10 +1022,19 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
       decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, A.pp, &oi, &osc, &ost);
     else
       decode_ident(im, ia, code != CODE_NONE_POD, make_ident_decode(A.pp), &oi, &osc, &ost);
-    out_idx[j] = oi;
-    if (out_score) out_score[j] = osc;  // optional output (NULL: not written)
-    out_status[j] = ost;
+    if ((MSH_WG_EXPT & 2) == 0 || oi == 0x7fffffff) {
+      out_idx[j] = oi;
+      if (out_score) out_score[j] = osc;  // optional output (NULL: not written)
+      out_status[j] = ost;
+    }
   }
+#ifdef MSH_STAMPS
+  MSH_STAMP(3);
+  if (lane == 0 && g_stamps) {
+    const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * W + wv;
+    for (int i = 0; i < 4; ++i) g_stamps[w * 4 + i] = stamp_t[i];
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1148,7 +1247,7 @@ __global__ __launch_bounds__(GEN_THREADS) void generic_kernel(GenericArgs a) {
 
 hipError_t launch_generic(const GenericArgs& a, hipStream_t s) {
   if (a.n_pods <= 0) return hipSuccess;
-  hipLaunchKernelGGL(generic_kernel, dim3((unsigned)((a.n_pods + GEN_PB - 1) / GEN_PB)), dim3(GEN_THREADS), 0, s, a);
+  MSH_TIMED_LAUNCH(generic_kernel, dim3((unsigned)((a.n_pods + GEN_PB - 1) / GEN_PB)), dim3(GEN_THREADS), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1680,7 +1779,7 @@ hipError_t launch_bits_s(const BatchArgs& a, hipStream_t s) {
   BatchArgs ka = a;
   ka.gps = (a.n_groups + S - 1) / S;
   const int64_t blocks = ((int64_t)a.n_pods + WAVE - 1) / WAVE;
-  hipLaunchKernelGGL((bits_kernel<S, KX, SHARD>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  MSH_TIMED_LAUNCH((bits_kernel<S, KX, SHARD>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
   return hipGetLastError();
 }
 
@@ -1689,7 +1788,7 @@ hipError_t launch_rows_s(const BatchArgs& a, hipStream_t s) {
   BatchArgs ka = a;
   ka.gps = (a.n_groups + S - 1) / S;
   const int64_t blocks = ((int64_t)a.n_pods + PPL * WAVE - 1) / (PPL * WAVE);
-  hipLaunchKernelGGL((rows_kernel<S, KX, SHARD, PPL>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
+  MSH_TIMED_LAUNCH((rows_kernel<S, KX, SHARD, PPL>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
   return hipGetLastError();
 }
 
@@ -1723,7 +1822,7 @@ int wg_waves(int64_t n_pods, const DeviceInfo& dev) {
 template <int W, bool KX, bool SHARD>
 hipError_t launch_wg_w(const BatchArgs& a, hipStream_t s) {
   const int64_t blocks = ((int64_t)a.n_pods + W * WAVE - 1) / (W * WAVE);
-  hipLaunchKernelGGL((wg_kernel<W, KX, SHARD, false>), dim3((unsigned)blocks), dim3(W * WAVE), 0, s, a);
+  MSH_TIMED_LAUNCH((wg_kernel<W, KX, SHARD, false>), dim3((unsigned)blocks), dim3(W * WAVE), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1737,13 +1836,10 @@ hipError_t launch_wg_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s)
 
 template <int W, bool KX>
 hipError_t launch_multi_w(MultiArgs& m, hipStream_t s) {
-  int32_t blocks = 0;
-  for (int b = 0; b < m.nb; ++b) {
-    blocks += (m.d[b].n_pods + W * WAVE - 1) / (W * WAVE);
-    m.d[b].blk_end = blocks;
-  }
+  int32_t blocks = 0;  // per batch: the largest batch's
+  for (int b = 0; b < m.nb; ++b) blocks = std::max(blocks, (m.d[b].n_pods + W * WAVE - 1) / (W * WAVE));
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((wg_kernel<W, KX, false, true>), dim3((unsigned)blocks), dim3(W * WAVE), 0, s, m);
+  MSH_TIMED_LAUNCH((wg_kernel<W, KX, false, true>), dim3((unsigned)blocks, (unsigned)m.nb), dim3(W * WAVE), 0, s, m);
   return hipGetLastError();
 }
 
@@ -1815,8 +1911,8 @@ hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  if (needs_kx(a.pp)) hipLaunchKernelGGL(kx, dim3(1), blk, lds, s, a);
-  else hipLaunchKernelGGL(id, dim3(1), blk, lds, s, a);
+  if (needs_kx(a.pp)) MSH_TIMED_LAUNCH(kx, dim3(1), blk, lds, s, a);
+  else MSH_TIMED_LAUNCH(id, dim3(1), blk, lds, s, a);
   return hipGetLastError();
 }
 

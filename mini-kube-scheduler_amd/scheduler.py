@@ -199,6 +199,17 @@ class DeviceContext:
         if rc:
             self._check(rc)
 
+    def timing_begin(self, max_launches: int) -> None:
+        """msh_timing_begin: the next hot-kernel launches of this ctx (from this thread) record their
+        own start / stop (the kernel-trace interval)."""
+        self._check(self._lib.msh_timing_begin(self.handle, int(max_launches)))
+
+    def timing_end(self) -> tuple[int, float, float]:
+        """msh_timing_end: (launches timed, summed ms, longest ms)."""
+        n, tot, mx = C.c_int32(), C.c_double(), C.c_double()
+        self._check(self._lib.msh_timing_end(self.handle, C.byref(n), C.byref(tot), C.byref(mx)))
+        return n.value, tot.value, mx.value
+
     def schedule_sequential(self, pod_digit: np.ndarray, pod_tol: np.ndarray, max_pods_per_node: int = 0,
                             on_commit: Callable[[int, int, int], None] | None = None, out=None):
         pod_digit = np.ascontiguousarray(pod_digit, np.int8)

@@ -23,16 +23,15 @@ mode = os.environ.get("MODE", "multi")
 norm = int(os.environ.get("NORM", 0))
 ctx = msh.DeviceContext(0)
 u, nd, pd, pt = synth.make_soa(n, p)
-if mode == "generic":
-    col = (np.arange(n, dtype=np.int64) * 7919) % 1000
-    ctx.set_score_columns([col])
+ctx.upload_nodes(u, nd)
+if mode == "generic":  # NodeNumber + one score column (weight 2, DefaultNormalizeScore)
+    ctx.upload_score_column(msh.SCORE_COLUMNS[0], (np.arange(n, dtype=np.int64) * 7919) % 1000)
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                     [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm)),
-                     msh.ScorePluginConfig(msh.SCORE_COLUMN0, 2, msh.Normalize(1))])
+                     msh.ScorePluginConfig(msh.SCORE_COLUMNS[0], 2, msh.Normalize(1))])
 else:
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                     [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm))])
-ctx.upload_nodes(u, nd)
 dev = torch.device("cuda:0")
 nb = msh._native.BATCHES_PER_LAUNCH if mode == "multi" else 1
 bufs = [(torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev), torch.empty(p, dtype=torch.int32, device=dev),

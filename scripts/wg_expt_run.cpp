@@ -1,0 +1,142 @@
+// wg_expt_run.cpp — phase experiments on wg_kernel (C3: 5,000 nodes, 100k-pod batches), for one
+// build of the library given on the command line (scripts/wg_expt.sh builds the variants: the
+// product source with -DMSH_STAMPS and an MSH_WG_EXPT mask; never the product library).
+//   wg_expt_run <lib.so> <tag> [batches per launch = 8]
+// Prints one JSON line: the kernel duration per launch (msh_timing_*: the kernel's own start / stop)
+// and, from the stamps of one launch, the per-wave phase durations (entry -> after the table copy and
+// barrier -> after the scan -> after the stores; percentiles in microseconds) and the wave start spread.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "minisched_hip.h"
+
+#define CHECK(x)                                   \
+  do {                                             \
+    int rc_ = (int)(x);                            \
+    if (rc_ != 0) {                                \
+      fprintf(stderr, "%s failed: %d\n", #x, rc_); \
+      return 1;                                    \
+    }                                              \
+  } while (0)
+
+template <typename F>
+F sym(void* h, const char* n) {
+  void* p = dlsym(h, n);
+  if (!p) {
+    fprintf(stderr, "missing %s\n", n);
+    exit(2);
+  }
+  return reinterpret_cast<F>(p);
+}
+
+static double pct(std::vector<double> v, double q) {
+  if (v.empty()) return -1;
+  std::sort(v.begin(), v.end());
+  return v[(size_t)(q * (v.size() - 1))];
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) return 2;
+  void* h = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    fprintf(stderr, "%s\n", dlerror());
+    return 2;
+  }
+  const int NB = argc > 3 ? atoi(argv[3]) : 8;
+  auto create = sym<int (*)(int, msh_ctx**)>(h, "msh_create");
+  auto upload = sym<int (*)(msh_ctx*, int32_t, const uint8_t*, const int8_t*)>(h, "msh_upload_nodes");
+  auto batches = sym<int (*)(msh_ctx*, int32_t, const msh_batch*, void*)>(h, "msh_schedule_batches_device");
+  auto tbegin = sym<int (*)(msh_ctx*, int32_t)>(h, "msh_timing_begin");
+  auto tend = sym<int (*)(msh_ctx*, int32_t*, double*, double*)>(h, "msh_timing_end");
+  auto stamps_set = reinterpret_cast<int (*)(void*)>(dlsym(h, "msh_stamps_set"));
+  const int N = 5000, P = 100000;
+  uint64_t x = 0x6d696e69;
+  auto rnd = [&]() {
+    x += 0x9e3779b97f4a7c15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+  };
+  std::vector<uint8_t> u(N), pt(P);
+  std::vector<int8_t> d(N), pd(P);
+  for (int i = 0; i < N; ++i) {
+    u[i] = rnd() % 10 == 0;
+    d[i] = (int8_t)(i % 10);
+  }
+  for (int j = 0; j < P; ++j) {
+    pd[j] = (int8_t)(rnd() % 100 == 0 ? -1 : rnd() % 10);
+    pt[j] = rnd() % 20 == 0;
+  }
+  msh_ctx* ctx = nullptr;
+  CHECK(create(0, &ctx));
+  CHECK(upload(ctx, N, u.data(), d.data()));
+  std::vector<msh_batch> desc(NB);
+  for (int b = 0; b < NB; ++b) {
+    int8_t* dpd;
+    uint8_t* dpt;
+    int32_t *doi, *dst;
+    int64_t* dsc;
+    CHECK(hipMalloc(&dpd, P));
+    CHECK(hipMalloc(&dpt, P));
+    CHECK(hipMalloc(&doi, P * 4));
+    CHECK(hipMalloc(&dst, P * 4));
+    CHECK(hipMalloc(&dsc, (size_t)P * 8));
+    CHECK(hipMemcpy(dpd, pd.data(), P, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dpt, pt.data(), P, hipMemcpyHostToDevice));
+    desc[b] = msh_batch{P, 0, dpd, dpt, doi, dsc, dst};
+  }
+  hipStream_t st;
+  CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  for (int i = 0; i < 10; ++i) CHECK(batches(ctx, NB, desc.data(), st));
+  CHECK(hipStreamSynchronize(st));
+  const int R = 30;
+  CHECK(tbegin(ctx, R));
+  for (int i = 0; i < R; ++i) CHECK(batches(ctx, NB, desc.data(), st));
+  int32_t n = 0;
+  double tot = 0, mx = 0;
+  CHECK(tend(ctx, &n, &tot, &mx));
+  printf("{\"tag\": \"%s\", \"batches_per_launch\": %d, \"kernel_us\": %.3f, \"us_per_batch\": %.3f", argv[2], NB,
+         tot * 1e3 / n, tot * 1e3 / n / NB);
+  if (stamps_set) {
+    const int blocks = (P + 255) / 256;
+    const size_t slots = (size_t)blocks * NB * 4 * 4;
+    unsigned long long* d_st;
+    CHECK(hipMalloc(&d_st, slots * 8));
+    CHECK(hipMemset(d_st, 0, slots * 8));
+    CHECK(stamps_set(d_st));
+    CHECK(batches(ctx, NB, desc.data(), st));
+    CHECK(hipStreamSynchronize(st));
+    std::vector<unsigned long long> hs(slots);
+    CHECK(hipMemcpy(hs.data(), d_st, slots * 8, hipMemcpyDeviceToHost));
+    unsigned long long t_min = ~0ull, t_max = 0;
+    for (size_t w = 0; w < slots / 4; ++w)
+      if (hs[w * 4]) {
+        t_min = std::min(t_min, hs[w * 4]);
+        t_max = std::max(t_max, hs[w * 4 + 3]);
+      }
+    std::vector<double> start, pro, scan, tail, life;
+    for (size_t w = 0; w < slots / 4; ++w) {
+      const unsigned long long* t = &hs[w * 4];
+      if (!t[0] || !t[3]) continue;
+      start.push_back((t[0] - t_min) * 0.01);
+      pro.push_back((t[1] - t[0]) * 0.01);
+      scan.push_back((t[2] - t[1]) * 0.01);
+      tail.push_back((t[3] - t[2]) * 0.01);
+      life.push_back((t[3] - t[0]) * 0.01);
+    }
+    printf(", \"waves\": %zu, \"span_us\": %.2f, \"start_us\": [%.2f, %.2f, %.2f, %.2f], \"prologue_us\": [%.2f, %.2f, %.2f], "
+           "\"scan_us\": [%.2f, %.2f, %.2f], \"tail_us\": [%.2f, %.2f, %.2f], \"life_us\": [%.2f, %.2f, %.2f]",
+           start.size(), (t_max - t_min) * 0.01, pct(start, 0.1), pct(start, 0.5), pct(start, 0.9), pct(start, 1.0),
+           pct(pro, 0.1), pct(pro, 0.5), pct(pro, 0.9), pct(scan, 0.1), pct(scan, 0.5), pct(scan, 0.9), pct(tail, 0.1),
+           pct(tail, 0.5), pct(tail, 0.9), pct(life, 0.1), pct(life, 0.5), pct(life, 0.9));
+  }
+  printf("}\n");
+  return 0;
+}

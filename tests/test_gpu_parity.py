@@ -731,15 +731,15 @@ def _desc(t):
 
 
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
-@pytest.mark.parametrize("nb", [1, 3, 8, 9, 17])
+@pytest.mark.parametrize("nb", [1, 3, 8, 9, 17, 32, 33, 70])
 def test_multi_batch_launch(msh, gpu_ctx, oracle, norm, nb):
-    """msh_schedule_batches_device (ABI v5): nb independent batches, up to 8 per launch, ragged pod
+    """msh_schedule_batches_device (ABI v5): nb independent batches, up to 32 per launch, ragged pod
     counts (empty and one-pod batches among them), some without scores; every batch bit-exact vs
     the oracle, and nothing written past a batch's end."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(77 * nb + norm)
-    sizes = [0, 1, 64, 65, 255, 257, 100_003, 5000, 333, 4096, 1, 2, 700, 64, 128, 129, 999][:nb]
+    sizes = ([0, 1, 64, 65, 255, 257, 100_003, 5000, 333, 4096, 1, 2, 700, 64, 128, 129, 999] * 5)[:nb]
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, norm)
     _set(gpu_ctx, msh, ps)
     u, nd, _, _ = _rand_case(rng, 5000, 1)
