@@ -46,22 +46,27 @@ sys.path.insert(0, str(ROOT))
 METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
 CLOCK_HZ = 2.4e9                   # MI355X_MICROARCH.md: max clock
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# The digit-row kernel (rows_kernel, the identity-like modes): per 8-word group and 64-pod wave,
-# four ds_read_b128 (the lane's row words of both chunks, and the group's X words at one address)
-# = 4 KiB through the LDS array (4 LDS cycles each, MI355X_MICROARCH.md LDS table), and 8 v_bitop3
-# + 4 ORs + compare + select + the running-first move = 15 VALU.
+# The persistent class-row kernel (wgp_kernel, tables up to 8,192 nodes; the identity-like modes):
+# per 256-node group and 64-pod wave, two ds_read_b128 of the lanes' class-row entries = 2 KiB
+# through the LDS array (1/8 B per pod-node pair), and 7.5 VALU (three v_bitop3 OR3 + a v_or over
+# the 8 words, the group flag v_min + v_lshl_or and its share of the pair's, the address).
 LDS_PEAK = 150e12                  # MI355X_MICROARCH.md: ~150 TB/s aggregate for ds_read_b64/b128
-ROWS_LDS_BYTES_PER_GROUP_WAVE = 4 * 1024
-# wg_kernel (round 3): per group and wave 8 v_bitop3 + the OR tree + the group flag
-WG_VALU_PER_GROUP = 14
+WGP_MAX_GROUPS = 32                # msh_kernels.hip: the persistent kernel's table limit (groups of 256 nodes)
+LDS_BYTES_PER_GROUP_WAVE = 2 * 1024
+VALU_PER_GROUP_WAVE = 7.5
 PMC_FILE = ROOT / "profiles" / "r3_pmc_c3.json"
 VALU_PEAK_FILE = ROOT / "profiles" / "r3_ubench_valu_peak.json"
 
 
 def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False,
                        multi: bool = False) -> str:
-    """The kernel msh_kernels.hip launch_batch / launch_batches dispatches (4-wave workgroups)."""
+    """The kernel msh_kernels.hip launch_batch / launch_batches dispatches (4-wave workgroups): the
+    persistent class-row kernel while the table has at most WGP_MAX_GROUPS groups (shard keys aside),
+    else the chunk-streaming wg_kernel."""
     b = lambda v: str(v).lower()
+    groups = max(-(-n_nodes // 1024) * 1024, 1024) // 256
+    if groups <= WGP_MAX_GROUPS and not shard:
+        return f"void msh::wgp_kernel<4, {b(kx)}>"
     return f"void msh::wg_kernel<4, {b(kx)}, {b(shard)}, {b(multi)}>"
 
 
@@ -408,14 +413,13 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
               and entry.get("batches_per_launch", 1) == batches_per_launch)
     n_groups = max(-(-n_local // 1024) * 1024, 1024) // 256
     group_waves = float(n_groups) * -(-p // 64) * batches_per_launch  # every 64-pod wave meets every group once
-    # achieved = ALGORITHMIC LDS-array bytes of the scan per launch (4 KiB per 256-node group and 64-pod
-    # wave: the lane's two 16-byte row reads and the group's two 16-byte X reads, 0.25 B per pod-node
-    # pair) / the launch's duration
-    lds_bytes = group_waves * ROWS_LDS_BYTES_PER_GROUP_WAVE
+    # achieved = ALGORITHMIC LDS-array bytes of the scan per launch (2 KiB per 256-node group and 64-pod
+    # wave: the lane's two 16-byte class-row reads, 1/8 B per pod-node pair) / the launch's duration
+    lds_bytes = group_waves * LDS_BYTES_PER_GROUP_WAVE
     lds_cycles = entry.get("SQ_LDS_IDX_ACTIVE") if pmc_ok else None
-    model_instr = group_waves * WG_VALU_PER_GROUP  # wave-instructions of the scan
+    model_instr = group_waves * VALU_PER_GROUP_WAVE  # wave-instructions of the scan
     valu_instr = entry.get("SQ_INSTS_VALU") if pmc_ok else None
-    uniq_bytes = (1.5 * n_local + 18.0 * p * batches_per_launch)  # rows + X once, pod records + outputs
+    uniq_bytes = (3.0 * n_local + 18.0 * p * batches_per_launch)  # class rows once, pod records + outputs
     survey_bytes = 2.0 * n_local * p * batches_per_launch + 18.0 * p * batches_per_launch
     out = {
         "bound": "lds",
@@ -444,7 +448,7 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
                                  f"x 1,024 SIMDs x 2.4 GHz" if ipc else "unmeasured"),
                  "achieved_model": model_instr / launch_s / 1e9,
                  "frac_model": (model_instr / launch_s / (valu_peak / 64)) if valu_peak else None,
-                 "instr_per_group_wave_model": WG_VALU_PER_GROUP,
+                 "instr_per_group_wave_model": VALU_PER_GROUP_WAVE,
                  "instr_measured": valu_instr,
                  "frac_counter": (valu_instr / launch_s / (valu_peak / 64)) if (valu_instr and valu_peak) else None,
                  "scan_share_of_valu": model_instr / valu_instr if valu_instr else None},
@@ -453,7 +457,7 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
                 "survey_8d_bytes_per_launch": survey_bytes,
                 "survey_8d_frac": survey_bytes / launch_s / HBM_PEAK,
                 "survey_8d_note": "2 B per pair counts every L1/L2/LDS re-read of the node table as HBM "
-                                  "traffic; the 7.5 KB table is read from HBM once per launch"},
+                                  "traffic; the 15 KB class-row table is read from HBM once per launch"},
     }
     return out
 

@@ -79,6 +79,7 @@ struct NodeTable {
   int8_t* d_digit = nullptr;
   uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout)
   uint32_t* d_erows = nullptr;   // digit rows (msh_internal.h ER_* layout)
+  uint32_t* d_hrows = nullptr;   // class rows (msh_internal.h HR_* layout)
   uint32_t* d_ball = nullptr;    // [0..1] first feasible node per pod class, as keys
   // score-column plugins (generic pipeline): GEN_COLS x cap int64, column k valid when col_ok[k]
   int64_t* d_cols = nullptr;
@@ -170,12 +171,14 @@ void free_table(NodeTable& t) {
   (void)hipFree(t.d_digit);
   (void)hipFree(t.d_planes);
   (void)hipFree(t.d_erows);
+  (void)hipFree(t.d_hrows);
   (void)hipFree(t.d_ball);
   t.d_cols = nullptr;
   t.d_unsched = nullptr;
   t.d_digit = nullptr;
   t.d_planes = nullptr;
   t.d_erows = nullptr;
+  t.d_hrows = nullptr;
   t.d_ball = nullptr;
   for (bool& ok : t.col_ok) ok = false;
   t.cap = 0;
@@ -354,6 +357,7 @@ int ensure_table(msh_ctx* c, NodeTable& t, size_t n_pad) {
   MSH_HIP(c, hipMalloc(&t.d_planes, n_pad / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
   // + ER_PAD groups: the batch kernel copies whole tiles without clamping (never read as rows)
   MSH_HIP(c, hipMalloc(&t.d_erows, (n_pad / msh::GROUP_NODES + msh::ER_PAD) * msh::ER_GD * sizeof(uint32_t)));
+  MSH_HIP(c, hipMalloc(&t.d_hrows, n_pad / msh::GROUP_NODES * msh::HR_GD * sizeof(uint32_t)));
   MSH_HIP(c, hipMalloc(&t.d_ball, 2 * sizeof(uint32_t)));
   t.cap = n_pad;
   return MSH_OK;
@@ -438,7 +442,7 @@ int rewrite(msh_ctx* c, const Rewrite& w) {
     MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_nstage, pbytes, hipMemcpyHostToDevice, ps));
   }
   hipError_t e = msh::launch_node_prep(dst.d_unsched, dst.d_digit, n, n_pad, c->pp.has_nu_filter, dst.d_ball,
-                                       dst.d_planes, dst.d_erows, ps, c->d_patch,
+                                       dst.d_planes, dst.d_erows, dst.d_hrows, ps, c->d_patch,
                                        w.kind == Rewrite::PATCH ? w.patch_count : 0);
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
   // an upload zeroes the sequential-mode counts (after the sequential launches in flight)
@@ -491,6 +495,7 @@ msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t
   const NodeTable& t = cur_table(c);
   a.planes = t.d_planes;
   a.erows = t.d_erows;
+  a.hrows = t.d_hrows;
   a.n_groups = c->n_pad / msh::GROUP_NODES;
   a.pod_digit = pd;
   a.pod_tol = pt;
@@ -681,7 +686,8 @@ bool read_knobs(msh::DeviceInfo& d, std::string* err) {
                   knob("MSH_HOST_IO", {{"zero-copy", 0}, {"zc", 1}, {"dma", 2}}, &io, err) &&
                   knob("MSH_HOST_SYNC", {{"wait", 0}, {"poll", 1}}, &poll, err) &&
                   knob("MSH_BATCH_KERNEL", {{"wg", 0}, {"slices", 1}, {"generic", 2}}, &d.batch_kernel, err) &&
-                  knob("MSH_WG_WAVES", {{"0", 0}, {"4", 4}, {"8", 8}}, &d.wg_waves, err);
+                  knob("MSH_WG_WAVES", {{"0", 0}, {"4", 4}, {"8", 8}}, &d.wg_waves, err) &&
+                  knob("MSH_WG_PERSIST", {{"1", 0}, {"0", 1}}, &d.wg_no_persist, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;
   d.host_sync_poll = poll;

@@ -49,6 +49,7 @@ struct DeviceInfo {
   int batch_kernel = 0;    // 0 = wg_kernel (default), 1 = the round-2 slice kernel rows_kernel (MSH_BATCH_KERNEL=slices,
                            // A/B), 2 = generic_kernel for every plugin list (MSH_BATCH_KERNEL=generic, A/B)
   int wg_waves = 0;        // A/B only (MSH_WG_WAVES=1|2|4|8): waves per workgroup of wg_kernel, 0 = auto
+  int wg_no_persist = 0;   // A/B only (MSH_WG_PERSIST=0): multi-batch launches on the 2-D wg_kernel grid
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit
@@ -90,13 +91,26 @@ constexpr int ER_Q = 2 * ER_ROWS;      // 16-byte row chunks per group
 constexpr int ER_GQ = ER_Q + 2;        // 16-byte chunks per group: the rows, then X
 constexpr int ER_GD = ER_GQ * 4;       // dwords per group
 constexpr int ER_TG = 8;               // groups per LDS tile of the batch kernel (3,072 B per wave)
+
+// Class rows (the input of the persistent batch kernel): the digit rows with the filter folded in per
+// pod class, t = 0 (does not tolerate the unschedulable taint) and t = 1 (tolerates), so that a pod's
+// hit words are one row read, H[t][r] = the word's nodes that pass NodeUnschedulable for class t AND
+// have suffix digit r (row 10 zero); then F[t] = the word's nodes feasible for class t (the REVERSE /
+// MINMAX modes' non-matches are F[t] & ~H[t][r]). Per group, for chunk c of 4 words:
+//   hrows[g * HR_GD + ((c * 2 + t) * ER_ROWS + r) * 4 + k] = H[t][r] of word g * PLANE_GW + 4 c + k
+//   hrows[g * HR_GD + (HR_Q + 2 t) * 4 + j]              = F[t] of word g * PLANE_GW + j
+// 3 B per node; a pod reads 32 B per 256-node group (two 16-byte entries), half of the digit rows + X.
+constexpr int HR_Q = 4 * ER_ROWS;      // 16-byte row entries per group (2 chunks x 2 classes x 11 rows)
+constexpr int HR_GQ = HR_Q + 4;        // ... then F[0], F[1] (two entries each)
+constexpr int HR_GD = HR_GQ * 4;       // dwords per group
 constexpr int ER_PAD = 2 * ER_TG;      // groups of padding: whole-tile copies need no clamp
 
 // ---- launchers (msh_kernels.hip) ----
 // Applies `patch_count` pending msh_patch_nodes entries (idx | unsched << 32 | (uint8)digit << 40)
 // to the raw columns, then rebuilds the planes and the first feasible node per class (ball).
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n, int32_t n_pad,
-                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows, hipStream_t s,
+                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows,
+                            uint32_t* d_hrows, hipStream_t s,
                             const unsigned long long* d_patch = nullptr, int32_t patch_count = 0);
 
 constexpr int64_t EXPORT_NONE = INT64_MIN;  // msh_export_results: no score recorded
@@ -108,6 +122,7 @@ hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_
 struct BatchArgs {
   const uint32_t* planes;    // bit-sliced node table, n_groups groups
   const uint32_t* erows;     // digit rows (ER_* layout), n_groups groups
+  const uint32_t* hrows;     // class rows (HR_* layout), n_groups groups
   int32_t n_groups;          // n_pad / GROUP_NODES
   int32_t gps;               // groups per slice wave (set by the launcher)
   const int8_t* pod_digit;
@@ -140,6 +155,7 @@ constexpr int MULTI_MAX = 32;  // batches per launch (kernel-argument descriptor
 struct MultiArgs {
   BatchArgs a;  // the node table, plugin set and launch geometry (its pod / output fields unused)
   int32_t nb;
+  int32_t bpb;  // pod blocks per batch (the largest batch's), set by the launcher
   BatchDesc d[MULTI_MAX];
 };
 

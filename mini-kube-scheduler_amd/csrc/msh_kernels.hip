@@ -80,7 +80,8 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
                                                                  int32_t n, int32_t has_nu,
                                                                  uint32_t* __restrict__ ball,
                                                                  uint32_t* __restrict__ planes,
-                                                                 uint32_t* __restrict__ erows) {
+                                                                 uint32_t* __restrict__ erows,
+                                                                 uint32_t* __restrict__ hrows) {
   constexpr int NWV = PREP_THREADS / WAVE;
   __shared__ uint32_t s_k0[NWV], s_k1[NWV];
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -121,6 +122,26 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
     const int half = lane & 1;
     const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
     erows[(size_t)(word / PLANE_GW) * ER_GD + ER_Q * 4 + word % PLANE_GW] = (uint32_t)(pm[PLANE_X] >> (32 * half));
+  }
+  // the class rows of the same two words (HR_* layout): lanes 0..43 write H[t][r] (row 10 zero),
+  // lanes 44..47 F[t]
+  {
+    const unsigned long long x0 = ~pm[PLANE_X];  // class 0 passes NodeUnschedulable where X is clear
+    if (lane < 4 * ER_ROWS) {
+      const int r = lane >> 2, t = (lane >> 1) & 1, half = lane & 1;
+      unsigned long long m = 0;
+#pragma unroll
+      for (int q = 0; q < ER_ROWS - 1; ++q) m = (r == q) ? em[q] : m;
+      if (t == 0) m &= x0;
+      const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;  // i - lane: the wave's first node
+      const uint32_t g = word / PLANE_GW, c = (word / 4) & 1u, k = word & 3u;
+      hrows[(size_t)g * HR_GD + ((c * 2 + (uint32_t)t) * ER_ROWS + (uint32_t)r) * 4 + k] = (uint32_t)(m >> (32 * half));
+    } else if (lane < 4 * ER_ROWS + 4) {
+      const int t = (lane >> 1) & 1, half = lane & 1;
+      const unsigned long long m = t == 0 ? (pm[PLANE_V] & x0) : pm[PLANE_V];
+      const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
+      hrows[(size_t)(word / PLANE_GW) * HR_GD + (HR_Q + 2 * t) * 4 + word % PLANE_GW] = (uint32_t)(m >> (32 * half));
+    }
   }
   const unsigned long long m0 = pm[PLANE_V] & ~pm[PLANE_X], m1 = pm[PLANE_V];
   if (lane == 0) {
@@ -1038,6 +1059,196 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
 }
 
 // ---------------------------------------------------------------------------------------
+// Persistent batch kernel (msh_schedule_batch_device / msh_schedule_batches_device when the table
+// has at most WGP_MAX_GROUPS groups, 8,192 nodes: BASELINE C2 and C3). A grid of as many workgroups
+// as stay resident (CUs x 8 at C3) copies the table's CLASS ROWS (msh_internal.h HR_*) into LDS once
+// per workgroup and then walks the launch's (batch, 256-pod block) space with a stride of the grid;
+// after the copy the waves are independent (no barrier per block), and each wave loads the next
+// block's pod bytes before it scans the current one.
+// Per lane (pod) and 256-node group the pair evaluation is one read of the pod's class row: the two
+// 16-byte entries H[t][r] of the group's two 4-word chunks, t = the pod tolerates the unschedulable
+// taint, r = its suffix digit (10 = none: the zero row). A set bit is a node that passes
+// NodeUnschedulable for the pod and scores 10 for it (NodeNumber). The 8 words are ORed into the
+// group's flag (three v_bitop3 OR3 and a v_or, then v_min + v_lshl_or into a per-lane bitmap of
+// groups); REVERSE / MINMAX also OR the feasible non-matches F[t] & ~H (one v_bitop3 per word).
+// 32 B of LDS per pod and group, 1/8 B per (pod, node) pair: half of wg_kernel's digit rows + X
+// words, and the scan is bound by the LDS array's read bandwidth. The first group
+// with a hit is the lowest set bit of the bitmap (groups walked in descending List order); its
+// exact first node is resolved from the same two entries (v_ffbl), as in wg_kernel.
+// ---------------------------------------------------------------------------------------
+#ifndef MSH_WGP_PIPE
+#define MSH_WGP_PIPE 0  // A/B: the software-pipelined scan (scripts/wg_expt.sh)
+#endif
+constexpr int WGP_MAX_GROUPS = 32;  // <= 8,192 nodes: 22.5 KB of LDS (24.6 KB with F)
+
+__device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xfe);
+}
+
+template <int W, bool KX>
+__global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
+  constexpr int GQL = KX ? HR_GQ : HR_Q;  // entries staged per group (F only for KX)
+  constexpr int NT = W * WAVE;
+  extern __shared__ uint4 s_tab[];        // n_groups * GQL entries
+  const BatchArgs& A = ka.a;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int32_t n_groups = A.n_groups;  // <= WGP_MAX_GROUPS (the launcher's condition)
+  {  // the table copy, once per workgroup: every load in flight before the first store
+    constexpr int EPT = (WGP_MAX_GROUPS * GQL + NT - 1) / NT;
+    const uint4* __restrict__ hr = reinterpret_cast<const uint4*>(A.hrows);
+    const int32_t tot = n_groups * GQL;
+    // loads unconditional (index clamped to the last entry: no branch around them, so all are in
+    // flight together), then the stores of the slots below tot; named registers, not an array (a
+    // uint4 array went to scratch)
+    static_assert(EPT <= 6, "wgp_kernel copies at most six 16-byte entries per thread");
+    auto src = [&](int k) {
+      const int32_t i = min((int32_t)threadIdx.x + k * NT, tot - 1);
+      const int32_t gi = i / GQL, q = i - gi * GQL;
+      return hr[(size_t)gi * HR_GQ + q];
+    };
+    const uint4 v0 = src(0), v1 = EPT > 1 ? src(1) : v0, v2 = EPT > 2 ? src(2) : v0, v3 = EPT > 3 ? src(3) : v0,
+                v4 = EPT > 4 ? src(4) : v0, v5 = EPT > 5 ? src(5) : v0;
+    const uint4 vs[6] = {v0, v1, v2, v3, v4, v5};
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int32_t i = (int32_t)threadIdx.x + k * NT;
+      if (i < tot) s_tab[i] = vs[k];
+    }
+  }
+  const uint32_t ball0 = A.ball[0], ball1 = A.ball[1];
+  const IdentDecode idd = make_ident_decode(A.pp);
+  __syncthreads();
+
+  // ---- the (batch, block) walk: item t = b * bpb + x, t = blockIdx.x, blockIdx.x + gridDim.x, ...
+  const int32_t bpb = ka.bpb, total = ka.nb * bpb, G = (int32_t)gridDim.x;
+  int32_t it = (int32_t)blockIdx.x;
+  int32_t b = it / bpb, x = it - b * bpb;
+  int dq = 0;
+  uint32_t tq = 0;
+  int32_t np = 0;
+  auto load_pods = [&]() {  // this wave's pod bytes of item (b, x), clamped offset
+    const BatchDesc& d = ka.d[b];
+    np = d.n_pods;
+    const uint32_t jj = min((uint32_t)(x * NT + wv * WAVE + lane), np > 0 ? (uint32_t)(np - 1) : 0u);
+    if (np > 0) {
+      dq = d.pod_digit[jj];
+      tq = d.pod_tol[jj];
+    }
+  };
+  if (it < total) load_pods();
+  while (it < total) {
+    const int32_t cb = b, cx = x, cnp = np;
+    const int cdq = dq;
+    const uint32_t ctq = tq;
+    it += G;  // the next item, its pod bytes in flight during this item's scan
+    x += G;
+    while (x >= bpb) {
+      x -= bpb;
+      ++b;
+    }
+    if (it < total) load_pods();
+    if (cx * NT + wv * WAVE >= cnp) continue;  // this wave's slice lies past the batch's end
+    const int32_t j = cx * NT + wv * WAVE + lane;
+    const bool act = j < cnp;
+    const uint32_t code = (act && cdq >= 0 && cdq <= 9) ? (uint32_t)cdq : CODE_NONE_POD;
+    const uint32_t tol = (act && ctq) ? 1u : 0u;
+    const uint32_t row = code <= 9u ? code : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
+    const uint32_t ra = tol * ER_ROWS + row;                            // chunk 0's entry; chunk 1 at +22
+    const uint32_t fa = HR_Q + 2 * tol;                                 // F[tol] (KX)
+    uint32_t bm = 0, bx = 0;
+    auto group = [&](const uint4* tg, uint32_t& h, uint32_t& n) {
+      const uint4 e0 = tg[ra], e1 = tg[ra + 2 * ER_ROWS];
+      h = or3(or3(e0.x, e0.y, e0.z), or3(e0.w, e1.x, e1.y), e1.z | e1.w);
+      if constexpr (KX) {
+        const uint4 f0 = tg[fa], f1 = tg[fa + 1];
+        n = andn(f0.x, e0.x);
+        n = acc_andn(n, f0.y, e0.y);
+        n = acc_andn(n, f0.z, e0.z);
+        n = acc_andn(n, f0.w, e0.w);
+        n = acc_andn(n, f1.x, e1.x);
+        n = acc_andn(n, f1.y, e1.y);
+        n = acc_andn(n, f1.z, e1.z);
+        n = acc_andn(n, f1.w, e1.w);
+      }
+    };
+    int32_t k = n_groups - 1;
+    if constexpr (!KX && MSH_WGP_PIPE) {
+      // software-pipelined: the next pair's four entries are read before this pair is reduced
+      auto or8 = [](const uint4& e0, const uint4& e1) {
+        return or3(or3(e0.x, e0.y, e0.z), or3(e0.w, e1.x, e1.y), e1.z | e1.w);
+      };
+      const uint4* tp = s_tab + k * GQL;
+      uint4 a1 = tp[ra], b1 = tp[ra + 2 * ER_ROWS], a0 = a1, b0 = b1;
+      if (k >= 1) {
+        a0 = (tp - GQL)[ra];
+        b0 = (tp - GQL)[ra + 2 * ER_ROWS];
+      }
+      for (; k >= 1; k -= 2) {
+        const uint4 c1 = a1, d1 = b1, c0 = a0, d0 = b0;
+        if (k >= 3) {
+          const uint4* tn = s_tab + (k - 2) * GQL;
+          a1 = tn[ra];
+          b1 = tn[ra + 2 * ER_ROWS];
+          a0 = (tn - GQL)[ra];
+          b0 = (tn - GQL)[ra + 2 * ER_ROWS];
+        } else if (k == 2) {
+          a1 = s_tab[ra];
+          b1 = s_tab[ra + 2 * ER_ROWS];
+        }
+        bm = lshl_or(bm, 2, lshl_or(min1(or8(c1, d1)), 1, min1(or8(c0, d0))));
+      }
+      if (k == 0) bm = lshl_or(bm, 1, min1(or8(a1, b1)));
+    } else {
+      for (; k >= 1; k -= 2) {  // two groups per step, descending
+        const uint4* t1 = s_tab + k * GQL;
+        uint32_t h1, h0, n1 = 0, n0 = 0;
+        group(t1, h1, n1);
+        group(t1 - GQL, h0, n0);
+        bm = lshl_or(bm, 2, lshl_or(min1(h1), 1, min1(h0)));
+        if constexpr (KX) bx = lshl_or(bx, 2, lshl_or(min1(n1), 1, min1(n0)));
+      }
+      if (k == 0) {
+        uint32_t h0, n0 = 0;
+        group(s_tab, h0, n0);
+        bm = lshl_or(bm, 1, min1(h0));
+        if constexpr (KX) bx = lshl_or(bx, 1, min1(n0));
+      }
+    }
+    uint32_t rm = NOFIT, rx = NOFIT;
+    if (bm) {
+      const uint32_t fm = lowbit(bm);
+      const uint4* tg = s_tab + fm * GQL;
+      const uint4 e0 = tg[ra], e1 = tg[ra + 2 * ER_ROWS];
+      const uint32_t h[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+      rm = hits_first(h, fm);
+    }
+    if constexpr (KX) {
+      if (bx) {
+        const uint32_t fx = lowbit(bx);
+        const uint4* tg = s_tab + fx * GQL;
+        const uint4 e0 = tg[ra], e1 = tg[ra + 2 * ER_ROWS], f0 = tg[fa], f1 = tg[fa + 1];
+        const uint32_t n[PLANE_GW] = {f0.x & ~e0.x, f0.y & ~e0.y, f0.z & ~e0.z, f0.w & ~e0.w,
+                                      f1.x & ~e1.x, f1.y & ~e1.y, f1.z & ~e1.z, f1.w & ~e1.w};
+        rx = hits_first(n, fx);
+      }
+    }
+    if (!act) continue;
+    int32_t oi, ost;
+    int64_t osc;
+    const int64_t im = rm != NOFIT ? (int64_t)rm : -1, ia = key_to_idx(tol ? ball1 : ball0);
+    if constexpr (KX)
+      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, A.pp, &oi, &osc, &ost);
+    else
+      decode_ident(im, ia, code != CODE_NONE_POD, idd, &oi, &osc, &ost);
+    const BatchDesc& d = ka.d[cb];
+    d.out_idx[j] = oi;
+    if (d.out_score) d.out_score[j] = osc;  // optional output (NULL: not written)
+    d.out_status[j] = ost;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Generic score pipeline: any score plugin list (NodeNumber and up to four score-column plugins,
 // MSH_PLUGIN_SCORE_COLUMN0..3), with the int64 score of every (pod, node) pair computed
 // explicitly. The bitmap kernels above are exact only because NodeNumber's raw score takes two
@@ -1682,15 +1893,15 @@ __global__ __launch_bounds__(256) void prep_reset_kernel(uint32_t* __restrict__ 
 }
 
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n, int32_t n_pad,
-                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows, hipStream_t s,
-                            const unsigned long long* d_patch, int32_t patch_count) {
+                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows,
+                            uint32_t* d_hrows, hipStream_t s, const unsigned long long* d_patch, int32_t patch_count) {
   hipLaunchKernelGGL(prep_reset_kernel, dim3(patch_count > 0 ? (patch_count + 255) / 256 : 1), dim3(256), 0, s,
                      d_ball, d_patch, patch_count, const_cast<uint8_t*>(d_unsched), const_cast<int8_t*>(d_digit));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (n_pad == 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel, dim3(n_pad / PREP_THREADS), dim3(PREP_THREADS), 0, s, d_unsched, d_digit, n,
-                     has_nu, d_ball, d_planes, d_erows);
+                     has_nu, d_ball, d_planes, d_erows, d_hrows);
   return hipGetLastError();
 }
 
@@ -1826,8 +2037,38 @@ hipError_t launch_wg_w(const BatchArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// The persistent kernel over m.nb batches: as many workgroups as stay resident (8 per CU with 4-wave
+// workgroups, fewer when the table's LDS copy limits them), never more than the launch's blocks.
+template <int W, bool KX>
+hipError_t launch_persistent(MultiArgs& m, const DeviceInfo& dev, hipStream_t s) {
+  const size_t lds = (size_t)m.a.n_groups * (KX ? HR_GQ : HR_Q) * sizeof(uint4);
+  const int64_t per_cu = std::min<int64_t>(32 / W, (int64_t)(160 * 1024 / std::max<size_t>(lds, 1)));
+  const int64_t grid = std::min<int64_t>((int64_t)m.bpb * m.nb, (int64_t)dev.cus * std::max<int64_t>(per_cu, 1));
+  MSH_TIMED_LAUNCH((wgp_kernel<W, KX>), dim3((unsigned)grid), dim3(W * WAVE), (unsigned)lds, s, m);
+  return hipGetLastError();
+}
+
+bool use_persistent(const BatchArgs& a, const DeviceInfo& dev) {
+  return a.n_groups <= WGP_MAX_GROUPS && !dev.wg_no_persist;
+}
+
+template <int W, bool KX>
+hipError_t launch_single_persistent(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
+  MultiArgs m{};
+  m.a = a;
+  m.nb = 1;
+  m.bpb = (a.n_pods + W * WAVE - 1) / (W * WAVE);
+  m.d[0] = BatchDesc{a.pod_digit, a.pod_tol, a.out_idx, a.out_score, a.out_status, a.n_pods, 0};
+  return launch_persistent<W, KX>(m, dev, s);
+}
+
 template <bool KX, bool SHARD>
 hipError_t launch_wg_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
+  if constexpr (!SHARD) {
+    if (use_persistent(a, dev))
+      return wg_waves(a.n_pods, dev) == 8 ? launch_single_persistent<8, KX>(a, dev, s)
+                                          : launch_single_persistent<4, KX>(a, dev, s);
+  }
   switch (wg_waves(a.n_pods, dev)) {
     case 8: return launch_wg_w<8, KX, SHARD>(a, s);
     default: return launch_wg_w<4, KX, SHARD>(a, s);
@@ -1835,10 +2076,12 @@ hipError_t launch_wg_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s)
 }
 
 template <int W, bool KX>
-hipError_t launch_multi_w(MultiArgs& m, hipStream_t s) {
+hipError_t launch_multi_w(MultiArgs& m, const DeviceInfo& dev, hipStream_t s) {
   int32_t blocks = 0;  // per batch: the largest batch's
   for (int b = 0; b < m.nb; ++b) blocks = std::max(blocks, (m.d[b].n_pods + W * WAVE - 1) / (W * WAVE));
   if (blocks == 0) return hipSuccess;
+  m.bpb = blocks;
+  if (use_persistent(m.a, dev)) return launch_persistent<W, KX>(m, dev, s);
   MSH_TIMED_LAUNCH((wg_kernel<W, KX, false, true>), dim3((unsigned)blocks, (unsigned)m.nb), dim3(W * WAVE), 0, s, m);
   return hipGetLastError();
 }
@@ -1881,8 +2124,8 @@ hipError_t launch_batches(const BatchArgs& a, const BatchDesc* d, int nb, const 
   }
   const bool kx = needs_kx(a.pp);
   switch (wg_waves(pods, dev)) {
-    case 8: return kx ? launch_multi_w<8, true>(m, s) : launch_multi_w<8, false>(m, s);
-    default: return kx ? launch_multi_w<4, true>(m, s) : launch_multi_w<4, false>(m, s);
+    case 8: return kx ? launch_multi_w<8, true>(m, dev, s) : launch_multi_w<8, false>(m, dev, s);
+    default: return kx ? launch_multi_w<4, true>(m, dev, s) : launch_multi_w<4, false>(m, dev, s);
   }
 }
 

@@ -1,9 +1,8 @@
-"""Where the time of a short timed region goes (the driver runs bench.py --steps 20 --warmup 5):
-host time after each launch of the C3 batch on 2 streams, the HIP-event time of the region, and
-the wall time to the final synchronize. Several repetitions, one JSON line each."""
+"""Where a K=20 bench region goes (the driver's command: 20 C3 batches, one launch of 20): host-side
+timestamps around each call of the timed region and the device-side spans (the region's events, the
+kernel's own start / stop from msh_timing_*). One JSON line per repetition."""
 import importlib
 import json
-import os
 import sys
 import time
 from pathlib import Path
@@ -13,68 +12,69 @@ import torch
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-if os.environ.get("SPIN"):  # A/B: completion waits spin instead of yielding / sleeping
-    import ctypes
-    import importlib.util as _u
-    _hip = ctypes.CDLL(str(Path(_u.find_spec("torch").submodule_search_locations[0]) / "lib" / "libamdhip64.so"),
-                       mode=ctypes.RTLD_GLOBAL)
-    print(json.dumps({"hipSetDeviceFlags(spin)": _hip.hipSetDeviceFlags(int(os.environ["SPIN"]))}), flush=True)
 msh = importlib.import_module("mini-kube-scheduler_amd")
 synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
-K = int(os.environ.get("K", 20))
-NS = int(os.environ.get("STREAMS", 2))
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 dev = torch.device("cuda:0")
 ctx = msh.DeviceContext(0)
 u, nd = synth.make_nodes(5000)[1:]
 ctx.upload_nodes(u, nd)
 p = 100_000
-pd_all, pt_all = synth._make_pods_fast(p * NS, synth.SEED)[1:]
-main = torch.cuda.current_stream()
-streams = [main] + [torch.cuda.Stream() for _ in range(NS - 1)]
+G = msh._native.BATCHES_PER_LAUNCH
+pd_all, pt_all = synth._make_pods_fast(p * G, synth.SEED)[1:]
 bufs = []
-for i in range(NS):
-    b = [torch.from_numpy(np.ascontiguousarray(pd_all[i * p:(i + 1) * p])).to(dev),
-         torch.from_numpy(np.ascontiguousarray(pt_all[i * p:(i + 1) * p])).to(dev),
-         torch.empty(p, dtype=torch.int32, device=dev), torch.empty(p, dtype=torch.int64, device=dev),
-         torch.empty(p, dtype=torch.int32, device=dev)]
-    bufs.append(b)
-fn, h = ctx._fast.schedule_batch_device, ctx._hv()
-args = [(h, p, *[t.data_ptr() for t in b], st.cuda_stream or None) for b, st in zip(bufs, streams)]
+for i in range(G):
+    pd, pt = pd_all[i * p:(i + 1) * p], pt_all[i * p:(i + 1) * p]
+    bufs.append([torch.from_numpy(np.ascontiguousarray(pd)).to(dev), torch.from_numpy(np.ascontiguousarray(pt)).to(dev),
+                 torch.empty(p, dtype=torch.int32, device=dev), torch.empty(p, dtype=torch.int64, device=dev),
+                 torch.empty(p, dtype=torch.int32, device=dev)])
+descs = ctx.batch_descs([(p, *[t.data_ptr() for t in b]) for b in bufs])
+import ctypes
+addr = ctypes.addressof(descs)
+fast, h = ctx._fast, ctx._hv()
+stream = torch.cuda.current_stream(dev)
+sh = stream.cuda_stream
 
 
-r0, r1, ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), torch.cuda.Event()
-jevs = [torch.cuda.Event() for _ in streams[1:]]
-for e in [r0, r1, ev] + jevs:
-    e.record(main)
+def submit(k):
+    for i0 in range(0, k, G):
+        rc = fast.schedule_batches_device(h, min(G, k - i0), addr, sh or None)
+        assert rc == 0
 
 
-def region(k):
-    torch.cuda.synchronize()
-    t = [time.perf_counter()]
-    r0.record(main)
-    ev.record(main)
-    for st in streams[1:]:
-        st.wait_event(ev)
-    t.append(time.perf_counter())
-    for i in range(k):
-        fn(*args[i % NS])
-        t.append(time.perf_counter())
-    for st, e in zip(streams[1:], jevs):
-        e.record(st)
-        main.wait_event(e)
-    r1.record(main)
-    t.append(time.perf_counter())
-    torch.cuda.synchronize()
-    t.append(time.perf_counter())
-    us = np.diff(np.array(t)) * 1e6
-    return {"k": k, "streams": NS, "wall_us": (t[-1] - t[0]) * 1e6, "event_us": r0.elapsed_time(r1) * 1e3,
-            "fork_us": us[0], "launch_us": [round(x, 2) for x in us[1:1 + k]], "join_us": us[1 + k],
-            "sync_us": us[2 + k]}
-
-
-for i in range(5):
-    fn(*args[0])
+submit(5)
 torch.cuda.synchronize()
-for rep in range(6):
-    print(json.dumps(region(K)), flush=True)
-    time.sleep(0.01 if rep % 2 else 0)
+r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for e in (r0, r1):
+    e.record(stream)
+torch.cuda.synchronize()
+for rep in range(8):
+    torch.cuda.synchronize()
+    time.sleep(0.001)
+    ctx.timing_begin(4)
+    t0 = time.perf_counter()
+    r0.record(stream)
+    t1 = time.perf_counter()
+    submit(K)
+    t2 = time.perf_counter()
+    r1.record(stream)
+    t3 = time.perf_counter()
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
+    n, tot, mx = ctx.timing_end()
+    us = lambda a, b: round((b - a) * 1e6, 2)
+    print(json.dumps({"K": K, "rep": rep, "host_total_us": us(t0, t4), "record_r0_us": us(t0, t1), "submit_us": us(t1, t2),
+                      "record_r1_us": us(t2, t3), "sync_us": us(t3, t4), "device_region_us": round(r0.elapsed_time(r1) * 1e3, 2),
+                      "kernel_us": round(tot * 1e3, 2), "launches": n}), flush=True)
+# the same without the events in the region (host clock only)
+for rep in range(4):
+    torch.cuda.synchronize()
+    time.sleep(0.001)
+    t0 = time.perf_counter()
+    submit(K)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(json.dumps({"K": K, "rep": rep, "no_events": True, "submit_us": round((t1 - t0) * 1e6, 2),
+                      "host_total_us": round((t2 - t0) * 1e6, 2)}), flush=True)
+ctx.close()

@@ -1,6 +1,7 @@
 """Summarise scripts/profile_r3.sh (gpurun_out/prof_r3) into profiles/r3_pmc_c3.json: per-launch
-counters of the hot kernels at C3 — wg_kernel with 8 batches per launch (bench.py's default
-submission, "batch_multi"), one batch per launch ("batch"), MIN-MAX ("batch_minmax"), the generic
+counters of the hot kernels at C3 — the persistent class-row kernel wgp_kernel with 32 batches per
+launch (bench.py's default submission, "batch_multi"), one batch per launch ("batch"), MIN-MAX
+("batch_minmax", 32 batches), the generic
 score pipeline ("generic") and seq_kernel at C5 ("sequential") — with the derived figures bench.py's
 roofline quotes. FETCH_SIZE / WRITE_SIZE are KiB (x 1024); WRITE_SIZE reads exact bytes for
 coalesced stores (MI355X_MICROARCH.md, HBM section); FETCH_SIZE is reported raw and with the guide's
@@ -14,7 +15,7 @@ from pathlib import Path
 src = Path(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_r3")
 out = Path(sys.argv[2] if len(sys.argv) > 2 else "profiles/r3_pmc_c3.json")
 N, P = 5000, 100000
-NB = 8  # batches per launch in the multi entries
+NB = 32  # batches per launch in the multi entries (MSH_BATCHES_PER_LAUNCH)
 GROUPS = -(-N // 1024) * 1024 // 256  # 256-node groups of the padded table
 
 
@@ -40,9 +41,9 @@ def stats_avg_ns(tag, prefix):
 
 res = {"source": str(src), "nodes": N, "pods": P, "kernels": {}, "stats": {}}
 for mode, prefix, tags, nb in (
-        ("batch_multi", "void msh::wg_kernel", ("m_sq", "m_sq2", "m_lds", "m_grbm", "m_fetch", "m_write"), NB),
-        ("batch", "void msh::wg_kernel", ("b_sq", "b_lds", "b_fetch", "b_write"), 1),
-        ("batch_minmax", "void msh::wg_kernel", ("k_sq",), NB),
+        ("batch_multi", "void msh::wgp_kernel", ("m_sq", "m_sq2", "m_lds", "m_grbm", "m_fetch", "m_write"), NB),
+        ("batch", "void msh::wgp_kernel", ("b_sq", "b_lds", "b_fetch", "b_write"), 1),
+        ("batch_minmax", "void msh::wgp_kernel", ("k_sq",), NB),
         ("generic", "msh::generic_kernel", ("g_sq", "g_fetch"), 1),
         ("sequential", "void msh::seq_kernel", ("s_sq", "s_fetch", "s_write"), 1)):
     e = {"nodes": N, "pods": P, "batches_per_launch": nb, "launches_per_counter": {}}
@@ -59,9 +60,10 @@ for mode, prefix, tags, nb in (
         e["hbm_bytes_per_launch_fetch_x2"] = 2 * e["fetch_bytes_raw"] + e["write_bytes"]
     if "SQ_INSTS_VALU" in e:
         e["valu_lane_ops_per_eval"] = e["SQ_INSTS_VALU"] * 64 / (N * P * nb)
-        # the scan's modelled VALU per 256-node group and 64-pod wave (wg_kernel: 8 v_bitop3 + the OR
-        # tree + the group flag = 14; with the non-match too, MIN-MAX, 30)
-        per_group = {"batch_multi": 14, "batch": 14, "batch_minmax": 30}.get(mode)
+        # the scan's modelled VALU per 256-node group and 64-pod wave (wgp_kernel: the OR of the 8
+        # class-row words, 4, the group flag, 2 + 1 shared by two groups, the address 0.5 = 7.5; with
+        # the non-matches too, MIN-MAX, 8 v_bitop3 and a second flag more = 17.5)
+        per_group = {"batch_multi": 7.5, "batch": 7.5, "batch_minmax": 17.5}.get(mode)
         if per_group:
             e["scan_model_share"] = per_group * GROUPS * (P / 64) * nb / e["SQ_INSTS_VALU"]
     if "SQ_WAVE_CYCLES" in e:
@@ -73,8 +75,8 @@ for mode, prefix, tags, nb in (
         e["gui_active_cycles_per_xcd"] = cyc
         e["valu_wave_instr_per_simd_cycle"] = e["SQ_INSTS_VALU"] / (1024 * cyc)
     res["kernels"][mode] = e
-for tag, prefix in (("stats", "void msh::wg_kernel"), ("stats_k20", "void msh::wg_kernel"),
-                    ("stats_single", "void msh::wg_kernel"), ("stats_kx", "void msh::wg_kernel"),
+for tag, prefix in (("stats", "void msh::wgp_kernel"), ("stats_k20", "void msh::wgp_kernel"),
+                    ("stats_single", "void msh::wgp_kernel"), ("stats_kx", "void msh::wgp_kernel"),
                     ("stats_generic", "msh::generic_kernel"), ("stats_seq", "void msh::seq_kernel")):
     name, avg, calls = stats_avg_ns(tag, prefix)
     if name:

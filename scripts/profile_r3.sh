@@ -39,6 +39,7 @@ pass m_sq2 multi 0 $SQ2 || exit 1
 pass m_lds multi 0 $LDS || exit 1
 pass m_grbm multi 0 GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
 pass m_fetch multi 0 FETCH_SIZE || exit 1
+pass m_sq3 multi 0 SQ_INSTS_SMEM SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA || exit 1
 pass m_write multi 0 WRITE_SIZE || exit 1
 pass b_sq batch 0 $SQ1 || exit 1
 pass b_lds batch 0 $LDS || exit 1
