@@ -16,16 +16,19 @@
 //   1. feasibility bitmask with wavefront __ballot (X / V words, first feasible per class) -> node_prep_kernel
 //   2. int64 score with the plugin weight fused                    -> decode_pod / decode_ident
 //   3. per-pod normalisation (DEFAULT / REVERSE / MINMAX need the extent of the raw scores over the
-//      feasible list: first feasible match / non-match)             -> wg_kernel<KX> + decode
+//      feasible list: first feasible match / non-match)             -> wgp_kernel / wg_kernel<KX> + decode
 //   4. argmax with a fixed lowest-index tie-break: the lowest group with a hit, then its first set
-//      bit (v_ffbl) in List order                                   -> wg_kernel
-//   5. node-table tiles staged in LDS once per 4-wave workgroup and reused by its 256 pods -> wg_kernel
+//      bit (v_ffbl) in List order                                   -> wgp_kernel / wg_kernel
+//   5. node-table tiles staged in LDS once per workgroup and reused by every pod it serves
+//                                                                   -> wgp_kernel / wg_kernel
 //   generic_kernel does stages 1-5 with an explicit int64 score per pair, for any score-plugin list
 //   (score-column plugins; a real LDS min/max reduction and a wave-shuffle argmax).
 //
 // Kernels, by entry point:
 //   node_prep_kernel (+ prep_reset_kernel)  every upload / patch / plugin change
-//   wg_kernel            msh_schedule_batch*, msh_schedule_batches_device (MULTI), msh_shard_keys_device
+//   wgp_kernel           msh_schedule_batch*, msh_schedule_batches_device on tables up to 8,192 nodes
+//                        (BASELINE C2 / C3): persistent grid, the pod-class rows copied once per workgroup
+//   wg_kernel            the same entry points on larger tables (chunk-streamed), and msh_shard_keys_device
 //   generic_kernel       the batch entry points when the score list names a score-column plugin
 //   rows_kernel          A/B (MSH_BATCH_KERNEL=slices): the round-2 slice kernel
 //   bits_kernel          A/B (MSH_KX_BITS=1): REVERSE / MINMAX on the code planes
