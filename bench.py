@@ -9,7 +9,7 @@ inputs already resident in HBM.
 Modes (the headline line)
   batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per batch per GPU. With N GPUs the
               pods are sharded (each rank its own 100k batches; no data-path collective) -> weak
-              scaling. The K steps are K independent batches (eight distinct pod batches, each with
+              scaling. The K steps are K independent batches (32 distinct pod batches, each with
               its own outputs, used in turn) submitted from one host thread on one HIP stream
               through msh_schedule_batches_device, MSH_BATCHES_PER_LAUNCH (32) batches per kernel
               launch: the submission a caller with several drained batches ready makes.
@@ -93,7 +93,7 @@ def parse():
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary configs (one GPU only)")
     ap.add_argument("--submit", choices=["multi", "single"], default="multi",
-                    help="batch mode: the K steps through msh_schedule_batches_device, 8 batches per launch "
+                    help="batch mode: the K steps through msh_schedule_batches_device, 32 batches per launch "
                          "(default), or (A/B) one msh_schedule_batch_device launch per step; one host thread "
                          "and one HIP stream either way")
     return ap.parse_args()
@@ -191,7 +191,7 @@ def main():
         ctx.upload_nodes(unsched, node_digit)
         node_base = 0
         # pod-sharded weak scaling: rank r owns pods [r*P*B, (r+1)*P*B) of one global stream, split
-        # into B distinct batches of P pods (batch mode: B = 8, step i schedules batch i mod 8)
+        # into B distinct batches of P pods (batch mode: B = 32, step i schedules batch i mod 32)
         nb = G if mode == "batch" else 1
         pd_all, pt_all = synth._make_pods_fast(p_total * world * nb, synth.SEED)[1:]
         batches = []
@@ -209,7 +209,7 @@ def main():
     klen = ctx.shard_keys_len(p) if mode == "nodeshard" else 0  # int32 keys one step all-reduces
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    # the msh_batch descriptors of the eight batches, built once (host memory, read at each call)
+    # the msh_batch descriptors of the 32 batches, built once (host memory, read at each call)
     descs = ctx.batch_descs([(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["idx"].data_ptr(), b["score"].data_ptr(),
                               b["status"].data_ptr()) for b in bufs])
     fast, handle = ctx._fast, ctx._hv()
@@ -220,7 +220,7 @@ def main():
     def submit(k: int) -> None:
         """Steps 0..k-1 of the current mode, in order, on `stream` (one host thread)."""
         if mode == "batch" and multi:
-            for i0 in range(0, k, G):  # batch i of a launch = buffer i (launches start at multiples of 8)
+            for i0 in range(0, k, G):  # batch i of a launch = buffer i (launches start at multiples of G)
                 rc = fast.schedule_batches_device(handle, min(G, k - i0), descs_addr, sh or None)
                 if rc:
                     ctx._check(rc)
@@ -245,29 +245,37 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # ---- the timed region: barrier (N > 1) + synchronize, K steps, synchronize (+ barrier) ----
-    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for e in (r0, r1):  # create the HIP events before the region (a torch Event makes its HIP event on first record)
-        e.record(stream)
+    # ---- the timed region: barrier (N > 1) + synchronize, K steps, synchronize (+ barrier). Nothing
+    # but the K steps between the clocks: no events (two event records cost ~15 us of a 40 us K = 20
+    # region, profiles/ab/r3_k20_probe.jsonl); the device span is taken from an untimed repeat below ----
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r0.record(stream)
     submit(args.steps)
-    r1.record(stream)
     torch.cuda.synchronize()
     if world > 1:  # the barrier and a second synchronize only where there is a barrier
         dist.barrier()
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    region_ms = r0.elapsed_time(r1)  # device span of the region on the launch stream
+
+    # the same K steps again, untimed by the clock, between two events on the launch stream: the
+    # device span of a region (reported beside the wall-clock figure, never as `value`)
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for e in (r0, r1):  # create the HIP events first (a torch Event makes its HIP event on first record)
+        e.record(stream)
+    torch.cuda.synchronize()
+    r0.record(stream)
+    submit(args.steps)
+    r1.record(stream)
+    torch.cuda.synchronize()
+    region_ms = r0.elapsed_time(r1)
 
     # ---- the dominant kernel's launch duration, for the roofline: R launches back to back on the
     # stream the kernels run on, each timed by its own start / stop events recorded at the kernel's
     # start and completion (msh_timing_begin: hipExtLaunchKernelGGL events, the interval rocprofv3's
-    # kernel trace averages); in batch mode the full 8-batch launches of the default submission ----
+    # kernel trace averages); in batch mode the full 32-batch launches of the default submission ----
     R = 50 if mode != "nodeshard" else min(args.steps, 20)
     ctx.timing_begin(R)
     for _ in range(R):

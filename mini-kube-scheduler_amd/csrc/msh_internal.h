@@ -96,13 +96,41 @@ constexpr int ER_TG = 8;               // groups per LDS tile of the batch kerne
 // pod class, t = 0 (does not tolerate the unschedulable taint) and t = 1 (tolerates), so that a pod's
 // hit words are one row read, H[t][r] = the word's nodes that pass NodeUnschedulable for class t AND
 // have suffix digit r (row 10 zero); then F[t] = the word's nodes feasible for class t (the REVERSE /
-// MINMAX modes' non-matches are F[t] & ~H[t][r]). Per group, for chunk c of 4 words:
-//   hrows[g * HR_GD + ((c * 2 + t) * ER_ROWS + r) * 4 + k] = H[t][r] of word g * PLANE_GW + 4 c + k
-//   hrows[g * HR_GD + (HR_Q + 2 t) * 4 + j]              = F[t] of word g * PLANE_GW + j
+// MINMAX modes' non-matches are F[t] & ~H[t][r]). Per group 48 16-byte entries: H[t][r] of chunk c
+// (words 4 c .. 4 c + 3 of the group) is entry hr_entry(c, t, r), F[t] entries HR_F + 2 t (words 0-3)
+// and HR_F + 2 t + 1 (words 4-7):
+//   hrows[g * HR_GD + hr_entry(c, t, r) * 4 + k] = H[t][r] of word g * PLANE_GW + 4 c + k
+//   hrows[g * HR_GD + (HR_F + 2 t) * 4 + j]      = F[t] of word g * PLANE_GW + j
 // 3 B per node; a pod reads 32 B per 256-node group (two 16-byte entries), half of the digit rows + X.
-constexpr int HR_Q = 4 * ER_ROWS;      // 16-byte row entries per group (2 chunks x 2 classes x 11 rows)
-constexpr int HR_GQ = HR_Q + 4;        // ... then F[0], F[1] (two entries each)
+// The order is LDS-bank aware: the lanes of one ds_read_b128 are served in groups of 16, each lane's
+// 16 B from bank slot (entry mod 16) (MI355X_MICROARCH.md, LDS), so two lanes of a group that read
+// different entries of one slot cost an extra LDS cycle. A scan instruction reads chunk 0 (or chunk 1)
+// for every lane: the 11 non-tolerating rows of a chunk take 11 slots and the tolerating rows the
+// other 5, tolerating rows 0-4 and 5-9 sharing them (a conflict needs two tolerating pods of different
+// rows in one 16-lane group); row 10 (pods without a digit suffix) of the tolerating class shares a
+// slot with a rare non-tolerating row. Rows [slot]:
+//   entries  0-15: chunk 0: t=0 r=0..10 [0..10], t=1 r=0..4 [11..15]
+//   entries 16-31: chunk 1: t=1 r=0..4 [0..4], t=0 r=0..10 [5..15]
+//   entries 32-47: chunk 1 t=1 r=5..9 [0..4], F[0] F[1] [5..8], chunk 1 t=1 r=10 [9],
+//                  chunk 0 t=1 r=10 [10], chunk 0 t=1 r=5..9 [11..15]
+// (with conflicting class rows, 16-lane groups holding a tolerating pod made the C3 scan ~10% slower,
+// profiles/ab/r3_wgp_ab.jsonl).
+// After the 48 row entries, 6 entries (48 uint16) of first-node offsets, written by hr_first_kernel
+// after each prep: [cls] = the first node of the group in H[t][r] (cls = 11 t + r), [24 + cls] = the
+// first in F[t] & ~H[t][r], as an offset 0..255, HR_NONE when the group has none. The batch kernel
+// resolves a pod's exact node from them once its scan has found the first pair of groups with a hit.
+// The group stride (54 entries) shifts every entry of a group by the same slot: no new conflicts.
+constexpr int HR_ROWQ = 48;            // 16-byte row entries per group
+constexpr int HR_FIRST = HR_ROWQ;      // first-node offsets (uint16) at entries 48-53
+constexpr int HR_CLS = 24;             // offsets per kind (22 pod classes, padded)
+constexpr int HR_GQ = HR_ROWQ + 6;     // 16-byte entries per group
 constexpr int HR_GD = HR_GQ * 4;       // dwords per group
+constexpr int HR_F = 37;               // F[0] at entries 37-38, F[1] at 39-40
+constexpr uint16_t HR_NONE = 0xFFFF;
+__host__ __device__ constexpr uint32_t hr_entry(uint32_t c, uint32_t t, uint32_t r) {
+  return t == 0 ? (c == 0 ? r : 21 + r)
+                : r < 5 ? (c == 0 ? 11 + r : 16 + r) : r < 10 ? (c == 0 ? 38 + r : 27 + r) : (c == 0 ? 42u : 41u);
+}
 constexpr int ER_PAD = 2 * ER_TG;      // groups of padding: whole-tile copies need no clamp
 
 // ---- launchers (msh_kernels.hip) ----

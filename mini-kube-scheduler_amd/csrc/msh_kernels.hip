@@ -138,12 +138,12 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
       if (t == 0) m &= x0;
       const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;  // i - lane: the wave's first node
       const uint32_t g = word / PLANE_GW, c = (word / 4) & 1u, k = word & 3u;
-      hrows[(size_t)g * HR_GD + ((c * 2 + (uint32_t)t) * ER_ROWS + (uint32_t)r) * 4 + k] = (uint32_t)(m >> (32 * half));
+      hrows[(size_t)g * HR_GD + hr_entry(c, (uint32_t)t, (uint32_t)r) * 4 + k] = (uint32_t)(m >> (32 * half));
     } else if (lane < 4 * ER_ROWS + 4) {
       const int t = (lane >> 1) & 1, half = lane & 1;
       const unsigned long long m = t == 0 ? (pm[PLANE_V] & x0) : pm[PLANE_V];
       const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
-      hrows[(size_t)(word / PLANE_GW) * HR_GD + (HR_Q + 2 * t) * 4 + word % PLANE_GW] = (uint32_t)(m >> (32 * half));
+      hrows[(size_t)(word / PLANE_GW) * HR_GD + (HR_F + 2 * t) * 4 + word % PLANE_GW] = (uint32_t)(m >> (32 * half));
     }
   }
   const unsigned long long m0 = pm[PLANE_V] & ~pm[PLANE_X], m1 = pm[PLANE_V];
@@ -543,10 +543,14 @@ __device__ __forceinline__ bool rows_hits(const uint4& e0, const uint4& e1, cons
   return ((h[0] | h[1] | h[2]) | (h[3] | h[4] | h[5]) | (h[6] | h[7])) != 0u;
 }
 
-#ifdef MSH_STAMPS
-// Timeline A/B build only (scripts/stamps.sh; never in libminisched_hip.so): per wave, the
-// 100 MHz wall clock at entry, after the prologue's loads, after the scan and before the stores.
+#if defined(MSH_STAMPS) || defined(MSH_CLOCK_STAMPS)
+// Timeline / clock A/B builds only (scripts/stamps.sh, scripts/ab_build.sh; never in
+// libminisched_hip.so): per wave, the 100 MHz wall clock at entry, after the prologue's loads, after
+// the scan and before the stores (MSH_STAMPS); or the shader and 100 MHz clocks at a persistent
+// wave's start and end (MSH_CLOCK_STAMPS, wgp_kernel).
 __device__ unsigned long long* g_stamps;
+#endif
+#ifdef MSH_STAMPS
 #define MSH_STAMP(i) (__builtin_amdgcn_s_waitcnt(0), stamp_t[i] = wall_clock64())
 #else
 #define MSH_STAMP(i) ((void)0)
@@ -808,8 +812,9 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
 // with its own pod columns and outputs, described in the kernel arguments; the grid is 2-D, batch =
 // blockIdx.y (one scalar load of its descriptor).
 // ---------------------------------------------------------------------------------------
-// Phase experiments of the stamps build only (scripts/wg_expt.sh; never the product library):
-// bit 0 skips the scan loop, bit 1 the output stores, bit 2 the table copy into LDS. MSH_WG_FLAG
+// Phase experiments of A/B builds only (scripts/wg_expt.sh, scripts/ab_build.sh; never the product
+// library): bit 0 skips the scan loop, bit 1 the output stores, bit 2 the table copy into LDS; bit 4
+// (wgp_kernel's quad scan) adds a second reduction tree per pair of groups. MSH_WG_FLAG
 // selects the form of the per-group flag (A/B of the same build).
 #ifndef MSH_WG_EXPT
 #define MSH_WG_EXPT 0
@@ -1079,10 +1084,7 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
 // with a hit is the lowest set bit of the bitmap (groups walked in descending List order); its
 // exact first node is resolved from the same two entries (v_ffbl), as in wg_kernel.
 // ---------------------------------------------------------------------------------------
-#ifndef MSH_WGP_PIPE
-#define MSH_WGP_PIPE 0  // A/B: the software-pipelined scan (scripts/wg_expt.sh)
-#endif
-constexpr int WGP_MAX_GROUPS = 32;  // <= 8,192 nodes: 22.5 KB of LDS (24.6 KB with F)
+constexpr int WGP_MAX_GROUPS = 32;  // <= 8,192 nodes: 27 KB of LDS (6 workgroups per CU; C3: 17 KB, 8)
 
 __device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0xfe);
@@ -1090,7 +1092,10 @@ __device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
 
 template <int W, bool KX>
 __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
-  constexpr int GQL = KX ? HR_GQ : HR_Q;  // entries staged per group (F only for KX)
+#ifdef MSH_CLOCK_STAMPS  // diagnostic build only (scripts/ab_build.sh): the in-kernel clock per wave
+  const unsigned long long ck_t0 = __builtin_amdgcn_s_memtime(), ck_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  constexpr int GQL = HR_GQ;  // entries staged per group: the whole record (rows, F, first-node offsets)
   constexpr int NT = W * WAVE;
   extern __shared__ uint4 s_tab[];        // n_groups * GQL entries
   const BatchArgs& A = ka.a;
@@ -1104,151 +1109,207 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
     // loads unconditional (index clamped to the last entry: no branch around them, so all are in
     // flight together), then the stores of the slots below tot; named registers, not an array (a
     // uint4 array went to scratch)
-    static_assert(EPT <= 6, "wgp_kernel copies at most six 16-byte entries per thread");
-    auto src = [&](int k) {
-      const int32_t i = min((int32_t)threadIdx.x + k * NT, tot - 1);
-      const int32_t gi = i / GQL, q = i - gi * GQL;
-      return hr[(size_t)gi * HR_GQ + q];
-    };
+    static_assert(EPT <= 7, "wgp_kernel copies at most seven 16-byte entries per thread");
+    auto src = [&](int k) { return hr[min((int32_t)threadIdx.x + k * NT, tot - 1)]; };
     const uint4 v0 = src(0), v1 = EPT > 1 ? src(1) : v0, v2 = EPT > 2 ? src(2) : v0, v3 = EPT > 3 ? src(3) : v0,
-                v4 = EPT > 4 ? src(4) : v0, v5 = EPT > 5 ? src(5) : v0;
-    const uint4 vs[6] = {v0, v1, v2, v3, v4, v5};
+                v4 = EPT > 4 ? src(4) : v0, v5 = EPT > 5 ? src(5) : v0, v6 = EPT > 6 ? src(6) : v0;
+    const uint4 vs[7] = {v0, v1, v2, v3, v4, v5, v6};
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int32_t i = (int32_t)threadIdx.x + k * NT;
-      if (i < tot) s_tab[i] = vs[k];
+      if ((MSH_WG_EXPT & 4) == 0 && i < tot) s_tab[i] = vs[k];
     }
   }
   const uint32_t ball0 = A.ball[0], ball1 = A.ball[1];
   const IdentDecode idd = make_ident_decode(A.pp);
   __syncthreads();
-
-  // ---- the (batch, block) walk: item t = b * bpb + x, t = blockIdx.x, blockIdx.x + gridDim.x, ...
-  const int32_t bpb = ka.bpb, total = ka.nb * bpb, G = (int32_t)gridDim.x;
+  // ---- the (batch, block) walk: item it = b * bpb + x (pods [NT x, NT x + NT) of batch b, 64 per
+  // wave), it = blockIdx.x, blockIdx.x + G, ... Per item a wave: scans the first two groups; issues the
+  // PREVIOUS item's output stores and then the NEXT item's pod-byte loads; scans the rest; decodes. The
+  // wait for the prefetched bytes (vmcnt counts loads and stores in issue order) thus falls a whole
+  // scan after both. Batch, block and descriptor fields are kept wave-uniform (v_readfirstlane), so
+  // the descriptor reads are scalar loads and the control flow on them scalar branches.
+  // Tried and not kept (profiles/ab/r3_wgp_ab.jsonl): items handed out per wave by an LDS ticket, and
+  // issue priority raised by the share of a workgroup's range still ahead. The waves of a CU do not
+  // progress at one rate (the issue arbiter favours older waves: a CU's first workgroup ends its 6
+  // items in ~13 us, its last in ~23 us), but the CU's LDS stays busy while most of them run, and
+  // either remedy cost more than the tail it shortened.
+  const int32_t bpb = __builtin_amdgcn_readfirstlane(ka.bpb), total = __builtin_amdgcn_readfirstlane(ka.nb * bpb);
+  const int32_t G = (int32_t)gridDim.x;
   int32_t it = (int32_t)blockIdx.x;
   int32_t b = it / bpb, x = it - b * bpb;
   int dq = 0;
   uint32_t tq = 0;
-  int32_t np = 0;
   auto load_pods = [&]() {  // this wave's pod bytes of item (b, x), clamped offset
-    const BatchDesc& d = ka.d[b];
-    np = d.n_pods;
-    const uint32_t jj = min((uint32_t)(x * NT + wv * WAVE + lane), np > 0 ? (uint32_t)(np - 1) : 0u);
-    if (np > 0) {
+    const BatchDesc& d = ka.d[__builtin_amdgcn_readfirstlane(b)];
+    const int32_t np = __builtin_amdgcn_readfirstlane(d.n_pods);
+    const int32_t w0 = __builtin_amdgcn_readfirstlane(x * NT + wv * WAVE);
+    const uint32_t jj = min((uint32_t)(w0 + lane), np > 0 ? (uint32_t)(np - 1) : 0u);
+    if (w0 < np) {
       dq = d.pod_digit[jj];
       tq = d.pod_tol[jj];
     }
   };
-  if (it < total) load_pods();
-  while (it < total) {
-    const int32_t cb = b, cx = x, cnp = np;
-    const int cdq = dq;
-    const uint32_t ctq = tq;
-    it += G;  // the next item, its pod bytes in flight during this item's scan
+  struct Item {
+    int32_t cb, wbase, j;  // batch, the wave's first pod, the lane's pod
+    bool live, act;        // the wave has pods in this item / the lane has a pod
+    uint32_t code, tol, cls, e0, e1;  // cls = 11 tol + row; e0 / e1: its class-row entries (hr_entry)
+  };
+  auto prepare = [&]() {  // the state of item (b, x) from its loaded pod bytes
+    Item m;
+    const bool in = it < total;
+    m.cb = __builtin_amdgcn_readfirstlane(in ? b : 0);
+    const int32_t np = __builtin_amdgcn_readfirstlane(in ? ka.d[m.cb].n_pods : 0);
+    m.wbase = __builtin_amdgcn_readfirstlane(x * NT + wv * WAVE);
+    m.live = __builtin_amdgcn_readfirstlane(m.wbase < np ? 1 : 0) != 0;
+    m.j = m.wbase + lane;
+    m.act = m.j < np;
+    m.code = (m.act && dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;
+    m.tol = (m.act && tq) ? 1u : 0u;
+    const uint32_t row = m.code <= 9u ? m.code : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
+    m.cls = m.tol * ER_ROWS + row;
+    m.e0 = hr_entry(0, m.tol, row);
+    m.e1 = hr_entry(1, m.tol, row);
+    return m;
+  };
+  auto advance = [&]() {  // to the next item of this workgroup, its pod bytes in flight
+    it += G;
     x += G;
     while (x >= bpb) {
       x -= bpb;
       ++b;
     }
     if (it < total) load_pods();
-    if (cx * NT + wv * WAVE >= cnp) continue;  // this wave's slice lies past the batch's end
-    const int32_t j = cx * NT + wv * WAVE + lane;
-    const bool act = j < cnp;
-    const uint32_t code = (act && cdq >= 0 && cdq <= 9) ? (uint32_t)cdq : CODE_NONE_POD;
-    const uint32_t tol = (act && ctq) ? 1u : 0u;
-    const uint32_t row = code <= 9u ? code : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
-    const uint32_t ra = tol * ER_ROWS + row;                            // chunk 0's entry; chunk 1 at +22
-    const uint32_t fa = HR_Q + 2 * tol;                                 // F[tol] (KX)
+  };
+  // the previous item's outputs, stored during the next scan (or after the loop): wave-uniform
+  // bases (the wave's first pod) plus the lane's constant offset, so the stores read no VGPR the scan
+  // writes (a VGPR an outstanding store still has to read would cost a vmcnt wait inside the scan)
+  const uint32_t lo4 = (uint32_t)lane * 4u, lo8 = (uint32_t)lane * 8u;  // the lane's byte offsets
+  int32_t s_cb = 0, s_wbase = 0, s_oi = 0, s_ost = 0;
+  int64_t s_osc = 0;
+  bool s_pending = false;  // the lane holds outputs not yet stored
+  // The store addresses too stay live until the scan has ended (pinned below with the values): a
+  // register an outstanding store reads may not be rewritten before the store completes, and the
+  // compiler would otherwise reuse them at once and wait for the stores (vmcnt) right there.
+  int32_t *p_oi = nullptr, *p_ot = nullptr;
+  int64_t* p_os = nullptr;
+  auto flush = [&]() {
+    if ((MSH_WG_EXPT & 2) != 0 && s_oi != 0x7fffffff) s_pending = false;  // phase experiment: no stores
+    const BatchDesc& d = ka.d[s_cb];
+    const bool has_score = d.out_score != nullptr;
+    p_oi = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d.out_idx + s_wbase) + lo4);
+    p_os = reinterpret_cast<int64_t*>(reinterpret_cast<char*>((has_score ? d.out_score : nullptr) + s_wbase) + lo8);
+    p_ot = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d.out_status + s_wbase) + lo4);
+    if (s_pending) {
+      *p_oi = s_oi;
+      if (has_score) *p_os = s_osc;  // optional output (NULL: not written)
+      *p_ot = s_ost;
+    }
+    s_pending = false;
+  };
+  if (it < total) load_pods();
+  Item cur = prepare();
+#ifdef MSH_CLOCK_STAMPS
+  int n_items = 0;
+#endif
+  while (it < total) {
+#ifdef MSH_CLOCK_STAMPS
+    ++n_items;
+#endif
+    if (!cur.live) {  // this wave's slice lies past its batch's end
+      flush();
+      advance();
+      cur = prepare();
+      continue;
+    }
+    const uint32_t tol = cur.tol;
+    const uint32_t e0 = cur.e0, e1 = cur.e1;  // the lane's chunk-0 and chunk-1 class-row entries
+    const uint32_t cls = cur.cls;               // its class (first-node tables)
+    const uint32_t fa = HR_F + 2 * tol;         // F[tol] (KX)
+    // Groups descending, four per step (eight ds_read_b128 in flight; n_groups is a multiple of 4:
+    // tables are padded to 1,024-node blocks), one flag per PAIR of groups: bit q of bm = group 2q or
+    // 2q + 1 holds a feasible digit match (the 16 words of a pair reduce in 8 VALU: 7 v_bitop3 OR3 and
+    // one more), and, KX, bit q of bx = one of them holds a feasible non-match (F[t] & ~H, one v_bitop3
+    // per word). The previous item's stores and the next item's loads go after the first step.
     uint32_t bm = 0, bx = 0;
-    auto group = [&](const uint4* tg, uint32_t& h, uint32_t& n) {
-      const uint4 e0 = tg[ra], e1 = tg[ra + 2 * ER_ROWS];
-      h = or3(or3(e0.x, e0.y, e0.z), or3(e0.w, e1.x, e1.y), e1.z | e1.w);
-      if constexpr (KX) {
-        const uint4 f0 = tg[fa], f1 = tg[fa + 1];
-        n = andn(f0.x, e0.x);
-        n = acc_andn(n, f0.y, e0.y);
-        n = acc_andn(n, f0.z, e0.z);
-        n = acc_andn(n, f0.w, e0.w);
-        n = acc_andn(n, f1.x, e1.x);
-        n = acc_andn(n, f1.y, e1.y);
-        n = acc_andn(n, f1.z, e1.z);
-        n = acc_andn(n, f1.w, e1.w);
-      }
+    auto or16 = [](const uint4& a, const uint4& b, const uint4& c, const uint4& d) {
+      return or3(or3(or3(a.x, a.y, a.z), or3(a.w, b.x, b.y), or3(b.z, b.w, c.x)),
+                 or3(or3(c.y, c.z, c.w), or3(d.x, d.y, d.z), d.w), 0u);
     };
-    int32_t k = n_groups - 1;
-    if constexpr (!KX && MSH_WGP_PIPE) {
-      // software-pipelined: the next pair's four entries are read before this pair is reduced
-      auto or8 = [](const uint4& e0, const uint4& e1) {
-        return or3(or3(e0.x, e0.y, e0.z), or3(e0.w, e1.x, e1.y), e1.z | e1.w);
-      };
-      const uint4* tp = s_tab + k * GQL;
-      uint4 a1 = tp[ra], b1 = tp[ra + 2 * ER_ROWS], a0 = a1, b0 = b1;
-      if (k >= 1) {
-        a0 = (tp - GQL)[ra];
-        b0 = (tp - GQL)[ra + 2 * ER_ROWS];
-      }
-      for (; k >= 1; k -= 2) {
-        const uint4 c1 = a1, d1 = b1, c0 = a0, d0 = b0;
-        if (k >= 3) {
-          const uint4* tn = s_tab + (k - 2) * GQL;
-          a1 = tn[ra];
-          b1 = tn[ra + 2 * ER_ROWS];
-          a0 = (tn - GQL)[ra];
-          b0 = (tn - GQL)[ra + 2 * ER_ROWS];
-        } else if (k == 2) {
-          a1 = s_tab[ra];
-          b1 = s_tab[ra + 2 * ER_ROWS];
-        }
-        bm = lshl_or(bm, 2, lshl_or(min1(or8(c1, d1)), 1, min1(or8(c0, d0))));
-      }
-      if (k == 0) bm = lshl_or(bm, 1, min1(or8(a1, b1)));
-    } else {
-      for (; k >= 1; k -= 2) {  // two groups per step, descending
-        const uint4* t1 = s_tab + k * GQL;
-        uint32_t h1, h0, n1 = 0, n0 = 0;
-        group(t1, h1, n1);
-        group(t1 - GQL, h0, n0);
-        bm = lshl_or(bm, 2, lshl_or(min1(h1), 1, min1(h0)));
-        if constexpr (KX) bx = lshl_or(bx, 2, lshl_or(min1(n1), 1, min1(n0)));
-      }
-      if (k == 0) {
-        uint32_t h0, n0 = 0;
-        group(s_tab, h0, n0);
-        bm = lshl_or(bm, 1, min1(h0));
-        if constexpr (KX) bx = lshl_or(bx, 1, min1(n0));
-      }
+    auto nm16 = [&](const uint4* tg, const uint4& a, const uint4& b, const uint4& c, const uint4& d) {
+      const uint4 f0 = tg[fa], f1 = tg[fa + 1], f2 = tg[GQL + fa], f3 = tg[GQL + fa + 1];
+      uint32_t n = andn(f0.x, a.x);
+      n = acc_andn(n, f0.y, a.y);
+      n = acc_andn(n, f0.z, a.z);
+      n = acc_andn(n, f0.w, a.w);
+      n = acc_andn(n, f1.x, b.x);
+      n = acc_andn(n, f1.y, b.y);
+      n = acc_andn(n, f1.z, b.z);
+      n = acc_andn(n, f1.w, b.w);
+      n = acc_andn(n, f2.x, c.x);
+      n = acc_andn(n, f2.y, c.y);
+      n = acc_andn(n, f2.z, c.z);
+      n = acc_andn(n, f2.w, c.w);
+      n = acc_andn(n, f3.x, d.x);
+      n = acc_andn(n, f3.y, d.y);
+      n = acc_andn(n, f3.z, d.z);
+      n = acc_andn(n, f3.w, d.w);
+      return n;
+    };
+    auto step = [&](int32_t q) {  // groups q .. q + 3
+      const uint4* t = s_tab + q * GQL;
+      const uint4 a0 = t[e0], b0 = t[e1], a1 = t[GQL + e0], b1 = t[GQL + e1];
+      const uint4 a2 = t[2 * GQL + e0], b2 = t[2 * GQL + e1], a3 = t[3 * GQL + e0], b3 = t[3 * GQL + e1];
+      bm = lshl_or(bm, 2, lshl_or(min1(or16(a2, b2, a3, b3)), 1, min1(or16(a0, b0, a1, b1))));
+      if constexpr (KX)
+        bx = lshl_or(bx, 2, lshl_or(min1(nm16(t + 2 * GQL, a2, b2, a3, b3)), 1, min1(nm16(t, a0, b0, a1, b1))));
+    };
+    int32_t q = (MSH_WG_EXPT & 1) ? -4 : n_groups - 4;
+    if (q >= 0) {
+      step(q);
+      q -= 4;
     }
+    flush();
+    advance();
+    for (; q >= 0; q -= 4) step(q);
+    // the stored values and their addresses live through the scan
+    asm volatile("" ::"v"(s_oi), "v"(s_ost), "v"(s_osc), "v"(p_oi), "v"(p_os), "v"(p_ot));
+    // the exact first node: the first flagged pair, its first group with one, the offset from the table
+    auto first_of = [&](uint32_t bits, uint32_t kind) {
+      const uint32_t pq = lowbit(bits);
+      const uint16_t* t0 = reinterpret_cast<const uint16_t*>(s_tab + 2 * pq * GQL + HR_FIRST) + kind + cls;
+      const uint16_t* t1 = reinterpret_cast<const uint16_t*>(s_tab + (2 * pq + 1) * GQL + HR_FIRST) + kind + cls;
+      const uint32_t f0 = *t0, f1 = *t1;
+      return f0 != HR_NONE ? 2 * pq * GROUP_NODES + f0 : (2 * pq + 1) * GROUP_NODES + f1;
+    };
     uint32_t rm = NOFIT, rx = NOFIT;
-    if (bm) {
-      const uint32_t fm = lowbit(bm);
-      const uint4* tg = s_tab + fm * GQL;
-      const uint4 e0 = tg[ra], e1 = tg[ra + 2 * ER_ROWS];
-      const uint32_t h[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-      rm = hits_first(h, fm);
-    }
-    if constexpr (KX) {
-      if (bx) {
-        const uint32_t fx = lowbit(bx);
-        const uint4* tg = s_tab + fx * GQL;
-        const uint4 e0 = tg[ra], e1 = tg[ra + 2 * ER_ROWS], f0 = tg[fa], f1 = tg[fa + 1];
-        const uint32_t n[PLANE_GW] = {f0.x & ~e0.x, f0.y & ~e0.y, f0.z & ~e0.z, f0.w & ~e0.w,
-                                      f1.x & ~e1.x, f1.y & ~e1.y, f1.z & ~e1.z, f1.w & ~e1.w};
-        rx = hits_first(n, fx);
-      }
-    }
-    if (!act) continue;
-    int32_t oi, ost;
-    int64_t osc;
+    if (bm) rm = first_of(bm, 0);
+    if constexpr (KX)
+      if (bx) rx = first_of(bx, HR_CLS);
     const int64_t im = rm != NOFIT ? (int64_t)rm : -1, ia = key_to_idx(tol ? ball1 : ball0);
     if constexpr (KX)
-      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, A.pp, &oi, &osc, &ost);
+      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, cur.code != CODE_NONE_POD, A.pp, &s_oi, &s_osc, &s_ost);
     else
-      decode_ident(im, ia, code != CODE_NONE_POD, idd, &oi, &osc, &ost);
-    const BatchDesc& d = ka.d[cb];
-    d.out_idx[j] = oi;
-    if (d.out_score) d.out_score[j] = osc;  // optional output (NULL: not written)
-    d.out_status[j] = ost;
+      decode_ident(im, ia, cur.code != CODE_NONE_POD, idd, &s_oi, &s_osc, &s_ost);
+    s_cb = cur.cb;
+    s_wbase = cur.wbase;
+    s_pending = cur.act;
+    cur = prepare();
   }
+  flush();
+#ifdef MSH_CLOCK_STAMPS
+  const unsigned long long ck_t1 = __builtin_amdgcn_s_memtime(), ck_r1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && g_stamps) {
+    unsigned long long* o = g_stamps + ((size_t)blockIdx.x * W + wv) * 8;
+    o[0] = ck_t0;
+    o[1] = ck_r0;
+    o[2] = ck_t1;
+    o[3] = ck_r1;
+    o[4] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID: cu / sh / se / simd / wave
+    o[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
+    o[6] = (unsigned long long)n_items;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1895,6 +1956,32 @@ __global__ __launch_bounds__(256) void prep_reset_kernel(uint32_t* __restrict__ 
   }
 }
 
+// The first-node offsets of every (group, pod class) behind the class rows (msh_internal.h HR_FIRST):
+// one thread per (group, kind, class) slot, after node_prep_kernel has written the rows.
+__global__ __launch_bounds__(256) void hr_first_kernel(uint32_t* __restrict__ hrows, int32_t n_groups) {
+  const int32_t i = (int32_t)(blockIdx.x * 256 + threadIdx.x);
+  if (i >= n_groups * 2 * HR_CLS) return;
+  const int32_t g = i / (2 * HR_CLS), j = i - g * (2 * HR_CLS);
+  const uint32_t kind = (uint32_t)j / HR_CLS, cls = (uint32_t)j - kind * HR_CLS;
+  uint16_t* out = reinterpret_cast<uint16_t*>(hrows + (size_t)g * HR_GD + HR_FIRST * 4) + j;
+  if (cls >= 2 * ER_ROWS) {
+    *out = HR_NONE;
+    return;
+  }
+  const uint32_t t = cls >= ER_ROWS ? 1u : 0u, r = cls - t * ER_ROWS;
+  const uint4* tg = reinterpret_cast<const uint4*>(hrows + (size_t)g * HR_GD);
+  const uint4 w0 = tg[hr_entry(0, t, r)], w1 = tg[hr_entry(1, t, r)];
+  uint32_t h[PLANE_GW] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  if (kind == 1) {  // the feasible non-matches F[t] & ~H[t][r]
+    const uint4 f0 = tg[HR_F + 2 * t], f1 = tg[HR_F + 2 * t + 1];
+    const uint32_t f[PLANE_GW] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+    for (int k = 0; k < PLANE_GW; ++k) h[k] = f[k] & ~h[k];
+  }
+  const uint32_t m = hits_first(h, 0);
+  *out = (uint16_t)(m < GROUP_NODES ? m : HR_NONE);
+}
+
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n, int32_t n_pad,
                             int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows,
                             uint32_t* d_hrows, hipStream_t s, const unsigned long long* d_patch, int32_t patch_count) {
@@ -1905,6 +1992,9 @@ hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int
   if (n_pad == 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel, dim3(n_pad / PREP_THREADS), dim3(PREP_THREADS), 0, s, d_unsched, d_digit, n,
                      has_nu, d_ball, d_planes, d_erows, d_hrows);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int32_t slots = n_pad / GROUP_NODES * 2 * HR_CLS;
+  hipLaunchKernelGGL(hr_first_kernel, dim3((slots + 255) / 256), dim3(256), 0, s, d_hrows, n_pad / GROUP_NODES);
   return hipGetLastError();
 }
 
@@ -2040,13 +2130,19 @@ hipError_t launch_wg_w(const BatchArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// The persistent kernel over m.nb batches: as many workgroups as stay resident (8 per CU with 4-wave
-// workgroups, fewer when the table's LDS copy limits them), never more than the launch's blocks.
-template <int W, bool KX>
+// The persistent kernel over m.nb batches of m.bpb 256-pod blocks: as many workgroups as stay
+// resident (8 per CU: 32 waves, the CU's limit; fewer when the table's LDS copy limits them), never
+// more than the launch's blocks.
+template <bool KX>
 hipError_t launch_persistent(MultiArgs& m, const DeviceInfo& dev, hipStream_t s) {
-  const size_t lds = (size_t)m.a.n_groups * (KX ? HR_GQ : HR_Q) * sizeof(uint4);
-  const int64_t per_cu = std::min<int64_t>(32 / W, (int64_t)(160 * 1024 / std::max<size_t>(lds, 1)));
-  const int64_t grid = std::min<int64_t>((int64_t)m.bpb * m.nb, (int64_t)dev.cus * std::max<int64_t>(per_cu, 1));
+  constexpr int W = 4;
+  int32_t maxp = 0;
+  for (int b = 0; b < m.nb; ++b) maxp = std::max(maxp, m.d[b].n_pods);
+  if (maxp == 0) return hipSuccess;
+  m.bpb = (maxp + W * WAVE - 1) / (W * WAVE);
+  const size_t lds = (size_t)m.a.n_groups * HR_GQ * sizeof(uint4);
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / W, (int64_t)(160 * 1024 / std::max<size_t>(lds, 1))));
+  const int64_t grid = std::min<int64_t>((int64_t)m.bpb * m.nb, (int64_t)dev.cus * per_cu);
   MSH_TIMED_LAUNCH((wgp_kernel<W, KX>), dim3((unsigned)grid), dim3(W * WAVE), (unsigned)lds, s, m);
   return hipGetLastError();
 }
@@ -2055,22 +2151,19 @@ bool use_persistent(const BatchArgs& a, const DeviceInfo& dev) {
   return a.n_groups <= WGP_MAX_GROUPS && !dev.wg_no_persist;
 }
 
-template <int W, bool KX>
+template <bool KX>
 hipError_t launch_single_persistent(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
   MultiArgs m{};
   m.a = a;
   m.nb = 1;
-  m.bpb = (a.n_pods + W * WAVE - 1) / (W * WAVE);
   m.d[0] = BatchDesc{a.pod_digit, a.pod_tol, a.out_idx, a.out_score, a.out_status, a.n_pods, 0};
-  return launch_persistent<W, KX>(m, dev, s);
+  return launch_persistent<KX>(m, dev, s);
 }
 
 template <bool KX, bool SHARD>
 hipError_t launch_wg_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
   if constexpr (!SHARD) {
-    if (use_persistent(a, dev))
-      return wg_waves(a.n_pods, dev) == 8 ? launch_single_persistent<8, KX>(a, dev, s)
-                                          : launch_single_persistent<4, KX>(a, dev, s);
+    if (use_persistent(a, dev)) return launch_single_persistent<KX>(a, dev, s);
   }
   switch (wg_waves(a.n_pods, dev)) {
     case 8: return launch_wg_w<8, KX, SHARD>(a, s);
@@ -2080,11 +2173,11 @@ hipError_t launch_wg_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s)
 
 template <int W, bool KX>
 hipError_t launch_multi_w(MultiArgs& m, const DeviceInfo& dev, hipStream_t s) {
+  if (use_persistent(m.a, dev)) return launch_persistent<KX>(m, dev, s);
   int32_t blocks = 0;  // per batch: the largest batch's
   for (int b = 0; b < m.nb; ++b) blocks = std::max(blocks, (m.d[b].n_pods + W * WAVE - 1) / (W * WAVE));
   if (blocks == 0) return hipSuccess;
   m.bpb = blocks;
-  if (use_persistent(m.a, dev)) return launch_persistent<W, KX>(m, dev, s);
   MSH_TIMED_LAUNCH((wg_kernel<W, KX, false, true>), dim3((unsigned)blocks, (unsigned)m.nb), dim3(W * WAVE), 0, s, m);
   return hipGetLastError();
 }
@@ -2212,7 +2305,7 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
   return launch_seq_nw<15, false>(ka, rs, s);
 }
 
-#ifdef MSH_STAMPS
+#if defined(MSH_STAMPS) || defined(MSH_CLOCK_STAMPS)
 extern "C" int msh_stamps_set(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
 #endif
 

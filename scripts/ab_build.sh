@@ -1,0 +1,31 @@
+#!/bin/bash
+# Build A/B variants of the kernel library (CPU, here) into scripts/expt/ (git-ignored; never the
+# product library): one libab_<name>.so per "name=flags" argument, the product sources compiled with
+# those -D flags; plus the timing driver scripts/expt/run (scripts/wg_expt_run.cpp).
+#   scripts/ab_build.sh base= quad=-DMSH_WGP_QUAD=1 pipe=-DMSH_WGP_PIPE=1
+# A SRC_<name>=<file> environment variable compiles <file> instead of msh_kernels.hip for that variant
+# (e.g. an older revision from git show, for a before / after comparison).
+# On the GPU box: scripts/expt/run scripts/expt/libab_<name>.so <name> [batches per launch].
+set -e
+cd "$(dirname "$0")/.."
+C=mini-kube-scheduler_amd/csrc
+E=scripts/expt
+mkdir -p $E
+O=$(mktemp -d)
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c $C/msh_capi.cpp -o $O/c.o &
+g++ -O2 -std=c++17 -fPIC -pthread -c $C/msh_pack.cpp -o $O/p.o &
+for a in "$@"; do
+  name=${a%%=*}
+  flags=${a#*=}
+  src_var=SRC_$name
+  src=${!src_var:-$C/msh_kernels.hip}
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$C $flags -x hip -c "$src" -o $O/k_$name.o &
+done
+wait
+for a in "$@"; do
+  name=${a%%=*}
+  hipcc --offload-arch=gfx950 -shared -fPIC $O/k_$name.o $O/c.o $O/p.o -o $E/libab_$name.so
+done
+hipcc -O2 -std=c++17 -Iinclude scripts/wg_expt_run.cpp -ldl -o $E/run
+rm -rf "$O"
+ls -la $E

@@ -1,6 +1,6 @@
 """Minimal driver for profiling: K launches of a hot kernel on the C3 workload.
 
-MODE=multi (bench.py's default submission: 8 independent 100k-pod batches per
+MODE=multi (bench.py's default submission: 32 independent 100k-pod batches per
 msh_schedule_batches_device launch), batch (one msh_schedule_batch_device launch per batch),
 sequential (C5), generic (the explicit int64 score pipeline, NodeNumber + one score column).
 NORM: msh_normalize of the NodeNumber entry (3 = MINMAX)."""

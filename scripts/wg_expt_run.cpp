@@ -1,7 +1,10 @@
 // wg_expt_run.cpp — phase experiments on wg_kernel (C3: 5,000 nodes, 100k-pod batches), for one
 // build of the library given on the command line (scripts/wg_expt.sh builds the variants: the
 // product source with -DMSH_STAMPS and an MSH_WG_EXPT mask; never the product library).
-//   wg_expt_run <lib.so> <tag> [batches per launch = 8]
+//   wg_expt_run <lib.so> <tag> [batches per launch = 8] [clock]
+// "clock" (a -DMSH_CLOCK_STAMPS build): about 2 s of back-to-back launches first, then one launch whose
+// persistent waves stamp the shader clock (s_memtime) and the 100 MHz clock (s_memrealtime) at start
+// and end; prints the median in-kernel clock over the waves (MI355X_MICROARCH.md, DVFS item 6).
 // Prints one JSON line: the kernel duration per launch (msh_timing_*: the kernel's own start / stop)
 // and, from the stamps of one launch, the per-wave phase durations (entry -> after the table copy and
 // barrier -> after the scan -> after the stores; percentiles in microseconds) and the wave start spread.
@@ -12,6 +15,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <string>
 #include <vector>
 
 #include "minisched_hip.h"
@@ -104,7 +109,82 @@ int main(int argc, char** argv) {
   CHECK(tend(ctx, &n, &tot, &mx));
   printf("{\"tag\": \"%s\", \"batches_per_launch\": %d, \"kernel_us\": %.3f, \"us_per_batch\": %.3f", argv[2], NB,
          tot * 1e3 / n, tot * 1e3 / n / NB);
-  if (stamps_set) {
+  const bool clock_mode = argc > 4 && std::string(argv[4]) == "clock";
+  if (stamps_set && clock_mode) {
+    const size_t slots = (size_t)4096 * 16 * 8;
+    unsigned long long* d_st;
+    CHECK(hipMalloc(&d_st, slots * 8));
+    CHECK(hipMemset(d_st, 0, slots * 8));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    CHECK(hipEventRecord(e0, st));
+    int warm = 0;
+    for (float ms = 0; ms < 2000.f; ++warm) {
+      for (int i = 0; i < 50; ++i) CHECK(batches(ctx, NB, desc.data(), st));
+      warm += 49;
+      CHECK(hipEventRecord(e1, st));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+    }
+    CHECK(stamps_set(d_st));
+    CHECK(tbegin(ctx, 1));
+    CHECK(batches(ctx, NB, desc.data(), st));
+    CHECK(tend(ctx, &n, &tot, &mx));
+    std::vector<unsigned long long> hs(slots);
+    CHECK(hipMemcpy(hs.data(), d_st, slots * 8, hipMemcpyDeviceToHost));
+    std::vector<double> ghz, life, beg, fin;
+    unsigned long long r_min = ~0ull;
+    for (size_t w = 0; w < slots / 8; ++w)
+      if (hs[w * 8 + 1]) r_min = std::min(r_min, hs[w * 8 + 1]);
+    // waves per CU (xcc, se, sh, cu from HW_ID / XCC_ID) and the per-CU mean end time
+    std::map<unsigned, std::pair<int, double>> cu;
+    std::map<int, int> items;
+    FILE* dump = getenv("CLOCK_DUMP") ? fopen(getenv("CLOCK_DUMP"), "w") : nullptr;
+    for (size_t w = 0; w < slots / 8; ++w) {
+      const unsigned long long* t = &hs[w * 8];
+      if (!t[1] || t[3] <= t[1]) continue;
+      const unsigned hw = (unsigned)t[4], xcc = (unsigned)t[5] & 0xf;
+      const unsigned key = (xcc << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xf);
+      cu[key].first++;
+      cu[key].second += (t[3] - r_min) * 0.01;
+      items[(int)t[6]]++;
+      if (dump) fprintf(dump, "%u %u %u %.2f %.2f %d\n", xcc, (hw >> 13) & 7, ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xf),
+                        (t[1] - r_min) * 0.01, (t[3] - r_min) * 0.01, (int)t[6]);
+    }
+    if (dump) fclose(dump);
+    std::map<int, std::pair<int, double>> by_waves;  // waves on the CU -> (CUs, mean end)
+    for (auto& kv : cu) {
+      by_waves[kv.second.first].first++;
+      by_waves[kv.second.first].second += kv.second.second / kv.second.first;
+    }
+    printf(", \"cus\": %zu, \"waves_per_cu\": {", cu.size());
+    bool first = true;
+    for (auto& kv : by_waves) {
+      printf("%s\"%d\": [%d, %.2f]", first ? "" : ", ", kv.first, kv.second.first, kv.second.second / kv.second.first);
+      first = false;
+    }
+    printf("}, \"items_per_wave\": {");
+    first = true;
+    for (auto& kv : items) {
+      printf("%s\"%d\": %d", first ? "" : ", ", kv.first, kv.second);
+      first = false;
+    }
+    printf("}");
+    for (size_t w = 0; w < slots / 8; ++w) {
+      const unsigned long long* t = &hs[w * 8];
+      if (!t[1] || t[3] <= t[1]) continue;
+      ghz.push_back((double)(t[2] - t[0]) / (double)(t[3] - t[1]) * 0.1);
+      life.push_back((t[3] - t[1]) * 0.01);
+      beg.push_back((t[1] - r_min) * 0.01);
+      fin.push_back((t[3] - r_min) * 0.01);
+    }
+    printf(", \"clock\": {\"warm_launches\": %d, \"stamped_kernel_us\": %.3f, \"waves\": %zu, \"ghz\": [%.3f, %.3f, %.3f], "
+           "\"wave_life_us\": [%.2f, %.2f, %.2f], \"start_us\": [%.2f, %.2f, %.2f, %.2f], \"end_us\": [%.2f, %.2f, %.2f, %.2f, %.2f]}",
+           warm, tot * 1e3, ghz.size(), pct(ghz, 0.1), pct(ghz, 0.5), pct(ghz, 0.9), pct(life, 0.1), pct(life, 0.5),
+           pct(life, 0.9), pct(beg, 0.1), pct(beg, 0.5), pct(beg, 0.9), pct(beg, 1.0), pct(fin, 0.0), pct(fin, 0.1),
+           pct(fin, 0.5), pct(fin, 0.9), pct(fin, 1.0));
+  } else if (stamps_set) {
     const int blocks = (P + 255) / 256;
     const size_t slots = (size_t)blocks * NB * 4 * 4;
     unsigned long long* d_st;
