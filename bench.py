@@ -48,12 +48,12 @@ CLOCK_HZ = 2.4e9                   # MI355X_MICROARCH.md: max clock
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # The persistent class-row kernel (wgp_kernel, tables up to 8,192 nodes; the identity-like modes):
 # per 256-node group and 64-pod wave, two ds_read_b128 of the lanes' class-row entries = 2 KiB
-# through the LDS array (1/8 B per pod-node pair), and 7.5 VALU (three v_bitop3 OR3 + a v_or over
-# the 8 words, the group flag v_min + v_lshl_or and its share of the pair's, the address).
+# through the LDS array (1/8 B per pod-node pair), and 5.5 VALU (four groups per step: 16 v_bitop3
+# OR3 over the 32 words, two pair flags of v_min + v_lshl_or, two address adds).
 LDS_PEAK = 150e12                  # MI355X_MICROARCH.md: ~150 TB/s aggregate for ds_read_b64/b128
 WGP_MAX_GROUPS = 32                # msh_kernels.hip: the persistent kernel's table limit (groups of 256 nodes)
 LDS_BYTES_PER_GROUP_WAVE = 2 * 1024
-VALU_PER_GROUP_WAVE = 7.5
+VALU_PER_GROUP_WAVE = 5.5
 PMC_FILE = ROOT / "profiles" / "r3_pmc_c3.json"
 VALU_PEAK_FILE = ROOT / "profiles" / "r3_ubench_valu_peak.json"
 
@@ -427,7 +427,7 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
     lds_cycles = entry.get("SQ_LDS_IDX_ACTIVE") if pmc_ok else None
     model_instr = group_waves * VALU_PER_GROUP_WAVE  # wave-instructions of the scan
     valu_instr = entry.get("SQ_INSTS_VALU") if pmc_ok else None
-    uniq_bytes = (3.0 * n_local + 18.0 * p * batches_per_launch)  # class rows once, pod records + outputs
+    uniq_bytes = (3.375 * n_local + 18.0 * p * batches_per_launch)  # class rows once, pod records + outputs
     survey_bytes = 2.0 * n_local * p * batches_per_launch + 18.0 * p * batches_per_launch
     out = {
         "bound": "lds",
@@ -465,7 +465,7 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
                 "survey_8d_bytes_per_launch": survey_bytes,
                 "survey_8d_frac": survey_bytes / launch_s / HBM_PEAK,
                 "survey_8d_note": "2 B per pair counts every L1/L2/LDS re-read of the node table as HBM "
-                                  "traffic; the 15 KB class-row table is read from HBM once per launch"},
+                                  "traffic; the 17 KB class-row table is read from HBM (L2) once per workgroup"},
     }
     return out
 

@@ -60,10 +60,11 @@ for mode, prefix, tags, nb in (
         e["hbm_bytes_per_launch_fetch_x2"] = 2 * e["fetch_bytes_raw"] + e["write_bytes"]
     if "SQ_INSTS_VALU" in e:
         e["valu_lane_ops_per_eval"] = e["SQ_INSTS_VALU"] * 64 / (N * P * nb)
-        # the scan's modelled VALU per 256-node group and 64-pod wave (wgp_kernel: the OR of the 8
-        # class-row words, 4, the group flag, 2 + 1 shared by two groups, the address 0.5 = 7.5; with
-        # the non-matches too, MIN-MAX, 8 v_bitop3 and a second flag more = 17.5)
-        per_group = {"batch_multi": 7.5, "batch": 7.5, "batch_minmax": 17.5}.get(mode)
+        # the scan's modelled VALU per 256-node group and 64-pod wave (wgp_kernel, four groups per
+        # step: 16 v_bitop3 OR3 over the 32 class-row words, two pair flags (2 v_min + 2 v_lshl_or)
+        # and two address adds = 22 per four groups, 5.5; MIN-MAX adds 32 v_bitop3 for the
+        # non-matches and their two flags, 58 per four groups, 14.5)
+        per_group = {"batch_multi": 5.5, "batch": 5.5, "batch_minmax": 14.5}.get(mode)
         if per_group:
             e["scan_model_share"] = per_group * GROUPS * (P / 64) * nb / e["SQ_INSTS_VALU"]
     if "SQ_WAVE_CYCLES" in e:
