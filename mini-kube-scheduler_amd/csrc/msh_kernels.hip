@@ -1084,6 +1084,9 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
 // with a hit is the lowest set bit of the bitmap (groups walked in descending List order); its
 // exact first node is resolved from the same two entries (v_ffbl), as in wg_kernel.
 // ---------------------------------------------------------------------------------------
+#ifndef MSH_WGP_W
+#define MSH_WGP_W 4  // waves per workgroup of the persistent kernel (A/B builds: 8, 16)
+#endif
 constexpr int WGP_MAX_GROUPS = 32;  // <= 8,192 nodes: 27 KB of LDS (6 workgroups per CU; C3: 17 KB, 8)
 
 __device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
@@ -2135,7 +2138,7 @@ hipError_t launch_wg_w(const BatchArgs& a, hipStream_t s) {
 // more than the launch's blocks.
 template <bool KX>
 hipError_t launch_persistent(MultiArgs& m, const DeviceInfo& dev, hipStream_t s) {
-  constexpr int W = 4;
+  constexpr int W = MSH_WGP_W;
   int32_t maxp = 0;
   for (int b = 0; b < m.nb; ++b) maxp = std::max(maxp, m.d[b].n_pods);
   if (maxp == 0) return hipSuccess;

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -110,6 +111,22 @@ int main(int argc, char** argv) {
   printf("{\"tag\": \"%s\", \"batches_per_launch\": %d, \"kernel_us\": %.3f, \"us_per_batch\": %.3f", argv[2], NB,
          tot * 1e3 / n, tot * 1e3 / n / NB);
   const bool clock_mode = argc > 4 && std::string(argv[4]) == "clock";
+  if (argc > 4 && std::string(argv[4]) == "region") {
+    // the bench's K = NB region from C: device synchronize, clock, one launch of NB batches, device
+    // synchronize, clock; 200 repetitions after 1 ms idle each; median and p10 / p90 in microseconds
+    std::vector<double> us;
+    for (int rep = 0; rep < 200; ++rep) {
+      CHECK(hipDeviceSynchronize());
+      const auto idle = std::chrono::steady_clock::now() + std::chrono::microseconds(1000);
+      while (std::chrono::steady_clock::now() < idle) {
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      CHECK(batches(ctx, NB, desc.data(), st));
+      CHECK(hipDeviceSynchronize());
+      us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    printf(", \"region_us\": [%.2f, %.2f, %.2f]", pct(us, 0.1), pct(us, 0.5), pct(us, 0.9));
+  }
   if (stamps_set && clock_mode) {
     const size_t slots = (size_t)4096 * 16 * 8;
     unsigned long long* d_st;
