@@ -179,11 +179,18 @@ struct BatchDesc {
   int32_t n_pods;
   int32_t reserved;
 };
+constexpr int RANK_MAX = 8;     // persistent kernel: workgroups per CU (age slots)
 constexpr int MULTI_MAX = 32;  // batches per launch (kernel-argument descriptors, 48 B each: ~1.7 KB)
 struct MultiArgs {
   BatchArgs a;  // the node table, plugin set and launch geometry (its pod / output fields unused)
   int32_t nb;
   int32_t bpb;  // pod blocks per batch (the largest batch's), set by the launcher
+  // persistent kernel: walk 0 = strided items (g, g + G, ...); walk 1 = workgroup g (age slot
+  // r = g / rank_wgs on its CU) owns a share of the item range [rank_lo[r], rank_lo[r + 1]), split
+  // evenly over the rank_wgs workgroups of the slot
+  int32_t walk;
+  int32_t rank_wgs;
+  int32_t rank_lo[RANK_MAX + 1];
   BatchDesc d[MULTI_MAX];
 };
 

@@ -1087,6 +1087,13 @@ __global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T k
 #ifndef MSH_WGP_W
 #define MSH_WGP_W 4  // waves per workgroup of the persistent kernel (A/B builds: 8, 16)
 #endif
+#ifndef MSH_WGP_AGE_SLOPE
+#define MSH_WGP_AGE_SLOPE 100  // per-slot fall of the item share, x 1e-3 (A/B builds)
+#endif
+#ifndef MSH_WGP_SHARE_MIN
+#define MSH_WGP_SHARE_MIN 5  // items per workgroup from which the age-slot shares are used (A/B builds)
+#endif
+constexpr int WGP_SHARE_MIN = MSH_WGP_SHARE_MIN;
 constexpr int WGP_MAX_GROUPS = 32;  // <= 8,192 nodes: 27 KB of LDS (6 workgroups per CU; C3: 17 KB, 8)
 
 __device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
@@ -1137,9 +1144,27 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
   // progress at one rate (the issue arbiter favours older waves: a CU's first workgroup ends its 6
   // items in ~13 us, its last in ~23 us), but the CU's LDS stays busy while most of them run, and
   // either remedy cost more than the tail it shortened.
-  const int32_t bpb = __builtin_amdgcn_readfirstlane(ka.bpb), total = __builtin_amdgcn_readfirstlane(ka.nb * bpb);
-  const int32_t G = (int32_t)gridDim.x;
-  int32_t it = (int32_t)blockIdx.x;
+  // Two walks (MultiArgs::walk): with few items per workgroup, items it = g, g + G, g + 2G, ... (the
+  // leftover items fall to the low-numbered, oldest workgroups); with many, workgroup g walks the
+  // contiguous range the launcher sized for its age slot on the CU (rank_lo). The issue arbiter
+  // favours older waves: with equal shares a CU's first workgroup finished in ~60% of the time of
+  // its last, and the CU ran its last microseconds on a few workgroups (profiles/ab/r3_wgp_clock.jsonl).
+  const int32_t bpb = __builtin_amdgcn_readfirstlane(ka.bpb);
+  int32_t it, total, step;
+  if (ka.walk == 0) {
+    it = (int32_t)blockIdx.x;
+    total = ka.nb * bpb;
+    step = (int32_t)gridDim.x;
+  } else {
+    const int32_t rk = (int32_t)blockIdx.x / ka.rank_wgs, rc = (int32_t)blockIdx.x - rk * ka.rank_wgs;
+    const int32_t pool_lo = ka.rank_lo[rk], pool = ka.rank_lo[rk + 1] - pool_lo;
+    it = pool_lo + (int32_t)((int64_t)pool * rc / ka.rank_wgs);
+    total = pool_lo + (int32_t)((int64_t)pool * (rc + 1) / ka.rank_wgs);
+    step = 1;
+  }
+  it = __builtin_amdgcn_readfirstlane(it);
+  total = __builtin_amdgcn_readfirstlane(total);
+  step = __builtin_amdgcn_readfirstlane(step);
   int32_t b = it / bpb, x = it - b * bpb;
   int dq = 0;
   uint32_t tq = 0;
@@ -1176,8 +1201,8 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
     return m;
   };
   auto advance = [&]() {  // to the next item of this workgroup, its pod bytes in flight
-    it += G;
-    x += G;
+    it += step;
+    x += step;
     while (x >= bpb) {
       x -= bpb;
       ++b;
@@ -1311,6 +1336,7 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
     o[4] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID: cu / sh / se / simd / wave
     o[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
     o[6] = (unsigned long long)n_items;
+    o[7] = blockIdx.x;
   }
 #endif
 }
@@ -2145,7 +2171,30 @@ hipError_t launch_persistent(MultiArgs& m, const DeviceInfo& dev, hipStream_t s)
   m.bpb = (maxp + W * WAVE - 1) / (W * WAVE);
   const size_t lds = (size_t)m.a.n_groups * HR_GQ * sizeof(uint4);
   const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / W, (int64_t)(160 * 1024 / std::max<size_t>(lds, 1))));
-  const int64_t grid = std::min<int64_t>((int64_t)m.bpb * m.nb, (int64_t)dev.cus * per_cu);
+  const int64_t items = (int64_t)m.bpb * m.nb;
+  const int64_t grid = std::min<int64_t>(items, (int64_t)dev.cus * per_cu);
+  // Item shares by age slot (blockIdx / CUs: the dispatcher fills every CU's slot r before slot r + 1)
+  // when the grid fills every slot and each workgroup has at least WGP_SHARE_MIN items: slot r's
+  // share falls by MSH_WGP_AGE_SLOPE / 1000 per slot relative to slot 0 (the rates of the slots
+  // measured under equal shares); otherwise the strided walk (C3, 32 batches per launch: 0.815 ->
+  // 0.777 us per batch; at 8 and 20 batches the strided walk was as fast or faster).
+  m.walk = 0;
+  if (grid == (int64_t)dev.cus * per_cu && per_cu > 1 && items >= WGP_SHARE_MIN * grid) {
+    m.walk = 1;
+    m.rank_wgs = dev.cus;
+    double wsum = 0, w[RANK_MAX];
+    for (int r = 0; r < per_cu; ++r) wsum += (w[r] = 1.0 - MSH_WGP_AGE_SLOPE * 1e-3 * r);
+    double acc = 0;
+    for (int r = 0; r <= per_cu; ++r) {
+      m.rank_lo[r] = (int32_t)std::llround(items * acc / wsum);
+      if (r < per_cu) acc += w[r];
+    }
+    m.rank_lo[per_cu] = (int32_t)items;
+  } else {
+    m.rank_wgs = (int32_t)grid;
+    m.rank_lo[0] = 0;
+    m.rank_lo[1] = (int32_t)items;
+  }
   MSH_TIMED_LAUNCH((wgp_kernel<W, KX>), dim3((unsigned)grid), dim3(W * WAVE), (unsigned)lds, s, m);
   return hipGetLastError();
 }

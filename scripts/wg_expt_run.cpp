@@ -166,8 +166,8 @@ int main(int argc, char** argv) {
       cu[key].first++;
       cu[key].second += (t[3] - r_min) * 0.01;
       items[(int)t[6]]++;
-      if (dump) fprintf(dump, "%u %u %u %.2f %.2f %d\n", xcc, (hw >> 13) & 7, ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xf),
-                        (t[1] - r_min) * 0.01, (t[3] - r_min) * 0.01, (int)t[6]);
+      if (dump) fprintf(dump, "%u %u %u %.2f %.2f %d %d\n", xcc, (hw >> 13) & 7, ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xf),
+                        (t[1] - r_min) * 0.01, (t[3] - r_min) * 0.01, (int)t[6], (int)t[7]);
     }
     if (dump) fclose(dump);
     std::map<int, std::pair<int, double>> by_waves;  // waves on the CU -> (CUs, mean end)

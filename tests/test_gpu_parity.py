@@ -768,6 +768,34 @@ def test_multi_batch_launch(msh, gpu_ctx, oracle, norm, nb):
         assert (t[2].cpu().numpy() == oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)[0]).all(), k
 
 
+@pytest.mark.parametrize("n,norm", [(5000, 0), (5000, 3), (8192, 0), (6000, 2)])
+def test_multi_batch_age_shares(msh, gpu_ctx, oracle, n, norm):
+    """A full multi-batch launch (32 batches of ~100k pods, ragged) takes the persistent kernel's
+    age-slot walk (at least WGP_SHARE_MIN items per workgroup: contiguous item ranges sized per
+    workgroup slot on its CU; 8 slots at 5k nodes, 5 at 8,192 nodes); every batch bit-exact vs the
+    oracle."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(4242 + n + norm)
+    sizes = [100_000, 99_937, 100_003, 64, 0, 1, 99_999, 98_304] + [100_000 - 7 * k for k in range(24)]
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
+    _set(gpu_ctx, msh, ps)
+    u, nd, _, _ = _rand_case(rng, n, 1)
+    gpu_ctx.upload_nodes(u, nd)
+    cases = []
+    for k, p in enumerate(sizes):
+        _, _, pd, pt = _rand_case(rng, 1, p)
+        cases.append((pd, pt, _dev_batch(torch, dev, pd, pt, scores=(k % 5 != 4))))
+    descs = gpu_ctx.batch_descs([_desc(c[2]) for c in cases])
+    gpu_ctx.schedule_batches_device(descs, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for k, (pd, pt, t) in enumerate(cases):
+        want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=16)
+        gi, gst = t[2].cpu().numpy(), t[4].cpu().numpy()
+        gs = t[3].cpu().numpy() if t[3] is not None else want[1]
+        _assert_same((gi, gs, gst), want, f"batch {k} (p={len(pd)}) n={n} norm={norm}")
+
+
 def test_multi_batch_invalid(msh, gpu_ctx):
     """Bad descriptors are rejected before any launch (MSH_ERR_INVALID), and nb = 0 is a no-op."""
     N = msh._native
