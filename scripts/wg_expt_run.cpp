@@ -82,6 +82,14 @@ int main(int argc, char** argv) {
   }
   msh_ctx* ctx = nullptr;
   CHECK(create(0, &ctx));
+  if (const char* nm = getenv("MSH_RUN_NORM")) {  // NodeNumber's normalize mode (3 = MIN-MAX: the KX kernel)
+    auto setp = sym<int (*)(msh_ctx*, const int32_t*, int32_t, const int32_t*, int32_t, const int32_t*, const int64_t*,
+                            const int32_t*, int32_t)>(h, "msh_set_plugins_ex");
+    const int32_t f[1] = {MSH_PLUGIN_NODE_UNSCHEDULABLE}, pre[1] = {MSH_PLUGIN_NODE_NUMBER},
+                  sc[1] = {MSH_PLUGIN_NODE_NUMBER}, norm[1] = {atoi(nm)};
+    const int64_t w[1] = {1};
+    CHECK(setp(ctx, f, 1, pre, 1, sc, w, norm, 1));
+  }
   CHECK(upload(ctx, N, u.data(), d.data()));
   std::vector<msh_batch> desc(NB);
   for (int b = 0; b < NB; ++b) {
