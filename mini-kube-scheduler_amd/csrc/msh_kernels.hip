@@ -2170,19 +2170,7 @@ hipError_t launch_persistent(MultiArgs& m, const DeviceInfo& dev, hipStream_t s)
   if (maxp == 0) return hipSuccess;
   m.bpb = (maxp + W * WAVE - 1) / (W * WAVE);
   const size_t lds = (size_t)m.a.n_groups * HR_GQ * sizeof(uint4);
-  // workgroups per CU that stay resident together (waves, VGPRs and this table's LDS): the runtime's
-  // occupancy query, per table size (the KX form's 78 VGPRs allow 6 waves per SIMD, not 8); a grid
-  // larger than that would leave workgroups waiting for a slot behind others' items
-  static thread_local size_t occ_lds[2] = {0, 0};
-  static thread_local int occ_n[2] = {0, 0};
-  if (occ_lds[KX] != lds || occ_n[KX] <= 0) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wgp_kernel<W, KX>, W * WAVE, lds) != hipSuccess || n <= 0)
-      n = std::max(1, std::min(32 / W, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
-    occ_lds[KX] = lds;
-    occ_n[KX] = n;
-  }
-  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>({(int64_t)occ_n[KX], 32 / W, (int64_t)RANK_MAX}));
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / W, (int64_t)(160 * 1024 / std::max<size_t>(lds, 1))));
   const int64_t items = (int64_t)m.bpb * m.nb;
   const int64_t grid = std::min<int64_t>(items, (int64_t)dev.cus * per_cu);
   // Item shares by age slot (blockIdx / CUs: the dispatcher fills every CU's slot r before slot r + 1)
