@@ -59,15 +59,19 @@ VALU_PEAK_FILE = ROOT / "profiles" / "r3_ubench_valu_peak.json"
 
 
 def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False,
-                       multi: bool = False) -> str:
-    """The kernel msh_kernels.hip launch_batch / launch_batches dispatches (4-wave workgroups): the
-    persistent class-row kernel while the table has at most WGP_MAX_GROUPS groups (shard keys aside),
-    else the chunk-streaming wg_kernel."""
+                       multi: bool = False, nb: int = 1, classrows: bool = False) -> str:
+    """The kernel msh_capi.cpp dispatches for a launch of nb batches of n_pods: pair_kernel<S, SHARD>,
+    S the slice waves per 64-pod block (msh_kernels.hip pair_slices), or the opt-in class-row
+    kernel wgp_kernel<4, KX> (tables up to WGP_MAX_GROUPS groups)."""
     b = lambda v: str(v).lower()
     groups = max(-(-n_nodes // 1024) * 1024, 1024) // 256
-    if groups <= WGP_MAX_GROUPS and not shard:
+    if classrows and groups <= WGP_MAX_GROUPS and not shard:
         return f"void msh::wgp_kernel<4, {b(kx)}>"
-    return f"void msh::wg_kernel<4, {b(kx)}, {b(shard)}, {b(multi)}>"
+    waves = -(-n_pods // 64) * (nb if multi else 1)
+    sl = 1
+    while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
+        sl *= 2
+    return f"void msh::pair_kernel<{sl}, {b(shard)}>"
 
 
 def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
@@ -414,7 +418,7 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
                 "note": "a serial mode: the floor is the kernel's own instruction count per pod (rocprofv3 "
                         "SQ_INSTS_VALU + SQ_INSTS_SALU / pods) x 4 cycles / 2.4 GHz, not a hardware roofline"}
     multi = batches_per_launch > 1
-    kname = batch_kernel_label(n_local, p, cus, shard=mode == "nodeshard", multi=multi)
+    kname = batch_kernel_label(n_local, p, cus, shard=mode == "nodeshard", multi=multi, nb=batches_per_launch)
     evals = float(n_local) * p * batches_per_launch
     entry = pmc.get("kernels", {}).get("batch_multi" if multi else "batch", {})
     pmc_ok = (entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p

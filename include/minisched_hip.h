@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSH_ABI_VERSION 6
+#define MSH_ABI_VERSION 7
 
 /* ---- error codes (return values) ---- */
 typedef enum msh_err {
@@ -70,8 +70,9 @@ typedef enum msh_plugin_id {
   /* Score-column plugins (ABI v5, build extension): a score plugin whose Score(pod, node) is an
    * int64 the host computed per node (msh_upload_score_column), e.g. a node-only scorer evaluated
    * once per snapshot. Score lists with one of these run on the generic pipeline (an explicit
-   * int64 score per pair, per-plugin NormalizeScore over the feasible list, weights, first max);
-   * the batch entry points only (shard keys, sequential mode and the export: MSH_ERR_UNSUPPORTED). */
+   * int64 score per pair, per-plugin NormalizeScore over the feasible list, weights, first max):
+   * the batch entry points and the node-sharded msh_generic_* entry points (shard keys, sequential
+   * mode and the export: MSH_ERR_UNSUPPORTED). */
   MSH_PLUGIN_SCORE_COLUMN0 = 16,
   MSH_PLUGIN_SCORE_COLUMN1 = 17,
   MSH_PLUGIN_SCORE_COLUMN2 = 18,
@@ -250,17 +251,14 @@ int msh_reset_node_pod_counts(msh_ctx* ctx);
 /* ---- node-sharded mode (a cluster's node table split over devices) ----
  * Each shard holds a contiguous slice [node_base, node_base + n) of the global List order and
  * produces int32 keys, key = 0x7FFFFFFF - global_idx (0 = none), so that the element-wise MAX
- * over shards (one RCCL allreduce MAX) is the global first node. Layout, msh_shard_keys_len
- * entries = p + s1:
- *   keys[j], j < p  first feasible node whose NodeNumber class is "match" for pod j
- *   keys[p + ...]   s1 = 2 when keys[1] is "first feasible of any class" (the identity-like
- *                   normalize modes: msh_keys_slot1_is_any = 1): that key depends on the pod
- *                   only through its class, keys[p] = non-tolerating pods, keys[p + 1] =
- *                   tolerating pods; s1 = p otherwise (REVERSE / MINMAX): keys[p + j] = first
- *                   feasible "non-match" node of pod j.
- * 4 B per pod cross the interconnect for the reference plugin set (selectHost over the merged
- * keys replaces minisched.go:304-325 across shards). msh_decode_keys_device then produces
- * idx/score/status exactly as msh_schedule_batch over the whole table. */
+ * over shards (one RCCL allreduce MAX) is the global first node. Layout (ABI v7), msh_shard_keys_len
+ * = 2p entries, every entry a property of pod j alone (evaluated per (pod, node) pair of the shard):
+ *   keys[j]      first feasible node whose NodeNumber score is 10 for pod j (feasible match)
+ *   keys[p + j]  first feasible node whose NodeNumber score is 0 for pod j (feasible non-match)
+ * 8 B per pod cross the interconnect (selectHost over the merged keys replaces minisched.go:304-325
+ * across shards; the first feasible node is the larger of the two keys). msh_decode_keys_device then
+ * produces idx/score/status exactly as msh_schedule_batch over the whole table. Score-column plugin
+ * lists use msh_generic_extents_device / msh_generic_best_device / msh_generic_decode_device below. */
 int msh_shard_keys_len(const msh_ctx* ctx, int32_t p, int32_t* out_len);
 int msh_shard_keys_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
                           const uint8_t* d_pod_tol, int64_t node_base, int32_t* d_keys,
@@ -269,9 +267,36 @@ int msh_decode_keys_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
                            const uint8_t* d_pod_tol, const int32_t* d_keys,
                            int32_t* d_out_idx, int64_t* d_out_score, int32_t* d_out_status,
                            void* stream);
-/* Whether keys[1] holds "first feasible of any class" (1, per class) or "first feasible
- * non-match" (0, per pod) under the ctx's current plugin set. */
+/* Kept for ABI compatibility: always 0 since ABI v7 (keys[p + j] is per pod, never per pod class). */
 int msh_keys_slot1_is_any(const msh_ctx* ctx, int32_t* out_flag);
+
+/* ---- node-sharded generic pipeline (ABI v7): any plugin list, score-column lists included ----
+ * Each shard (a contiguous List-order slice, as above) computes per pod its best (int64 total, global
+ * node index) over its nodes; the merge is two all-reduces, MAX over the totals, then MIN over the
+ * indices of the shards that hold the maximum (the global first maximum: selectHost,
+ * minisched.go:304-325, across shards). A plugin that normalizes needs the pod's extent (max, min of
+ * its raw scores) over the feasible nodes of EVERY shard before any total is formed:
+ *   1. len = msh_generic_ext_len(ctx, p); when len > 0: msh_generic_extents_device on every shard into
+ *      len int64 (the minima stored negated), then one all-reduce MAX of them;
+ *   2. msh_generic_best_device(..., d_ext (the merged extents, or NULL when len == 0), node_base,
+ *      d_total, d_idx): this shard's best per pod (INT64_MIN / INT32_MAX: no feasible node here);
+ *   3. d_merged = copy of d_total, all-reduce MAX over d_merged;
+ *   4. msh_generic_candidates_device(p, d_total, d_merged, d_idx): d_idx[j] = INT32_MAX unless this
+ *      shard holds pod j's maximum; then all-reduce MIN over d_idx;
+ *   5. msh_generic_decode_device(..., d_merged, d_idx, outputs): idx / score / status exactly as
+ *      msh_schedule_batch over the whole table (FitError when no shard has a feasible node).
+ * Device pointers, asynchronous on `stream` (hipStream_t as void*, NULL = the null stream). */
+int msh_generic_ext_len(const msh_ctx* ctx, int32_t p, int64_t* out_len);
+int msh_generic_extents_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit, const uint8_t* d_pod_tol,
+                               int64_t* d_ext, void* stream);
+int msh_generic_best_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit, const uint8_t* d_pod_tol,
+                            const int64_t* d_ext, int64_t node_base, int64_t* d_best_total, int32_t* d_best_idx,
+                            void* stream);
+int msh_generic_candidates_device(msh_ctx* ctx, int32_t p, const int64_t* d_local_total, const int64_t* d_merged_total,
+                                  int32_t* d_best_idx, void* stream);
+int msh_generic_decode_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit, const int64_t* d_merged_total,
+                              const int32_t* d_merged_idx, int32_t* d_out_idx, int64_t* d_out_score,
+                              int32_t* d_out_status, void* stream);
 
 /* ---- kernel timing (measurement hook) ----
  * msh_timing_begin arms up to max_launches (1..4096) event pairs: each following hot-kernel launch of

@@ -56,6 +56,8 @@ EXPORTED = (
     "msh_schedule_batches_device", "msh_schedule_sequential",
     "msh_schedule_sequential_device", "msh_node_pod_counts", "msh_reset_node_pod_counts",
     "msh_shard_keys_len", "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
+    "msh_generic_ext_len", "msh_generic_extents_device", "msh_generic_best_device",
+    "msh_generic_candidates_device", "msh_generic_decode_device",
     "msh_timing_begin", "msh_timing_end",
     "msh_pack_nodes", "msh_pack_pods", "msh_toleration_tolerates_unschedulable",
 )
@@ -117,6 +119,11 @@ _SIGS = {
     "msh_shard_keys_device": (C.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
     "msh_decode_keys_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "msh_keys_slot1_is_any": (C.c_int, [_P, C.POINTER(_I32)]),
+    "msh_generic_ext_len": (C.c_int, [_P, _I32, C.POINTER(_I64)]),
+    "msh_generic_extents_device": (C.c_int, [_P, _I32, _P, _P, _P, _P]),
+    "msh_generic_best_device": (C.c_int, [_P, _I32, _P, _P, _P, _I64, _P, _P, _P]),
+    "msh_generic_candidates_device": (C.c_int, [_P, _I32, _P, _P, _P, _P]),
+    "msh_generic_decode_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "msh_pack_nodes": (C.c_int, [_I32, C.c_char_p, _P, _P, _P, _P, _P]),
     "msh_pack_pods": (C.c_int, [_I32, C.c_char_p, _P, C.POINTER(Toleration), _P, _P, _P]),
     "msh_toleration_tolerates_unschedulable": (C.c_int, [C.POINTER(Toleration)]),

@@ -77,12 +77,14 @@ struct NodeTable {
   size_t cap = 0;
   uint8_t* d_unsched = nullptr;  // the uploaded columns
   int8_t* d_digit = nullptr;
-  uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout)
-  uint32_t* d_erows = nullptr;   // digit rows (msh_internal.h ER_* layout)
-  uint32_t* d_hrows = nullptr;   // class rows (msh_internal.h HR_* layout)
+  uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout): pair_kernel, seq_kernel
+  uint32_t* d_hrows = nullptr;   // class rows (msh_internal.h HR_* layout): the opt-in class-row kernel
   uint32_t* d_ball = nullptr;    // [0..1] first feasible node per pod class, as keys
-  // score-column plugins (generic pipeline): GEN_COLS x cap int64, column k valid when col_ok[k]
+  uint32_t* d_nrec = nullptr;    // node records (msh_internal.h NREC): generic_kernel
+  // score-column plugins (generic pipeline): GEN_COLS x cap int64, column k valid when col_ok[k], and
+  // the same x 100 as doubles (the normalizing columns' numerators)
   int64_t* d_cols = nullptr;
+  double* d_cols100 = nullptr;
   bool col_ok[msh::GEN_COLS] = {};
   // launches that read this version: one event per caller stream, re-recorded after each launch
   std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
@@ -167,17 +169,19 @@ NodeTable& cur_table(msh_ctx* c) { return c->tab[c->cur]; }
 
 void free_table(NodeTable& t) {
   (void)hipFree(t.d_cols);
+  (void)hipFree(t.d_cols100);
+  (void)hipFree(t.d_nrec);
   (void)hipFree(t.d_unsched);
   (void)hipFree(t.d_digit);
   (void)hipFree(t.d_planes);
-  (void)hipFree(t.d_erows);
   (void)hipFree(t.d_hrows);
   (void)hipFree(t.d_ball);
   t.d_cols = nullptr;
+  t.d_cols100 = nullptr;
+  t.d_nrec = nullptr;
   t.d_unsched = nullptr;
   t.d_digit = nullptr;
   t.d_planes = nullptr;
-  t.d_erows = nullptr;
   t.d_hrows = nullptr;
   t.d_ball = nullptr;
   for (bool& ok : t.col_ok) ok = false;
@@ -358,16 +362,22 @@ int ensure_table(msh_ctx* c, NodeTable& t, size_t n_pad) {
   MSH_HIP(c, hipMalloc(&t.d_unsched, n_pad));
   MSH_HIP(c, hipMalloc(&t.d_digit, n_pad));
   MSH_HIP(c, hipMalloc(&t.d_planes, n_pad / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
-  // + ER_PAD groups: the batch kernel copies whole tiles without clamping (never read as rows)
-  MSH_HIP(c, hipMalloc(&t.d_erows, (n_pad / msh::GROUP_NODES + msh::ER_PAD) * msh::ER_GD * sizeof(uint32_t)));
   MSH_HIP(c, hipMalloc(&t.d_hrows, n_pad / msh::GROUP_NODES * msh::HR_GD * sizeof(uint32_t)));
+  MSH_HIP(c, hipMalloc(&t.d_nrec, n_pad * msh::NREC * sizeof(uint32_t)));
   MSH_HIP(c, hipMalloc(&t.d_ball, 2 * sizeof(uint32_t)));
   t.cap = n_pad;
   return MSH_OK;
 }
 
 int ensure_cols(msh_ctx* c, NodeTable& t) {
-  if (!t.d_cols) MSH_HIP(c, hipMalloc(&t.d_cols, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t)));
+  if (!t.d_cols) {
+    MSH_HIP(c, hipMalloc(&t.d_cols, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t)));
+    MSH_HIP(c, hipMemset(t.d_cols, 0, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t)));
+  }
+  if (!t.d_cols100) {
+    MSH_HIP(c, hipMalloc(&t.d_cols100, (size_t)msh::GEN_COLS * t.cap * sizeof(double)));
+    MSH_HIP(c, hipMemset(t.d_cols100, 0, (size_t)msh::GEN_COLS * t.cap * sizeof(double)));
+  }
   return MSH_OK;
 }
 
@@ -445,9 +455,14 @@ int rewrite(msh_ctx* c, const Rewrite& w) {
     MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_nstage, pbytes, hipMemcpyHostToDevice, ps));
   }
   hipError_t e = msh::launch_node_prep(dst.d_unsched, dst.d_digit, n, n_pad, c->pp.has_nu_filter, dst.d_ball,
-                                       dst.d_planes, dst.d_erows, dst.d_hrows, ps, c->d_patch,
+                                       dst.d_planes, dst.d_hrows, dst.d_nrec, ps, c->d_patch,
                                        w.kind == Rewrite::PATCH ? w.patch_count : 0);
   if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
+  uint32_t col_mask = 0;
+  for (int k = 0; k < msh::GEN_COLS; ++k) col_mask |= dst.col_ok[k] ? 1u << k : 0u;
+  if (col_mask && (e = msh::launch_cols100(dst.d_cols, dst.d_cols100, (int64_t)dst.cap, n, n_pad, col_mask, ps)) !=
+                      hipSuccess)
+    return hip_fail(c, e, "cols100_kernel");
   // an upload zeroes the sequential-mode counts (after the sequential launches in flight)
   if (up) {
     if ((size_t)n_pad > c->counts_cap) {
@@ -493,19 +508,55 @@ int ready(msh_ctx* c) {
   return MSH_OK;
 }
 
-msh::BatchArgs batch_args(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t* pt) {
+// The class-row kernel's arguments (MSH_BATCH_KERNEL=classrows).
+msh::BatchArgs classrow_args(msh_ctx* c) {
   msh::BatchArgs a{};
   const NodeTable& t = cur_table(c);
-  a.planes = t.d_planes;
-  a.erows = t.d_erows;
   a.hrows = t.d_hrows;
   a.n_groups = c->n_pad / msh::GROUP_NODES;
-  a.pod_digit = pd;
-  a.pod_tol = pt;
-  a.n_pods = p;
   a.ball = t.d_ball;
   a.pp = c->pp;
   return a;
+}
+
+// pair_kernel's arguments for the current table (the batches are filled in by the caller).
+msh::PairArgs pair_args(msh_ctx* c) {
+  msh::PairArgs a{};
+  const NodeTable& t = cur_table(c);
+  a.planes = t.d_planes;
+  a.n_groups = c->n_pad / msh::GROUP_NODES;
+  a.g_full = c->n_nodes / msh::GROUP_NODES;
+  a.pp = c->pp;
+  return a;
+}
+
+// The opt-in class-row kernel serves this table (it holds at most 8,192 nodes).
+bool use_classrows(const msh_ctx* c) {
+  return c->dev.batch_kernel == 1 && msh::classrows_fit(c->n_pad / msh::GROUP_NODES);
+}
+
+// nb batches on the per-pair kernel (or the opt-in class-row kernel), MULTI_MAX per launch.
+int launch_generic_descs(msh_ctx* c, const msh::BatchDesc* d, int32_t nb, hipStream_t s);
+bool use_generic(const msh_ctx* c);
+
+int launch_batch_descs(msh_ctx* c, const msh::BatchDesc* d, int32_t nb, hipStream_t s) {
+  if (use_generic(c)) return launch_generic_descs(c, d, nb, s);
+  for (int32_t i0 = 0; i0 < nb; i0 += msh::MULTI_MAX) {
+    const int n = std::min<int32_t>(msh::MULTI_MAX, nb - i0);
+    TimedLaunch tl(c);
+    hipError_t e;
+    if (use_classrows(c)) {
+      e = msh::launch_classrows(classrow_args(c), d + i0, n, c->dev, s);
+      if (e != hipSuccess) return hip_fail(c, e, "wgp_kernel");
+    } else {
+      msh::PairArgs a = pair_args(c);
+      a.nb = n;
+      for (int k = 0; k < n; ++k) a.d[k] = d[i0 + k];
+      e = msh::launch_pairs(a, false, c->dev, s);
+      if (e != hipSuccess) return hip_fail(c, e, "pair_kernel");
+    }
+  }
+  return MSH_OK;
 }
 
 // The generic pipeline runs the batch entry points when the score list names a score column (or
@@ -515,41 +566,45 @@ bool use_generic(const msh_ctx* c) { return c->generic || c->dev.batch_kernel ==
 int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   g = msh::GenericArgs{};
   const NodeTable& t = cur_table(c);
-  g.unsched = t.d_unsched;
-  g.digit = t.d_digit;
+  g.nrec = t.d_nrec;
   g.cols = t.d_cols;
+  g.cols100 = t.d_cols100;
   g.col_stride = (int64_t)t.cap;
   g.n_nodes = c->n_nodes;
-  g.has_nu = c->pp.has_nu_filter;
+  g.n_chunks = (c->n_nodes + msh::GEN_CH - 1) / msh::GEN_CH;
   g.nn_prescore = c->pp.nn_prescore;
-  g.nn_score = c->pp.has_nn_score;
-  g.ns = (int32_t)c->score_ids.size();
-  for (int32_t k = 0; k < g.ns; ++k) {
+  for (size_t k = 0; k < c->score_ids.size(); ++k) {
     const int32_t id = c->score_ids[k];
-    g.kind[k] = id == MSH_PLUGIN_NODE_NUMBER ? 0 : 1 + (id - MSH_PLUGIN_SCORE_COLUMN0);
-    if (g.kind[k] > 0 && !t.col_ok[g.kind[k] - 1])
-      return fail(c, MSH_ERR_STATE, "score column " + std::to_string(id) + " not uploaded since the last node upload");
-    g.mode[k] = c->normalize[k];
-    g.weight[k] = c->weights[k];
-    g.need_ext = g.need_ext || g.mode[k] != MSH_NORMALIZE_NONE;
+    if (id == MSH_PLUGIN_NODE_NUMBER) {
+      g.nn_score = 1;
+      g.nn_mode = c->normalize[k];
+      g.nn_weight = c->weights[k];
+    } else {
+      const int32_t col = id - MSH_PLUGIN_SCORE_COLUMN0;
+      if (!t.col_ok[col])
+        return fail(c, MSH_ERR_STATE, "score column " + std::to_string(id) + " not uploaded since the last node upload");
+      g.ccol[g.ncol] = col;
+      g.cmode[g.ncol] = c->normalize[k];
+      g.cweight[g.ncol] = c->weights[k];
+      ++g.ncol;
+    }
+    g.need_ext = g.need_ext || c->normalize[k] != MSH_NORMALIZE_NONE;
   }
   return MSH_OK;
 }
 
-int launch_generic_batch(msh_ctx* c, int32_t p, const int8_t* pd, const uint8_t* pt, int32_t* oi, int64_t* os,
-                         int32_t* ost, hipStream_t s) {
+// nb batches on generic_kernel, MULTI_MAX per launch.
+int launch_generic_descs(msh_ctx* c, const msh::BatchDesc* d, int32_t nb, hipStream_t s) {
   msh::GenericArgs g;
   int rc = generic_args(c, g);
   if (rc != MSH_OK) return rc;
-  g.pod_digit = pd;
-  g.pod_tol = pt;
-  g.n_pods = p;
-  g.out_idx = oi;
-  g.out_score = os;
-  g.out_status = ost;
-  TimedLaunch tl(c);
-  hipError_t e = msh::launch_generic(g, s);
-  if (e != hipSuccess) return hip_fail(c, e, "generic_kernel");
+  for (int32_t i0 = 0; i0 < nb; i0 += msh::MULTI_MAX) {
+    g.nb = std::min<int32_t>(msh::MULTI_MAX, nb - i0);
+    for (int k = 0; k < g.nb; ++k) g.d[k] = d[i0 + k];
+    TimedLaunch tl(c);
+    hipError_t e = msh::launch_generic(g, 0, c->dev, s);
+    if (e != hipSuccess) return hip_fail(c, e, "generic_kernel");
+  }
   return MSH_OK;
 }
 
@@ -682,15 +737,11 @@ bool knob(const char* name, std::initializer_list<std::pair<const char*, int>> a
 
 bool read_knobs(msh::DeviceInfo& d, std::string* err) {
   int io = 0, poll = 0;
-  const bool ok = knob("MSH_BITS_SLICES", {{"0", 0}, {"1", 1}, {"2", 2}, {"4", 4}, {"8", 8}, {"16", 16}}, &d.bits_slices, err) &&
+  const bool ok = knob("MSH_BITS_SLICES", {{"0", 0}, {"1", 1}, {"2", 2}, {"4", 4}}, &d.bits_slices, err) &&
                   knob("MSH_SEQ_WAVES", {{"0", 0}, {"1", 1}, {"4", 4}, {"15", 15}, {"16", 16}}, &d.seq_waves, err) &&
-                  knob("MSH_ROWS_PPL", {{"1", 1}, {"2", 2}}, &d.rows_ppl, err) &&
-                  knob("MSH_KX_BITS", {{"0", 0}, {"1", 1}}, &d.kx_bits, err) &&
                   knob("MSH_HOST_IO", {{"zero-copy", 0}, {"zc", 1}, {"dma", 2}}, &io, err) &&
                   knob("MSH_HOST_SYNC", {{"wait", 0}, {"poll", 1}}, &poll, err) &&
-                  knob("MSH_BATCH_KERNEL", {{"wg", 0}, {"slices", 1}, {"generic", 2}}, &d.batch_kernel, err) &&
-                  knob("MSH_WG_WAVES", {{"0", 0}, {"4", 4}, {"8", 8}}, &d.wg_waves, err) &&
-                  knob("MSH_WG_PERSIST", {{"1", 0}, {"0", 1}}, &d.wg_no_persist, err);
+                  knob("MSH_BATCH_KERNEL", {{"pair", 0}, {"classrows", 1}, {"generic", 2}}, &d.batch_kernel, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;
   d.host_sync_poll = poll;
@@ -990,23 +1041,10 @@ int msh_schedule_batch_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = ready(c);
   if (rc != MSH_OK) return rc;
-  if (use_generic(c)) {
-    if (p == 0) return MSH_OK;
-    if ((rc = launch_generic_batch(c, p, d_pod_digit, d_pod_tol, d_out_idx, d_out_score, d_out_status, s)) != MSH_OK)
-      return rc;
-    return track_launch(c, s);
-  }
-  msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
-  a.out_idx = d_out_idx;
-  a.out_score = d_out_score;
-  a.out_status = d_out_status;
-  hipError_t e;
-  {
-    TimedLaunch tl(c);
-    e = msh::launch_batch(a, false, c->dev, s);
-  }
-  if (e != hipSuccess) return hip_fail(c, e, "batch kernel");
-  return p > 0 ? track_launch(c, s) : MSH_OK;
+  if (p == 0) return MSH_OK;
+  const msh::BatchDesc d{d_pod_digit, d_pod_tol, d_out_idx, d_out_score, d_out_status, p, 0};
+  if ((rc = launch_batch_descs(c, &d, 1, s)) != MSH_OK) return rc;
+  return track_launch(c, s);
 }
 
 int msh_schedule_batches_device(msh_ctx* c, int32_t nb, const msh_batch* batches, void* stream) {
@@ -1024,36 +1062,14 @@ int msh_schedule_batches_device(msh_ctx* c, int32_t nb, const msh_batch* batches
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = ready(c);
   if (rc != MSH_OK) return rc;
-  if (use_generic(c)) {  // one generic launch per batch
-    for (int32_t i = 0; i < nb; ++i) {
-      const msh_batch& b = batches[i];
-      if (b.p > 0 &&
-          (rc = launch_generic_batch(c, b.p, b.pod_digit, b.pod_tol, b.out_idx, b.out_score, b.out_status, s)) != MSH_OK)
-        return rc;
-    }
-    return nb > 0 ? track_launch(c, s) : MSH_OK;
-  }
-  const bool single = c->dev.batch_kernel == 1 || (msh::needs_kx(c->pp) && c->dev.kx_bits);  // A/B kernels
-  for (int32_t i0 = 0; i0 < nb; i0 += msh::MULTI_MAX) {
-    const int n = std::min<int32_t>(msh::MULTI_MAX, nb - i0);
+  for (int32_t i0 = 0; i0 < nb; i0 += msh::MULTI_MAX) {  // MULTI_MAX batches per launch
+    const int32_t n = std::min<int32_t>(msh::MULTI_MAX, nb - i0);
     msh::BatchDesc d[msh::MULTI_MAX];
-    for (int k = 0; k < n; ++k) {
+    for (int32_t k = 0; k < n; ++k) {
       const msh_batch& b = batches[i0 + k];
       d[k] = msh::BatchDesc{b.pod_digit, b.pod_tol, b.out_idx, b.out_score, b.out_status, b.p, 0};
-      if (single && b.p > 0) {
-        msh::BatchArgs a = batch_args(c, b.p, b.pod_digit, b.pod_tol);
-        a.out_idx = b.out_idx;
-        a.out_score = b.out_score;
-        a.out_status = b.out_status;
-        TimedLaunch tl(c);
-        hipError_t e = msh::launch_batch(a, false, c->dev, s);
-        if (e != hipSuccess) return hip_fail(c, e, "batch kernel");
-      }
     }
-    if (single) continue;
-    TimedLaunch tl(c);
-    hipError_t e = msh::launch_batches(batch_args(c, 0, nullptr, nullptr), d, n, c->dev, s);
-    if (e != hipSuccess) return hip_fail(c, e, "wg_kernel (multi-batch)");
+    if ((rc = launch_batch_descs(c, d, n, s)) != MSH_OK) return rc;
   }
   return nb > 0 ? track_launch(c, s) : MSH_OK;
 }
@@ -1224,13 +1240,13 @@ int msh_reset_node_pod_counts(msh_ctx* c) {
 
 int msh_keys_slot1_is_any(const msh_ctx* c, int32_t* out_flag) {
   if (!c || !out_flag) return MSH_ERR_INVALID;
-  *out_flag = msh::needs_kx(c->pp) ? 0 : 1;
+  *out_flag = 0;  // ABI v7: keys[p + j] is always pod j's own first feasible non-match
   return MSH_OK;
 }
 
 int msh_shard_keys_len(const msh_ctx* c, int32_t p, int32_t* out_len) {
   if (!c || !out_len || p < 0) return MSH_ERR_INVALID;
-  const int64_t len = (int64_t)p + (msh::needs_kx(c->pp) ? (int64_t)p : 2);
+  const int64_t len = 2 * (int64_t)p;  // per pod: first feasible match, first feasible non-match
   if (len > INT32_MAX) return MSH_ERR_INVALID;
   *out_len = (int32_t)len;
   return MSH_OK;
@@ -1244,17 +1260,26 @@ int msh_shard_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
   if (p < 0 || node_base < 0) return fail(c, MSH_ERR_INVALID, "negative argument");
   if (p > 0 && (!d_pod_digit || !d_pod_tol || !d_keys)) return fail(c, MSH_ERR_INVALID, "null device pointer");
   if (node_base + (int64_t)c->n_nodes >= msh::GKEY_MAX) return fail(c, MSH_ERR_INVALID, "global node index overflows the key");
-  if (c->generic) return fail(c, MSH_ERR_UNSUPPORTED, "score-column plugins run on the batch entry points only");
+  if (c->generic)
+    return fail(c, MSH_ERR_UNSUPPORTED, "score-column plugin lists shard through msh_generic_extents_device / "
+                                        "msh_generic_best_device");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc = ready(c);
   if (rc != MSH_OK) return rc;
-  msh::BatchArgs a = batch_args(c, p, d_pod_digit, d_pod_tol);
+  if (p == 0) return MSH_OK;
+  msh::PairArgs a = pair_args(c);
+  a.nb = 1;
+  a.d[0] = msh::BatchDesc{d_pod_digit, d_pod_tol, nullptr, nullptr, nullptr, p, 0};
   a.keys = d_keys;
   a.node_base = node_base;
-  hipError_t e = msh::launch_batch(a, true, c->dev, s);
-  if (e != hipSuccess) return hip_fail(c, e, "batch kernel (shard keys)");
-  return p > 0 ? track_launch(c, s) : MSH_OK;
+  hipError_t e;
+  {
+    TimedLaunch tl(c);
+    e = msh::launch_pairs(a, true, c->dev, s);
+  }
+  if (e != hipSuccess) return hip_fail(c, e, "pair_kernel (shard keys)");
+  return track_launch(c, s);
 }
 
 int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
@@ -1267,10 +1292,110 @@ int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
     return fail(c, MSH_ERR_INVALID, "null device pointer");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int32_t slot1_any = msh::needs_kx(c->pp) ? 0 : 1;
-  hipError_t e = msh::launch_decode_keys(d_pod_digit, d_pod_tol, p, d_keys, slot1_any, c->pp,
+  hipError_t e = msh::launch_decode_keys(d_pod_digit, d_pod_tol, p, d_keys, 0, c->pp,
                                          d_out_idx, d_out_score, d_out_status, s);
   if (e != hipSuccess) return hip_fail(c, e, "decode_keys_kernel");
+  return MSH_OK;
+}
+
+int msh_generic_ext_len(const msh_ctx* c, int32_t p, int64_t* out_len) {
+  if (!c || !out_len || p < 0) return MSH_ERR_INVALID;
+  bool ext = false;
+  int32_t ncol = 0;
+  for (size_t k = 0; k < c->score_ids.size(); ++k) {
+    ext = ext || c->normalize[k] != MSH_NORMALIZE_NONE;
+    ncol += is_column(c->score_ids[k]) ? 1 : 0;
+  }
+  *out_len = ext ? 2 * (int64_t)(1 + ncol) * p : 0;
+  return MSH_OK;
+}
+
+namespace {
+// One sharded generic launch (mode 1: extents, mode 2: best) over this ctx's node slice.
+int generic_shard_launch(msh_ctx* c, int mode, int32_t p, const int8_t* pd, const uint8_t* pt, int64_t* ext,
+                         int64_t node_base, int64_t* bt, int32_t* bi, hipStream_t s) {
+  msh::GenericArgs g;
+  int rc = generic_args(c, g);
+  if (rc != MSH_OK) return rc;
+  g.nb = 1;
+  g.d[0] = msh::BatchDesc{pd, pt, nullptr, nullptr, nullptr, p, 0};
+  g.ext = ext;
+  g.node_base = node_base;
+  g.best_total = bt;
+  g.best_idx = bi;
+  hipError_t e;
+  {
+    TimedLaunch tl(c);
+    e = msh::launch_generic(g, mode, c->dev, s);
+  }
+  if (e != hipSuccess) return hip_fail(c, e, "generic_kernel (node-sharded)");
+  return track_launch(c, s);
+}
+}  // namespace
+
+int msh_generic_extents_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit, const uint8_t* d_pod_tol,
+                               int64_t* d_ext, void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  int64_t len = 0;
+  msh_generic_ext_len(c, p, &len);
+  if (p == 0 || len == 0) return MSH_OK;  // no plugin normalizes: nothing to merge
+  if (!d_pod_digit || !d_pod_tol || !d_ext) return fail(c, MSH_ERR_INVALID, "null device pointer");
+  DeviceGuard g(c->device);
+  int rc = ready(c);
+  if (rc != MSH_OK) return rc;
+  return generic_shard_launch(c, 1, p, d_pod_digit, d_pod_tol, d_ext, 0, nullptr, nullptr,
+                              reinterpret_cast<hipStream_t>(stream));
+}
+
+int msh_generic_best_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit, const uint8_t* d_pod_tol,
+                            const int64_t* d_ext, int64_t node_base, int64_t* d_best_total, int32_t* d_best_idx,
+                            void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0 || node_base < 0) return fail(c, MSH_ERR_INVALID, "negative argument");
+  if (node_base + (int64_t)c->n_nodes >= (int64_t)INT32_MAX)
+    return fail(c, MSH_ERR_INVALID, "global node index overflows int32");
+  int64_t len = 0;
+  msh_generic_ext_len(c, p, &len);
+  if (p == 0) return MSH_OK;
+  if (!d_pod_digit || !d_pod_tol || !d_best_total || !d_best_idx || (len > 0 && !d_ext))
+    return fail(c, MSH_ERR_INVALID, "null device pointer");
+  DeviceGuard g(c->device);
+  int rc = ready(c);
+  if (rc != MSH_OK) return rc;
+  return generic_shard_launch(c, 2, p, d_pod_digit, d_pod_tol, const_cast<int64_t*>(d_ext), node_base, d_best_total,
+                              d_best_idx, reinterpret_cast<hipStream_t>(stream));
+}
+
+int msh_generic_candidates_device(msh_ctx* c, int32_t p, const int64_t* d_local_total, const int64_t* d_merged_total,
+                                  int32_t* d_best_idx, void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  if (p > 0 && (!d_local_total || !d_merged_total || !d_best_idx)) return fail(c, MSH_ERR_INVALID, "null device pointer");
+  DeviceGuard g(c->device);
+  hipError_t e = msh::launch_generic_candidates(p, d_local_total, d_merged_total, d_best_idx,
+                                                reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(c, e, "generic_candidate_kernel");
+  return MSH_OK;
+}
+
+int msh_generic_decode_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit, const int64_t* d_merged_total,
+                              const int32_t* d_merged_idx, int32_t* d_out_idx, int64_t* d_out_score,
+                              int32_t* d_out_status, void* stream) {
+  if (!c) return MSH_ERR_INVALID;
+  c->err.clear();
+  if (p < 0) return fail(c, MSH_ERR_INVALID, "negative pod count");
+  if (p > 0 && (!d_pod_digit || !d_merged_total || !d_merged_idx || !d_out_idx || !d_out_status))
+    return fail(c, MSH_ERR_INVALID, "null device pointer");  // d_out_score optional
+  DeviceGuard g(c->device);
+  int32_t nn_score = 0;
+  for (int32_t id : c->score_ids) nn_score |= id == MSH_PLUGIN_NODE_NUMBER ? 1 : 0;
+  hipError_t e = msh::launch_generic_decode(d_pod_digit, p, d_merged_total, d_merged_idx, nn_score, c->pp.nn_prescore,
+                                            d_out_idx, d_out_score, d_out_status, reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(c, e, "generic_decode_kernel");
   return MSH_OK;
 }
 

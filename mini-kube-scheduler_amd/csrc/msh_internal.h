@@ -36,20 +36,20 @@ inline bool needs_kx(const PluginParams& pp) {
 // Device facts and launch choices, resolved once in msh_create (never on the launch path).
 struct DeviceInfo {
   int cus = 256;
-  int bits_slices = 0;   // tests / A-B only (MSH_BITS_SLICES at msh_create): slice waves per pod block, 0 = auto
+  int bits_slices = 0;   // tests / A-B only (MSH_BITS_SLICES at msh_create): pair_kernel slice waves per pod block
+                         // (1, 2, 4), 0 = auto
   int seq_waves = 0;     // tests / A-B only (MSH_SEQ_WAVES at msh_create): sequential scanning waves, 0 = auto
-  int rows_ppl = 1;      // pods per lane of the digit-row kernel (1 or 2; MSH_ROWS_PPL at msh_create, A/B)
-  int kx_bits = 0;       // A/B only (MSH_KX_BITS=1 at msh_create): REVERSE / MINMAX on the code-plane kernel
   // Host-buffer calls (msh_schedule_batch / _sequential): the kernel reads the pod columns from and
   // writes the outputs to page-locked host memory (default). A/B only, MSH_HOST_IO at msh_create:
   // "dma" = columns and outputs DMA'd through device scratch, "zc" = columns DMA'd, outputs zero-copy.
   int host_io_dma = 0;
   int host_io_zc_in = 1;
   int host_sync_poll = 0;  // A/B only (MSH_HOST_SYNC=poll): poll an event instead of hipStreamSynchronize
-  int batch_kernel = 0;    // 0 = wg_kernel (default), 1 = the round-2 slice kernel rows_kernel (MSH_BATCH_KERNEL=slices,
-                           // A/B), 2 = generic_kernel for every plugin list (MSH_BATCH_KERNEL=generic, A/B)
-  int wg_waves = 0;        // A/B only (MSH_WG_WAVES=1|2|4|8): waves per workgroup of wg_kernel, 0 = auto
-  int wg_no_persist = 0;   // A/B only (MSH_WG_PERSIST=0): multi-batch launches on the 2-D wg_kernel grid
+  // Batch kernel (MSH_BATCH_KERNEL at msh_create): 0 = pair_kernel, the per-pair evaluation (default);
+  // 1 = the class-row kernel wgp_kernel (opt-in "classrows": a pod's verdicts read from tables indexed
+  // by its class, tables up to 8,192 nodes; larger tables and shard keys stay on pair_kernel);
+  // 2 = generic_kernel for every plugin list ("generic", A/B)
+  int batch_kernel = 0;
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit
@@ -76,21 +76,8 @@ constexpr int GROUP_NODES = PLANE_GW * 32;
 constexpr int GROUP_DWORDS = PLANE_GW * PLANE_N;
 constexpr int32_t NODE_PAD = 1024;  // tables are padded to whole 1,024-node prep blocks (4 groups)
 
-// Digit rows (a bitmap index on NodeNumber's node digit; the input of the identity-mode batch
-// kernel): for every word, ER_ROWS row words, row r = the word's real nodes whose suffix digit is
-// r (r = 0..9); row 10 stays zero (the row of pods without a digit suffix). Per group, two chunks
-// of 4 consecutive words, each chunk row-major with a row's 4 words contiguous, then the group's 8
-// X words (the PLANE_X plane again, so that one copy brings a group's whole input):
-//   erows[g * ER_GD + (c * ER_ROWS + r) * 4 + k] = row r of word g * PLANE_GW + 4 c + k
-//   erows[g * ER_GD + ER_Q * 4 + j]              = X of word g * PLANE_GW + j
-// so a pod's row words of one chunk are one 16-byte read, and the 11 rows of a chunk (44 dwords)
-// sit in distinct LDS banks. 1.5 B per node. (The REVERSE / MINMAX modes also read the V plane,
-// from the code planes.)
+// Row count of the class rows below: rows 0..9 = suffix digits, row 10 = pods without a digit.
 constexpr int ER_ROWS = 11;
-constexpr int ER_Q = 2 * ER_ROWS;      // 16-byte row chunks per group
-constexpr int ER_GQ = ER_Q + 2;        // 16-byte chunks per group: the rows, then X
-constexpr int ER_GD = ER_GQ * 4;       // dwords per group
-constexpr int ER_TG = 8;               // groups per LDS tile of the batch kernel (3,072 B per wave)
 
 // Class rows (the input of the persistent batch kernel): the digit rows with the filter folded in per
 // pod class, t = 0 (does not tolerate the unschedulable taint) and t = 1 (tolerates), so that a pod's
@@ -131,14 +118,13 @@ __host__ __device__ constexpr uint32_t hr_entry(uint32_t c, uint32_t t, uint32_t
   return t == 0 ? (c == 0 ? r : 21 + r)
                 : r < 5 ? (c == 0 ? 11 + r : 16 + r) : r < 10 ? (c == 0 ? 38 + r : 27 + r) : (c == 0 ? 42u : 41u);
 }
-constexpr int ER_PAD = 2 * ER_TG;      // groups of padding: whole-tile copies need no clamp
 
 // ---- launchers (msh_kernels.hip) ----
 // Applies `patch_count` pending msh_patch_nodes entries (idx | unsched << 32 | (uint8)digit << 40)
 // to the raw columns, then rebuilds the planes and the first feasible node per class (ball).
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n, int32_t n_pad,
-                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows,
-                            uint32_t* d_hrows, hipStream_t s,
+                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_hrows,
+                            uint32_t* d_nrec, hipStream_t s,
                             const unsigned long long* d_patch = nullptr, int32_t patch_count = 0);
 
 constexpr int64_t EXPORT_NONE = INT64_MIN;  // msh_export_results: no score recorded
@@ -147,29 +133,15 @@ hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_
                          const PluginParams& pp, uint8_t* d_filter, int64_t* d_raw, int64_t* d_fin,
                          hipStream_t s);
 
+// The class-row kernel's table and plugin set (MSH_BATCH_KERNEL=classrows).
 struct BatchArgs {
-  const uint32_t* planes;    // bit-sliced node table, n_groups groups
-  const uint32_t* erows;     // digit rows (ER_* layout), n_groups groups
   const uint32_t* hrows;     // class rows (HR_* layout), n_groups groups
   int32_t n_groups;          // n_pad / GROUP_NODES
-  int32_t gps;               // groups per slice wave (set by the launcher)
-  const int8_t* pod_digit;
-  const uint8_t* pod_tol;
-  int32_t n_pods;
   const uint32_t* ball;      // [2] first feasible key per pod class (0: !tol, 1: tol)
   PluginParams pp;
-  int32_t* out_idx;
-  int64_t* out_score;
-  int32_t* out_status;
-  int32_t* keys;             // shard mode: [n_pods + slot-1 count] global keys (msh_shard_keys_len)
-  int64_t node_base;
 };
 
-hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s);
-
-// One batch of a multi-batch launch (msh_schedule_batches_device): its own pod columns and
-// outputs. The launch grid is 2-D: blockIdx.y = the batch, blockIdx.x = the pod block within it
-// (the x extent is the largest batch's; a workgroup past its batch's end exits at once).
+// One batch of a (multi-batch) launch: its own pod columns and outputs.
 struct BatchDesc {
   const int8_t* pod_digit;
   const uint8_t* pod_tol;
@@ -180,9 +152,9 @@ struct BatchDesc {
   int32_t reserved;
 };
 constexpr int RANK_MAX = 8;     // persistent kernel: workgroups per CU (age slots)
-constexpr int MULTI_MAX = 32;  // batches per launch (kernel-argument descriptors, 48 B each: ~1.7 KB)
+constexpr int MULTI_MAX = 32;  // batches per launch (kernel-argument descriptors, 40 B each: ~1.3 KB)
 struct MultiArgs {
-  BatchArgs a;  // the node table, plugin set and launch geometry (its pod / output fields unused)
+  BatchArgs a;  // the node table and plugin set
   int32_t nb;
   int32_t bpb;  // pod blocks per batch (the largest batch's), set by the launcher
   // persistent kernel: walk 0 = strided items (g, g + G, ...); walk 1 = workgroup g (age slot
@@ -194,9 +166,25 @@ struct MultiArgs {
   BatchDesc d[MULTI_MAX];
 };
 
-// nb (1..MULTI_MAX) independent batches of device-resident pods in ONE launch of the workgroup
-// kernel. `a` carries the table and plugin set.
-hipError_t launch_batches(const BatchArgs& a, const BatchDesc* d, int nb, const DeviceInfo& dev, hipStream_t s);
+// The class-row kernel (opt-in): nb (1..MULTI_MAX) batches in ONE launch; tables up to
+// classrows_fit groups.
+bool classrows_fit(int32_t n_groups);
+hipError_t launch_classrows(const BatchArgs& a, const BatchDesc* d, int nb, const DeviceInfo& dev, hipStream_t s);
+
+// The per-pair kernel (pair_kernel): nb (1..MULTI_MAX) batches in one launch, or (shard) the
+// per-pod shard keys of ONE batch, d[0].
+struct PairArgs {
+  const uint32_t* planes;  // bit-sliced node table (PLANE_* layout), n_groups groups
+  int32_t n_groups;
+  int32_t g_full;          // groups [0, g_full) hold real nodes only (no padding slot)
+  int32_t gps;             // groups per slice wave (set by the launcher)
+  int32_t nb;
+  PluginParams pp;
+  int64_t node_base;       // shard mode: global index of local node 0
+  int32_t* keys;           // shard mode: [2 * d[0].n_pods] keys (first feasible match, non-match)
+  BatchDesc d[MULTI_MAX];
+};
+hipError_t launch_pairs(PairArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s);
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,
                               const int32_t* keys, int32_t slot1_any, PluginParams pp,
@@ -206,28 +194,46 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, i
 // ---- generic score pipeline (any score plugin list; generic_kernel) ----
 constexpr int GEN_MAX_SCORE = 5;  // score plugins per list: NodeNumber + up to four score columns
 constexpr int GEN_COLS = 4;       // score-column plugins MSH_PLUGIN_SCORE_COLUMN0..3
+constexpr int GEN_CH = 8;         // nodes per scalar-load chunk of generic_kernel
+// Node record of generic_kernel (NREC uint32 per node, n_pad records, written by the prep):
+// [0] NodeNumber code (suffix digit 0..9, or 15), [1] 0, [2..3] a 64-bit lane mask: all-ones when
+// NodeUnschedulable passes the node for every pod, 0 when it is Spec.Unschedulable with the filter listed
+// (then only the lanes of pods that tolerate the taint pass: OR with the wave's tolerates ballot).
+constexpr int NREC = 4;
 struct GenericArgs {
-  const uint8_t* unsched;  // the uploaded columns, List order
-  const int8_t* digit;
-  const int64_t* cols;     // GEN_COLS x col_stride int64: column k at cols + k * col_stride
+  const uint32_t* nrec;    // node records (NREC per node), List order
+  const int64_t* cols;     // GEN_COLS x col_stride raw column values, List order
+  const double* cols100;   // GEN_COLS x col_stride: 100 x the column value as a double (exact)
   int64_t col_stride;
   int32_t n_nodes;
-  int32_t has_nu;          // NodeUnschedulable in the filter list
-  int32_t nn_prescore;     // NodeNumber in the prescore list
+  int32_t n_chunks;        // ceil(n / GEN_CH) node chunks scanned (the last may be partial)
+  int32_t cps;             // chunks per slice wave (set by the launcher)
   int32_t nn_score;        // NodeNumber in the score list
-  int32_t ns;              // score plugins
-  int32_t need_ext;        // some plugin normalizes: the extent pass runs
-  int32_t kind[GEN_MAX_SCORE];   // 0 = NodeNumber, 1 + k = score column k
-  int32_t mode[GEN_MAX_SCORE];   // msh_normalize
-  int64_t weight[GEN_MAX_SCORE];
-  const int8_t* pod_digit;
-  const uint8_t* pod_tol;
-  int32_t n_pods;
-  int32_t* out_idx;
-  int64_t* out_score;      // may be null
-  int32_t* out_status;
+  int32_t nn_prescore;     // NodeNumber in the prescore list (its PreScore state is written)
+  int32_t nn_mode;         // NodeNumber's msh_normalize
+  int64_t nn_weight;
+  int32_t ncol;            // score-column plugins in the list
+  int32_t ccol[GEN_COLS];  // ... their column (0..GEN_COLS-1), msh_normalize and weight, list order
+  int32_t cmode[GEN_COLS];
+  int64_t cweight[GEN_COLS];
+  int32_t need_ext;        // some plugin normalizes: the extent sweep runs
+  int32_t nb;              // batches (mode 0: up to MULTI_MAX; sharded modes: 1)
+  int64_t node_base;       // sharded modes: global index of local node 0
+  int64_t* ext;            // mode 1: out, mode 2: in; [2 (1 + ncol)][p] per-pod extents, mins negated
+  int64_t* best_total;     // mode 2 out: per pod, the shard's best total (INT64_MIN: no feasible node)
+  int32_t* best_idx;       // mode 2 out: its global node index (INT32_MAX: none)
+  BatchDesc d[MULTI_MAX];
 };
-hipError_t launch_generic(const GenericArgs& a, hipStream_t s);
+// mode 0: schedule nb batches; 1: per-pod extents over this shard; 2: per-pod best over this shard.
+hipError_t launch_generic(GenericArgs& a, int mode, const DeviceInfo& dev, hipStream_t s);
+hipError_t launch_generic_candidates(int32_t p, const int64_t* local_total, const int64_t* merged_total, int32_t* idx,
+                                     hipStream_t s);
+hipError_t launch_generic_decode(const int8_t* pod_digit, int32_t p, const int64_t* best_total, const int32_t* best_idx,
+                                 int32_t nn_score, int32_t nn_prescore, int32_t* out_idx, int64_t* out_score,
+                                 int32_t* out_status, hipStream_t s);
+// 100 x each valid column as a double, for the normalizing columns (after a column changes)
+hipError_t launch_cols100(const int64_t* cols, double* cols100, int64_t stride, int32_t n, int32_t n_pad,
+                          uint32_t col_mask, hipStream_t s);
 
 struct SeqArgs {
   const uint32_t* planes;    // bit-sliced node table (PLANE_* layout)

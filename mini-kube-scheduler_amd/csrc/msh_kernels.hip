@@ -83,8 +83,8 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
                                                                  int32_t n, int32_t has_nu,
                                                                  uint32_t* __restrict__ ball,
                                                                  uint32_t* __restrict__ planes,
-                                                                 uint32_t* __restrict__ erows,
-                                                                 uint32_t* __restrict__ hrows) {
+                                                                 uint32_t* __restrict__ hrows,
+                                                                 uint32_t* __restrict__ nrec) {
   constexpr int NWV = PREP_THREADS / WAVE;
   __shared__ uint32_t s_k0[NWV], s_k1[NWV];
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -99,6 +99,12 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
   const uint32_t code = has_digit ? (uint32_t)d : CODE_NONE_NODE;  // NodeNumber: Atoi of the last byte
   const unsigned long long pm[PLANE_N] = {__ballot(code & 1u), __ballot(code & 2u), __ballot(code & 4u),
                                           __ballot(code & 8u), __ballot(valid && !feas0), __ballot(valid)};
+  // the node record of generic_kernel: the code, and the NodeUnschedulable mask (all-ones: every pod
+  // passes; 0: only pods that tolerate the taint pass)
+  {
+    const uint32_t xm = feas0 ? 0xFFFFFFFFu : 0u;
+    reinterpret_cast<uint4*>(nrec)[i] = make_uint4(code, 0u, xm, xm);
+  }
   // this wave's 64 nodes are words 2t and 2t + 1 of the PLANE_* layout: lanes 0..11 write them
   if (lane < 2 * PLANE_N) {
     const int k = lane >> 1, half = lane & 1;
@@ -108,24 +114,10 @@ __global__ __launch_bounds__(PREP_THREADS) void node_prep_kernel(const uint8_t* 
     const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;  // i - lane: the wave's first node
     planes[((word / PLANE_GW) * PLANE_N + k) * PLANE_GW + word % PLANE_GW] = (uint32_t)(m >> (32 * half));
   }
-  // the digit rows of the same two words (ER_* layout): row r = real nodes with digit r; lanes
-  // 0..21 write rows 0..10 (row 10, pods without a digit, stays zero)
+  // per digit r, the real nodes with suffix digit r (padding: code 15), for the class rows below
   unsigned long long em[ER_ROWS - 1];
 #pragma unroll
-  for (int r = 0; r < ER_ROWS - 1; ++r) em[r] = __ballot(code == (uint32_t)r);  // padding: code 15
-  if (lane < 2 * ER_ROWS) {
-    const int r = lane >> 1, half = lane & 1;
-    unsigned long long m = 0;
-#pragma unroll
-    for (int q = 0; q < ER_ROWS - 1; ++q) m = (r == q) ? em[q] : m;
-    const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
-    const uint32_t g = word / PLANE_GW, c = (word / 4) & 1u, k = word & 3u;
-    erows[(size_t)g * ER_GD + (c * ER_ROWS + (uint32_t)r) * 4 + k] = (uint32_t)(m >> (32 * half));
-  } else if (lane < 2 * ER_ROWS + 2) {  // lanes 22, 23: the X words behind the rows
-    const int half = lane & 1;
-    const uint32_t word = ((uint32_t)(i - lane) >> 5) + (uint32_t)half;
-    erows[(size_t)(word / PLANE_GW) * ER_GD + ER_Q * 4 + word % PLANE_GW] = (uint32_t)(pm[PLANE_X] >> (32 * half));
-  }
+  for (int r = 0; r < ER_ROWS - 1; ++r) em[r] = __ballot(code == (uint32_t)r);
   // the class rows of the same two words (HR_* layout): lanes 0..43 write H[t][r] (row 10 zero),
   // lanes 44..47 F[t]
   {
@@ -212,12 +204,6 @@ __device__ __forceinline__ void decode_pod(int64_t im, int64_t ix, int64_t ia, b
 __device__ __forceinline__ int32_t shard_key(int64_t node_base, uint32_t local_idx) {
   return GKEY_MAX - (int32_t)(node_base + (int64_t)local_idx);
 }
-__device__ __forceinline__ void write_class_keys(const BatchArgs& a) {
-  if (blockIdx.x == 0 && threadIdx.x < 2) {
-    const uint32_t b = a.ball[threadIdx.x];
-    a.keys[(size_t)a.n_pods + threadIdx.x] = b ? shard_key(a.node_base, KMAX - b) : 0;
-  }
-}
 
 // decode_pod for the identity-like modes (NONE, DEFAULT: everything that does not need the
 // first feasible non-match), as selects on launch-constant flags instead of a branch per mode.
@@ -249,32 +235,6 @@ __device__ __forceinline__ int64_t key_to_idx(uint32_t k) {
   return k ? (int64_t)(KMAX - k) : (int64_t)-1;
 }
 
-// ---------------------------------------------------------------------------------------
-// Bit-sliced batched kernel: stages 1-4 for every normalize mode (the default batch path).
-//
-// "Lanes = pods": lane l of the workgroup's waves holds pod 64 b + l. The node table is the
-// bit-sliced PLANE_* layout (msh_internal.h): one 32-bit word per plane covers 32 nodes, and the
-// planes of a word are wave-uniform, so they arrive by scalar loads and sit in SGPRs. Per lane
-// and word, with the pod's code bits as all-ones / all-zero masks P0..P3 and nT = ~tolerates:
-//   miss = (X & nT) | (D0 ^ P0) | (D1 ^ P1) | (D2 ^ P2) | (D3 ^ P3)      1 v_and + 4 v_bitop3
-// has a zero bit exactly at each node that passes NodeUnschedulable for this pod AND whose suffix
-// digit equals the pod's (NodeNumber.Score = 10): 32 (pod, node) pairs evaluated per lane-op
-// chain, 5 VALU per 32 x 64 pairs. Padding slots carry code 15, pods without a digit code 14: they
-// never match. Pairs of words AND into a per-group accumulator (v_bitop3, 3 inputs); a group of
-// PLANE_GW words with a zero bit is remembered (groups are walked in DESCENDING List order, so the
-// last one remembered is the first); the exact node is the first word of that group with a zero
-// bit, then its lowest zero bit (see below for where the words come from). No
-// cross-lane reduction at all: the first maximum of selectHost (minisched.go:304-325) falls out of
-// the List order of words and bits.
-//
-// KX (REVERSE / MINMAX normalizers) also needs the first feasible NON-match:
-//   nmiss = ~dm | (X & nT) | ~V,  dm = (D0 ^ P0) | ... | (D3 ^ P3)
-// (8 VALU per word). The first feasible node of the pod's class comes from the prep (ball).
-//
-// S slice waves per workgroup split the groups of the table for the same 64 pods (small batches
-// against large tables keep the chip busy); their firsts meet in LDS (slices ascend in List
-// order, so the minimum is the first).
-// ---------------------------------------------------------------------------------------
 // t | (d ^ p) in one v_bitop3_b32 (truth table over S0 = t, S1 = d, S2 = p), d wave-uniform.
 // Written as asm: the backend prefers v_xor + v_or3 pairs, 7.75 VALU per word instead of 5.
 __device__ __forceinline__ uint32_t or_xor_s(uint32_t t, uint32_t d, uint32_t p) {
@@ -302,7 +262,7 @@ typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 // flight, then ONE s_waitcnt that takes the loaded registers as operands, so that no use of them
 // can be scheduled in front of it (the backend does not count asm-issued scalar loads).
 template <int NPL>
-__device__ __forceinline__ void sload_group(u32x8 (&pl)[NPL], const uint32_t* src) {
+__device__ __forceinline__ void sload_group(u32x8* pl, const uint32_t* src) {
 #pragma unroll
   for (int k = 0; k < NPL; ++k)
     asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(pl[k]) : "s"(src), "n"(k * PLANE_GW * 4));
@@ -359,141 +319,7 @@ __device__ __forceinline__ uint32_t kept_first(const uint32_t (&k)[PLANE_GW], ui
   return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
 }
 
-// The lowest group of a slice is scanned last (groups descend) and its miss words are still in
-// registers: a lane whose first hit lies there (nearly every lane: a 256-node group almost always
-// holds a feasible node of each digit) reads it off them (kept_first). Only a lane whose first hit
-// lies in a higher group re-reads that group's planes (group_first, vector loads), behind an
-// exec-mask branch the wave skips when no lane needs it. The groups above the lowest only track
-// the first group with a hit: 5 VALU per word, the pair ANDs and one select per group.
-template <int S, bool KX, bool SHARD>
-__global__ __launch_bounds__(S * WAVE) void bits_kernel(BatchArgs a) {
-  __shared__ uint32_t s_res[S][KX ? 2 : 1][WAVE];
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int32_t j = (int32_t)blockIdx.x * WAVE + lane;
-  const bool act = j < a.n_pods;
-  uint32_t code = CODE_NONE_POD, tol = 0;
-  if (act) {
-    const int d = a.pod_digit[j];
-    code = (d >= 0 && d <= 9) ? (uint32_t)d : CODE_NONE_POD;
-    tol = a.pod_tol[j] ? 1u : 0u;
-  }
-  const uint32_t P0 = 0u - (code & 1u), P1 = 0u - ((code >> 1) & 1u), P2 = 0u - ((code >> 2) & 1u),
-                 P3 = 0u - (code >> 3);
-  const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
-  const int32_t g_lo = min(s * a.gps, a.n_groups), g_hi = min(g_lo + a.gps, a.n_groups);
-  constexpr int NPL = KX ? PLANE_N : PLANE_V;  // planes the scan reads
-  // One group: the miss words (gm; KX: gx, the non-match miss words) and whether any has a zero bit.
-  auto scan_group = [&](int32_t g, uint32_t (&gm)[PLANE_GW], uint32_t (&gx)[PLANE_GW], bool& hm, bool& hx) {
-    // the group's planes, wave-uniform: one s_load_dwordx8 per plane, all in flight together,
-    // one wait (left to itself the backend interleaves single-dword scalar loads with the
-    // bitop3 chain, one lgkmcnt wait every few instructions)
-    u32x8 pl[NPL];
-    sload_group<NPL>(pl, a.planes + (size_t)g * GROUP_DWORDS);
-    uint32_t pg[NPL * PLANE_GW];
-#pragma unroll
-    for (int k = 0; k < NPL; ++k)
-#pragma unroll
-      for (int c = 0; c < PLANE_GW; ++c) pg[k * PLANE_GW + c] = pl[k][c];
-    uint32_t am = 0xFFFFFFFFu, ax = 0xFFFFFFFFu;
-#pragma unroll
-    for (int w = 0; w < PLANE_GW; w += 2) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = w + q;
-        const uint32_t xi = and_s(pg[PLANE_X * PLANE_GW + c], nT);
-        if constexpr (KX) {
-          uint32_t dm = pg[c] ^ P0;
-          dm = or_xor_s(dm, pg[PLANE_GW + c], P1);
-          dm = or_xor_s(dm, pg[2 * PLANE_GW + c], P2);
-          dm = or_xor_s(dm, pg[3 * PLANE_GW + c], P3);
-          gm[c] = dm | xi;
-          gx[c] = nmiss_s(dm, xi, pg[PLANE_V * PLANE_GW + c]);
-        } else {
-          uint32_t t = or_xor_s(xi, pg[c], P0);
-          t = or_xor_s(t, pg[PLANE_GW + c], P1);
-          t = or_xor_s(t, pg[2 * PLANE_GW + c], P2);
-          gm[c] = or_xor_s(t, pg[3 * PLANE_GW + c], P3);
-        }
-      }
-      am &= gm[w] & gm[w + 1];
-      if constexpr (KX) ax &= gx[w] & gx[w + 1];
-    }
-    hm = am != 0xFFFFFFFFu;
-    hx = KX && ax != 0xFFFFFFFFu;
-  };
-  uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group above the lowest with a feasible match / non-match
-  uint32_t gm[PLANE_GW], gx[PLANE_GW];
-  bool hm = false, hx = false;
-  for (int32_t g = g_hi - 1; g > g_lo; --g) {
-    scan_group(g, gm, gx, hm, hx);
-    fm = hm ? (uint32_t)g : fm;
-    if constexpr (KX) fx = hx ? (uint32_t)g : fx;
-  }
-  uint32_t rm = NOFIT, rx = NOFIT;  // node index of the first feasible match / non-match
-  if (g_lo < g_hi) {
-    scan_group(g_lo, gm, gx, hm, hx);
-    if (hm) rm = kept_first(gm, (uint32_t)g_lo);
-    if (KX && hx) rx = kept_first(gx, (uint32_t)g_lo);
-    if (!hm && fm != NO_GROUP) rm = group_first<false>(a.planes, fm, P0, P1, P2, P3, nT);
-    if (KX && !hx && fx != NO_GROUP) rx = group_first<true>(a.planes, fx, P0, P1, P2, P3, nT);
-  }
-  if constexpr (S > 1) {
-    s_res[s][0][lane] = rm;
-    if constexpr (KX) s_res[s][1][lane] = rx;
-    __syncthreads();
-    if (s != 0) return;
-#pragma unroll
-    for (int k = 1; k < S; ++k) {
-      rm = umin(rm, s_res[k][0][lane]);
-      if constexpr (KX) rx = umin(rx, s_res[k][1][lane]);
-    }
-  }
-  // after the scan: a store in front of it would keep the backend from proving the planes
-  // unclobbered, and the scalar loads would become vector loads
-  if (SHARD && !KX) write_class_keys(a);
-  if (!act) return;
-  if constexpr (SHARD) {
-    a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
-    if constexpr (KX) a.keys[(size_t)a.n_pods + j] = rx != NOFIT ? shard_key(a.node_base, rx) : 0;
-  } else {
-    const int64_t ia = key_to_idx(a.ball[tol]);
-    const int64_t im = rm != NOFIT ? (int64_t)rm : -1;
-    int32_t oi, ost;
-    int64_t osc;
-    if constexpr (KX)
-      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
-    else
-      decode_ident(im, ia, code != CODE_NONE_POD, make_ident_decode(a.pp), &oi, &osc, &ost);
-    a.out_idx[j] = oi;
-    if (a.out_score) a.out_score[j] = osc;  // optional output (NULL: not written)
-    a.out_status[j] = ost;
-  }
-}
 
-// ---------------------------------------------------------------------------------------
-// Digit-row batched kernel: stages 1-4 for every normalize mode, the default batch path.
-//
-// Lanes = pods as in bits_kernel, but the node side is the digit-row bitmap index (ER_* layout,
-// msh_internal.h): for a word of 32 nodes, row r holds the nodes whose suffix digit is r, so a pod
-// reads the ONE row of its own digit instead of combining four code planes. Per lane and word:
-//   hit = E[row] & ~(X & nT)          one v_bitop3_b32
-// is set exactly at the nodes that pass NodeUnschedulable for this pod AND score 10 for it
-// (NodeNumber.Score, digit equal): 32 (pod, node) pairs per lane-op. The KX modes (REVERSE,
-// MINMAX) also need the first feasible non-match, nm = V & ~E[row] & ~(X & nT), two more VALU.
-// Each wave stages its slice's rows and X words in LDS tiles of ER_TG groups (16-byte copies,
-// wave-private, no barrier; KX: the V words too, from the code planes), and per group a lane reads
-// its row of each 4-word chunk with one ds_read_b128 (lanes of one digit share the address and
-// broadcast; the 11 rows of a chunk occupy distinct banks) and the group's X words at one address.
-// The group's hits are ORed (v_or3) and a group with one is remembered; groups are walked in
-// DESCENDING List order, so the last remembered is the first, and the lowest group of the slice,
-// scanned last, keeps its hit words in registers for the exact node (first word with a hit, its
-// lowest set bit). A lane whose first hit lies in a higher group re-reads that group from memory
-// behind an exec-mask branch (rare: 256 nodes almost always hold a match). ~2 VALU and two
-// ds_read_b128 per 32 x 64 pairs (bits_kernel: 5.75 VALU); at C3 the launches are bound by VALU
-// issue with the LDS array about half busy. Slices and the LDS merge of their
-// firsts as in bits_kernel.
-// ---------------------------------------------------------------------------------------
 
 // The first node among 8 hit words of group g (words ascend in List order, bits within a word):
 // v_ffbl_b32 gives each word's lowest set bit, all-ones for an empty word, which ORed with the
@@ -512,36 +338,191 @@ __device__ __forceinline__ uint32_t hits_first(const uint32_t (&h)[PLANE_GW], ui
   return g * GROUP_NODES + m;
 }
 
-// The lane's first feasible match in group g, from memory (its row words and the X plane).
-__device__ __forceinline__ uint32_t rows_group_first(const BatchArgs& a, uint32_t g, uint32_t row, uint32_t nT) {
-  const uint4* er = reinterpret_cast<const uint4*>(a.erows) + (size_t)g * ER_GQ;
-  const uint4 e0 = er[row], e1 = er[ER_ROWS + row], x0 = er[ER_Q], x1 = er[ER_Q + 1];
-  const uint32_t e[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-  const uint32_t x[PLANE_GW] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-  uint32_t h[PLANE_GW];
-#pragma unroll
-  for (int k = 0; k < PLANE_GW; ++k) h[k] = e[k] & ~(x[k] & nT);
-  return hits_first(h, g);
+// ---------------------------------------------------------------------------------------
+// Per-pair batch kernel: the default batch path (msh_schedule_batch*, msh_schedule_batches_device,
+// msh_shard_keys_device) for the reference's plugins, in every normalize mode.
+//
+// EVERY (pod, node) pair is evaluated, from the node's own bits and the pod's own bits; no table
+// indexed by a pod's class (its digit or tolerates bit) is read. "Lanes = pods": lane l of a wave
+// holds one pod; the node table is bit-sliced (msh_internal.h PLANE_*: node i is bit i mod 32 of word
+// i / 32), and a group's planes are wave-uniform, so they arrive by scalar loads into SGPRs. Per lane
+// and word (32 nodes), with the pod's NodeNumber code bits as all-ones / all-zero masks P0..P3 and
+// nT = all-ones unless the pod tolerates the unschedulable taint:
+//   xi  = X & nT                                  NodeUnschedulable.Filter rejects the pair
+//   dm' = xi | (D0 ^ P0) | (D1 ^ P1) | (D2 ^ P2) | (D3 ^ P3)
+//         zero exactly at the feasible pairs whose NodeNumber.Score is 10 (suffix digits equal; node
+//         code 15 = no digit or padding and pod code 14 = no digit never match)
+//   nm  = dm' & ~xi (& V in a group holding padding)   the feasible pairs whose score is 0
+// v_and + 4 v_bitop3 for dm', then the group accumulators am = AND of the dm' words (one v_bitop3
+// AND3 per two words) and ax |= nm (one v_bitop3 per word): 6.5 VALU per 32 x 64 pairs.
+// Stages 2-4 on NodeNumber's two-valued raw score: every total is weight x NormalizeScore(raw) of 0
+// or 10, so selectHost's first maximum is the first feasible pair of the better level. A pod
+// therefore needs its first feasible match (im) and its first feasible non-match (ix); its first
+// feasible node is min(im, ix); decode_pod turns them into the status, the node and the int64 score
+// for the plugin list and normalize mode (minisched.go:50-87, 143-148, 164-199, 304-325).
+// Groups are walked in DESCENDING List order and a group with a hit is remembered (the last one
+// remembered is the first); the lowest group of the wave's range keeps its words in registers for
+// the exact node (v_ffbl of each word); a lane whose first hit lies in a higher group re-reads that
+// group (vector loads behind an exec-masked branch: rare, a 256-node group nearly always holds a
+// feasible node of each digit). S slice waves share a 64-pod block when a launch has few pods for
+// the chip: each scans a contiguous range of groups, and their firsts meet by min in LDS (slices
+// ascend in List order). The grid is (workgroup blocks x batches): blockIdx.y = the batch of a
+// multi-batch launch, its descriptor read by scalar loads.
+// ---------------------------------------------------------------------------------------
+constexpr int PAIR_WAVES = 4;  // waves per workgroup
+
+__device__ __forceinline__ uint32_t bop3_andn(uint32_t a, uint32_t b) {  // a & ~b
+  return __builtin_amdgcn_bitop3_b32(a, b, b, 0x30);
+}
+__device__ __forceinline__ uint32_t bop3_and3(uint32_t a, uint32_t b, uint32_t c) {  // a & b & c
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x80);
+}
+__device__ __forceinline__ uint32_t bop3_or_andn(uint32_t acc, uint32_t a, uint32_t b) {  // acc | (a & ~b)
+  return __builtin_amdgcn_bitop3_b32(acc, a, b, 0xf4);
+}
+__device__ __forceinline__ uint32_t bop3_andn_and(uint32_t a, uint32_t b, uint32_t v) {  // a & ~b & v
+  return __builtin_amdgcn_bitop3_b32(a, b, v, 0x20);
 }
 
-// e & ~(x & m) in one v_bitop3_b32, all three in VGPRs (x: the same in every lane)
-__device__ __forceinline__ uint32_t hit_v(uint32_t e, uint32_t x, uint32_t m) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x70" : "=v"(r) : "v"(e), "v"(x), "v"(m));
-  return r;
+// t | (d ^ p), d the node plane (SGPR), p the pod's mask. The builtin, not inline asm: the backend
+// then knows the instruction's hazards (after inline asm it inserts an s_nop every other VALU).
+__device__ __forceinline__ uint32_t bop3_or_xor(uint32_t t, uint32_t d, uint32_t p) {
+  return __builtin_amdgcn_bitop3_b32(t, d, p, 0xf6);
 }
 
-// One group's hits: the lane's row words of both chunks and the group's X words (four
-// ds_read_b128 of the staged tile, the X reads at one address for all lanes); returns whether any
-// word has a hit.
-__device__ __forceinline__ bool rows_hits(const uint4& e0, const uint4& e1, const uint4& x0, const uint4& x1,
-                                          uint32_t nT, uint32_t (&h)[PLANE_GW]) {
-  const uint32_t e[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-  const uint32_t x[PLANE_GW] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-  for (int k = 0; k < PLANE_GW; ++k) h[k] = hit_v(e[k], x[k], nT);
-  return ((h[0] | h[1] | h[2]) | (h[3] | h[4] | h[5]) | (h[6] | h[7])) != 0u;
+// dm' of word w of a group's planes (SGPRs) for one lane; xi out
+__device__ __forceinline__ uint32_t pair_miss(const u32x8 (&pl)[PLANE_N], int w, uint32_t P0, uint32_t P1,
+                                              uint32_t P2, uint32_t P3, uint32_t nT, uint32_t& xi) {
+  xi = __builtin_amdgcn_bitop3_b32(pl[PLANE_X][w], nT, nT, 0xc0);  // X & nT
+  uint32_t t = bop3_or_xor(xi, pl[0][w], P0);
+  t = bop3_or_xor(t, pl[1][w], P1);
+  t = bop3_or_xor(t, pl[2][w], P2);
+  return bop3_or_xor(t, pl[3][w], P3);
 }
+
+// One group above the lowest of the range: whether it holds a feasible match (hm) / non-match (hx).
+template <bool PAD>
+__device__ __forceinline__ void pair_group(const u32x8 (&pl)[PLANE_N], uint32_t P0, uint32_t P1, uint32_t P2,
+                                           uint32_t P3, uint32_t nT, bool& hm, bool& hx) {
+  uint32_t am = 0xFFFFFFFFu, ax = 0u;
+#pragma unroll
+  for (int w = 0; w < PLANE_GW; w += 2) {
+    uint32_t x0, x1;
+    const uint32_t t0 = pair_miss(pl, w, P0, P1, P2, P3, nT, x0);
+    const uint32_t t1 = pair_miss(pl, w + 1, P0, P1, P2, P3, nT, x1);
+    am = bop3_and3(am, t0, t1);
+    if constexpr (PAD) {
+      ax |= bop3_andn_and(t0, x0, pl[PLANE_V][w]);
+      ax |= bop3_andn_and(t1, x1, pl[PLANE_V][w + 1]);
+    } else {
+      ax = bop3_or_andn(ax, t0, x0);
+      ax = bop3_or_andn(ax, t1, x1);
+    }
+  }
+  hm = am != 0xFFFFFFFFu;
+  hx = ax != 0u;
+}
+
+// The lowest group of the range: its dm' words (km) and feasible non-match words (kx) kept.
+template <bool PAD>
+__device__ __forceinline__ void pair_group_keep(const u32x8 (&pl)[PLANE_N], uint32_t P0, uint32_t P1, uint32_t P2,
+                                                uint32_t P3, uint32_t nT, uint32_t (&km)[PLANE_GW],
+                                                uint32_t (&kx)[PLANE_GW]) {
+#pragma unroll
+  for (int w = 0; w < PLANE_GW; ++w) {
+    uint32_t xi;
+    km[w] = pair_miss(pl, w, P0, P1, P2, P3, nT, xi);
+    kx[w] = PAD ? bop3_andn_and(km[w], xi, pl[PLANE_V][w]) : bop3_andn(km[w], xi);
+  }
+}
+
+template <int S, bool SHARD>
+__global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
+  constexpr int PB = PAIR_WAVES / S;  // 64-pod blocks per workgroup
+  __shared__ uint32_t s_res[S > 1 ? PAIR_WAVES : 1][2][WAVE];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int sl = wv % S, pb = wv / S;
+  const BatchDesc& d = a.d[blockIdx.y];
+  const int32_t np = d.n_pods;
+  if ((int32_t)blockIdx.x * PB * WAVE >= np) return;  // the whole workgroup lies past its batch's end
+  const int32_t wbase = ((int32_t)blockIdx.x * PB + pb) * WAVE;
+  const int32_t j = wbase + lane;
+  const bool act = j < np;
+  uint32_t code = CODE_NONE_POD, tol = 0u;
+  if (act) {
+    const int dq = d.pod_digit[j];
+    code = (dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;  // NodeNumber.PreScore: Atoi of the last byte
+    tol = d.pod_tol[j] ? 1u : 0u;
+  }
+  const uint32_t P0 = 0u - (code & 1u), P1 = 0u - ((code >> 1) & 1u), P2 = 0u - ((code >> 2) & 1u),
+                 P3 = 0u - (code >> 3);
+  const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
+  const bool live = wbase < np;  // wave-uniform: this wave's block holds pods
+  const int32_t g_lo = min(sl * a.gps, a.n_groups);
+  const int32_t g_hi = live ? min(g_lo + a.gps, a.n_groups) : g_lo;
+  const int32_t g_full = a.g_full;  // groups below it hold no padding slot
+  uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group above g_lo with a feasible match / non-match
+  for (int32_t g = g_hi - 1; g > g_lo; --g) {
+    u32x8 pl[PLANE_N];
+    bool hm, hx;
+    if (g < g_full) {
+      sload_group<PLANE_V>(pl, a.planes + (size_t)g * GROUP_DWORDS);
+      pair_group<false>(pl, P0, P1, P2, P3, nT, hm, hx);
+    } else {
+      sload_group<PLANE_N>(pl, a.planes + (size_t)g * GROUP_DWORDS);
+      pair_group<true>(pl, P0, P1, P2, P3, nT, hm, hx);
+    }
+    fm = hm ? (uint32_t)g : fm;
+    fx = hx ? (uint32_t)g : fx;
+  }
+  uint32_t rm = NOFIT, rx = NOFIT;  // node index of the first feasible match / non-match
+  if (g_lo < g_hi) {
+    uint32_t km[PLANE_GW], kx[PLANE_GW];
+    u32x8 pl[PLANE_N];
+    sload_group<PLANE_N>(pl, a.planes + (size_t)g_lo * GROUP_DWORDS);
+    if (g_lo < g_full) pair_group_keep<false>(pl, P0, P1, P2, P3, nT, km, kx);
+    else pair_group_keep<true>(pl, P0, P1, P2, P3, nT, km, kx);
+    const uint32_t am = bop3_and3(bop3_and3(km[0], km[1], km[2]), bop3_and3(km[3], km[4], km[5]), km[6] & km[7]);
+    const uint32_t ax = (kx[0] | kx[1] | kx[2]) | (kx[3] | kx[4] | kx[5]) | (kx[6] | kx[7]);
+    if (am != 0xFFFFFFFFu) {
+      uint32_t h[PLANE_GW];
+#pragma unroll
+      for (int w = 0; w < PLANE_GW; ++w) h[w] = ~km[w];
+      rm = hits_first(h, (uint32_t)g_lo);
+    } else if (fm != NO_GROUP) {
+      rm = group_first<false>(a.planes, fm, P0, P1, P2, P3, nT);
+    }
+    if (ax != 0u) rx = hits_first(kx, (uint32_t)g_lo);
+    else if (fx != NO_GROUP) rx = group_first<true>(a.planes, fx, P0, P1, P2, P3, nT);
+  }
+  if constexpr (S > 1) {
+    s_res[wv][0][lane] = rm;
+    s_res[wv][1][lane] = rx;
+    __syncthreads();
+    if (sl != 0) return;
+#pragma unroll
+    for (int k = 1; k < S; ++k) {
+      rm = umin(rm, s_res[wv + k][0][lane]);
+      rx = umin(rx, s_res[wv + k][1][lane]);
+    }
+  }
+  if (!act) return;
+  if constexpr (SHARD) {  // per-pod keys: the element-wise MAX over node shards is the global first
+    a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
+    a.keys[(size_t)np + j] = rx != NOFIT ? shard_key(a.node_base, rx) : 0;
+  } else {
+    const uint32_t ra = umin(rm, rx);
+    int32_t oi, ost;
+    int64_t osc;
+    decode_pod(rm != NOFIT ? (int64_t)rm : -1, rx != NOFIT ? (int64_t)rx : -1, ra != NOFIT ? (int64_t)ra : -1,
+               code != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
+    d.out_idx[j] = oi;
+    if (d.out_score) d.out_score[j] = osc;  // optional output (NULL: not written)
+    d.out_status[j] = ost;
+  }
+}
+
 
 #if defined(MSH_STAMPS) || defined(MSH_CLOCK_STAMPS)
 // Timeline / clock A/B builds only (scripts/stamps.sh, scripts/ab_build.sh; never in
@@ -556,262 +537,7 @@ __device__ unsigned long long* g_stamps;
 #define MSH_STAMP(i) ((void)0)
 #endif
 
-// One group's feasible non-matches (KX modes): nm = V & ~E & ~(X & nT), two VALU per word
-// (xm = X & nT, then one v_bitop3 with truth table 0x10 = S0 & ~S1 & ~S2).
-__device__ __forceinline__ uint32_t nonmatch_v(uint32_t v, uint32_t e, uint32_t xm) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x10" : "=v"(r) : "v"(v), "v"(e), "v"(xm));
-  return r;
-}
-__device__ __forceinline__ bool rows_nonmatch(const uint4& e0, const uint4& e1, const uint4& x0, const uint4& x1,
-                                              const uint4& v0, const uint4& v1, uint32_t nT,
-                                              uint32_t (&n)[PLANE_GW]) {
-  const uint32_t e[PLANE_GW] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-  const uint32_t x[PLANE_GW] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-  const uint32_t v[PLANE_GW] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-  for (int k = 0; k < PLANE_GW; ++k) n[k] = nonmatch_v(v[k], e[k], x[k] & nT);
-  return ((n[0] | n[1] | n[2]) | (n[3] | n[4] | n[5]) | (n[6] | n[7])) != 0u;
-}
-// The lane's first feasible non-match in group g, from memory (rare path of the KX modes): the
-// rows and X from the digit rows, V from the code planes.
-__device__ __forceinline__ uint32_t rows_group_first_nm(const BatchArgs& a, uint32_t g, uint32_t row, uint32_t nT) {
-  const uint4* er = reinterpret_cast<const uint4*>(a.erows) + (size_t)g * ER_GQ;
-  const uint4* vp = reinterpret_cast<const uint4*>(a.planes + (size_t)g * GROUP_DWORDS + PLANE_V * PLANE_GW);
-  uint32_t n[PLANE_GW];
-  rows_nonmatch(er[row], er[ER_ROWS + row], er[ER_Q], er[ER_Q + 1], vp[0], vp[1], nT, n);
-  return hits_first(n, g);
-}
 
-template <int S, bool KX, bool SHARD, int PPL>
-__global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
-#ifdef MSH_STAMPS
-  unsigned long long stamp_t[4] = {0, 0, 0, 0};
-  MSH_STAMP(0);
-  auto stamps_out = [&]() {
-    if ((threadIdx.x & (WAVE - 1)) == 0)
-      for (int i = 0; i < 4; ++i) g_stamps[((size_t)blockIdx.x * S + (threadIdx.x >> 6)) * 4 + i] = stamp_t[i];
-  };
-#endif
-  constexpr int NR = KX ? 2 : 1;  // results per pod: first feasible match (+ first feasible non-match)
-  __shared__ uint4 s_tile[S][ER_TG * ER_GQ];
-  __shared__ uint4 s_vw[KX ? S : 1][KX ? 2 * ER_TG : 1];  // KX: the tile's V words (from the code planes)
-  __shared__ uint32_t s_res[S][NR][PPL][WAVE];
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  // PPL pods per lane: lane l holds pods base + q * 64 + l (q < PPL); the group's X words and the
-  // staged row tile serve all of them
-  const int32_t block0 = (int32_t)blockIdx.x * (PPL * WAVE);
-  const int32_t base = block0 + lane;
-  const int32_t g_lo = min(s * a.gps, a.n_groups), g_hi = min(g_lo + a.gps, a.n_groups);
-  const int32_t ng = g_hi - g_lo;
-  const uint4* __restrict__ er = reinterpret_cast<const uint4*>(a.erows);
-  uint4* tile = s_tile[s];
-  // This wave's tile, read only by this wave: a whole ER_TG-group tile is copied, three 16-byte
-  // copies per lane (the table carries padding, so no copy needs a clamp; rows past the slice are
-  // never read), and in the KX modes the tile's V words from the code planes (16 lanes, one group
-  // half each, clamped to the table). Loads and stores are separate so that the prologue can put
-  // the pod-byte loads between them.
-  static_assert(ER_TG * ER_GQ == 3 * WAVE, "fill: three 16-byte copies per lane");
-  uint4 f0, f1, f2, fv;
-  uint4* vtile = s_vw[KX ? s : 0];
-  auto fill_load = [&](int32_t t_lo) {
-    const uint4* src = er + (uint32_t)(t_lo * ER_GQ);  // wave-uniform base, 32-bit lane offsets
-    f0 = src[(uint32_t)lane];
-    f1 = src[(uint32_t)(lane + WAVE)];
-    f2 = src[(uint32_t)(lane + 2 * WAVE)];
-    if constexpr (KX) {
-      const int32_t gv = min(t_lo + (lane >> 1) % ER_TG, a.n_groups - 1);
-      fv = reinterpret_cast<const uint4*>(a.planes + (size_t)gv * GROUP_DWORDS + PLANE_V * PLANE_GW)[lane & 1];
-    }
-  };
-  auto fill_store = [&]() {
-    tile[lane] = f0;
-    tile[lane + WAVE] = f1;
-    tile[lane + 2 * WAVE] = f2;
-    if (KX && lane < 2 * ER_TG) vtile[lane] = fv;
-    __builtin_amdgcn_wave_barrier();
-  };
-  // Prologue: the top tile's row words, the pod bytes (clamped offset: no branch, so nothing waits
-  // for them yet) and the class firsts are all requested before the first use of any of them.
-  const int32_t t_top = ng > 0 ? (ng - 1) / ER_TG : -1;
-  fill_load(g_lo + max(t_top, 0) * ER_TG);  // (an empty slice copies a padding tile it never reads)
-  int dq[PPL];
-  uint8_t tq[PPL];
-  const uint32_t last = (uint32_t)(a.n_pods - 1 - block0);  // n_pods > block0 (empty batches never launch)
-  const int8_t* pdb = a.pod_digit + block0;                   // wave-uniform bases, 32-bit lane offsets
-  const uint8_t* ptb = a.pod_tol + block0;
-#pragma unroll
-  for (int q = 0; q < PPL; ++q) {
-    const uint32_t off = min((uint32_t)(lane + q * WAVE), last);
-    dq[q] = pdb[off];
-    tq[q] = ptb[off];
-  }
-  const uint32_t ball0 = a.ball[0], ball1 = a.ball[1];
-  fill_store();
-  bool act[PPL];
-  uint32_t code[PPL], tol[PPL], nT[PPL], row[PPL];
-  const uint4* lrow[PPL];  // the lane's row in chunk 0 of a tile's first group
-#pragma unroll
-  for (int q = 0; q < PPL; ++q) {
-    act[q] = base + q * WAVE < a.n_pods;
-    code[q] = (act[q] && dq[q] >= 0 && dq[q] <= 9) ? (uint32_t)dq[q] : CODE_NONE_POD;
-    tol[q] = (act[q] && tq[q]) ? 1u : 0u;
-    nT[q] = tol[q] ? 0u : 0xFFFFFFFFu;
-    row[q] = code[q] <= 9u ? code[q] : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
-    lrow[q] = tile + row[q];
-  }
-  MSH_STAMP(1);
-  uint32_t h[PPL][PLANE_GW], hn[PPL][PLANE_GW];
-  // first group above the lowest with a feasible match / non-match (NO_GROUP - 1: in h / hn)
-  uint32_t fm[PPL], fx[PPL];
-#pragma unroll
-  for (int q = 0; q < PPL; ++q) fm[q] = fx[q] = NO_GROUP;
-  // One group g of the tile for pod q: hits into hq (and non-matches into nq); returns the flags.
-  auto group = [&](int32_t g, int32_t t_lo, int q, uint32_t (&hq)[PLANE_GW], uint32_t (&nq)[PLANE_GW], bool& am,
-                   bool& ax) {
-    const uint4* tg = tile + (g - t_lo) * ER_GQ;
-    const uint4* r0 = lrow[q] + (g - t_lo) * ER_GQ;
-    const uint4 e0 = r0[0], e1 = r0[ER_ROWS], x0 = tg[ER_Q], x1 = tg[ER_Q + 1];
-    am = rows_hits(e0, e1, x0, x1, nT[q], hq);
-    if constexpr (KX) {
-      const uint4* vg = vtile + 2 * (g - t_lo);
-      ax = rows_nonmatch(e0, e1, x0, x1, vg[0], vg[1], nT[q], nq);
-    }
-  };
-  // Tiles from the top down, each one's groups descending; the lowest group of the slice last.
-  for (int32_t t = t_top; t >= 0; --t) {
-    const int32_t t_lo = g_lo + t * ER_TG, t_hi = min(t_lo + ER_TG, g_hi);
-    if (t != t_top) {
-      fill_load(t_lo);
-      fill_store();
-    }
-    const int32_t g_end = t == 0 ? g_lo + 1 : t_lo;  // tile 0: all but the lowest group
-    int32_t g = t_hi - 1;
-    for (; g - 1 >= g_end; g -= 2) {  // two groups per step
-#pragma unroll
-      for (int q = 0; q < PPL; ++q) {
-        uint32_t h1[PLANE_GW], h2[PLANE_GW], n1[PLANE_GW], n2[PLANE_GW];  // (only the lowest group's are kept)
-        bool m1, m2, x1 = false, x2 = false;
-        group(g, t_lo, q, h1, n1, m1, x1);
-        group(g - 1, t_lo, q, h2, n2, m2, x2);
-        fm[q] = m1 ? (uint32_t)g : fm[q];
-        fm[q] = m2 ? (uint32_t)(g - 1) : fm[q];
-        if constexpr (KX) {
-          fx[q] = x1 ? (uint32_t)g : fx[q];
-          fx[q] = x2 ? (uint32_t)(g - 1) : fx[q];
-        }
-      }
-    }
-    if (g >= g_end) {
-#pragma unroll
-      for (int q = 0; q < PPL; ++q) {
-        uint32_t h1[PLANE_GW], n1[PLANE_GW];
-        bool m1, x1 = false;
-        group(g, t_lo, q, h1, n1, m1, x1);
-        fm[q] = m1 ? (uint32_t)g : fm[q];
-        if constexpr (KX) fx[q] = x1 ? (uint32_t)g : fx[q];
-      }
-    }
-    if (t == 0) {  // the lowest group: its hit (and non-match) words stay in registers
-#pragma unroll
-      for (int q = 0; q < PPL; ++q) {
-        bool m1, x1 = false;
-        group(g_lo, t_lo, q, h[q], hn[q], m1, x1);
-        fm[q] = m1 ? NO_GROUP - 1 : fm[q];
-        if constexpr (KX) fx[q] = x1 ? NO_GROUP - 1 : fx[q];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  uint32_t rm[PPL], rx[PPL];  // node index of the first feasible match / non-match
-  MSH_STAMP(2);
-#pragma unroll
-  for (int q = 0; q < PPL; ++q) {
-    rm[q] = rx[q] = NOFIT;
-    if (fm[q] == NO_GROUP - 1) rm[q] = hits_first(h[q], (uint32_t)g_lo);
-    else if (fm[q] != NO_GROUP) rm[q] = rows_group_first(a, fm[q], row[q], nT[q]);
-    if constexpr (KX) {
-      if (fx[q] == NO_GROUP - 1) rx[q] = hits_first(hn[q], (uint32_t)g_lo);
-      else if (fx[q] != NO_GROUP) rx[q] = rows_group_first_nm(a, fx[q], row[q], nT[q]);
-    }
-  }
-  if constexpr (S > 1) {
-#pragma unroll
-    for (int q = 0; q < PPL; ++q) {
-      s_res[s][0][q][lane] = rm[q];
-      if constexpr (KX) s_res[s][NR - 1][q][lane] = rx[q];
-    }
-    __syncthreads();
-#ifdef MSH_STAMPS
-    if (s != 0) {
-      stamps_out();
-      return;
-    }
-#else
-    if (s != 0) return;
-#endif
-#pragma unroll
-    for (int k = 1; k < S; ++k)
-#pragma unroll
-      for (int q = 0; q < PPL; ++q) {
-        rm[q] = umin(rm[q], s_res[k][0][q][lane]);
-        if constexpr (KX) rx[q] = umin(rx[q], s_res[k][NR - 1][q][lane]);
-      }
-  }
-  if (SHARD && !KX) write_class_keys(a);
-#ifdef MSH_STAMPS
-  MSH_STAMP(3);
-  stamps_out();
-#endif
-#pragma unroll
-  for (int q = 0; q < PPL; ++q) {
-    if (!act[q]) continue;
-    const int32_t j = base + q * WAVE;
-    if constexpr (SHARD) {
-      a.keys[j] = rm[q] != NOFIT ? shard_key(a.node_base, rm[q]) : 0;
-      if constexpr (KX) a.keys[(size_t)a.n_pods + j] = rx[q] != NOFIT ? shard_key(a.node_base, rx[q]) : 0;
-    } else {
-      int32_t oi, ost;
-      int64_t osc;
-      const int64_t im = rm[q] != NOFIT ? (int64_t)rm[q] : -1, ia = key_to_idx(tol[q] ? ball1 : ball0);
-      if constexpr (KX)
-        decode_pod(im, rx[q] != NOFIT ? (int64_t)rx[q] : -1, ia, code[q] != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
-      else
-        decode_ident(im, ia, code[q] != CODE_NONE_POD, make_ident_decode(a.pp), &oi, &osc, &ost);
-      a.out_idx[j] = oi;
-      if (a.out_score) a.out_score[j] = osc;  // optional output (NULL: not written)
-      a.out_status[j] = ost;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Workgroup-table batched kernel (the default batch path since round 3).
-//
-// Lanes = pods, as in rows_kernel, but the node side is staged ONCE per workgroup: the W waves of a
-// workgroup (W x 64 pods) copy the digit rows and X words (KX: and the V words) of up to WG_CHUNK
-// groups into LDS together, and every wave then scans every group of the table for its own 64 pods.
-// No slices, so no slice merge and no per-wave tile copies. Per lane and 256-node group the scan
-// folds the pair evaluation and the group's OR into one v_bitop3 per 32-node word:
-//   acc = acc | (E[row] & ~X')        truth table 0xF4 (the first word: E & ~X', 0x44)
-// where X' is the group's X words for a pod that does not tolerate the unschedulable taint and a
-// zero block staged next to them for one that does (NodeUnschedulable per pair: a tolerating pod
-// passes every real node); the lane picks its block once, by address. A group whose acc is non-zero
-// holds a feasible digit match: it pushes a 1 into a per-chunk bitmap (bit k = group lo + k; v_min +
-// v_lshl_or per group). 11 VALU per group and lane (8 bitop3, the flag, the addresses) against
-// rows_kernel's 16; KX also accumulates the feasible non-matches, acc' |= V & ~(E | X') (v_or +
-// v_bitop3 per word). Groups are walked in descending List order; the first group with a hit is the
-// lowest set bit of the lowest chunk's bitmap that has one, and its hit words are recomputed once per
-// lane at the end (from LDS, or from memory when it lies in a chunk no longer staged: more than
-// WG_CHUNK groups above the first with a hit, rare). Tables larger than one chunk are streamed chunk
-// by chunk, descending: the next chunk's copy is in flight in registers while the current one is
-// scanned (two workgroup barriers per chunk).
-//
-// MULTI: the launch serves up to MULTI_MAX independent batches (msh_schedule_batches_device), each
-// with its own pod columns and outputs, described in the kernel arguments; the grid is 2-D, batch =
-// blockIdx.y (one scalar load of its descriptor).
-// ---------------------------------------------------------------------------------------
 // Phase experiments of A/B builds only (scripts/wg_expt.sh, scripts/ab_build.sh; never the product
 // library): bit 0 skips the scan loop, bit 1 the output stores, bit 2 the table copy into LDS; bit 4
 // (wgp_kernel's quad scan) adds a second reduction tree per pair of groups. MSH_WG_FLAG
@@ -822,21 +548,6 @@ __global__ __launch_bounds__(S * WAVE) void rows_kernel(BatchArgs a) {
 #ifndef MSH_WG_FLAG
 #define MSH_WG_FLAG 0
 #endif
-constexpr int WG_CHUNK = 32;  // groups per staged chunk (8,192 nodes; 13 KiB, 14 KiB with V words)
-// LDS layout of a staged group, in 16-byte entries: the 22 row chunks, X (2), a zero block Z (2) that
-// tolerating pods read instead of X, and (KX) V (2)
-constexpr int LQ_X = ER_Q, LQ_Z = ER_GQ, LQ_V = ER_GQ + 2;
-
-template <bool MULTI>
-struct KArgs {
-  using T = BatchArgs;
-};
-template <>
-struct KArgs<true> {
-  using T = MultiArgs;
-};
-__device__ __forceinline__ const BatchArgs& base_args(const BatchArgs& a) { return a; }
-__device__ __forceinline__ const BatchArgs& base_args(const MultiArgs& m) { return m.a; }
 
 // acc | (e & ~x), one v_bitop3_b32 (S0 = acc, S1 = e, S2 = x). The builtin, not inline asm: the
 // compiler then knows the instruction's hazards (inline asm got a conservative s_nop after each pair).
@@ -856,215 +567,6 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t sh, uint32_t b)
   return r;
 }
 
-// One staged group for one lane: the OR over its 8 words of the feasible digit matches (hit) and, KX,
-// of the feasible non-matches (nm). tr: the lane's row entry, tx: the lane's X or Z entry, tv: V.
-template <bool KX>
-__device__ __forceinline__ void group_acc(const uint4* tr, const uint4* tx, const uint4* tv, uint32_t& hit,
-                                          uint32_t& nm) {
-  const uint4 e0 = tr[0], e1 = tr[ER_ROWS], x0 = tx[0], x1 = tx[1];
-  hit = andn(e0.x, x0.x);
-  hit = acc_andn(hit, e0.y, x0.y);
-  hit = acc_andn(hit, e0.z, x0.z);
-  hit = acc_andn(hit, e0.w, x0.w);
-  hit = acc_andn(hit, e1.x, x1.x);
-  hit = acc_andn(hit, e1.y, x1.y);
-  hit = acc_andn(hit, e1.z, x1.z);
-  hit = acc_andn(hit, e1.w, x1.w);
-  if constexpr (KX) {
-    const uint4 v0 = tv[0], v1 = tv[1];
-    nm = andn(v0.x, e0.x | x0.x);
-    nm = acc_andn(nm, v0.y, e0.y | x0.y);
-    nm = acc_andn(nm, v0.z, e0.z | x0.z);
-    nm = acc_andn(nm, v0.w, e0.w | x0.w);
-    nm = acc_andn(nm, v1.x, e1.x | x1.x);
-    nm = acc_andn(nm, v1.y, e1.y | x1.y);
-    nm = acc_andn(nm, v1.z, e1.z | x1.z);
-    nm = acc_andn(nm, v1.w, e1.w | x1.w);
-  }
-}
-
-template <int W, bool KX, bool SHARD, bool MULTI>
-__global__ __launch_bounds__(W * WAVE) void wg_kernel(typename KArgs<MULTI>::T ka) {
-  static_assert(!(SHARD && MULTI), "shard keys come from single-batch launches");
-  constexpr int GQ = KX ? ER_GQ + 2 : ER_GQ;                     // 16-byte entries per group in memory
-  constexpr int GQL = KX ? LQ_V + 2 : LQ_Z + 2;                  // ... per staged group in LDS
-  constexpr int NT = W * WAVE;                                   // threads per workgroup
-  constexpr int EPT = (WG_CHUNK * GQ + NT - 1) / NT;             // staged entries per thread per chunk
-  __shared__ uint4 s_tab[WG_CHUNK * GQL];
-#ifdef MSH_STAMPS
-  unsigned long long stamp_t[4] = {0, 0, 0, 0};
-  MSH_STAMP(0);
-#endif
-  const BatchArgs& A = base_args(ka);
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-
-  // ---- this workgroup's batch ----
-  int32_t blk = (int32_t)blockIdx.x;
-  const int8_t* pod_digit = A.pod_digit;
-  const uint8_t* pod_tol = A.pod_tol;
-  int32_t* out_idx = A.out_idx;
-  int64_t* out_score = A.out_score;
-  int32_t* out_status = A.out_status;
-  int32_t n_pods = A.n_pods;
-  if constexpr (MULTI) {
-    const BatchDesc& d = ka.d[blockIdx.y];
-    if (blk * NT >= d.n_pods) return;  // past this batch's end (the grid's x extent is the largest batch's)
-    pod_digit = d.pod_digit;
-    pod_tol = d.pod_tol;
-    out_idx = d.out_idx;
-    out_score = d.out_score;
-    out_status = d.out_status;
-    n_pods = d.n_pods;
-  }
-  const int32_t wbase = blk * NT + wv * WAVE;  // this wave's first pod (may lie past the batch)
-  const int32_t j = wbase + lane;
-
-  // ---- staging: chunk c = groups [c * WG_CHUNK, min(+WG_CHUNK, n_groups)) ----
-  const int32_t n_groups = A.n_groups;
-  const int32_t n_chunks = (n_groups + WG_CHUNK - 1) / WG_CHUNK;  // >= 1 (tables are never empty)
-  const uint4* __restrict__ er = reinterpret_cast<const uint4*>(A.erows);
-  // Every thread loads EPT (<= 4) entries unconditionally (indices past the chunk clamped to its
-  // last entry: no divergent branch around a load, so the copies stay in flight) and stores every
-  // slot of the staging array it owns (slots past the chunk are never read). Four named registers,
-  // not an array: an array of uint4 captured by the lambdas went to scratch.
-  static_assert(EPT <= 4, "wg_kernel stages at most four 16-byte entries per thread and chunk");
-  uint4 st0, st1, st2, st3;
-  auto st_ref = [&](int k) -> uint4& { return k == 0 ? st0 : k == 1 ? st1 : k == 2 ? st2 : st3; };
-  auto chunk_load = [&](int32_t c) {
-    if constexpr ((MSH_WG_EXPT & 4) != 0) return;
-    const int32_t glo = c * WG_CHUNK, last = min(WG_CHUNK, n_groups - glo) * GQ - 1;
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      const int32_t i = min((int32_t)threadIdx.x + k * NT, last);
-      if constexpr (KX) {
-        const int32_t gi = i / GQ, q = i - gi * GQ;
-        const uint4* src = q < ER_GQ ? er + (size_t)(glo + gi) * ER_GQ + q
-                                     : reinterpret_cast<const uint4*>(A.planes + (size_t)(glo + gi) * GROUP_DWORDS +
-                                                                      PLANE_V * PLANE_GW) + (q - ER_GQ);
-        st_ref(k) = *src;
-      } else {
-        st_ref(k) = er[(size_t)glo * ER_GQ + i];
-      }
-    }
-  };
-  auto chunk_store = [&]() {  // memory entry i of group gi -> LDS entry gi * GQL + q (V past Z)
-    if constexpr ((MSH_WG_EXPT & 4) != 0) return;
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      const int32_t i = (int32_t)threadIdx.x + k * NT;
-      const int32_t gi = i / GQ, q = i - gi * GQ;
-      if ((k + 1) * NT <= WG_CHUNK * GQ || i < WG_CHUNK * GQ) s_tab[gi * GQL + q + (q >= ER_GQ ? 2 : 0)] = st_ref(k);
-    }
-  };
-
-  // ---- prologue: the top chunk's copy, the pod bytes (clamped offset) and the class firsts in
-  // flight together; the zero blocks written once ----
-  chunk_load(n_chunks - 1);
-  const uint32_t lastp = n_pods > 0 ? (uint32_t)(n_pods - 1) : 0u;
-  const uint32_t jj = min((uint32_t)j, lastp);
-  const int dq = pod_digit[jj];
-  const uint8_t tq = pod_tol[jj];
-  const uint32_t ball0 = A.ball[0], ball1 = A.ball[1];
-  if (threadIdx.x < 2 * WG_CHUNK) s_tab[(threadIdx.x >> 1) * GQL + LQ_Z + (threadIdx.x & 1)] = make_uint4(0, 0, 0, 0);
-  chunk_store();
-  const bool act = j < n_pods;
-  const uint32_t code = (act && dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;
-  const uint32_t tol = (act && tq) ? 1u : 0u;
-  const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
-  const uint32_t row = code <= 9u ? code : (uint32_t)(ER_ROWS - 1);  // no digit: the zero row
-  const uint32_t xq = tol ? (uint32_t)LQ_Z : (uint32_t)LQ_X;           // X, or the zero block
-  __syncthreads();
-  MSH_STAMP(1);
-
-  uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group with a feasible match / non-match
-  for (int32_t c = n_chunks - 1; c >= 0; --c) {
-    const int32_t glo = c * WG_CHUNK, ng = min(WG_CHUNK, n_groups - glo);
-    if (c != n_chunks - 1) {
-      __syncthreads();  // every wave is done with chunk c + 1
-      chunk_store();
-      __syncthreads();
-    }
-    if (c > 0) chunk_load(c - 1);  // in flight during this chunk's scan
-    uint32_t bm = 0, bx = 0;        // bit k: group glo + k has a feasible match / non-match
-    int32_t k = (MSH_WG_EXPT & 1) ? -1 : ng - 1;
-    for (; k >= 1; k -= 2) {  // two groups per step
-      const uint4* t1 = s_tab + k * GQL;
-      const uint4* t0 = t1 - GQL;
-      uint32_t h1, h0, n1 = 0, n0 = 0;
-      group_acc<KX>(t1 + row, t1 + xq, t1 + LQ_V, h1, n1);
-      group_acc<KX>(t0 + row, t0 + xq, t0 + LQ_V, h0, n0);
-#if MSH_WG_FLAG == 1
-      bm = (bm << 2) + (h1 != 0 ? 2u : 0u) + (h0 != 0 ? 1u : 0u);
-      if constexpr (KX) bx = (bx << 2) + (n1 != 0 ? 2u : 0u) + (n0 != 0 ? 1u : 0u);
-#else
-      bm = lshl_or(bm, 2, lshl_or(min1(h1), 1, min1(h0)));
-      if constexpr (KX) bx = lshl_or(bx, 2, lshl_or(min1(n1), 1, min1(n0)));
-#endif
-    }
-    if (k == 0) {
-      uint32_t h0, n0 = 0;
-      group_acc<KX>(s_tab + row, s_tab + xq, s_tab + LQ_V, h0, n0);
-      bm = lshl_or(bm, 1, min1(h0));
-      if constexpr (KX) bx = lshl_or(bx, 1, min1(n0));
-    }
-    if (bm) fm = (uint32_t)glo + lowbit(bm);
-    if constexpr (KX)
-      if (bx) fx = (uint32_t)glo + lowbit(bx);
-  }
-  MSH_STAMP(2);
-  // the exact first node of the first group with a hit: chunk 0 is still staged
-  uint32_t rm = NOFIT, rx = NOFIT;
-  const uint32_t staged_hi = (uint32_t)min(WG_CHUNK, n_groups);
-  if (fm != NO_GROUP) {
-    if (fm < staged_hi) {
-      uint32_t h[PLANE_GW];
-      const uint4* tg = s_tab + fm * GQL;
-      rows_hits(tg[row], tg[ER_ROWS + row], tg[LQ_X], tg[LQ_X + 1], nT, h);
-      rm = hits_first(h, fm);
-    } else {
-      rm = rows_group_first(A, fm, row, nT);
-    }
-  }
-  if constexpr (KX) {
-    if (fx != NO_GROUP) {
-      if (fx < staged_hi) {
-        uint32_t n[PLANE_GW];
-        const uint4* tg = s_tab + fx * GQL;
-        rows_nonmatch(tg[row], tg[ER_ROWS + row], tg[LQ_X], tg[LQ_X + 1], tg[LQ_V], tg[LQ_V + 1], nT, n);
-        rx = hits_first(n, fx);
-      } else {
-        rx = rows_group_first_nm(A, fx, row, nT);
-      }
-    }
-  }
-  if constexpr (SHARD && !KX) write_class_keys(A);
-  if (!act) return;
-  if constexpr (SHARD) {
-    A.keys[j] = rm != NOFIT ? shard_key(A.node_base, rm) : 0;
-    if constexpr (KX) A.keys[(size_t)n_pods + j] = rx != NOFIT ? shard_key(A.node_base, rx) : 0;
-  } else {
-    int32_t oi, ost;
-    int64_t osc;
-    const int64_t im = rm != NOFIT ? (int64_t)rm : -1, ia = key_to_idx(tol ? ball1 : ball0);
-    if constexpr (KX)
-      decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, code != CODE_NONE_POD, A.pp, &oi, &osc, &ost);
-    else
-      decode_ident(im, ia, code != CODE_NONE_POD, make_ident_decode(A.pp), &oi, &osc, &ost);
-    if ((MSH_WG_EXPT & 2) == 0 || oi == 0x7fffffff) {
-      out_idx[j] = oi;
-      if (out_score) out_score[j] = osc;  // optional output (NULL: not written)
-      out_status[j] = ost;
-    }
-  }
-#ifdef MSH_STAMPS
-  MSH_STAMP(3);
-  if (lane == 0 && g_stamps) {
-    const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * W + wv;
-    for (int i = 0; i < 4; ++i) g_stamps[w * 4 + i] = stamp_t[i];
-  }
-#endif
-}
 
 // ---------------------------------------------------------------------------------------
 // Persistent batch kernel (msh_schedule_batch_device / msh_schedule_batches_device when the table
@@ -1343,35 +845,37 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
 
 // ---------------------------------------------------------------------------------------
 // Generic score pipeline: any score plugin list (NodeNumber and up to four score-column plugins,
-// MSH_PLUGIN_SCORE_COLUMN0..3), with the int64 score of every (pod, node) pair computed
-// explicitly. The bitmap kernels above are exact only because NodeNumber's raw score takes two
-// values; this kernel is the general form of RunScorePlugins (minisched.go:164-199), north_star's
-// stages one to one:
-//   5. node-table tiles: GEN_TILE nodes (the raw columns and the score columns in use) staged in
-//      LDS once per workgroup and reused by its GEN_PB pods;
-//   1. feasibility: one node per lane, NodeUnschedulable per pair; the wave's ballot is the
-//      feasibility bitmask of its 64 nodes (the feasible count comes from its popcount);
-//   3. per-pod extent of every score plugin over the feasible nodes (a pass of its own, only
-//      when some plugin normalizes): per-lane max / min, a wave-shuffle reduction, then an LDS
-//      reduction across the waves (64-bit LDS atomics);
-//   2. the int64 total of each pair: sum over plugins of weight x NormalizeScore(raw) (upstream
-//      helper.DefaultNormalizeScore, reverse, or min-max), in Go int64 arithmetic (wrapping);
-//   4. selectHost: per lane the first maximum of its nodes (they ascend), then a wave-shuffle
-//      argmax on (total desc, index asc) and a cross-wave merge in LDS.
-// One workgroup of GEN_THREADS lanes per GEN_PB pods; lanes take nodes i = tid + k * GEN_THREADS
-// of each tile. Status as the reference routes it: FitError when no node is feasible, the
-// NodeNumber score error (no PreScore state) when some node is.
+// MSH_PLUGIN_SCORE_COLUMN0..3) with the int64 total of EVERY (pod, node) pair computed explicitly:
+// the general form of RunFilterPlugins + RunScorePlugins + selectHost (minisched.go:115-199,
+// 304-325), north_star's stages one to one.
+// "Lanes = pods": lane l of a wave holds one pod; the node side is wave-uniform and arrives by scalar
+// loads (GEN_CH nodes per chunk: node words, and the columns in use), so everything that depends on
+// the node alone runs on the scalar unit once per wave, and the vector unit does per-pair work only.
+//   1. feasibility: NodeUnschedulable per pair, from the node word (X: Spec.Unschedulable with the
+//      filter listed; V: a real node) and the lane's tolerates bit: a lane mask per node (the wave's
+//      ballot of its 64 pods), built by the scalar unit;
+//   3. per-pod extent (max, min) of every normalizing plugin's raw score over the pod's feasible
+//      nodes: a sweep of its own, only when some plugin normalizes; slice waves meet in an LDS
+//      reduction;
+//   2. the int64 total of each pair: the sum over the plugins of weight x NormalizeScore(raw) in Go
+//      int64 arithmetic (wrapping). NodeNumber: per pod, its two weighted normalized values (raw 10 on
+//      a digit match, else 0), selected per pair by one compare. A column plugin without a normalizer:
+//      weight x column, node-only, summed by the scalar unit. A normalizing column: per pair
+//      q = (100 raw - b) x r with the pod's reciprocal r = (1 / m)(1 + 2^-49) (b, m from its extent),
+//      truncated toward zero: exactly Go's int64 100 raw / m (|100 raw| < 2^39; the bias makes an
+//      exact quotient come out at or just above the integer, and keeps every other quotient below
+//      the next one);
+//   4. selectHost: per lane a running first maximum over the nodes in List order (strict '>', the
+//      first feasible node always taken), the node index kept as a chunk-relative inline constant;
+//      slice waves meet in LDS (slices ascend in List order).
+//   5. the node table is read once per wave through the scalar cache and reused by its 64 pods.
+// MODE 0: the whole batch (status, node, score per pod). Node-sharded mode (msh_generic_*): MODE 1
+// writes each pod's extents over this shard's nodes (ext, mins negated: one all-reduce MAX merges
+// them), MODE 2 takes the merged extents and writes each pod's best (total, global node index) over
+// the shard.
 // ---------------------------------------------------------------------------------------
-constexpr int GEN_PB = 8;           // pods per workgroup
-constexpr int GEN_TILE = 1024;      // nodes per staged tile (2 KiB + 8 KiB per score column in use)
-constexpr int GEN_THREADS = 256;
-constexpr int GEN_WAVES = GEN_THREADS / WAVE;
-constexpr uint8_t GEN_PAD = 2;      // s_un value of a slot past the table
-
-__device__ __forceinline__ int64_t shfl_xor64(int64_t v, int m) {
-  const int lo = __shfl_xor((int)(uint32_t)(uint64_t)v, m), hi = __shfl_xor((int)((uint64_t)v >> 32), m);
-  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
-}
+constexpr int GEN_WAVES = 4;   // waves per workgroup
+constexpr double GEN_RCP_BIAS = 1.0 + 0x1p-49;
 
 // NormalizeScore of one raw score given the pod's extent of that plugin over its feasible nodes
 // (mx, mn): upstream helper.DefaultNormalizeScore(MaxNodeScore = 100, reverse) — maxCount starts at
@@ -1391,167 +895,338 @@ __device__ __forceinline__ int64_t gen_normalize(int64_t raw, int32_t mode, int6
   }
 }
 
-__global__ __launch_bounds__(GEN_THREADS) void generic_kernel(GenericArgs a) {
-  __shared__ uint8_t s_un[GEN_TILE];
-  __shared__ int8_t s_dg[GEN_TILE];
-  __shared__ int64_t s_col[GEN_COLS][GEN_TILE];
-  __shared__ int64_t s_max[GEN_PB][GEN_MAX_SCORE], s_min[GEN_PB][GEN_MAX_SCORE];
-  __shared__ int64_t s_btot[GEN_PB][GEN_WAVES];
-  __shared__ int32_t s_bidx[GEN_PB][GEN_WAVES];
-  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int32_t j0 = (int32_t)blockIdx.x * GEN_PB;
-  const int npb = min(GEN_PB, a.n_pods - j0);
-  // the score columns the plugin list reads (a mask over GEN_COLS)
-  int colmask = 0;
-  for (int s = 0; s < a.ns; ++s)
-    if (a.kind[s] > 0) colmask |= 1 << (a.kind[s] - 1);
-  if (tid < GEN_PB * GEN_MAX_SCORE) {
-    (&s_max[0][0])[tid] = INT64_MIN;
-    (&s_min[0][0])[tid] = INT64_MAX;
+template <int S, int NCOL, int MODE>
+__global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a) {
+  static_assert(MODE == 0 || S == 1, "the node-sharded modes run one wave per 64-pod block");
+  constexpr int PB = GEN_WAVES / S;  // 64-pod blocks per workgroup
+  constexpr int NE = 1 + NCOL;       // extents: [0] NodeNumber, [1 + c] column c of the list
+  constexpr int SW = S > 1 ? GEN_WAVES : 1;
+  __shared__ int64_t s_mx[SW][NE][WAVE], s_mn[SW][NE][WAVE];
+  __shared__ int64_t s_bt[SW][WAVE];
+  __shared__ int32_t s_bi[SW][WAVE];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int sl = wv % S, pb = wv / S;
+  const BatchDesc& d = a.d[blockIdx.y];
+  const int32_t np = d.n_pods;
+  if ((int32_t)blockIdx.x * PB * WAVE >= np) return;  // the whole workgroup lies past its batch's end
+  const int32_t wbase = ((int32_t)blockIdx.x * PB + pb) * WAVE;
+  const int32_t j = wbase + lane;
+  const bool act = j < np;
+  int pdg = -1;
+  bool tol = false;
+  if (act) {
+    pdg = d.pod_digit[j];
+    tol = d.pod_tol[j] != 0;
   }
-  if (tid < GEN_PB * GEN_WAVES) {
-    (&s_btot[0][0])[tid] = 0;
-    (&s_bidx[0][0])[tid] = -1;
-  }
-  const int32_t n_tiles = (a.n_nodes + GEN_TILE - 1) / GEN_TILE;
-  constexpr int NPT = GEN_TILE / GEN_THREADS;  // nodes per lane and tile
-  for (int sweep = a.need_ext ? 0 : 1; sweep < 2; ++sweep) {
-    for (int32_t t = 0; t < n_tiles; ++t) {
-      __syncthreads();  // the previous tile (or sweep) is done with the staged columns
-      const int32_t base = t * GEN_TILE;
-      for (int i = tid; i < GEN_TILE; i += GEN_THREADS) {  // coalesced copies of the tile
-        const int32_t node = base + i;
-        const bool v = node < a.n_nodes;
-        s_un[i] = v ? (a.unsched[node] ? 1 : 0) : GEN_PAD;
-        s_dg[i] = v ? a.digit[node] : (int8_t)-1;
+  const bool pd_ok = pdg >= 0 && pdg <= 9;  // NodeNumber.PreScore: Atoi of the last byte
+  const uint32_t pcode = pd_ok ? (uint32_t)pdg : CODE_NONE_POD;
+  const bool live = wbase < np;  // wave-uniform
+  const int32_t c_lo = min(sl * a.cps, a.n_chunks);
+  const int32_t c_hi = live ? min(c_lo + a.cps, a.n_chunks) : c_lo;
+  const int32_t n_nodes = a.n_nodes;
+  const uint32_t* __restrict__ nrec = a.nrec;
+  // Lane masks are kept explicitly (the wave's ballot of its pods): the scalar unit builds and
+  // combines them, and a select reads one through inverse_ballot (the SGPR pair as the lane
+  // condition, no VALU). NodeUnschedulable.Filter per pair: the node record's mask is all-ones unless
+  // the node is Spec.Unschedulable (with the filter listed), when only the tolerating lanes pass.
+  const uint64_t tolm = __ballot(tol);
+  auto lanes = [](uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); };
+  // The wave's node range in chunks of GEN_CH: a chunk's records (and column values) are loaded
+  // up front from one wave-uniform base (scalar loads, immediate offsets, one wait); a partial last
+  // chunk runs a copy of the body with a node-count guard.
+  struct Chunk {
+    uint32_t code[GEN_CH];
+    uint64_t fm[GEN_CH];  // NodeUnschedulable: the lanes that pass the node
+  };
+  auto load_chunk = [&](int32_t i0, auto cnt, Chunk& ch) {
+    const uint32_t* __restrict__ r = nrec + (size_t)i0 * NREC;
 #pragma unroll
-        for (int k = 0; k < GEN_COLS; ++k)
-          if (colmask & (1 << k)) s_col[k][i] = v ? a.cols[k * a.col_stride + node] : 0;
+    for (int k = 0; k < GEN_CH; ++k) {
+      if (k >= cnt) break;
+      ch.code[k] = r[k * NREC];
+      ch.fm[k] = tolm | ((uint64_t)r[k * NREC + 3] << 32 | r[k * NREC + 2]);
+    }
+  };
+  auto for_chunks = [&](auto&& body) {
+    for (int32_t c = c_lo; c < c_hi; ++c) {
+      const int32_t i0 = c * GEN_CH;
+      const int32_t cnt = min(GEN_CH, n_nodes - i0);
+      if (cnt == GEN_CH) body(i0, std::integral_constant<int, GEN_CH>{});
+      else body(i0, cnt);
+    }
+  };
+
+  // ---- stage 3: extents over the feasible nodes (normalizing plugins only) ----
+  int64_t emx[NE], emn[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    emx[e] = INT64_MIN;
+    emn[e] = INT64_MAX;
+  }
+  if (MODE != 2 && a.need_ext) {
+    uint64_t fmm = 0, fxm = 0;  // NodeNumber: lanes with a feasible match / non-match seen
+    for_chunks([&](int32_t i0, auto cnt) {
+      Chunk ch;
+      load_chunk(i0, cnt, ch);
+#pragma unroll
+      for (int k = 0; k < GEN_CH; ++k) {
+        if (k >= cnt) break;
+        const uint64_t f = ch.fm[k];
+        const uint64_t m = __ballot(ch.code[k] == pcode);
+        fmm |= f & m;
+        fxm |= f & ~m;
+#pragma unroll
+        for (int cc = 0; cc < NCOL; ++cc) {
+          if (a.cmode[cc] == 0) continue;
+          const int64_t v = (a.cols + (size_t)a.ccol[cc] * a.col_stride + i0)[k];
+          emx[1 + cc] = lanes(f & __ballot(v > emx[1 + cc])) ? v : emx[1 + cc];
+          emn[1 + cc] = lanes(f & __ballot(v < emn[1 + cc])) ? v : emn[1 + cc];
+        }
+      }
+    });
+    const bool fm = lanes(fmm), fx = lanes(fxm);
+    emx[0] = fm ? 10 : (fx ? 0 : INT64_MIN);  // NodeNumber's raw scores are 10 / 0
+    emn[0] = fx ? 0 : (fm ? 10 : INT64_MAX);
+    if constexpr (S > 1) {  // the slices' partial extents meet in LDS
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        s_mx[wv][e][lane] = emx[e];
+        s_mn[wv][e][lane] = emn[e];
       }
       __syncthreads();
-      for (int q = 0; q < npb; ++q) {
-        const int pd = a.pod_digit[j0 + q];
-        const bool tol = a.pod_tol[j0 + q] != 0;
-        const bool pd_ok = pd >= 0 && pd <= 9;
-        // raw score of plugin s at staged node i (NodeNumber: 10 on a suffix-digit match)
-        auto raw = [&](int s, int i) -> int64_t {
-          const int kd = a.kind[s];
-          if (kd == 0) return (pd_ok && s_dg[i] == pd) ? 10 : 0;
-          return s_col[kd - 1][i];
-        };
-        if (sweep == 0) {  // ---- stage 3: the extent of every score plugin over the feasible nodes
-          int64_t lmx[GEN_MAX_SCORE], lmn[GEN_MAX_SCORE];
 #pragma unroll
-          for (int s = 0; s < GEN_MAX_SCORE; ++s) {
-            lmx[s] = INT64_MIN;
-            lmn[s] = INT64_MAX;
-          }
+      for (int k = 0; k < S; ++k) {
+        const int ow = pb * S + k;
 #pragma unroll
-          for (int k = 0; k < NPT; ++k) {
-            const int i = tid + k * GEN_THREADS;
-            const uint8_t u = s_un[i];
-            const bool feas = u != GEN_PAD && !(a.has_nu && u && !tol);  // stage 1: NodeUnschedulable
-            if (feas)
-#pragma unroll
-              for (int s = 0; s < GEN_MAX_SCORE; ++s)
-                if (s < a.ns) {
-                  const int64_t r = raw(s, i);
-                  lmx[s] = r > lmx[s] ? r : lmx[s];
-                  lmn[s] = r < lmn[s] ? r : lmn[s];
-                }
-          }
-#pragma unroll
-          for (int s = 0; s < GEN_MAX_SCORE; ++s) {
-            if (s >= a.ns) break;
-#pragma unroll
-            for (int m = 32; m > 0; m >>= 1) {  // wave-shuffle reduction
-              const int64_t ox = shfl_xor64(lmx[s], m), on = shfl_xor64(lmn[s], m);
-              lmx[s] = ox > lmx[s] ? ox : lmx[s];
-              lmn[s] = on < lmn[s] ? on : lmn[s];
-            }
-            if (lane == 0 && lmx[s] != INT64_MIN) {  // LDS reduction across the waves
-              atomicMax((long long*)&s_max[q][s], (long long)lmx[s]);
-              atomicMin((long long*)&s_min[q][s], (long long)lmn[s]);
-            }
-          }
-        } else {  // ---- stages 1, 2, 4: feasibility, the weighted int64 total, the first maximum
-          int64_t mx[GEN_MAX_SCORE], mn[GEN_MAX_SCORE];
-#pragma unroll
-          for (int s = 0; s < GEN_MAX_SCORE; ++s) {
-            mx[s] = s_max[q][s];
-            mn[s] = s_min[q][s];
-          }
-          int64_t btot = 0;
-          int32_t bidx = -1;
-          uint64_t fmask = 0;  // this wave's feasibility bitmask (stage 1), one tile slice at a time
-#pragma unroll
-          for (int k = 0; k < NPT; ++k) {
-            const int i = tid + k * GEN_THREADS;
-            const uint8_t u = s_un[i];
-            const bool feas = u != GEN_PAD && !(a.has_nu && u && !tol);
-            fmask |= __ballot(feas);
-            if (feas) {
-              uint64_t tot = 0;  // Go int64: wrapping
-#pragma unroll
-              for (int s = 0; s < GEN_MAX_SCORE; ++s)
-                if (s < a.ns) tot += (uint64_t)gen_normalize(raw(s, i), a.mode[s], mx[s], mn[s]) * (uint64_t)a.weight[s];
-              const int64_t ts = (int64_t)tot;
-              if (bidx < 0 || ts > btot) {  // nodes ascend per lane: the first maximum
-                btot = ts;
-                bidx = base + i;
-              }
-            }
-          }
-          if (fmask) {  // some node of this wave's slice is feasible for pod q
-#pragma unroll
-            for (int m = 32; m > 0; m >>= 1) {  // wave-shuffle argmax: total desc, index asc
-              const int64_t ot = shfl_xor64(btot, m);
-              const int32_t oi = __shfl_xor(bidx, m);
-              const bool take = oi >= 0 && (bidx < 0 || ot > btot || (ot == btot && oi < bidx));
-              btot = take ? ot : btot;
-              bidx = take ? oi : bidx;
-            }
-            if (lane == 0) {  // this wave's running best across tiles (tiles ascend)
-              const int32_t ci = s_bidx[q][wv];
-              if (ci < 0 || btot > s_btot[q][wv]) {
-                s_btot[q][wv] = btot;
-                s_bidx[q][wv] = bidx;
-              }
-            }
-          }
+        for (int e = 0; e < NE; ++e) {
+          const int64_t ox = s_mx[ow][e][lane], on = s_mn[ow][e][lane];
+          emx[e] = ox > emx[e] ? ox : emx[e];
+          emn[e] = on < emn[e] ? on : emn[e];
         }
       }
     }
-  }
-  __syncthreads();
-  if (tid < npb) {  // merge the waves' bests (LDS), decode, write
-    const int q = tid, j = j0 + q;
-    int64_t bt = 0;
-    int32_t bi = -1;
+    if constexpr (MODE == 1) {  // node-sharded: this shard's extents, mins negated (one MAX merges both)
+      if (act) {
 #pragma unroll
-    for (int w = 0; w < GEN_WAVES; ++w) {
-      const int32_t oi = s_bidx[q][w];
-      const int64_t ot = s_btot[q][w];
-      if (oi >= 0 && (bi < 0 || ot > bt || (ot == bt && oi < bi))) {
-        bt = ot;
-        bi = oi;
+        for (int e = 0; e < NE; ++e) {
+          a.ext[(size_t)(2 * e) * np + j] = emx[e];
+          a.ext[(size_t)(2 * e + 1) * np + j] = -emn[e];  // emn <= INT64_MAX: no overflow
+        }
+      }
+      return;
+    }
+  }
+  if constexpr (MODE == 1) return;
+  if (MODE == 2 && a.need_ext && act) {  // the extents merged over every shard
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      emx[e] = a.ext[(size_t)(2 * e) * np + j];
+      emn[e] = -a.ext[(size_t)(2 * e + 1) * np + j];
+    }
+  }
+
+  // ---- per pod: NodeNumber's two weighted values, each normalizing column's reciprocal ----
+  int64_t c1 = 0, c0 = 0;  // both 0 when NodeNumber does not score: the per-pair select adds 0
+  if (a.nn_score && emx[0] != INT64_MIN) {
+    c1 = (int64_t)((uint64_t)gen_normalize(10, a.nn_mode, emx[0], emn[0]) * (uint64_t)a.nn_weight);
+    c0 = (int64_t)((uint64_t)gen_normalize(0, a.nn_mode, emx[0], emn[0]) * (uint64_t)a.nn_weight);
+  } else if (a.nn_score) {
+    c1 = (int64_t)((uint64_t)10 * (uint64_t)a.nn_weight);  // NONE (no extent sweep): raw x weight
+  }
+  double rr[NCOL > 0 ? NCOL : 1], bb[NCOL > 0 ? NCOL : 1];
+#pragma unroll
+  for (int cc = 0; cc < NCOL; ++cc) {
+    rr[cc] = 0.0;
+    bb[cc] = 0.0;
+    const int32_t md = a.cmode[cc];
+    const int64_t mx = emx[1 + cc], mn = emn[1 + cc];
+    if (md == 0 || mx == INT64_MIN) continue;  // no normalizer, or no feasible node
+    if (md == 3) {  // min-max: (raw - mn) x 100 / (mx - mn), 0 when mx == mn
+      if (mx != mn) {
+        rr[cc] = (1.0 / (double)(mx - mn)) * GEN_RCP_BIAS;
+        bb[cc] = 100.0 * (double)mn;
+      }
+    } else {  // DefaultNormalizeScore: 100 raw / max(mx, 0); DEFAULT leaves an all-zero list (m = 100 -> raw)
+      const int64_t m = mx > 0 ? mx : 0;
+      if (m != 0) rr[cc] = (1.0 / (double)m) * GEN_RCP_BIAS;
+      else if (md == 1) rr[cc] = 0.01 * GEN_RCP_BIAS;
+      // REVERSE with m == 0: r = 0, 100 - 0 = 100 for every node
+    }
+  }
+
+  // ---- stages 1, 2, 4: feasibility, the total, the first maximum ----
+  uint64_t best = 0x8000000000000000ull;  // INT64_MIN; the first feasible node is always taken
+  int32_t bidx = -1;
+  uint64_t fdm = 0;  // lanes with a feasible node seen
+  const uint64_t cw1 = (uint64_t)c1, cw0 = (uint64_t)c0;
+  for_chunks([&](int32_t i0, auto cnt) {
+    Chunk ch;
+    load_chunk(i0, cnt, ch);
+    int32_t bk = 0;
+    uint64_t took = 0;  // lanes whose maximum moved in this chunk
+#pragma unroll
+    for (int k = 0; k < GEN_CH; ++k) {
+      if (k >= cnt) break;
+      const uint64_t f = ch.fm[k];
+      // the node-only part: weight x column of the columns without a normalizer (scalar unit)
+      uint64_t tot = 0;
+#pragma unroll
+      for (int cc = 0; cc < NCOL; ++cc)
+        if (a.cmode[cc] == 0)
+          tot += (uint64_t)(a.cols + (size_t)a.ccol[cc] * a.col_stride + i0)[k] * (uint64_t)a.cweight[cc];
+      tot += (ch.code[k] == pcode) ? cw1 : cw0;  // NodeNumber: 10 on a suffix-digit match
+#pragma unroll
+      for (int cc = 0; cc < NCOL; ++cc) {
+        const int32_t md = a.cmode[cc];
+        if (md == 0) continue;
+        const double A = (a.cols100 + (size_t)a.ccol[cc] * a.col_stride + i0)[k];  // 100 x raw, exact
+        const double q = (md == 3 ? A - bb[cc] : A) * rr[cc];
+        int64_t n;
+        if (md == 3 || A >= 0.0) {  // |q| <= 100 on a feasible pair: the 32-bit conversion (clamped)
+          n = (int32_t)__builtin_fmin(__builtin_fmax(q, -2147483648.0), 2147483647.0);
+        } else {
+          n = (int64_t)q;  // |q| < 2^40
+        }
+        if (md == 2) n = 100 - n;
+        tot += (uint64_t)n * (uint64_t)a.cweight[cc];
+      }
+      const uint64_t take = f & (~fdm | __ballot((int64_t)tot > (int64_t)best));  // strict '>': the first max
+      best = lanes(take) ? tot : best;
+      bk = lanes(take) ? k : bk;
+      took |= take;
+      fdm |= f;
+    }
+    bidx = lanes(took) ? i0 + bk : bidx;
+  });
+  bool found = lanes(fdm);
+  if constexpr (S > 1) {  // slices ascend in List order: a later slice wins only with a larger total
+    s_bt[wv][lane] = (int64_t)best;
+    s_bi[wv][lane] = found ? bidx : -1;
+    __syncthreads();
+    if (sl != 0) return;
+#pragma unroll
+    for (int k = 1; k < S; ++k) {
+      const int32_t oi = s_bi[wv + k][lane];
+      const int64_t ot = s_bt[wv + k][lane];
+      if (oi >= 0 && (!found || ot > (int64_t)best)) {
+        best = (uint64_t)ot;
+        bidx = oi;
+        found = true;
       }
     }
-    const int pd = a.pod_digit[j];
-    const bool pd_ok = pd >= 0 && pd <= 9;
+  }
+  if (!act) return;
+  if constexpr (MODE == 2) {  // this shard's best: merged by MAX total, then MIN global index
+    a.best_total[j] = found ? (int64_t)best : INT64_MIN;
+    a.best_idx[j] = found ? (int32_t)(a.node_base + bidx) : INT32_MAX;
+  } else {
     int32_t st = 0;
-    if (bi < 0) st = 1;                                           // FitError (minisched.go:143-148)
-    else if (a.nn_score && (!a.nn_prescore || !pd_ok)) st = 2;    // NodeNumber.Score error (nodenumber.go:74-77)
-    a.out_idx[j] = st ? -1 : bi;
-    if (a.out_score) a.out_score[j] = st ? 0 : bt;
-    a.out_status[j] = st;
+    if (!found) st = 1;                                          // FitError (minisched.go:143-148)
+    else if (a.nn_score && (!a.nn_prescore || !pd_ok)) st = 2;   // NodeNumber.Score error (nodenumber.go:74-77)
+    d.out_idx[j] = st ? -1 : bidx;
+    if (d.out_score) d.out_score[j] = st ? 0 : (int64_t)best;
+    d.out_status[j] = st;
   }
 }
 
-hipError_t launch_generic(const GenericArgs& a, hipStream_t s) {
-  if (a.n_pods <= 0) return hipSuccess;
-  MSH_TIMED_LAUNCH(generic_kernel, dim3((unsigned)((a.n_pods + GEN_PB - 1) / GEN_PB)), dim3(GEN_THREADS), 0, s, a);
+// The decode of the node-sharded generic path, after the merge (msh_generic_decode_device).
+__global__ __launch_bounds__(256) void generic_decode_kernel(const int8_t* __restrict__ pod_digit, int32_t p,
+                                                             const int64_t* __restrict__ best_total,
+                                                             const int32_t* __restrict__ best_idx,
+                                                             int32_t nn_score, int32_t nn_prescore,
+                                                             int32_t* __restrict__ out_idx,
+                                                             int64_t* __restrict__ out_score,
+                                                             int32_t* __restrict__ out_status) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p) return;
+  const int pd = pod_digit[j];
+  const bool pd_ok = pd >= 0 && pd <= 9;
+  const int32_t bi = best_idx[j];
+  int32_t st = 0;
+  if (bi == INT32_MAX) st = 1;                          // no shard has a feasible node: FitError
+  else if (nn_score && (!nn_prescore || !pd_ok)) st = 2;  // NodeNumber.Score error
+  out_idx[j] = st ? -1 : bi;
+  if (out_score) out_score[j] = st ? 0 : best_total[j];
+  out_status[j] = st;
+}
+
+// Per pod of a shard: its best index if its best total equals the merged maximum, else INT32_MAX
+// (the second, MIN, all-reduce then yields the lowest global index among the maxima).
+__global__ __launch_bounds__(256) void generic_candidate_kernel(int32_t p, const int64_t* __restrict__ local_total,
+                                                                const int64_t* __restrict__ merged_total,
+                                                                int32_t* __restrict__ idx) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p) return;
+  if (idx[j] != INT32_MAX && local_total[j] != merged_total[j]) idx[j] = INT32_MAX;
+}
+
+namespace {
+int gen_slices(int64_t waves, int32_t n_chunks, int mode, const DeviceInfo& dev) {
+  if (mode != 0) return 1;
+  if (dev.bits_slices > 0) return dev.bits_slices;
+  const int64_t want = (int64_t)dev.cus * 4 * 4;
+  int sl = 1;
+  while (sl < GEN_WAVES && waves * sl < want && n_chunks >= 64 * sl) sl *= 2;
+  return sl;
+}
+
+template <int S, int NCOL, int MODE>
+hipError_t launch_gen_k(GenericArgs& a, int32_t bx, hipStream_t s) {
+  a.cps = (a.n_chunks + S - 1) / S;
+  MSH_TIMED_LAUNCH((generic_kernel<S, NCOL, MODE>), dim3((unsigned)bx, (unsigned)a.nb), dim3(GEN_WAVES * WAVE), 0, s,
+                   a);
+  return hipGetLastError();
+}
+
+template <int NCOL>
+hipError_t launch_gen_n(GenericArgs& a, int mode, int S, int32_t blocks, hipStream_t s) {
+  auto bx = [&](int sl) { return (blocks * sl + GEN_WAVES - 1) / GEN_WAVES; };
+  if (mode == 1) return launch_gen_k<1, NCOL, 1>(a, bx(1), s);
+  if (mode == 2) return launch_gen_k<1, NCOL, 2>(a, bx(1), s);
+  switch (S) {
+    case 1: return launch_gen_k<1, NCOL, 0>(a, bx(1), s);
+    case 2: return launch_gen_k<2, NCOL, 0>(a, bx(2), s);
+    default: return launch_gen_k<4, NCOL, 0>(a, bx(4), s);
+  }
+}
+}  // namespace
+
+hipError_t launch_generic(GenericArgs& a, int mode, const DeviceInfo& dev, hipStream_t s) {
+  if (a.nb <= 0 || a.nb > MULTI_MAX || a.ncol < 0 || a.ncol > GEN_COLS || (mode != 0 && a.nb != 1))
+    return hipErrorInvalidValue;
+  int32_t maxp = 0;
+  int64_t waves = 0;
+  for (int b = 0; b < a.nb; ++b) {
+    maxp = std::max(maxp, a.d[b].n_pods);
+    waves += (a.d[b].n_pods + WAVE - 1) / WAVE;
+  }
+  if (maxp == 0) return hipSuccess;
+  const int32_t blocks = (maxp + WAVE - 1) / WAVE;
+  const int S = gen_slices(waves, a.n_chunks, mode, dev);
+  switch (a.ncol) {
+    case 0: return launch_gen_n<0>(a, mode, S, blocks, s);
+    case 1: return launch_gen_n<1>(a, mode, S, blocks, s);
+    case 2: return launch_gen_n<2>(a, mode, S, blocks, s);
+    case 3: return launch_gen_n<3>(a, mode, S, blocks, s);
+    default: return launch_gen_n<4>(a, mode, S, blocks, s);
+  }
+}
+
+hipError_t launch_generic_candidates(int32_t p, const int64_t* local_total, const int64_t* merged_total, int32_t* idx,
+                                     hipStream_t s) {
+  if (p <= 0) return hipSuccess;
+  hipLaunchKernelGGL(generic_candidate_kernel, dim3((p + 255) / 256), dim3(256), 0, s, p, local_total, merged_total,
+                     idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_generic_decode(const int8_t* pod_digit, int32_t p, const int64_t* best_total, const int32_t* best_idx,
+                                 int32_t nn_score, int32_t nn_prescore, int32_t* out_idx, int64_t* out_score,
+                                 int32_t* out_status, hipStream_t s) {
+  if (p <= 0) return hipSuccess;
+  hipLaunchKernelGGL(generic_decode_kernel, dim3((p + 255) / 256), dim3(256), 0, s, pod_digit, p, best_total, best_idx,
+                     nn_score, nn_prescore, out_idx, out_score, out_status);
   return hipGetLastError();
 }
 
@@ -2012,18 +1687,34 @@ __global__ __launch_bounds__(256) void hr_first_kernel(uint32_t* __restrict__ hr
 }
 
 hipError_t launch_node_prep(const uint8_t* d_unsched, const int8_t* d_digit, int32_t n, int32_t n_pad,
-                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_erows,
-                            uint32_t* d_hrows, hipStream_t s, const unsigned long long* d_patch, int32_t patch_count) {
+                            int32_t has_nu, uint32_t* d_ball, uint32_t* d_planes, uint32_t* d_hrows,
+                            uint32_t* d_nrec, hipStream_t s, const unsigned long long* d_patch, int32_t patch_count) {
   hipLaunchKernelGGL(prep_reset_kernel, dim3(patch_count > 0 ? (patch_count + 255) / 256 : 1), dim3(256), 0, s,
                      d_ball, d_patch, patch_count, const_cast<uint8_t*>(d_unsched), const_cast<int8_t*>(d_digit));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (n_pad == 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel, dim3(n_pad / PREP_THREADS), dim3(PREP_THREADS), 0, s, d_unsched, d_digit, n,
-                     has_nu, d_ball, d_planes, d_erows, d_hrows);
+                     has_nu, d_ball, d_planes, d_hrows, d_nrec);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int32_t slots = n_pad / GROUP_NODES * 2 * HR_CLS;
   hipLaunchKernelGGL(hr_first_kernel, dim3((slots + 255) / 256), dim3(256), 0, s, d_hrows, n_pad / GROUP_NODES);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void cols100_kernel(const int64_t* __restrict__ cols, double* __restrict__ cols100,
+                                                     int64_t stride, int32_t n, int32_t n_pad, uint32_t col_mask) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (i >= n_pad || !((col_mask >> k) & 1u)) return;
+  cols100[(size_t)k * stride + i] = i < n ? 100.0 * (double)cols[(size_t)k * stride + i] : 0.0;
+}
+
+hipError_t launch_cols100(const int64_t* cols, double* cols100, int64_t stride, int32_t n, int32_t n_pad,
+                          uint32_t col_mask, hipStream_t s) {
+  if (n_pad <= 0 || !col_mask) return hipSuccess;
+  hipLaunchKernelGGL(cols100_kernel, dim3((n_pad + 255) / 256, GEN_COLS), dim3(256), 0, s, cols, cols100, stride, n,
+                     n_pad, col_mask);
   return hipGetLastError();
 }
 
@@ -2094,74 +1785,23 @@ hipError_t launch_export(const uint8_t* d_unsched, const int8_t* d_digit, int32_
   return hipGetLastError();
 }
 
+
 namespace {
-// Slice waves per 64-pod block of the bit-sliced kernel: enough waves for ~6 per SIMD, each
-// slice at least two groups (512 nodes) so the per-wave fixed cost (pod bytes, the first-node
-// decode, the LDS merge) stays small next to the scan.
-int bits_slices(int64_t n_pods, int32_t n_groups, const DeviceInfo& dev) {
-  if (dev.bits_slices > 0) return dev.bits_slices;
-  const int64_t blocks = (n_pods + WAVE - 1) / WAVE;
-  const int64_t want = (int64_t)dev.cus * 4 * 6;
-  int sl = 1;
-  while (sl < 16 && blocks * sl < want && n_groups / (2 * sl) >= 2) sl *= 2;
-  return sl;
-}
-
-template <int S, bool KX, bool SHARD>
-hipError_t launch_bits_s(const BatchArgs& a, hipStream_t s) {
-  BatchArgs ka = a;
-  ka.gps = (a.n_groups + S - 1) / S;
-  const int64_t blocks = ((int64_t)a.n_pods + WAVE - 1) / WAVE;
-  MSH_TIMED_LAUNCH((bits_kernel<S, KX, SHARD>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
-  return hipGetLastError();
-}
-
-template <int S, bool KX, bool SHARD, int PPL>
-hipError_t launch_rows_s(const BatchArgs& a, hipStream_t s) {
-  BatchArgs ka = a;
-  ka.gps = (a.n_groups + S - 1) / S;
-  const int64_t blocks = ((int64_t)a.n_pods + PPL * WAVE - 1) / (PPL * WAVE);
-  MSH_TIMED_LAUNCH((rows_kernel<S, KX, SHARD, PPL>), dim3((unsigned)blocks), dim3(S * WAVE), 0, s, ka);
-  return hipGetLastError();
-}
-
-template <bool KX, bool SHARD, int PPL>
-hipError_t launch_rows_p(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
-  // slices for the launch's pod blocks of PPL * 64 pods
-  switch (bits_slices((a.n_pods + PPL - 1) / PPL, a.n_groups, dev)) {
-    case 1: return launch_rows_s<1, KX, SHARD, PPL>(a, s);
-    case 2: return launch_rows_s<2, KX, SHARD, PPL>(a, s);
-    case 4: return launch_rows_s<4, KX, SHARD, PPL>(a, s);
-    case 8: return launch_rows_s<8, KX, SHARD, PPL>(a, s);
-    default: return launch_rows_s<16, KX, SHARD, PPL>(a, s);
+// Occupancy of a kernel at a block size and dynamic LDS, from the runtime (workgroups per CU).
+int resident_per_cu(const void* kern, int threads, size_t lds) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, lds) != hipSuccess) {
+    (void)hipGetLastError();
+    return 1;
   }
+  return std::max(nb, 1);
 }
 
-template <bool KX, bool SHARD>
-hipError_t launch_rows_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
-  if constexpr (KX)  // (two pods per lane, an A/B of the identity modes, would spill here)
-    return launch_rows_p<KX, SHARD, 1>(a, dev, s);
-  else
-    return dev.rows_ppl == 1 ? launch_rows_p<KX, SHARD, 1>(a, dev, s) : launch_rows_p<KX, SHARD, 2>(a, dev, s);
-}
-
-// Waves per workgroup of wg_kernel: 4 (one staged copy of the table per 256 pods), or 8 (A/B,
-// MSH_WG_WAVES=8).
-int wg_waves(int64_t n_pods, const DeviceInfo& dev) {
-  (void)n_pods;
-  return dev.wg_waves == 8 ? 8 : 4;
-}
-
-template <int W, bool KX, bool SHARD>
-hipError_t launch_wg_w(const BatchArgs& a, hipStream_t s) {
-  const int64_t blocks = ((int64_t)a.n_pods + W * WAVE - 1) / (W * WAVE);
-  MSH_TIMED_LAUNCH((wg_kernel<W, KX, SHARD, false>), dim3((unsigned)blocks), dim3(W * WAVE), 0, s, a);
-  return hipGetLastError();
-}
-
-// The persistent kernel over m.nb batches of m.bpb 256-pod blocks: as many workgroups as stay
-// resident (8 per CU: 32 waves, the CU's limit; fewer when the table's LDS copy limits them), never
-// more than the launch's blocks.
+// The class-row kernel over m.nb batches of m.bpb 256-pod blocks (MSH_BATCH_KERNEL=classrows, an
+// opt-in): as many workgroups as the runtime reports resident (its occupancy query for this kernel,
+// block size and LDS: 8 per CU for the identity-like form at C3, 6 for the REVERSE / MINMAX form and
+// its 78 VGPRs), never more than the launch's blocks; a launch larger than what stays resident would
+// run its extra workgroups after the persistent ones and break the age-slot shares below.
 template <bool KX>
 hipError_t launch_persistent(MultiArgs& m, const DeviceInfo& dev, hipStream_t s) {
   constexpr int W = MSH_WGP_W;
@@ -2170,14 +1810,14 @@ hipError_t launch_persistent(MultiArgs& m, const DeviceInfo& dev, hipStream_t s)
   if (maxp == 0) return hipSuccess;
   m.bpb = (maxp + W * WAVE - 1) / (W * WAVE);
   const size_t lds = (size_t)m.a.n_groups * HR_GQ * sizeof(uint4);
-  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / W, (int64_t)(160 * 1024 / std::max<size_t>(lds, 1))));
+  const int64_t per_cu = std::min<int64_t>(
+      RANK_MAX, resident_per_cu(reinterpret_cast<const void*>(wgp_kernel<W, KX>), W * WAVE, lds));
   const int64_t items = (int64_t)m.bpb * m.nb;
   const int64_t grid = std::min<int64_t>(items, (int64_t)dev.cus * per_cu);
   // Item shares by age slot (blockIdx / CUs: the dispatcher fills every CU's slot r before slot r + 1)
-  // when the grid fills every slot and each workgroup has at least WGP_SHARE_MIN items: slot r's
-  // share falls by MSH_WGP_AGE_SLOPE / 1000 per slot relative to slot 0 (the rates of the slots
-  // measured under equal shares); otherwise the strided walk (C3, 32 batches per launch: 0.815 ->
-  // 0.777 us per batch; at 8 and 20 batches the strided walk was as fast or faster).
+  // when the grid fills every resident slot and each workgroup has at least WGP_SHARE_MIN items: slot
+  // r's share falls by MSH_WGP_AGE_SLOPE / 1000 per slot relative to slot 0 (the rates of the slots
+  // measured under equal shares); otherwise the strided walk.
   m.walk = 0;
   if (grid == (int64_t)dev.cus * per_cu && per_cu > 1 && items >= WGP_SHARE_MIN * grid) {
     m.walk = 1;
@@ -2199,82 +1839,57 @@ hipError_t launch_persistent(MultiArgs& m, const DeviceInfo& dev, hipStream_t s)
   return hipGetLastError();
 }
 
-bool use_persistent(const BatchArgs& a, const DeviceInfo& dev) {
-  return a.n_groups <= WGP_MAX_GROUPS && !dev.wg_no_persist;
+// Slice waves per 64-pod block of pair_kernel: one, unless the launch has fewer than ~4 waves per
+// SIMD; then 2 or 4, while each slice keeps at least two groups.
+int pair_slices(int64_t waves, int32_t n_groups, const DeviceInfo& dev) {
+  if (dev.bits_slices > 0) return dev.bits_slices;
+  const int64_t want = (int64_t)dev.cus * 4 * 4;
+  int sl = 1;
+  while (sl < PAIR_WAVES && waves * sl < want && n_groups >= 4 * sl) sl *= 2;
+  return sl;
 }
 
-template <bool KX>
-hipError_t launch_single_persistent(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
-  MultiArgs m{};
-  m.a = a;
-  m.nb = 1;
-  m.d[0] = BatchDesc{a.pod_digit, a.pod_tol, a.out_idx, a.out_score, a.out_status, a.n_pods, 0};
-  return launch_persistent<KX>(m, dev, s);
-}
-
-template <bool KX, bool SHARD>
-hipError_t launch_wg_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
-  if constexpr (!SHARD) {
-    if (use_persistent(a, dev)) return launch_single_persistent<KX>(a, dev, s);
-  }
-  switch (wg_waves(a.n_pods, dev)) {
-    case 8: return launch_wg_w<8, KX, SHARD>(a, s);
-    default: return launch_wg_w<4, KX, SHARD>(a, s);
-  }
-}
-
-template <int W, bool KX>
-hipError_t launch_multi_w(MultiArgs& m, const DeviceInfo& dev, hipStream_t s) {
-  if (use_persistent(m.a, dev)) return launch_persistent<KX>(m, dev, s);
-  int32_t blocks = 0;  // per batch: the largest batch's
-  for (int b = 0; b < m.nb; ++b) blocks = std::max(blocks, (m.d[b].n_pods + W * WAVE - 1) / (W * WAVE));
-  if (blocks == 0) return hipSuccess;
-  m.bpb = blocks;
-  MSH_TIMED_LAUNCH((wg_kernel<W, KX, false, true>), dim3((unsigned)blocks, (unsigned)m.nb), dim3(W * WAVE), 0, s, m);
+template <int S, bool SHARD>
+hipError_t launch_pair_s(PairArgs& a, int32_t bx, hipStream_t s) {
+  a.gps = (a.n_groups + S - 1) / S;
+  MSH_TIMED_LAUNCH((pair_kernel<S, SHARD>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PAIR_WAVES * WAVE), 0, s, a);
   return hipGetLastError();
 }
 
-template <bool KX, bool SHARD>
-hipError_t launch_bits_t(const BatchArgs& a, const DeviceInfo& dev, hipStream_t s) {
-  switch (bits_slices(a.n_pods, a.n_groups, dev)) {
-    case 1: return launch_bits_s<1, KX, SHARD>(a, s);
-    case 2: return launch_bits_s<2, KX, SHARD>(a, s);
-    case 4: return launch_bits_s<4, KX, SHARD>(a, s);
-    case 8: return launch_bits_s<8, KX, SHARD>(a, s);
-    default: return launch_bits_s<16, KX, SHARD>(a, s);
+template <bool SHARD>
+hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
+  int32_t maxp = 0;
+  int64_t waves = 0;
+  for (int b = 0; b < a.nb; ++b) {
+    maxp = std::max(maxp, a.d[b].n_pods);
+    waves += (a.d[b].n_pods + WAVE - 1) / WAVE;
+  }
+  if (maxp == 0) return hipSuccess;
+  const int S = pair_slices(waves, a.n_groups, dev);
+  const int32_t blocks = (maxp + WAVE - 1) / WAVE;  // 64-pod blocks of the largest batch
+  auto bx = [&](int sl) { return (blocks * sl + PAIR_WAVES - 1) / PAIR_WAVES; };
+  switch (S) {
+    case 1: return launch_pair_s<1, SHARD>(a, bx(1), s);
+    case 2: return launch_pair_s<2, SHARD>(a, bx(2), s);
+    default: return launch_pair_s<4, SHARD>(a, bx(4), s);
   }
 }
 }  // namespace
 
-hipError_t launch_batch(const BatchArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s) {
-  if (a.n_pods == 0) return hipSuccess;
-  const bool kx = needs_kx(a.pp);
-  // every mode on the digit rows (REVERSE / MINMAX also track the first feasible non-match)
-  if (kx && dev.kx_bits)  // A/B: the code-plane kernel for REVERSE / MINMAX
-    return shard ? launch_bits_t<true, true>(a, dev, s) : launch_bits_t<true, false>(a, dev, s);
-  if (dev.batch_kernel == 1) {  // A/B: the round-2 slice kernel
-    if (shard) return kx ? launch_rows_t<true, true>(a, dev, s) : launch_rows_t<false, true>(a, dev, s);
-    return kx ? launch_rows_t<true, false>(a, dev, s) : launch_rows_t<false, false>(a, dev, s);
-  }
-  if (shard) return kx ? launch_wg_t<true, true>(a, dev, s) : launch_wg_t<false, true>(a, dev, s);
-  return kx ? launch_wg_t<true, false>(a, dev, s) : launch_wg_t<false, false>(a, dev, s);
+hipError_t launch_pairs(PairArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s) {
+  if (a.nb <= 0 || a.nb > MULTI_MAX || (shard && a.nb != 1)) return hipErrorInvalidValue;
+  return shard ? launch_pair_t<true>(a, dev, s) : launch_pair_t<false>(a, dev, s);
 }
 
-hipError_t launch_batches(const BatchArgs& a, const BatchDesc* d, int nb, const DeviceInfo& dev, hipStream_t s) {
-  if (nb <= 0 || nb > MULTI_MAX) return hipErrorInvalidValue;
+bool classrows_fit(int32_t n_groups) { return n_groups <= WGP_MAX_GROUPS; }
+
+hipError_t launch_classrows(const BatchArgs& a, const BatchDesc* d, int nb, const DeviceInfo& dev, hipStream_t s) {
+  if (nb <= 0 || nb > MULTI_MAX || !classrows_fit(a.n_groups)) return hipErrorInvalidValue;
   MultiArgs m{};
   m.a = a;
   m.nb = nb;
-  int64_t pods = 0;
-  for (int b = 0; b < nb; ++b) {
-    m.d[b] = d[b];
-    pods += d[b].n_pods;
-  }
-  const bool kx = needs_kx(a.pp);
-  switch (wg_waves(pods, dev)) {
-    case 8: return kx ? launch_multi_w<8, true>(m, dev, s) : launch_multi_w<8, false>(m, dev, s);
-    default: return kx ? launch_multi_w<4, true>(m, dev, s) : launch_multi_w<4, false>(m, dev, s);
-  }
+  for (int b = 0; b < nb; ++b) m.d[b] = d[b];
+  return needs_kx(a.pp) ? launch_persistent<true>(m, dev, s) : launch_persistent<false>(m, dev, s);
 }
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, const uint8_t* pod_tol, int32_t p,

@@ -28,8 +28,9 @@ from .snapshot import NodeTable, PodTable, pack_nodes, pack_pods
 FILTER_IDS = {NODE_UNSCHEDULABLE: N.MSH_PLUGIN_NODE_UNSCHEDULABLE}
 SCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER,
              **{name: N.MSH_PLUGIN_SCORE_COLUMN0 + k for k, name in enumerate(SCORE_COLUMNS)}}
-PRESCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER,
-             **{name: N.MSH_PLUGIN_SCORE_COLUMN0 + k for k, name in enumerate(SCORE_COLUMNS)}}
+# Only NodeNumber implements PreScore (nodenumber.go:50-64); a score column has none, so naming one in
+# the prescore list is MSH_ERR_UNSUPPORTED here exactly as in msh_set_plugins_ex.
+PRESCORE_IDS = {NODE_NUMBER: N.MSH_PLUGIN_NODE_NUMBER}
 
 
 @dataclass(frozen=True)
@@ -265,7 +266,7 @@ class DeviceContext:
             self._check(rc)
 
     def shard_keys_len(self, p: int) -> int:
-        """int32 entries msh_shard_keys_device writes for p pods: p + (2 or p)."""
+        """int32 entries msh_shard_keys_device writes for p pods: 2p (ABI v7)."""
         v = C.c_int32(0)
         self._check(self._lib.msh_shard_keys_len(self.handle, int(p), C.byref(v)))
         return int(v.value)
@@ -288,6 +289,34 @@ class DeviceContext:
         v = C.c_int32(0)
         self._check(self._lib.msh_keys_slot1_is_any(self.handle, C.byref(v)))
         return bool(v.value)
+
+    # -- node-sharded generic pipeline (msh_generic_*: any plugin list, score columns included) --
+    def generic_ext_len(self, p: int) -> int:
+        """int64 entries of the per-pod extents msh_generic_extents_device writes (0: no plugin
+        normalizes, nothing to merge before the bests)."""
+        v = C.c_int64(0)
+        self._check(self._lib.msh_generic_ext_len(self.handle, int(p), C.byref(v)))
+        return int(v.value)
+
+    def generic_extents_device(self, p: int, d_pod_digit: int, d_pod_tol: int, d_ext: int, stream: int = 0) -> None:
+        self._check(self._lib.msh_generic_extents_device(self.handle, int(p), d_pod_digit, d_pod_tol, d_ext,
+                                                         stream or None))
+
+    def generic_best_device(self, p: int, d_pod_digit: int, d_pod_tol: int, d_ext: int, node_base: int,
+                            d_best_total: int, d_best_idx: int, stream: int = 0) -> None:
+        self._check(self._lib.msh_generic_best_device(self.handle, int(p), d_pod_digit, d_pod_tol, d_ext or None,
+                                                      int(node_base), d_best_total, d_best_idx, stream or None))
+
+    def generic_candidates_device(self, p: int, d_local_total: int, d_merged_total: int, d_best_idx: int,
+                                  stream: int = 0) -> None:
+        self._check(self._lib.msh_generic_candidates_device(self.handle, int(p), d_local_total, d_merged_total,
+                                                            d_best_idx, stream or None))
+
+    def generic_decode_device(self, p: int, d_pod_digit: int, d_merged_total: int, d_merged_idx: int, d_idx: int,
+                              d_score: int, d_status: int, stream: int = 0) -> None:
+        self._check(self._lib.msh_generic_decode_device(self.handle, int(p), d_pod_digit, d_merged_total,
+                                                        d_merged_idx, d_idx, d_score or None, d_status,
+                                                        stream or None))
 
 
 class Scheduler:

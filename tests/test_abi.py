@@ -62,7 +62,7 @@ def test_fast_call_module(msh):
 def test_abi_version(msh):
     header = (ROOT / "include" / "minisched_hip.h").read_text()
     assert f"#define MSH_ABI_VERSION {msh._native.lib().msh_abi_version()}" in header
-    assert msh._native.lib().msh_abi_version() == 6
+    assert msh._native.lib().msh_abi_version() == 7
 
 
 def test_no_device_is_an_error_not_a_fallback(msh):

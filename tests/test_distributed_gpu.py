@@ -11,6 +11,10 @@ non-match (MINMAX) key layouts.
 The same again through NodeShardedScheduler.schedule on a busy non-default stream with the keys
 on the GPU (the stream-ordering of keys kernel -> all-reduce -> decode, as bench.py runs it).
 
+The node-sharded generic pipeline (GenericNodeShardedScheduler: per-pod extents merged by MAX, per-shard
+bests by MAX total then MIN global index) on score-column plugin lists with MINMAX and DEFAULT
+normalizers, against the oracle's RunScorePlugins over the whole table.
+
 Pod sharding of sequential mode: each rank schedules its pod range one pod at a time against
 the full table, and PodShardedScheduler.merge_node_counts sums the per-node commit counts; with
 no capacity (the reference semantics) they must equal the oracle's serial loop over all pods.
@@ -139,3 +143,68 @@ def test_sharded_paths_across_processes(oracle, world, norm):
     seq_st = np.concatenate([np.array(x[1][2], np.int64) for x in parts])
     assert (seq_idx == si).all() and (seq_st == sst).all()
     assert (counts == want_counts).all()
+
+
+GENERIC_LISTS = {
+    "minmax": [("NodeNumber", 3, 3), ("ScoreColumn0", 3, 3)],
+    "default": [("NodeNumber", 1, 1), ("ScoreColumn0", 2, 1), ("ScoreColumn1", 1, 0)],
+}
+
+
+def _generic_cols(seed, n):
+    rng = np.random.default_rng(seed + 7)
+    return {0: rng.integers(-(1 << 31), (1 << 31) + 1, n), 1: rng.integers(0, 5, n) * 11}
+
+
+def _worker_generic(rank, world, port, seed, n, p, name, out_q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        msh = importlib.import_module("mini-kube-scheduler_amd")
+        D = importlib.import_module("mini-kube-scheduler_amd.distributed")
+        u, nd, pd, pt = _case(seed, n, p)
+        cols = _generic_cols(seed, n)
+        pl = GENERIC_LISTS[name]
+        dev = torch.device("cuda:0")
+        ctx = msh.DeviceContext(0)
+        ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                        [msh.ScorePluginConfig(nm, w, msh.Normalize(m)) for nm, w, m in pl])
+        sched = D.GenericNodeShardedScheduler(ctx, u, nd, world, rank,
+                                              columns={f"ScoreColumn{k}": c for k, c in cols.items()})
+        d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+        out = [torch.full((p,), -7, dtype=dt, device=dev) for dt in (torch.int32, torch.int64, torch.int32)]
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream())
+        sched.schedule(d_pd, d_pt, *out, stream=side)
+        torch.cuda.synchronize()
+        if rank == 0:
+            out_q.put(tuple(t.cpu().numpy() for t in out))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", sorted(GENERIC_LISTS))
+def test_generic_node_sharding_across_processes(oracle, world, name):
+    n, p, seed = 7000 + 13 * world, 3000, 50 * world + len(name)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_generic, args=(r, world, port, seed, n, p, name, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        gi, gs, gst = q.get(timeout=180)
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+    assert all(pr.exitcode == 0 for pr in procs)
+    u, nd, pd, pt = _case(seed, n, p)
+    pl = GENERIC_LISTS[name]
+    ps = oracle.PluginSet(score=[nm for nm, _, _ in pl], weights=[w for _, w, _ in pl], normalize=[m for _, _, m in pl])
+    wi, ws, wst, _ = oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=_generic_cols(seed, n))
+    assert (gi == wi).all() and (gs == ws).all() and (gst == wst).all()

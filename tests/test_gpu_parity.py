@@ -363,8 +363,8 @@ def test_node_shards_merge(msh, gpu_ctx, oracle, norm):
         _set(c, msh, ps)
         c.upload_nodes(u[a:b], nd[a:b])
         klen = c.shard_keys_len(p)
-        # 4 B per pod + 2 class keys for the identity-like modes, 8 B per pod for REVERSE / MINMAX
-        assert klen == (2 * p if norm in (2, 3) else p + 2)
+        # ABI v7: per pod, the first feasible match and the first feasible non-match (8 B per pod)
+        assert klen == 2 * p and not c.keys_slot1_is_any()
         keys = torch.full((klen,), -7, dtype=torch.int32, device=dev)  # every entry must be written
         c.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), a, keys.data_ptr(),
                             torch.cuda.current_stream().cuda_stream)
@@ -586,21 +586,17 @@ def test_maximum_node_table(msh, gpu_ctx, synth):
     _assert_same(gpu_ctx.schedule_batch(pd, pt), closed_form(u[:10], nd[:10], pd, pt), "after reject")
 
 
-@pytest.mark.parametrize("slices", ["1", "2", "4", "8", "16"])
+@pytest.mark.parametrize("slices", ["1", "2", "4"])
 @pytest.mark.parametrize("n", [20_000, 70_000])
-@pytest.mark.parametrize("ppl,kx_bits", [("1", "0"), ("2", "0"), ("1", "1")])
-def test_bits_slices(msh, oracle, n, slices, ppl, kx_bits, monkeypatch):
-    """Few pods against a large table: SLICES waves share each 64-pod block, each scanning a range
-    of 256-node groups, firsts merged by min in LDS. Every slice count (MSH_BITS_SLICES, read once
-    by msh_create) against the oracle, for the batch and the shard-key entry points, in the
-    identity-like and the non-match (MINMAX) modes."""
+def test_pair_slices(msh, oracle, n, slices, monkeypatch):
+    """Few pods against a large table: SLICES waves of pair_kernel share each 64-pod block, each
+    scanning a range of 256-node groups, firsts merged by min in LDS. Every slice count
+    (MSH_BITS_SLICES, read once by msh_create) against the oracle, for the batch and the shard-key
+    entry points, in the identity-like and the non-match (MINMAX) modes."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_BATCH_KERNEL", "slices")  # the round-2 slice kernel (A/B)
     monkeypatch.setenv("MSH_BITS_SLICES", slices)
-    monkeypatch.setenv("MSH_ROWS_PPL", ppl)  # pods per lane of the digit-row kernel
-    monkeypatch.setenv("MSH_KX_BITS", kx_bits)  # MINMAX on the code-plane kernel (A/B) or the rows
     rng = np.random.default_rng(n + int(slices))
-    u, nd, pd, pt = _rand_case(rng, n, 1500 + int(ppl) * 37, p_unsched=0.2, p_tol=0.3)
+    u, nd, pd, pt = _rand_case(rng, n, 1537, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4  # digit 3 only in the second half: late first matches
     dev = torch.device("cuda:0")
     d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
@@ -611,7 +607,7 @@ def test_bits_slices(msh, oracle, n, slices, ppl, kx_bits, monkeypatch):
             _set(ctx, msh, ps)
             ctx.upload_nodes(u, nd)
             want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
-            _assert_same(ctx.schedule_batch(pd, pt), want, f"slices={slices} ppl={ppl} n={n} norm={norm}")
+            _assert_same(ctx.schedule_batch(pd, pt), want, f"slices={slices} n={n} norm={norm}")
             keys = torch.empty(ctx.shard_keys_len(p), dtype=torch.int32, device=dev)
             ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream)
@@ -769,31 +765,33 @@ def test_multi_batch_launch(msh, gpu_ctx, oracle, norm, nb):
 
 
 @pytest.mark.parametrize("n,norm", [(5000, 0), (5000, 3), (8192, 0), (6000, 2)])
-def test_multi_batch_age_shares(msh, gpu_ctx, oracle, n, norm):
-    """A full multi-batch launch (32 batches of ~100k pods, ragged) takes the persistent kernel's
-    age-slot walk (at least WGP_SHARE_MIN items per workgroup: contiguous item ranges sized per
-    workgroup slot on its CU; 8 slots at 5k nodes, 5 at 8,192 nodes); every batch bit-exact vs the
-    oracle."""
+def test_multi_batch_age_shares(msh, oracle, n, norm, monkeypatch):
+    """A full multi-batch launch (32 batches of ~100k pods, ragged) on the opt-in class-row kernel
+    (MSH_BATCH_KERNEL=classrows) takes its age-slot walk (at least WGP_SHARE_MIN items per workgroup:
+    contiguous item ranges sized per resident workgroup slot on its CU, the slot count from the
+    runtime's occupancy query); the same launch on the default per-pair kernel; every batch bit-exact
+    vs the oracle."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(4242 + n + norm)
     sizes = [100_000, 99_937, 100_003, 64, 0, 1, 99_999, 98_304] + [100_000 - 7 * k for k in range(24)]
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
-    _set(gpu_ctx, msh, ps)
     u, nd, _, _ = _rand_case(rng, n, 1)
-    gpu_ctx.upload_nodes(u, nd)
-    cases = []
-    for k, p in enumerate(sizes):
-        _, _, pd, pt = _rand_case(rng, 1, p)
-        cases.append((pd, pt, _dev_batch(torch, dev, pd, pt, scores=(k % 5 != 4))))
-    descs = gpu_ctx.batch_descs([_desc(c[2]) for c in cases])
-    gpu_ctx.schedule_batches_device(descs, stream=torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    for k, (pd, pt, t) in enumerate(cases):
-        want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=16)
-        gi, gst = t[2].cpu().numpy(), t[4].cpu().numpy()
-        gs = t[3].cpu().numpy() if t[3] is not None else want[1]
-        _assert_same((gi, gs, gst), want, f"batch {k} (p={len(pd)}) n={n} norm={norm}")
+    pods = [_rand_case(rng, 1, p)[2:] for p in sizes]
+    wants = [oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=16) for pd, pt in pods]
+    for kernel in ("classrows", "pair"):
+        monkeypatch.setenv("MSH_BATCH_KERNEL", kernel)
+        with msh.DeviceContext(0) as ctx:
+            _set(ctx, msh, ps)
+            ctx.upload_nodes(u, nd)
+            bufs = [_dev_batch(torch, dev, pd, pt, scores=(k % 5 != 4)) for k, (pd, pt) in enumerate(pods)]
+            ctx.schedule_batches_device(ctx.batch_descs([_desc(t) for t in bufs]),
+                                        stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            for k, (t, want) in enumerate(zip(bufs, wants)):
+                gi, gst = t[2].cpu().numpy(), t[4].cpu().numpy()
+                gs = t[3].cpu().numpy() if t[3] is not None else want[1]
+                _assert_same((gi, gs, gst), want, f"{kernel} batch {k} (p={len(pods[k][0])}) n={n} norm={norm}")
 
 
 def test_multi_batch_invalid(msh, gpu_ctx):
@@ -811,16 +809,14 @@ def test_multi_batch_invalid(msh, gpu_ctx):
         gpu_ctx.schedule_batches_device(bad)
 
 
-@pytest.mark.parametrize("waves", ["4", "8"])
 @pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 70_000])
-def test_wg_kernel_chunks(msh, oracle, n, waves, monkeypatch):
-    """wg_kernel streams tables above 32 groups (8,192 nodes) through LDS chunk by chunk, and
-    re-reads the first group with a hit from memory when it lies above the staged chunk 0: digit 3
-    only in the second half of the table makes those pods' first matches late. 4- and 8-wave
-    workgroups (MSH_WG_WAVES), batch, multi-batch and shard-key entry points, NONE and MINMAX."""
+def test_pair_kernel_late_matches(msh, oracle, n):
+    """pair_kernel re-reads the first group with a hit from memory when it lies above the lowest group
+    of the wave's range (kept in registers): digit 3 only in the second half of the table makes those
+    pods' first matches late. Batch, multi-batch and shard-key entry points, NONE and MINMAX, on tables
+    with and without a padded top group."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_WG_WAVES", waves)
-    rng = np.random.default_rng(n + int(waves))
+    rng = np.random.default_rng(n + 4)
     u, nd, pd, pt = _rand_case(rng, n, 3000, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4
     dev = torch.device("cuda:0")
@@ -831,7 +827,7 @@ def test_wg_kernel_chunks(msh, oracle, n, waves, monkeypatch):
             _set(ctx, msh, ps)
             ctx.upload_nodes(u, nd)
             want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
-            _assert_same(ctx.schedule_batch(pd, pt), want, f"wg n={n} W={waves} norm={norm}")
+            _assert_same(ctx.schedule_batch(pd, pt), want, f"pair n={n} norm={norm}")
             halves = [_dev_batch(torch, dev, pd[: p // 3], pt[: p // 3]), _dev_batch(torch, dev, pd[p // 3:], pt[p // 3:])]
             descs = ctx.batch_descs([_desc(t) for t in halves])
             ctx.schedule_batches_device(descs, stream=torch.cuda.current_stream().cuda_stream)
@@ -845,14 +841,14 @@ def test_wg_kernel_chunks(msh, oracle, n, waves, monkeypatch):
                                    out[3].data_ptr(), out[4].data_ptr(), torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
             got = [np.concatenate([t0[i].cpu().numpy(), t1[i].cpu().numpy()]) for i in (2, 3, 4)]
-            _assert_same(got, want, f"multi n={n} W={waves} norm={norm}")
-            _assert_same([out[i].cpu().numpy() for i in (2, 3, 4)], want, f"keys n={n} W={waves} norm={norm}")
+            _assert_same(got, want, f"multi n={n} norm={norm}")
+            _assert_same([out[i].cpu().numpy() for i in (2, 3, 4)], want, f"keys n={n} norm={norm}")
 
 
-@pytest.mark.parametrize("kernel", ["wg", "slices"])
+@pytest.mark.parametrize("kernel", ["pair", "classrows"])
 def test_batch_kernel_ab(msh, oracle, kernel, monkeypatch):
-    """The default workgroup-table kernel and the round-2 slice kernel (MSH_BATCH_KERNEL=slices, an
-    A/B switch read once by msh_create) place identically at C3 size, multi-batch included."""
+    """The default per-pair kernel and the opt-in class-row kernel (MSH_BATCH_KERNEL=classrows, read
+    once by msh_create) place identically at C3 size, multi-batch included."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("MSH_BATCH_KERNEL", kernel)
     rng = np.random.default_rng(5)
