@@ -2,44 +2,40 @@ package minisched
 
 // The batched scheduling loop: scheduleOne's selection part (minisched.go:40-87) for a whole batch
 // drained from activeQ, on the device through gpusched; Permit and Bind stay per pod, exactly as
-// scheduleOne runs them (:89-112). Wire it in place of Run when the plugin lists are the device's:
+// scheduleOne runs them (:89-112). The device's node table follows the Node informer
+// (gpusched.NodeSnapshot: a cordon flip is an O(1) patch, an Add or a Delete one upload) instead of
+// the per-cycle LIST (:40). Wire it in place of Run when the plugin lists are the device's:
 //
+//	snap := gpusched.NewNodeSnapshot()
+//	informerFactory.Core().V1().Nodes().Informer().AddEventHandler(snap.Handlers()) // before Start
 //	gpu, err := gpusched.New(0, sched.filterPlugins, sched.preScorePlugins, gpusched.Scores(sched.scorePlugins))
-//	if errors.Is(err, gpusched.ErrUnsupported) { sched.Run(ctx) } else { sched.RunBatched(ctx, gpu, 100000) }
+//	if errors.Is(err, gpusched.ErrUnsupported) { sched.Run(ctx) } else { sched.RunBatched(ctx, gpu, snap, 100000) }
 
 import (
 	"context"
 
 	"github.com/sanposhiho/mini-kube-scheduler/minisched/gpusched"
 	v1 "k8s.io/api/core/v1"
-	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
 	"k8s.io/apimachinery/pkg/util/wait"
 	"k8s.io/klog/v2"
 	"k8s.io/kubernetes/pkg/scheduler/framework"
 )
 
 // RunBatched is Run (minisched.go:28-30) with batches of up to maxBatch pods per device call.
-func (sched *Scheduler) RunBatched(ctx context.Context, gpu *gpusched.Ctx, maxBatch int) {
+func (sched *Scheduler) RunBatched(ctx context.Context, gpu *gpusched.Ctx, snap *gpusched.NodeSnapshot, maxBatch int) {
 	hb, err := gpusched.NewHostBatch(maxBatch)
 	if err != nil {
 		klog.Error(err)
 		return
 	}
-	wait.UntilWithContext(ctx, func(ctx context.Context) { sched.scheduleBatch(ctx, gpu, hb, maxBatch) }, 0)
+	wait.UntilWithContext(ctx, func(ctx context.Context) { sched.scheduleBatch(ctx, gpu, snap, hb, maxBatch) }, 0)
 }
 
-func (sched *Scheduler) scheduleBatch(ctx context.Context, gpu *gpusched.Ctx, hb *gpusched.HostBatch, maxBatch int) {
+func (sched *Scheduler) scheduleBatch(ctx context.Context, gpu *gpusched.Ctx, snap *gpusched.NodeSnapshot,
+	hb *gpusched.HostBatch, maxBatch int) {
 	pods := sched.SchedulingQueue.NextPods(maxBatch)
-	// one LIST per batch instead of one per pod (:40); informer deltas could use gpu.UpdateNode
-	nodes, err := sched.client.CoreV1().Nodes().List(ctx, metav1.ListOptions{})
-	if err != nil {
-		klog.Error(err)
-		for _, pod := range pods {
-			sched.ErrorFunc(pod, err)
-		}
-		return
-	}
-	if _, err := gpu.UploadNodes(nodes.Items); err != nil {
+	// the informer's deltas since the last batch: a patch, an upload, or nothing (no LIST, :40)
+	if _, err := snap.Sync(gpu); err != nil {
 		klog.Error(err)
 		for _, pod := range pods {
 			sched.ErrorFunc(pod, err)

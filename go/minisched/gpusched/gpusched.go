@@ -28,10 +28,12 @@ import (
 	"fmt"
 	"runtime"
 	"sort"
+	"sync"
 	"unsafe"
 
 	v1 "k8s.io/api/core/v1"
 	"k8s.io/apimachinery/pkg/util/sets"
+	"k8s.io/client-go/tools/cache"
 	"k8s.io/kubernetes/pkg/scheduler/framework"
 )
 
@@ -172,22 +174,151 @@ func (x *Ctx) UploadNodes(nodes []v1.Node) ([]*v1.Node, error) {
 // UpdateNode applies an informer Update that keeps the node's name (eventhandler.go:45-50, e.g. a
 // cordon flipping Spec.Unschedulable) in O(1) host->device traffic. Adds, deletes and renames
 // change List positions: call UploadNodes for those.
-func (x *Ctx) UpdateNode(n *v1.Node) error {
-	i := sort.Search(len(x.byIndex), func(k int) bool { return x.byIndex[k].Name >= n.Name })
-	if i == len(x.byIndex) || x.byIndex[i].Name != n.Name {
-		return fmt.Errorf("gpusched: node %q is not in the uploaded snapshot", n.Name)
+func (x *Ctx) UpdateNode(n *v1.Node) error { return x.UpdateNodes([]*v1.Node{n}) }
+
+// UpdateNodes is UpdateNode for several nodes in one msh_patch_nodes call.
+func (x *Ctx) UpdateNodes(nodes []*v1.Node) error {
+	if len(nodes) == 0 {
+		return nil
 	}
-	idx := []C.int32_t{C.int32_t(i)}
-	uns := []C.uint8_t{0}
-	if n.Spec.Unschedulable {
-		uns[0] = 1
+	idx := make([]C.int32_t, len(nodes))
+	uns := make([]C.uint8_t, len(nodes))
+	dig := make([]C.int8_t, len(nodes))
+	for k, n := range nodes {
+		i := sort.Search(len(x.byIndex), func(q int) bool { return x.byIndex[q].Name >= n.Name })
+		if i == len(x.byIndex) || x.byIndex[i].Name != n.Name {
+			return fmt.Errorf("gpusched: node %q is not in the uploaded snapshot", n.Name)
+		}
+		idx[k] = C.int32_t(i)
+		if n.Spec.Unschedulable {
+			uns[k] = 1
+		}
+		dig[k] = C.int8_t(suffixDigit(n.Name))
 	}
-	dig := []C.int8_t{C.int8_t(suffixDigit(n.Name))}
-	if rc := C.msh_patch_nodes(x.c, 1, ptrI32(idx), ptrU8(uns), ptrI8(dig)); rc != C.MSH_OK {
+	if rc := C.msh_patch_nodes(x.c, C.int32_t(len(nodes)), ptrI32(idx), ptrU8(uns), ptrI8(dig)); rc != C.MSH_OK {
 		return x.lastErr("msh_patch_nodes", rc)
 	}
-	x.byIndex[i] = n
+	for k, n := range nodes { // same names, same List positions: batches in flight decode the same way
+		x.byIndex[idx[k]] = n
+	}
 	return nil
+}
+
+// NodeSnapshot keeps a Ctx's node table in step with the Node informer (eventhandler.go:45-65)
+// instead of a LIST per cycle (minisched.go:40): an Add or a Delete changes List positions and marks
+// the table for one full upload; an Update of an existing name (a cordon flip, or any other field
+// change) queues an O(1) patch. Sync brings the Ctx up to date before a batch. The handlers run on
+// the informer's goroutine, Sync on the scheduling loop's: both take the lock. Register it next to
+// the reference's own handlers (which requeue pods on Node events):
+//
+//	snap := gpusched.NewNodeSnapshot()
+//	informerFactory.Core().V1().Nodes().Informer().AddEventHandler(snap.Handlers())
+//
+// The Python mirror is mini-kube-scheduler_amd/nodecache.py (NodeCache.sync).
+type NodeSnapshot struct {
+	mu         sync.Mutex
+	nodes      map[string]*v1.Node
+	structural bool                // List positions changed since the last Sync
+	patched    map[string]*v1.Node // names updated in place since the last Sync
+}
+
+// NewNodeSnapshot starts empty and structurally dirty: the first Sync uploads.
+func NewNodeSnapshot() *NodeSnapshot {
+	return &NodeSnapshot{nodes: map[string]*v1.Node{}, structural: true, patched: map[string]*v1.Node{}}
+}
+
+// Handlers are the informer callbacks (a cache.ResourceEventHandler).
+func (s *NodeSnapshot) Handlers() cache.ResourceEventHandlerFuncs {
+	return cache.ResourceEventHandlerFuncs{AddFunc: s.OnAdd, UpdateFunc: s.OnUpdate, DeleteFunc: s.OnDelete}
+}
+
+// OnAdd: a new name is a structural change; an Add for a name already present is an Update.
+func (s *NodeSnapshot) OnAdd(obj interface{}) {
+	n, ok := obj.(*v1.Node)
+	if !ok {
+		return
+	}
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	if _, had := s.nodes[n.Name]; had {
+		s.nodes[n.Name] = n
+		s.patched[n.Name] = n
+		return
+	}
+	s.nodes[n.Name] = n
+	s.structural = true
+}
+
+// OnUpdate: names are immutable, so an Update keeps the node's List position: a patch.
+func (s *NodeSnapshot) OnUpdate(_, newObj interface{}) {
+	n, ok := newObj.(*v1.Node)
+	if !ok {
+		return
+	}
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	if _, had := s.nodes[n.Name]; !had {
+		s.nodes[n.Name] = n
+		s.structural = true
+		return
+	}
+	s.nodes[n.Name] = n
+	s.patched[n.Name] = n
+}
+
+// OnDelete: every later List position shifts: a structural change.
+func (s *NodeSnapshot) OnDelete(obj interface{}) {
+	var name string
+	switch t := obj.(type) {
+	case *v1.Node:
+		name = t.Name
+	case cache.DeletedFinalStateUnknown:
+		n, ok := t.Obj.(*v1.Node)
+		if !ok {
+			return
+		}
+		name = n.Name
+	default:
+		return
+	}
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	if _, had := s.nodes[name]; had {
+		delete(s.nodes, name)
+		delete(s.patched, name)
+		s.structural = true
+	}
+}
+
+// Sync brings x's device table up to date: "upload" (msh_upload_nodes of every node, after an Add
+// or a Delete), "patch" (msh_patch_nodes of the updated nodes only) or "clean".
+func (s *NodeSnapshot) Sync(x *Ctx) (string, error) {
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	if s.structural {
+		all := make([]v1.Node, 0, len(s.nodes))
+		for _, n := range s.nodes {
+			all = append(all, *n)
+		}
+		if _, err := x.UploadNodes(all); err != nil {
+			return "", err
+		}
+		s.structural = false
+		s.patched = map[string]*v1.Node{}
+		return "upload", nil
+	}
+	if len(s.patched) > 0 {
+		upd := make([]*v1.Node, 0, len(s.patched))
+		for _, n := range s.patched {
+			upd = append(upd, n)
+		}
+		if err := x.UpdateNodes(upd); err != nil {
+			return "", err
+		}
+		s.patched = map[string]*v1.Node{}
+		return "patch", nil
+	}
+	return "clean", nil
 }
 
 // Result of scheduleOne's selection part (minisched.go:50-87) for one pod.
@@ -210,6 +341,7 @@ type HostBatch struct {
 	score       []C.int64_t
 	ticket      C.uint64_t // the pending msh_schedule_batch_async ticket, 0 = none
 	pods        []*v1.Pod
+	byIndex     []*v1.Node // the Ctx's device index -> node mapping when the batch was launched
 }
 
 // NewHostBatch allocates a HostBatch for up to `cap` pods (18 B per pod).
@@ -232,8 +364,11 @@ func NewHostBatch(cap int) (*HostBatch, error) {
 
 // pack writes the pods' PreScore / Filter inputs: the name suffix digit (NodeNumber.PreScore,
 // nodenumber.go:50-64) and whether the tolerations tolerate the unschedulable taint
-// (NodeUnschedulable.Filter, upstream v1.22.0).
-func (b *HostBatch) pack(pods []*v1.Pod) error {
+// (NodeUnschedulable.Filter, upstream v1.22.0), and keeps the Ctx's current index -> node mapping:
+// the launch reads the table version published now, so its indices decode against this mapping even
+// if UploadNodes replaces it before Wait (an upload builds a new slice; UpdateNodes keeps names and
+// positions).
+func (x *Ctx) pack(b *HostBatch, pods []*v1.Pod) error {
 	if len(pods) > b.cap {
 		return fmt.Errorf("gpusched: batch of %d pods exceeds the HostBatch capacity %d", len(pods), b.cap)
 	}
@@ -245,6 +380,7 @@ func (b *HostBatch) pack(pods []*v1.Pod) error {
 		}
 	}
 	b.pods = pods
+	b.byIndex = x.byIndex
 	return nil
 }
 
@@ -255,10 +391,10 @@ func (x *Ctx) results(b *HostBatch) []Result {
 	for j, pod := range b.pods {
 		switch b.status[j] {
 		case C.MSH_PLACED:
-			out[j] = Result{Node: x.byIndex[b.idx[j]], Score: int64(b.score[j])}
+			out[j] = Result{Node: b.byIndex[b.idx[j]], Score: int64(b.score[j])}
 		case C.MSH_FIT_ERROR:
 			diag := framework.Diagnosis{NodeToStatusMap: framework.NodeToStatusMap{}, UnschedulablePlugins: sets.NewString()}
-			if len(x.byIndex) > 0 { // some node failed NodeUnschedulable
+			if len(b.byIndex) > 0 { // some node failed NodeUnschedulable
 				diag.UnschedulablePlugins.Insert("NodeUnschedulable")
 			}
 			out[j] = Result{FitErr: &framework.FitError{Pod: pod, Diagnosis: diag}} // as minisched.go:143-148
@@ -274,7 +410,7 @@ func (x *Ctx) ScheduleBatch(pods []*v1.Pod, b *HostBatch) ([]Result, error) {
 	if !x.hasNodes {
 		return nil, errors.New("gpusched: UploadNodes has not been called")
 	}
-	if err := b.pack(pods); err != nil {
+	if err := x.pack(b, pods); err != nil {
 		return nil, err
 	}
 	p := len(pods)
@@ -295,7 +431,7 @@ func (x *Ctx) Submit(pods []*v1.Pod, b *HostBatch) error {
 	if b.ticket != 0 {
 		return errors.New("gpusched: HostBatch has a batch in flight; Wait for it first")
 	}
-	if err := b.pack(pods); err != nil {
+	if err := x.pack(b, pods); err != nil {
 		return err
 	}
 	p := len(pods)
@@ -327,7 +463,7 @@ func (x *Ctx) ScheduleSequential(pods []*v1.Pod, b *HostBatch, maxPodsPerNode in
 	if !x.hasNodes {
 		return nil, errors.New("gpusched: UploadNodes has not been called")
 	}
-	if err := b.pack(pods); err != nil {
+	if err := x.pack(b, pods); err != nil {
 		return nil, err
 	}
 	p := len(pods)

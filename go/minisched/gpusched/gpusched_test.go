@@ -246,6 +246,91 @@ func TestBatchMatchesReferencePlugins(t *testing.T) {
 	compare(t, rp, append(r1, r2...), pods, x.byIndex)
 }
 
+// The informer path of batch.go (verdict r3 #6): nodes arrive through NodeSnapshot's handlers; a
+// cordon flip between two batches (the Node Update handler, eventhandler.go:45-65) reaches the device
+// as a patch, not a re-upload, and the second batch sees it; an Add then forces one upload. Mirrored
+// on the Python side by tests/test_pipeline.py::test_node_cache_cordon_flip_between_batches_gpu.
+func TestNodeSnapshotCordonFlipBetweenBatches(t *testing.T) {
+	rp := newRefPlugins(t)
+	x := newDevice(t, rp)
+	defer x.Close()
+	nodes, pods := synth(2000, 4000, 0x5eed)
+	snap := NewNodeSnapshot()
+	for i := range nodes {
+		snap.OnAdd(&nodes[i])
+	}
+	if kind, err := snap.Sync(x); err != nil || kind != "upload" {
+		t.Fatalf("first sync: %q %v", kind, err)
+	}
+	b, err := NewHostBatch(len(pods))
+	if err != nil {
+		t.Fatal(err)
+	}
+	got, err := x.ScheduleBatch(pods, b)
+	if err != nil {
+		t.Fatal(err)
+	}
+	compare(t, rp, got, pods, x.byIndex)
+	if kind, _ := snap.Sync(x); kind != "clean" {
+		t.Fatalf("no event: want clean, got %q", kind)
+	}
+	// cordon the first schedulable node of the List and uncordon the first unschedulable one
+	var flips []*v1.Node
+	for _, n := range x.byIndex {
+		if (len(flips) == 0 && !n.Spec.Unschedulable) || (len(flips) == 1 && n.Spec.Unschedulable) {
+			c := n.DeepCopy()
+			c.Spec.Unschedulable = !c.Spec.Unschedulable
+			snap.OnUpdate(n, c)
+			flips = append(flips, c)
+		}
+	}
+	if kind, err := snap.Sync(x); err != nil || kind != "patch" {
+		t.Fatalf("cordon flip: want patch, got %q %v", kind, err)
+	}
+	got, err = x.ScheduleBatch(pods, b)
+	if err != nil {
+		t.Fatal(err)
+	}
+	compare(t, rp, got, pods, x.byIndex) // the reference loop over the updated snapshot
+	snap.OnAdd(&v1.Node{ObjectMeta: metav1.ObjectMeta{Name: "node0000"}})
+	if kind, err := snap.Sync(x); err != nil || kind != "upload" {
+		t.Fatalf("add: want upload, got %q %v", kind, err)
+	}
+	got, err = x.ScheduleBatch(pods, b)
+	if err != nil {
+		t.Fatal(err)
+	}
+	compare(t, rp, got, pods, x.byIndex)
+}
+
+// An upload between Submit and Wait must not change how the batch in flight decodes (advisor r3):
+// the launch read the table published at Submit, and Wait maps its indices through that table's nodes.
+func TestWaitDecodesAgainstTheSubmittedTable(t *testing.T) {
+	rp := newRefPlugins(t)
+	x := newDevice(t, rp)
+	defer x.Close()
+	nodes, pods := synth(1000, 2000, 0x77)
+	before, err := x.UploadNodes(nodes)
+	if err != nil {
+		t.Fatal(err)
+	}
+	b, err := NewHostBatch(len(pods))
+	if err != nil {
+		t.Fatal(err)
+	}
+	if err := x.Submit(pods, b); err != nil {
+		t.Fatal(err)
+	}
+	if _, err := x.UploadNodes(nodes[:500]); err != nil { // a different table, published meanwhile
+		t.Fatal(err)
+	}
+	got, err := x.Wait(b)
+	if err != nil {
+		t.Fatal(err)
+	}
+	compare(t, rp, got, pods, before)
+}
+
 func BenchmarkReferenceLoopC3(b *testing.B) {
 	rp := newRefPlugins(b)
 	nodes, pods := synth(5000, 2000, 0x6d696e69) // a bounded sample of the 100k-pod batch

@@ -197,11 +197,12 @@ int msh_wait(msh_ctx* ctx, uint64_t ticket);
 
 /* Same, device-resident inputs/outputs, asynchronous on `stream` (hipStream_t).
  * Launches on different streams may overlap (independent batches pipelined): each needs its own
- * pod and output buffers. The ctx's node tables are read-only during batches; when an upload,
- * patch or plugin change left them to be re-prepared, the first launch after it prepares them and
- * waits for that before returning. The ctx records an event on `stream` after each launch: a later
- * upload, patch, plugin change or count reset of THIS ctx is ordered after the ctx's own launches
- * in flight (on its internal stream), and never waits for other ctxs' or the caller's other work. */
+ * pod and output buffers. The node table is double-buffered: an upload, patch, score-column upload or
+ * filter-list change rebuilds the version no launch reads, on the ctx's own high-priority stream,
+ * and publishes it before the call returns (the rebuild is synchronous; launches made after it read
+ * the new version, launches already queued keep reading the old one). The ctx records an event on
+ * `stream` after each launch; a rebuild waits on the host only for the launches of two rebuilds ago,
+ * which read the version it overwrites, and never for other ctxs' or the caller's other work. */
 int msh_schedule_batch_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit,
                               const uint8_t* d_pod_tol, int32_t* d_out_idx,
                               int64_t* d_out_score, int32_t* d_out_status, void* stream);

@@ -28,6 +28,7 @@
 #include <iterator>
 #include <mutex>
 #include <new>
+#include <optional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -53,8 +54,11 @@ struct CopyJob {
 void par_copy(const CopyJob* jobs, int n_jobs) {
   size_t total = 0;
   for (int i = 0; i < n_jobs; ++i) total += jobs[i].bytes;
-  PoolLease lease;
-  HostPool* pool = total >= (256u << 10) ? lease.get() : nullptr;
+  // small copies stay on the calling thread without touching the pool (no lease, no busy flag: a
+  // concurrent large pack keeps every pool thread)
+  std::optional<PoolLease> lease;
+  if (total >= (256u << 10)) lease.emplace();
+  HostPool* pool = lease ? lease->get() : nullptr;
   if (!pool) {
     for (int i = 0; i < n_jobs; ++i) std::memcpy(jobs[i].dst, jobs[i].src, jobs[i].bytes);
     return;
@@ -880,37 +884,48 @@ int msh_set_plugins_ex(msh_ctx* c, const int32_t* filter_ids, int32_t nf,
     const int32_t m = normalize ? normalize[i] : MSH_NORMALIZE_NONE;
     if (m < MSH_NORMALIZE_NONE || m > MSH_NORMALIZE_MINMAX) return fail(c, MSH_ERR_INVALID, "bad normalize mode");
   }
-  c->filter_ids.assign(filter_ids, filter_ids + nf);
-  c->prescore_ids.assign(prescore_ids, prescore_ids + npre);
-  c->score_ids.assign(score_ids, score_ids + ns);
-  c->weights.clear();
-  c->normalize.clear();
+  std::vector<int32_t> f_ids(filter_ids, filter_ids + nf), p_ids(prescore_ids, prescore_ids + npre),
+      s_ids(score_ids, score_ids + ns), norms;
+  std::vector<int64_t> ws;
   for (int32_t i = 0; i < ns; i++) {
-    c->weights.push_back(weights ? weights[i] : 1);
-    c->normalize.push_back(normalize ? normalize[i] : MSH_NORMALIZE_NONE);
+    ws.push_back(weights ? weights[i] : 1);
+    norms.push_back(normalize ? normalize[i] : MSH_NORMALIZE_NONE);
   }
   PluginParams pp{};
-  pp.has_nu_filter = contains(c->filter_ids, MSH_PLUGIN_NODE_UNSCHEDULABLE) ? 1 : 0;
-  pp.nn_prescore = contains(c->prescore_ids, MSH_PLUGIN_NODE_NUMBER) ? 1 : 0;
+  pp.has_nu_filter = contains(f_ids, MSH_PLUGIN_NODE_UNSCHEDULABLE) ? 1 : 0;
+  pp.nn_prescore = contains(p_ids, MSH_PLUGIN_NODE_NUMBER) ? 1 : 0;
   pp.has_nn_score = 0;
   pp.mode = MSH_NORMALIZE_NONE;
   pp.weight = 1;
+  bool generic = false;
   for (int32_t i = 0; i < ns; i++) {
-    if (c->score_ids[i] == MSH_PLUGIN_NODE_NUMBER) {
+    if (s_ids[i] == MSH_PLUGIN_NODE_NUMBER) {
       pp.has_nn_score = 1;
-      pp.mode = c->normalize[i];
-      pp.weight = c->weights[i];
+      pp.mode = norms[i];
+      pp.weight = ws[i];
     }
+    generic = generic || is_column(s_ids[i]);
   }
-  const bool reprep = pp.has_nu_filter != c->pp.has_nu_filter;  // the X words depend on the filter list
-  c->pp = pp;
-  c->generic = false;
-  for (int32_t i = 0; i < ns; i++) c->generic = c->generic || is_column(c->score_ids[i]);
-  if (reprep && c->have_nodes) {
+  // The filter planes depend on the filter list: rebuild the table first, and publish the new plugin
+  // set only once the rebuild succeeded (a failed rebuild leaves the old set with its old table).
+  if (pp.has_nu_filter != c->pp.has_nu_filter && c->have_nodes) {
+    const PluginParams old = c->pp;
+    c->pp = pp;  // rewrite() builds the X plane and the node records from c->pp
     DeviceGuard g(c->device);
     Rewrite w{Rewrite::REPREP};
-    return rewrite(c, w);
+    const int rc2 = rewrite(c, w);
+    if (rc2 != MSH_OK) {
+      c->pp = old;
+      return rc2;
+    }
   }
+  c->filter_ids = std::move(f_ids);
+  c->prescore_ids = std::move(p_ids);
+  c->score_ids = std::move(s_ids);
+  c->weights = std::move(ws);
+  c->normalize = std::move(norms);
+  c->pp = pp;
+  c->generic = generic;
   return MSH_OK;
 }
 

@@ -367,3 +367,40 @@ def test_loop_random_stream_gpu_vs_oracle(gpu_ctx, seed):
     lg, cg = make_loop(ctx=gpu_ctx)
     lo, co = make_loop()
     assert drive(lg, cg, events) == drive(lo, co, events)
+
+
+@pytest.mark.gpu
+def test_node_cache_cordon_flip_between_batches_gpu(gpu_ctx, oracle):
+    """The informer path the Go binding runs (go/minisched/gpusched NodeSnapshot.Sync, verdict r3 #6):
+    nodes arrive through the Add handler (one upload), a cordon flip between two batches through the
+    Update handler reaches the device as a patch (msh_patch_nodes), not a re-upload, and the second
+    batch sees it; an Add then forces one upload. Every batch bit-exact vs the oracle on the cache's
+    List-order columns. The Go test of the same sequence: TestNodeSnapshotCordonFlipBetweenBatches."""
+    gpu_ctx.set_plugins(["NodeUnschedulable"], ["NodeNumber"], [S.ScorePluginConfig("NodeNumber")])
+    rng = random.Random(0x5eed)
+    nodes = [O.Node(f"node{i}", rng.random() < 0.1) for i in range(2000)]
+    rng.shuffle(nodes)
+    pd = np.array([rng.randrange(-1, 10) for _ in range(4000)], np.int8)
+    pt = np.array([rng.random() < 0.05 for _ in range(4000)], np.uint8)
+    cache = NC.NodeCache()
+    for n in nodes:
+        cache.add(n)
+
+    def check():
+        got = gpu_ctx.schedule_batch(pd, pt)
+        want = oracle.c_schedule_batch(cache.unsched, cache.digit, pd, pt)
+        assert all((g == w).all() for g, w in zip(got, want[:3]))
+
+    assert cache.sync(gpu_ctx) == "upload"
+    check()
+    assert cache.sync(gpu_ctx) == "clean"
+    first_ok = next(i for i in range(len(cache)) if cache.unsched[i] == 0)
+    first_cordoned = next(i for i in range(len(cache)) if cache.unsched[i] == 1)
+    for i in (first_ok, first_cordoned):
+        name, u = cache.names[i], bool(cache.unsched[i])
+        cache.update(O.Node(name, u), O.Node(name, not u))
+    assert cache.sync(gpu_ctx) == "patch"
+    check()
+    cache.add(O.Node("node0000"))
+    assert cache.sync(gpu_ctx) == "upload"
+    check()
