@@ -7,21 +7,26 @@ minisched/minisched.go:50-87 for every pod of a batch) over one batch of synthet
 inputs already resident in HBM.
 
 Modes (the headline line)
-  batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per batch per GPU. With N GPUs the
-              pods are sharded (each rank its own 100k batches; no data-path collective) -> weak
-              scaling. The K steps are K independent batches (32 distinct pod batches, each with
-              its own outputs, used in turn) submitted from one host thread on one HIP stream
-              through msh_schedule_batches_device, MSH_BATCHES_PER_LAUNCH (32) batches per kernel
-              launch: the submission a caller with several drained batches ready makes.
+  batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per batch per GPU, on pair_kernel, the
+              per-pair kernel (every (pod, node) pair's filter and score evaluated from the node's and
+              the pod's own bits, 32 pairs per 32-bit lane-op). With N GPUs the pods are sharded (each
+              rank its own 100k batches; no data-path collective) -> weak scaling. The K steps are K
+              independent batches (32 distinct pod batches, each with its own outputs, used in turn)
+              submitted from one host thread on one HIP stream through msh_schedule_batches_device,
+              MSH_BATCHES_PER_LAUNCH (32) batches per kernel launch: the submission a caller with
+              several drained batches ready makes.
   sequential  BASELINE C5: same sizes, one pod at a time with node-state commits.
-  nodeshard   BASELINE C4 shape: the node table split over the ranks, per-shard first keys
-              merged with an RCCL all-reduce(MAX), then decoded (--nodes 100000 --pods 1000000).
+  nodeshard   BASELINE C4 shape: the node table split over the ranks, per-pod first keys of every
+              shard merged with an RCCL all-reduce(MAX), then decoded (--nodes 100000 --pods 1000000).
 
-With one GPU, rank 0 also measures the other BASELINE configs and paths after the timed region
-and reports them as extra keys of the same line: C3 with weight 3 + DefaultNormalizeScore, C3 with
-min-max normalisation, C5 sequential, C4 (100k nodes x 1M pods) on one GPU (whole table, and the
-node-shard keys + decode of a one-rank shard), C2, and the host-buffer path (e2e: the C-ABI call a
-cgo caller makes, PCIe included). Every one is checked bit-exact against the closed form.
+With one GPU, rank 0 also measures, after the timed region, and reports as extra keys of the same
+line: generic_kernel (the explicit int64 score per pair, north_star's five stages) on the reference
+plugin list and on NodeNumber + a DEFAULT-normalized score column; the opt-in class-row kernel
+(pod verdicts read from per-class tables: reported apart, never as `value`); C3 with weight 3 +
+DefaultNormalizeScore, MIN-MAX and REVERSE; C5 sequential; C4 (100k nodes x 1M pods) on one GPU;
+C2; and the host-buffer path (e2e: the C-ABI call a cgo caller makes, PCIe included). Each is checked
+bit-exact against an independent checker (tests/closed_form.py; a sampled direct evaluation for the
+score-column list).
 
 Launch: `python bench.py` (1 GPU) or
 `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N`.
@@ -46,15 +51,17 @@ sys.path.insert(0, str(ROOT))
 METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
 CLOCK_HZ = 2.4e9                   # MI355X_MICROARCH.md: max clock
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# The persistent class-row kernel (wgp_kernel, tables up to 8,192 nodes; the identity-like modes):
-# per 256-node group and 64-pod wave, two ds_read_b128 of the lanes' class-row entries = 2 KiB
-# through the LDS array (1/8 B per pod-node pair), and 5.5 VALU (four groups per step: 16 v_bitop3
-# OR3 over the 32 words, two pair flags of v_min + v_lshl_or, two address adds).
-LDS_PEAK = 150e12                  # MI355X_MICROARCH.md: ~150 TB/s aggregate for ds_read_b64/b128
-WGP_MAX_GROUPS = 32                # msh_kernels.hip: the persistent kernel's table limit (groups of 256 nodes)
-LDS_BYTES_PER_GROUP_WAVE = 2 * 1024
-VALU_PER_GROUP_WAVE = 5.5
-PMC_FILE = ROOT / "profiles" / "r3_pmc_c3.json"
+LANES_PER_SIMD_CYCLE = 32          # MI355X_MICROARCH.md: SIMD-32, a wave64 VALU instruction over 2 cycles
+# pair_kernel's scan (msh_kernels.hip): per 32-node word and 64-pod wave, v_bitop3 (X & nT) + 4 v_bitop3
+# (the code-bit mismatches ORed in: dm'), half a v_bitop3 AND3 (two words' dm' into the group's match
+# flag) and one v_bitop3 OR-accumulate of the feasible non-matches: 6.5 VALU per 32 x 64 pairs
+PAIR_VALU_PER_WORD = 6.5
+# generic_kernel's main sweep on the reference list (NodeNumber only): per pair v_cmp_eq (suffix
+# digits), 2 v_cndmask (the lane's two weighted values), v_cmp_gt_i64 (strict first max), 3 v_cndmask
+# (best total, chunk-relative index): 7 VALU lane-ops per pair
+GEN_VALU_PER_PAIR_REF = 7.0
+WGP_MAX_GROUPS = 32                # msh_kernels.hip: the class-row kernel's table limit (groups of 256 nodes)
+PMC_FILE = ROOT / "profiles" / "r4_pmc_c3.json"
 VALU_PEAK_FILE = ROOT / "profiles" / "r3_ubench_valu_peak.json"
 
 
@@ -389,14 +396,59 @@ def load_valu_peak():
     return d.get("scan_forms_wave_instr_per_simd_cycle") or d.get("int_valu_wave_instr_per_simd_cycle"), d
 
 
-def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
-    """Roofline of the dominant kernel, per launch: algorithmic bytes (or instructions) of one
-    launch / the launch's average duration, measured with HIP events on the launch stream around
-    each of R launches (bench.py main), the quantity rocprofv3's per-kernel average reports."""
+def pmc_entry(key: str, kname: str, n_local: int, p: int, nb: int):
+    """The profiles/r4_pmc_c3.json entry for this kernel, size and batch count (None if it does not
+    match what this run timed)."""
+    e = (load_json(PMC_FILE) or {}).get("kernels", {}).get(key, {})
+    ok = (e.get("kernel") == kname and e.get("nodes") == n_local and e.get("pods") == p
+          and e.get("batches_per_launch", 1) == nb)
+    return e if ok else None
+
+
+def valu_roofline(kname, launch_ms, evals, model_lane_ops_per_eval, cus, entry, model_note):
+    """VALU roofline of an integer kernel: the modelled lane-ops per launch (the kernel's per-pair
+    instruction count x the pairs it evaluates) / the launch's duration, against the MI355X VALU peak
+    (CUs x 4 SIMD x 32 lanes per cycle x 2.4 GHz); the counter form uses rocprofv3 SQ_INSTS_VALU x 64
+    of the same kernel, size and batch count (profiles/r4_pmc_c3.json)."""
     launch_s = launch_ms * 1e-3
-    pmc = load_json(PMC_FILE) or {}
-    ipc, peak_src = load_valu_peak()
-    valu_peak = (ipc * 4 * 64 * cus * CLOCK_HZ) if ipc else None  # lane-ops/s
+    peak = cus * 4 * LANES_PER_SIMD_CYCLE * CLOCK_HZ  # lane-ops/s
+    ipc, _ = load_valu_peak()
+    peak_meas = ipc * 4 * 64 * cus * CLOCK_HZ if ipc else None
+    model = evals * model_lane_ops_per_eval
+    instr = entry.get("SQ_INSTS_VALU") if entry else None
+    cnt = instr * 64 if instr else None
+    return {
+        "bound": "valu",
+        "achieved": model / launch_s / 1e9,
+        "peak": peak / 1e9,
+        "unit": "Glane-op/s",
+        "frac": model / launch_s / peak,
+        "traffic": entry.get("hbm_bytes_per_launch") if entry else None,
+        "traffic_note": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024), same kernel, size and batches",
+        "kernel": kname,
+        "kernel_ms": launch_ms,
+        "kernel_ms_note": ("mean duration of R back-to-back launches, each timed from the kernel's own start "
+                           "to its completion (msh_timing_begin / _end: hipExtLaunchKernelGGL events), the "
+                           "interval rocprofv3's kernel trace averages"),
+        "lane_ops_per_eval_model": model_lane_ops_per_eval,
+        "model": model_note,
+        "lane_ops_per_eval_counter": cnt / evals if cnt else None,
+        "frac_counter": cnt / launch_s / peak if cnt else None,
+        "counter_source": (f"rocprofv3 SQ_INSTS_VALU x 64 per launch ({PMC_FILE.name})" if cnt
+                           else "no PMC entry for this kernel, size and batch count"),
+        "peak_note": "MI355X_MICROARCH.md: SIMD-32 (a wave64 VALU instruction over 2 cycles), 4 SIMD per CU, 2.4 GHz",
+        "peak_measured_issue": peak_meas / 1e9 if peak_meas else None,
+        "frac_of_measured_issue": model / launch_s / peak_meas if peak_meas else None,
+        "peak_measured_note": ("the integer VALU issue rate measured for v_bitop3-class forms (8 waves per SIMD, "
+                               f"{VALU_PEAK_FILE.name}): {ipc:.3f} wave-instr per SIMD-cycle" if ipc else None),
+    }
+
+
+def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
+    """Roofline of the dominant kernel, per launch: algorithmic work of one launch / the launch's
+    average duration, measured with HIP events at the kernel's start and completion (bench.py main),
+    the quantity rocprofv3's per-kernel average reports."""
+    launch_s = launch_ms * 1e-3
     if mode == "sequential":
         # One wave decides the pods in order; alone on its SIMD it issues about one instruction per
         # 4 cycles of any kind (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so the floor
@@ -404,79 +456,59 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
         # this kernel at C5) x 4 cycles at 2.4 GHz. That is an issue floor of the code as written,
         # not a hardware roofline: reported as issue_floor_frac, not frac.
         kname = seq_kernel_label(n_local)
-        entry = pmc.get("kernels", {}).get("sequential", {})
-        ok = entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
-        instr = (entry.get("SQ_INSTS_VALU", 0) + entry.get("SQ_INSTS_SALU", 0)) / p if ok else None
+        entry = pmc_entry("sequential", kname, n_local, p, 1)
+        instr = (entry.get("SQ_INSTS_VALU", 0) + entry.get("SQ_INSTS_SALU", 0)) / p if entry else None
         floor_us = instr * 4 / 2.4e3 if instr else None
         achieved = launch_ms * 1e3 / p
         return {"bound": "issue latency (one wave, serial)", "achieved": achieved, "unit": "us/pod",
                 "issue_floor_us_per_pod": floor_us,
                 "issue_floor_frac": floor_us / achieved if floor_us else None,
                 "kernel": kname, "kernel_ms": launch_ms,
-                "traffic": entry.get("hbm_bytes_per_launch") if ok else None,
+                "traffic": entry.get("hbm_bytes_per_launch") if entry else None,
                 "instructions_per_pod": instr,
                 "note": "a serial mode: the floor is the kernel's own instruction count per pod (rocprofv3 "
                         "SQ_INSTS_VALU + SQ_INSTS_SALU / pods) x 4 cycles / 2.4 GHz, not a hardware roofline"}
-    multi = batches_per_launch > 1
-    kname = batch_kernel_label(n_local, p, cus, shard=mode == "nodeshard", multi=multi, nb=batches_per_launch)
-    evals = float(n_local) * p * batches_per_launch
-    entry = pmc.get("kernels", {}).get("batch_multi" if multi else "batch", {})
-    pmc_ok = (entry.get("kernel") == kname and entry.get("nodes") == n_local and entry.get("pods") == p
-              and entry.get("batches_per_launch", 1) == batches_per_launch)
-    n_groups = max(-(-n_local // 1024) * 1024, 1024) // 256
-    group_waves = float(n_groups) * -(-p // 64) * batches_per_launch  # every 64-pod wave meets every group once
-    # achieved = ALGORITHMIC LDS-array bytes of the scan per launch (2 KiB per 256-node group and 64-pod
-    # wave: the lane's two 16-byte class-row reads, 1/8 B per pod-node pair) / the launch's duration
-    lds_bytes = group_waves * LDS_BYTES_PER_GROUP_WAVE
-    lds_cycles = entry.get("SQ_LDS_IDX_ACTIVE") if pmc_ok else None
-    model_instr = group_waves * VALU_PER_GROUP_WAVE  # wave-instructions of the scan
-    valu_instr = entry.get("SQ_INSTS_VALU") if pmc_ok else None
-    uniq_bytes = (3.375 * n_local + 18.0 * p * batches_per_launch)  # class rows once, pod records + outputs
-    survey_bytes = 2.0 * n_local * p * batches_per_launch + 18.0 * p * batches_per_launch
-    out = {
-        "bound": "lds",
-        "achieved": lds_bytes / launch_s / 1e9,
-        "peak": LDS_PEAK / 1e9,
-        "unit": "GB/s",
-        "frac": lds_bytes / launch_s / LDS_PEAK,
-        "traffic": entry.get("hbm_bytes_per_launch") if pmc_ok else None,
-        "traffic_note": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024), same kernel, size and batches",
-        "kernel": kname,
-        "kernel_ms": launch_ms,
-        "kernel_ms_note": ("mean duration of R back-to-back launches, each timed from the kernel's own start "
-                           "to its completion (msh_timing_begin / _end: hipExtLaunchKernelGGL events), the "
-                           "interval rocprofv3's kernel trace averages"),
-        "batches_per_launch": batches_per_launch,
-        "ms_per_batch": launch_ms / batches_per_launch,
-        "lds_bytes_per_launch": lds_bytes,
-        "lds_bytes_per_eval": lds_bytes / evals,
-        "frac_counter": (lds_cycles / (cus * launch_s * LDS_PEAK / (256 * 256))) if lds_cycles else None,
-        "counter_source": (f"rocprofv3 SQ_LDS_IDX_ACTIVE per launch ({PMC_FILE.name})" if lds_cycles
-                           else "no PMC entry for this kernel, size and batch count"),
-        "peak_note": "MI355X_MICROARCH.md LDS: 256 B/clk/CU for ds_read_b128, ~150 TB/s aggregate",
-        "valu": {"bound": "valu (integer, measured issue rate)", "unit": "Gwave-instr/s",
-                 "peak": (valu_peak / 64 / 1e9) if valu_peak else None,
-                 "peak_source": (f"{VALU_PEAK_FILE.name}: {ipc:.3f} wave64 integer instructions per SIMD-cycle "
-                                 f"x 1,024 SIMDs x 2.4 GHz" if ipc else "unmeasured"),
-                 "achieved_model": model_instr / launch_s / 1e9,
-                 "frac_model": (model_instr / launch_s / (valu_peak / 64)) if valu_peak else None,
-                 "instr_per_group_wave_model": VALU_PER_GROUP_WAVE,
-                 "instr_measured": valu_instr,
-                 "frac_counter": (valu_instr / launch_s / (valu_peak / 64)) if (valu_instr and valu_peak) else None,
-                 "scan_share_of_valu": model_instr / valu_instr if valu_instr else None},
-        "hbm": {"bound": "hbm", "achieved": uniq_bytes / launch_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": uniq_bytes / launch_s / HBM_PEAK, "bytes_per_launch": uniq_bytes,
-                "survey_8d_bytes_per_launch": survey_bytes,
-                "survey_8d_frac": survey_bytes / launch_s / HBM_PEAK,
-                "survey_8d_note": "2 B per pair counts every L1/L2/LDS re-read of the node table as HBM "
-                                  "traffic; the 17 KB class-row table is read from HBM (L2) once per workgroup"},
-    }
+    nb = batches_per_launch
+    kname = batch_kernel_label(n_local, p, cus, shard=mode == "nodeshard", multi=nb > 1, nb=nb)
+    evals = float(n_local) * p * nb
+    n_pad = max(-(-n_local // 1024) * 1024, 1024)
+    # every 64-pod wave meets every 32-node word of the padded table once
+    model_per_eval = PAIR_VALU_PER_WORD * (n_pad / 32) * (-(-p // 64) * 64) / (float(n_local) * p)
+    entry = pmc_entry("pair_multi" if nb > 1 else "pair_single", kname, n_local, p, nb)
+    out = valu_roofline(kname, launch_ms, evals, model_per_eval, cus, entry,
+                        "6.5 VALU per 32-node word and 64-pod wave (pair_kernel's scan, msh_kernels.hip): per "
+                        "lane-op 32 (pod, node) pairs get NodeUnschedulable's verdict and NodeNumber's digit "
+                        "compare; lane-ops per eval = 6.5 x padded words x padded pods / (n x p)")
+    out["batches_per_launch"] = nb
+    out["ms_per_batch"] = launch_ms / nb
+    # HBM: the bit planes once (0.75 B per node: 6 planes of 32 nodes per 4 B), 2 B in + 16 B out per pod
+    uniq = 0.75 * n_pad + 18.0 * p * nb
+    out["hbm"] = {"bound": "hbm", "achieved": uniq / launch_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                  "frac": uniq / launch_s / HBM_PEAK, "bytes_per_launch": uniq,
+                  "note": "unique algorithmic bytes: the table is read by every wave through the scalar "
+                          "cache / L2, never re-fetched from HBM (traffic, above, is the counter)"}
     return out
 
 
+def multi_launch_ms(torch, ctx, descs, nb, R, stream):
+    """Mean kernel duration of R launches of nb batches (msh_timing_begin / _end), after 3 untimed."""
+    for _ in range(3):
+        ctx.schedule_batches_device(descs, nb, stream)
+    torch.cuda.synchronize()
+    ctx.timing_begin(R)
+    for _ in range(R):
+        ctx.schedule_batches_device(descs, nb, stream)
+    n_t, tot, _ = ctx.timing_end()
+    torch.cuda.synchronize()
+    return tot / max(n_t, 1)
+
+
 def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
-    """Secondary BASELINE configs and the host-buffer path, each timed and checked bit-exact."""
+    """Secondary BASELINE configs, the generic and class-row kernels, and the host-buffer path, each
+    timed and checked bit-exact."""
+    from closed_form import direct_plugins
     out = {}
+    G = msh._native.BATCHES_PER_LAUNCH
 
     def dbufs(pd, pt):
         p = len(pd)
@@ -489,42 +521,98 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     def same(a, b):
         return all((x == y).all() for x, y in zip(a, b))
 
+    def new_ctx(kernel=None):
+        if kernel:
+            os.environ["MSH_BATCH_KERNEL"] = kernel  # read once by msh_create
+        try:
+            return msh.DeviceContext(dev.index or 0)
+        finally:
+            os.environ.pop("MSH_BATCH_KERNEL", None)
+
     S2 = Streams(torch, dev, 2)
+    sh = torch.cuda.current_stream(dev).cuda_stream
 
-    def batch_rate(ctx, n, pairs, k, norm=0, weight=1):
-        """ms per batch of k launches over 2 streams (2 independent pod batches)."""
-        bs = [dbufs(*pp) for pp in pairs]
-        p = len(pairs[0][0])
-        launch = lambda i, sh: ctx.schedule_batch_device(p, *[t.data_ptr() for t in bs[i % 2]], sh)
-        S2.time(launch, 4)
-        ms = S2.time(launch, k)
-        ok = all(same(got(b), closed_form_modes(*ctx_nodes[ctx], pp[0], pp[1], weight, norm)) for b, pp in zip(bs, pairs))
-        return ms, ok
-
-    ctx_nodes = {}
-    # ---- C3 (5k x 100k): weight 3 + DefaultNormalizeScore, and min-max (north_star stage 3) ----
+    # ---- C3 (5k x 100k): 32 batches per launch, on several kernels and plugin lists ----
     n, p = 5000, 100_000
     u, nd = synth.make_nodes(n)[1:]
-    pd_all, pt_all = synth._make_pods_fast(2 * p, synth.SEED)[1:]
-    pairs = [(np.ascontiguousarray(pd_all[:p]), np.ascontiguousarray(pt_all[:p])),
-             (np.ascontiguousarray(pd_all[p:]), np.ascontiguousarray(pt_all[p:]))]
-    ctx = msh.DeviceContext(dev.index or 0)
+    pd_all, pt_all = synth._make_pods_fast(G * p, synth.SEED + 1)[1:]
+    pods = [(np.ascontiguousarray(pd_all[i * p:(i + 1) * p]), np.ascontiguousarray(pt_all[i * p:(i + 1) * p]))
+            for i in range(G)]
+    bufs = [dbufs(*pp) for pp in pods]
+    descs = msh.DeviceContext.batch_descs([(p, *[t.data_ptr() for t in b]) for b in bufs])
+
+    def run_multi(ctx, R=20):
+        for b in bufs:
+            b[2].fill_(-7)
+        return multi_launch_ms(torch, ctx, descs, G, R, sh)
+
+    def check_all(weight=1, norm=0):
+        return all(same(got(b), closed_form_modes(u, nd, pp[0], pp[1], weight, norm)) for b, pp in zip(bufs, pods))
+
+    ctx = new_ctx()
     ctx.upload_nodes(u, nd)
-    ctx_nodes[ctx] = (u, nd)
     variants = {}
     for name, weight, norm in (("weight3_default_normalize", 3, 1), ("minmax_normalize", 1, 3),
                                ("reverse_normalize", 1, 2)):
         ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                         [msh.ScorePluginConfig(msh.NODE_NUMBER, weight, msh.Normalize(norm))])
-        ms, ok = batch_rate(ctx, n, pairs, 100, norm, weight)
-        variants[name] = {"kernel": batch_kernel_label(n, p, cus, kx=norm in (2, 3)), "ms_per_step": ms,
-                          "evals_per_s": n * p / (ms * 1e-3), "streams": 2,
-                          "check": "bit-exact vs closed form" if ok else "MISMATCH"}
+        ms = run_multi(ctx)
+        variants[name] = {"kernel": batch_kernel_label(n, p, cus, multi=True, nb=G), "kernel_ms": ms,
+                          "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
+                          "check": "bit-exact vs closed form" if check_all(weight, norm) else "MISMATCH"}
     out["c3_normalize_variants"] = variants
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
 
+    # ---- generic_kernel: an explicit int64 score per (pod, node) pair (north_star's five stages) ----
+    gen = {}
+    gctx = new_ctx("generic")  # every plugin list on generic_kernel (the reference list included)
+    gctx.upload_nodes(u, nd)
+    gctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+    ms = run_multi(gctx, R=5)
+    kname = "void msh::generic_kernel<1, 0, 0>"
+    rl = valu_roofline(kname, ms, float(n) * p * G, GEN_VALU_PER_PAIR_REF, cus,
+                       pmc_entry("generic_ref", kname, n, p, G),
+                       "7 VALU per pair (generic_kernel's main sweep, NodeNumber only: v_cmp_eq, 2 v_cndmask for "
+                       "the weighted score, v_cmp_gt_i64, 3 v_cndmask for the running first maximum)")
+    gen["reference_list"] = {"kernel": kname, "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G,
+                             "evals_per_s": n * p * G / (ms * 1e-3), "pods_per_s": p * G / (ms * 1e-3),
+                             "check": "bit-exact vs closed form" if check_all() else "MISMATCH", "roofline": rl}
+    col = (np.arange(n, dtype=np.int64) * 7919) % 1000 - 300
+    plugins = [("NodeNumber", 1, 0), ("ScoreColumn0", 2, 1)]
+    gctx.upload_score_column("ScoreColumn0", col)
+    gctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                     [msh.ScorePluginConfig(nm, w, msh.Normalize(m)) for nm, w, m in plugins])
+    ms = run_multi(gctx, R=5)
+    sample = slice(0, 1500)
+    ok = all(same(tuple(x[sample] for x in got(b)),
+                  direct_plugins(u, nd, pp[0][sample], pp[1][sample], plugins, {0: col}))
+             for b, pp in list(zip(bufs, pods))[:2])
+    kname = "void msh::generic_kernel<1, 1, 0>"
+    entry = pmc_entry("generic_col", kname, n, p, G)
+    gen["nodenumber_plus_default_column"] = {
+        "kernel": kname, "plugins": "score=[NodeNumber w=1, ScoreColumn0 w=2 DefaultNormalizeScore]",
+        "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
+        "lane_ops_per_eval_counter": entry["SQ_INSTS_VALU"] * 64 / (float(n) * p * G) if entry else None,
+        "check": "sampled (1,500 pods of 2 batches) bit-exact vs a direct evaluation" if ok else "MISMATCH"}
+    out["generic"] = gen
+    gctx.close()
+
+    # ---- the opt-in class-row kernel: reported apart, its pods/s (not a per-pair evaluation) ----
+    cctx = new_ctx("classrows")
+    cctx.upload_nodes(u, nd)
+    ms = run_multi(cctx)
+    out["classrows_opt_in"] = {
+        "kernel": batch_kernel_label(n, p, cus, multi=True, nb=G, classrows=True), "kernel_ms": ms,
+        "batches_per_launch": G, "ms_per_batch": ms / G, "pods_per_s": p * G / (ms * 1e-3),
+        "check": "bit-exact vs closed form" if check_all() else "MISMATCH",
+        "note": "MSH_BATCH_KERNEL=classrows: each pod's verdicts are read from per-(tolerates, digit)-class "
+                "tables built at upload, so its per-pod work does not evaluate the pairs; a placement rate "
+                "of a class-specialised path, never the headline evals/s"}
+    cctx.close()
+    del bufs
+
     # ---- e2e: the host-buffer C-ABI call (msh_schedule_batch), PCIe in and out ----
-    pd, pt = pairs[0]
+    pd, pt = pods[0]
     want = closed_form_modes(u, nd, pd, pt)
     hpd, hpt = msh.pinned_empty(p, np.int8), msh.pinned_empty(p, np.uint8)
     hpd[:], hpt[:] = pd, pt
@@ -639,15 +727,19 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
                             "roofline": make_roofline("sequential", n, p, ms, 1, cus)}
     ctx.close()
 
-    # ---- C2: 1k x 10k ----
+    # ---- C2: 1k x 10k, one launch per batch over two streams ----
     n2, p2 = 1000, 10_000
     u2, nd2 = synth.make_nodes(n2)[1:]
     pd2, pt2 = synth._make_pods_fast(2 * p2, synth.SEED)[1:]
-    ctx = msh.DeviceContext(dev.index or 0)
+    ctx = new_ctx()
     ctx.upload_nodes(u2, nd2)
-    ctx_nodes[ctx] = (u2, nd2)
-    ms, ok = batch_rate(ctx, n2, [(np.ascontiguousarray(pd2[:p2]), np.ascontiguousarray(pt2[:p2])),
-                                  (np.ascontiguousarray(pd2[p2:]), np.ascontiguousarray(pt2[p2:]))], 100)
+    pairs2 = [(np.ascontiguousarray(pd2[:p2]), np.ascontiguousarray(pt2[:p2])),
+              (np.ascontiguousarray(pd2[p2:]), np.ascontiguousarray(pt2[p2:]))]
+    bs = [dbufs(*pp) for pp in pairs2]
+    launch = lambda i, sh: ctx.schedule_batch_device(p2, *[t.data_ptr() for t in bs[i % 2]], sh)
+    S2.time(launch, 4)
+    ms = S2.time(launch, 100)
+    ok = all(same(got(b2), closed_form_modes(u2, nd2, pp[0], pp[1])) for b2, pp in zip(bs, pairs2))
     out["c2"] = {"kernel": batch_kernel_label(n2, p2, cus), "ms_per_step": ms, "evals_per_s": n2 * p2 / (ms * 1e-3),
                  "streams": 2, "check": "bit-exact vs closed form" if ok else "MISMATCH"}
     ctx.close()
@@ -657,7 +749,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     u4, nd4 = synth.make_nodes(n4)[1:]
     pd4, pt4 = synth._make_pods_fast(p4, synth.SEED)[1:]
     want4 = closed_form_modes(u4, nd4, pd4, pt4)
-    ctx = msh.DeviceContext(dev.index or 0)
+    ctx = new_ctx()
     ctx.upload_nodes(u4, nd4)
     b4 = dbufs(pd4, pt4)
     launch = lambda i, sh: ctx.schedule_batch_device(p4, *[t.data_ptr() for t in b4], sh)

@@ -1,8 +1,16 @@
-"""Minimal driver for profiling: K launches of a hot kernel on the C3 workload.
+"""Minimal driver for profiling: K launches of a hot kernel on the C3 workload (5,000 nodes x 100,000
+pods per batch, bench.py's synthetic snapshot).
 
-MODE=multi (bench.py's default submission: 32 independent 100k-pod batches per
-msh_schedule_batches_device launch), batch (one msh_schedule_batch_device launch per batch),
-sequential (C5), generic (the explicit int64 score pipeline, NodeNumber + one score column).
+MODE
+  multi        bench.py's default submission: 32 independent batches per msh_schedule_batches_device
+               launch (pair_kernel, the per-pair kernel; with MSH_BATCH_KERNEL=classrows in the
+               environment, the opt-in class-row kernel)
+  batch        one msh_schedule_batch_device launch per batch
+  generic      generic_kernel (explicit int64 score per pair) on the reference plugin list, 32 batches
+               per launch (MSH_BATCH_KERNEL=generic is set here)
+  generic_col  generic_kernel on NodeNumber + ScoreColumn0 (weight 2, DefaultNormalizeScore), 32 batches
+               per launch
+  sequential   C5: one pod at a time (seq_kernel)
 NORM: msh_normalize of the NodeNumber entry (3 = MINMAX)."""
 import importlib
 import os
@@ -10,7 +18,12 @@ import sys
 from pathlib import Path
 
 import numpy as np
-import torch
+
+mode = os.environ.get("MODE", "multi")
+if mode == "generic":
+    os.environ["MSH_BATCH_KERNEL"] = "generic"  # read by msh_create
+
+import torch  # noqa: E402
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
@@ -19,12 +32,11 @@ synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
 n = int(os.environ.get("NODES", 5000))
 p = int(os.environ.get("PODS", 100000))
 k = int(os.environ.get("LAUNCHES", 20))
-mode = os.environ.get("MODE", "multi")
 norm = int(os.environ.get("NORM", 0))
 ctx = msh.DeviceContext(0)
 u, nd, pd, pt = synth.make_soa(n, p)
 ctx.upload_nodes(u, nd)
-if mode == "generic":  # NodeNumber + one score column (weight 2, DefaultNormalizeScore)
+if mode == "generic_col":
     ctx.upload_score_column(msh.SCORE_COLUMNS[0], (np.arange(n, dtype=np.int64) * 7919) % 1000)
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                     [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm)),
@@ -33,7 +45,7 @@ else:
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                     [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm))])
 dev = torch.device("cuda:0")
-nb = msh._native.BATCHES_PER_LAUNCH if mode == "multi" else 1
+nb = msh._native.BATCHES_PER_LAUNCH if mode in ("multi", "generic", "generic_col") else 1
 bufs = [(torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev), torch.empty(p, dtype=torch.int32, device=dev),
          torch.empty(p, dtype=torch.int64, device=dev), torch.empty(p, dtype=torch.int32, device=dev))
         for _ in range(nb)]
@@ -41,11 +53,11 @@ descs = ctx.batch_descs([(p, *[t.data_ptr() for t in b]) for b in bufs])
 s = torch.cuda.current_stream().cuda_stream
 b = bufs[0]
 for _ in range(k):
-    if mode == "multi":
+    if nb > 1:
         ctx.schedule_batches_device(descs, nb, s)
-    elif mode in ("batch", "generic"):
+    elif mode == "batch":
         ctx.schedule_batch_device(p, *[t.data_ptr() for t in b], s)
     else:
         ctx.schedule_sequential_device(p, b[0].data_ptr(), b[1].data_ptr(), 0, *[t.data_ptr() for t in b[2:]], s)
 torch.cuda.synchronize()
-print("ok", n, p, k, mode, nb)
+print("ok", n, p, k, mode, nb, os.environ.get("MSH_BATCH_KERNEL", "pair"))

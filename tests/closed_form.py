@@ -83,3 +83,55 @@ def closed_form_modes(unsched, node_digit, pod_digit, pod_tol, weight: int = 1, 
             else:
                 idx[sel], score[sel] = (im, 100 * weight if ix >= 0 else 0) if im >= 0 else (ia, 0)
     return idx, score, status
+
+
+def _trunc_div(a: np.ndarray, b) -> np.ndarray:
+    """Go / C integer division (truncates toward zero), int64 arrays."""
+    q = np.abs(a) // np.abs(b)
+    return np.where((a >= 0) == (np.asarray(b) >= 0), q, -q)
+
+
+def direct_plugins(unsched, node_digit, pod_digit, pod_tol, plugins, cols=None, has_nu: bool = True,
+                   nn_prescore: bool = True):
+    """Direct per-pod evaluation of any plugin list over the whole node list, vectorised over the
+    nodes (a second, independent statement of RunFilterPlugins + RunScorePlugins + first-max
+    selectHost, not the oracle's code): `plugins` = [(name, weight, mode)], name "NodeNumber" or
+    "ScoreColumnK" (cols[K] the int64 per-node scores). Go int64 arithmetic (wrapping), normalize
+    modes as msh_normalize. For sampled checks of the generic pipeline at full size."""
+    unsched = np.asarray(unsched, bool)
+    node_digit = np.asarray(node_digit, np.int64)
+    p = len(pod_digit)
+    idx = np.full(p, -1, np.int32)
+    score = np.zeros(p, np.int64)
+    status = np.zeros(p, np.int32)
+    nn = any(nm == "NodeNumber" for nm, _, _ in plugins)
+    with np.errstate(over="ignore"):
+        for j in range(p):
+            feas = np.ones(len(unsched), bool) if (pod_tol[j] or not has_nu) else ~unsched
+            f = np.flatnonzero(feas)
+            if f.size == 0:
+                status[j] = 1
+                continue
+            if nn and (not nn_prescore or not 0 <= pod_digit[j] <= 9):
+                status[j] = 2
+                continue
+            tot = np.zeros(f.size, np.int64)
+            for name, w, mode in plugins:
+                if name == "NodeNumber":
+                    raw = np.where(node_digit[f] == pod_digit[j], 10, 0).astype(np.int64)
+                else:
+                    raw = np.asarray(cols[int(name[-1])], np.int64)[f]
+                if mode in (1, 2):
+                    m = max(int(raw.max()), 0)
+                    if m == 0:
+                        raw = raw if mode == 1 else np.full(f.size, 100, np.int64)
+                    else:
+                        raw = _trunc_div(100 * raw, m)
+                        raw = raw if mode == 1 else 100 - raw
+                elif mode == 3:
+                    mx, mn = int(raw.max()), int(raw.min())
+                    raw = np.zeros(f.size, np.int64) if mx == mn else _trunc_div((raw - mn) * 100, mx - mn)
+                tot = tot + raw * np.int64(w) if w < (1 << 63) else tot
+            b = int(np.argmax(tot))  # the first maximum
+            idx[j], score[j] = f[b], tot[b]
+    return idx, score, status
