@@ -89,6 +89,16 @@ int oracle_schedule_sequential_soa(int32_t n, const uint8_t* unsched, const int8
                                    int32_t* out_status);
 int oracle_suffix_digit(const char* name, int64_t len);
 
+/* Pod-parallel drivers (msh_oracle_omp.c): identical results, pods split over threads. */
+int oracle_schedule_batch_soa_cols_omp(int32_t n, const uint8_t* unsched, const int8_t* node_digit,
+                                       int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                                       const int32_t* filter_ids, int32_t nf,
+                                       const int32_t* prescore_ids, int32_t npre,
+                                       const int32_t* score_ids, const int64_t* weights,
+                                       const int32_t* norm, int32_t ns, const int64_t* cols,
+                                       int32_t threads, int32_t* out_idx, int64_t* out_score,
+                                       int32_t* out_status);
+
 #ifdef __cplusplus
 }
 #endif

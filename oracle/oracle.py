@@ -265,7 +265,7 @@ def c_schedule_batch(unsched, node_digit, pod_digit, pod_tol, plugins: PluginSet
     cols: {k: int64 array of n} for the ScoreColumn<k> plugins (List order)."""
     plugins = plugins or PluginSet()
     if any(x.startswith("ScoreColumn") for x in plugins.score):
-        return _c_schedule_batch_cols(unsched, node_digit, pod_digit, pod_tol, plugins, cols or {})
+        return _c_schedule_batch_cols(unsched, node_digit, pod_digit, pod_tol, plugins, cols or {}, threads)
     unsched = np.ascontiguousarray(unsched, np.uint8)
     node_digit = np.ascontiguousarray(node_digit, np.int8)
     pod_digit = np.ascontiguousarray(pod_digit, np.int8)
@@ -314,7 +314,7 @@ def c_schedule_sequential(unsched, node_digit, pod_digit, pod_tol, plugins: Plug
     return idx, score, status, counts[:n]
 
 
-def _c_schedule_batch_cols(unsched, node_digit, pod_digit, pod_tol, plugins: PluginSet, cols: dict):
+def _c_schedule_batch_cols(unsched, node_digit, pod_digit, pod_tol, plugins: PluginSet, cols: dict, threads: int = 1):
     unsched = np.ascontiguousarray(unsched, np.uint8)
     node_digit = np.ascontiguousarray(node_digit, np.int8)
     pod_digit = np.ascontiguousarray(pod_digit, np.int8)
@@ -328,10 +328,16 @@ def _c_schedule_batch_cols(unsched, node_digit, pod_digit, pod_tol, plugins: Plu
     idx = np.empty(p, np.int32)
     score = np.empty(p, np.int64)
     status = np.empty(p, np.int32)
-    rc = clib().oracle_schedule_batch_soa_cols(
-        C.c_int32(n), _p(unsched), _p(node_digit), C.c_int32(p), _p(pod_digit), _p(pod_tol),
-        _p(f), C.c_int32(len(f)), _p(pre), C.c_int32(len(pre)), _p(s), _p(w), _p(nm),
-        C.c_int32(len(s)), _p(allc), _p(idx), _p(score), _p(status))
+    if threads > 1:
+        rc = clib().oracle_schedule_batch_soa_cols_omp(
+            C.c_int32(n), _p(unsched), _p(node_digit), C.c_int32(p), _p(pod_digit), _p(pod_tol),
+            _p(f), C.c_int32(len(f)), _p(pre), C.c_int32(len(pre)), _p(s), _p(w), _p(nm),
+            C.c_int32(len(s)), _p(allc), C.c_int32(threads), _p(idx), _p(score), _p(status))
+    else:
+        rc = clib().oracle_schedule_batch_soa_cols(
+            C.c_int32(n), _p(unsched), _p(node_digit), C.c_int32(p), _p(pod_digit), _p(pod_tol),
+            _p(f), C.c_int32(len(f)), _p(pre), C.c_int32(len(pre)), _p(s), _p(w), _p(nm),
+            C.c_int32(len(s)), _p(allc), _p(idx), _p(score), _p(status))
     if rc != 0:
         raise RuntimeError(f"oracle failed rc={rc}")
     return idx, score, status, np.zeros(p, np.uint32)

@@ -974,3 +974,47 @@ def test_generic_kernel_cross_checks_bitmap_kernel(msh, oracle, combo, norm, mon
         ctx.upload_nodes(u, nd)
         _assert_same(ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8),
                      f"generic combo={combo} norm={norm}")
+
+
+# ---- BASELINE C3 in full on the per-pair kernels, against the oracle (verdict r3, next #3) ----
+def _c3_cols(n):
+    rng = np.random.default_rng(0xC3)
+    return {0: rng.integers(-(1 << 31), (1 << 31) + 1, n), 1: rng.integers(0, 7, n) * 13}
+
+
+@pytest.mark.parametrize("kernel", ["pair", "generic"])
+def test_c3_reference_list_vs_oracle(msh, oracle, synth, kernel, monkeypatch):
+    """5,000 nodes x 100,000 pods (BASELINE C3, the headline workload), the reference plugin list,
+    weight 1, no normalizer, through the batch and the 32-batch entry points of the per-pair kernel
+    (pair_kernel, the headline) and of generic_kernel (explicit int64 scores, MSH_BATCH_KERNEL=generic):
+    bit-exact vs oracle.c_schedule_batch (the restatement of minisched.go:115-199,304-325)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_BATCH_KERNEL", kernel)
+    u, nd, pd, pt = synth.make_soa(5000, 100_000)
+    want = oracle.c_schedule_batch(u, nd, pd, pt, oracle.PluginSet(), threads=16)
+    dev = torch.device("cuda:0")
+    with msh.DeviceContext(0) as ctx:
+        ctx.upload_nodes(u, nd)
+        _assert_same(ctx.schedule_batch(pd, pt), want, f"C3 {kernel}")
+        ts = [_dev_batch(torch, dev, pd, pt) for _ in range(3)]
+        ctx.schedule_batches_device(ctx.batch_descs([_desc(t) for t in ts]), stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for t in ts:
+            _assert_same([t[i].cpu().numpy() for i in (2, 3, 4)], want, f"C3 {kernel} multi")
+
+
+@pytest.mark.parametrize("norm,weight", [(3, 3), (1, 2)])
+def test_c3_score_column_vs_oracle(msh, gpu_ctx, oracle, synth, norm, weight):
+    """C3 in full on generic_kernel with NodeNumber + ScoreColumn0 (columns spanning [-2^31, 2^31]),
+    both normalized (MIN-MAX at weight 3, DefaultNormalizeScore at weight 2): the per-pair division
+    by the pod's exact reciprocal, the first maximum over int64 totals, bit-exact vs the oracle."""
+    u, nd, pd, pt = synth.make_soa(5000, 100_000)
+    cols = _c3_cols(5000)
+    ps = oracle.PluginSet(score=["NodeNumber", "ScoreColumn0"], weights=[weight, weight], normalize=[norm, norm])
+    want = oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols, threads=16)
+    gpu_ctx.set_plugins(ps.filters, ps.prescore, [msh.ScorePluginConfig(s, w, msh.Normalize(m))
+                                                  for s, w, m in zip(ps.score, ps.weights, ps.normalize)])
+    gpu_ctx.upload_nodes(u, nd)
+    gpu_ctx.upload_score_column("ScoreColumn0", cols[0])
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, f"C3 column norm={norm} w={weight}")
+    gpu_ctx.set_plugins(["NodeUnschedulable"], ["NodeNumber"], [msh.ScorePluginConfig("NodeNumber")])
