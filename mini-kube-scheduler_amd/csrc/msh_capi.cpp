@@ -330,9 +330,6 @@ int record_on(msh_ctx* c, std::vector<std::pair<hipStream_t, hipEvent_t>>& evs, 
 // After a launch on caller stream s that reads the current table version (seq: and updates the
 // sequential-mode counts).
 int track_launch(msh_ctx* c, hipStream_t s, bool seq = false) {
-#ifdef MSH_AB_NO_TRACK  // A/B measurement builds only (scripts/ab_build.sh): no reader events
-  if (!seq) return MSH_OK;
-#endif
   int rc = record_on(c, cur_table(c).readers, s);
   if (rc == MSH_OK && seq) rc = record_on(c, c->seq_inflight, s);
   return rc;

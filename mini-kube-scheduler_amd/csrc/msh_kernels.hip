@@ -6,33 +6,22 @@
 //   RunScorePlugins    minisched/minisched.go:164-199  (NodeNumber.Score, nodenumber.go:73-95)
 //   selectHost         minisched/minisched.go:304-325  (argmax; ties -> lowest index here)
 //
-// Layout (msh_internal.h): per group of 256 List-order nodes, the digit rows ER[r] (bit i of row r:
-// node i is feasible-relevant and scores 10 for a digit-r pod; row 10 all zero), the X words
-// (NodeUnschedulable verdict for non-tolerating pods) and, for REVERSE / MINMAX, the V words (real
-// node), plus the bit planes of the node codes the sequential / A/B kernels read. The batched kernels
-// put one POD per lane: a lane's hit word for 32 nodes is ER[row] & ~(X & nT), one v_bitop3, so every
-// VALU operation evaluates 32 (pod, node) pairs.
-// Stages (north_star):
-//   1. feasibility bitmask with wavefront __ballot (X / V words, first feasible per class) -> node_prep_kernel
-//   2. int64 score with the plugin weight fused                    -> decode_pod / decode_ident
-//   3. per-pod normalisation (DEFAULT / REVERSE / MINMAX need the extent of the raw scores over the
-//      feasible list: first feasible match / non-match)             -> wgp_kernel / wg_kernel<KX> + decode
-//   4. argmax with a fixed lowest-index tie-break: the lowest group with a hit, then its first set
-//      bit (v_ffbl) in List order                                   -> wgp_kernel / wg_kernel
-//   5. node-table tiles staged in LDS once per workgroup and reused by every pod it serves
-//                                                                   -> wgp_kernel / wg_kernel
-//   generic_kernel does stages 1-5 with an explicit int64 score per pair, for any score-plugin list
-//   (score-column plugins; a real LDS min/max reduction and a wave-shuffle argmax).
-//
+// Every batch kernel puts one POD per lane and reads the node side wave-uniformly (scalar loads into
+// SGPRs), so the node data is read once per 64 pods and the vector unit does per-pair work only.
 // Kernels, by entry point:
-//   node_prep_kernel (+ prep_reset_kernel)  every upload / patch / plugin change
-//   wgp_kernel           msh_schedule_batch*, msh_schedule_batches_device on tables up to 8,192 nodes
-//                        (BASELINE C2 / C3): persistent grid, the pod-class rows copied once per workgroup
-//   wg_kernel            the same entry points on larger tables (chunk-streamed), and msh_shard_keys_device
-//   generic_kernel       the batch entry points when the score list names a score-column plugin
-//   rows_kernel          A/B (MSH_BATCH_KERNEL=slices): the round-2 slice kernel
-//   bits_kernel          A/B (MSH_KX_BITS=1): REVERSE / MINMAX on the code planes
-//   decode_keys_kernel   node-sharded mode: decode the merged int32 shard keys
+//   node_prep_kernel (+ prep_reset_kernel)  every upload / patch / filter-list change: the bit planes
+//                        (pair_kernel, seq_kernel), the node records (generic_kernel), the class rows
+//                        and first-node offsets (the opt-in class-row kernel)
+//   pair_kernel          msh_schedule_batch*, msh_schedule_batches_device, msh_shard_keys_device for the
+//                        reference plugins, every normalize mode (the default batch path): every (pod,
+//                        node) pair's filter verdict and NodeNumber score evaluated from the bit planes,
+//                        32 pairs per lane-op
+//   generic_kernel       any plugin list with an explicit int64 score per pair (score-column plugins;
+//                        the node-sharded msh_generic_* entry points): north_star's five stages literally
+//                        (feasibility lane masks, weighted int64 totals, per-pod min/max extents with an
+//                        LDS reduction, a running first maximum, node tiles read once per wave)
+//   wgp_kernel           the opt-in class-row kernel (MSH_BATCH_KERNEL=classrows, tables <= 8,192 nodes)
+//   decode_keys_kernel   node-sharded mode: decode the merged per-pod shard keys
 //   seq_kernel           sequential commit, one pod at a time, one workgroup
 //   export_kernel        per-pair result export (simulator result store)
 // See DESIGN.md for the roofline / instruction budget of each kernel.
@@ -524,30 +513,6 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
 }
 
 
-#if defined(MSH_STAMPS) || defined(MSH_CLOCK_STAMPS)
-// Timeline / clock A/B builds only (scripts/stamps.sh, scripts/ab_build.sh; never in
-// libminisched_hip.so): per wave, the 100 MHz wall clock at entry, after the prologue's loads, after
-// the scan and before the stores (MSH_STAMPS); or the shader and 100 MHz clocks at a persistent
-// wave's start and end (MSH_CLOCK_STAMPS, wgp_kernel).
-__device__ unsigned long long* g_stamps;
-#endif
-#ifdef MSH_STAMPS
-#define MSH_STAMP(i) (__builtin_amdgcn_s_waitcnt(0), stamp_t[i] = wall_clock64())
-#else
-#define MSH_STAMP(i) ((void)0)
-#endif
-
-
-// Phase experiments of A/B builds only (scripts/wg_expt.sh, scripts/ab_build.sh; never the product
-// library): bit 0 skips the scan loop, bit 1 the output stores, bit 2 the table copy into LDS; bit 4
-// (wgp_kernel's quad scan) adds a second reduction tree per pair of groups. MSH_WG_FLAG
-// selects the form of the per-group flag (A/B of the same build).
-#ifndef MSH_WG_EXPT
-#define MSH_WG_EXPT 0
-#endif
-#ifndef MSH_WG_FLAG
-#define MSH_WG_FLAG 0
-#endif
 
 // acc | (e & ~x), one v_bitop3_b32 (S0 = acc, S1 = e, S2 = x). The builtin, not inline asm: the
 // compiler then knows the instruction's hazards (inline asm got a conservative s_nop after each pair).
@@ -569,12 +534,14 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t sh, uint32_t b)
 
 
 // ---------------------------------------------------------------------------------------
-// Persistent batch kernel (msh_schedule_batch_device / msh_schedule_batches_device when the table
-// has at most WGP_MAX_GROUPS groups, 8,192 nodes: BASELINE C2 and C3). A grid of as many workgroups
-// as stay resident (CUs x 8 at C3) copies the table's CLASS ROWS (msh_internal.h HR_*) into LDS once
-// per workgroup and then walks the launch's (batch, 256-pod block) space with a stride of the grid;
-// after the copy the waves are independent (no barrier per block), and each wave loads the next
-// block's pod bytes before it scans the current one.
+// The opt-in class-row kernel (MSH_BATCH_KERNEL=classrows; tables up to WGP_MAX_GROUPS groups, 8,192
+// nodes). NOT a per-pair evaluation: a pod's verdicts come from rows indexed by its class (tolerates,
+// digit) that the prep built per upload; kept for what it is, a placement path specialised to the
+// reference plugins, and reported apart from the per-pair kernels. A persistent grid of as many
+// workgroups as the runtime reports resident copies the table's class rows (msh_internal.h HR_*) into
+// LDS once per workgroup and then walks the launch's (batch, 256-pod block) space; after the copy the
+// waves are independent (no barrier per block), and each wave loads the next block's pod bytes before
+// it scans the current one.
 // Per lane (pod) and 256-node group the pair evaluation is one read of the pod's class row: the two
 // 16-byte entries H[t][r] of the group's two 4-word chunks, t = the pod tolerates the unschedulable
 // taint, r = its suffix digit (10 = none: the zero row). A set bit is a node that passes
@@ -604,9 +571,6 @@ __device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
 
 template <int W, bool KX>
 __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
-#ifdef MSH_CLOCK_STAMPS  // diagnostic build only (scripts/ab_build.sh): the in-kernel clock per wave
-  const unsigned long long ck_t0 = __builtin_amdgcn_s_memtime(), ck_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
   constexpr int GQL = HR_GQ;  // entries staged per group: the whole record (rows, F, first-node offsets)
   constexpr int NT = W * WAVE;
   extern __shared__ uint4 s_tab[];        // n_groups * GQL entries
@@ -629,7 +593,7 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int32_t i = (int32_t)threadIdx.x + k * NT;
-      if ((MSH_WG_EXPT & 4) == 0 && i < tot) s_tab[i] = vs[k];
+      if (i < tot) s_tab[i] = vs[k];
     }
   }
   const uint32_t ball0 = A.ball[0], ball1 = A.ball[1];
@@ -724,7 +688,6 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
   int32_t *p_oi = nullptr, *p_ot = nullptr;
   int64_t* p_os = nullptr;
   auto flush = [&]() {
-    if ((MSH_WG_EXPT & 2) != 0 && s_oi != 0x7fffffff) s_pending = false;  // phase experiment: no stores
     const BatchDesc& d = ka.d[s_cb];
     const bool has_score = d.out_score != nullptr;
     p_oi = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d.out_idx + s_wbase) + lo4);
@@ -739,13 +702,7 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
   };
   if (it < total) load_pods();
   Item cur = prepare();
-#ifdef MSH_CLOCK_STAMPS
-  int n_items = 0;
-#endif
   while (it < total) {
-#ifdef MSH_CLOCK_STAMPS
-    ++n_items;
-#endif
     if (!cur.live) {  // this wave's slice lies past its batch's end
       flush();
       advance();
@@ -794,7 +751,7 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
       if constexpr (KX)
         bx = lshl_or(bx, 2, lshl_or(min1(nm16(t + 2 * GQL, a2, b2, a3, b3)), 1, min1(nm16(t, a0, b0, a1, b1))));
     };
-    int32_t q = (MSH_WG_EXPT & 1) ? -4 : n_groups - 4;
+    int32_t q = n_groups - 4;
     if (q >= 0) {
       step(q);
       q -= 4;
@@ -827,20 +784,6 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
     cur = prepare();
   }
   flush();
-#ifdef MSH_CLOCK_STAMPS
-  const unsigned long long ck_t1 = __builtin_amdgcn_s_memtime(), ck_r1 = __builtin_amdgcn_s_memrealtime();
-  if (lane == 0 && g_stamps) {
-    unsigned long long* o = g_stamps + ((size_t)blockIdx.x * W + wv) * 8;
-    o[0] = ck_t0;
-    o[1] = ck_r0;
-    o[2] = ck_t1;
-    o[3] = ck_r1;
-    o[4] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID: cu / sh / se / simd / wave
-    o[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
-    o[6] = (unsigned long long)n_items;
-    o[7] = blockIdx.x;
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1972,8 +1915,5 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
   return launch_seq_nw<15, false>(ka, rs, s);
 }
 
-#if defined(MSH_STAMPS) || defined(MSH_CLOCK_STAMPS)
-extern "C" int msh_stamps_set(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
-#endif
 
 }  // namespace msh
