@@ -53,9 +53,11 @@ CLOCK_HZ = 2.4e9                   # MI355X_MICROARCH.md: max clock
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 LANES_PER_SIMD_CYCLE = 32          # MI355X_MICROARCH.md: SIMD-32, a wave64 VALU instruction over 2 cycles
 # pair_kernel's scan (msh_kernels.hip): per 32-node word and 64-pod wave, v_bitop3 (X & nT) + 4 v_bitop3
-# (the code-bit mismatches ORed in: dm'), half a v_bitop3 AND3 (two words' dm' into the group's match
-# flag) and one v_bitop3 OR-accumulate of the feasible non-matches: 6.5 VALU per 32 x 64 pairs
-PAIR_VALU_PER_WORD = 6.5
+# (the code-bit mismatches ORed in: dm') and half a v_bitop3 AND3 (two words' dm' into the group's match
+# flag): 5.5 VALU per 32 x 64 pairs in the identity-like modes (NONE, DEFAULT); REVERSE / MINMAX add one
+# v_bitop3 OR-accumulate of the feasible non-matches: 6.5
+PAIR_VALU_PER_WORD = 5.5
+PAIR_VALU_PER_WORD_KX = 6.5
 # generic_kernel's main sweep on the reference list (NodeNumber only): per pair v_cmp_eq (suffix
 # digits), 2 v_cndmask (the lane's two weighted values), v_cmp_gt_i64 (strict first max), 3 v_cndmask
 # (best total, chunk-relative index): 7 VALU lane-ops per pair
@@ -67,9 +69,9 @@ VALU_PEAK_FILE = ROOT / "profiles" / "r3_ubench_valu_peak.json"
 
 def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False,
                        multi: bool = False, nb: int = 1, classrows: bool = False) -> str:
-    """The kernel msh_capi.cpp dispatches for a launch of nb batches of n_pods: pair_kernel<S, SHARD>,
-    S the slice waves per 64-pod block (msh_kernels.hip pair_slices), or the opt-in class-row
-    kernel wgp_kernel<4, KX> (tables up to WGP_MAX_GROUPS groups)."""
+    """The kernel msh_capi.cpp dispatches for a launch of nb batches of n_pods: pair_kernel<S, SHARD, KX>,
+    S the slice waves per 64-pod block (msh_kernels.hip pair_slices), KX for REVERSE / MINMAX, or the
+    opt-in class-row kernel wgp_kernel<4, KX> (tables up to WGP_MAX_GROUPS groups)."""
     b = lambda v: str(v).lower()
     groups = max(-(-n_nodes // 1024) * 1024, 1024) // 256
     if classrows and groups <= WGP_MAX_GROUPS and not shard:
@@ -78,7 +80,7 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2
-    return f"void msh::pair_kernel<{sl}, {b(shard)}>"
+    return f"void msh::pair_kernel<{sl}, {b(shard)}, {b(kx)}>"
 
 
 def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
@@ -476,9 +478,9 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
     model_per_eval = PAIR_VALU_PER_WORD * (n_pad / 32) * (-(-p // 64) * 64) / (float(n_local) * p)
     entry = pmc_entry("pair_multi" if nb > 1 else "pair_single", kname, n_local, p, nb)
     out = valu_roofline(kname, launch_ms, evals, model_per_eval, cus, entry,
-                        "6.5 VALU per 32-node word and 64-pod wave (pair_kernel's scan, msh_kernels.hip): per "
-                        "lane-op 32 (pod, node) pairs get NodeUnschedulable's verdict and NodeNumber's digit "
-                        "compare; lane-ops per eval = 6.5 x padded words x padded pods / (n x p)")
+                        "5.5 VALU per 32-node word and 64-pod wave (pair_kernel's scan, msh_kernels.hip, NONE "
+                        "normalize): per lane-op 32 (pod, node) pairs get NodeUnschedulable's verdict and "
+                        "NodeNumber's digit compare; lane-ops per eval = 5.5 x padded words x padded pods / (n x p)")
     out["batches_per_launch"] = nb
     out["ms_per_batch"] = launch_ms / nb
     # HBM: the bit planes once (0.75 B per node: 6 planes of 32 nodes per 4 B), 2 B in + 16 B out per pod
@@ -557,7 +559,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                         [msh.ScorePluginConfig(msh.NODE_NUMBER, weight, msh.Normalize(norm))])
         ms = run_multi(ctx)
-        variants[name] = {"kernel": batch_kernel_label(n, p, cus, multi=True, nb=G), "kernel_ms": ms,
+        variants[name] = {"kernel": batch_kernel_label(n, p, cus, kx=norm in (2, 3), multi=True, nb=G), "kernel_ms": ms,
                           "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
                           "check": "bit-exact vs closed form" if check_all(weight, norm) else "MISMATCH"}
     out["c3_normalize_variants"] = variants
@@ -601,10 +603,19 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     cctx = new_ctx("classrows")
     cctx.upload_nodes(u, nd)
     ms = run_multi(cctx)
+    ok = check_all()
+    cctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                     [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(3))])
+    ms_mm = run_multi(cctx)
+    ok_mm = check_all(1, 3)
     out["classrows_opt_in"] = {
         "kernel": batch_kernel_label(n, p, cus, multi=True, nb=G, classrows=True), "kernel_ms": ms,
         "batches_per_launch": G, "ms_per_batch": ms / G, "pods_per_s": p * G / (ms * 1e-3),
-        "check": "bit-exact vs closed form" if check_all() else "MISMATCH",
+        "check": "bit-exact vs closed form" if ok else "MISMATCH",
+        "minmax": {"kernel": batch_kernel_label(n, p, cus, kx=True, multi=True, nb=G, classrows=True),
+                   "kernel_ms": ms_mm, "pods_per_s": p * G / (ms_mm * 1e-3),
+                   "check": "bit-exact vs closed form" if ok_mm else "MISMATCH",
+                   "grid": "workgroups per CU from hipOccupancyMaxActiveBlocksPerMultiprocessor"},
         "note": "MSH_BATCH_KERNEL=classrows: each pod's verdicts are read from per-(tolerates, digit)-class "
                 "tables built at upload, so its per-pod work does not evaluate the pairs; a placement rate "
                 "of a class-specialised path, never the headline evals/s"}

@@ -255,9 +255,10 @@ int msh_reset_node_pod_counts(msh_ctx* ctx);
  * over shards (one RCCL allreduce MAX) is the global first node. Layout (ABI v7), msh_shard_keys_len
  * = 2p entries, every entry a property of pod j alone (evaluated per (pod, node) pair of the shard):
  *   keys[j]      first feasible node whose NodeNumber score is 10 for pod j (feasible match)
- *   keys[p + j]  first feasible node whose NodeNumber score is 0 for pod j (feasible non-match)
+ *   keys[p + j]  REVERSE / MINMAX normalize: first feasible node whose NodeNumber score is 0 for pod j
+ *                (feasible non-match); every other mode: first feasible node for pod j
  * 8 B per pod cross the interconnect (selectHost over the merged keys replaces minisched.go:304-325
- * across shards; the first feasible node is the larger of the two keys). msh_decode_keys_device then
+ * across shards; the first feasible node is the larger of the two keys in either case). msh_decode_keys_device then
  * produces idx/score/status exactly as msh_schedule_batch over the whole table. Score-column plugin
  * lists use msh_generic_extents_device / msh_generic_best_device / msh_generic_decode_device below. */
 int msh_shard_keys_len(const msh_ctx* ctx, int32_t p, int32_t* out_len);

@@ -264,52 +264,6 @@ __device__ __forceinline__ void sload_group(u32x8* pl, const uint32_t* src) {
 
 constexpr uint32_t NO_GROUP = 0xFFFFFFFFu;
 
-// The lane's first node in group g (per-lane vector loads of the group's planes): the first word
-// with a zero bit in the miss word, then its lowest zero bit. NONMATCH: the first feasible
-// non-match instead of the first feasible match. Returns a node index (g has one by construction).
-template <bool NONMATCH>
-__device__ __forceinline__ uint32_t group_first(const uint32_t* __restrict__ planes, uint32_t g, uint32_t P0,
-                                                uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT) {
-  const uint4* q = reinterpret_cast<const uint4*>(planes + (size_t)g * GROUP_DWORDS);
-  constexpr int NP = NONMATCH ? PLANE_N : PLANE_V;
-  uint32_t pl[NP][PLANE_GW];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    const uint4 lo = q[k * 2], hi = q[k * 2 + 1];
-    pl[k][0] = lo.x; pl[k][1] = lo.y; pl[k][2] = lo.z; pl[k][3] = lo.w;
-    pl[k][4] = hi.x; pl[k][5] = hi.y; pl[k][6] = hi.z; pl[k][7] = hi.w;
-  }
-  uint32_t bw = 0;
-  int32_t bj = 0;
-#pragma unroll
-  for (int c = PLANE_GW - 1; c >= 0; --c) {
-    const uint32_t dm = (pl[0][c] ^ P0) | (pl[1][c] ^ P1) | (pl[2][c] ^ P2) | (pl[3][c] ^ P3);
-    const uint32_t xi = pl[PLANE_X][c] & nT;
-    uint32_t hit;
-    if constexpr (NONMATCH) hit = dm & ~xi & pl[PLANE_N - 1][c];
-    else hit = ~(dm | xi);
-    bj = hit ? c : bj;
-    bw = hit ? hit : bw;
-  }
-  return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
-}
-
-// The first node with a zero bit among the 8 kept miss words of group g (words ascend in List
-// order, and bits within a word): descending selects, then the lowest zero bit.
-__device__ __forceinline__ uint32_t kept_first(const uint32_t (&k)[PLANE_GW], uint32_t g) {
-  uint32_t bw = 0;
-  int32_t bj = 0;
-#pragma unroll
-  for (int c = PLANE_GW - 1; c >= 0; --c) {
-    const uint32_t hit = ~k[c];
-    bj = hit ? c : bj;
-    bw = hit ? hit : bw;
-  }
-  return (g * PLANE_GW + (uint32_t)bj) * 32u + (uint32_t)__builtin_ctz(bw);
-}
-
-
-
 // The first node among 8 hit words of group g (words ascend in List order, bits within a word):
 // v_ffbl_b32 gives each word's lowest set bit, all-ones for an empty word, which ORed with the
 // word's offset (32 c) stays all-ones; the unsigned minimum over the words is the first hit.
@@ -389,18 +343,19 @@ __device__ __forceinline__ uint32_t pair_miss(const u32x8 (&pl)[PLANE_N], int w,
   return bop3_or_xor(t, pl[3][w], P3);
 }
 
-// One group above the lowest of the range: whether it holds a feasible match (hm) / non-match (hx).
-template <bool PAD>
+// One group above the lowest of the range, accumulated into am (AND of the dm' words: not all-ones
+// iff a feasible match) and, KX, ax (OR of the feasible non-match words).
+template <bool PAD, bool KX>
 __device__ __forceinline__ void pair_group(const u32x8 (&pl)[PLANE_N], uint32_t P0, uint32_t P1, uint32_t P2,
-                                           uint32_t P3, uint32_t nT, bool& hm, bool& hx) {
-  uint32_t am = 0xFFFFFFFFu, ax = 0u;
+                                           uint32_t P3, uint32_t nT, uint32_t& am, uint32_t& ax) {
 #pragma unroll
   for (int w = 0; w < PLANE_GW; w += 2) {
     uint32_t x0, x1;
     const uint32_t t0 = pair_miss(pl, w, P0, P1, P2, P3, nT, x0);
     const uint32_t t1 = pair_miss(pl, w + 1, P0, P1, P2, P3, nT, x1);
     am = bop3_and3(am, t0, t1);
-    if constexpr (PAD) {
+    if constexpr (!KX) {
+    } else if constexpr (PAD) {
       ax |= bop3_andn_and(t0, x0, pl[PLANE_V][w]);
       ax |= bop3_andn_and(t1, x1, pl[PLANE_V][w + 1]);
     } else {
@@ -408,12 +363,10 @@ __device__ __forceinline__ void pair_group(const u32x8 (&pl)[PLANE_N], uint32_t 
       ax = bop3_or_andn(ax, t1, x1);
     }
   }
-  hm = am != 0xFFFFFFFFu;
-  hx = ax != 0u;
 }
 
-// The lowest group of the range: its dm' words (km) and feasible non-match words (kx) kept.
-template <bool PAD>
+// The lowest group of the range: its dm' words (km) and, KX, feasible non-match words (kx) kept.
+template <bool PAD, bool KX>
 __device__ __forceinline__ void pair_group_keep(const u32x8 (&pl)[PLANE_N], uint32_t P0, uint32_t P1, uint32_t P2,
                                                 uint32_t P3, uint32_t nT, uint32_t (&km)[PLANE_GW],
                                                 uint32_t (&kx)[PLANE_GW]) {
@@ -421,11 +374,73 @@ __device__ __forceinline__ void pair_group_keep(const u32x8 (&pl)[PLANE_N], uint
   for (int w = 0; w < PLANE_GW; ++w) {
     uint32_t xi;
     km[w] = pair_miss(pl, w, P0, P1, P2, P3, nT, xi);
-    kx[w] = PAD ? bop3_andn_and(km[w], xi, pl[PLANE_V][w]) : bop3_andn(km[w], xi);
+    if constexpr (KX) kx[w] = PAD ? bop3_andn_and(km[w], xi, pl[PLANE_V][w]) : bop3_andn(km[w], xi);
   }
 }
 
-template <int S, bool SHARD>
+// NodeUnschedulable's verdict depends on the pod only through its tolerates bit, so the node side of
+// "is there a feasible node" is the same for every pod of one tolerates value: V & ~X for a pod that
+// does not tolerate the taint, V for one that does. The identity-like modes (NONE, DEFAULT: a pod
+// without a feasible match takes its first feasible node) evaluate it here, on the scalar unit, once
+// per wave and group, instead of a per-lane OR per word; the lane picks its value by its tolerates bit.
+template <bool PAD>
+__device__ __forceinline__ void group_feasible_s(const u32x8 (&pl)[PLANE_N], bool& fn, bool& ft) {
+  if constexpr (PAD) {
+    uint32_t on = 0u, ot = 0u;
+#pragma unroll
+    for (int w = 0; w < PLANE_GW; ++w) {
+      on |= pl[PLANE_V][w] & ~pl[PLANE_X][w];
+      ot |= pl[PLANE_V][w];
+    }
+    fn = on != 0u;
+    ft = ot != 0u;
+  } else {  // no padding slot: every node is real
+    uint32_t ax = 0xFFFFFFFFu;
+#pragma unroll
+    for (int w = 0; w < PLANE_GW; ++w) ax &= pl[PLANE_X][w];
+    fn = ax != 0xFFFFFFFFu;
+    ft = true;
+  }
+}
+// The first node of group g (planes pl, all six loaded) feasible for a pod that does not tolerate the
+// taint (NT) or that does; NOFIT if none. Scalar.
+template <bool NT>
+__device__ __forceinline__ uint32_t group_first_feasible_s(const u32x8 (&pl)[PLANE_N], uint32_t g) {
+  uint32_t r = NOFIT;
+#pragma unroll
+  for (int w = PLANE_GW - 1; w >= 0; --w) {
+    const uint32_t h = NT ? (pl[PLANE_V][w] & ~pl[PLANE_X][w]) : pl[PLANE_V][w];
+    r = h ? (g * PLANE_GW + (uint32_t)w) * 32u + (uint32_t)__builtin_ctz(h) : r;
+  }
+  return r;
+}
+
+// The lane's first feasible match (or, NONMATCH, feasible non-match) in group g, NOFIT if none:
+// per-lane vector loads of the group's planes (the rare path: a first hit above the lowest group).
+template <bool NONMATCH>
+__device__ __forceinline__ uint32_t group_first_or_none(const uint32_t* __restrict__ planes, uint32_t g,
+                                                        uint32_t P0, uint32_t P1, uint32_t P2, uint32_t P3,
+                                                        uint32_t nT) {
+  const uint4* q = reinterpret_cast<const uint4*>(planes + (size_t)g * GROUP_DWORDS);
+  uint32_t pl[PLANE_N][PLANE_GW];
+#pragma unroll
+  for (int k = 0; k < PLANE_N; ++k) {
+    const uint4 lo = q[k * 2], hi = q[k * 2 + 1];
+    pl[k][0] = lo.x; pl[k][1] = lo.y; pl[k][2] = lo.z; pl[k][3] = lo.w;
+    pl[k][4] = hi.x; pl[k][5] = hi.y; pl[k][6] = hi.z; pl[k][7] = hi.w;
+  }
+  uint32_t h[PLANE_GW];
+#pragma unroll
+  for (int c = 0; c < PLANE_GW; ++c) {
+    const uint32_t dm = (pl[0][c] ^ P0) | (pl[1][c] ^ P1) | (pl[2][c] ^ P2) | (pl[3][c] ^ P3);
+    const uint32_t fe = ~(pl[PLANE_X][c] & nT) & pl[PLANE_V][c];
+    h[c] = NONMATCH ? (dm & fe) : (~dm & fe);
+  }
+  const uint32_t m = hits_first(h, 0u);  // all-ones when the group holds none
+  return m < GROUP_NODES ? g * GROUP_NODES + m : NOFIT;
+}
+
+template <int S, bool SHARD, bool KX>
 __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
   constexpr int PB = PAIR_WAVES / S;  // 64-pod blocks per workgroup
   __shared__ uint32_t s_res[S > 1 ? PAIR_WAVES : 1][2][WAVE];
@@ -451,39 +466,78 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
   const int32_t g_lo = min(sl * a.gps, a.n_groups);
   const int32_t g_hi = live ? min(g_lo + a.gps, a.n_groups) : g_lo;
   const int32_t g_full = a.g_full;  // groups below it hold no padding slot
-  uint32_t fm = NO_GROUP, fx = NO_GROUP;  // first group above g_lo with a feasible match / non-match
-  for (int32_t g = g_hi - 1; g > g_lo; --g) {
-    u32x8 pl[PLANE_N];
-    bool hm, hx;
-    if (g < g_full) {
-      sload_group<PLANE_V>(pl, a.planes + (size_t)g * GROUP_DWORDS);
-      pair_group<false>(pl, P0, P1, P2, P3, nT, hm, hx);
-    } else {
-      sload_group<PLANE_N>(pl, a.planes + (size_t)g * GROUP_DWORDS);
-      pair_group<true>(pl, P0, P1, P2, P3, nT, hm, hx);
+  // Groups above g_lo, descending, two per step: the pair's flags are one AND / OR over its 16 words,
+  // and fm / fx remember the lower group of the lowest pair with a hit (its hit may lie in that group
+  // or the one above). Identity-like modes: fn / ft, the lowest group with a node feasible for a pod
+  // that does not tolerate / that tolerates the taint (scalar).
+  uint32_t fm = NO_GROUP, fx = NO_GROUP;
+  uint32_t fn = NO_GROUP, ft = NO_GROUP;
+  for (int32_t g = g_hi - 1; g > g_lo; g -= 2) {
+    uint32_t am = 0xFFFFFFFFu, ax = 0u;
+    const int32_t g2 = g - 1 > g_lo ? g - 1 : g;  // the pair's lower group (g itself when alone)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int32_t gg = h == 0 ? g : g - 1;
+      if (h == 1 && gg <= g_lo) break;
+      u32x8 pl[PLANE_N];
+      bool sn, st;
+      if (gg < g_full) {
+        sload_group<PLANE_V>(pl, a.planes + (size_t)gg * GROUP_DWORDS);
+        pair_group<false, KX>(pl, P0, P1, P2, P3, nT, am, ax);
+        if constexpr (!KX) group_feasible_s<false>(pl, sn, st);
+      } else {
+        sload_group<PLANE_N>(pl, a.planes + (size_t)gg * GROUP_DWORDS);
+        pair_group<true, KX>(pl, P0, P1, P2, P3, nT, am, ax);
+        if constexpr (!KX) group_feasible_s<true>(pl, sn, st);
+      }
+      if constexpr (!KX) {
+        fn = sn ? (uint32_t)gg : fn;
+        ft = st ? (uint32_t)gg : ft;
+      }
     }
-    fm = hm ? (uint32_t)g : fm;
-    fx = hx ? (uint32_t)g : fx;
+    fm = am != 0xFFFFFFFFu ? (uint32_t)g2 : fm;
+    if constexpr (KX) fx = ax != 0u ? (uint32_t)g2 : fx;
   }
-  uint32_t rm = NOFIT, rx = NOFIT;  // node index of the first feasible match / non-match
+  uint32_t rm = NOFIT, rx = NOFIT;  // first feasible match / KX: non-match, identity-like: feasible node
   if (g_lo < g_hi) {
     uint32_t km[PLANE_GW], kx[PLANE_GW];
     u32x8 pl[PLANE_N];
     sload_group<PLANE_N>(pl, a.planes + (size_t)g_lo * GROUP_DWORDS);
-    if (g_lo < g_full) pair_group_keep<false>(pl, P0, P1, P2, P3, nT, km, kx);
-    else pair_group_keep<true>(pl, P0, P1, P2, P3, nT, km, kx);
+    if (g_lo < g_full) pair_group_keep<false, KX>(pl, P0, P1, P2, P3, nT, km, kx);
+    else pair_group_keep<true, KX>(pl, P0, P1, P2, P3, nT, km, kx);
     const uint32_t am = bop3_and3(bop3_and3(km[0], km[1], km[2]), bop3_and3(km[3], km[4], km[5]), km[6] & km[7]);
-    const uint32_t ax = (kx[0] | kx[1] | kx[2]) | (kx[3] | kx[4] | kx[5]) | (kx[6] | kx[7]);
     if (am != 0xFFFFFFFFu) {
       uint32_t h[PLANE_GW];
 #pragma unroll
       for (int w = 0; w < PLANE_GW; ++w) h[w] = ~km[w];
       rm = hits_first(h, (uint32_t)g_lo);
-    } else if (fm != NO_GROUP) {
-      rm = group_first<false>(a.planes, fm, P0, P1, P2, P3, nT);
+    } else if (fm != NO_GROUP) {  // the lowest hit pair: its lower group, else the one above
+      rm = group_first_or_none<false>(a.planes, fm, P0, P1, P2, P3, nT);
+      if (rm == NOFIT) rm = group_first_or_none<false>(a.planes, fm + 1, P0, P1, P2, P3, nT);
     }
-    if (ax != 0u) rx = hits_first(kx, (uint32_t)g_lo);
-    else if (fx != NO_GROUP) rx = group_first<true>(a.planes, fx, P0, P1, P2, P3, nT);
+    if constexpr (KX) {
+      const uint32_t ax = (kx[0] | kx[1] | kx[2]) | (kx[3] | kx[4] | kx[5]) | (kx[6] | kx[7]);
+      if (ax != 0u) {
+        rx = hits_first(kx, (uint32_t)g_lo);
+      } else if (fx != NO_GROUP) {
+        rx = group_first_or_none<true>(a.planes, fx, P0, P1, P2, P3, nT);
+        if (rx == NOFIT) rx = group_first_or_none<true>(a.planes, fx + 1, P0, P1, P2, P3, nT);
+      }
+    } else {  // the first feasible node for each tolerates value (scalar), then the lane's
+      uint32_t an = group_first_feasible_s<true>(pl, (uint32_t)g_lo);
+      uint32_t at = group_first_feasible_s<false>(pl, (uint32_t)g_lo);
+      if (an == NOFIT && fn != NO_GROUP) {
+        u32x8 p2[PLANE_N];
+        sload_group<PLANE_N>(p2, a.planes + (size_t)fn * GROUP_DWORDS);
+        an = group_first_feasible_s<true>(p2, fn);
+      }
+      if (at == NOFIT && ft != NO_GROUP) {
+        u32x8 p2[PLANE_N];
+        sload_group<PLANE_N>(p2, a.planes + (size_t)ft * GROUP_DWORDS);
+        at = group_first_feasible_s<false>(p2, ft);
+      }
+      rx = tol ? at : an;
+    }
   }
   if constexpr (S > 1) {
     s_res[wv][0][lane] = rm;
@@ -501,11 +555,11 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
     a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
     a.keys[(size_t)np + j] = rx != NOFIT ? shard_key(a.node_base, rx) : 0;
   } else {
-    const uint32_t ra = umin(rm, rx);
+    const uint32_t ra = umin(rm, rx);  // the first feasible node (identity-like: rx already is)
     int32_t oi, ost;
     int64_t osc;
-    decode_pod(rm != NOFIT ? (int64_t)rm : -1, rx != NOFIT ? (int64_t)rx : -1, ra != NOFIT ? (int64_t)ra : -1,
-               code != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
+    decode_pod(rm != NOFIT ? (int64_t)rm : -1, (KX && rx != NOFIT) ? (int64_t)rx : -1,
+               ra != NOFIT ? (int64_t)ra : -1, code != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
     d.out_idx[j] = oi;
     if (d.out_score) d.out_score[j] = osc;  // optional output (NULL: not written)
     d.out_status[j] = ost;
@@ -1792,14 +1846,15 @@ int pair_slices(int64_t waves, int32_t n_groups, const DeviceInfo& dev) {
   return sl;
 }
 
-template <int S, bool SHARD>
+template <int S, bool SHARD, bool KX>
 hipError_t launch_pair_s(PairArgs& a, int32_t bx, hipStream_t s) {
   a.gps = (a.n_groups + S - 1) / S;
-  MSH_TIMED_LAUNCH((pair_kernel<S, SHARD>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PAIR_WAVES * WAVE), 0, s, a);
+  MSH_TIMED_LAUNCH((pair_kernel<S, SHARD, KX>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PAIR_WAVES * WAVE), 0, s,
+                   a);
   return hipGetLastError();
 }
 
-template <bool SHARD>
+template <bool SHARD, bool KX>
 hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   int32_t maxp = 0;
   int64_t waves = 0;
@@ -1812,16 +1867,18 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   const int32_t blocks = (maxp + WAVE - 1) / WAVE;  // 64-pod blocks of the largest batch
   auto bx = [&](int sl) { return (blocks * sl + PAIR_WAVES - 1) / PAIR_WAVES; };
   switch (S) {
-    case 1: return launch_pair_s<1, SHARD>(a, bx(1), s);
-    case 2: return launch_pair_s<2, SHARD>(a, bx(2), s);
-    default: return launch_pair_s<4, SHARD>(a, bx(4), s);
+    case 1: return launch_pair_s<1, SHARD, KX>(a, bx(1), s);
+    case 2: return launch_pair_s<2, SHARD, KX>(a, bx(2), s);
+    default: return launch_pair_s<4, SHARD, KX>(a, bx(4), s);
   }
 }
 }  // namespace
 
 hipError_t launch_pairs(PairArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s) {
   if (a.nb <= 0 || a.nb > MULTI_MAX || (shard && a.nb != 1)) return hipErrorInvalidValue;
-  return shard ? launch_pair_t<true>(a, dev, s) : launch_pair_t<false>(a, dev, s);
+  // KX: the normalize mode needs each pod's first feasible non-match (REVERSE, MINMAX)
+  if (needs_kx(a.pp)) return shard ? launch_pair_t<true, true>(a, dev, s) : launch_pair_t<false, true>(a, dev, s);
+  return shard ? launch_pair_t<true, false>(a, dev, s) : launch_pair_t<false, false>(a, dev, s);
 }
 
 bool classrows_fit(int32_t n_groups) { return n_groups <= WGP_MAX_GROUPS; }

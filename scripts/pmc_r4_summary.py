@@ -68,9 +68,11 @@ for mode, prefix, tags, nb in (
     if "SQ_INSTS_VALU" in e:
         e["valu_lane_ops_per_eval"] = e["SQ_INSTS_VALU"] * 64 / (N * P * nb)
         if mode.startswith("pair"):
-            # the scan's model: 6.5 VALU per 32-node word and 64-pod wave (v_bitop3 AND + 4 v_bitop3 for
-            # dm', AND3 of two words' dm', one OR-accumulate of the feasible non-matches)
-            e["scan_model_share"] = 6.5 * WORDS * (P / 64) * nb / e["SQ_INSTS_VALU"]
+            # the scan's model per 32-node word and 64-pod wave: v_bitop3 (X & nT) + 4 v_bitop3 for dm' and
+            # half an AND3 of two words' dm' = 5.5 VALU (NONE); MIN-MAX adds one OR-accumulate of the
+            # feasible non-matches (6.5)
+            per_word = 6.5 if mode == "pair_minmax" else 5.5
+            e["scan_model_share"] = per_word * WORDS * (-(-P // 64)) * nb / e["SQ_INSTS_VALU"]
     if "SQ_WAVE_CYCLES" in e:
         for k in ("SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in e:

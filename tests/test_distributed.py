@@ -44,8 +44,9 @@ def _case(seed, n, p):
 
 
 def _shard_keys_oracle(dist_mod, u, nd, pd, pt, lo, hi):
-    """Per-shard keys exactly as msh_shard_keys_device defines them (ABI v7): p first feasible
-    match keys, then p first feasible NON-match keys, both per pod."""
+    """Per-shard keys exactly as msh_shard_keys_device defines them (ABI v7) for NONE normalize: p
+    first feasible match keys, then p first feasible node keys, both per pod (REVERSE / MINMAX put the
+    first feasible NON-match in the second slot; the decode below reads either form)."""
     us, ns = u[lo:hi], nd[lo:hi]
     p = len(pd)
     fm = np.full(p, -1, np.int64)
@@ -53,7 +54,7 @@ def _shard_keys_oracle(dist_mod, u, nd, pd, pt, lo, hi):
     for j in range(p):
         feas = np.ones(hi - lo, bool) if pt[j] else (us == 0)
         m = feas & (ns == pd[j]) & (pd[j] >= 0)
-        x = feas & ~m
+        x = feas
         if m.any():
             fm[j] = lo + int(np.argmax(m))
         if x.any():

@@ -845,6 +845,43 @@ def test_pair_kernel_late_matches(msh, oracle, n):
             _assert_same([out[i].cpu().numpy() for i in (2, 3, 4)], want, f"keys n={n} norm={norm}")
 
 
+@pytest.mark.parametrize("slices", [0, 1, 2, 4])
+@pytest.mark.parametrize("n", [1000, 5000, 20_000])
+def test_pair_kernel_late_feasible(msh, oracle, n, slices, monkeypatch):
+    """The identity-like modes take a pod's first feasible node from the scalar unit's per-group
+    feasibility (V & ~X, V): with the first 60% of the table unschedulable and digit 7 only there,
+    a non-tolerating pod of digit 7 has no feasible match and its first feasible node lies far above
+    the lowest group of every slice; tolerating pods match early. NONE, DEFAULT, no NodeNumber score,
+    MINMAX; batch and shard keys; every slice count."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_BITS_SLICES", str(slices))
+    rng = np.random.default_rng(n + slices)
+    u, nd, pd, pt = _rand_case(rng, n, 2000, p_unsched=0.0, p_tol=0.2)
+    cut = int(n * 0.6)
+    u[:cut] = 1
+    nd[cut:][nd[cut:] == 7] = 8
+    pd[: 600] = 7
+    dev = torch.device("cuda:0")
+    p = len(pd)
+    lists = [(["NodeNumber"], 1, 0), (["NodeNumber"], 2, 1), ([], 1, 0), (["NodeNumber"], 1, 3)]
+    with msh.DeviceContext(0) as ctx:
+        for score, w, norm in lists:
+            ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], score, w, norm)
+            _set(ctx, msh, ps)
+            ctx.upload_nodes(u, nd)
+            want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8)
+            _assert_same(ctx.schedule_batch(pd, pt), want, f"late-feasible n={n} {score} norm={norm}")
+            keys = torch.empty(ctx.shard_keys_len(p), dtype=torch.int32, device=dev)
+            d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+            st = torch.cuda.current_stream().cuda_stream
+            ctx.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), 0, keys.data_ptr(), st)
+            out = _dev_batch(torch, dev, pd, pt)
+            ctx.decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), keys.data_ptr(), out[2].data_ptr(),
+                                   out[3].data_ptr(), out[4].data_ptr(), st)
+            torch.cuda.synchronize()
+            _assert_same([out[i].cpu().numpy() for i in (2, 3, 4)], want, f"late-feasible keys n={n} norm={norm}")
+
+
 @pytest.mark.parametrize("kernel", ["pair", "classrows"])
 def test_batch_kernel_ab(msh, oracle, kernel, monkeypatch):
     """The default per-pair kernel and the opt-in class-row kernel (MSH_BATCH_KERNEL=classrows, read
