@@ -370,14 +370,17 @@ int ensure_table(msh_ctx* c, NodeTable& t, size_t n_pad) {
   return MSH_OK;
 }
 
+// The zero fill goes on prep_stream, ahead of the column copies queued there: a plain hipMemset runs
+// on the null stream, which a non-blocking prep_stream does not order against (the fill landed
+// after the first column upload and zeroed it).
 int ensure_cols(msh_ctx* c, NodeTable& t) {
   if (!t.d_cols) {
     MSH_HIP(c, hipMalloc(&t.d_cols, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t)));
-    MSH_HIP(c, hipMemset(t.d_cols, 0, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t)));
+    MSH_HIP(c, hipMemsetAsync(t.d_cols, 0, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t), c->prep_stream));
   }
   if (!t.d_cols100) {
     MSH_HIP(c, hipMalloc(&t.d_cols100, (size_t)msh::GEN_COLS * t.cap * sizeof(double)));
-    MSH_HIP(c, hipMemset(t.d_cols100, 0, (size_t)msh::GEN_COLS * t.cap * sizeof(double)));
+    MSH_HIP(c, hipMemsetAsync(t.d_cols100, 0, (size_t)msh::GEN_COLS * t.cap * sizeof(double), c->prep_stream));
   }
   return MSH_OK;
 }
