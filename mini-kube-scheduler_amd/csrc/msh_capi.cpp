@@ -745,7 +745,8 @@ bool read_knobs(msh::DeviceInfo& d, std::string* err) {
                   knob("MSH_SEQ_WAVES", {{"0", 0}, {"1", 1}, {"4", 4}, {"15", 15}, {"16", 16}}, &d.seq_waves, err) &&
                   knob("MSH_HOST_IO", {{"zero-copy", 0}, {"zc", 1}, {"dma", 2}}, &io, err) &&
                   knob("MSH_HOST_SYNC", {{"wait", 0}, {"poll", 1}}, &poll, err) &&
-                  knob("MSH_BATCH_KERNEL", {{"pair", 0}, {"classrows", 1}, {"generic", 2}}, &d.batch_kernel, err);
+                  knob("MSH_BATCH_KERNEL", {{"pair", 0}, {"classrows", 1}, {"generic", 2}}, &d.batch_kernel, err) &&
+                  knob("MSH_PAIR_PLANES", {{"auto", 0}, {"sgpr", 1}, {"lds", 2}}, &d.pair_planes, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;
   d.host_sync_poll = poll;

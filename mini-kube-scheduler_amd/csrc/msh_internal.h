@@ -50,6 +50,10 @@ struct DeviceInfo {
   // by its class, tables up to 8,192 nodes; larger tables and shard keys stay on pair_kernel);
   // 2 = generic_kernel for every plugin list ("generic", A/B)
   int batch_kernel = 0;
+  // Where pair_kernel's node planes come from (MSH_PAIR_PLANES at msh_create): 0 = auto (LDS-staged
+  // for tables up to PAIR_LDS_MAX_GROUPS groups and launches that fill the chip, scalar loads
+  // otherwise), 1 = scalar loads into SGPRs, 2 = LDS-staged (tables that fit)
+  int pair_planes = 0;
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit

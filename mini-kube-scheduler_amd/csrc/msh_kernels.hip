@@ -568,6 +568,212 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
 
 
 
+// ---------------------------------------------------------------------------------------
+// pair_kernel with the node planes staged in LDS (the default for tables up to PAIR_LDS_MAX_GROUPS
+// groups and launches that fill the chip). The same per-pair evaluation as pair_kernel, but every
+// v_bitop3 reads VGPRs only: an SGPR operand caps a wave64 VALU instruction at ~0.21 issues per
+// SIMD-cycle on MI355X where the all-VGPR forms reach 0.30-0.34 (scripts/ubench_valu_r4.hip,
+// profiles/r4_ubench_valu.jsonl), and pair_kernel's scan ran at that cap (0.215, profiles/r4_pmc_c3.json).
+// A workgroup copies the table's planes into LDS once and its waves then read each group's words as
+// wave-uniform ds_read_b128 (every lane the same address: a broadcast, no bank conflict) into VGPRs.
+// Each wave handles PL_BPW 64-pod blocks in turn, so the copy is amortised over 4 x PL_BPW blocks.
+// Per lane and 32-node word: xi = X & nT, dm' (4 v_bitop3), and per two words one AND3 into the
+// group's match flag, plus, KX, one OR of the feasible non-matches (dm' & ~xi), or, identity-like
+// modes, one AND3 of two words' xi per two words (the group holds a feasible node iff not all-ones).
+// ---------------------------------------------------------------------------------------
+constexpr int PL_WAVES = 4;  // waves per workgroup
+constexpr int PL_BPW = 4;    // 64-pod blocks per wave
+constexpr int PAIR_LDS_MAX_GROUPS = 128;  // 32,768 nodes, 24 KB of LDS per workgroup
+
+// The planes of group g from LDS (NPL planes, 8 words each) into VGPRs.
+template <int NPL>
+__device__ __forceinline__ void lds_group(uint32_t (&pl)[PLANE_N][PLANE_GW], const uint4* __restrict__ s_tab,
+                                          int32_t g) {
+  const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const uint4 lo = q[2 * k], hi = q[2 * k + 1];
+    pl[k][0] = lo.x; pl[k][1] = lo.y; pl[k][2] = lo.z; pl[k][3] = lo.w;
+    pl[k][4] = hi.x; pl[k][5] = hi.y; pl[k][6] = hi.z; pl[k][7] = hi.w;
+  }
+}
+
+__device__ __forceinline__ uint32_t pair_miss_v(const uint32_t (&pl)[PLANE_N][PLANE_GW], int w, uint32_t P0,
+                                                uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT, uint32_t& xi) {
+  xi = __builtin_amdgcn_bitop3_b32(pl[PLANE_X][w], nT, nT, 0xc0);  // X & nT
+  uint32_t t = bop3_or_xor(xi, pl[0][w], P0);
+  t = bop3_or_xor(t, pl[1][w], P1);
+  t = bop3_or_xor(t, pl[2][w], P2);
+  return bop3_or_xor(t, pl[3][w], P3);
+}
+
+// One group: am &= its dm' words; KX: ax |= its feasible non-matches; else af &= its xi words (not
+// all-ones iff the group holds a node feasible for the pod; a padding group also ORs ~V into xi).
+template <bool PAD, bool KX>
+__device__ __forceinline__ void pair_group_v(const uint32_t (&pl)[PLANE_N][PLANE_GW], uint32_t P0, uint32_t P1,
+                                             uint32_t P2, uint32_t P3, uint32_t nT, uint32_t& am, uint32_t& ax) {
+#pragma unroll
+  for (int w = 0; w < PLANE_GW; w += 2) {
+    uint32_t x0, x1;
+    const uint32_t t0 = pair_miss_v(pl, w, P0, P1, P2, P3, nT, x0);
+    const uint32_t t1 = pair_miss_v(pl, w + 1, P0, P1, P2, P3, nT, x1);
+    am = bop3_and3(am, t0, t1);
+    if constexpr (KX) {
+      if constexpr (PAD) {
+        ax |= bop3_andn_and(t0, x0, pl[PLANE_V][w]);
+        ax |= bop3_andn_and(t1, x1, pl[PLANE_V][w + 1]);
+      } else {
+        ax = bop3_or_andn(ax, t0, x0);
+        ax = bop3_or_andn(ax, t1, x1);
+      }
+    } else {
+      if constexpr (PAD) {  // infeasible: xi or not a real node
+        ax = bop3_and3(ax, x0 | ~pl[PLANE_V][w], x1 | ~pl[PLANE_V][w + 1]);
+      } else {
+        ax = bop3_and3(ax, x0, x1);
+      }
+    }
+  }
+}
+
+// The lane's first feasible node in group g (identity-like modes), NOFIT if none.
+__device__ __forceinline__ uint32_t group_first_feasible_v(const uint32_t (&pl)[PLANE_N][PLANE_GW], uint32_t g,
+                                                           uint32_t nT) {
+  uint32_t h[PLANE_GW];
+#pragma unroll
+  for (int c = 0; c < PLANE_GW; ++c) h[c] = pl[PLANE_V][c] & ~(pl[PLANE_X][c] & nT);
+  const uint32_t m = hits_first(h, 0u);
+  return m < GROUP_NODES ? g * GROUP_NODES + m : NOFIT;
+}
+
+// The lane's first feasible match (KIND 0), feasible non-match (1) or feasible node (2) in group g
+// of the LDS table, NOFIT if none.
+template <int KIND>
+__device__ __forceinline__ uint32_t group_first_lds(const uint4* __restrict__ s_tab, uint32_t g, uint32_t P0,
+                                                    uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT) {
+  uint32_t pl[PLANE_N][PLANE_GW];
+  lds_group<PLANE_N>(pl, s_tab, (int32_t)g);
+  if constexpr (KIND == 2) return group_first_feasible_v(pl, g, nT);
+  uint32_t h[PLANE_GW];
+#pragma unroll
+  for (int c = 0; c < PLANE_GW; ++c) {
+    const uint32_t dm = (pl[0][c] ^ P0) | (pl[1][c] ^ P1) | (pl[2][c] ^ P2) | (pl[3][c] ^ P3);
+    const uint32_t fe = ~(pl[PLANE_X][c] & nT) & pl[PLANE_V][c];
+    h[c] = KIND == 1 ? (dm & fe) : (~dm & fe);
+  }
+  const uint32_t m = hits_first(h, 0u);
+  return m < GROUP_NODES ? g * GROUP_NODES + m : NOFIT;
+}
+
+template <bool SHARD, bool KX>
+__global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
+  extern __shared__ uint4 s_tab[];  // n_groups * GROUP_DWORDS / 4
+  const BatchDesc& d = a.d[blockIdx.y];
+  const int32_t np = d.n_pods;
+  const int32_t wg0 = (int32_t)blockIdx.x * PL_WAVES * PL_BPW * WAVE;  // first pod of this workgroup
+  if (wg0 >= np) return;  // the whole workgroup lies past its batch's end
+  {
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(a.planes);
+    const int32_t nq = a.n_groups * (GROUP_DWORDS / 4);
+    for (int32_t i = threadIdx.x; i < nq; i += PL_WAVES * WAVE) s_tab[i] = src[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int32_t n_groups = a.n_groups, g_full = a.g_full;
+  for (int b = 0; b < PL_BPW; ++b) {
+    const int32_t wbase = wg0 + (b * PL_WAVES + wv) * WAVE;  // the workgroup's waves take adjacent blocks
+    if (wbase >= np) break;  // wave-uniform
+    const int32_t j = wbase + lane;
+    const bool act = j < np;
+    uint32_t code = CODE_NONE_POD, tol = 0u;
+    if (act) {
+      const int dq = d.pod_digit[j];
+      code = (dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;  // NodeNumber.PreScore: Atoi of the last byte
+      tol = d.pod_tol[j] ? 1u : 0u;
+    }
+    const uint32_t P0 = 0u - (code & 1u), P1 = 0u - ((code >> 1) & 1u), P2 = 0u - ((code >> 2) & 1u),
+                   P3 = 0u - (code >> 3);
+    const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
+    // groups above 0, descending, two per step (as pair_kernel): fm / fx the lower group of the lowest
+    // pair with a feasible match / KX: feasible non-match, identity-like: feasible node
+    uint32_t fm = NO_GROUP, fx = NO_GROUP;
+    for (int32_t g = n_groups - 1; g > 0; g -= 2) {
+      uint32_t am = 0xFFFFFFFFu, ax = KX ? 0u : 0xFFFFFFFFu;
+      const int32_t g2 = g - 1 > 0 ? g - 1 : g;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int32_t gg = h == 0 ? g : g - 1;
+        if (h == 1 && gg <= 0) break;
+        uint32_t pl[PLANE_N][PLANE_GW];
+        if (gg < g_full) {
+          lds_group<KX ? PLANE_V : PLANE_V>(pl, s_tab, gg);
+          pair_group_v<false, KX>(pl, P0, P1, P2, P3, nT, am, ax);
+        } else {
+          lds_group<PLANE_N>(pl, s_tab, gg);
+          pair_group_v<true, KX>(pl, P0, P1, P2, P3, nT, am, ax);
+        }
+      }
+      fm = am != 0xFFFFFFFFu ? (uint32_t)g2 : fm;
+      fx = (KX ? ax != 0u : ax != 0xFFFFFFFFu) ? (uint32_t)g2 : fx;
+    }
+    // group 0: its words kept
+    uint32_t rm = NOFIT, rx = NOFIT;
+    {
+      uint32_t pl[PLANE_N][PLANE_GW];
+      lds_group<PLANE_N>(pl, s_tab, 0);
+      uint32_t km[PLANE_GW], kx[PLANE_GW];
+#pragma unroll
+      for (int w = 0; w < PLANE_GW; ++w) {
+        uint32_t xi;
+        km[w] = pair_miss_v(pl, w, P0, P1, P2, P3, nT, xi);
+        if constexpr (KX) kx[w] = bop3_andn_and(km[w], xi, pl[PLANE_V][w]);
+      }
+      const uint32_t am = bop3_and3(bop3_and3(km[0], km[1], km[2]), bop3_and3(km[3], km[4], km[5]), km[6] & km[7]);
+      if (am != 0xFFFFFFFFu) {
+        uint32_t h[PLANE_GW];
+#pragma unroll
+        for (int w = 0; w < PLANE_GW; ++w) h[w] = ~km[w];
+        rm = hits_first(h, 0u);
+      } else if (fm != NO_GROUP) {  // the lowest hit pair: its lower group, else the one above
+        rm = group_first_lds<0>(s_tab, fm, P0, P1, P2, P3, nT);
+        if (rm == NOFIT) rm = group_first_lds<0>(s_tab, fm + 1, P0, P1, P2, P3, nT);
+      }
+      if constexpr (KX) {
+        const uint32_t ax = (kx[0] | kx[1] | kx[2]) | (kx[3] | kx[4] | kx[5]) | (kx[6] | kx[7]);
+        if (ax != 0u) {
+          rx = hits_first(kx, 0u);
+        } else if (fx != NO_GROUP) {
+          rx = group_first_lds<1>(s_tab, fx, P0, P1, P2, P3, nT);
+          if (rx == NOFIT) rx = group_first_lds<1>(s_tab, fx + 1, P0, P1, P2, P3, nT);
+        }
+      } else {
+        rx = group_first_feasible_v(pl, 0u, nT);
+        if (rx == NOFIT && fx != NO_GROUP) {
+          rx = group_first_lds<2>(s_tab, fx, P0, P1, P2, P3, nT);
+          if (rx == NOFIT) rx = group_first_lds<2>(s_tab, fx + 1, P0, P1, P2, P3, nT);
+        }
+      }
+    }
+    if (act) {
+      if constexpr (SHARD) {
+        a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
+        a.keys[(size_t)np + j] = rx != NOFIT ? shard_key(a.node_base, rx) : 0;
+      } else {
+        const uint32_t ra = umin(rm, rx);
+        int32_t oi, ost;
+        int64_t osc;
+        decode_pod(rm != NOFIT ? (int64_t)rm : -1, (KX && rx != NOFIT) ? (int64_t)rx : -1,
+                   ra != NOFIT ? (int64_t)ra : -1, code != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
+        d.out_idx[j] = oi;
+        if (d.out_score) d.out_score[j] = osc;
+        d.out_status[j] = ost;
+      }
+    }
+  }
+}
+
+
 // acc | (e & ~x), one v_bitop3_b32 (S0 = acc, S1 = e, S2 = x). The builtin, not inline asm: the
 // compiler then knows the instruction's hazards (inline asm got a conservative s_nop after each pair).
 __device__ __forceinline__ uint32_t acc_andn(uint32_t acc, uint32_t e, uint32_t x) {
@@ -1863,6 +2069,19 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
     waves += (a.d[b].n_pods + WAVE - 1) / WAVE;
   }
   if (maxp == 0) return hipSuccess;
+  // LDS-staged planes when the table fits and the launch fills the chip with whole workgroups (the
+  // copy is amortised over PL_WAVES x PL_BPW blocks); scalar-loaded planes (with slice waves) otherwise
+  const bool fits = a.n_groups <= PAIR_LDS_MAX_GROUPS;
+  const bool lds = fits && (dev.pair_planes == 2 ||
+                            (dev.pair_planes == 0 && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW && dev.bits_slices == 0));
+  if (lds) {
+    const int32_t blocks = (maxp + WAVE - 1) / WAVE;
+    const int32_t bx = (blocks + PL_WAVES * PL_BPW - 1) / (PL_WAVES * PL_BPW);
+    const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
+    MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PL_WAVES * WAVE),
+                     (unsigned)bytes, s, a);
+    return hipGetLastError();
+  }
   const int S = pair_slices(waves, a.n_groups, dev);
   const int32_t blocks = (maxp + WAVE - 1) / WAVE;  // 64-pod blocks of the largest batch
   auto bx = [&](int sl) { return (blocks * sl + PAIR_WAVES - 1) / PAIR_WAVES; };

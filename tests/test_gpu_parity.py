@@ -779,8 +779,9 @@ def test_multi_batch_age_shares(msh, oracle, n, norm, monkeypatch):
     u, nd, _, _ = _rand_case(rng, n, 1)
     pods = [_rand_case(rng, 1, p)[2:] for p in sizes]
     wants = [oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=16) for pd, pt in pods]
-    for kernel in ("classrows", "pair"):
+    for kernel, planes in (("classrows", "auto"), ("pair", "auto"), ("pair", "sgpr")):
         monkeypatch.setenv("MSH_BATCH_KERNEL", kernel)
+        monkeypatch.setenv("MSH_PAIR_PLANES", planes)  # auto: this launch takes the LDS-staged pair kernel
         with msh.DeviceContext(0) as ctx:
             _set(ctx, msh, ps)
             ctx.upload_nodes(u, nd)
@@ -791,7 +792,34 @@ def test_multi_batch_age_shares(msh, oracle, n, norm, monkeypatch):
             for k, (t, want) in enumerate(zip(bufs, wants)):
                 gi, gst = t[2].cpu().numpy(), t[4].cpu().numpy()
                 gs = t[3].cpu().numpy() if t[3] is not None else want[1]
-                _assert_same((gi, gs, gst), want, f"{kernel} batch {k} (p={len(pods[k][0])}) n={n} norm={norm}")
+                _assert_same((gi, gs, gst), want, f"{kernel}/{planes} batch {k} (p={len(pods[k][0])}) n={n} norm={norm}")
+
+
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+@pytest.mark.parametrize("nb", [1, 9, 33])
+def test_multi_batch_launch_lds(msh, oracle, norm, nb, monkeypatch):
+    """The LDS-staged pair kernel forced on small ragged multi-batch launches (MSH_PAIR_PLANES=lds):
+    workgroups whose blocks end inside or before a batch, empty and one-pod batches, NULL scores."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_PAIR_PLANES", "lds")
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(99 * nb + norm)
+    sizes = ([0, 1, 64, 65, 255, 257, 20_003, 5000, 333, 4096, 1, 2, 700, 64, 128, 1025, 999] * 2)[:nb]
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, norm)
+    u, nd, _, _ = _rand_case(rng, 7000, 1)
+    pods = [_rand_case(rng, 1, p)[2:] for p in sizes]
+    with msh.DeviceContext(0) as ctx:
+        _set(ctx, msh, ps)
+        ctx.upload_nodes(u, nd)
+        bufs = [_dev_batch(torch, dev, pd, pt, scores=(k % 4 != 3)) for k, (pd, pt) in enumerate(pods)]
+        ctx.schedule_batches_device(ctx.batch_descs([_desc(t) for t in bufs]),
+                                    stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for k, (t, (pd, pt)) in enumerate(zip(bufs, pods)):
+            want = oracle.c_schedule_batch(u, nd, pd, pt, ps)
+            gi, gst = t[2].cpu().numpy(), t[4].cpu().numpy()
+            gs = t[3].cpu().numpy() if t[3] is not None else want[1]
+            _assert_same((gi, gs, gst), want, f"lds batch {k} (p={len(pd)}) norm={norm}")
 
 
 def test_multi_batch_invalid(msh, gpu_ctx):
@@ -809,13 +837,15 @@ def test_multi_batch_invalid(msh, gpu_ctx):
         gpu_ctx.schedule_batches_device(bad)
 
 
-@pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 70_000])
-def test_pair_kernel_late_matches(msh, oracle, n):
+@pytest.mark.parametrize("planes", ["sgpr", "lds"])
+@pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 32_768, 70_000])
+def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
     """pair_kernel re-reads the first group with a hit from memory when it lies above the lowest group
     of the wave's range (kept in registers): digit 3 only in the second half of the table makes those
     pods' first matches late. Batch, multi-batch and shard-key entry points, NONE and MINMAX, on tables
     with and without a padded top group."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_PAIR_PLANES", planes)  # lds: tables up to 32,768 nodes (70,000 falls back)
     rng = np.random.default_rng(n + 4)
     u, nd, pd, pt = _rand_case(rng, n, 3000, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4
@@ -845,9 +875,9 @@ def test_pair_kernel_late_matches(msh, oracle, n):
             _assert_same([out[i].cpu().numpy() for i in (2, 3, 4)], want, f"keys n={n} norm={norm}")
 
 
-@pytest.mark.parametrize("slices", [0, 1, 2, 4])
+@pytest.mark.parametrize("planes,slices", [("sgpr", 0), ("sgpr", 1), ("sgpr", 2), ("sgpr", 4), ("lds", 0)])
 @pytest.mark.parametrize("n", [1000, 5000, 20_000])
-def test_pair_kernel_late_feasible(msh, oracle, n, slices, monkeypatch):
+def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices, monkeypatch):
     """The identity-like modes take a pod's first feasible node from the scalar unit's per-group
     feasibility (V & ~X, V): with the first 60% of the table unschedulable and digit 7 only there,
     a non-tolerating pod of digit 7 has no feasible match and its first feasible node lies far above
@@ -855,6 +885,7 @@ def test_pair_kernel_late_feasible(msh, oracle, n, slices, monkeypatch):
     MINMAX; batch and shard keys; every slice count."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("MSH_BITS_SLICES", str(slices))
+    monkeypatch.setenv("MSH_PAIR_PLANES", planes)  # "lds": the LDS-staged form whatever the launch size
     rng = np.random.default_rng(n + slices)
     u, nd, pd, pt = _rand_case(rng, n, 2000, p_unsched=0.0, p_tol=0.2)
     cut = int(n * 0.6)
@@ -1033,7 +1064,8 @@ def test_c3_reference_list_vs_oracle(msh, oracle, synth, kernel, monkeypatch):
     with msh.DeviceContext(0) as ctx:
         ctx.upload_nodes(u, nd)
         _assert_same(ctx.schedule_batch(pd, pt), want, f"C3 {kernel}")
-        ts = [_dev_batch(torch, dev, pd, pt) for _ in range(3)]
+        # 12 batches: enough waves for the launcher's LDS-staged pair kernel (bench.py's 32-batch launch)
+        ts = [_dev_batch(torch, dev, pd, pt) for _ in range(12)]
         ctx.schedule_batches_device(ctx.batch_descs([_desc(t) for t in ts]), stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         for t in ts:
