@@ -576,13 +576,14 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
 // profiles/r4_ubench_valu.jsonl), and pair_kernel's scan ran at that cap (0.215, profiles/r4_pmc_c3.json).
 // A workgroup copies the table's planes into LDS once and its waves then read each group's words as
 // wave-uniform ds_read_b128 (every lane the same address: a broadcast, no bank conflict) into VGPRs.
-// Each wave handles PL_BPW 64-pod blocks in turn, so the copy is amortised over 4 x PL_BPW blocks.
+// Each wave evaluates PL_BPW 64-pod blocks together: a group's planes are read from LDS once per wave
+// and applied to all of them, and the table copy is amortised over PL_WAVES x PL_BPW blocks.
 // Per lane and 32-node word: xi = X & nT, dm' (4 v_bitop3), and per two words one AND3 into the
 // group's match flag, plus, KX, one OR of the feasible non-matches (dm' & ~xi), or, identity-like
 // modes, one AND3 of two words' xi per two words (the group holds a feasible node iff not all-ones).
 // ---------------------------------------------------------------------------------------
 constexpr int PL_WAVES = 4;  // waves per workgroup
-constexpr int PL_BPW = 4;    // 64-pod blocks per wave
+constexpr int PL_BPW_MAX = 4;  // 64-pod blocks per wave (the kernel's PL_BPW: 2 or 4, DeviceInfo::pair_lds_bpw)
 constexpr int PAIR_LDS_MAX_GROUPS = 128;  // 32,768 nodes, 24 KB of LDS per workgroup
 
 // The planes of group g from LDS (NPL planes, 8 words each) into VGPRs.
@@ -665,7 +666,7 @@ __device__ __forceinline__ uint32_t group_first_lds(const uint4* __restrict__ s_
   return m < GROUP_NODES ? g * GROUP_NODES + m : NOFIT;
 }
 
-template <bool SHARD, bool KX>
+template <bool SHARD, bool KX, int PL_BPW>
 __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
   extern __shared__ uint4 s_tab[];  // n_groups * GROUP_DWORDS / 4
   const BatchDesc& d = a.d[blockIdx.y];
@@ -681,81 +682,102 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int32_t n_groups = a.n_groups, g_full = a.g_full;
+  // The wave's PL_BPW pod blocks are evaluated together: each group's planes are read from LDS once
+  // and applied to all of them (the LDS broadcast reads, ~6 CU-cycles each, would otherwise bound it).
+  const int32_t wbase = wg0 + wv * PL_BPW * WAVE;
+  if (wbase >= np) return;  // wave-uniform; no barrier below
+  uint32_t P0[PL_BPW], P1[PL_BPW], P2[PL_BPW], P3[PL_BPW], nT[PL_BPW], code[PL_BPW];
+#pragma unroll
   for (int b = 0; b < PL_BPW; ++b) {
-    const int32_t wbase = wg0 + (b * PL_WAVES + wv) * WAVE;  // the workgroup's waves take adjacent blocks
-    if (wbase >= np) break;  // wave-uniform
-    const int32_t j = wbase + lane;
-    const bool act = j < np;
-    uint32_t code = CODE_NONE_POD, tol = 0u;
-    if (act) {
+    const int32_t j = wbase + b * WAVE + lane;
+    uint32_t c = CODE_NONE_POD, t = 0u;
+    if (j < np) {
       const int dq = d.pod_digit[j];
-      code = (dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;  // NodeNumber.PreScore: Atoi of the last byte
-      tol = d.pod_tol[j] ? 1u : 0u;
+      c = (dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;  // NodeNumber.PreScore: Atoi of the last byte
+      t = d.pod_tol[j] ? 1u : 0u;
     }
-    const uint32_t P0 = 0u - (code & 1u), P1 = 0u - ((code >> 1) & 1u), P2 = 0u - ((code >> 2) & 1u),
-                   P3 = 0u - (code >> 3);
-    const uint32_t nT = tol ? 0u : 0xFFFFFFFFu;
-    // groups above 0, descending, two per step (as pair_kernel): fm / fx the lower group of the lowest
-    // pair with a feasible match / KX: feasible non-match, identity-like: feasible node
-    uint32_t fm = NO_GROUP, fx = NO_GROUP;
-    for (int32_t g = n_groups - 1; g > 0; g -= 2) {
-      uint32_t am = 0xFFFFFFFFu, ax = KX ? 0u : 0xFFFFFFFFu;
-      const int32_t g2 = g - 1 > 0 ? g - 1 : g;
+    code[b] = c;
+    P0[b] = 0u - (c & 1u);
+    P1[b] = 0u - ((c >> 1) & 1u);
+    P2[b] = 0u - ((c >> 2) & 1u);
+    P3[b] = 0u - (c >> 3);
+    nT[b] = t ? 0u : 0xFFFFFFFFu;
+  }
+  // groups above 0, descending, two per step (as pair_kernel): fm / fx the lower group of the lowest
+  // pair with a feasible match / KX: feasible non-match, identity-like: feasible node
+  uint32_t fm[PL_BPW], fx[PL_BPW];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int32_t gg = h == 0 ? g : g - 1;
-        if (h == 1 && gg <= 0) break;
-        uint32_t pl[PLANE_N][PLANE_GW];
-        if (gg < g_full) {
-          lds_group<KX ? PLANE_V : PLANE_V>(pl, s_tab, gg);
-          pair_group_v<false, KX>(pl, P0, P1, P2, P3, nT, am, ax);
-        } else {
-          lds_group<PLANE_N>(pl, s_tab, gg);
-          pair_group_v<true, KX>(pl, P0, P1, P2, P3, nT, am, ax);
-        }
-      }
-      fm = am != 0xFFFFFFFFu ? (uint32_t)g2 : fm;
-      fx = (KX ? ax != 0u : ax != 0xFFFFFFFFu) ? (uint32_t)g2 : fx;
+  for (int b = 0; b < PL_BPW; ++b) fm[b] = fx[b] = NO_GROUP;
+  for (int32_t g = n_groups - 1; g > 0; g -= 2) {
+    uint32_t am[PL_BPW], ax[PL_BPW];
+#pragma unroll
+    for (int b = 0; b < PL_BPW; ++b) {
+      am[b] = 0xFFFFFFFFu;
+      ax[b] = KX ? 0u : 0xFFFFFFFFu;
     }
-    // group 0: its words kept
-    uint32_t rm = NOFIT, rx = NOFIT;
-    {
+    const int32_t g2 = g - 1 > 0 ? g - 1 : g;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int32_t gg = h == 0 ? g : g - 1;
+      if (h == 1 && gg <= 0) break;
       uint32_t pl[PLANE_N][PLANE_GW];
-      lds_group<PLANE_N>(pl, s_tab, 0);
-      uint32_t km[PLANE_GW], kx[PLANE_GW];
+      if (gg < g_full) {
+        lds_group<PLANE_V>(pl, s_tab, gg);
 #pragma unroll
-      for (int w = 0; w < PLANE_GW; ++w) {
-        uint32_t xi;
-        km[w] = pair_miss_v(pl, w, P0, P1, P2, P3, nT, xi);
-        if constexpr (KX) kx[w] = bop3_andn_and(km[w], xi, pl[PLANE_V][w]);
-      }
-      const uint32_t am = bop3_and3(bop3_and3(km[0], km[1], km[2]), bop3_and3(km[3], km[4], km[5]), km[6] & km[7]);
-      if (am != 0xFFFFFFFFu) {
-        uint32_t h[PLANE_GW];
-#pragma unroll
-        for (int w = 0; w < PLANE_GW; ++w) h[w] = ~km[w];
-        rm = hits_first(h, 0u);
-      } else if (fm != NO_GROUP) {  // the lowest hit pair: its lower group, else the one above
-        rm = group_first_lds<0>(s_tab, fm, P0, P1, P2, P3, nT);
-        if (rm == NOFIT) rm = group_first_lds<0>(s_tab, fm + 1, P0, P1, P2, P3, nT);
-      }
-      if constexpr (KX) {
-        const uint32_t ax = (kx[0] | kx[1] | kx[2]) | (kx[3] | kx[4] | kx[5]) | (kx[6] | kx[7]);
-        if (ax != 0u) {
-          rx = hits_first(kx, 0u);
-        } else if (fx != NO_GROUP) {
-          rx = group_first_lds<1>(s_tab, fx, P0, P1, P2, P3, nT);
-          if (rx == NOFIT) rx = group_first_lds<1>(s_tab, fx + 1, P0, P1, P2, P3, nT);
-        }
+        for (int b = 0; b < PL_BPW; ++b) pair_group_v<false, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
       } else {
-        rx = group_first_feasible_v(pl, 0u, nT);
-        if (rx == NOFIT && fx != NO_GROUP) {
-          rx = group_first_lds<2>(s_tab, fx, P0, P1, P2, P3, nT);
-          if (rx == NOFIT) rx = group_first_lds<2>(s_tab, fx + 1, P0, P1, P2, P3, nT);
-        }
+        lds_group<PLANE_N>(pl, s_tab, gg);
+#pragma unroll
+        for (int b = 0; b < PL_BPW; ++b) pair_group_v<true, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
       }
     }
-    if (act) {
+#pragma unroll
+    for (int b = 0; b < PL_BPW; ++b) {
+      fm[b] = am[b] != 0xFFFFFFFFu ? (uint32_t)g2 : fm[b];
+      fx[b] = (KX ? ax[b] != 0u : ax[b] != 0xFFFFFFFFu) ? (uint32_t)g2 : fx[b];
+    }
+  }
+  // group 0 (its words kept), the exact first nodes, the decode: one block at a time
+  uint32_t pl[PLANE_N][PLANE_GW];
+  lds_group<PLANE_N>(pl, s_tab, 0);
+#pragma unroll
+  for (int b = 0; b < PL_BPW; ++b) {
+    const int32_t j = wbase + b * WAVE + lane;
+    if (wbase + b * WAVE >= np) break;  // wave-uniform
+    uint32_t rm = NOFIT, rx = NOFIT;
+    uint32_t km[PLANE_GW], kx[PLANE_GW];
+#pragma unroll
+    for (int w = 0; w < PLANE_GW; ++w) {
+      uint32_t xi;
+      km[w] = pair_miss_v(pl, w, P0[b], P1[b], P2[b], P3[b], nT[b], xi);
+      if constexpr (KX) kx[w] = bop3_andn_and(km[w], xi, pl[PLANE_V][w]);
+    }
+    const uint32_t am = bop3_and3(bop3_and3(km[0], km[1], km[2]), bop3_and3(km[3], km[4], km[5]), km[6] & km[7]);
+    if (am != 0xFFFFFFFFu) {
+      uint32_t h[PLANE_GW];
+#pragma unroll
+      for (int w = 0; w < PLANE_GW; ++w) h[w] = ~km[w];
+      rm = hits_first(h, 0u);
+    } else if (fm[b] != NO_GROUP) {  // the lowest hit pair: its lower group, else the one above
+      rm = group_first_lds<0>(s_tab, fm[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
+      if (rm == NOFIT) rm = group_first_lds<0>(s_tab, fm[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
+    }
+    if constexpr (KX) {
+      const uint32_t ax = (kx[0] | kx[1] | kx[2]) | (kx[3] | kx[4] | kx[5]) | (kx[6] | kx[7]);
+      if (ax != 0u) {
+        rx = hits_first(kx, 0u);
+      } else if (fx[b] != NO_GROUP) {
+        rx = group_first_lds<1>(s_tab, fx[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
+        if (rx == NOFIT) rx = group_first_lds<1>(s_tab, fx[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
+      }
+    } else {
+      rx = group_first_feasible_v(pl, 0u, nT[b]);
+      if (rx == NOFIT && fx[b] != NO_GROUP) {
+        rx = group_first_lds<2>(s_tab, fx[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
+        if (rx == NOFIT) rx = group_first_lds<2>(s_tab, fx[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
+      }
+    }
+    if (j < np) {
       if constexpr (SHARD) {
         a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
         a.keys[(size_t)np + j] = rx != NOFIT ? shard_key(a.node_base, rx) : 0;
@@ -764,7 +786,7 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
         int32_t oi, ost;
         int64_t osc;
         decode_pod(rm != NOFIT ? (int64_t)rm : -1, (KX && rx != NOFIT) ? (int64_t)rx : -1,
-                   ra != NOFIT ? (int64_t)ra : -1, code != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
+                   ra != NOFIT ? (int64_t)ra : -1, code[b] != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
         d.out_idx[j] = oi;
         if (d.out_score) d.out_score[j] = osc;
         d.out_status[j] = ost;
@@ -1103,6 +1125,7 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
   static_assert(MODE == 0 || S == 1, "the node-sharded modes run one wave per 64-pod block");
   constexpr int PB = GEN_WAVES / S;  // 64-pod blocks per workgroup
   constexpr int NE = 1 + NCOL;       // extents: [0] NodeNumber, [1 + c] column c of the list
+  constexpr int NC = NCOL > 0 ? NCOL : 1;
   constexpr int SW = S > 1 ? GEN_WAVES : 1;
   __shared__ int64_t s_mx[SW][NE][WAVE], s_mn[SW][NE][WAVE];
   __shared__ int64_t s_bt[SW][WAVE];
@@ -1135,12 +1158,12 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
   // the node is Spec.Unschedulable (with the filter listed), when only the tolerating lanes pass.
   const uint64_t tolm = __ballot(tol);
   auto lanes = [](uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); };
-  // The wave's node range in chunks of GEN_CH: a chunk's records (and column values) are loaded
-  // up front from one wave-uniform base (scalar loads, immediate offsets, one wait); a partial last
-  // chunk runs a copy of the body with a node-count guard.
+  // Per column of the list (wave-uniform): its raw values as int64 (a column without a normalizer) or
+  // as the exact double 100 x raw (a normalizing one), each read 8 nodes at a time by scalar loads.
   struct Chunk {
     uint32_t code[GEN_CH];
-    uint64_t fm[GEN_CH];  // NodeUnschedulable: the lanes that pass the node
+    uint64_t fm[GEN_CH];      // NodeUnschedulable: the lanes that pass the node
+    uint64_t cv[NC][GEN_CH];  // column values (raw bits: int64 or double)
   };
   auto load_chunk = [&](int32_t i0, auto cnt, Chunk& ch) {
     const uint32_t* __restrict__ r = nrec + (size_t)i0 * NREC;
@@ -1149,6 +1172,17 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
       if (k >= cnt) break;
       ch.code[k] = r[k * NREC];
       ch.fm[k] = tolm | ((uint64_t)r[k * NREC + 3] << 32 | r[k * NREC + 2]);
+    }
+#pragma unroll
+    for (int cc = 0; cc < NCOL; ++cc) {
+      const size_t off = (size_t)a.ccol[cc] * a.col_stride + i0;
+      const uint64_t* __restrict__ cb = a.cmode[cc] == 0 ? reinterpret_cast<const uint64_t*>(a.cols + off)
+                                                         : reinterpret_cast<const uint64_t*>(a.cols100 + off);
+#pragma unroll
+      for (int k = 0; k < GEN_CH; ++k) {
+        if (k >= cnt) break;
+        ch.cv[cc][k] = cb[k];
+      }
     }
   };
   auto for_chunks = [&](auto&& body) {
@@ -1159,8 +1193,18 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
       else body(i0, cnt);
     }
   };
+  auto as_f64 = [](uint64_t v) { return __builtin_bit_cast(double, v); };
+  // bit cc: column cc of the list normalizes (wave-uniform, in an SGPR)
+  int32_t nmask = 0;
+#pragma unroll
+  for (int cc = 0; cc < NCOL; ++cc) nmask |= a.cmode[cc] != 0 ? 1 << cc : 0;
+  nmask = __builtin_amdgcn_readfirstlane(nmask);
+  auto norm_col = [&](int cc) { return ((nmask >> cc) & 1) != 0; };
 
   // ---- stage 3: extents over the feasible nodes (normalizing plugins only) ----
+  // NodeNumber's raw scores are 10 / 0: its extent is which of the two a feasible node gives. A
+  // normalizing column's extent is a running f64 max / min of 100 x raw (exact) over the lanes that
+  // pass the node: one v_max_f64 / v_min_f64 each, under the feasibility mask as the exec mask.
   int64_t emx[NE], emn[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
@@ -1169,6 +1213,13 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
   }
   if (MODE != 2 && a.need_ext) {
     uint64_t fmm = 0, fxm = 0;  // NodeNumber: lanes with a feasible match / non-match seen
+    double dmx[NC], dmn[NC];
+#pragma unroll
+    for (int cc = 0; cc < NC; ++cc) {
+      dmx[cc] = -__builtin_inf();
+      dmn[cc] = __builtin_inf();
+    }
+    const bool nn_ext = a.nn_score && a.nn_mode != 0;
     for_chunks([&](int32_t i0, auto cnt) {
       Chunk ch;
       load_chunk(i0, cnt, ch);
@@ -1176,21 +1227,43 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
       for (int k = 0; k < GEN_CH; ++k) {
         if (k >= cnt) break;
         const uint64_t f = ch.fm[k];
-        const uint64_t m = __ballot(ch.code[k] == pcode);
-        fmm |= f & m;
-        fxm |= f & ~m;
+        if (nn_ext) {
+          const uint64_t m = __ballot(ch.code[k] == pcode);
+          fmm |= f & m;
+          fxm |= f & ~m;
+        }
 #pragma unroll
         for (int cc = 0; cc < NCOL; ++cc) {
-          if (a.cmode[cc] == 0) continue;
-          const int64_t v = (a.cols + (size_t)a.ccol[cc] * a.col_stride + i0)[k];
-          emx[1 + cc] = lanes(f & __ballot(v > emx[1 + cc])) ? v : emx[1 + cc];
-          emn[1 + cc] = lanes(f & __ballot(v < emn[1 + cc])) ? v : emn[1 + cc];
+          if (!norm_col(cc)) continue;
+          const double v = as_f64(ch.cv[cc][k]);
+          // v_max_f64 / v_min_f64 (inline: fmax adds a NaN canonicalisation per operand; no NaN
+          // here): every lane passes a schedulable node (f all-ones, the common case), only the
+          // tolerating lanes an unschedulable one (their update kept by a select)
+          const double hi = dmx[cc], lo = dmn[cc];
+          double h2, l2;
+          asm("v_max_f64 %0, %1, %2" : "=v"(h2) : "v"(hi), "s"(v));
+          asm("v_min_f64 %0, %1, %2" : "=v"(l2) : "v"(lo), "s"(v));
+          if (~f == 0) {
+            dmx[cc] = h2;
+            dmn[cc] = l2;
+          } else {
+            dmx[cc] = lanes(f) ? h2 : hi;
+            dmn[cc] = lanes(f) ? l2 : lo;
+          }
         }
       }
     });
     const bool fm = lanes(fmm), fx = lanes(fxm);
     emx[0] = fm ? 10 : (fx ? 0 : INT64_MIN);  // NodeNumber's raw scores are 10 / 0
     emn[0] = fx ? 0 : (fm ? 10 : INT64_MAX);
+#pragma unroll
+    for (int cc = 0; cc < NCOL; ++cc) {
+      if (a.cmode[cc] == 0) continue;
+      if (dmx[cc] != -__builtin_inf()) {  // 100 x raw / 100: exact (|raw| <= 2^31)
+        emx[1 + cc] = (int64_t)(dmx[cc] * 0.01);
+        emn[1 + cc] = (int64_t)(dmn[cc] * 0.01);
+      }
+    }
     if constexpr (S > 1) {  // the slices' partial extents meet in LDS
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
@@ -1230,18 +1303,21 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
   }
 
   // ---- per pod: NodeNumber's two weighted values, each normalizing column's reciprocal ----
-  int64_t c1 = 0, c0 = 0;  // both 0 when NodeNumber does not score: the per-pair select adds 0
-  if (a.nn_score && emx[0] != INT64_MIN) {
+  int64_t c1 = 0, c0 = 0;
+  if (a.nn_score && a.nn_mode != 0 && emx[0] != INT64_MIN) {
     c1 = (int64_t)((uint64_t)gen_normalize(10, a.nn_mode, emx[0], emn[0]) * (uint64_t)a.nn_weight);
     c0 = (int64_t)((uint64_t)gen_normalize(0, a.nn_mode, emx[0], emn[0]) * (uint64_t)a.nn_weight);
   } else if (a.nn_score) {
-    c1 = (int64_t)((uint64_t)10 * (uint64_t)a.nn_weight);  // NONE (no extent sweep): raw x weight
+    c1 = (int64_t)((uint64_t)10 * (uint64_t)a.nn_weight);  // NONE: raw x weight
   }
-  double rr[NCOL > 0 ? NCOL : 1], bb[NCOL > 0 ? NCOL : 1];
+  double rr[NC], bb[NC];
 #pragma unroll
-  for (int cc = 0; cc < NCOL; ++cc) {
+  for (int cc = 0; cc < NC; ++cc) {
     rr[cc] = 0.0;
     bb[cc] = 0.0;
+  }
+#pragma unroll
+  for (int cc = 0; cc < NCOL; ++cc) {
     const int32_t md = a.cmode[cc];
     const int64_t mx = emx[1 + cc], mn = emn[1 + cc];
     if (md == 0 || mx == INT64_MIN) continue;  // no normalizer, or no feasible node
@@ -1257,6 +1333,28 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
       // REVERSE with m == 0: r = 0, 100 - 0 = 100 for every node
     }
   }
+  // Wave-uniform: the normalizing columns' signed weights (REVERSE adds 100 w - n w: the 100 w of every
+  // REVERSE column is a constant of the total, summed once), and whether all of them fit 31 bits
+  // (then n x w + total is one v_mad_i64_i32).
+  int64_t cws[NC];
+  uint64_t tot0 = 0;
+  bool wsmall = true;
+#pragma unroll
+  for (int cc = 0; cc < NCOL; ++cc) {
+    const int32_t md = a.cmode[cc];
+    const int64_t w = a.cweight[cc];
+    cws[cc] = md == 2 ? -w : w;
+    if (md == 2) tot0 += (uint64_t)100 * (uint64_t)w;
+    if (md != 0) wsmall = wsmall && w < ((int64_t)1 << 31);
+    if (md != 3) bb[cc] = 0.0;  // (100 raw - b) with b = 0: one v_add_f64 for every mode, exact
+  }
+  // the fast path's per-column modes as one uniform bit set: bit cc = MIN-MAX (its numerator is never
+  // negative on a feasible pair)
+  int32_t mmask = 0;
+#pragma unroll
+  for (int cc = 0; cc < NCOL; ++cc) mmask |= a.cmode[cc] == 3 ? 1 << cc : 0;
+  mmask = __builtin_amdgcn_readfirstlane(mmask);
+  const int32_t wsm = __builtin_amdgcn_readfirstlane(wsmall ? 1 : 0);
 
   // ---- stages 1, 2, 4: feasibility, the total, the first maximum ----
   uint64_t best = 0x8000000000000000ull;  // INT64_MIN; the first feasible node is always taken
@@ -1272,27 +1370,34 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
     for (int k = 0; k < GEN_CH; ++k) {
       if (k >= cnt) break;
       const uint64_t f = ch.fm[k];
-      // the node-only part: weight x column of the columns without a normalizer (scalar unit)
-      uint64_t tot = 0;
+      // the node-only part (scalar unit): weight x column of the columns without a normalizer
+      uint64_t ts = tot0;
 #pragma unroll
       for (int cc = 0; cc < NCOL; ++cc)
-        if (a.cmode[cc] == 0)
-          tot += (uint64_t)(a.cols + (size_t)a.ccol[cc] * a.col_stride + i0)[k] * (uint64_t)a.cweight[cc];
-      tot += (ch.code[k] == pcode) ? cw1 : cw0;  // NodeNumber: 10 on a suffix-digit match
+        if (!norm_col(cc)) ts += ch.cv[cc][k] * (uint64_t)a.cweight[cc];
+      // NodeNumber: 10 on a suffix-digit match (c1 = c0 = 0 when it does not score)
+      uint64_t tot = ts + ((ch.code[k] == pcode) ? cw1 : cw0);
 #pragma unroll
       for (int cc = 0; cc < NCOL; ++cc) {
-        const int32_t md = a.cmode[cc];
-        if (md == 0) continue;
-        const double A = (a.cols100 + (size_t)a.ccol[cc] * a.col_stride + i0)[k];  // 100 x raw, exact
-        const double q = (md == 3 ? A - bb[cc] : A) * rr[cc];
-        int64_t n;
-        if (md == 3 || A >= 0.0) {  // |q| <= 100 on a feasible pair: the 32-bit conversion (clamped)
-          n = (int32_t)__builtin_fmin(__builtin_fmax(q, -2147483648.0), 2147483647.0);
+        if (!norm_col(cc)) continue;
+        const uint64_t bits = ch.cv[cc][k];
+        const double q = (as_f64(bits) - bb[cc]) * rr[cc];  // (100 raw - b) x r: both operations exact
+        // the numerator's sign from the node value's top dword (scalar unit): MIN-MAX numerators of
+        // feasible pairs are never negative
+        // (readfirstlane keeps the test a 32-bit scalar compare: folded to a 64-bit compare, which the
+        // scalar unit lacks, it became a VALU v_cmp_gt_i64 per pair)
+        const bool nonneg =
+            ((mmask >> cc) & 1) != 0 || __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(bits >> 32)) >= 0;
+        if (nonneg && wsm) {
+          // |q| <= 100 on a feasible pair: v_cvt_i32_f64 (saturating in hardware: the value of an
+          // infeasible pair converts without a fault and is never taken), then n x w + total in one
+          // v_mad_i64_i32
+          const int32_t n = (int32_t)q;
+          tot = (uint64_t)((int64_t)n * (int64_t)(int32_t)cws[cc] + (int64_t)tot);
         } else {
-          n = (int64_t)q;  // |q| < 2^40
+          const int64_t n = (int64_t)__builtin_fmin(__builtin_fmax(q, -0x1p62), 0x1p62);  // |q| < 2^40 if feasible
+          tot += (uint64_t)n * (uint64_t)cws[cc];
         }
-        if (md == 2) n = 100 - n;
-        tot += (uint64_t)n * (uint64_t)a.cweight[cc];
       }
       const uint64_t take = f & (~fdm | __ballot((int64_t)tot > (int64_t)best));  // strict '>': the first max
       best = lanes(take) ? tot : best;
@@ -2073,13 +2178,18 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   // copy is amortised over PL_WAVES x PL_BPW blocks); scalar-loaded planes (with slice waves) otherwise
   const bool fits = a.n_groups <= PAIR_LDS_MAX_GROUPS;
   const bool lds = fits && (dev.pair_planes == 2 ||
-                            (dev.pair_planes == 0 && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW && dev.bits_slices == 0));
+                            (dev.pair_planes == 0 && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX && dev.bits_slices == 0));
   if (lds) {
+    const int bpw = dev.pair_lds_bpw == 2 ? 2 : 4;
     const int32_t blocks = (maxp + WAVE - 1) / WAVE;
-    const int32_t bx = (blocks + PL_WAVES * PL_BPW - 1) / (PL_WAVES * PL_BPW);
+    const int32_t bx = (blocks + PL_WAVES * bpw - 1) / (PL_WAVES * bpw);
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
-    MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PL_WAVES * WAVE),
-                     (unsigned)bytes, s, a);
+    if (bpw == 2)
+      MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PL_WAVES * WAVE),
+                       (unsigned)bytes, s, a);
+    else
+      MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 4>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PL_WAVES * WAVE),
+                       (unsigned)bytes, s, a);
     return hipGetLastError();
   }
   const int S = pair_slices(waves, a.n_groups, dev);
