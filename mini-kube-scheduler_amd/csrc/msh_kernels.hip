@@ -796,13 +796,6 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
 }
 
 
-// acc | (e & ~x), one v_bitop3_b32 (S0 = acc, S1 = e, S2 = x). The builtin, not inline asm: the
-// compiler then knows the instruction's hazards (inline asm got a conservative s_nop after each pair).
-__device__ __forceinline__ uint32_t acc_andn(uint32_t acc, uint32_t e, uint32_t x) {
-  return __builtin_amdgcn_bitop3_b32(acc, e, x, 0xf4);
-}
-// e & ~x (the first word of a group: S0 is a don't-care)
-__device__ __forceinline__ uint32_t andn(uint32_t e, uint32_t x) { return __builtin_amdgcn_bitop3_b32(e, e, x, 0x44); }
 __device__ __forceinline__ uint32_t min1(uint32_t x) {  // x != 0 as 0 / 1 in one v_min_u32
   uint32_t r;
   asm("v_min_u32 %0, 1, %1" : "=v"(r) : "v"(x));
@@ -994,44 +987,31 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
     const uint32_t tol = cur.tol;
     const uint32_t e0 = cur.e0, e1 = cur.e1;  // the lane's chunk-0 and chunk-1 class-row entries
     const uint32_t cls = cur.cls;               // its class (first-node tables)
-    const uint32_t fa = HR_F + 2 * tol;         // F[tol] (KX)
     // Groups descending, four per step (eight ds_read_b128 in flight; n_groups is a multiple of 4:
     // tables are padded to 1,024-node blocks), one flag per PAIR of groups: bit q of bm = group 2q or
     // 2q + 1 holds a feasible digit match (the 16 words of a pair reduce in 8 VALU: 7 v_bitop3 OR3 and
-    // one more), and, KX, bit q of bx = one of them holds a feasible non-match (F[t] & ~H, one v_bitop3
-    // per word). The previous item's stores and the next item's loads go after the first step.
+    // one more), and, KX, bit q of bx = one of them holds a feasible non-match (below). The previous
+    // item's stores and the next item's loads go after the first step.
     uint32_t bm = 0, bx = 0;
     auto or16 = [](const uint4& a, const uint4& b, const uint4& c, const uint4& d) {
       return or3(or3(or3(a.x, a.y, a.z), or3(a.w, b.x, b.y), or3(b.z, b.w, c.x)),
                  or3(or3(c.y, c.z, c.w), or3(d.x, d.y, d.z), d.w), 0u);
     };
-    auto nm16 = [&](const uint4* tg, const uint4& a, const uint4& b, const uint4& c, const uint4& d) {
-      const uint4 f0 = tg[fa], f1 = tg[fa + 1], f2 = tg[GQL + fa], f3 = tg[GQL + fa + 1];
-      uint32_t n = andn(f0.x, a.x);
-      n = acc_andn(n, f0.y, a.y);
-      n = acc_andn(n, f0.z, a.z);
-      n = acc_andn(n, f0.w, a.w);
-      n = acc_andn(n, f1.x, b.x);
-      n = acc_andn(n, f1.y, b.y);
-      n = acc_andn(n, f1.z, b.z);
-      n = acc_andn(n, f1.w, b.w);
-      n = acc_andn(n, f2.x, c.x);
-      n = acc_andn(n, f2.y, c.y);
-      n = acc_andn(n, f2.z, c.z);
-      n = acc_andn(n, f2.w, c.w);
-      n = acc_andn(n, f3.x, d.x);
-      n = acc_andn(n, f3.y, d.y);
-      n = acc_andn(n, f3.z, d.z);
-      n = acc_andn(n, f3.w, d.w);
-      return n;
+    // KX: whether a group holds a feasible non-match for the pod's class is its first-node offset
+    // (hr_first_kernel, per upload) != HR_NONE: one 2-byte LDS read per group instead of the F[t] & ~H
+    // words (8 ds_read_b128 and 34 VALU per four groups; the MIN-MAX launch took 1.8x the identity's)
+    const uint16_t* __restrict__ offx = reinterpret_cast<const uint16_t*>(s_tab + HR_FIRST) + HR_CLS + cls;
+    constexpr int GQ16 = GQL * 8;  // a group's stride in uint16
+    auto nx2 = [&](int32_t g) {    // groups g, g + 1: 1 if either holds a feasible non-match
+      const uint32_t o0 = offx[g * GQ16], o1 = offx[(g + 1) * GQ16];
+      return min1(umin(o0, o1) ^ (uint32_t)HR_NONE);
     };
     auto step = [&](int32_t q) {  // groups q .. q + 3
       const uint4* t = s_tab + q * GQL;
       const uint4 a0 = t[e0], b0 = t[e1], a1 = t[GQL + e0], b1 = t[GQL + e1];
       const uint4 a2 = t[2 * GQL + e0], b2 = t[2 * GQL + e1], a3 = t[3 * GQL + e0], b3 = t[3 * GQL + e1];
       bm = lshl_or(bm, 2, lshl_or(min1(or16(a2, b2, a3, b3)), 1, min1(or16(a0, b0, a1, b1))));
-      if constexpr (KX)
-        bx = lshl_or(bx, 2, lshl_or(min1(nm16(t + 2 * GQL, a2, b2, a3, b3)), 1, min1(nm16(t, a0, b0, a1, b1))));
+      if constexpr (KX) bx = lshl_or(bx, 2, lshl_or(nx2(q + 2), 1, nx2(q)));
     };
     int32_t q = n_groups - 4;
     if (q >= 0) {
