@@ -58,11 +58,15 @@ LANES_PER_SIMD_CYCLE = 32          # MI355X_MICROARCH.md: SIMD-32, a wave64 VALU
 # v_bitop3 OR-accumulate of the feasible non-matches: 6.5
 PAIR_VALU_PER_WORD = 5.5
 PAIR_VALU_PER_WORD_KX = 6.5
+# the LDS-staged form (pair_lds_kernel) also ANDs two words' xi per two words (its first feasible node
+# is tracked per lane, not on the scalar unit): 6.0 in NONE
+PAIR_VALU_PER_WORD_LDS = 6.0
 # generic_kernel's main sweep on the reference list (NodeNumber only): per pair v_cmp_eq (suffix
 # digits), 2 v_cndmask (the lane's two weighted values), v_cmp_gt_i64 (strict first max), 3 v_cndmask
 # (best total, chunk-relative index): 7 VALU lane-ops per pair
 GEN_VALU_PER_PAIR_REF = 7.0
 WGP_MAX_GROUPS = 32                # msh_kernels.hip: the class-row kernel's table limit (groups of 256 nodes)
+PAIR_LDS_MAX_GROUPS = 128          # msh_kernels.hip: tables the LDS-staged pair kernel takes
 PMC_FILE = ROOT / "profiles" / "r4_pmc_c3.json"
 VALU_PEAK_FILE = ROOT / "profiles" / "r3_ubench_valu_peak.json"
 
@@ -77,6 +81,8 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
     if classrows and groups <= WGP_MAX_GROUPS and not shard:
         return f"void msh::wgp_kernel<4, {b(kx)}>"
     waves = -(-n_pods // 64) * (nb if multi else 1)
+    if groups <= PAIR_LDS_MAX_GROUPS and not kx and waves >= cus * 4 * 4 * 4:  # the LDS-staged form
+        return f"void msh::pair_lds_kernel<{b(shard)}, false, 2>"
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2
@@ -475,12 +481,15 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
     evals = float(n_local) * p * nb
     n_pad = max(-(-n_local // 1024) * 1024, 1024)
     # every 64-pod wave meets every 32-node word of the padded table once
-    model_per_eval = PAIR_VALU_PER_WORD * (n_pad / 32) * (-(-p // 64) * 64) / (float(n_local) * p)
+    lds = "pair_lds_kernel" in kname
+    per_word = PAIR_VALU_PER_WORD_LDS if lds else PAIR_VALU_PER_WORD
+    model_per_eval = per_word * (n_pad / 32) * (-(-p // 64) * 64) / (float(n_local) * p)
     entry = pmc_entry("pair_multi" if nb > 1 else "pair_single", kname, n_local, p, nb)
     out = valu_roofline(kname, launch_ms, evals, model_per_eval, cus, entry,
-                        "5.5 VALU per 32-node word and 64-pod wave (pair_kernel's scan, msh_kernels.hip, NONE "
-                        "normalize): per lane-op 32 (pod, node) pairs get NodeUnschedulable's verdict and "
-                        "NodeNumber's digit compare; lane-ops per eval = 5.5 x padded words x padded pods / (n x p)")
+                        f"{per_word} VALU per 32-node word and 64-pod wave ({kname.split('<')[0][10:]}'s scan, "
+                        "msh_kernels.hip, NONE normalize): per lane-op 32 (pod, node) pairs get NodeUnschedulable's "
+                        f"verdict and NodeNumber's digit compare; lane-ops per eval = {per_word} x padded words x "
+                        "padded pods / (n x p)")
     out["batches_per_launch"] = nb
     out["ms_per_batch"] = launch_ms / nb
     # HBM: the bit planes once (0.75 B per node: 6 planes of 32 nodes per 4 B), 2 B in + 16 B out per pod

@@ -2156,11 +2156,15 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   if (maxp == 0) return hipSuccess;
   // LDS-staged planes when the table fits and the launch fills the chip with whole workgroups (the
   // copy is amortised over PL_WAVES x PL_BPW blocks); scalar-loaded planes (with slice waves) otherwise
+  // (auto: the identity-like modes only; REVERSE / MINMAX ran slower LDS-staged, 101.5 / 104.2 us per
+  // 32-batch C3 launch against 97.6 with scalar-loaded planes, where NONE gained 97.0 -> 89.8 us:
+  // profiles/r4_ab_pair_planes.txt)
   const bool fits = a.n_groups <= PAIR_LDS_MAX_GROUPS;
   const bool lds = fits && (dev.pair_planes == 2 ||
-                            (dev.pair_planes == 0 && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX && dev.bits_slices == 0));
+                            (dev.pair_planes == 0 && !KX && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX &&
+                             dev.bits_slices == 0));
   if (lds) {
-    const int bpw = dev.pair_lds_bpw == 2 ? 2 : 4;
+    const int bpw = dev.pair_lds_bpw == 4 ? 4 : 2;
     const int32_t blocks = (maxp + WAVE - 1) / WAVE;
     const int32_t bx = (blocks + PL_WAVES * bpw - 1) / (PL_WAVES * bpw);
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);

@@ -45,8 +45,8 @@ def stats_avg_ns(tag, prefix):
 
 res = {"source": str(src), "nodes": N, "pods": P, "kernels": {}, "stats": {}}
 for mode, prefix, tags, nb in (
-        ("pair_multi", "msh::pair_kernel", ("m_sq", "m_sq2", "m_grbm", "m_fetch", "m_write"), NB),
-        ("pair_minmax", "msh::pair_kernel", ("k_sq",), NB),
+        ("pair_multi", "msh::pair", ("m_sq", "m_sq2", "m_grbm", "m_fetch", "m_write"), NB),
+        ("pair_minmax", "msh::pair", ("k_sq",), NB),
         ("classrows_multi", "msh::wgp_kernel", ("c_sq",), NB),
         ("generic_ref", "msh::generic_kernel", ("g_sq", "g_grbm", "g_fetch"), NB),
         ("generic_col", "msh::generic_kernel", ("gc_sq",), NB),
@@ -71,7 +71,9 @@ for mode, prefix, tags, nb in (
             # the scan's model per 32-node word and 64-pod wave: v_bitop3 (X & nT) + 4 v_bitop3 for dm' and
             # half an AND3 of two words' dm' = 5.5 VALU (NONE); MIN-MAX adds one OR-accumulate of the
             # feasible non-matches (6.5)
-            per_word = 6.5 if mode == "pair_minmax" else 5.5
+            # (the LDS-staged form adds half an AND3 of two words' xi per word in NONE: 6.0)
+            lds = "pair_lds" in e.get("kernel", "")
+            per_word = 6.5 if mode == "pair_minmax" else (6.0 if lds else 5.5)
             e["scan_model_share"] = per_word * WORDS * (-(-P // 64)) * nb / e["SQ_INSTS_VALU"]
     if "SQ_WAVE_CYCLES" in e:
         for k in ("SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):
@@ -82,9 +84,9 @@ for mode, prefix, tags, nb in (
         e["gui_active_cycles_per_xcd"] = cyc
         e["valu_wave_instr_per_simd_cycle"] = e["SQ_INSTS_VALU"] / (1024 * cyc)
     res["kernels"][mode] = e
-for tag, prefix in (("stats", "msh::pair_kernel"), ("stats_k20", "msh::pair_kernel"),
-                    ("stats_multi", "msh::pair_kernel"), ("stats_single", "msh::pair_kernel"),
-                    ("stats_kx", "msh::pair_kernel"), ("stats_classrows", "msh::wgp_kernel"),
+for tag, prefix in (("stats", "msh::pair"), ("stats_k20", "msh::pair"),
+                    ("stats_multi", "msh::pair"), ("stats_single", "msh::pair"),
+                    ("stats_kx", "msh::pair"), ("stats_classrows", "msh::wgp_kernel"),
                     ("stats_classrows_kx", "msh::wgp_kernel"), ("stats_generic", "msh::generic_kernel"),
                     ("stats_generic_col", "msh::generic_kernel"), ("stats_seq", "msh::seq_kernel")):
     name, avg, calls = stats_avg_ns(tag, prefix)
