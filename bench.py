@@ -68,7 +68,7 @@ GEN_VALU_PER_PAIR_REF = 7.0
 WGP_MAX_GROUPS = 32                # msh_kernels.hip: the class-row kernel's table limit (groups of 256 nodes)
 PAIR_LDS_MAX_GROUPS = 128          # msh_kernels.hip: tables the LDS-staged pair kernel takes
 PMC_FILE = ROOT / "profiles" / "r4_pmc_c3.json"
-VALU_PEAK_FILE = ROOT / "profiles" / "r3_ubench_valu_peak.json"
+VALU_PEAK_FILE = ROOT / "profiles" / "r4_ubench_valu.json"
 
 
 def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False,
@@ -398,10 +398,11 @@ def main():
 
 
 def load_valu_peak():
-    """The integer VALU issue rate measured on MI355X (scripts/ubench_valu_peak.hip ->
-    profiles/r3_ubench_valu_peak.json): wave64 instructions per SIMD per cycle for the scan's forms."""
+    """The integer VALU issue rates measured on MI355X (scripts/ubench_valu_r4.hip ->
+    profiles/r4_ubench_valu.json), wave64 instructions per SIMD per cycle at 8 waves per SIMD: the best
+    VGPR-only form (the issue peak) and the cap with one SGPR operand."""
     d = load_json(VALU_PEAK_FILE) or {}
-    return d.get("scan_forms_wave_instr_per_simd_cycle") or d.get("int_valu_wave_instr_per_simd_cycle"), d
+    return d.get("vgpr_only_max"), d
 
 
 def pmc_entry(key: str, kname: str, n_local: int, p: int, nb: int):
@@ -420,8 +421,9 @@ def valu_roofline(kname, launch_ms, evals, model_lane_ops_per_eval, cus, entry, 
     of the same kernel, size and batch count (profiles/r4_pmc_c3.json)."""
     launch_s = launch_ms * 1e-3
     peak = cus * 4 * LANES_PER_SIMD_CYCLE * CLOCK_HZ  # lane-ops/s
-    ipc, _ = load_valu_peak()
+    ipc, vd = load_valu_peak()
     peak_meas = ipc * 4 * 64 * cus * CLOCK_HZ if ipc else None
+    sgpr_cap = vd.get("sgpr_operand_max")
     model = evals * model_lane_ops_per_eval
     instr = entry.get("SQ_INSTS_VALU") if entry else None
     cnt = instr * 64 if instr else None
@@ -447,8 +449,10 @@ def valu_roofline(kname, launch_ms, evals, model_lane_ops_per_eval, cus, entry, 
         "peak_note": "MI355X_MICROARCH.md: SIMD-32 (a wave64 VALU instruction over 2 cycles), 4 SIMD per CU, 2.4 GHz",
         "peak_measured_issue": peak_meas / 1e9 if peak_meas else None,
         "frac_of_measured_issue": model / launch_s / peak_meas if peak_meas else None,
-        "peak_measured_note": ("the integer VALU issue rate measured for v_bitop3-class forms (8 waves per SIMD, "
-                               f"{VALU_PEAK_FILE.name}): {ipc:.3f} wave-instr per SIMD-cycle" if ipc else None),
+        "peak_measured_note": ("the best integer VALU issue rate measured with VGPR operands only (8 waves per "
+                               f"SIMD, {VALU_PEAK_FILE.name}): {ipc:.3f} wave-instr per SIMD-cycle; with one SGPR "
+                               f"operand the same forms cap at {sgpr_cap:.3f}" if ipc and sgpr_cap else None),
+        "sgpr_operand_cap": sgpr_cap * 4 * 64 * cus * CLOCK_HZ / 1e9 if sgpr_cap else None,
     }
 
 
