@@ -648,22 +648,36 @@ __device__ __forceinline__ uint32_t group_first_feasible_v(const uint32_t (&pl)[
 }
 
 // The lane's first feasible match (KIND 0), feasible non-match (1) or feasible node (2) in group g
-// of the LDS table, NOFIT if none.
+// of the LDS table, NOFIT if none: half a group (four words, 6 x 4 plane words live) at a time.
 template <int KIND>
 __device__ __forceinline__ uint32_t group_first_lds(const uint4* __restrict__ s_tab, uint32_t g, uint32_t P0,
                                                     uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT) {
-  uint32_t pl[PLANE_N][PLANE_GW];
-  lds_group<PLANE_N>(pl, s_tab, (int32_t)g);
-  if constexpr (KIND == 2) return group_first_feasible_v(pl, g, nT);
-  uint32_t h[PLANE_GW];
+  const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
 #pragma unroll
-  for (int c = 0; c < PLANE_GW; ++c) {
-    const uint32_t dm = (pl[0][c] ^ P0) | (pl[1][c] ^ P1) | (pl[2][c] ^ P2) | (pl[3][c] ^ P3);
-    const uint32_t fe = ~(pl[PLANE_X][c] & nT) & pl[PLANE_V][c];
-    h[c] = KIND == 1 ? (dm & fe) : (~dm & fe);
+  for (int hh = 0; hh < 2; ++hh) {
+    uint32_t pl[PLANE_N][4];
+#pragma unroll
+    for (int k = 0; k < PLANE_N; ++k) {
+      const uint4 v = q[2 * k + hh];
+      pl[k][0] = v.x; pl[k][1] = v.y; pl[k][2] = v.z; pl[k][3] = v.w;
+    }
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t fe = ~(pl[PLANE_X][c] & nT) & pl[PLANE_V][c];
+      uint32_t h;
+      if constexpr (KIND == 2) {
+        h = fe;
+      } else {
+        const uint32_t dm = (pl[0][c] ^ P0) | (pl[1][c] ^ P1) | (pl[2][c] ^ P2) | (pl[3][c] ^ P3);
+        h = KIND == 1 ? (dm & fe) : (~dm & fe);
+      }
+      t[c] = lowbit(h) | (uint32_t)(32 * c);  // all-ones when the word has none
+    }
+    const uint32_t m = umin(umin(t[0], t[1]), umin(t[2], t[3]));
+    if (m < 128u) return g * GROUP_NODES + (uint32_t)(hh * 128) + m;
   }
-  const uint32_t m = hits_first(h, 0u);
-  return m < GROUP_NODES ? g * GROUP_NODES + m : NOFIT;
+  return NOFIT;
 }
 
 template <bool SHARD, bool KX, int PL_BPW>
@@ -703,89 +717,118 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
     P3[b] = 0u - (c >> 3);
     nT[b] = t ? 0u : 0xFFFFFFFFu;
   }
-  // groups above 0, descending, two per step (as pair_kernel): fm / fx the lower group of the lowest
-  // pair with a feasible match / KX: feasible non-match, identity-like: feasible node
-  uint32_t fm[PL_BPW], fx[PL_BPW];
+  // Groups above 0, descending, one group per iteration and a half-group (four words) per LDS read set,
+  // so that only 5-6 x 4 plane words are live (the whole group's 48 held the kernel to 4 waves per
+  // SIMD). Flags per pair of groups (as pair_kernel): fm / fx the lower group of the lowest pair with a
+  // feasible match / KX: feasible non-match, identity-like: feasible node.
+  uint32_t fm[PL_BPW], fx[PL_BPW], am[PL_BPW], ax[PL_BPW];
 #pragma unroll
-  for (int b = 0; b < PL_BPW; ++b) fm[b] = fx[b] = NO_GROUP;
-  for (int32_t g = n_groups - 1; g > 0; g -= 2) {
-    uint32_t am[PL_BPW], ax[PL_BPW];
-#pragma unroll
-    for (int b = 0; b < PL_BPW; ++b) {
-      am[b] = 0xFFFFFFFFu;
-      ax[b] = KX ? 0u : 0xFFFFFFFFu;
-    }
-    const int32_t g2 = g - 1 > 0 ? g - 1 : g;
+  for (int b = 0; b < PL_BPW; ++b) {
+    fm[b] = fx[b] = NO_GROUP;
+    am[b] = 0xFFFFFFFFu;
+    ax[b] = KX ? 0u : 0xFFFFFFFFu;
+  }
+#pragma unroll 1
+  for (int32_t g = n_groups - 1; g > 0; --g) {
+    const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
+    const bool pad = g >= g_full;  // wave-uniform
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int32_t gg = h == 0 ? g : g - 1;
-      if (h == 1 && gg <= 0) break;
-      uint32_t pl[PLANE_N][PLANE_GW];
-      if (gg < g_full) {
-        lds_group<PLANE_V>(pl, s_tab, gg);
+      uint32_t pl[PLANE_N][4];
 #pragma unroll
-        for (int b = 0; b < PL_BPW; ++b) pair_group_v<false, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-      } else {
-        lds_group<PLANE_N>(pl, s_tab, gg);
+      for (int k = 0; k < PLANE_N; ++k) {
+        if (k == PLANE_V && !pad) {
+          pl[k][0] = pl[k][1] = pl[k][2] = pl[k][3] = 0xFFFFFFFFu;
+          continue;
+        }
+        const uint4 v = q[2 * k + h];
+        pl[k][0] = v.x; pl[k][1] = v.y; pl[k][2] = v.z; pl[k][3] = v.w;
+      }
 #pragma unroll
-        for (int b = 0; b < PL_BPW; ++b) pair_group_v<true, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+      for (int b = 0; b < PL_BPW; ++b) {
+#pragma unroll
+        for (int w = 0; w < 4; w += 2) {
+          uint32_t x0, x1;
+          auto miss = [&](int ww, uint32_t& xi) {
+            xi = __builtin_amdgcn_bitop3_b32(pl[PLANE_X][ww], nT[b], nT[b], 0xc0);  // X & nT
+            uint32_t t = bop3_or_xor(xi, pl[0][ww], P0[b]);
+            t = bop3_or_xor(t, pl[1][ww], P1[b]);
+            t = bop3_or_xor(t, pl[2][ww], P2[b]);
+            return bop3_or_xor(t, pl[3][ww], P3[b]);
+          };
+          const uint32_t t0 = miss(w, x0), t1 = miss(w + 1, x1);
+          am[b] = bop3_and3(am[b], t0, t1);
+          if constexpr (KX) {
+            // feasible non-matches: dm' & ~xi (& V: all-ones outside a padding group)
+            ax[b] |= bop3_andn_and(t0, x0, pl[PLANE_V][w]);
+            ax[b] |= bop3_andn_and(t1, x1, pl[PLANE_V][w + 1]);
+          } else {  // infeasible: xi, or not a real node
+            ax[b] = bop3_and3(ax[b], x0 | ~pl[PLANE_V][w], x1 | ~pl[PLANE_V][w + 1]);
+          }
+        }
       }
     }
+    // the pair (n_groups - 1 - g even: g is its upper group) ends at its lower group, or at group 1
+    if (((n_groups - 1 - g) & 1) != 0 || g == 1) {
 #pragma unroll
-    for (int b = 0; b < PL_BPW; ++b) {
-      fm[b] = am[b] != 0xFFFFFFFFu ? (uint32_t)g2 : fm[b];
-      fx[b] = (KX ? ax[b] != 0u : ax[b] != 0xFFFFFFFFu) ? (uint32_t)g2 : fx[b];
+      for (int b = 0; b < PL_BPW; ++b) {
+        fm[b] = am[b] != 0xFFFFFFFFu ? (uint32_t)g : fm[b];
+        fx[b] = (KX ? ax[b] != 0u : ax[b] != 0xFFFFFFFFu) ? (uint32_t)g : fx[b];
+        am[b] = 0xFFFFFFFFu;
+        ax[b] = KX ? 0u : 0xFFFFFFFFu;
+      }
     }
   }
-  // group 0 (its words kept), the exact first nodes, the decode: one block at a time
-  uint32_t pl[PLANE_N][PLANE_GW];
-  lds_group<PLANE_N>(pl, s_tab, 0);
+  // group 0: every block's first hits in it (its planes live only here), then the rare re-reads of a
+  // higher pair, then the decode
+  uint32_t rm[PL_BPW], rx[PL_BPW];
+  {
+    uint32_t pl[PLANE_N][PLANE_GW];
+    lds_group<PLANE_N>(pl, s_tab, 0);
+#pragma unroll
+    for (int b = 0; b < PL_BPW; ++b) {
+      uint32_t km[PLANE_GW], kx[PLANE_GW];
+#pragma unroll
+      for (int w = 0; w < PLANE_GW; ++w) {
+        uint32_t xi;
+        km[w] = pair_miss_v(pl, w, P0[b], P1[b], P2[b], P3[b], nT[b], xi);
+        if constexpr (KX) kx[w] = bop3_andn_and(km[w], xi, pl[PLANE_V][w]);
+      }
+      uint32_t h[PLANE_GW];
+#pragma unroll
+      for (int w = 0; w < PLANE_GW; ++w) h[w] = ~km[w];
+      const uint32_t m0 = hits_first(h, 0u);  // all-ones (wrapped past 255) when none
+      rm[b] = m0 < GROUP_NODES ? m0 : NOFIT;
+      if constexpr (KX) {
+        const uint32_t x0 = hits_first(kx, 0u);
+        rx[b] = x0 < GROUP_NODES ? x0 : NOFIT;
+      } else {
+        rx[b] = group_first_feasible_v(pl, 0u, nT[b]);
+      }
+    }
+  }
 #pragma unroll
   for (int b = 0; b < PL_BPW; ++b) {
     const int32_t j = wbase + b * WAVE + lane;
     if (wbase + b * WAVE >= np) break;  // wave-uniform
-    uint32_t rm = NOFIT, rx = NOFIT;
-    uint32_t km[PLANE_GW], kx[PLANE_GW];
-#pragma unroll
-    for (int w = 0; w < PLANE_GW; ++w) {
-      uint32_t xi;
-      km[w] = pair_miss_v(pl, w, P0[b], P1[b], P2[b], P3[b], nT[b], xi);
-      if constexpr (KX) kx[w] = bop3_andn_and(km[w], xi, pl[PLANE_V][w]);
+    if (rm[b] == NOFIT && fm[b] != NO_GROUP) {  // the lowest hit pair: its lower group, else the one above
+      rm[b] = group_first_lds<0>(s_tab, fm[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
+      if (rm[b] == NOFIT) rm[b] = group_first_lds<0>(s_tab, fm[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
     }
-    const uint32_t am = bop3_and3(bop3_and3(km[0], km[1], km[2]), bop3_and3(km[3], km[4], km[5]), km[6] & km[7]);
-    if (am != 0xFFFFFFFFu) {
-      uint32_t h[PLANE_GW];
-#pragma unroll
-      for (int w = 0; w < PLANE_GW; ++w) h[w] = ~km[w];
-      rm = hits_first(h, 0u);
-    } else if (fm[b] != NO_GROUP) {  // the lowest hit pair: its lower group, else the one above
-      rm = group_first_lds<0>(s_tab, fm[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
-      if (rm == NOFIT) rm = group_first_lds<0>(s_tab, fm[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
-    }
-    if constexpr (KX) {
-      const uint32_t ax = (kx[0] | kx[1] | kx[2]) | (kx[3] | kx[4] | kx[5]) | (kx[6] | kx[7]);
-      if (ax != 0u) {
-        rx = hits_first(kx, 0u);
-      } else if (fx[b] != NO_GROUP) {
-        rx = group_first_lds<1>(s_tab, fx[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
-        if (rx == NOFIT) rx = group_first_lds<1>(s_tab, fx[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
-      }
-    } else {
-      rx = group_first_feasible_v(pl, 0u, nT[b]);
-      if (rx == NOFIT && fx[b] != NO_GROUP) {
-        rx = group_first_lds<2>(s_tab, fx[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
-        if (rx == NOFIT) rx = group_first_lds<2>(s_tab, fx[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
-      }
+    if (rx[b] == NOFIT && fx[b] != NO_GROUP) {
+      constexpr int KIND = KX ? 1 : 2;
+      rx[b] = group_first_lds<KIND>(s_tab, fx[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
+      if (rx[b] == NOFIT) rx[b] = group_first_lds<KIND>(s_tab, fx[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
     }
     if (j < np) {
       if constexpr (SHARD) {
-        a.keys[j] = rm != NOFIT ? shard_key(a.node_base, rm) : 0;
-        a.keys[(size_t)np + j] = rx != NOFIT ? shard_key(a.node_base, rx) : 0;
+        a.keys[j] = rm[b] != NOFIT ? shard_key(a.node_base, rm[b]) : 0;
+        a.keys[(size_t)np + j] = rx[b] != NOFIT ? shard_key(a.node_base, rx[b]) : 0;
       } else {
-        const uint32_t ra = umin(rm, rx);
+        const uint32_t ra = umin(rm[b], rx[b]);
         int32_t oi, ost;
         int64_t osc;
-        decode_pod(rm != NOFIT ? (int64_t)rm : -1, (KX && rx != NOFIT) ? (int64_t)rx : -1,
+        decode_pod(rm[b] != NOFIT ? (int64_t)rm[b] : -1, (KX && rx[b] != NOFIT) ? (int64_t)rx[b] : -1,
                    ra != NOFIT ? (int64_t)ra : -1, code[b] != CODE_NONE_POD, a.pp, &oi, &osc, &ost);
         d.out_idx[j] = oi;
         if (d.out_score) d.out_score[j] = osc;
