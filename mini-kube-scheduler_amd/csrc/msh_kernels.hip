@@ -653,7 +653,7 @@ template <int KIND>
 __device__ __forceinline__ uint32_t group_first_lds(const uint4* __restrict__ s_tab, uint32_t g, uint32_t P0,
                                                     uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT) {
   const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
-#pragma unroll
+#pragma unroll 1
   for (int hh = 0; hh < 2; ++hh) {
     uint32_t pl[PLANE_N][4];
 #pragma unroll
@@ -732,8 +732,8 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
   for (int32_t g = n_groups - 1; g > 0; --g) {
     const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
     const bool pad = g >= g_full;  // wave-uniform
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {  // (not unrolled: both halves' planes live at once cost 24 VGPRs)
       uint32_t pl[PLANE_N][4];
 #pragma unroll
       for (int k = 0; k < PLANE_N; ++k) {
@@ -779,33 +779,15 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
       }
     }
   }
-  // group 0: every block's first hits in it (its planes live only here), then the rare re-reads of a
+  // group 0: every block's first hits in it, by the half-group reads of the rare path (a group's 48
+  // plane words held at once would set the kernel's register count), then the rare re-reads of a
   // higher pair, then the decode
+  constexpr int KIND_X = KX ? 1 : 2;  // KX: first feasible non-match; else first feasible node
   uint32_t rm[PL_BPW], rx[PL_BPW];
-  {
-    uint32_t pl[PLANE_N][PLANE_GW];
-    lds_group<PLANE_N>(pl, s_tab, 0);
 #pragma unroll
-    for (int b = 0; b < PL_BPW; ++b) {
-      uint32_t km[PLANE_GW], kx[PLANE_GW];
-#pragma unroll
-      for (int w = 0; w < PLANE_GW; ++w) {
-        uint32_t xi;
-        km[w] = pair_miss_v(pl, w, P0[b], P1[b], P2[b], P3[b], nT[b], xi);
-        if constexpr (KX) kx[w] = bop3_andn_and(km[w], xi, pl[PLANE_V][w]);
-      }
-      uint32_t h[PLANE_GW];
-#pragma unroll
-      for (int w = 0; w < PLANE_GW; ++w) h[w] = ~km[w];
-      const uint32_t m0 = hits_first(h, 0u);  // all-ones (wrapped past 255) when none
-      rm[b] = m0 < GROUP_NODES ? m0 : NOFIT;
-      if constexpr (KX) {
-        const uint32_t x0 = hits_first(kx, 0u);
-        rx[b] = x0 < GROUP_NODES ? x0 : NOFIT;
-      } else {
-        rx[b] = group_first_feasible_v(pl, 0u, nT[b]);
-      }
-    }
+  for (int b = 0; b < PL_BPW; ++b) {
+    rm[b] = group_first_lds<0>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b]);
+    rx[b] = group_first_lds<KIND_X>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b]);
   }
 #pragma unroll
   for (int b = 0; b < PL_BPW; ++b) {
@@ -816,9 +798,8 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
       if (rm[b] == NOFIT) rm[b] = group_first_lds<0>(s_tab, fm[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
     }
     if (rx[b] == NOFIT && fx[b] != NO_GROUP) {
-      constexpr int KIND = KX ? 1 : 2;
-      rx[b] = group_first_lds<KIND>(s_tab, fx[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
-      if (rx[b] == NOFIT) rx[b] = group_first_lds<KIND>(s_tab, fx[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
+      rx[b] = group_first_lds<KIND_X>(s_tab, fx[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
+      if (rx[b] == NOFIT) rx[b] = group_first_lds<KIND_X>(s_tab, fx[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
     }
     if (j < np) {
       if constexpr (SHARD) {
