@@ -717,66 +717,41 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
     P3[b] = 0u - (c >> 3);
     nT[b] = t ? 0u : 0xFFFFFFFFu;
   }
-  // Groups above 0, descending, one group per iteration and a half-group (four words) per LDS read set,
-  // so that only 5-6 x 4 plane words are live (the whole group's 48 held the kernel to 4 waves per
-  // SIMD). Flags per pair of groups (as pair_kernel): fm / fx the lower group of the lowest pair with a
-  // feasible match / KX: feasible non-match, identity-like: feasible node.
-  uint32_t fm[PL_BPW], fx[PL_BPW], am[PL_BPW], ax[PL_BPW];
+  // Groups above 0, descending, two per step (as pair_kernel): each group's 40 / 48 plane words read
+  // into VGPRs at once and applied to every block. fm / fx: the lower group of the lowest pair with a
+  // feasible match / KX: feasible non-match, identity-like: feasible node. (Reading half a group at a
+  // time, one group per iteration, cut the kernel to 52 VGPRs and 8 waves per SIMD but ran slower:
+  // 95.6 against 89.8 us per 32-batch C3 launch, profiles/r4_ab_pair_planes.txt.)
+  uint32_t fm[PL_BPW], fx[PL_BPW];
 #pragma unroll
-  for (int b = 0; b < PL_BPW; ++b) {
-    fm[b] = fx[b] = NO_GROUP;
-    am[b] = 0xFFFFFFFFu;
-    ax[b] = KX ? 0u : 0xFFFFFFFFu;
-  }
-#pragma unroll 1
-  for (int32_t g = n_groups - 1; g > 0; --g) {
-    const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
-    const bool pad = g >= g_full;  // wave-uniform
-#pragma unroll 1
-    for (int h = 0; h < 2; ++h) {  // (not unrolled: both halves' planes live at once cost 24 VGPRs)
-      uint32_t pl[PLANE_N][4];
+  for (int b = 0; b < PL_BPW; ++b) fm[b] = fx[b] = NO_GROUP;
+  for (int32_t g = n_groups - 1; g > 0; g -= 2) {
+    uint32_t am[PL_BPW], ax[PL_BPW];
 #pragma unroll
-      for (int k = 0; k < PLANE_N; ++k) {
-        if (k == PLANE_V && !pad) {
-          pl[k][0] = pl[k][1] = pl[k][2] = pl[k][3] = 0xFFFFFFFFu;
-          continue;
-        }
-        const uint4 v = q[2 * k + h];
-        pl[k][0] = v.x; pl[k][1] = v.y; pl[k][2] = v.z; pl[k][3] = v.w;
-      }
+    for (int b = 0; b < PL_BPW; ++b) {
+      am[b] = 0xFFFFFFFFu;
+      ax[b] = KX ? 0u : 0xFFFFFFFFu;
+    }
+    const int32_t g2 = g - 1 > 0 ? g - 1 : g;
 #pragma unroll
-      for (int b = 0; b < PL_BPW; ++b) {
+    for (int h = 0; h < 2; ++h) {
+      const int32_t gg = h == 0 ? g : g - 1;
+      if (h == 1 && gg <= 0) break;
+      uint32_t pl[PLANE_N][PLANE_GW];
+      if (gg < g_full) {
+        lds_group<PLANE_V>(pl, s_tab, gg);
 #pragma unroll
-        for (int w = 0; w < 4; w += 2) {
-          uint32_t x0, x1;
-          auto miss = [&](int ww, uint32_t& xi) {
-            xi = __builtin_amdgcn_bitop3_b32(pl[PLANE_X][ww], nT[b], nT[b], 0xc0);  // X & nT
-            uint32_t t = bop3_or_xor(xi, pl[0][ww], P0[b]);
-            t = bop3_or_xor(t, pl[1][ww], P1[b]);
-            t = bop3_or_xor(t, pl[2][ww], P2[b]);
-            return bop3_or_xor(t, pl[3][ww], P3[b]);
-          };
-          const uint32_t t0 = miss(w, x0), t1 = miss(w + 1, x1);
-          am[b] = bop3_and3(am[b], t0, t1);
-          if constexpr (KX) {
-            // feasible non-matches: dm' & ~xi (& V: all-ones outside a padding group)
-            ax[b] |= bop3_andn_and(t0, x0, pl[PLANE_V][w]);
-            ax[b] |= bop3_andn_and(t1, x1, pl[PLANE_V][w + 1]);
-          } else {  // infeasible: xi, or not a real node
-            ax[b] = bop3_and3(ax[b], x0 | ~pl[PLANE_V][w], x1 | ~pl[PLANE_V][w + 1]);
-          }
-        }
+        for (int b = 0; b < PL_BPW; ++b) pair_group_v<false, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+      } else {
+        lds_group<PLANE_N>(pl, s_tab, gg);
+#pragma unroll
+        for (int b = 0; b < PL_BPW; ++b) pair_group_v<true, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
       }
     }
-    // the pair (n_groups - 1 - g even: g is its upper group) ends at its lower group, or at group 1
-    if (((n_groups - 1 - g) & 1) != 0 || g == 1) {
 #pragma unroll
-      for (int b = 0; b < PL_BPW; ++b) {
-        fm[b] = am[b] != 0xFFFFFFFFu ? (uint32_t)g : fm[b];
-        fx[b] = (KX ? ax[b] != 0u : ax[b] != 0xFFFFFFFFu) ? (uint32_t)g : fx[b];
-        am[b] = 0xFFFFFFFFu;
-        ax[b] = KX ? 0u : 0xFFFFFFFFu;
-      }
+    for (int b = 0; b < PL_BPW; ++b) {
+      fm[b] = am[b] != 0xFFFFFFFFu ? (uint32_t)g2 : fm[b];
+      fx[b] = (KX ? ax[b] != 0u : ax[b] != 0xFFFFFFFFu) ? (uint32_t)g2 : fx[b];
     }
   }
   // group 0: every block's first hits in it, by the half-group reads of the rare path (a group's 48

@@ -795,13 +795,16 @@ def test_multi_batch_age_shares(msh, oracle, n, norm, monkeypatch):
                 _assert_same((gi, gs, gst), want, f"{kernel}/{planes} batch {k} (p={len(pods[k][0])}) n={n} norm={norm}")
 
 
+@pytest.mark.parametrize("bpw", ["2", "4"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("nb", [1, 9, 33])
-def test_multi_batch_launch_lds(msh, oracle, norm, nb, monkeypatch):
-    """The LDS-staged pair kernel forced on small ragged multi-batch launches (MSH_PAIR_PLANES=lds):
-    workgroups whose blocks end inside or before a batch, empty and one-pod batches, NULL scores."""
+def test_multi_batch_launch_lds(msh, oracle, norm, nb, bpw, monkeypatch):
+    """The LDS-staged pair kernel forced on small ragged multi-batch launches (MSH_PAIR_PLANES=lds,
+    2 and 4 pod blocks per wave): workgroups whose blocks end inside or before a batch, empty and
+    one-pod batches, NULL scores."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("MSH_PAIR_PLANES", "lds")
+    monkeypatch.setenv("MSH_PAIR_LDS_BPW", bpw)
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(99 * nb + norm)
     sizes = ([0, 1, 64, 65, 255, 257, 20_003, 5000, 333, 4096, 1, 2, 700, 64, 128, 1025, 999] * 2)[:nb]
