@@ -1179,7 +1179,6 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   const NodeTable& t = cur_table(c);
   a.planes = t.d_planes;
   a.n_words = c->n_pad / 32;
-  a.ball = t.d_ball;
   a.n_nodes = c->n_nodes;
   a.pod_digit = d_pod_digit;
   a.pod_tol = d_pod_tol;

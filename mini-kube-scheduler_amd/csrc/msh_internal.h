@@ -243,7 +243,6 @@ hipError_t launch_cols100(const int64_t* cols, double* cols100, int64_t stride, 
 struct SeqArgs {
   const uint32_t* planes;    // bit-sliced node table (PLANE_* layout)
   int32_t n_words;           // n_pad / 32
-  const uint32_t* ball;      // [2] first feasible key per pod class (no capacity: constant)
   int32_t n_nodes;
   const int8_t* pod_digit;
   const uint8_t* pod_tol;

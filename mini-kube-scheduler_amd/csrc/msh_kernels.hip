@@ -1696,6 +1696,26 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   if (LDSC)  // ordered before the first commit by the first pod's exchange / barrier
     for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) lcnt[i] = a.counts[i];
   if (threadIdx.x < 9 * U) (&xs[0][0][0])[threadIdx.x] = NONE;
+  // The first feasible node for a pod that does not tolerate the unschedulable taint (V & ~X) and for
+  // one that does (V), evaluated here from the register-resident planes once per launch (lanes and
+  // waves hold ascending word ranges: the first lane with one, then the smallest over the waves).
+  __shared__ uint32_t s_first[NW + 1][2];
+  {
+    uint32_t fn = NONE, ft = NONE;
+#pragma unroll
+    for (int r = RS - 1; r >= 0; --r) {
+      const uint32_t base = (uint32_t)((wv * WAVE + lane) * RS + r) << 5;
+      const uint32_t hn = VV[r] & ~XX[r], ht = VV[r];
+      fn = hn ? base + (uint32_t)__builtin_ctz(hn) : fn;
+      ft = ht ? base + (uint32_t)__builtin_ctz(ht) : ft;
+    }
+    fn = wave_first(fn);
+    ft = wave_first(ft);
+    if (lane == 0) {
+      s_first[wv][0] = fn;
+      s_first[wv][1] = ft;
+    }
+  }
   __syncthreads();
   int sl = 0;
   // Drain the node-state loads here: otherwise the waitcnt pass, unsure they have landed on every
@@ -1717,12 +1737,17 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
                "+s"(pp.weight));
   int32_t max_pods = a.max_pods;
   asm volatile("" : "+s"(max_pods));
-  const uint32_t ball0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.ball[0]);
-  const uint32_t ball1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.ball[1]);
   int32_t* counts = a.counts;
   const IdentDecode idec = make_ident_decode(pp);
-  // first feasible node of each pod class (no capacity: constant over the launch), -1 = none
-  const int32_t ia0 = ball0 ? (int32_t)(KMAX - ball0) : -1, ia1 = ball1 ? (int32_t)(KMAX - ball1) : -1;
+  // the first feasible node for each tolerates value (no capacity: constant over the launch), -1 = none
+  uint32_t fa0 = NONE, fa1 = NONE;
+#pragma unroll
+  for (int w = 0; w < NW + (FIN ? 1 : 0); ++w) {
+    fa0 = umin(fa0, s_first[w][0]);
+    fa1 = umin(fa1, s_first[w][1]);
+  }
+  const int32_t ia0 = fa0 != NONE ? (int32_t)__builtin_amdgcn_readfirstlane((int)fa0) : -1;
+  const int32_t ia1 = fa1 != NONE ? (int32_t)__builtin_amdgcn_readfirstlane((int)fa1) : -1;
   // A pod's lane word: code | does-not-tolerate << 4 | class status << 5 (bit 4 set for pods that
   // do not tolerate, so one sign-extending bit extract gives the ~tolerates mask), where the class status is
   // decode_ident's status, which without a capacity depends on the pod's class alone (FitError when
