@@ -1363,10 +1363,11 @@ __global__ __launch_bounds__(GEN_WAVES * WAVE) void generic_kernel(GenericArgs a
         const double q = (as_f64(bits) - bb[cc]) * rr[cc];  // (100 raw - b) x r: both operations exact
         // the numerator's sign from the node value's top dword (scalar unit): MIN-MAX numerators of
         // feasible pairs are never negative
-        // (readfirstlane keeps the test a 32-bit scalar compare: folded to a 64-bit compare, which the
-        // scalar unit lacks, it became a VALU v_cmp_gt_i64 per pair)
-        const bool nonneg =
-            ((mmask >> cc) & 1) != 0 || __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(bits >> 32)) >= 0;
+        // (the sign bit by a scalar shift in asm: as C the test folds to a 64-bit compare, which the
+        // scalar unit lacks, and became a VALU v_cmp_lt_i64 per pair)
+        uint32_t sgn;
+        asm("s_lshr_b32 %0, %1, 31" : "=s"(sgn) : "s"((uint32_t)(bits >> 32)));
+        const bool nonneg = ((mmask >> cc) & 1) != 0 || sgn == 0;
         if (nonneg && wsm) {
           // |q| <= 100 on a feasible pair: v_cvt_i32_f64 (saturating in hardware: the value of an
           // infeasible pair converts without a fault and is never taken), then n x w + total in one
