@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import importlib
 import re
 from pathlib import Path
 
@@ -117,3 +118,15 @@ def test_plain_c_consumer_scenario(msh):
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["known_answer"] is True and out["phase2"]["node"] == "node10"
+
+
+def test_prescore_ids_match_the_c_check(msh):
+    """Only NodeNumber has a PreScore (nodenumber.go:50-64); msh_set_plugins_ex rejects any other
+    prescore id (check_ids, kind 1), and the Python mirror rejects the same names before the call, so
+    a plugin list that passes the host check also passes the C-ABI's."""
+    S = importlib.import_module("mini-kube-scheduler_amd.scheduler")
+    assert set(S.PRESCORE_IDS) == {"NodeNumber"}
+    assert "ScoreColumn0" in S.SCORE_IDS  # a score plugin, never a prescore one
+    with pytest.raises(msh.MshError) as e:
+        S._ids(["ScoreColumn0"], S.PRESCORE_IDS, "prescore")
+    assert e.value.code == msh._native.MSH_ERR_UNSUPPORTED
