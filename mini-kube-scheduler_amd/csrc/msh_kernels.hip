@@ -583,7 +583,7 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
 // modes, one AND3 of two words' xi per two words (the group holds a feasible node iff not all-ones).
 // ---------------------------------------------------------------------------------------
 constexpr int PL_WAVES = 4;  // waves per workgroup
-constexpr int PL_BPW_MAX = 4;  // 64-pod blocks per wave (the kernel's PL_BPW: 2 or 4, DeviceInfo::pair_lds_bpw)
+constexpr int PL_BPW_MAX = 4;  // 64-pod blocks per wave (the kernel's PL_BPW: 1-4, DeviceInfo::pair_lds_bpw)
 constexpr int PAIR_LDS_MAX_GROUPS = 128;  // 32,768 nodes, 24 KB of LDS per workgroup
 
 // The planes of group g from LDS (NPL planes, 8 words each) into VGPRs.
@@ -2189,16 +2189,17 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
                             (dev.pair_planes == 0 && !KX && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX &&
                              dev.bits_slices == 0));
   if (lds) {
-    const int bpw = dev.pair_lds_bpw == 4 ? 4 : 2;
+    const int bpw = dev.pair_lds_bpw >= 1 && dev.pair_lds_bpw <= 4 ? dev.pair_lds_bpw : 2;
     const int32_t blocks = (maxp + WAVE - 1) / WAVE;
     const int32_t bx = (blocks + PL_WAVES * bpw - 1) / (PL_WAVES * bpw);
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
-    if (bpw == 2)
-      MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PL_WAVES * WAVE),
-                       (unsigned)bytes, s, a);
-    else
-      MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 4>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PL_WAVES * WAVE),
-                       (unsigned)bytes, s, a);
+    const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(PL_WAVES * WAVE);
+    switch (bpw) {
+      case 1: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 1>), grid, blk, (unsigned)bytes, s, a); break;
+      case 3: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 3>), grid, blk, (unsigned)bytes, s, a); break;
+      case 4: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 4>), grid, blk, (unsigned)bytes, s, a); break;
+      default: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2>), grid, blk, (unsigned)bytes, s, a); break;
+    }
     return hipGetLastError();
   }
   const int S = pair_slices(waves, a.n_groups, dev);

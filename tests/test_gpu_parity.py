@@ -795,7 +795,7 @@ def test_multi_batch_age_shares(msh, oracle, n, norm, monkeypatch):
                 _assert_same((gi, gs, gst), want, f"{kernel}/{planes} batch {k} (p={len(pods[k][0])}) n={n} norm={norm}")
 
 
-@pytest.mark.parametrize("bpw", ["2", "4"])
+@pytest.mark.parametrize("bpw", ["1", "2", "3", "4"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("nb", [1, 9, 33])
 def test_multi_batch_launch_lds(msh, oracle, norm, nb, bpw, monkeypatch):
