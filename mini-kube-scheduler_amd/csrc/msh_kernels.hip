@@ -630,9 +630,8 @@ __device__ __forceinline__ void pair_group_v(const uint32_t (&pl)[PLANE_N][PLANE
     } else {
       if constexpr (PAD) {  // infeasible: xi or not a real node
         ax = bop3_and3(ax, x0 | ~pl[PLANE_V][w], x1 | ~pl[PLANE_V][w + 1]);
-      } else {
-        ax = bop3_and3(ax, x0, x1);
       }
+      // (a group without padding: the caller folds nT & AND(X) into ax once per group)
     }
   }
 }
@@ -742,6 +741,13 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
         lds_group<PLANE_V>(pl, s_tab, gg);
 #pragma unroll
         for (int b = 0; b < PL_BPW; ++b) pair_group_v<false, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+        if constexpr (!KX) {  // no padding: the AND of the group's xi words is nT & AND(X), X shared
+          const uint32_t axg = bop3_and3(bop3_and3(pl[PLANE_X][0], pl[PLANE_X][1], pl[PLANE_X][2]),
+                                         bop3_and3(pl[PLANE_X][3], pl[PLANE_X][4], pl[PLANE_X][5]),
+                                         pl[PLANE_X][6] & pl[PLANE_X][7]);
+#pragma unroll
+          for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
+        }
       } else {
         lds_group<PLANE_N>(pl, s_tab, gg);
 #pragma unroll
