@@ -679,6 +679,36 @@ __device__ __forceinline__ uint32_t group_first_lds(const uint4* __restrict__ s_
   return NOFIT;
 }
 
+// Both firsts of group g in one pass over its planes (half a group at a time): the first feasible
+// match (rm) and, KX, the first feasible non-match or, else, the first feasible node (rx); NOFIT
+// where the group has none.
+template <bool KX>
+__device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab, uint32_t g, uint32_t P0,
+                                                 uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT, uint32_t& rm,
+                                                 uint32_t& rx) {
+  const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
+  uint32_t bm = 0xFFFFFFFFu, bx = 0xFFFFFFFFu;
+#pragma unroll 1
+  for (int hh = 0; hh < 2; ++hh) {
+    uint32_t pl[PLANE_N][4];
+#pragma unroll
+    for (int k = 0; k < PLANE_N; ++k) {
+      const uint4 v = q[2 * k + hh];
+      pl[k][0] = v.x; pl[k][1] = v.y; pl[k][2] = v.z; pl[k][3] = v.w;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t fe = ~(pl[PLANE_X][c] & nT) & pl[PLANE_V][c];
+      const uint32_t dm = (pl[0][c] ^ P0) | (pl[1][c] ^ P1) | (pl[2][c] ^ P2) | (pl[3][c] ^ P3);
+      const uint32_t off = (uint32_t)(32 * (c + 4 * hh));
+      bm = umin(bm, lowbit(~dm & fe) | off);  // all-ones stays all-ones for a word without one
+      bx = umin(bx, lowbit(KX ? (dm & fe) : fe) | off);
+    }
+  }
+  rm = bm < GROUP_NODES ? g * GROUP_NODES + bm : NOFIT;
+  rx = bx < GROUP_NODES ? g * GROUP_NODES + bx : NOFIT;
+}
+
 template <bool SHARD, bool KX, int PL_BPW>
 __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
   extern __shared__ uint4 s_tab[];  // n_groups * GROUP_DWORDS / 4
@@ -766,10 +796,7 @@ __global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
   constexpr int KIND_X = KX ? 1 : 2;  // KX: first feasible non-match; else first feasible node
   uint32_t rm[PL_BPW], rx[PL_BPW];
 #pragma unroll
-  for (int b = 0; b < PL_BPW; ++b) {
-    rm[b] = group_first_lds<0>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b]);
-    rx[b] = group_first_lds<KIND_X>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b]);
-  }
+  for (int b = 0; b < PL_BPW; ++b) group_firsts_lds<KX>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b], rm[b], rx[b]);
 #pragma unroll
   for (int b = 0; b < PL_BPW; ++b) {
     const int32_t j = wbase + b * WAVE + lane;
