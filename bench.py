@@ -81,8 +81,8 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
     if classrows and groups <= WGP_MAX_GROUPS and not shard:
         return f"void msh::wgp_kernel<4, {b(kx)}>"
     waves = -(-n_pods // 64) * (nb if multi else 1)
-    if groups <= PAIR_LDS_MAX_GROUPS and not kx and waves >= cus * 4 * 4 * 4:  # the LDS-staged form
-        return f"void msh::pair_lds_kernel<{b(shard)}, false, 2>"
+    if groups <= PAIR_LDS_MAX_GROUPS and waves >= cus * 4 * 4 * 4:  # the LDS-staged form
+        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2>"
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2

@@ -2214,12 +2214,11 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   if (maxp == 0) return hipSuccess;
   // LDS-staged planes when the table fits and the launch fills the chip with whole workgroups (the
   // copy is amortised over PL_WAVES x PL_BPW blocks); scalar-loaded planes (with slice waves) otherwise
-  // (auto: the identity-like modes only; REVERSE / MINMAX ran slower LDS-staged, 101.5 / 104.2 us per
-  // 32-batch C3 launch against 97.6 with scalar-loaded planes, where NONE gained 97.0 -> 89.8 us:
-  // profiles/r4_ab_pair_planes.txt)
+  // (auto: every normalize mode; per 32-batch C3 launch NONE 96.5 -> 85.0 us and MINMAX 95.4 -> 91.5 us
+  // against scalar-loaded planes, profiles/r4_ab_pair_planes.txt)
   const bool fits = a.n_groups <= PAIR_LDS_MAX_GROUPS;
   const bool lds = fits && (dev.pair_planes == 2 ||
-                            (dev.pair_planes == 0 && !KX && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX &&
+                            (dev.pair_planes == 0 && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX &&
                              dev.bits_slices == 0));
   if (lds) {
     const int bpw = dev.pair_lds_bpw >= 1 && dev.pair_lds_bpw <= 4 ? dev.pair_lds_bpw : 2;
