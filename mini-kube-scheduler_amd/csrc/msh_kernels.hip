@@ -582,7 +582,10 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
 // group's match flag, plus, KX, one OR of the feasible non-matches (dm' & ~xi), or, identity-like
 // modes, one AND3 of two words' xi per two words (the group holds a feasible node iff not all-ones).
 // ---------------------------------------------------------------------------------------
-constexpr int PL_WAVES = 4;  // waves per workgroup
+constexpr int PL_WAVES = 4;  // waves per workgroup (tables up to PAIR_LDS_MAX_GROUPS groups)
+constexpr int PL_WAVES_BIG = 16;  // waves per workgroup for larger tables: one copy of up to 80 KB serves
+                                  // 16 waves (two workgroups per CU: 8 waves per SIMD)
+constexpr int PAIR_LDS_BIG_GROUPS = 416;  // 106,496 nodes, 78 KB per workgroup
 constexpr int PL_BPW_MAX = 4;  // 64-pod blocks per wave (the kernel's PL_BPW: 1-4, DeviceInfo::pair_lds_bpw)
 constexpr int PAIR_LDS_MAX_GROUPS = 128;  // 32,768 nodes, 24 KB of LDS per workgroup
 
@@ -709,17 +712,17 @@ __device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab
   rx = bx < GROUP_NODES ? g * GROUP_NODES + bx : NOFIT;
 }
 
-template <bool SHARD, bool KX, int PL_BPW>
-__global__ __launch_bounds__(PL_WAVES * WAVE) void pair_lds_kernel(PairArgs a) {
+template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES>
+__global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
   extern __shared__ uint4 s_tab[];  // n_groups * GROUP_DWORDS / 4
   const BatchDesc& d = a.d[blockIdx.y];
   const int32_t np = d.n_pods;
-  const int32_t wg0 = (int32_t)blockIdx.x * PL_WAVES * PL_BPW * WAVE;  // first pod of this workgroup
+  const int32_t wg0 = (int32_t)blockIdx.x * W * PL_BPW * WAVE;  // first pod of this workgroup
   if (wg0 >= np) return;  // the whole workgroup lies past its batch's end
   {
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(a.planes);
     const int32_t nq = a.n_groups * (GROUP_DWORDS / 4);
-    for (int32_t i = threadIdx.x; i < nq; i += PL_WAVES * WAVE) s_tab[i] = src[i];
+    for (int32_t i = threadIdx.x; i < nq; i += W * WAVE) s_tab[i] = src[i];
   }
   __syncthreads();
   const int lane = threadIdx.x & (WAVE - 1);
@@ -2217,15 +2220,27 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   // (auto: every normalize mode; per 32-batch C3 launch NONE 96.5 -> 85.0 us and MINMAX 95.4 -> 91.5 us
   // against scalar-loaded planes, profiles/r4_ab_pair_planes.txt)
   const bool fits = a.n_groups <= PAIR_LDS_MAX_GROUPS;
-  const bool lds = fits && (dev.pair_planes == 2 ||
-                            (dev.pair_planes == 0 && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX &&
-                             dev.bits_slices == 0));
+  const bool big = !fits && a.n_groups <= PAIR_LDS_BIG_GROUPS;  // 16-wave workgroups, two blocks per wave
+  const bool lds = (fits || big) && (dev.pair_planes == 2 ||
+                                     (dev.pair_planes == 0 && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX &&
+                                      dev.bits_slices == 0));
   if (lds) {
-    const int bpw = dev.pair_lds_bpw >= 1 && dev.pair_lds_bpw <= 4 ? dev.pair_lds_bpw : 2;
+    const int bpw = big ? 2 : (dev.pair_lds_bpw >= 1 && dev.pair_lds_bpw <= 4 ? dev.pair_lds_bpw : 2);
+    const int w = big ? PL_WAVES_BIG : PL_WAVES;
     const int32_t blocks = (maxp + WAVE - 1) / WAVE;
-    const int32_t bx = (blocks + PL_WAVES * bpw - 1) / (PL_WAVES * bpw);
+    const int32_t bx = (blocks + w * bpw - 1) / (w * bpw);
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
-    const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(PL_WAVES * WAVE);
+    const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(w * WAVE);
+    if (big) {
+      auto k = pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG>;
+      if (bytes > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return e;
+      }
+      MSH_TIMED_LAUNCH(k, grid, blk, (unsigned)bytes, s, a);
+      return hipGetLastError();
+    }
     switch (bpw) {
       case 1: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 1>), grid, blk, (unsigned)bytes, s, a); break;
       case 3: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 3>), grid, blk, (unsigned)bytes, s, a); break;

@@ -841,14 +841,15 @@ def test_multi_batch_invalid(msh, gpu_ctx):
 
 
 @pytest.mark.parametrize("planes", ["sgpr", "lds"])
-@pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 32_768, 70_000])
+@pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 32_768, 70_000, 106_496, 106_497])
 def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
     """pair_kernel re-reads the first group with a hit from memory when it lies above the lowest group
     of the wave's range (kept in registers): digit 3 only in the second half of the table makes those
     pods' first matches late. Batch, multi-batch and shard-key entry points, NONE and MINMAX, on tables
     with and without a padded top group."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_PAIR_PLANES", planes)  # lds: tables up to 32,768 nodes (70,000 falls back)
+    monkeypatch.setenv("MSH_PAIR_PLANES", planes)  # lds: 4-wave workgroups up to 32,768 nodes, 16-wave up to
+    # 106,496 (106,497 falls back to scalar-loaded planes)
     rng = np.random.default_rng(n + 4)
     u, nd, pd, pt = _rand_case(rng, n, 3000, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4
