@@ -66,7 +66,8 @@ PAIR_VALU_PER_WORD_LDS = 6.0
 # (best total, chunk-relative index): 7 VALU lane-ops per pair
 GEN_VALU_PER_PAIR_REF = 7.0
 WGP_MAX_GROUPS = 32                # msh_kernels.hip: the class-row kernel's table limit (groups of 256 nodes)
-PAIR_LDS_MAX_GROUPS = 128          # msh_kernels.hip: tables the LDS-staged pair kernel takes
+PAIR_LDS_MAX_GROUPS = 128          # msh_kernels.hip: tables the LDS-staged pair kernel takes (4-wave workgroups)
+PAIR_LDS_BIG_GROUPS = 416          # ... and with 16-wave workgroups
 PMC_FILE = ROOT / "profiles" / "r4_pmc_c3.json"
 VALU_PEAK_FILE = ROOT / "profiles" / "r4_ubench_valu.json"
 
@@ -82,7 +83,9 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
         return f"void msh::wgp_kernel<4, {b(kx)}>"
     waves = -(-n_pods // 64) * (nb if multi else 1)
     if groups <= PAIR_LDS_MAX_GROUPS and waves >= cus * 4 * 4 * 4:  # the LDS-staged form
-        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2>"
+        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2, 4>"
+    if PAIR_LDS_MAX_GROUPS < groups <= PAIR_LDS_BIG_GROUPS and waves >= cus * 2 * 16:  # 16-wave workgroups
+        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2, 16>"
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2

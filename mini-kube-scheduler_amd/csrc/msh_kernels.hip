@@ -2221,9 +2221,10 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   // against scalar-loaded planes, profiles/r4_ab_pair_planes.txt)
   const bool fits = a.n_groups <= PAIR_LDS_MAX_GROUPS;
   const bool big = !fits && a.n_groups <= PAIR_LDS_BIG_GROUPS;  // 16-wave workgroups, two blocks per wave
+  // (big: two 16-wave workgroups per CU fill it from 32 blocks per CU on)
+  const int64_t min_waves = (int64_t)dev.cus * (big ? 2 * PL_WAVES_BIG : 4 * 4 * PL_BPW_MAX);
   const bool lds = (fits || big) && (dev.pair_planes == 2 ||
-                                     (dev.pair_planes == 0 && waves >= (int64_t)dev.cus * 4 * 4 * PL_BPW_MAX &&
-                                      dev.bits_slices == 0));
+                                     (dev.pair_planes == 0 && waves >= min_waves && dev.bits_slices == 0));
   if (lds) {
     const int bpw = big ? 2 : (dev.pair_lds_bpw >= 1 && dev.pair_lds_bpw <= 4 ? dev.pair_lds_bpw : 2);
     const int w = big ? PL_WAVES_BIG : PL_WAVES;
