@@ -54,7 +54,10 @@ struct DeviceInfo {
   // for tables up to PAIR_LDS_MAX_GROUPS groups and launches that fill the chip, scalar loads
   // otherwise), 1 = scalar loads into SGPRs, 2 = LDS-staged (tables that fit)
   int pair_planes = 0;
-  int pair_lds_bpw = 2;  // A/B (MSH_PAIR_LDS_BPW): 64-pod blocks per wave of the LDS-staged form, 2 or 4
+  int pair_lds_bpw = 2;  // A/B (MSH_PAIR_LDS_BPW): 64-pod blocks per wave of the LDS-staged form, 1-4
+  // MSH_PAIR_COMPACT: the LDS-staged form (2 blocks per wave) reorders each workgroup's pods by their
+  // tolerates bit first, so that most blocks scan with the filter term folded (1 = on)
+  int pair_compact = 0;
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit

@@ -639,6 +639,40 @@ __device__ __forceinline__ void pair_group_v(const uint32_t (&pl)[PLANE_N][PLANE
   }
 }
 
+// pair_group_v for a block whose 64 pods share their tolerates bit (TY 0: none tolerates, TY 1: every
+// one does): the filter term X & nT is X itself or zero, so it folds into the first code compare
+// (v_bitop3 X | (D0 ^ P0)), or drops out: 4 VALU per word for dm' instead of 5.
+template <bool PAD, bool KX, int TY>
+__device__ __forceinline__ void pair_group_ty(const uint32_t (&pl)[PLANE_N][PLANE_GW], uint32_t P0, uint32_t P1,
+                                              uint32_t P2, uint32_t P3, uint32_t& am, uint32_t& ax) {
+#pragma unroll
+  for (int w = 0; w < PLANE_GW; w += 2) {
+    uint32_t t[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ww = w + h;
+      uint32_t u = TY == 0 ? bop3_or_xor(pl[PLANE_X][ww], pl[0][ww], P0) : (pl[0][ww] ^ P0);
+      u = bop3_or_xor(u, pl[1][ww], P1);
+      u = bop3_or_xor(u, pl[2][ww], P2);
+      t[h] = bop3_or_xor(u, pl[3][ww], P3);
+    }
+    am = bop3_and3(am, t[0], t[1]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ww = w + h;
+      if constexpr (KX) {  // feasible non-matches: dm' & ~X (TY 0) or dm' (TY 1), & V in a padding group
+        if constexpr (TY == 0) ax = PAD ? (ax | bop3_andn_and(t[h], pl[PLANE_X][ww], pl[PLANE_V][ww]))
+                                       : bop3_or_andn(ax, t[h], pl[PLANE_X][ww]);
+        else ax = PAD ? (ax | (t[h] & pl[PLANE_V][ww])) : (ax | t[h]);
+      }
+    }
+    if constexpr (!KX && PAD) {  // infeasible: X (TY 0) or not a real node
+      if constexpr (TY == 0) ax = bop3_and3(ax, pl[PLANE_X][w] | ~pl[PLANE_V][w], pl[PLANE_X][w + 1] | ~pl[PLANE_V][w + 1]);
+      else ax = bop3_and3(ax, ~pl[PLANE_V][w], ~pl[PLANE_V][w + 1]);
+    }
+  }
+}
+
 // The lane's first feasible node in group g (identity-like modes), NOFIT if none.
 __device__ __forceinline__ uint32_t group_first_feasible_v(const uint32_t (&pl)[PLANE_N][PLANE_GW], uint32_t g,
                                                            uint32_t nT) {
@@ -712,43 +746,95 @@ __device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab
   rx = bx < GROUP_NODES ? g * GROUP_NODES + bx : NOFIT;
 }
 
-template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES>
+template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES, bool CMP = false>
 __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
   extern __shared__ uint4 s_tab[];  // n_groups * GROUP_DWORDS / 4
+  constexpr int NSL = W * PL_BPW;   // 64-pod slices of the workgroup
+  __shared__ uint32_t s_cnt[CMP ? NSL : 1];
+  __shared__ uint32_t s_pod[CMP ? NSL * WAVE : 1];
   const BatchDesc& d = a.d[blockIdx.y];
   const int32_t np = d.n_pods;
-  const int32_t wg0 = (int32_t)blockIdx.x * W * PL_BPW * WAVE;  // first pod of this workgroup
+  const int32_t wg0 = (int32_t)blockIdx.x * NSL * WAVE;  // first pod of this workgroup
   if (wg0 >= np) return;  // the whole workgroup lies past its batch's end
   {
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(a.planes);
     const int32_t nq = a.n_groups * (GROUP_DWORDS / 4);
     for (int32_t i = threadIdx.x; i < nq; i += W * WAVE) s_tab[i] = src[i];
   }
-  __syncthreads();
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int32_t n_groups = a.n_groups, g_full = a.g_full;
   // The wave's PL_BPW pod blocks are evaluated together: each group's planes are read from LDS once
   // and applied to all of them (the LDS broadcast reads, ~6 CU-cycles each, would otherwise bound it).
-  const int32_t wbase = wg0 + wv * PL_BPW * WAVE;
-  if (wbase >= np) return;  // wave-uniform; no barrier below
-  uint32_t P0[PL_BPW], P1[PL_BPW], P2[PL_BPW], P3[PL_BPW], nT[PL_BPW], code[PL_BPW];
+  // CMP: the workgroup's pods are first reordered (stable, through LDS) so that those that do not
+  // tolerate the unschedulable taint come first and those that do last: most 64-pod blocks then hold
+  // one tolerates value, and their scan folds the filter term into the first code compare
+  // (pair_group_ty). Every pair is still evaluated; only the order in which the lanes take the pods
+  // changes, and each result is written back to its pod's own index.
+  uint32_t pk[PL_BPW];  // per block, the lane's pod: index in the workgroup << 8 | tolerates << 4 | code
 #pragma unroll
   for (int b = 0; b < PL_BPW; ++b) {
-    const int32_t j = wbase + b * WAVE + lane;
+    const int32_t pos0 = (wv * PL_BPW + b) * WAVE + lane;
+    const int32_t j = wg0 + pos0;
     uint32_t c = CODE_NONE_POD, t = 0u;
     if (j < np) {
       const int dq = d.pod_digit[j];
       c = (dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;  // NodeNumber.PreScore: Atoi of the last byte
       t = d.pod_tol[j] ? 1u : 0u;
     }
+    pk[b] = ((uint32_t)pos0 << 8) | (t << 4) | c;
+  }
+  if constexpr (CMP) {
+    uint64_t mn[PL_BPW];  // per block: the lanes whose pod does not tolerate (padding lanes count here)
+#pragma unroll
+    for (int b = 0; b < PL_BPW; ++b) {
+      mn[b] = __ballot(((pk[b] >> 4) & 1u) == 0u);
+      if (lane == 0) s_cnt[wv * PL_BPW + b] = (uint32_t)__builtin_popcountll(mn[b]);
+    }
+    __syncthreads();
+    uint32_t tot = 0, pre[PL_BPW];
+#pragma unroll
+    for (int k = 0; k < NSL; ++k) {
+      const uint32_t c = s_cnt[k];
+#pragma unroll
+      for (int b = 0; b < PL_BPW; ++b)
+        if (k == wv * PL_BPW + b) pre[b] = tot;
+      tot += c;
+    }
+#pragma unroll
+    for (int b = 0; b < PL_BPW; ++b) {
+      const uint32_t sl = (uint32_t)(wv * PL_BPW + b);
+      const bool nt = ((pk[b] >> 4) & 1u) == 0u;
+      const uint32_t below = nt ? __builtin_amdgcn_mbcnt_hi((uint32_t)(mn[b] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mn[b], 0u))
+                                : __builtin_amdgcn_mbcnt_hi((uint32_t)(~mn[b] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)~mn[b], 0u));
+      const uint32_t pos = nt ? pre[b] + below : tot + (sl * WAVE - pre[b]) + below;
+      s_pod[pos] = pk[b];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < PL_BPW; ++b) pk[b] = s_pod[(wv * PL_BPW + b) * WAVE + lane];
+  } else {
+    __syncthreads();
+  }
+  uint32_t P0[PL_BPW], P1[PL_BPW], P2[PL_BPW], P3[PL_BPW], nT[PL_BPW], code[PL_BPW];
+  int32_t jj[PL_BPW];
+  int ty[PL_BPW];  // wave-uniform per block: 0 no pod tolerates, 1 every pod does, 2 mixed
+  bool any_act = false;
+#pragma unroll
+  for (int b = 0; b < PL_BPW; ++b) {
+    const uint32_t c = pk[b] & 15u, t = (pk[b] >> 4) & 1u;
+    jj[b] = wg0 + (int32_t)(pk[b] >> 8);
     code[b] = c;
     P0[b] = 0u - (c & 1u);
     P1[b] = 0u - ((c >> 1) & 1u);
     P2[b] = 0u - ((c >> 2) & 1u);
     P3[b] = 0u - (c >> 3);
     nT[b] = t ? 0u : 0xFFFFFFFFu;
+    const uint64_t tm = __ballot(t != 0u);
+    ty[b] = CMP ? (tm == 0 ? 0 : (~tm == 0 ? 1 : 2)) : 2;
+    any_act = any_act || __ballot(jj[b] < np) != 0;
   }
+  if (!any_act) return;  // wave-uniform; no barrier below
   // Groups above 0, descending, two per step (as pair_kernel): each group's 40 / 48 plane words read
   // into VGPRs at once and applied to every block. fm / fx: the lower group of the lowest pair with a
   // feasible match / KX: feasible non-match, identity-like: feasible node. (Reading half a group at a
@@ -773,7 +859,11 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
       if (gg < g_full) {
         lds_group<PLANE_V>(pl, s_tab, gg);
 #pragma unroll
-        for (int b = 0; b < PL_BPW; ++b) pair_group_v<false, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+        for (int b = 0; b < PL_BPW; ++b) {
+          if (ty[b] == 0) pair_group_ty<false, KX, 0>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
+          else if (ty[b] == 1) pair_group_ty<false, KX, 1>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
+          else pair_group_v<false, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+        }
         if constexpr (!KX) {  // no padding: the AND of the group's xi words is nT & AND(X), X shared
           const uint32_t axg = bop3_and3(bop3_and3(pl[PLANE_X][0], pl[PLANE_X][1], pl[PLANE_X][2]),
                                          bop3_and3(pl[PLANE_X][3], pl[PLANE_X][4], pl[PLANE_X][5]),
@@ -784,7 +874,11 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
       } else {
         lds_group<PLANE_N>(pl, s_tab, gg);
 #pragma unroll
-        for (int b = 0; b < PL_BPW; ++b) pair_group_v<true, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+        for (int b = 0; b < PL_BPW; ++b) {
+          if (ty[b] == 0) pair_group_ty<true, KX, 0>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
+          else if (ty[b] == 1) pair_group_ty<true, KX, 1>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
+          else pair_group_v<true, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+        }
       }
     }
 #pragma unroll
@@ -802,8 +896,8 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
   for (int b = 0; b < PL_BPW; ++b) group_firsts_lds<KX>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b], rm[b], rx[b]);
 #pragma unroll
   for (int b = 0; b < PL_BPW; ++b) {
-    const int32_t j = wbase + b * WAVE + lane;
-    if (wbase + b * WAVE >= np) break;  // wave-uniform
+    const int32_t j = jj[b];
+    if (__ballot(j < np) == 0) continue;  // wave-uniform: a block of padding lanes only
     if (rm[b] == NOFIT && fm[b] != NO_GROUP) {  // the lowest hit pair: its lower group, else the one above
       rm[b] = group_first_lds<0>(s_tab, fm[b], P0[b], P1[b], P2[b], P3[b], nT[b]);
       if (rm[b] == NOFIT) rm[b] = group_first_lds<0>(s_tab, fm[b] + 1, P0[b], P1[b], P2[b], P3[b], nT[b]);
@@ -2233,7 +2327,8 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
     const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(w * WAVE);
     if (big) {
-      auto k = pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG>;
+      auto k = dev.pair_compact ? pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG, true>
+                                : pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG, false>;
       if (bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -2246,7 +2341,12 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
       case 1: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 1>), grid, blk, (unsigned)bytes, s, a); break;
       case 3: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 3>), grid, blk, (unsigned)bytes, s, a); break;
       case 4: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 4>), grid, blk, (unsigned)bytes, s, a); break;
-      default: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2>), grid, blk, (unsigned)bytes, s, a); break;
+      default:
+        if (dev.pair_compact)
+          MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, true>), grid, blk, (unsigned)bytes, s, a);
+        else
+          MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2>), grid, blk, (unsigned)bytes, s, a);
+        break;
     }
     return hipGetLastError();
   }
