@@ -58,6 +58,9 @@ struct DeviceInfo {
   // MSH_PAIR_COMPACT: the LDS-staged form (2 blocks per wave) reorders each workgroup's pods by their
   // tolerates bit first, so that most blocks scan with the filter term folded (1 = on)
   int pair_compact = 0;
+  // MSH_PAIR_HYBRID (A/B): the LDS-staged form reads a full group's X and D3 planes by scalar loads
+  // and D0-D2 from LDS (6 broadcast reads per group instead of 10)
+  int pair_hybrid = 0;
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit

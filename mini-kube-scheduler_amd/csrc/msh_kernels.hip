@@ -673,6 +673,44 @@ __device__ __forceinline__ void pair_group_ty(const uint32_t (&pl)[PLANE_N][PLAN
   }
 }
 
+// A full group (no padding slot) with planes 0-2 from LDS (VGPRs) and X, D3 by scalar loads (SGPRs):
+// 6 LDS reads per group instead of 10, at the price of two SGPR-operand v_bitop3 per word (the
+// "hybrid" form, MSH_PAIR_HYBRID). TY as pair_group_ty (2: mixed tolerates, X & nT per word).
+template <bool KX, int TY>
+__device__ __forceinline__ void pair_group_hy(const uint32_t (&pl)[PLANE_N][PLANE_GW], const u32x8& X,
+                                              const u32x8& D3, uint32_t P0, uint32_t P1, uint32_t P2, uint32_t P3,
+                                              uint32_t nT, uint32_t& am, uint32_t& ax) {
+#pragma unroll
+  for (int w = 0; w < PLANE_GW; w += 2) {
+    uint32_t t[2], xi[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ww = w + h;
+      uint32_t u;
+      if constexpr (TY == 0) {
+        u = bop3_or_xor(X[ww], pl[0][ww], P0);
+      } else if constexpr (TY == 1) {
+        u = pl[0][ww] ^ P0;
+      } else {
+        xi[h] = __builtin_amdgcn_bitop3_b32(X[ww], nT, nT, 0xc0);  // X & nT
+        u = bop3_or_xor(xi[h], pl[0][ww], P0);
+      }
+      u = bop3_or_xor(u, pl[1][ww], P1);
+      u = bop3_or_xor(u, pl[2][ww], P2);
+      t[h] = bop3_or_xor(u, D3[ww], P3);
+    }
+    am = bop3_and3(am, t[0], t[1]);
+    if constexpr (KX) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if constexpr (TY == 0) ax = bop3_or_andn(ax, t[h], X[w + h]);
+        else if constexpr (TY == 1) ax |= t[h];
+        else ax = bop3_or_andn(ax, t[h], xi[h]);
+      }
+    }
+  }
+}
+
 // The lane's first feasible node in group g (identity-like modes), NOFIT if none.
 __device__ __forceinline__ uint32_t group_first_feasible_v(const uint32_t (&pl)[PLANE_N][PLANE_GW], uint32_t g,
                                                            uint32_t nT) {
@@ -746,7 +784,7 @@ __device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab
   rx = bx < GROUP_NODES ? g * GROUP_NODES + bx : NOFIT;
 }
 
-template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES, bool CMP = false>
+template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES, bool CMP = false, bool HY = false>
 __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
   extern __shared__ uint4 s_tab[];  // n_groups * GROUP_DWORDS / 4
   constexpr int NSL = W * PL_BPW;   // 64-pod slices of the workgroup
@@ -856,7 +894,24 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
       const int32_t gg = h == 0 ? g : g - 1;
       if (h == 1 && gg <= 0) break;
       uint32_t pl[PLANE_N][PLANE_GW];
-      if (gg < g_full) {
+      if (HY && gg < g_full) {
+        u32x8 sp[2];  // X, D3
+        asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(sp[0]), "=s"(sp[1])
+                     : "s"(a.planes + (size_t)gg * GROUP_DWORDS), "n"(PLANE_X * PLANE_GW * 4), "n"(3 * PLANE_GW * 4));
+        lds_group<3>(pl, s_tab, gg);
+#pragma unroll
+        for (int b = 0; b < PL_BPW; ++b) {
+          if (ty[b] == 0) pair_group_hy<KX, 0>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+          else if (ty[b] == 1) pair_group_hy<KX, 1>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+          else pair_group_hy<KX, 2>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+        }
+        if constexpr (!KX) {  // nT & AND(X): the AND on the scalar unit
+          const uint32_t axg = sp[0][0] & sp[0][1] & sp[0][2] & sp[0][3] & sp[0][4] & sp[0][5] & sp[0][6] & sp[0][7];
+#pragma unroll
+          for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
+        }
+      } else if (gg < g_full) {
         lds_group<PLANE_V>(pl, s_tab, gg);
 #pragma unroll
         for (int b = 0; b < PL_BPW; ++b) {
@@ -2342,7 +2397,11 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
       case 3: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 3>), grid, blk, (unsigned)bytes, s, a); break;
       case 4: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 4>), grid, blk, (unsigned)bytes, s, a); break;
       default:
-        if (dev.pair_compact)
+        if (dev.pair_hybrid && dev.pair_compact)
+          MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, true, true>), grid, blk, (unsigned)bytes, s, a);
+        else if (dev.pair_hybrid)
+          MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, false, true>), grid, blk, (unsigned)bytes, s, a);
+        else if (dev.pair_compact)
           MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, true>), grid, blk, (unsigned)bytes, s, a);
         else
           MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2>), grid, blk, (unsigned)bytes, s, a);

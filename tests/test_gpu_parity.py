@@ -40,6 +40,14 @@ def _set(ctx, msh, ps):
                     [msh.ScorePluginConfig(s, w, msh.Normalize(m)) for s, w, m in zip(ps.score, ps.weights, ps.normalize)])
 
 
+def _pair_env(monkeypatch, spec):
+    """Pair-kernel A/B switches from a spec "planes[-compact][-hybrid]" (planes: sgpr, lds or auto)."""
+    parts = spec.split("-")
+    monkeypatch.setenv("MSH_PAIR_PLANES", parts[0])
+    monkeypatch.setenv("MSH_PAIR_COMPACT", "1" if "compact" in parts else "0")
+    monkeypatch.setenv("MSH_PAIR_HYBRID", "1" if "hybrid" in parts else "0")
+
+
 def _assert_same(got, want, what=""):
     gi, gs, gst = got
     wi, ws, wst = want[:3]
@@ -795,7 +803,7 @@ def test_multi_batch_age_shares(msh, oracle, n, norm, monkeypatch):
                 _assert_same((gi, gs, gst), want, f"{kernel}/{planes} batch {k} (p={len(pods[k][0])}) n={n} norm={norm}")
 
 
-@pytest.mark.parametrize("bpw", ["1", "2", "3", "4", "2-compact"])
+@pytest.mark.parametrize("bpw", ["1", "2", "3", "4", "2-compact", "2-hybrid", "2-compact-hybrid"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("nb", [1, 9, 33])
 def test_multi_batch_launch_lds(msh, oracle, norm, nb, bpw, monkeypatch):
@@ -803,9 +811,8 @@ def test_multi_batch_launch_lds(msh, oracle, norm, nb, bpw, monkeypatch):
     2 and 4 pod blocks per wave): workgroups whose blocks end inside or before a batch, empty and
     one-pod batches, NULL scores."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_PAIR_PLANES", "lds")
+    _pair_env(monkeypatch, "-".join(["lds"] + bpw.split("-")[1:]))
     monkeypatch.setenv("MSH_PAIR_LDS_BPW", bpw.split("-")[0])
-    monkeypatch.setenv("MSH_PAIR_COMPACT", "1" if bpw.endswith("compact") else "0")
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(99 * nb + norm)
     sizes = ([0, 1, 64, 65, 255, 257, 20_003, 5000, 333, 4096, 1, 2, 700, 64, 128, 1025, 999] * 2)[:nb]
@@ -841,7 +848,7 @@ def test_multi_batch_invalid(msh, gpu_ctx):
         gpu_ctx.schedule_batches_device(bad)
 
 
-@pytest.mark.parametrize("planes", ["sgpr", "lds", "lds-compact"])
+@pytest.mark.parametrize("planes", ["sgpr", "lds", "lds-compact", "lds-compact-hybrid"])
 @pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 32_768, 70_000, 106_496, 106_497])
 def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
     """pair_kernel re-reads the first group with a hit from memory when it lies above the lowest group
@@ -849,9 +856,7 @@ def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
     pods' first matches late. Batch, multi-batch and shard-key entry points, NONE and MINMAX, on tables
     with and without a padded top group."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_PAIR_COMPACT", "1" if planes.endswith("compact") else "0")
-    planes = planes.split("-")[0]
-    monkeypatch.setenv("MSH_PAIR_PLANES", planes)  # lds: 4-wave workgroups up to 32,768 nodes, 16-wave up to
+    _pair_env(monkeypatch, planes)  # lds: 4-wave workgroups up to 32,768 nodes, 16-wave up to
     # 106,496 (106,497 falls back to scalar-loaded planes)
     rng = np.random.default_rng(n + 4)
     u, nd, pd, pt = _rand_case(rng, n, 3000, p_unsched=0.2, p_tol=0.3)
@@ -883,7 +888,7 @@ def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
 
 
 @pytest.mark.parametrize("planes,slices", [("sgpr", 0), ("sgpr", 1), ("sgpr", 2), ("sgpr", 4), ("lds", 0),
-                                           ("lds-compact", 0)])
+                                           ("lds-compact", 0), ("lds-hybrid", 0), ("lds-compact-hybrid", 0)])
 @pytest.mark.parametrize("n", [1000, 5000, 20_000])
 def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices, monkeypatch):
     """The identity-like modes take a pod's first feasible node from the scalar unit's per-group
@@ -893,8 +898,7 @@ def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices, monkeypatch):
     MINMAX; batch and shard keys; every slice count."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("MSH_BITS_SLICES", str(slices))
-    monkeypatch.setenv("MSH_PAIR_PLANES", planes.split("-")[0])  # "lds": the LDS-staged form at any size
-    monkeypatch.setenv("MSH_PAIR_COMPACT", "1" if planes.endswith("compact") else "0")
+    _pair_env(monkeypatch, planes)  # "lds": the LDS-staged form at any launch size
     rng = np.random.default_rng(n + slices)
     u, nd, pd, pt = _rand_case(rng, n, 2000, p_unsched=0.0, p_tol=0.2)
     cut = int(n * 0.6)
@@ -1059,14 +1063,14 @@ def _c3_cols(n):
     return {0: rng.integers(-(1 << 31), (1 << 31) + 1, n), 1: rng.integers(0, 7, n) * 13}
 
 
-@pytest.mark.parametrize("kernel", ["pair", "pair-compact", "generic"])
+@pytest.mark.parametrize("kernel", ["pair", "pair-compact", "pair-compact-hybrid", "generic"])
 def test_c3_reference_list_vs_oracle(msh, oracle, synth, kernel, monkeypatch):
     """5,000 nodes x 100,000 pods (BASELINE C3, the headline workload), the reference plugin list,
     weight 1, no normalizer, through the batch and the 32-batch entry points of the per-pair kernel
     (pair_kernel, the headline) and of generic_kernel (explicit int64 scores, MSH_BATCH_KERNEL=generic):
     bit-exact vs oracle.c_schedule_batch (the restatement of minisched.go:115-199,304-325)."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_PAIR_COMPACT", "1" if kernel.endswith("compact") else "0")
+    _pair_env(monkeypatch, "-".join(["auto"] + kernel.split("-")[1:]))
     kernel = kernel.split("-")[0]
     monkeypatch.setenv("MSH_BATCH_KERNEL", kernel)
     u, nd, pd, pt = synth.make_soa(5000, 100_000)
