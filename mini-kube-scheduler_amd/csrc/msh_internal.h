@@ -57,10 +57,12 @@ struct DeviceInfo {
   int pair_lds_bpw = 2;  // A/B (MSH_PAIR_LDS_BPW): 64-pod blocks per wave of the LDS-staged form, 1-4
   // MSH_PAIR_COMPACT: the LDS-staged form (2 blocks per wave) reorders each workgroup's pods by their
   // tolerates bit first, so that most blocks scan with the filter term folded (1 = on)
-  int pair_compact = 0;
-  // MSH_PAIR_HYBRID (A/B): the LDS-staged form reads a full group's X and D3 planes by scalar loads
-  // and D0-D2 from LDS (6 broadcast reads per group instead of 10)
-  int pair_hybrid = 0;
+  // (-1 = auto: on for REVERSE / MINMAX, where it measured 2% faster, off for the identity-like modes)
+  int pair_compact = -1;
+  // MSH_PAIR_HYBRID: the LDS-staged form (4-wave workgroups) reads a full group's X and D3 planes by
+  // scalar loads and D0-D2 from LDS, 6 broadcast reads per group instead of 10 (default on: 81.1
+  // against 86.1 us per 32-batch C3 launch, profiles/r4_ab_pair_planes.txt)
+  int pair_hybrid = 1;
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit

@@ -2381,9 +2381,10 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
     const int32_t bx = (blocks + w * bpw - 1) / (w * bpw);
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
     const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(w * WAVE);
+    const bool cmp = dev.pair_compact < 0 ? KX : dev.pair_compact != 0;
     if (big) {
-      auto k = dev.pair_compact ? pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG, true>
-                                : pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG, false>;
+      auto k = cmp ? pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG, true>
+                   : pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG, false>;
       if (bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -2397,11 +2398,11 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
       case 3: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 3>), grid, blk, (unsigned)bytes, s, a); break;
       case 4: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 4>), grid, blk, (unsigned)bytes, s, a); break;
       default:
-        if (dev.pair_hybrid && dev.pair_compact)
+        if (dev.pair_hybrid && cmp)
           MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, true, true>), grid, blk, (unsigned)bytes, s, a);
         else if (dev.pair_hybrid)
           MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, false, true>), grid, blk, (unsigned)bytes, s, a);
-        else if (dev.pair_compact)
+        else if (cmp)
           MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, true>), grid, blk, (unsigned)bytes, s, a);
         else
           MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2>), grid, blk, (unsigned)bytes, s, a);
