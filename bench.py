@@ -82,11 +82,13 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
     if classrows and groups <= WGP_MAX_GROUPS and not shard:
         return f"void msh::wgp_kernel<4, {b(kx)}>"
     waves = -(-n_pods // 64) * (nb if multi else 1)
-    # the LDS-staged form: <SHARD, KX, blocks per wave, waves per workgroup, compact (auto: KX), hybrid>
+    # the LDS-staged form: <SHARD, KX, blocks per wave, waves per workgroup, compact (auto: KX),
+    # hybrid planes (auto: 2 for KX, else 1)>
+    hy = 2 if kx else 1
     if groups <= PAIR_LDS_MAX_GROUPS and waves >= cus * 4 * 4 * 4:
-        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2, 4, {b(kx)}, true>"
+        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2, 4, {b(kx)}, {hy}>"
     if PAIR_LDS_MAX_GROUPS < groups <= PAIR_LDS_BIG_GROUPS and waves >= cus * 2 * 16:  # 16-wave workgroups
-        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2, 16, {b(kx)}, false>"
+        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2, 16, {b(kx)}, {hy}>"
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2

@@ -784,7 +784,7 @@ __device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab
   rx = bx < GROUP_NODES ? g * GROUP_NODES + bx : NOFIT;
 }
 
-template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES, bool CMP = false, bool HY = false>
+template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES, bool CMP = false, int HY = 0>
 __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
   extern __shared__ uint4 s_tab[];  // n_groups * GROUP_DWORDS / 4
   constexpr int NSL = W * PL_BPW;   // 64-pod slices of the workgroup
@@ -889,6 +889,14 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
       ax[b] = KX ? 0u : 0xFFFFFFFFu;
     }
     const int32_t g2 = g - 1 > 0 ? g - 1 : g;
+    u32x8 spp[2][2];  // HY 2: X, D3 of both groups of the step, one wait for the four scalar loads
+    if constexpr (HY == 2) {
+      asm volatile("s_load_dwordx8 %0, %4, %6\n\ts_load_dwordx8 %1, %4, %7\n\t"
+                   "s_load_dwordx8 %2, %5, %6\n\ts_load_dwordx8 %3, %5, %7\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&s"(spp[0][0]), "=&s"(spp[0][1]), "=&s"(spp[1][0]), "=&s"(spp[1][1])
+                   : "s"(a.planes + (size_t)g * GROUP_DWORDS), "s"(a.planes + (size_t)g2 * GROUP_DWORDS),
+                     "n"(PLANE_X * PLANE_GW * 4), "n"(3 * PLANE_GW * 4));
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int32_t gg = h == 0 ? g : g - 1;
@@ -896,9 +904,14 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
       uint32_t pl[PLANE_N][PLANE_GW];
       if (HY && gg < g_full) {
         u32x8 sp[2];  // X, D3
-        asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
-                     : "=s"(sp[0]), "=s"(sp[1])
-                     : "s"(a.planes + (size_t)gg * GROUP_DWORDS), "n"(PLANE_X * PLANE_GW * 4), "n"(3 * PLANE_GW * 4));
+        if constexpr (HY == 2) {
+          sp[0] = spp[h][0];
+          sp[1] = spp[h][1];
+        } else {
+          asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                       : "=&s"(sp[0]), "=&s"(sp[1])
+                       : "s"(a.planes + (size_t)gg * GROUP_DWORDS), "n"(PLANE_X * PLANE_GW * 4), "n"(3 * PLANE_GW * 4));
+        }
         lds_group<3>(pl, s_tab, gg);
 #pragma unroll
         for (int b = 0; b < PL_BPW; ++b) {
@@ -1057,7 +1070,29 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
   }
   const uint32_t ball0 = A.ball[0], ball1 = A.ball[1];
   const IdentDecode idd = make_ident_decode(A.pp);
+  constexpr int GQ16 = GQL * 8;  // a group's stride in uint16
+  __shared__ uint32_t s_xb[KX ? HR_CLS : 1];
   __syncthreads();
+  if constexpr (KX) {
+    // REVERSE / MIN-MAX: per pod class, bit g = group g holds a feasible non-match (its first-node
+    // offset, hr_first_kernel, is not HR_NONE), once per workgroup from the staged table: 8 lanes per
+    // class, four groups each (<= 32 groups), OR-reduced over the 8 lanes. The scan then reads one word
+    // per pod instead of a 2-byte offset per group (4 ds_read_u16 and ~10 VALU per four groups).
+    static_assert(NT >= HR_CLS * 8 && WGP_MAX_GROUPS <= 32, "one lane per (class, four groups)");
+    const int32_t t = (int32_t)threadIdx.x, c = t >> 3, g0 = (t & 7) * 4;
+    uint32_t bits = 0;
+    if (c < HR_CLS) {
+      const uint16_t* o = reinterpret_cast<const uint16_t*>(s_tab + HR_FIRST) + HR_CLS + c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (g0 + k < n_groups && o[(g0 + k) * GQ16] != HR_NONE) bits |= 1u << (g0 + k);
+    }
+    bits |= __shfl_xor(bits, 1);
+    bits |= __shfl_xor(bits, 2);
+    bits |= __shfl_xor(bits, 4);
+    if (c < HR_CLS && (t & 7) == 0) s_xb[c] = bits;
+    __syncthreads();
+  }
   // ---- the (batch, block) walk: item it = b * bpb + x (pods [NT x, NT x + NT) of batch b, 64 per
   // wave), it = blockIdx.x, blockIdx.x + G, ... Per item a wave: scans the first two groups; issues the
   // PREVIOUS item's output stores and then the NEXT item's pod-byte loads; scans the rest; decodes. The
@@ -1174,28 +1209,18 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
     // Groups descending, four per step (eight ds_read_b128 in flight; n_groups is a multiple of 4:
     // tables are padded to 1,024-node blocks), one flag per PAIR of groups: bit q of bm = group 2q or
     // 2q + 1 holds a feasible digit match (the 16 words of a pair reduce in 8 VALU: 7 v_bitop3 OR3 and
-    // one more), and, KX, bit q of bx = one of them holds a feasible non-match (below). The previous
-    // item's stores and the next item's loads go after the first step.
-    uint32_t bm = 0, bx = 0;
+    // one more); KX takes the first feasible non-match from the class's group bitmap (s_xb). The
+    // previous item's stores and the next item's loads go after the first step.
+    uint32_t bm = 0;
     auto or16 = [](const uint4& a, const uint4& b, const uint4& c, const uint4& d) {
       return or3(or3(or3(a.x, a.y, a.z), or3(a.w, b.x, b.y), or3(b.z, b.w, c.x)),
                  or3(or3(c.y, c.z, c.w), or3(d.x, d.y, d.z), d.w), 0u);
-    };
-    // KX: whether a group holds a feasible non-match for the pod's class is its first-node offset
-    // (hr_first_kernel, per upload) != HR_NONE: one 2-byte LDS read per group instead of the F[t] & ~H
-    // words (8 ds_read_b128 and 34 VALU per four groups; the MIN-MAX launch took 1.8x the identity's)
-    const uint16_t* __restrict__ offx = reinterpret_cast<const uint16_t*>(s_tab + HR_FIRST) + HR_CLS + cls;
-    constexpr int GQ16 = GQL * 8;  // a group's stride in uint16
-    auto nx2 = [&](int32_t g) {    // groups g, g + 1: 1 if either holds a feasible non-match
-      const uint32_t o0 = offx[g * GQ16], o1 = offx[(g + 1) * GQ16];
-      return min1(umin(o0, o1) ^ (uint32_t)HR_NONE);
     };
     auto step = [&](int32_t q) {  // groups q .. q + 3
       const uint4* t = s_tab + q * GQL;
       const uint4 a0 = t[e0], b0 = t[e1], a1 = t[GQL + e0], b1 = t[GQL + e1];
       const uint4 a2 = t[2 * GQL + e0], b2 = t[2 * GQL + e1], a3 = t[3 * GQL + e0], b3 = t[3 * GQL + e1];
       bm = lshl_or(bm, 2, lshl_or(min1(or16(a2, b2, a3, b3)), 1, min1(or16(a0, b0, a1, b1))));
-      if constexpr (KX) bx = lshl_or(bx, 2, lshl_or(nx2(q + 2), 1, nx2(q)));
     };
     int32_t q = n_groups - 4;
     if (q >= 0) {
@@ -1217,8 +1242,13 @@ __global__ __launch_bounds__(W * WAVE) void wgp_kernel(MultiArgs ka) {
     };
     uint32_t rm = NOFIT, rx = NOFIT;
     if (bm) rm = first_of(bm, 0);
-    if constexpr (KX)
-      if (bx) rx = first_of(bx, HR_CLS);
+    if constexpr (KX) {
+      const uint32_t xb = s_xb[cls];  // the class's groups with a feasible non-match
+      if (xb) {
+        const uint32_t g = lowbit(xb);
+        rx = g * GROUP_NODES + reinterpret_cast<const uint16_t*>(s_tab + g * GQL + HR_FIRST)[HR_CLS + cls];
+      }
+    }
     const int64_t im = rm != NOFIT ? (int64_t)rm : -1, ia = key_to_idx(tol ? ball1 : ball0);
     if constexpr (KX)
       decode_pod(im, rx != NOFIT ? (int64_t)rx : -1, ia, cur.code != CODE_NONE_POD, A.pp, &s_oi, &s_osc, &s_ost);
@@ -2382,32 +2412,35 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
     const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(w * WAVE);
     const bool cmp = dev.pair_compact < 0 ? KX : dev.pair_compact != 0;
-    if (big) {
-      auto k = cmp ? pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG, true>
-                   : pair_lds_kernel<SHARD, KX, 2, PL_WAVES_BIG, false>;
-      if (bytes > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        if (e != hipSuccess) return e;
+    const int hy = dev.pair_hybrid >= 0 && dev.pair_hybrid <= 2 ? dev.pair_hybrid : (KX ? 2 : 1);
+    // (bpw, compaction, hybrid) -> instance: 1 block per wave in the plain LDS form only
+    using PairKernel = void (*)(PairArgs);
+    auto pick = [&](auto bpw_c, auto w_c) -> PairKernel {
+      constexpr int B = decltype(bpw_c)::value, WW = decltype(w_c)::value;
+      if constexpr (B == 1) {
+        return pair_lds_kernel<SHARD, KX, B, WW>;
+      } else {
+        const PairKernel t[2][3] = {
+            {pair_lds_kernel<SHARD, KX, B, WW, false, 0>,
+             pair_lds_kernel<SHARD, KX, B, WW, false, 1>,
+             pair_lds_kernel<SHARD, KX, B, WW, false, 2>},
+            {pair_lds_kernel<SHARD, KX, B, WW, true, 0>,
+             pair_lds_kernel<SHARD, KX, B, WW, true, 1>,
+             pair_lds_kernel<SHARD, KX, B, WW, true, 2>}};
+        return t[cmp ? 1 : 0][hy];
       }
-      MSH_TIMED_LAUNCH(k, grid, blk, (unsigned)bytes, s, a);
-      return hipGetLastError();
+    };
+    PairKernel k;
+    if (big) k = pick(std::integral_constant<int, 2>{}, std::integral_constant<int, PL_WAVES_BIG>{});
+    else if (bpw == 1) k = pick(std::integral_constant<int, 1>{}, std::integral_constant<int, PL_WAVES>{});
+    else if (bpw == 3) k = pick(std::integral_constant<int, 3>{}, std::integral_constant<int, PL_WAVES>{});
+    else if (bpw == 4) k = pick(std::integral_constant<int, 4>{}, std::integral_constant<int, PL_WAVES>{});
+    else k = pick(std::integral_constant<int, 2>{}, std::integral_constant<int, PL_WAVES>{});
+    if (bytes > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+      if (e != hipSuccess) return e;
     }
-    switch (bpw) {
-      case 1: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 1>), grid, blk, (unsigned)bytes, s, a); break;
-      case 3: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 3>), grid, blk, (unsigned)bytes, s, a); break;
-      case 4: MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 4>), grid, blk, (unsigned)bytes, s, a); break;
-      default:
-        if (dev.pair_hybrid && cmp)
-          MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, true, true>), grid, blk, (unsigned)bytes, s, a);
-        else if (dev.pair_hybrid)
-          MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, false, true>), grid, blk, (unsigned)bytes, s, a);
-        else if (cmp)
-          MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2, PL_WAVES, true>), grid, blk, (unsigned)bytes, s, a);
-        else
-          MSH_TIMED_LAUNCH((pair_lds_kernel<SHARD, KX, 2>), grid, blk, (unsigned)bytes, s, a);
-        break;
-    }
+    MSH_TIMED_LAUNCH(k, grid, blk, (unsigned)bytes, s, a);
     return hipGetLastError();
   }
   const int S = pair_slices(waves, a.n_groups, dev);

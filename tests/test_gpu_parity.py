@@ -41,11 +41,12 @@ def _set(ctx, msh, ps):
 
 
 def _pair_env(monkeypatch, spec):
-    """Pair-kernel A/B switches from a spec "planes[-compact][-hybrid]" (planes: sgpr, lds or auto)."""
+    """Pair-kernel A/B switches from a spec "planes[-compact][-hybrid|-hybrid2]" (planes: sgpr, lds or
+    auto; hybrid2: both groups' scalar planes of a step loaded under one wait)."""
     parts = spec.split("-")
     monkeypatch.setenv("MSH_PAIR_PLANES", parts[0])
     monkeypatch.setenv("MSH_PAIR_COMPACT", "1" if "compact" in parts else "0")
-    monkeypatch.setenv("MSH_PAIR_HYBRID", "1" if "hybrid" in parts else "0")
+    monkeypatch.setenv("MSH_PAIR_HYBRID", "2" if "hybrid2" in parts else "1" if "hybrid" in parts else "0")
 
 
 def _assert_same(got, want, what=""):
@@ -803,7 +804,8 @@ def test_multi_batch_age_shares(msh, oracle, n, norm, monkeypatch):
                 _assert_same((gi, gs, gst), want, f"{kernel}/{planes} batch {k} (p={len(pods[k][0])}) n={n} norm={norm}")
 
 
-@pytest.mark.parametrize("bpw", ["1", "2", "3", "4", "2-compact", "2-hybrid", "2-compact-hybrid"])
+@pytest.mark.parametrize("bpw", ["1", "2", "3", "4", "2-compact", "2-hybrid", "2-compact-hybrid", "2-hybrid2",
+                                 "2-compact-hybrid2", "3-hybrid", "3-compact-hybrid2", "4-hybrid2"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("nb", [1, 9, 33])
 def test_multi_batch_launch_lds(msh, oracle, norm, nb, bpw, monkeypatch):
@@ -848,7 +850,7 @@ def test_multi_batch_invalid(msh, gpu_ctx):
         gpu_ctx.schedule_batches_device(bad)
 
 
-@pytest.mark.parametrize("planes", ["sgpr", "lds", "lds-compact", "lds-compact-hybrid"])
+@pytest.mark.parametrize("planes", ["sgpr", "lds", "lds-compact", "lds-compact-hybrid", "lds-hybrid2"])
 @pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 32_768, 70_000, 106_496, 106_497])
 def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
     """pair_kernel re-reads the first group with a hit from memory when it lies above the lowest group
@@ -888,7 +890,8 @@ def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
 
 
 @pytest.mark.parametrize("planes,slices", [("sgpr", 0), ("sgpr", 1), ("sgpr", 2), ("sgpr", 4), ("lds", 0),
-                                           ("lds-compact", 0), ("lds-hybrid", 0), ("lds-compact-hybrid", 0)])
+                                           ("lds-compact", 0), ("lds-hybrid", 0), ("lds-compact-hybrid", 0),
+                                           ("lds-hybrid2", 0), ("lds-compact-hybrid2", 0)])
 @pytest.mark.parametrize("n", [1000, 5000, 20_000])
 def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices, monkeypatch):
     """The identity-like modes take a pod's first feasible node from the scalar unit's per-group
@@ -945,6 +948,36 @@ def test_batch_kernel_ab(msh, oracle, kernel, monkeypatch):
         torch.cuda.synchronize()
         for t in ts:
             _assert_same([t[i].cpu().numpy() for i in (2, 3, 4)], want, f"{kernel} multi")
+
+
+@pytest.mark.parametrize("n", [1000, 5000, 8192])
+def test_classrows_late_nonmatch(msh, oracle, n, monkeypatch):
+    """The class-row kernel's REVERSE / MIN-MAX first feasible non-match comes from a per-class group
+    bitmap built once per workgroup: digit 7 on the first 70% of the nodes (digit-7 pods' first
+    non-match late), then on every node (none at all); DEFAULT, REVERSE and MIN-MAX, batch and
+    multi-batch."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MSH_BATCH_KERNEL", "classrows")
+    rng = np.random.default_rng(n + 77)
+    u, nd, pd, pt = _rand_case(rng, n, 4000, p_unsched=0.15, p_tol=0.3)
+    pd[:1500] = 7
+    dev = torch.device("cuda:0")
+    with msh.DeviceContext(0) as ctx:
+        for frac in (0.7, 1.0):
+            nd2 = nd.copy()
+            nd2[: int(n * frac)] = 7
+            for norm in (1, 2, 3):
+                ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
+                _set(ctx, msh, ps)
+                ctx.upload_nodes(u, nd2)
+                want = oracle.c_schedule_batch(u, nd2, pd, pt, ps, threads=8)
+                _assert_same(ctx.schedule_batch(pd, pt), want, f"classrows n={n} frac={frac} norm={norm}")
+                ts = [_dev_batch(torch, dev, pd, pt) for _ in range(2)]
+                ctx.schedule_batches_device(ctx.batch_descs([_desc(t) for t in ts]),
+                                            stream=torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                for t in ts:
+                    _assert_same([t[i].cpu().numpy() for i in (2, 3, 4)], want, f"classrows multi n={n} norm={norm}")
 
 
 # ---- the generic score pipeline (score-column plugins; north_star stages 1-5 with explicit int64 scores)
