@@ -754,13 +754,13 @@ __device__ __forceinline__ uint32_t group_first_lds(const uint4* __restrict__ s_
   return NOFIT;
 }
 
-// Both firsts of group g in one pass over its planes (half a group at a time): the first feasible
-// match (rm) and, KX, the first feasible non-match or, else, the first feasible node (rx); NOFIT
-// where the group has none.
+// Both firsts of group g in one pass over its planes (half a group at a time, the upper half only
+// when some lane needs it): the first feasible match (rm) and, KX, the first feasible non-match or,
+// else, the first feasible node (rx); NOFIT where the group has none. Called by whole waves.
 template <bool KX>
 __device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab, uint32_t g, uint32_t P0,
-                                                 uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT, uint32_t& rm,
-                                                 uint32_t& rx) {
+                                                 uint32_t P1, uint32_t P2, uint32_t P3, uint32_t nT, bool digit,
+                                                 uint32_t& rm, uint32_t& rx) {
   const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
   uint32_t bm = 0xFFFFFFFFu, bx = 0xFFFFFFFFu;
 #pragma unroll 1
@@ -779,6 +779,10 @@ __device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab
       bm = umin(bm, lowbit(~dm & fe) | off);  // all-ones stays all-ones for a word without one
       bx = umin(bx, lowbit(KX ? (dm & fe) : fe) | off);
     }
+    // the upper half only when some lane's first match (a pod without a digit has none: its code
+    // matches no node's) or first feasible (non-match) is not in the lower one: with random digits
+    // almost never, and the scan of group 0 halves
+    if (hh == 0 && __ballot((digit && bm == 0xFFFFFFFFu) || bx == 0xFFFFFFFFu) == 0) break;
   }
   rm = bm < GROUP_NODES ? g * GROUP_NODES + bm : NOFIT;
   rx = bx < GROUP_NODES ? g * GROUP_NODES + bx : NOFIT;
@@ -961,7 +965,7 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
   constexpr int KIND_X = KX ? 1 : 2;  // KX: first feasible non-match; else first feasible node
   uint32_t rm[PL_BPW], rx[PL_BPW];
 #pragma unroll
-  for (int b = 0; b < PL_BPW; ++b) group_firsts_lds<KX>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b], rm[b], rx[b]);
+  for (int b = 0; b < PL_BPW; ++b) group_firsts_lds<KX>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b], code[b] != CODE_NONE_POD, rm[b], rx[b]);
 #pragma unroll
   for (int b = 0; b < PL_BPW; ++b) {
     const int32_t j = jj[b];

@@ -208,3 +208,59 @@ def test_generic_node_sharding_across_processes(oracle, world, name):
     ps = oracle.PluginSet(score=[nm for nm, _, _ in pl], weights=[w for _, w, _ in pl], normalize=[m for _, _, m in pl])
     wi, ws, wst, _ = oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=_generic_cols(seed, n))
     assert (gi == wi).all() and (gs == ws).all() and (gst == wst).all()
+
+
+def _worker_c4(rank, world, port, n, p, norm, out_q):
+    """BASELINE C4's shape: the 100k-node table in contiguous List-order shards, every rank scanning
+    all 1M pods against its shard (the LDS-staged pair kernel with SHARD keys: 25,000 nodes per rank),
+    keys merged by all_reduce MAX (gloo here), decoded on the device."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        msh = importlib.import_module("mini-kube-scheduler_amd")
+        D = importlib.import_module("mini-kube-scheduler_amd.distributed")
+        synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
+        u, nd, pd, pt = synth.make_soa(n, p)
+        dev = torch.device("cuda:0")
+        ctx = msh.DeviceContext(0)
+        ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                        [msh.ScorePluginConfig(msh.NODE_NUMBER, 2, msh.Normalize(norm))])
+        sched = D.NodeShardedScheduler(ctx, u, nd, world, rank)
+        d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+        keys = torch.zeros(ctx.shard_keys_len(p), dtype=torch.int32, device=dev)
+        out = [torch.full((p,), -7, dtype=dt, device=dev) for dt in (torch.int32, torch.int64, torch.int32)]
+        sched.schedule(d_pd, d_pt, keys, *out)
+        torch.cuda.synchronize()
+        if rank == 0:
+            out_q.put(tuple(t.cpu().numpy() for t in out))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("norm", [0, 3])
+def test_c4_node_sharded_vs_oracle(oracle, norm):
+    """C4 at full size (100,000 nodes x 1,000,000 pods, bench.py's synthetic snapshot) node-sharded
+    over 4 processes: every decision bit-exact against the oracle over the whole table."""
+    n, p, world = 100_000, 1_000_000, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_c4, args=(r, world, port, n, p, norm, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        gi, gs, gst = q.get(timeout=240)
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+    assert all(pr.exitcode == 0 for pr in procs)
+    synth = importlib.import_module("mini-kube-scheduler_amd.synthetic")
+    u, nd, pd, pt = synth.make_soa(n, p)
+    wi, ws, wst, _ = oracle.c_schedule_batch(u, nd, pd, pt, oracle.PluginSet(weights=[2], normalize=[norm]),
+                                             threads=16)
+    bad = np.nonzero((gi != wi) | (gs != ws) | (gst != wst))[0]
+    assert bad.size == 0, f"{bad.size} pods differ; first {bad[:5]}"
