@@ -967,6 +967,11 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
         if constexpr (HY == 2) {
           sp[0] = spp[h][0];
           sp[1] = spp[h][1];
+        } else if constexpr (HY == 4) {  // compiler-scheduled scalar loads (constant address space)
+          const __attribute__((address_space(4))) u32x8* q =
+              (const __attribute__((address_space(4))) u32x8*)(a.planes + (size_t)gg * GROUP_DWORDS);
+          sp[0] = q[PLANE_X];
+          sp[1] = q[3];
         } else {
           asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
                        : "=&s"(sp[0]), "=&s"(sp[1])
@@ -2472,7 +2477,7 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
     const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(w * WAVE);
     const bool cmp = dev.pair_compact < 0 ? KX : dev.pair_compact != 0;
-    const int hy = dev.pair_hybrid >= 0 && dev.pair_hybrid <= 3 ? dev.pair_hybrid : (KX ? 2 : 1);
+    const int hy = dev.pair_hybrid >= 0 && dev.pair_hybrid <= 4 ? dev.pair_hybrid : (KX ? 2 : 1);
     // (bpw, compaction, hybrid) -> instance: 1 block per wave in the plain LDS form only
     using PairKernel = void (*)(PairArgs);
     auto pick = [&](auto bpw_c, auto w_c) -> PairKernel {
@@ -2480,15 +2485,17 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
       if constexpr (B == 1) {
         return pair_lds_kernel<SHARD, KX, B, WW>;
       } else {
-        const PairKernel t[2][4] = {
+        const PairKernel t[2][5] = {
             {pair_lds_kernel<SHARD, KX, B, WW, false, 0>,
              pair_lds_kernel<SHARD, KX, B, WW, false, 1>,
              pair_lds_kernel<SHARD, KX, B, WW, false, 2>,
-             pair_lds_kernel<SHARD, KX, B, WW, false, 3>},
+             pair_lds_kernel<SHARD, KX, B, WW, false, 3>,
+             pair_lds_kernel<SHARD, KX, B, WW, false, 4>},
             {pair_lds_kernel<SHARD, KX, B, WW, true, 0>,
              pair_lds_kernel<SHARD, KX, B, WW, true, 1>,
              pair_lds_kernel<SHARD, KX, B, WW, true, 2>,
-             pair_lds_kernel<SHARD, KX, B, WW, true, 3>}};
+             pair_lds_kernel<SHARD, KX, B, WW, true, 3>,
+             pair_lds_kernel<SHARD, KX, B, WW, true, 4>}};
         return t[cmp ? 1 : 0][hy];
       }
     };
