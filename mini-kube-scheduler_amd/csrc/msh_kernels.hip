@@ -825,8 +825,8 @@ __device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab
   rx = bx < GROUP_NODES ? g * GROUP_NODES + bx : NOFIT;
 }
 
-template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES, bool CMP = false, int HY = 0>
-__global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
+template <bool SHARD, bool KX, int PL_BPW, int W, bool CMP, int HY>
+__device__ __forceinline__ void pair_lds_body(PairArgs a) {
   extern __shared__ uint4 s_tab[];  // n_groups * GROUP_DWORDS / 4
   constexpr int NSL = W * PL_BPW;   // 64-pod slices of the workgroup
   __shared__ uint32_t s_cnt[CMP ? NSL : 1];
@@ -1057,6 +1057,12 @@ __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
   }
 }
 
+// (the body is a device function so that A/B builds can wrap it with other register budgets: a
+// 7-waves-per-SIMD build, 72 VGPRs with a few spilled, ran 1-5% slower, profiles/r4_ab_pair_planes.txt)
+template <bool SHARD, bool KX, int PL_BPW, int W = PL_WAVES, bool CMP = false, int HY = 0>
+__global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
+  pair_lds_body<SHARD, KX, PL_BPW, W, CMP, HY>(a);
+}
 
 __device__ __forceinline__ uint32_t min1(uint32_t x) {  // x != 0 as 0 / 1 in one v_min_u32
   uint32_t r;
