@@ -65,6 +65,12 @@ struct DeviceInfo {
   // identity-like modes (81.1 against 86.1 us per 32-batch C3 launch), 2 for REVERSE / MINMAX (87.9
   // against 90.7 with 1), profiles/r4_ab_pair_planes.txt
   int pair_hybrid = -1;
+  // MSH_PAIR_NOAX: the LDS-staged form scans group 0 first and drops the non-match / feasible
+  // reduction from the scan of the other groups when group 0 has settled it for every lane of the
+  // wave (1), or scans group 0 last and never drops it (0). -1 = auto: 1 for REVERSE / MINMAX (78.1
+  // against 89.0 us per 32-batch C3 launch), 0 for the identity-like modes (77.3-78.3 against
+  // 80.9-81.2), profiles/r4_ab_pair_planes.txt
+  int pair_noax = -1;
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit
@@ -193,6 +199,7 @@ struct PairArgs {
   int32_t n_groups;
   int32_t g_full;          // groups [0, g_full) hold real nodes only (no padding slot)
   int32_t gps;             // groups per slice wave (set by the launcher)
+  int32_t noax;            // pair_lds_kernel: group 0 may settle the non-match reduction (launcher)
   int32_t nb;
   PluginParams pp;
   int64_t node_base;       // shard mode: global index of local node 0

@@ -922,111 +922,131 @@ __device__ __forceinline__ void pair_lds_body(PairArgs a) {
   uint32_t fm[PL_BPW], fx[PL_BPW];
 #pragma unroll
   for (int b = 0; b < PL_BPW; ++b) fm[b] = fx[b] = NO_GROUP;
-  for (int32_t g = n_groups - 1; g > 0; g -= 2) {
-    uint32_t am[PL_BPW], ax[PL_BPW];
-#pragma unroll
-    for (int b = 0; b < PL_BPW; ++b) {
-      am[b] = 0xFFFFFFFFu;
-      ax[b] = KX ? 0u : 0xFFFFFFFFu;
-    }
-    const int32_t g2 = g - 1 > 0 ? g - 1 : g;
-    u32x8 spp[2][2];  // HY 2: X, D3 of both groups of the step, one wait for the four scalar loads
-    if constexpr (HY == 2) {
-      asm volatile("s_load_dwordx8 %0, %4, %6\n\ts_load_dwordx8 %1, %4, %7\n\t"
-                   "s_load_dwordx8 %2, %5, %6\n\ts_load_dwordx8 %3, %5, %7\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&s"(spp[0][0]), "=&s"(spp[0][1]), "=&s"(spp[1][0]), "=&s"(spp[1][1])
-                   : "s"(a.planes + (size_t)g * GROUP_DWORDS), "s"(a.planes + (size_t)g2 * GROUP_DWORDS),
-                     "n"(PLANE_X * PLANE_GW * 4), "n"(3 * PLANE_GW * 4));
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int32_t gg = h == 0 ? g : g - 1;
-      if (h == 1 && gg <= 0) break;
-      uint32_t pl[PLANE_N][PLANE_GW];
-      if (HY == 3 && gg < g_full) {
-        u32x8 sp[3];  // X, D2, D3
-        asm volatile("s_load_dwordx8 %0, %3, %4\n\ts_load_dwordx8 %1, %3, %5\n\ts_load_dwordx8 %2, %3, %6\n\t"
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=&s"(sp[0]), "=&s"(sp[1]), "=&s"(sp[2])
-                     : "s"(a.planes + (size_t)gg * GROUP_DWORDS), "n"(PLANE_X * PLANE_GW * 4), "n"(2 * PLANE_GW * 4),
-                       "n"(3 * PLANE_GW * 4));
-        lds_group<2>(pl, s_tab, gg);
-#pragma unroll
-        for (int b = 0; b < PL_BPW; ++b) {
-          if (ty[b] == 0) pair_group_hy3<KX, 0>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-          else if (ty[b] == 1) pair_group_hy3<KX, 1>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-          else pair_group_hy3<KX, 2>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-        }
-        if constexpr (!KX) {
-          const uint32_t axg = sp[0][0] & sp[0][1] & sp[0][2] & sp[0][3] & sp[0][4] & sp[0][5] & sp[0][6] & sp[0][7];
-#pragma unroll
-          for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
-        }
-      } else if (HY && gg < g_full) {
-        u32x8 sp[2];  // X, D3
-        if constexpr (HY == 2) {
-          sp[0] = spp[h][0];
-          sp[1] = spp[h][1];
-        } else if constexpr (HY == 4) {  // compiler-scheduled scalar loads (constant address space)
-          const __attribute__((address_space(4))) u32x8* q =
-              (const __attribute__((address_space(4))) u32x8*)(a.planes + (size_t)gg * GROUP_DWORDS);
-          sp[0] = q[PLANE_X];
-          sp[1] = q[3];
-        } else {
-          asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
-                       : "=&s"(sp[0]), "=&s"(sp[1])
-                       : "s"(a.planes + (size_t)gg * GROUP_DWORDS), "n"(PLANE_X * PLANE_GW * 4), "n"(3 * PLANE_GW * 4));
-        }
-        lds_group<3>(pl, s_tab, gg);
-#pragma unroll
-        for (int b = 0; b < PL_BPW; ++b) {
-          if (ty[b] == 0) pair_group_hy<KX, 0>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-          else if (ty[b] == 1) pair_group_hy<KX, 1>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-          else pair_group_hy<KX, 2>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-        }
-        if constexpr (!KX) {  // nT & AND(X): the AND on the scalar unit
-          const uint32_t axg = sp[0][0] & sp[0][1] & sp[0][2] & sp[0][3] & sp[0][4] & sp[0][5] & sp[0][6] & sp[0][7];
-#pragma unroll
-          for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
-        }
-      } else if (gg < g_full) {
-        lds_group<PLANE_V>(pl, s_tab, gg);
-#pragma unroll
-        for (int b = 0; b < PL_BPW; ++b) {
-          if (ty[b] == 0) pair_group_ty<false, KX, 0>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
-          else if (ty[b] == 1) pair_group_ty<false, KX, 1>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
-          else pair_group_v<false, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-        }
-        if constexpr (!KX) {  // no padding: the AND of the group's xi words is nT & AND(X), X shared
-          const uint32_t axg = bop3_and3(bop3_and3(pl[PLANE_X][0], pl[PLANE_X][1], pl[PLANE_X][2]),
-                                         bop3_and3(pl[PLANE_X][3], pl[PLANE_X][4], pl[PLANE_X][5]),
-                                         pl[PLANE_X][6] & pl[PLANE_X][7]);
-#pragma unroll
-          for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
-        }
-      } else {
-        lds_group<PLANE_N>(pl, s_tab, gg);
-#pragma unroll
-        for (int b = 0; b < PL_BPW; ++b) {
-          if (ty[b] == 0) pair_group_ty<true, KX, 0>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
-          else if (ty[b] == 1) pair_group_ty<true, KX, 1>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
-          else pair_group_v<true, KX>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-        }
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < PL_BPW; ++b) {
-      fm[b] = am[b] != 0xFFFFFFFFu ? (uint32_t)g2 : fm[b];
-      fx[b] = (KX ? ax[b] != 0u : ax[b] != 0xFFFFFFFFu) ? (uint32_t)g2 : fx[b];
-    }
-  }
-  // group 0: every block's first hits in it, by the half-group reads of the rare path (a group's 48
-  // plane words held at once would set the kernel's register count), then the rare re-reads of a
-  // higher pair, then the decode
+  // Group 0 first: every block's first hits in it (half-group reads; the upper half only when some
+  // lane needs it). When every lane already has its first feasible non-match (KX) or first feasible
+  // node there, the scan of the groups above needs only the match flags: every pair is still
+  // evaluated (dm' per word), but the non-match / feasible reduction, whose answer group 0 has
+  // settled, is left out (KX: 5.5 instead of 6.5 VALU per word).
   constexpr int KIND_X = KX ? 1 : 2;  // KX: first feasible non-match; else first feasible node
   uint32_t rm[PL_BPW], rx[PL_BPW];
+  auto group0 = [&]() {
 #pragma unroll
-  for (int b = 0; b < PL_BPW; ++b) group_firsts_lds<KX>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b], code[b] != CODE_NONE_POD, rm[b], rx[b]);
+    for (int b = 0; b < PL_BPW; ++b) group_firsts_lds<KX>(s_tab, 0u, P0[b], P1[b], P2[b], P3[b], nT[b], code[b] != CODE_NONE_POD, rm[b], rx[b]);
+  };
+  auto scan = [&](auto noax) {
+    constexpr bool NOAX = decltype(noax)::value;
+    constexpr bool KXS = KX && !NOAX;  // the non-match flags are tracked
+    for (int32_t g = n_groups - 1; g > 0; g -= 2) {
+      uint32_t am[PL_BPW], ax[PL_BPW];
+#pragma unroll
+      for (int b = 0; b < PL_BPW; ++b) {
+        am[b] = 0xFFFFFFFFu;
+        ax[b] = KX ? 0u : 0xFFFFFFFFu;
+      }
+      const int32_t g2 = g - 1 > 0 ? g - 1 : g;
+      u32x8 spp[2][2];  // HY 2: X, D3 of both groups of the step, one wait for the four scalar loads
+      if constexpr (HY == 2) {
+        asm volatile("s_load_dwordx8 %0, %4, %6\n\ts_load_dwordx8 %1, %4, %7\n\t"
+                     "s_load_dwordx8 %2, %5, %6\n\ts_load_dwordx8 %3, %5, %7\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&s"(spp[0][0]), "=&s"(spp[0][1]), "=&s"(spp[1][0]), "=&s"(spp[1][1])
+                     : "s"(a.planes + (size_t)g * GROUP_DWORDS), "s"(a.planes + (size_t)g2 * GROUP_DWORDS),
+                       "n"(PLANE_X * PLANE_GW * 4), "n"(3 * PLANE_GW * 4));
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int32_t gg = h == 0 ? g : g - 1;
+        if (h == 1 && gg <= 0) break;
+        uint32_t pl[PLANE_N][PLANE_GW];
+        if (HY == 3 && gg < g_full) {
+          u32x8 sp[3];  // X, D2, D3
+          asm volatile("s_load_dwordx8 %0, %3, %4\n\ts_load_dwordx8 %1, %3, %5\n\ts_load_dwordx8 %2, %3, %6\n\t"
+                       "s_waitcnt lgkmcnt(0)"
+                       : "=&s"(sp[0]), "=&s"(sp[1]), "=&s"(sp[2])
+                       : "s"(a.planes + (size_t)gg * GROUP_DWORDS), "n"(PLANE_X * PLANE_GW * 4), "n"(2 * PLANE_GW * 4),
+                         "n"(3 * PLANE_GW * 4));
+          lds_group<2>(pl, s_tab, gg);
+#pragma unroll
+          for (int b = 0; b < PL_BPW; ++b) {
+            if (ty[b] == 0) pair_group_hy3<KXS, 0>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+            else if (ty[b] == 1) pair_group_hy3<KXS, 1>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+            else pair_group_hy3<KXS, 2>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+          }
+          if constexpr (!KX && !NOAX) {
+            const uint32_t axg = sp[0][0] & sp[0][1] & sp[0][2] & sp[0][3] & sp[0][4] & sp[0][5] & sp[0][6] & sp[0][7];
+#pragma unroll
+            for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
+          }
+        } else if (HY && gg < g_full) {
+          u32x8 sp[2];  // X, D3
+          if constexpr (HY == 2) {
+            sp[0] = spp[h][0];
+            sp[1] = spp[h][1];
+          } else if constexpr (HY == 4) {  // compiler-scheduled scalar loads (constant address space)
+            const __attribute__((address_space(4))) u32x8* q =
+                (const __attribute__((address_space(4))) u32x8*)(a.planes + (size_t)gg * GROUP_DWORDS);
+            sp[0] = q[PLANE_X];
+            sp[1] = q[3];
+          } else {
+            asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&s"(sp[0]), "=&s"(sp[1])
+                         : "s"(a.planes + (size_t)gg * GROUP_DWORDS), "n"(PLANE_X * PLANE_GW * 4), "n"(3 * PLANE_GW * 4));
+          }
+          lds_group<3>(pl, s_tab, gg);
+#pragma unroll
+          for (int b = 0; b < PL_BPW; ++b) {
+            if (ty[b] == 0) pair_group_hy<KXS, 0>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+            else if (ty[b] == 1) pair_group_hy<KXS, 1>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+            else pair_group_hy<KXS, 2>(pl, sp[0], sp[1], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+          }
+          if constexpr (!KX && !NOAX) {  // nT & AND(X): the AND on the scalar unit
+            const uint32_t axg = sp[0][0] & sp[0][1] & sp[0][2] & sp[0][3] & sp[0][4] & sp[0][5] & sp[0][6] & sp[0][7];
+#pragma unroll
+            for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
+          }
+        } else if (gg < g_full) {
+          lds_group<PLANE_V>(pl, s_tab, gg);
+#pragma unroll
+          for (int b = 0; b < PL_BPW; ++b) {
+            if (ty[b] == 0) pair_group_ty<false, KXS, 0>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
+            else if (ty[b] == 1) pair_group_ty<false, KXS, 1>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
+            else pair_group_v<false, KXS>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+          }
+          if constexpr (!KX && !NOAX) {  // no padding: the AND of the group's xi words is nT & AND(X), X shared
+            const uint32_t axg = bop3_and3(bop3_and3(pl[PLANE_X][0], pl[PLANE_X][1], pl[PLANE_X][2]),
+                                           bop3_and3(pl[PLANE_X][3], pl[PLANE_X][4], pl[PLANE_X][5]),
+                                           pl[PLANE_X][6] & pl[PLANE_X][7]);
+#pragma unroll
+            for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
+          }
+        } else {
+          lds_group<PLANE_N>(pl, s_tab, gg);
+#pragma unroll
+          for (int b = 0; b < PL_BPW; ++b) {
+            if (ty[b] == 0) pair_group_ty<true, KXS, 0>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
+            else if (ty[b] == 1) pair_group_ty<true, KXS, 1>(pl, P0[b], P1[b], P2[b], P3[b], am[b], ax[b]);
+            else pair_group_v<true, KXS>(pl, P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < PL_BPW; ++b) {
+        fm[b] = am[b] != 0xFFFFFFFFu ? (uint32_t)g2 : fm[b];
+        if constexpr (!NOAX) fx[b] = (KX ? ax[b] != 0u : ax[b] != 0xFFFFFFFFu) ? (uint32_t)g2 : fx[b];
+      }
+    }
+  };
+  if (a.noax) {
+    group0();
+    bool xdone = true;
+#pragma unroll
+    for (int b = 0; b < PL_BPW; ++b) xdone = xdone && __ballot(rx[b] == NOFIT) == 0;
+    if (xdone) scan(std::true_type{});
+    else scan(std::false_type{});
+  } else {  // group 0 after the scan (its registers free during it)
+    scan(std::false_type{});
+    group0();
+  }
+  // then the rare re-reads of a higher pair, then the decode
 #pragma unroll
   for (int b = 0; b < PL_BPW; ++b) {
     const int32_t j = jj[b];
@@ -2484,6 +2504,7 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
     const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(w * WAVE);
     const bool cmp = dev.pair_compact < 0 ? KX : dev.pair_compact != 0;
     const int hy = dev.pair_hybrid >= 0 && dev.pair_hybrid <= 4 ? dev.pair_hybrid : (KX ? 2 : 1);
+    a.noax = dev.pair_noax >= 0 ? dev.pair_noax : (KX ? 1 : 0);
     // (bpw, compaction, hybrid) -> instance: 1 block per wave in the plain LDS form only
     using PairKernel = void (*)(PairArgs);
     auto pick = [&](auto bpw_c, auto w_c) -> PairKernel {
