@@ -71,9 +71,10 @@ for mode, prefix, tags, nb in (
             # the scan's model per 32-node word and 64-pod wave: v_bitop3 (X & nT) + 4 v_bitop3 for dm' and
             # half an AND3 of two words' dm' = 5.5 VALU (NONE); MIN-MAX adds one OR-accumulate of the
             # feasible non-matches (6.5)
-            # (the LDS-staged form adds one v_bitop3 per group and block in NONE: 5.625)
+            # (the LDS-staged form adds one v_bitop3 per group and block in NONE: 5.625; in MIN-MAX it
+            # drops the OR-accumulate when group 0 settled the first non-match, MSH_PAIR_NOAX: 5.5)
             lds = "pair_lds" in e.get("kernel", "")
-            per_word = 6.5 if mode == "pair_minmax" else (5.625 if lds else 5.5)
+            per_word = (5.5 if lds else 6.5) if mode == "pair_minmax" else (5.625 if lds else 5.5)
             e["scan_model_share"] = per_word * WORDS * (-(-P // 64)) * nb / e["SQ_INSTS_VALU"]
     if "SQ_WAVE_CYCLES" in e:
         for k in ("SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):
