@@ -72,9 +72,10 @@ for mode, prefix, tags, nb in (
             # half an AND3 of two words' dm' = 5.5 VALU (NONE); MIN-MAX adds one OR-accumulate of the
             # feasible non-matches (6.5)
             # (the LDS-staged form adds one v_bitop3 per group and block in NONE: 5.625; in MIN-MAX it
-            # drops the OR-accumulate when group 0 settled the first non-match, MSH_PAIR_NOAX: 5.5)
+            # drops the OR-accumulate when group 0 settled the first non-match, MSH_PAIR_NOAX, and with
+            # tolerates compaction 7 of a workgroup's 8 blocks fold X into the first compare: 4.625)
             lds = "pair_lds" in e.get("kernel", "")
-            per_word = (5.5 if lds else 6.5) if mode == "pair_minmax" else (5.625 if lds else 5.5)
+            per_word = (4.625 if lds else 6.5) if mode == "pair_minmax" else (5.625 if lds else 5.5)
             e["scan_model_share"] = per_word * WORDS * (-(-P // 64)) * nb / e["SQ_INSTS_VALU"]
     if "SQ_WAVE_CYCLES" in e:
         for k in ("SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):
