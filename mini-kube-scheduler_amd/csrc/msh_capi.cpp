@@ -749,7 +749,7 @@ bool read_knobs(msh::DeviceInfo& d, std::string* err) {
                   knob("MSH_PAIR_PLANES", {{"auto", 0}, {"sgpr", 1}, {"lds", 2}}, &d.pair_planes, err) &&
                   knob("MSH_PAIR_LDS_BPW", {{"2", 2}, {"1", 1}, {"3", 3}, {"4", 4}}, &d.pair_lds_bpw, err) &&
                   knob("MSH_PAIR_COMPACT", {{"auto", -1}, {"0", 0}, {"1", 1}}, &d.pair_compact, err) &&
-                  knob("MSH_PAIR_HYBRID", {{"auto", -1}, {"1", 1}, {"0", 0}, {"2", 2}, {"3", 3}, {"4", 4}}, &d.pair_hybrid, err) &&
+                  knob("MSH_PAIR_HYBRID", {{"auto", -1}, {"1", 1}, {"0", 0}, {"2", 2}}, &d.pair_hybrid, err) &&
                   knob("MSH_PAIR_NOAX", {{"auto", -1}, {"1", 1}, {"0", 0}}, &d.pair_noax, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;

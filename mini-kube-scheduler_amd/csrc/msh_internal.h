@@ -61,7 +61,8 @@ struct DeviceInfo {
   int pair_compact = -1;
   // MSH_PAIR_HYBRID: the LDS-staged form reads a full group's X and D3 planes by scalar loads and
   // D0-D2 from LDS, 6 broadcast reads per group instead of 10 (1: per group, one wait each; 2: both
-  // groups of a step under one wait; 3: D2 too from SGPRs, slower; 4: compiler-scheduled loads; 0: off). -1 = auto: 1 for the
+  // groups of a step under one wait; 0: off; A/B builds with D2 too from SGPRs, or compiler-
+  // scheduled loads, measured slower / the same). -1 = auto: 1 for the
   // identity-like modes (81.1 against 86.1 us per 32-batch C3 launch), 2 for REVERSE / MINMAX (87.9
   // against 90.7 with 1), profiles/r4_ab_pair_planes.txt
   int pair_hybrid = -1;

@@ -711,43 +711,6 @@ __device__ __forceinline__ void pair_group_hy(const uint32_t (&pl)[PLANE_N][PLAN
   }
 }
 
-// pair_group_hy with D2 too from SGPRs (HY 3: 4 LDS reads per group, three of a word's five v_bitop3
-// with an SGPR operand).
-template <bool KX, int TY>
-__device__ __forceinline__ void pair_group_hy3(const uint32_t (&pl)[PLANE_N][PLANE_GW], const u32x8& X,
-                                               const u32x8& D2, const u32x8& D3, uint32_t P0, uint32_t P1,
-                                               uint32_t P2, uint32_t P3, uint32_t nT, uint32_t& am, uint32_t& ax) {
-#pragma unroll
-  for (int w = 0; w < PLANE_GW; w += 2) {
-    uint32_t t[2], xi[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ww = w + h;
-      uint32_t u;
-      if constexpr (TY == 0) {
-        u = bop3_or_xor(X[ww], pl[0][ww], P0);
-      } else if constexpr (TY == 1) {
-        u = pl[0][ww] ^ P0;
-      } else {
-        xi[h] = __builtin_amdgcn_bitop3_b32(X[ww], nT, nT, 0xc0);  // X & nT
-        u = bop3_or_xor(xi[h], pl[0][ww], P0);
-      }
-      u = bop3_or_xor(u, pl[1][ww], P1);
-      u = bop3_or_xor(u, D2[ww], P2);
-      t[h] = bop3_or_xor(u, D3[ww], P3);
-    }
-    am = bop3_and3(am, t[0], t[1]);
-    if constexpr (KX) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if constexpr (TY == 0) ax = bop3_or_andn(ax, t[h], X[w + h]);
-        else if constexpr (TY == 1) ax |= t[h];
-        else ax = bop3_or_andn(ax, t[h], xi[h]);
-      }
-    }
-  }
-}
-
 // The lane's first feasible node in group g (identity-like modes), NOFIT if none.
 __device__ __forceinline__ uint32_t group_first_feasible_v(const uint32_t (&pl)[PLANE_N][PLANE_GW], uint32_t g,
                                                            uint32_t nT) {
@@ -957,35 +920,11 @@ __device__ __forceinline__ void pair_lds_body(PairArgs a) {
         const int32_t gg = h == 0 ? g : g - 1;
         if (h == 1 && gg <= 0) break;
         uint32_t pl[PLANE_N][PLANE_GW];
-        if (HY == 3 && gg < g_full) {
-          u32x8 sp[3];  // X, D2, D3
-          asm volatile("s_load_dwordx8 %0, %3, %4\n\ts_load_dwordx8 %1, %3, %5\n\ts_load_dwordx8 %2, %3, %6\n\t"
-                       "s_waitcnt lgkmcnt(0)"
-                       : "=&s"(sp[0]), "=&s"(sp[1]), "=&s"(sp[2])
-                       : "s"(a.planes + (size_t)gg * GROUP_DWORDS), "n"(PLANE_X * PLANE_GW * 4), "n"(2 * PLANE_GW * 4),
-                         "n"(3 * PLANE_GW * 4));
-          lds_group<2>(pl, s_tab, gg);
-#pragma unroll
-          for (int b = 0; b < PL_BPW; ++b) {
-            if (ty[b] == 0) pair_group_hy3<KXS, 0>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-            else if (ty[b] == 1) pair_group_hy3<KXS, 1>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-            else pair_group_hy3<KXS, 2>(pl, sp[0], sp[1], sp[2], P0[b], P1[b], P2[b], P3[b], nT[b], am[b], ax[b]);
-          }
-          if constexpr (!KX && !NOAX) {
-            const uint32_t axg = sp[0][0] & sp[0][1] & sp[0][2] & sp[0][3] & sp[0][4] & sp[0][5] & sp[0][6] & sp[0][7];
-#pragma unroll
-            for (int b = 0; b < PL_BPW; ++b) ax[b] = bop3_and3(ax[b], nT[b], axg);
-          }
-        } else if (HY && gg < g_full) {
+        if (HY && gg < g_full) {
           u32x8 sp[2];  // X, D3
           if constexpr (HY == 2) {
             sp[0] = spp[h][0];
             sp[1] = spp[h][1];
-          } else if constexpr (HY == 4) {  // compiler-scheduled scalar loads (constant address space)
-            const __attribute__((address_space(4))) u32x8* q =
-                (const __attribute__((address_space(4))) u32x8*)(a.planes + (size_t)gg * GROUP_DWORDS);
-            sp[0] = q[PLANE_X];
-            sp[1] = q[3];
           } else {
             asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
                          : "=&s"(sp[0]), "=&s"(sp[1])
@@ -2503,26 +2442,24 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
     const size_t bytes = (size_t)a.n_groups * GROUP_DWORDS * sizeof(uint32_t);
     const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(w * WAVE);
     const bool cmp = dev.pair_compact < 0 ? KX : dev.pair_compact != 0;
-    const int hy = dev.pair_hybrid >= 0 && dev.pair_hybrid <= 4 ? dev.pair_hybrid : (KX ? 2 : 1);
+    const int hy = dev.pair_hybrid >= 0 && dev.pair_hybrid <= 2 ? dev.pair_hybrid : (KX ? 2 : 1);
     a.noax = dev.pair_noax >= 0 ? dev.pair_noax : (KX ? 1 : 0);
     // (bpw, compaction, hybrid) -> instance: 1 block per wave in the plain LDS form only
     using PairKernel = void (*)(PairArgs);
+    // (bpw, compaction, hybrid) -> instance: 1, 3 and 4 blocks per wave in the plain LDS form only (with
+    // hybrid planes they measured slower, profiles/r4_ab_pair_planes.txt)
     auto pick = [&](auto bpw_c, auto w_c) -> PairKernel {
       constexpr int B = decltype(bpw_c)::value, WW = decltype(w_c)::value;
-      if constexpr (B == 1) {
+      if constexpr (B != 2) {
         return pair_lds_kernel<SHARD, KX, B, WW>;
       } else {
-        const PairKernel t[2][5] = {
+        const PairKernel t[2][3] = {
             {pair_lds_kernel<SHARD, KX, B, WW, false, 0>,
              pair_lds_kernel<SHARD, KX, B, WW, false, 1>,
-             pair_lds_kernel<SHARD, KX, B, WW, false, 2>,
-             pair_lds_kernel<SHARD, KX, B, WW, false, 3>,
-             pair_lds_kernel<SHARD, KX, B, WW, false, 4>},
+             pair_lds_kernel<SHARD, KX, B, WW, false, 2>},
             {pair_lds_kernel<SHARD, KX, B, WW, true, 0>,
              pair_lds_kernel<SHARD, KX, B, WW, true, 1>,
-             pair_lds_kernel<SHARD, KX, B, WW, true, 2>,
-             pair_lds_kernel<SHARD, KX, B, WW, true, 3>,
-             pair_lds_kernel<SHARD, KX, B, WW, true, 4>}};
+             pair_lds_kernel<SHARD, KX, B, WW, true, 2>}};
         return t[cmp ? 1 : 0][hy];
       }
     };

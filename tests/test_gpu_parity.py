@@ -41,13 +41,13 @@ def _set(ctx, msh, ps):
 
 
 def _pair_env(monkeypatch, spec):
-    """Pair-kernel A/B switches from a spec "planes[-compact][-hybrid|-hybrid2|-hybrid3]" (planes: sgpr,
-    lds or auto; hybrid2: both groups' scalar planes of a step loaded under one wait; hybrid3: D2 too
-    from SGPRs; hybrid4: compiler-scheduled scalar loads; noax / axlast: MSH_PAIR_NOAX 1 / 0, else auto)."""
+    """Pair-kernel A/B switches from a spec "planes[-compact][-hybrid|-hybrid2][-noax|-axlast]" (planes:
+    sgpr, lds or auto; hybrid2: both groups' scalar planes of a step loaded under one wait; noax /
+    axlast: MSH_PAIR_NOAX 1 / 0, else auto)."""
     parts = spec.split("-")
     monkeypatch.setenv("MSH_PAIR_PLANES", parts[0])
     monkeypatch.setenv("MSH_PAIR_COMPACT", "1" if "compact" in parts else "0")
-    hy = {"hybrid": "1", "hybrid2": "2", "hybrid3": "3", "hybrid4": "4"}
+    hy = {"hybrid": "1", "hybrid2": "2"}
     monkeypatch.setenv("MSH_PAIR_HYBRID", next((hy[x] for x in parts if x in hy), "0"))
     # noax: group 0 first, the non-match / feasible reduction dropped when it settles it; axlast: never
     monkeypatch.setenv("MSH_PAIR_NOAX", "1" if "noax" in parts else "0" if "axlast" in parts else "auto")
@@ -809,9 +809,8 @@ def test_multi_batch_age_shares(msh, oracle, n, norm, monkeypatch):
 
 
 @pytest.mark.parametrize("bpw", ["1", "2", "3", "4", "2-compact", "2-hybrid", "2-compact-hybrid", "2-hybrid2",
-                                 "2-compact-hybrid2", "3-hybrid", "3-compact-hybrid2", "4-hybrid2", "2-hybrid3",
-                                 "2-compact-hybrid3", "3-hybrid3", "2-hybrid4", "2-compact-hybrid4",
-                                 "2-hybrid-noax", "2-compact-hybrid2-axlast", "1-noax"])
+                                 "2-compact-hybrid2", "2-hybrid-noax", "2-compact-hybrid2-axlast", "1-noax",
+                                 "3-noax", "4-axlast"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("nb", [1, 9, 33])
 def test_multi_batch_launch_lds(msh, oracle, norm, nb, bpw, monkeypatch):
@@ -857,7 +856,7 @@ def test_multi_batch_invalid(msh, gpu_ctx):
 
 
 @pytest.mark.parametrize("planes", ["sgpr", "lds", "lds-compact", "lds-compact-hybrid", "lds-hybrid2",
-                                    "lds-hybrid3", "lds-hybrid4", "lds-hybrid-noax", "lds-compact-hybrid2-axlast"])
+                                    "lds-hybrid-noax", "lds-compact-hybrid2-axlast"])
 @pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 32_768, 70_000, 106_496, 106_497])
 def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
     """pair_kernel re-reads the first group with a hit from memory when it lies above the lowest group
@@ -898,8 +897,7 @@ def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
 
 @pytest.mark.parametrize("planes,slices", [("sgpr", 0), ("sgpr", 1), ("sgpr", 2), ("sgpr", 4), ("lds", 0),
                                            ("lds-compact", 0), ("lds-hybrid", 0), ("lds-compact-hybrid", 0),
-                                           ("lds-hybrid2", 0), ("lds-compact-hybrid2", 0), ("lds-hybrid3", 0),
-                                           ("lds-compact-hybrid3", 0), ("lds-hybrid4", 0), ("lds-compact-hybrid4", 0),
+                                           ("lds-hybrid2", 0), ("lds-compact-hybrid2", 0),
                                            ("lds-hybrid-noax", 0), ("lds-compact-hybrid2-axlast", 0)])
 @pytest.mark.parametrize("n", [1000, 5000, 20_000])
 def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices, monkeypatch):
