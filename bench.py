@@ -52,7 +52,7 @@ METRIC = "pod-node evals/sec + pods placed/sec at 5k nodes, 1/2/4/8 MI355X"
 CLOCK_HZ = 2.4e9                   # MI355X_MICROARCH.md: max clock
 HBM_PEAK = 8.0e12                  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 LANES_PER_SIMD_CYCLE = 32          # MI355X_MICROARCH.md: SIMD-32, a wave64 VALU instruction over 2 cycles
-# pair_kernel's scan (msh_kernels.hip): per 32-node word and 64-pod wave, v_bitop3 (X & nT) + 4 v_bitop3
+# pair_kernel's scan (msh_pair.hip): per 32-node word and 64-pod wave, v_bitop3 (X & nT) + 4 v_bitop3
 # (the code-bit mismatches ORed in: dm') and half a v_bitop3 AND3 (two words' dm' into the group's match
 # flag): 5.5 VALU per 32 x 64 pairs in the identity-like modes (NONE, DEFAULT); REVERSE / MINMAX add one
 # v_bitop3 OR-accumulate of the feasible non-matches: 6.5
@@ -61,34 +61,41 @@ PAIR_VALU_PER_WORD_KX = 6.5
 # the LDS-staged form (pair_lds_kernel) tracks its first feasible node per lane: one v_bitop3 per
 # group and block (nT & the scalar AND of the group's X words), 5.5 + 1/8 per word in NONE
 PAIR_VALU_PER_WORD_LDS = 5.625
+# REVERSE / MINMAX in the LDS-staged form: group 0 scanned first settles the first feasible non-match for
+# nearly every wave, so the other groups drop that reduction (5.5), and with the tolerates compaction 7
+# of a workgroup's 8 pod blocks fold X & nT into the first code compare (4.625)
+PAIR_VALU_PER_WORD_LDS_KX = 4.625
 # generic_kernel's main sweep on the reference list (NodeNumber only): per pair v_cmp_eq (suffix
 # digits), 2 v_cndmask (the lane's two weighted values), v_cmp_gt_i64 (strict first max), 3 v_cndmask
 # (best total, chunk-relative index): 7 VALU lane-ops per pair
 GEN_VALU_PER_PAIR_REF = 7.0
-WGP_MAX_GROUPS = 32                # msh_kernels.hip: the class-row kernel's table limit (groups of 256 nodes)
-PAIR_LDS_MAX_GROUPS = 128          # msh_kernels.hip: tables the LDS-staged pair kernel takes (4-wave workgroups)
+PAIR_LDS_MAX_GROUPS = 128          # msh_pair.hip: tables the LDS-staged pair kernel takes (4-wave workgroups)
 PAIR_LDS_BIG_GROUPS = 416          # ... and with 16-wave workgroups
-PMC_FILE = ROOT / "profiles" / "r4_pmc_c3.json"
+PMC_FILE = ROOT / "profiles" / "r5_pmc_c3.json"
+# The headline plugin set (BASELINE C3: "nodenumber prescore/score + weighted NormalizeScore"): the
+# reference's filter and prescore lists, NodeNumber scored at weight 3 with upstream's
+# helper.DefaultNormalizeScore (MaxNodeScore 100) as its NormalizeScore. The reference itself has no
+# weight (minisched.go:187 "TODO: plugin weight") and no ScoreExtensions (nodenumber.go:98-100): its
+# w = 1 / no-normalizer list is timed beside it (extras "reference_weight1_none").
+HEADLINE_WEIGHT = 3
+HEADLINE_NORM = 1  # msh_normalize: MSH_NORMALIZE_DEFAULT
+NORM_NAMES = {0: "none", 1: "DefaultNormalizeScore", 2: "DefaultNormalizeScore(reverse)", 3: "min-max"}
 VALU_PEAK_FILE = ROOT / "profiles" / "r4_ubench_valu.json"
 
 
 def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, shard: bool = False,
-                       multi: bool = False, nb: int = 1, classrows: bool = False) -> str:
-    """The kernel msh_capi.cpp dispatches for a launch of nb batches of n_pods: pair_kernel<S, SHARD, KX>,
-    S the slice waves per 64-pod block (msh_kernels.hip pair_slices), KX for REVERSE / MINMAX, or the
-    opt-in class-row kernel wgp_kernel<4, KX> (tables up to WGP_MAX_GROUPS groups)."""
+                       multi: bool = False, nb: int = 1) -> str:
+    """The kernel msh_capi.cpp dispatches for a launch of nb batches of n_pods (msh_pair.hip
+    launch_pair_t): pair_lds_kernel<SHARD, KX, W> (planes staged in LDS, W waves per workgroup) when the
+    launch fills the chip, else pair_kernel<S, SHARD, KX> (S slice waves per 64-pod block); KX for
+    REVERSE / MINMAX."""
     b = lambda v: str(v).lower()
     groups = max(-(-n_nodes // 1024) * 1024, 1024) // 256
-    if classrows and groups <= WGP_MAX_GROUPS and not shard:
-        return f"void msh::wgp_kernel<4, {b(kx)}>"
     waves = -(-n_pods // 64) * (nb if multi else 1)
-    # the LDS-staged form: <SHARD, KX, blocks per wave, waves per workgroup, compact (auto: KX),
-    # hybrid planes (auto: 2 for KX, else 1)>
-    hy = 2 if kx else 1
-    if groups <= PAIR_LDS_MAX_GROUPS and waves >= cus * 4 * 4 * 4:
-        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2, 4, {b(kx)}, {hy}>"
+    if groups <= PAIR_LDS_MAX_GROUPS and waves >= cus * 64:
+        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 4>"
     if PAIR_LDS_MAX_GROUPS < groups <= PAIR_LDS_BIG_GROUPS and waves >= cus * 2 * 16:  # 16-wave workgroups
-        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 2, 16, {b(kx)}, {hy}>"
+        return f"void msh::pair_lds_kernel<{b(shard)}, {b(kx)}, 16>"
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2
@@ -204,7 +211,8 @@ def main():
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
 
     ctx = msh.DeviceContext(local)
-    ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+    ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                    [msh.ScorePluginConfig(msh.NODE_NUMBER, HEADLINE_WEIGHT, msh.Normalize(HEADLINE_NORM))])
     unsched, node_digit = synth.make_nodes(n_total)[1:]
     G = msh._native.BATCHES_PER_LAUNCH  # batches per msh_schedule_batches_device launch
     multi = mode == "batch" and args.submit == "multi"
@@ -336,7 +344,7 @@ def main():
     if rank == 0 and not args.no_check:
         ok = True
         for (pod_digit, pod_tol), b in zip(batches, bufs):
-            want = closed_form_modes(unsched, node_digit, pod_digit, pod_tol)
+            want = closed_form_modes(unsched, node_digit, pod_digit, pod_tol, HEADLINE_WEIGHT, HEADLINE_NORM)
             got = (b["idx"].cpu().numpy(), b["score"].cpu().numpy(), b["status"].cpu().numpy())
             ok = ok and all((g == w).all() for g, w in zip(got, want))
         check = "bit-exact vs closed form" if ok else "MISMATCH"
@@ -385,7 +393,8 @@ def main():
             "dtype": "u32 (bit-sliced: 32 pod-node pairs per lane-op)",
             "data": "synthetic (splitmix64 seed 0x6d696e69: 10% unschedulable nodes, 1% non-digit pods, 5% tolerating)",
             "config": {"workload": wl, "nodes": n_total, "pods_per_step": int(p if mode != "nodeshard" else p_total),
-                       "plugins": "filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber w=1]",
+                       "plugins": (f"filter=[NodeUnschedulable] prescore=[NodeNumber] score=[NodeNumber "
+                                   f"w={HEADLINE_WEIGHT} normalize={NORM_NAMES[HEADLINE_NORM]}]"),
                        "parallelism": f"{'pod' if mode != 'nodeshard' else 'node'}-sharded x{world}",
                        "streams": 1, "submit": (f"multi ({G} batches per launch)" if multi else "single") if mode == "batch"
                        else "per step",
@@ -411,12 +420,17 @@ def load_valu_peak():
     return d.get("vgpr_only_max"), d
 
 
-def pmc_entry(key: str, kname: str, n_local: int, p: int, nb: int):
-    """The profiles/r4_pmc_c3.json entry for this kernel, size and batch count (None if it does not
-    match what this run timed)."""
+def plugin_tag(weight: int, norm: int) -> str:
+    """The NodeNumber score entry as profiles/r5_pmc_c3.json records it (scripts/run_batch.py)."""
+    return f"NodeNumber w={weight} norm={norm}"
+
+
+def pmc_entry(key: str, kname: str, n_local: int, p: int, nb: int, plugins: str | None = None):
+    """The profiles/r5_pmc_c3.json entry for this kernel, size, batch count and plugin list (None if
+    it does not match what this run timed)."""
     e = (load_json(PMC_FILE) or {}).get("kernels", {}).get(key, {})
     ok = (e.get("kernel") == kname and e.get("nodes") == n_local and e.get("pods") == p
-          and e.get("batches_per_launch", 1) == nb)
+          and e.get("batches_per_launch", 1) == nb and (plugins is None or e.get("plugins") == plugins))
     return e if ok else None
 
 
@@ -439,8 +453,10 @@ def valu_roofline(kname, launch_ms, evals, model_lane_ops_per_eval, cus, entry, 
         "peak": peak / 1e9,
         "unit": "Glane-op/s",
         "frac": model / launch_s / peak,
-        "traffic": entry.get("hbm_bytes_per_launch") if entry else None,
-        "traffic_note": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024), same kernel, size and batches",
+        "traffic": entry.get("hbm_bytes_per_launch_fetch_x2") if entry else None,
+        "traffic_note": ("rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch (KiB x 1024; FETCH_SIZE doubled as "
+                         "MI355X_MICROARCH.md's HBM section prescribes for gfx950), same kernel, size, batches "
+                         "and plugin list, separate --pmc passes"),
         "kernel": kname,
         "kernel_ms": launch_ms,
         "kernel_ms_note": ("mean duration of R back-to-back launches, each timed from the kernel's own start "
@@ -494,10 +510,12 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
     lds = "pair_lds_kernel" in kname
     per_word = PAIR_VALU_PER_WORD_LDS if lds else PAIR_VALU_PER_WORD
     model_per_eval = per_word * (n_pad / 32) * (-(-p // 64) * 64) / (float(n_local) * p)
-    entry = pmc_entry("pair_multi" if nb > 1 else "pair_single", kname, n_local, p, nb)
+    entry = pmc_entry("pair_multi" if nb > 1 else "pair_single", kname, n_local, p, nb,
+                      plugin_tag(HEADLINE_WEIGHT, HEADLINE_NORM))
     out = valu_roofline(kname, launch_ms, evals, model_per_eval, cus, entry,
                         f"{per_word} VALU per 32-node word and 64-pod wave ({kname.split('<')[0][10:]}'s scan, "
-                        "msh_kernels.hip, NONE normalize): per lane-op 32 (pod, node) pairs get NodeUnschedulable's "
+                        "msh_pair.hip, the identity-like normalize modes: NONE, DefaultNormalizeScore): per "
+                        "lane-op 32 (pod, node) pairs get NodeUnschedulable's "
                         f"verdict and NodeNumber's digit compare; lane-ops per eval = {per_word} x padded words x "
                         "padded pods / (n x p)")
     out["batches_per_launch"] = nb
@@ -546,9 +564,12 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         if kernel:
             os.environ["MSH_BATCH_KERNEL"] = kernel  # read once by msh_create
         try:
-            return msh.DeviceContext(dev.index or 0)
+            c = msh.DeviceContext(dev.index or 0)
         finally:
             os.environ.pop("MSH_BATCH_KERNEL", None)
+        c.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                      [msh.ScorePluginConfig(msh.NODE_NUMBER, HEADLINE_WEIGHT, msh.Normalize(HEADLINE_NORM))])
+        return c
 
     S2 = Streams(torch, dev, 2)
     sh = torch.cuda.current_stream(dev).cuda_stream
@@ -572,17 +593,30 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
 
     ctx = new_ctx()
     ctx.upload_nodes(u, nd)
+    # the other NormalizeScore modes and the reference's own list (w = 1, no normalizer) on the same
+    # 32-batch launches as the headline, each with its VALU roofline (the counter form from its own
+    # profiles/r5_pmc_c3.json entry)
     variants = {}
-    for name, weight, norm in (("weight3_default_normalize", 3, 1), ("minmax_normalize", 1, 3),
-                               ("reverse_normalize", 1, 2)):
+    for name, key, weight, norm in (("reference_weight1_none", "pair_multi_ref", 1, 0),
+                                    ("minmax_weight3", "pair_minmax", 3, 3),
+                                    ("reverse_weight3", "pair_reverse", 3, 2)):
         ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                         [msh.ScorePluginConfig(msh.NODE_NUMBER, weight, msh.Normalize(norm))])
         ms = run_multi(ctx)
-        variants[name] = {"kernel": batch_kernel_label(n, p, cus, kx=norm in (2, 3), multi=True, nb=G), "kernel_ms": ms,
+        kx = norm in (2, 3)
+        kname = batch_kernel_label(n, p, cus, kx=kx, multi=True, nb=G)
+        per_word = PAIR_VALU_PER_WORD_LDS_KX if kx else PAIR_VALU_PER_WORD_LDS
+        model = per_word * (-(-n // 1024) * 1024 / 32) * (-(-p // 64) * 64) / (float(n) * p)
+        rl = valu_roofline(kname, ms, float(n) * p * G, model, cus, pmc_entry(key, kname, n, p, G, plugin_tag(weight, norm)),
+                           f"{per_word} VALU per 32-node word and 64-pod wave (pair_lds_kernel's scan in this mode)")
+        variants[name] = {"plugins": f"score=[NodeNumber w={weight} normalize={NORM_NAMES[norm]}]",
+                          "kernel": kname, "kernel_ms": ms,
                           "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
-                          "check": "bit-exact vs closed form" if check_all(weight, norm) else "MISMATCH"}
-    out["c3_normalize_variants"] = variants
-    ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+                          "check": "bit-exact vs closed form" if check_all(weight, norm) else "MISMATCH",
+                          "roofline": rl}
+    out["c3_plugin_variants"] = variants
+    ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                    [msh.ScorePluginConfig(msh.NODE_NUMBER, HEADLINE_WEIGHT, msh.Normalize(HEADLINE_NORM))])
 
     # ---- generic_kernel: an explicit int64 score per (pod, node) pair (north_star's five stages) ----
     gen = {}
@@ -590,7 +624,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     gctx.upload_nodes(u, nd)
     gctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
     ms = run_multi(gctx, R=5)
-    kname = "void msh::generic_kernel<1, 0, 0>"
+    kname = "void msh::generic_kernel<0, false, false, 0, false>"
     rl = valu_roofline(kname, ms, float(n) * p * G, GEN_VALU_PER_PAIR_REF, cus,
                        pmc_entry("generic_ref", kname, n, p, G),
                        "7 VALU per pair (generic_kernel's main sweep, NodeNumber only: v_cmp_eq, 2 v_cndmask for "
@@ -608,7 +642,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     ok = all(same(tuple(x[sample] for x in got(b)),
                   direct_plugins(u, nd, pp[0][sample], pp[1][sample], plugins, {0: col}))
              for b, pp in list(zip(bufs, pods))[:2])
-    kname = "void msh::generic_kernel<1, 1, 0>"
+    kname = "void msh::generic_kernel<0, false, false, 1, false>"
     entry = pmc_entry("generic_col", kname, n, p, G)
     gen["nodenumber_plus_default_column"] = {
         "kernel": kname, "plugins": "score=[NodeNumber w=1, ScoreColumn0 w=2 DefaultNormalizeScore]",
@@ -618,32 +652,9 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     out["generic"] = gen
     gctx.close()
 
-    # ---- the opt-in class-row kernel: reported apart, its pods/s (not a per-pair evaluation) ----
-    cctx = new_ctx("classrows")
-    cctx.upload_nodes(u, nd)
-    ms = run_multi(cctx)
-    ok = check_all()
-    cctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
-                     [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(3))])
-    ms_mm = run_multi(cctx)
-    ok_mm = check_all(1, 3)
-    out["classrows_opt_in"] = {
-        "kernel": batch_kernel_label(n, p, cus, multi=True, nb=G, classrows=True), "kernel_ms": ms,
-        "batches_per_launch": G, "ms_per_batch": ms / G, "pods_per_s": p * G / (ms * 1e-3),
-        "check": "bit-exact vs closed form" if ok else "MISMATCH",
-        "minmax": {"kernel": batch_kernel_label(n, p, cus, kx=True, multi=True, nb=G, classrows=True),
-                   "kernel_ms": ms_mm, "pods_per_s": p * G / (ms_mm * 1e-3),
-                   "check": "bit-exact vs closed form" if ok_mm else "MISMATCH",
-                   "grid": "workgroups per CU from hipOccupancyMaxActiveBlocksPerMultiprocessor"},
-        "note": "MSH_BATCH_KERNEL=classrows: each pod's verdicts are read from per-(tolerates, digit)-class "
-                "tables built at upload, so its per-pod work does not evaluate the pairs; a placement rate "
-                "of a class-specialised path, never the headline evals/s"}
-    cctx.close()
-    del bufs
-
     # ---- e2e: the host-buffer C-ABI call (msh_schedule_batch), PCIe in and out ----
     pd, pt = pods[0]
-    want = closed_form_modes(u, nd, pd, pt)
+    want = closed_form_modes(u, nd, pd, pt, HEADLINE_WEIGHT, HEADLINE_NORM)
     hpd, hpt = msh.pinned_empty(p, np.int8), msh.pinned_empty(p, np.uint8)
     hpd[:], hpt[:] = pd, pt
     e2e = {}
@@ -692,7 +703,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         if i >= 5:
             ts_pack.append(t1 - t0)
             ts_all.append(t2 - t0)
-    ok = (hpd == pdn).all() and (hpt == ptn).all() and same(outs, closed_form_modes(u, nd, pdn, ptn))
+    ok = (hpd == pdn).all() and (hpt == ptn).all() and same(outs, closed_form_modes(u, nd, pdn, ptn, HEADLINE_WEIGHT, HEADLINE_NORM))
     e2e["pinned_with_pack"] = {"us_per_batch": float(np.median(ts_all)) * 1e6,
                                "pack_us": float(np.median(ts_pack)) * 1e6,
                                "check": "packed columns == generator, outputs bit-exact vs closed form" if ok
@@ -724,7 +735,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         t0 = time.perf_counter()
         pipelined(40)
         ts.append((time.perf_counter() - t0) / 40)
-    want_n = closed_form_modes(u, nd, pdn, ptn)
+    want_n = closed_form_modes(u, nd, pdn, ptn, HEADLINE_WEIGHT, HEADLINE_NORM)
     ok = all((spd == pdn).all() and (spt == ptn).all() and same(o, want_n) for spd, spt, o in sets)
     e2e["pinned_with_pack_pipelined"] = {
         "us_per_batch": float(np.median(ts)) * 1e6, "pods_per_s": p / float(np.median(ts)),
@@ -769,7 +780,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     launch = lambda i, sh: ctx.schedule_batch_device(p2, *[t.data_ptr() for t in bs[i % 2]], sh)
     S2.time(launch, 4)
     ms = S2.time(launch, 100)
-    ok = all(same(got(b2), closed_form_modes(u2, nd2, pp[0], pp[1])) for b2, pp in zip(bs, pairs2))
+    ok = all(same(got(b2), closed_form_modes(u2, nd2, pp[0], pp[1], HEADLINE_WEIGHT, HEADLINE_NORM)) for b2, pp in zip(bs, pairs2))
     out["c2"] = {"kernel": batch_kernel_label(n2, p2, cus), "ms_per_step": ms, "evals_per_s": n2 * p2 / (ms * 1e-3),
                  "streams": 2, "check": "bit-exact vs closed form" if ok else "MISMATCH"}
     ctx.close()
@@ -778,7 +789,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     n4, p4 = 100_000, 1_000_000
     u4, nd4 = synth.make_nodes(n4)[1:]
     pd4, pt4 = synth._make_pods_fast(p4, synth.SEED)[1:]
-    want4 = closed_form_modes(u4, nd4, pd4, pt4)
+    want4 = closed_form_modes(u4, nd4, pd4, pt4, HEADLINE_WEIGHT, HEADLINE_NORM)
     ctx = new_ctx()
     ctx.upload_nodes(u4, nd4)
     b4 = dbufs(pd4, pt4)
@@ -833,6 +844,7 @@ def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode:
     same workload: pods in chunks against the full node table until the budget is spent."""
     importlib.import_module("oracle.build").build_oracle()
     O = importlib.import_module("oracle.oracle")
+    plugins = O.PluginSet(weights=[HEADLINE_WEIGHT], normalize=[HEADLINE_NORM])  # the headline list
     n = len(unsched)
     p = len(pod_digit)
     chunk = min(2000 * threads, p)
@@ -842,9 +854,9 @@ def cpu_baseline(unsched, node_digit, pod_digit, pod_tol, budget_s: float, mode:
         sl = slice(pos, min(pos + chunk, p))
         t0 = time.perf_counter()
         if mode == "sequential":
-            O.c_schedule_sequential(unsched, node_digit, pod_digit[sl], pod_tol[sl])
+            O.c_schedule_sequential(unsched, node_digit, pod_digit[sl], pod_tol[sl], plugins)
         else:
-            O.c_schedule_batch(unsched, node_digit, pod_digit[sl], pod_tol[sl], threads=threads)
+            O.c_schedule_batch(unsched, node_digit, pod_digit[sl], pod_tol[sl], plugins, threads=threads)
         t += time.perf_counter() - t0
         done += sl.stop - sl.start
         pos = 0 if sl.stop >= p else sl.stop

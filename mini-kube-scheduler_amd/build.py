@@ -23,12 +23,15 @@ INCLUDE = REPO / "include"
 ARCH = os.environ.get("MSH_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [
-    # (source, compiler, extra flags)
-    ("msh_kernels.hip", "hipcc", ["-x", "hip"]),
+    # (source, compiler, extra flags): one translation unit per kernel family, compiled in parallel
+    ("msh_pair.hip", "hipcc", ["-x", "hip"]),
+    ("msh_generic.hip", "hipcc", ["-x", "hip"]),
+    ("msh_seq.hip", "hipcc", ["-x", "hip"]),
+    ("msh_prep.hip", "hipcc", ["-x", "hip"]),
     ("msh_capi.cpp", "hipcc", []),
     ("msh_pack.cpp", "g++", []),
 ]
-HEADERS = [CSRC / "msh_internal.h", CSRC / "msh_pool.h", INCLUDE / "minisched_hip.h"]
+HEADERS = [CSRC / "msh_internal.h", CSRC / "msh_device.h", CSRC / "msh_pool.h", INCLUDE / "minisched_hip.h"]
 
 
 def _hipcc() -> str:
@@ -57,7 +60,7 @@ def _build_lib(force: bool, verbose: bool) -> None:
     if not force and not _stale(LIB, [CSRC / src for src, _, _ in SOURCES] + HEADERS):
         return  # up to date (objects need not be present, e.g. on the GPU box)
     OBJ.mkdir(exist_ok=True)
-    objs = []
+    objs, jobs = [], []
     for src, cc, extra in SOURCES:
         s = CSRC / src
         o = OBJ / (s.stem + ".o")
@@ -72,7 +75,10 @@ def _build_lib(force: bool, verbose: bool) -> None:
             cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wextra", "-c", str(s), "-o", str(o)]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        jobs.append((src, subprocess.Popen(cmd)))
+    failed = [src for src, pr in jobs if pr.wait() != 0]
+    if failed:
+        raise RuntimeError(f"compile failed: {', '.join(failed)}")
     if force or _stale(LIB, objs):
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
         if verbose:

@@ -79,17 +79,14 @@ void par_copy(const CopyJob* jobs, int n_jobs) {
 // One version of the node-side device tables (List order, padded to cap nodes).
 struct NodeTable {
   size_t cap = 0;
-  uint8_t* d_unsched = nullptr;  // the uploaded columns
+  uint8_t* d_unsched = nullptr;  // the uploaded columns (read by generic_kernel and the export as they are)
   int8_t* d_digit = nullptr;
-  uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout): pair_kernel, seq_kernel
-  uint32_t* d_hrows = nullptr;   // class rows (msh_internal.h HR_* layout): the opt-in class-row kernel
-  uint32_t* d_ball = nullptr;    // [0..1] first feasible node per pod class, as keys
-  uint32_t* d_nrec = nullptr;    // node records (msh_internal.h NREC): generic_kernel
-  // score-column plugins (generic pipeline): GEN_COLS x cap int64, column k valid when col_ok[k], and
-  // the same x 100 as doubles (the normalizing columns' numerators)
+  uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout): pair / seq kernels
+  // score-column plugins (generic pipeline): GEN_COLS x cap int64, column k valid when col_ok[k], with the
+  // range of its values (host side: the generic launch bounds the totals from it)
   int64_t* d_cols = nullptr;
-  double* d_cols100 = nullptr;
   bool col_ok[msh::GEN_COLS] = {};
+  int64_t col_lo[msh::GEN_COLS] = {}, col_hi[msh::GEN_COLS] = {};
   // launches that read this version: one event per caller stream, re-recorded after each launch
   std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
 };
@@ -173,21 +170,13 @@ NodeTable& cur_table(msh_ctx* c) { return c->tab[c->cur]; }
 
 void free_table(NodeTable& t) {
   (void)hipFree(t.d_cols);
-  (void)hipFree(t.d_cols100);
-  (void)hipFree(t.d_nrec);
   (void)hipFree(t.d_unsched);
   (void)hipFree(t.d_digit);
   (void)hipFree(t.d_planes);
-  (void)hipFree(t.d_hrows);
-  (void)hipFree(t.d_ball);
   t.d_cols = nullptr;
-  t.d_cols100 = nullptr;
-  t.d_nrec = nullptr;
   t.d_unsched = nullptr;
   t.d_digit = nullptr;
   t.d_planes = nullptr;
-  t.d_hrows = nullptr;
-  t.d_ball = nullptr;
   for (bool& ok : t.col_ok) ok = false;
   t.cap = 0;
 }
@@ -363,9 +352,6 @@ int ensure_table(msh_ctx* c, NodeTable& t, size_t n_pad) {
   MSH_HIP(c, hipMalloc(&t.d_unsched, n_pad));
   MSH_HIP(c, hipMalloc(&t.d_digit, n_pad));
   MSH_HIP(c, hipMalloc(&t.d_planes, n_pad / msh::GROUP_NODES * msh::GROUP_DWORDS * sizeof(uint32_t)));
-  MSH_HIP(c, hipMalloc(&t.d_hrows, n_pad / msh::GROUP_NODES * msh::HR_GD * sizeof(uint32_t)));
-  MSH_HIP(c, hipMalloc(&t.d_nrec, n_pad * msh::NREC * sizeof(uint32_t)));
-  MSH_HIP(c, hipMalloc(&t.d_ball, 2 * sizeof(uint32_t)));
   t.cap = n_pad;
   return MSH_OK;
 }
@@ -377,10 +363,6 @@ int ensure_cols(msh_ctx* c, NodeTable& t) {
   if (!t.d_cols) {
     MSH_HIP(c, hipMalloc(&t.d_cols, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t)));
     MSH_HIP(c, hipMemsetAsync(t.d_cols, 0, (size_t)msh::GEN_COLS * t.cap * sizeof(int64_t), c->prep_stream));
-  }
-  if (!t.d_cols100) {
-    MSH_HIP(c, hipMalloc(&t.d_cols100, (size_t)msh::GEN_COLS * t.cap * sizeof(double)));
-    MSH_HIP(c, hipMemsetAsync(t.d_cols100, 0, (size_t)msh::GEN_COLS * t.cap * sizeof(double), c->prep_stream));
   }
   return MSH_OK;
 }
@@ -412,20 +394,40 @@ int rewrite(msh_ctx* c, const Rewrite& w) {
   wait_events(dst.readers);
   int rc = ensure_table(c, dst, (size_t)n_pad);
   if (rc != MSH_OK) return rc;
-  // the raw columns: uploaded, or the published ones
-  if (up && n > 0) {
-    if ((rc = node_stage(c, 2 * (size_t)n)) != MSH_OK) return rc;
-    std::memcpy(c->h_nstage, w.unsched, (size_t)n);
-    std::memcpy(c->h_nstage + n, w.digit, (size_t)n);
-    MSH_HIP(c, hipMemcpyAsync(dst.d_unsched, c->h_nstage, (size_t)n, hipMemcpyHostToDevice, ps));
-    MSH_HIP(c, hipMemcpyAsync(dst.d_digit, c->h_nstage + n, (size_t)n, hipMemcpyHostToDevice, ps));
-  } else if (!up && n > 0) {
-    MSH_HIP(c, hipMemcpyAsync(dst.d_unsched, src.d_unsched, (size_t)n, hipMemcpyDeviceToDevice, ps));
-    MSH_HIP(c, hipMemcpyAsync(dst.d_digit, src.d_digit, (size_t)n, hipMemcpyDeviceToDevice, ps));
+  hipError_t e = hipSuccess;
+  // the uploaded columns and the planes: uploaded and prepped, or copied from the published version (a
+  // patch of at most PATCH_INLINE nodes applied on the way, its words' planes rebuilt)
+  const bool inline_patch = w.kind == Rewrite::PATCH && w.patch_count <= msh::PATCH_INLINE;
+  if (up) {
+    if (n > 0) {
+      if ((rc = node_stage(c, 2 * (size_t)n)) != MSH_OK) return rc;
+      std::memcpy(c->h_nstage, w.unsched, (size_t)n);
+      std::memcpy(c->h_nstage + n, w.digit, (size_t)n);
+      MSH_HIP(c, hipMemcpyAsync(dst.d_unsched, c->h_nstage, (size_t)n, hipMemcpyHostToDevice, ps));
+      MSH_HIP(c, hipMemcpyAsync(dst.d_digit, c->h_nstage + n, (size_t)n, hipMemcpyHostToDevice, ps));
+    }
+  } else {
+    msh::TableCopyArgs t{};
+    t.src_unsched = src.d_unsched;
+    t.src_digit = src.d_digit;
+    t.src_planes = src.d_planes;
+    t.dst_unsched = dst.d_unsched;
+    t.dst_digit = dst.d_digit;
+    t.dst_planes = dst.d_planes;
+    t.n = n;
+    t.n_words = n_pad / 32;
+    t.has_nu = c->pp.has_nu_filter;
+    if (inline_patch) {
+      t.count = w.patch_count;
+      std::copy(c->h_patch.begin(), c->h_patch.begin() + w.patch_count, t.inl);
+    }
+    if ((e = msh::launch_table_copy(t, ps)) != hipSuccess) return hip_fail(c, e, "table_copy_kernel");
   }
   // score columns: an upload drops them (they belong to the previous table's nodes)
   for (int k = 0; k < msh::GEN_COLS; ++k) {
     dst.col_ok[k] = !up && src.col_ok[k];
+    dst.col_lo[k] = src.col_lo[k];
+    dst.col_hi[k] = src.col_hi[k];
     if (w.kind == Rewrite::COLUMN && k == w.col) continue;
     if (dst.col_ok[k] && n > 0) {
       if ((rc = ensure_cols(c, dst)) != MSH_OK) return rc;
@@ -435,16 +437,22 @@ int rewrite(msh_ctx* c, const Rewrite& w) {
   }
   if (w.kind == Rewrite::COLUMN) {
     if ((rc = ensure_cols(c, dst)) != MSH_OK) return rc;
+    int64_t lo = 0, hi = 0;
     if (n > 0) {
       const size_t bytes = (size_t)n * sizeof(int64_t);
       if ((rc = node_stage(c, bytes)) != MSH_OK) return rc;
       std::memcpy(c->h_nstage, w.scores, bytes);
       MSH_HIP(c, hipMemcpyAsync(dst.d_cols + (size_t)w.col * dst.cap, c->h_nstage, bytes, hipMemcpyHostToDevice, ps));
+      const auto mm = std::minmax_element(w.scores, w.scores + n);
+      lo = *mm.first;
+      hi = *mm.second;
     }
     dst.col_ok[w.col] = true;
+    dst.col_lo[w.col] = lo;
+    dst.col_hi[w.col] = hi;
   }
-  // patch entries, applied to the copied columns by the prep's reset launch
-  if (w.kind == Rewrite::PATCH) {
+  // a larger patch: its entries scattered into the copied columns, then the full prep below
+  if (w.kind == Rewrite::PATCH && !inline_patch) {
     const size_t pbytes = (size_t)w.patch_count * sizeof(unsigned long long);
     if ((size_t)w.patch_count > c->patch_cap) {
       (void)hipFree(c->d_patch);  // last read by a rewrite that has completed
@@ -457,16 +465,16 @@ int rewrite(msh_ctx* c, const Rewrite& w) {
     if ((rc = node_stage(c, pbytes)) != MSH_OK) return rc;
     std::memcpy(c->h_nstage, c->h_patch.data(), pbytes);
     MSH_HIP(c, hipMemcpyAsync(c->d_patch, c->h_nstage, pbytes, hipMemcpyHostToDevice, ps));
+    if ((e = msh::launch_patch_scatter(c->d_patch, w.patch_count, dst.d_unsched, dst.d_digit, ps)) != hipSuccess)
+      return hip_fail(c, e, "patch_scatter_kernel");
   }
-  hipError_t e = msh::launch_node_prep(dst.d_unsched, dst.d_digit, n, n_pad, c->pp.has_nu_filter, dst.d_ball,
-                                       dst.d_planes, dst.d_hrows, dst.d_nrec, ps, c->d_patch,
-                                       w.kind == Rewrite::PATCH ? w.patch_count : 0);
-  if (e != hipSuccess) return hip_fail(c, e, "node_prep_kernel");
-  uint32_t col_mask = 0;
-  for (int k = 0; k < msh::GEN_COLS; ++k) col_mask |= dst.col_ok[k] ? 1u << k : 0u;
-  if (col_mask && (e = msh::launch_cols100(dst.d_cols, dst.d_cols100, (int64_t)dst.cap, n, n_pad, col_mask, ps)) !=
-                      hipSuccess)
-    return hip_fail(c, e, "cols100_kernel");
+  // the planes: rebuilt whole after an upload, a filter-list change or a large patch; a small patch and a
+  // score column leave the copied (patched) planes as they are
+  if (up || w.kind == Rewrite::REPREP || (w.kind == Rewrite::PATCH && !inline_patch)) {
+    if ((e = msh::launch_node_prep(dst.d_unsched, dst.d_digit, n, n_pad, c->pp.has_nu_filter, dst.d_planes, ps)) !=
+        hipSuccess)
+      return hip_fail(c, e, "node_prep_kernel");
+  }
   // an upload zeroes the sequential-mode counts (after the sequential launches in flight)
   if (up) {
     if ((size_t)n_pad > c->counts_cap) {
@@ -512,17 +520,6 @@ int ready(msh_ctx* c) {
   return MSH_OK;
 }
 
-// The class-row kernel's arguments (MSH_BATCH_KERNEL=classrows).
-msh::BatchArgs classrow_args(msh_ctx* c) {
-  msh::BatchArgs a{};
-  const NodeTable& t = cur_table(c);
-  a.hrows = t.d_hrows;
-  a.n_groups = c->n_pad / msh::GROUP_NODES;
-  a.ball = t.d_ball;
-  a.pp = c->pp;
-  return a;
-}
-
 // pair_kernel's arguments for the current table (the batches are filled in by the caller).
 msh::PairArgs pair_args(msh_ctx* c) {
   msh::PairArgs a{};
@@ -534,12 +531,7 @@ msh::PairArgs pair_args(msh_ctx* c) {
   return a;
 }
 
-// The opt-in class-row kernel serves this table (it holds at most 8,192 nodes).
-bool use_classrows(const msh_ctx* c) {
-  return c->dev.batch_kernel == 1 && msh::classrows_fit(c->n_pad / msh::GROUP_NODES);
-}
-
-// nb batches on the per-pair kernel (or the opt-in class-row kernel), MULTI_MAX per launch.
+// nb batches on the per-pair kernel, MULTI_MAX per launch.
 int launch_generic_descs(msh_ctx* c, const msh::BatchDesc* d, int32_t nb, hipStream_t s);
 bool use_generic(const msh_ctx* c);
 
@@ -548,17 +540,11 @@ int launch_batch_descs(msh_ctx* c, const msh::BatchDesc* d, int32_t nb, hipStrea
   for (int32_t i0 = 0; i0 < nb; i0 += msh::MULTI_MAX) {
     const int n = std::min<int32_t>(msh::MULTI_MAX, nb - i0);
     TimedLaunch tl(c);
-    hipError_t e;
-    if (use_classrows(c)) {
-      e = msh::launch_classrows(classrow_args(c), d + i0, n, c->dev, s);
-      if (e != hipSuccess) return hip_fail(c, e, "wgp_kernel");
-    } else {
-      msh::PairArgs a = pair_args(c);
-      a.nb = n;
-      for (int k = 0; k < n; ++k) a.d[k] = d[i0 + k];
-      e = msh::launch_pairs(a, false, c->dev, s);
-      if (e != hipSuccess) return hip_fail(c, e, "pair_kernel");
-    }
+    msh::PairArgs a = pair_args(c);
+    a.nb = n;
+    for (int k = 0; k < n; ++k) a.d[k] = d[i0 + k];
+    const hipError_t e = msh::launch_pairs(a, false, c->dev, s);
+    if (e != hipSuccess) return hip_fail(c, e, "pair_kernel");
   }
   return MSH_OK;
 }
@@ -567,33 +553,63 @@ int launch_batch_descs(msh_ctx* c, const msh::BatchDesc* d, int32_t nb, hipStrea
 // for every list with MSH_BATCH_KERNEL=generic, an A/B switch).
 bool use_generic(const msh_ctx* c) { return c->generic || c->dev.batch_kernel == 2; }
 
+// The largest |NormalizeScore(raw)| one plugin can give a feasible pair: NodeNumber's raw
+// scores are 0 / 10; a column's raw scores lie in [lo, hi] (its upload). DefaultNormalizeScore gives
+// 100 raw / m with m = the largest feasible raw (raw unchanged when m <= 0); reverse 100 - that;
+// min-max [0, 100].
+long double score_bound(bool column, int32_t mode, int64_t lo, int64_t hi) {
+  const long double alo = lo < 0 ? -(long double)lo : (long double)lo, ahi = hi < 0 ? -(long double)hi : (long double)hi;
+  switch (mode) {
+    case MSH_NORMALIZE_DEFAULT: return !column || lo >= 0 ? 100.0L : std::max(100.0L, 100.0L * alo);
+    case MSH_NORMALIZE_DEFAULT_REVERSE: return !column || lo >= 0 ? 100.0L : 100.0L + 100.0L * alo;
+    case MSH_NORMALIZE_MINMAX: return 100.0L;
+    default: return column ? std::max(alo, ahi) : 10.0L;
+  }
+}
+
 int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   g = msh::GenericArgs{};
   const NodeTable& t = cur_table(c);
-  g.nrec = t.d_nrec;
+  g.unsched = t.d_unsched;
+  g.digit = t.d_digit;
   g.cols = t.d_cols;
-  g.cols100 = t.d_cols100;
   g.col_stride = (int64_t)t.cap;
   g.n_nodes = c->n_nodes;
-  g.n_chunks = (c->n_nodes + msh::GEN_CH - 1) / msh::GEN_CH;
+  g.has_nu = c->pp.has_nu_filter;
   g.nn_prescore = c->pp.nn_prescore;
+  long double bound = 0;  // the largest |total| a feasible pair can reach
   for (size_t k = 0; k < c->score_ids.size(); ++k) {
     const int32_t id = c->score_ids[k];
+    const int32_t mode = c->normalize[k];
+    const int64_t w = c->weights[k];
     if (id == MSH_PLUGIN_NODE_NUMBER) {
       g.nn_score = 1;
-      g.nn_mode = c->normalize[k];
-      g.nn_weight = c->weights[k];
+      g.nn_mode = mode;
+      g.nn_weight = w;
+      bound += (long double)w * score_bound(false, mode, 0, 10);
     } else {
       const int32_t col = id - MSH_PLUGIN_SCORE_COLUMN0;
       if (!t.col_ok[col])
         return fail(c, MSH_ERR_STATE, "score column " + std::to_string(id) + " not uploaded since the last node upload");
-      g.ccol[g.ncol] = col;
-      g.cmode[g.ncol] = c->normalize[k];
-      g.cweight[g.ncol] = c->weights[k];
+      if (mode != MSH_NORMALIZE_NONE) {
+        g.ncc[g.nnc] = col;
+        g.npos[g.nnc] = g.ncol;
+        g.nmode[g.nnc] = mode;
+        g.nw[g.nnc] = w;
+        ++g.nnc;
+      } else {
+        g.tcc[g.nts] = col;
+        g.tw[g.nts] = w;
+        ++g.nts;
+      }
       ++g.ncol;
+      bound += (long double)w * score_bound(true, mode, t.col_lo[col], t.col_hi[col]);
     }
-    g.need_ext = g.need_ext || c->normalize[k] != MSH_NORMALIZE_NONE;
+    g.need_ext = g.need_ext || mode != MSH_NORMALIZE_NONE;
   }
+  // 32-bit totals when every feasible pair's total is bounded away from +-2^31 (biased by 2^31, the
+  // key of a feasible pair is then never 0, the infeasible key); otherwise Go's int64
+  g.w64 = bound > (long double)(((int64_t)1 << 31) - 2) ? 1 : 0;
   return MSH_OK;
 }
 
@@ -745,11 +761,8 @@ bool read_knobs(msh::DeviceInfo& d, std::string* err) {
                   knob("MSH_SEQ_WAVES", {{"0", 0}, {"1", 1}, {"4", 4}, {"15", 15}, {"16", 16}}, &d.seq_waves, err) &&
                   knob("MSH_HOST_IO", {{"zero-copy", 0}, {"zc", 1}, {"dma", 2}}, &io, err) &&
                   knob("MSH_HOST_SYNC", {{"wait", 0}, {"poll", 1}}, &poll, err) &&
-                  knob("MSH_BATCH_KERNEL", {{"pair", 0}, {"classrows", 1}, {"generic", 2}}, &d.batch_kernel, err) &&
+                  knob("MSH_BATCH_KERNEL", {{"pair", 0}, {"generic", 2}}, &d.batch_kernel, err) &&
                   knob("MSH_PAIR_PLANES", {{"auto", 0}, {"sgpr", 1}, {"lds", 2}}, &d.pair_planes, err) &&
-                  knob("MSH_PAIR_LDS_BPW", {{"2", 2}, {"1", 1}, {"3", 3}, {"4", 4}}, &d.pair_lds_bpw, err) &&
-                  knob("MSH_PAIR_COMPACT", {{"auto", -1}, {"0", 0}, {"1", 1}}, &d.pair_compact, err) &&
-                  knob("MSH_PAIR_HYBRID", {{"auto", -1}, {"1", 1}, {"0", 0}, {"2", 2}}, &d.pair_hybrid, err) &&
                   knob("MSH_PAIR_NOAX", {{"auto", -1}, {"1", 1}, {"0", 0}}, &d.pair_noax, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;
@@ -1311,8 +1324,7 @@ int msh_decode_keys_device(msh_ctx* c, int32_t p, const int8_t* d_pod_digit,
     return fail(c, MSH_ERR_INVALID, "null device pointer");
   DeviceGuard g(c->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipError_t e = msh::launch_decode_keys(d_pod_digit, d_pod_tol, p, d_keys, 0, c->pp,
-                                         d_out_idx, d_out_score, d_out_status, s);
+  hipError_t e = msh::launch_decode_keys(d_pod_digit, p, d_keys, c->pp, d_out_idx, d_out_score, d_out_status, s);
   if (e != hipSuccess) return hip_fail(c, e, "decode_keys_kernel");
   return MSH_OK;
 }

@@ -1,0 +1,658 @@
+// msh_generic.hip — the generic score pipeline (gfx950): any score plugin list (NodeNumber and up to four
+// score-column plugins, MSH_PLUGIN_SCORE_COLUMN0..3) with the int64 total of EVERY (pod, node) pair
+// computed explicitly — the general form of RunFilterPlugins + RunScorePlugins + selectHost
+// (minisched/minisched.go:115-199, 304-325) and north_star's five stages one to one.
+//
+// "Lanes = pods": lane l of a wave holds one pod of each of its two 64-pod blocks. The node table is
+// streamed through LDS in tiles shared by the workgroup's waves (stage 5): per node a record {code, xm}
+// (the NodeNumber code — suffix digit, or 15 — and xm = all-ones when NodeUnschedulable rejects the node
+// for pods that do not tolerate the taint), the node-only sum of the columns without a normalizer, and
+// 100 x raw as an exact double per normalizing column; the waves read them as wave-uniform ds_read_b128
+// broadcasts into VGPRs. Per pair, everything is VGPR-only vector work:
+//   1. feasibility: NodeUnschedulable's verdict, infeasible = xm & ~tolerates, clears the pair's key
+//      (one v_bitop3): an infeasible pair never becomes a pod's maximum;
+//   3. extents (max, min) of every normalizing plugin's raw score over the pod's feasible nodes: a pass
+//      of its own, only when some plugin normalizes (an infeasible pair's column value becomes a quiet
+//      NaN, which v_max_f64 / v_min_f64 skip; NodeNumber's 0 / 10 becomes all-ones); slice waves meet in
+//      an LDS reduction;
+//   2. the total of each pair: Σ weight x NormalizeScore(raw) in Go int64 arithmetic. NodeNumber is one
+//      compare + select between the pod's two weighted values; a normalizing column is
+//      q = (100 raw - b) x r with the pod's exact reciprocal r, truncated; the
+//      columns without a normalizer are the staged node-only sum;
+//   4. selectHost: the total as an unsigned key (total + 2^31, or total ^ 2^63 with 64-bit totals; 0 =
+//      infeasible), a running v_max per lane, and per 16-node chunk the chunk where the maximum last rose;
+//      after the scan the winner's chunk is re-evaluated for the first node with that key (the first
+//      maximum in List order: strict '>' as selectHost's scan, minisched.go:311-315).
+// Totals are 32-bit (W64 = false) when the host has bounded every feasible pair's |total| below 2^31 - 1
+// from the weights, the modes and the uploaded columns' range; otherwise 64-bit (Go's wrapping int64).
+// MODE 0: the whole batch (status, node, score per pod). Node-sharded mode (msh_generic_*): MODE 1 writes
+// each pod's extents over this shard's nodes (ext, mins negated: one all-reduce MAX merges them), MODE 2
+// takes the merged extents and writes each pod's best (total, global node index) over the shard.
+#include "msh_device.h"
+
+namespace msh {
+
+constexpr int GEN_W = 8;       // waves per workgroup
+constexpr int GEN_BPW = 2;     // 64-pod blocks per wave: one LDS read of a node serves both
+constexpr int GEN_CHUNK = 16;  // nodes per first-maximum chunk
+constexpr double GEN_RCP_BIAS = 1.0 + 0x1p-49;
+constexpr uint32_t GEN_NONE = 0xFFFFFFFFu;
+
+// NormalizeScore of one raw score given the pod's extent of that plugin over its feasible nodes
+// (mx, mn): upstream helper.DefaultNormalizeScore(MaxNodeScore = 100, reverse) — maxCount starts at 0,
+// an all-zero list is left alone (reverse: all 100) — or min-max (0 when max == min).
+__device__ __forceinline__ int64_t gen_normalize(int64_t raw, int32_t mode, int64_t mx, int64_t mn) {
+  switch (mode) {
+    case 1: {
+      const int64_t m = mx > 0 ? mx : 0;
+      return m == 0 ? raw : 100 * raw / m;
+    }
+    case 2: {
+      const int64_t m = mx > 0 ? mx : 0;
+      return m == 0 ? 100 : 100 - 100 * raw / m;
+    }
+    case 3: return mx == mn ? 0 : (raw - mn) * 100 / (mx - mn);
+    default: return raw;
+  }
+}
+
+// v_max_f64 / v_min_f64 as the instructions (fmax adds a NaN canonicalisation per operand): IEEE mode,
+// a quiet NaN operand yields the other one
+__device__ __forceinline__ double vmax_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// v with its high dword ORed with m: m all-ones turns it into a quiet NaN (exponent and quiet bit set)
+__device__ __forceinline__ double nan_if(double v, uint32_t x, uint32_t nt) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t hi = bop3_or_and((uint32_t)(b >> 32), x, nt);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | (uint32_t)b);
+}
+
+// Per-pair key of the main pass: Key = uint32_t (32-bit totals, biased by 2^31) or uint64_t (biased by
+// 2^63); 0 = infeasible.
+template <bool W64>
+using GKey = typename std::conditional<W64, uint64_t, uint32_t>::type;
+
+template <bool W64>
+__device__ __forceinline__ GKey<W64> key_mask(GKey<W64> t, uint32_t xm, uint32_t nt) {
+  if constexpr (W64) {
+    const uint32_t lo = bop3_andn_of_and((uint32_t)t, xm, nt), hi = bop3_andn_of_and((uint32_t)(t >> 32), xm, nt);
+    return ((uint64_t)hi << 32) | lo;
+  } else {
+    return bop3_andn_of_and(t, xm, nt);
+  }
+}
+
+// One lane's scoring state of one 64-pod block (main pass).
+template <bool W64, int NC>
+struct GLane {
+  GKey<W64> k1, k0;  // NodeNumber's weighted normalized value on a digit match / otherwise, biased
+  double rr[NC], bb[NC];  // per normalizing column: the reciprocal and the min-max offset
+};
+
+// The contribution of normalizing column c to a pair's total: w x trunc((v - b) x r), v = 100 x raw.
+template <bool W64, bool SUB>
+__device__ __forceinline__ GKey<W64> col_term(double v, double b, double r, GKey<W64> cw) {
+  const double q = (SUB ? v - b : v) * r;
+  if constexpr (W64) {
+    // |q| < 2^40 on a feasible pair; an infeasible pair's value is clamped, converted and masked out
+    const int64_t n = (int64_t)__builtin_fmin(__builtin_fmax(q, -0x1p62), 0x1p62);
+    return (uint64_t)n * cw;
+  } else {
+    // |n| within the host's bound on a feasible pair (v_cvt_i32_f64 saturates on the others)
+    const int32_t n = (int32_t)q;
+    return (uint32_t)n * cw;
+  }
+}
+
+template <int MODE, bool W64, bool TS, int NNC, bool MMX>
+__global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
+  using Key = GKey<W64>;
+  constexpr int NC = NNC > 0 ? NNC : 1;
+  extern __shared__ uint4 s_dyn[];
+  __shared__ uint32_t s_ffs;  // the first node NodeUnschedulable passes for every pod (GEN_NONE: none)
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int S = a.slices;           // waves per pod group (1, 2, 4, 8), each scanning a slice of every tile
+  const int sl = wv % S, pg = wv / S;
+  const int pgs = GEN_W / S;        // pod groups per workgroup
+  const BatchDesc& d = a.d[blockIdx.y];
+  const int32_t np = d.n_pods;
+  const int32_t wg0 = (int32_t)blockIdx.x * pgs * GEN_BPW * WAVE;
+  if (wg0 >= np) return;  // the whole workgroup lies past its batch's end
+  const int32_t n = a.n_nodes, TN = a.tile;
+  const int nnc = NNC == 4 ? a.nnc : NNC;  // normalizing columns (the general instance: a runtime count)
+  // dynamic LDS: the tile (records, node-only sums, normalizing columns), then the slice-merge area
+  uint2* s_cx = reinterpret_cast<uint2*>(s_dyn);
+  Key* s_ts = reinterpret_cast<Key*>(s_cx + TN);
+  double* s_v = reinterpret_cast<double*>(reinterpret_cast<char*>(s_ts) + (TS ? (size_t)TN * sizeof(Key) : 0));
+  char* s_merge = reinterpret_cast<char*>(s_v + (size_t)nnc * TN);
+  if (threadIdx.x == 0) s_ffs = GEN_NONE;
+  __syncthreads();
+
+  // ---- the lane's pods ----
+  uint32_t pcode[GEN_BPW], ntol[GEN_BPW];
+  int32_t jj[GEN_BPW];
+  bool pdok[GEN_BPW];
+  const int32_t pbase = wg0 + pg * GEN_BPW * WAVE;
+#pragma unroll
+  for (int b = 0; b < GEN_BPW; ++b) {
+    const int32_t j = pbase + b * WAVE + lane;
+    jj[b] = j;
+    int dq = -1, tq = 0;
+    if (j < np) {
+      dq = d.pod_digit[j];
+      tq = d.pod_tol[j];
+    }
+    pdok[b] = dq >= 0 && dq <= 9;  // NodeNumber.PreScore: Atoi of the last byte
+    pcode[b] = pdok[b] ? (uint32_t)dq : CODE_NONE_POD;
+    ntol[b] = tq ? 0u : 0xFFFFFFFFu;
+  }
+
+  // ---- stage 5: tiles of the node table through LDS, shared by the workgroup's waves ----
+  const int n_tiles = n > 0 ? (n + TN - 1) / TN : 0;
+  auto stage = [&](int32_t t0) {
+    const int32_t tn = min(TN, n - t0);
+    for (int32_t k = threadIdx.x; k < ((tn + WAVE - 1) & ~(WAVE - 1)); k += GEN_W * WAVE) {
+      const int32_t i = t0 + k;
+      const bool in = k < tn;
+      uint32_t xm = 0u;
+      if (in) {
+        const int dg = a.digit[i];
+        xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
+        s_cx[k] = make_uint2((dg >= 0 && dg <= 9) ? (uint32_t)dg : CODE_NONE_NODE, xm);
+        if constexpr (TS) {  // the node-only part: weight x raw of the columns without a normalizer
+          Key ts = 0;
+          for (int c = 0; c < a.nts; ++c) ts += (Key)a.cols[(size_t)a.tcc[c] * a.col_stride + i] * (Key)a.tw[c];
+          s_ts[k] = ts;
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+          if (c < nnc) s_v[(size_t)c * TN + k] = 100.0 * (double)a.cols[(size_t)a.ncc[c] * a.col_stride + i];
+      }
+      const uint64_t m = __ballot(in && xm == 0u);
+      if (m && lane == 0) atomicMin(&s_ffs, (uint32_t)(i - lane) + (uint32_t)__builtin_ctzll(m));
+    }
+  };
+  // the wave's slice of a tile of tn nodes: [lo, hi)
+  auto slice_of = [&](int32_t tn, int32_t& lo, int32_t& hi) {
+    const int32_t L = (((tn + S - 1) / S) + GEN_CHUNK - 1) & ~(GEN_CHUNK - 1);
+    lo = min(sl * L, tn);
+    hi = min(lo + L, tn);
+  };
+
+  // ---- stage 3: extents over the feasible nodes (normalizing plugins only) ----
+  int64_t emx[GEN_BPW][1 + NC], emn[GEN_BPW][1 + NC];  // [0] NodeNumber, [1 + c] normalizing column c
+#pragma unroll
+  for (int b = 0; b < GEN_BPW; ++b)
+#pragma unroll
+    for (int e = 0; e < 1 + NC; ++e) {
+      emx[b][e] = INT64_MIN;
+      emn[b][e] = INT64_MAX;
+    }
+  const bool nn_ext = a.nn_score && a.nn_mode != 0;
+  bool staged = false;  // the one tile of a single-tile table is staged once for both passes
+  if (MODE != 2 && a.need_ext) {
+    int32_t mxn[GEN_BPW];   // NodeNumber: the largest raw score (10 / 0) over feasible nodes, -1 none
+    uint32_t mnn[GEN_BPW];  // the smallest, all-ones none
+    double dmx[GEN_BPW][NC], dmn[GEN_BPW][NC];
+#pragma unroll
+    for (int b = 0; b < GEN_BPW; ++b) {
+      mxn[b] = -1;
+      mnn[b] = 0xFFFFFFFFu;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        dmx[b][c] = -__builtin_inf();
+        dmn[b][c] = __builtin_inf();
+      }
+    }
+    auto ext_scan = [&](auto nnx) {
+      constexpr bool NNX = decltype(nnx)::value;
+      for (int t = 0; t < n_tiles; ++t) {
+        const int32_t t0 = t * TN, tn = min(TN, n - t0);
+        if (n_tiles > 1 || !staged) {
+          if (t > 0) __syncthreads();  // every wave is done with the previous tile
+          stage(t0);
+          __syncthreads();
+          staged = true;
+        }
+        int32_t lo, hi;
+        slice_of(tn, lo, hi);
+        for (int32_t k = lo; k < hi; ++k) {
+          const uint2 cx = s_cx[k];
+          double v[NC];
+#pragma unroll
+          for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
+#pragma unroll
+          for (int b = 0; b < GEN_BPW; ++b) {
+            if constexpr (NNX) {  // NodeNumber's raw score, all-ones where the pair is infeasible
+              const uint32_t raw = bop3_or_and(cx.x == pcode[b] ? 10u : 0u, cx.y, ntol[b]);
+              mxn[b] = max(mxn[b], (int32_t)raw);
+              mnn[b] = umin(mnn[b], raw);
+            }
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+              if (c >= nnc) break;
+              const double vv = nan_if(v[c], cx.y, ntol[b]);
+              dmx[b][c] = vmax_f64(dmx[b][c], vv);
+              if (MMX) dmn[b][c] = vmin_f64(dmn[b][c], vv);
+            }
+          }
+        }
+      }
+    };
+    if (nn_ext) ext_scan(std::true_type{});
+    else ext_scan(std::false_type{});
+    // slice waves of a pod group meet in LDS (every wave of the group takes the merged extents)
+    if (S > 1) {
+      int32_t* m_nn = reinterpret_cast<int32_t*>(s_merge);                       // [GEN_W][BPW][2][64]
+      double* m_col = reinterpret_cast<double*>(s_merge + GEN_W * GEN_BPW * 2 * WAVE * 4);  // [GEN_W][BPW][NC][2][64]
+      __syncthreads();
+#pragma unroll
+      for (int b = 0; b < GEN_BPW; ++b) {
+        m_nn[((wv * GEN_BPW + b) * 2 + 0) * WAVE + lane] = mxn[b];
+        m_nn[((wv * GEN_BPW + b) * 2 + 1) * WAVE + lane] = (int32_t)mnn[b];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (c >= nnc) break;
+          m_col[(((wv * GEN_BPW + b) * NC + c) * 2 + 0) * WAVE + lane] = dmx[b][c];
+          m_col[(((wv * GEN_BPW + b) * NC + c) * 2 + 1) * WAVE + lane] = dmn[b][c];
+        }
+      }
+      __syncthreads();
+      for (int k = 0; k < S; ++k) {
+        const int ow = pg * S + k;
+#pragma unroll
+        for (int b = 0; b < GEN_BPW; ++b) {
+          mxn[b] = max(mxn[b], m_nn[((ow * GEN_BPW + b) * 2 + 0) * WAVE + lane]);
+          mnn[b] = umin(mnn[b], (uint32_t)m_nn[((ow * GEN_BPW + b) * 2 + 1) * WAVE + lane]);
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            if (c >= nnc) break;
+            dmx[b][c] = vmax_f64(dmx[b][c], m_col[(((ow * GEN_BPW + b) * NC + c) * 2 + 0) * WAVE + lane]);
+            dmn[b][c] = vmin_f64(dmn[b][c], m_col[(((ow * GEN_BPW + b) * NC + c) * 2 + 1) * WAVE + lane]);
+          }
+        }
+      }
+      __syncthreads();  // the merge area is reused by the main pass
+    }
+#pragma unroll
+    for (int b = 0; b < GEN_BPW; ++b) {
+      if (nn_ext && mxn[b] >= 0) {  // NodeNumber's raw scores are 10 / 0
+        emx[b][0] = mxn[b];
+        emn[b][0] = (int64_t)mnn[b];
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (c >= nnc) break;
+        if (dmx[b][c] != -__builtin_inf()) {  // 100 x raw / 100: exact (|raw| <= 2^31)
+          emx[b][1 + c] = (int64_t)(dmx[b][c] * 0.01);
+          emn[b][1 + c] = MMX ? (int64_t)(dmn[b][c] * 0.01) : INT64_MAX;
+        }
+      }
+    }
+    if constexpr (MODE == 1) {  // node-sharded: this shard's extents, mins negated (one MAX merges both)
+      if (sl == 0) {
+        const int ne = 1 + a.ncol;
+#pragma unroll
+        for (int b = 0; b < GEN_BPW; ++b) {
+          const int32_t j = jj[b];
+          if (j >= np) continue;
+          for (int e = 0; e < ne; ++e) {  // list positions without a normalizer: no extent
+            a.ext[(size_t)(2 * e) * np + j] = INT64_MIN;
+            a.ext[(size_t)(2 * e + 1) * np + j] = -INT64_MAX;
+          }
+          a.ext[j] = emx[b][0];
+          a.ext[(size_t)np + j] = -emn[b][0];  // emn <= INT64_MAX: no overflow
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            if (c >= nnc) break;
+            const int e = 1 + a.npos[c];
+            a.ext[(size_t)(2 * e) * np + j] = emx[b][1 + c];
+            a.ext[(size_t)(2 * e + 1) * np + j] = -emn[b][1 + c];
+          }
+        }
+      }
+      return;
+    }
+  }
+  if constexpr (MODE == 1) return;
+  if (MODE == 2 && a.need_ext) {  // the extents merged over every shard
+#pragma unroll
+    for (int b = 0; b < GEN_BPW; ++b) {
+      const int32_t j = jj[b];
+      if (j >= np) continue;
+      emx[b][0] = a.ext[j];
+      emn[b][0] = -a.ext[(size_t)np + j];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (c >= nnc) break;
+        const int e = 1 + a.npos[c];
+        emx[b][1 + c] = a.ext[(size_t)(2 * e) * np + j];
+        emn[b][1 + c] = -a.ext[(size_t)(2 * e + 1) * np + j];
+      }
+    }
+  }
+
+  // ---- per pod: NodeNumber's two weighted values, each normalizing column's reciprocal ----
+  Key cw[NC];  // the normalizing columns' weights, negated for REVERSE (its 100 w is in the keys' base)
+  uint64_t tot0 = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    cw[c] = 0;
+    if (c >= nnc) break;
+    const bool rev = a.nmode[c] == 2;
+    cw[c] = rev ? (Key)(0 - (uint64_t)a.nw[c]) : (Key)a.nw[c];
+    if (rev) tot0 += (uint64_t)100 * (uint64_t)a.nw[c];
+  }
+  GLane<W64, NC> L[GEN_BPW];
+#pragma unroll
+  for (int b = 0; b < GEN_BPW; ++b) {
+    int64_t c1 = 0, c0 = 0;
+    if (a.nn_score && a.nn_mode != 0 && emx[b][0] != INT64_MIN) {
+      c1 = (int64_t)((uint64_t)gen_normalize(10, a.nn_mode, emx[b][0], emn[b][0]) * (uint64_t)a.nn_weight);
+      c0 = (int64_t)((uint64_t)gen_normalize(0, a.nn_mode, emx[b][0], emn[b][0]) * (uint64_t)a.nn_weight);
+    } else if (a.nn_score) {
+      c1 = (int64_t)((uint64_t)10 * (uint64_t)a.nn_weight);  // NONE: raw x weight
+    }
+    if constexpr (W64) {
+      L[b].k1 = ((uint64_t)c1 + tot0) ^ 0x8000000000000000ull;
+      L[b].k0 = ((uint64_t)c0 + tot0) ^ 0x8000000000000000ull;
+    } else {
+      L[b].k1 = (uint32_t)((uint64_t)c1 + tot0) + 0x80000000u;
+      L[b].k0 = (uint32_t)((uint64_t)c0 + tot0) + 0x80000000u;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      L[b].rr[c] = 0.0;
+      L[b].bb[c] = 0.0;
+      if (c >= nnc) break;
+      const int32_t md = a.nmode[c];
+      const int64_t mx = emx[b][1 + c], mn = emn[b][1 + c];
+      if (mx == INT64_MIN) continue;  // no feasible node
+      if (md == 3) {                  // min-max: (raw - mn) x 100 / (mx - mn), 0 when mx == mn
+        if (mx != mn) {
+          L[b].rr[c] = (1.0 / (double)(mx - mn)) * GEN_RCP_BIAS;
+          L[b].bb[c] = 100.0 * (double)mn;
+        }
+      } else {  // DefaultNormalizeScore: 100 raw / max(mx, 0); DEFAULT leaves an all-zero list (m = 0 -> raw)
+        const int64_t m = mx > 0 ? mx : 0;
+        if (m != 0) L[b].rr[c] = (1.0 / (double)m) * GEN_RCP_BIAS;
+        else if (md == 1) L[b].rr[c] = 0.01 * GEN_RCP_BIAS;
+        // REVERSE with m == 0: r = 0, 100 - 0 = 100 for every node
+      }
+    }
+  }
+  // the key of one pair, from a node's staged (or re-read) values
+  auto pair_key = [&](int b, uint32_t code, uint32_t xm, Key ts, const double (&v)[NC]) -> Key {
+    Key t = code == pcode[b] ? L[b].k1 : L[b].k0;
+    if constexpr (TS) t += ts;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (c >= nnc) break;
+      t += col_term<W64, MMX>(v[c], L[b].bb[c], L[b].rr[c], cw[c]);
+    }
+    return key_mask<W64>(t, xm, ntol[b]);
+  };
+
+  // ---- stages 1, 2, 4: feasibility, the total, the first maximum ----
+  Key best[GEN_BPW];
+  int32_t cidx[GEN_BPW];
+#pragma unroll
+  for (int b = 0; b < GEN_BPW; ++b) {
+    best[b] = 0;
+    cidx[b] = -1;
+  }
+  for (int t = 0; t < n_tiles; ++t) {
+    const int32_t t0 = t * TN, tn = min(TN, n - t0);
+    if (n_tiles > 1 || !staged) {
+      __syncthreads();
+      stage(t0);
+      __syncthreads();
+      staged = true;
+    }
+    int32_t lo, hi;
+    slice_of(tn, lo, hi);
+    auto node = [&](int32_t k, Key (&bst)[GEN_BPW]) {
+      const uint2 cx = s_cx[k];
+      Key ts = 0;
+      if constexpr (TS) ts = s_ts[k];
+      double v[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
+#pragma unroll
+      for (int b = 0; b < GEN_BPW; ++b) {
+        const Key key = pair_key(b, cx.x, cx.y, ts, v);
+        bst[b] = key > bst[b] ? key : bst[b];
+      }
+    };
+    int32_t k = lo;
+    for (; k + GEN_CHUNK <= hi; k += GEN_CHUNK) {
+      Key prev[GEN_BPW];
+#pragma unroll
+      for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
+#pragma unroll
+      for (int q = 0; q < GEN_CHUNK; ++q) node(k + q, best);
+#pragma unroll
+      for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
+    }
+    if (k < hi) {  // the slice's last, partial chunk
+      Key prev[GEN_BPW];
+#pragma unroll
+      for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
+      for (int32_t q = k; q < hi; ++q) node(q, best);
+#pragma unroll
+      for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
+    }
+  }
+  // the exact node: the first of the winning chunk whose key is the maximum (re-read from the uploaded
+  // columns, the same arithmetic as the staged values)
+  int32_t bidx[GEN_BPW];
+#pragma unroll
+  for (int b = 0; b < GEN_BPW; ++b) {
+    bidx[b] = INT32_MAX;
+    if (best[b] == 0 || jj[b] >= np) continue;
+    const int32_t e = min(cidx[b] + GEN_CHUNK, n);
+    for (int32_t i = cidx[b]; i < e; ++i) {
+      const int dg = a.digit[i];
+      const uint32_t code = (dg >= 0 && dg <= 9) ? (uint32_t)dg : CODE_NONE_NODE;
+      const uint32_t xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
+      Key ts = 0;
+      if constexpr (TS)
+        for (int c = 0; c < a.nts; ++c) ts += (Key)a.cols[(size_t)a.tcc[c] * a.col_stride + i] * (Key)a.tw[c];
+      double v[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        v[c] = c < nnc ? 100.0 * (double)a.cols[(size_t)a.ncc[c] * a.col_stride + i] : 0.0;
+      if (pair_key(b, code, xm, ts, v) == best[b]) {
+        bidx[b] = i;
+        break;
+      }
+    }
+  }
+  // slice waves of a pod group meet in LDS: the larger key, then the lower index (slices of one tile
+  // ascend in List order, but a later tile's first slice follows an earlier tile's last)
+  if (S > 1) {
+    Key* m_key = reinterpret_cast<Key*>(s_merge);                                      // [GEN_W][BPW][64]
+    int32_t* m_idx = reinterpret_cast<int32_t*>(s_merge + GEN_W * GEN_BPW * WAVE * sizeof(Key));
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < GEN_BPW; ++b) {
+      m_key[(wv * GEN_BPW + b) * WAVE + lane] = best[b];
+      m_idx[(wv * GEN_BPW + b) * WAVE + lane] = bidx[b];
+    }
+    __syncthreads();
+    if (sl != 0) return;
+    for (int k = 1; k < S; ++k) {
+      const int ow = pg * S + k;
+#pragma unroll
+      for (int b = 0; b < GEN_BPW; ++b) {
+        const Key ok = m_key[(ow * GEN_BPW + b) * WAVE + lane];
+        const int32_t oi = m_idx[(ow * GEN_BPW + b) * WAVE + lane];
+        if (ok > best[b] || (ok == best[b] && oi < bidx[b])) {
+          best[b] = ok;
+          bidx[b] = oi;
+        }
+      }
+    }
+  }
+  const uint32_t ffs = s_ffs;  // complete: every tile has been staged (barriers above)
+#pragma unroll
+  for (int b = 0; b < GEN_BPW; ++b) {
+    const int32_t j = jj[b];
+    if (j >= np) continue;
+    // the first feasible node: node 0 for a pod that tolerates the taint, else the first one the filter
+    // passes for every pod
+    const uint32_t ff = n == 0 ? GEN_NONE : (ntol[b] == 0u ? 0u : ffs);
+    const bool found = ff != GEN_NONE;
+    int64_t total;
+    int32_t idx;
+    if (best[b] == 0) {  // every feasible total is INT64_MIN (64-bit totals only): the first feasible node
+      total = INT64_MIN;
+      idx = (int32_t)ff;
+    } else {
+      total = W64 ? (int64_t)((uint64_t)best[b] ^ 0x8000000000000000ull)
+                  : (int64_t)(int32_t)((uint32_t)best[b] - 0x80000000u);
+      idx = bidx[b];
+    }
+    if constexpr (MODE == 2) {  // this shard's best: merged by MAX total, then MIN global index
+      a.best_total[j] = found ? total : INT64_MIN;
+      a.best_idx[j] = found ? (int32_t)(a.node_base + idx) : INT32_MAX;
+    } else {
+      int32_t st = 0;
+      if (!found) st = 1;                                             // FitError (minisched.go:143-148)
+      else if (a.nn_score && (!a.nn_prescore || !pdok[b])) st = 2;    // NodeNumber.Score error (nodenumber.go:74-77)
+      d.out_idx[j] = st ? -1 : idx;
+      if (d.out_score) d.out_score[j] = st ? 0 : total;
+      d.out_status[j] = st;
+    }
+  }
+}
+
+// The decode of the node-sharded generic path, after the merge (msh_generic_decode_device).
+__global__ __launch_bounds__(256) void generic_decode_kernel(const int8_t* __restrict__ pod_digit, int32_t p,
+                                                             const int64_t* __restrict__ best_total,
+                                                             const int32_t* __restrict__ best_idx,
+                                                             int32_t nn_score, int32_t nn_prescore,
+                                                             int32_t* __restrict__ out_idx,
+                                                             int64_t* __restrict__ out_score,
+                                                             int32_t* __restrict__ out_status) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p) return;
+  const int pd = pod_digit[j];
+  const bool pd_ok = pd >= 0 && pd <= 9;
+  const int32_t bi = best_idx[j];
+  int32_t st = 0;
+  if (bi == INT32_MAX) st = 1;                            // no shard has a feasible node: FitError
+  else if (nn_score && (!nn_prescore || !pd_ok)) st = 2;  // NodeNumber.Score error
+  out_idx[j] = st ? -1 : bi;
+  if (out_score) out_score[j] = st ? 0 : best_total[j];
+  out_status[j] = st;
+}
+
+// Per pod of a shard: its best index if its best total equals the merged maximum, else INT32_MAX
+// (the second, MIN, all-reduce then yields the lowest global index among the maxima).
+__global__ __launch_bounds__(256) void generic_candidate_kernel(int32_t p, const int64_t* __restrict__ local_total,
+                                                                const int64_t* __restrict__ merged_total,
+                                                                int32_t* __restrict__ idx) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p) return;
+  if (idx[j] != INT32_MAX && local_total[j] != merged_total[j]) idx[j] = INT32_MAX;
+}
+
+namespace {
+constexpr size_t GEN_LDS_BUDGET = 40 * 1024;  // tile bytes per workgroup (4 workgroups per CU)
+
+// Slice waves per pod group: one, unless the launch has fewer than ~2 pod groups per SIMD.
+int gen_slices(int64_t groups, int32_t n, const DeviceInfo& dev) {
+  if (dev.bits_slices > 0) return std::min(dev.bits_slices, GEN_W);
+  const int64_t want = (int64_t)dev.cus * 4 * 2;
+  int sl = 1;
+  while (sl < GEN_W && groups * sl < want && n >= 256 * sl) sl *= 2;
+  return sl;
+}
+
+template <int MODE, bool W64, bool TS, int NNC, bool MMX>
+hipError_t launch_gen_k(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
+  auto k = generic_kernel<MODE, W64, TS, NNC, MMX>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  MSH_TIMED_LAUNCH(k, dim3((unsigned)bx, (unsigned)a.nb), dim3(GEN_W * WAVE), (unsigned)lds, s, a);
+  return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch_gen_mode(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
+  const bool ts = a.nts > 0;
+  if (a.w64 || a.nnc > 1) return launch_gen_k<MODE, true, true, 4, true>(a, bx, lds, s);  // the general form
+  if (a.nnc == 0) return ts ? launch_gen_k<MODE, false, true, 0, false>(a, bx, lds, s)
+                            : launch_gen_k<MODE, false, false, 0, false>(a, bx, lds, s);
+  const bool mm = a.nmode[0] == 3;
+  if (ts) return mm ? launch_gen_k<MODE, false, true, 1, true>(a, bx, lds, s)
+                    : launch_gen_k<MODE, false, true, 1, false>(a, bx, lds, s);
+  return mm ? launch_gen_k<MODE, false, false, 1, true>(a, bx, lds, s)
+            : launch_gen_k<MODE, false, false, 1, false>(a, bx, lds, s);
+}
+}  // namespace
+
+hipError_t launch_generic(GenericArgs& a, int mode, const DeviceInfo& dev, hipStream_t s) {
+  if (a.nb <= 0 || a.nb > MULTI_MAX || a.nnc < 0 || a.nnc > GEN_COLS || a.nts < 0 || a.nts > GEN_COLS ||
+      (mode != 0 && a.nb != 1))
+    return hipErrorInvalidValue;
+  int32_t maxp = 0;
+  int64_t groups = 0;
+  for (int b = 0; b < a.nb; ++b) {
+    maxp = std::max(maxp, a.d[b].n_pods);
+    groups += (a.d[b].n_pods + GEN_BPW * WAVE - 1) / (GEN_BPW * WAVE);
+  }
+  if (maxp == 0) return hipSuccess;
+  const bool general = a.w64 || a.nnc > 1;
+  const size_t key = general ? 8 : 4;
+  const int nnc = general ? a.nnc : std::min(a.nnc, 1);
+  // bytes per staged node: the record, the node-only sum (the general form always stages it), the
+  // normalizing columns
+  const size_t per_node = 8 + ((general || a.nts > 0) ? key : 0) + 8 * (size_t)nnc;
+  int32_t tile = (int32_t)(GEN_LDS_BUDGET / per_node) & ~(GEN_CHUNK - 1);
+  tile = std::max<int32_t>(GEN_CHUNK, std::min<int32_t>(tile, (a.n_nodes + GEN_CHUNK - 1) & ~(GEN_CHUNK - 1)));
+  a.tile = tile;
+  a.slices = gen_slices(groups, a.n_nodes, dev);
+  // the slice merge (S > 1): the extents (NodeNumber's two int32, (max, min) per column of the
+  // instance's column array), then (key, index)
+  const size_t ncx = general ? 4 : 1;
+  const size_t merge = a.slices > 1 ? (size_t)GEN_W * GEN_BPW * WAVE * std::max<size_t>(8 + 16 * ncx, key + 4) : 0;
+  const size_t lds = (size_t)tile * per_node + merge;
+  const int pgs = GEN_W / a.slices;
+  const int32_t bx = (maxp + pgs * GEN_BPW * WAVE - 1) / (pgs * GEN_BPW * WAVE);
+  if (mode == 1) return launch_gen_mode<1>(a, bx, lds, s);
+  if (mode == 2) return launch_gen_mode<2>(a, bx, lds, s);
+  return launch_gen_mode<0>(a, bx, lds, s);
+}
+
+hipError_t launch_generic_candidates(int32_t p, const int64_t* local_total, const int64_t* merged_total, int32_t* idx,
+                                     hipStream_t s) {
+  if (p <= 0) return hipSuccess;
+  hipLaunchKernelGGL(generic_candidate_kernel, dim3((p + 255) / 256), dim3(256), 0, s, p, local_total, merged_total,
+                     idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_generic_decode(const int8_t* pod_digit, int32_t p, const int64_t* best_total, const int32_t* best_idx,
+                                 int32_t nn_score, int32_t nn_prescore, int32_t* out_idx, int64_t* out_score,
+                                 int32_t* out_status, hipStream_t s) {
+  if (p <= 0) return hipSuccess;
+  hipLaunchKernelGGL(generic_decode_kernel, dim3((p + 255) / 256), dim3(256), 0, s, pod_digit, p, best_total, best_idx,
+                     nn_score, nn_prescore, out_idx, out_score, out_status);
+  return hipGetLastError();
+}
+
+}  // namespace msh

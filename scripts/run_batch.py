@@ -3,15 +3,14 @@ pods per batch, bench.py's synthetic snapshot).
 
 MODE
   multi        bench.py's default submission: 32 independent batches per msh_schedule_batches_device
-               launch (pair_kernel, the per-pair kernel; with MSH_BATCH_KERNEL=classrows in the
-               environment, the opt-in class-row kernel)
+               launch (the per-pair kernel)
   batch        one msh_schedule_batch_device launch per batch
   generic      generic_kernel (explicit int64 score per pair) on the reference plugin list, 32 batches
                per launch (MSH_BATCH_KERNEL=generic is set here)
   generic_col  generic_kernel on NodeNumber + ScoreColumn0 (weight 2, DefaultNormalizeScore), 32 batches
-               per launch
+               per launch (bench.py's generic.nodenumber_plus_default_column)
   sequential   C5: one pod at a time (seq_kernel)
-NORM: msh_normalize of the NodeNumber entry (3 = MINMAX)."""
+NORM / WEIGHT: msh_normalize and weight of the NodeNumber entry (bench.py's headline: WEIGHT=3 NORM=1)."""
 import importlib
 import os
 import sys
@@ -33,17 +32,18 @@ n = int(os.environ.get("NODES", 5000))
 p = int(os.environ.get("PODS", 100000))
 k = int(os.environ.get("LAUNCHES", 20))
 norm = int(os.environ.get("NORM", 0))
+weight = int(os.environ.get("WEIGHT", 1))
 ctx = msh.DeviceContext(0)
 u, nd, pd, pt = synth.make_soa(n, p)
 ctx.upload_nodes(u, nd)
 if mode == "generic_col":
-    ctx.upload_score_column(msh.SCORE_COLUMNS[0], (np.arange(n, dtype=np.int64) * 7919) % 1000)
+    ctx.upload_score_column(msh.SCORE_COLUMNS[0], (np.arange(n, dtype=np.int64) * 7919) % 1000 - 300)
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                     [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm)),
                      msh.ScorePluginConfig(msh.SCORE_COLUMNS[0], 2, msh.Normalize(1))])
 else:
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
-                    [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm))])
+                    [msh.ScorePluginConfig(msh.NODE_NUMBER, weight, msh.Normalize(norm))])
 dev = torch.device("cuda:0")
 nb = msh._native.BATCHES_PER_LAUNCH if mode in ("multi", "generic", "generic_col") else 1
 bufs = [(torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev), torch.empty(p, dtype=torch.int32, device=dev),
@@ -60,4 +60,4 @@ for _ in range(k):
     else:
         ctx.schedule_sequential_device(p, b[0].data_ptr(), b[1].data_ptr(), 0, *[t.data_ptr() for t in b[2:]], s)
 torch.cuda.synchronize()
-print("ok", n, p, k, mode, nb, os.environ.get("MSH_BATCH_KERNEL", "pair"))
+print("ok", n, p, k, mode, nb, os.environ.get("MSH_BATCH_KERNEL", "pair"), f"NodeNumber w={weight} norm={norm}")
