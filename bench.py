@@ -542,6 +542,17 @@ def multi_launch_ms(torch, ctx, descs, nb, R, stream):
     return tot / max(n_t, 1)
 
 
+def median_us(fn, k: int) -> float:
+    """Median host wall time of k calls of fn (after one untimed call), in microseconds."""
+    fn()
+    ts = []
+    for _ in range(k):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)) * 1e6
+
+
 def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     """Secondary BASELINE configs, the generic and class-row kernels, and the host-buffer path, each
     timed and checked bit-exact."""
@@ -767,6 +778,36 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
                             "check": ("seq == batch (closed form), node counts == 3 x placements" if ok else "MISMATCH"),
                             "roofline": make_roofline("sequential", n, p, ms, 1, cus)}
     ctx.close()
+
+    # ---- f2: node-table maintenance (an informer Update / Add, eventhandler.go:37-57, replacing the
+    # per-cycle LIST of minisched.go:40), host wall time of the synchronous call, median of 50 ----
+    tm = {}
+    for n_t in (5000, 100_000):
+        u_t, nd_t = synth.make_nodes(n_t)[1:]
+        ctx = new_ctx()
+        ctx.upload_nodes(u_t, nd_t)
+        row = {"full_upload_us": median_us(lambda: ctx.upload_nodes(u_t, nd_t), 50)}
+        rng = np.random.default_rng(n_t)
+        for k in (1, 64, 1024):
+            idx = rng.choice(n_t, k, replace=False).astype(np.int32)
+            flip = [(1 - u_t[idx]).astype(np.uint8), u_t[idx].astype(np.uint8)]
+            state = [0]
+
+            def patch():
+                ctx.patch_nodes(idx, flip[state[0]], nd_t[idx])
+                state[0] ^= 1
+
+            row[f"patch_{k}_nodes_us"] = median_us(patch, 50)
+        # the table after an even number of flips is the uploaded one: check a batch against it
+        pd_t, pt_t = synth._make_pods_fast(4096, synth.SEED)[1:]
+        ok = same(ctx.schedule_batch(pd_t, pt_t), closed_form_modes(u_t, nd_t, pd_t, pt_t, HEADLINE_WEIGHT, HEADLINE_NORM))
+        row["check"] = "bit-exact vs closed form after the flips" if ok else "MISMATCH"
+        tm[f"{n_t}_nodes"] = row
+        ctx.close()
+    tm["note"] = ("msh_patch_nodes of up to 64 nodes: one launch that copies the published table version and "
+                  "rebuilds only the patched 32-node words' planes; more nodes: copy + scatter + the O(N) prep; "
+                  "msh_upload_nodes: the H2D copy of 2 B/node + the prep")
+    out["table_maintenance"] = tm
 
     # ---- C2: 1k x 10k, one launch per batch over two streams ----
     n2, p2 = 1000, 10_000

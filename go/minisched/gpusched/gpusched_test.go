@@ -22,6 +22,8 @@ import (
 	v1 "k8s.io/api/core/v1"
 	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
 	"k8s.io/apimachinery/pkg/types"
+	corelisters "k8s.io/client-go/listers/core/v1"
+	"k8s.io/client-go/tools/cache"
 	"k8s.io/kubernetes/pkg/scheduler/framework"
 	"k8s.io/kubernetes/pkg/scheduler/framework/plugins/nodeunschedulable"
 )
@@ -301,6 +303,57 @@ func TestNodeSnapshotCordonFlipBetweenBatches(t *testing.T) {
 		t.Fatal(err)
 	}
 	compare(t, rp, got, pods, x.byIndex)
+}
+
+// The store has synced (WaitForCacheSync returned, scheduler.go:72-75) but the handlers have been
+// called for only part of it (advisor r4): the first Sync of a lister-backed snapshot uploads the whole
+// store, so the first batch matches the reference's per-cycle LIST; the late Adds then patch identical
+// values, and the batch after them is unchanged.
+func TestNodeSnapshotFirstSyncReadsTheStore(t *testing.T) {
+	rp := newRefPlugins(t)
+	x := newDevice(t, rp)
+	defer x.Close()
+	nodes, pods := synth(2000, 4000, 0x51)
+	store := cache.NewIndexer(cache.MetaNamespaceKeyFunc, cache.Indexers{})
+	for i := range nodes {
+		if err := store.Add(&nodes[i]); err != nil {
+			t.Fatal(err)
+		}
+	}
+	snap := NewNodeSnapshotFromLister(corelisters.NewNodeLister(store))
+	for i := 0; i < len(nodes)/3; i++ { // the handlers lag behind the store
+		snap.OnAdd(&nodes[i])
+	}
+	if kind, err := snap.Sync(x); err != nil || kind != "upload" {
+		t.Fatalf("first sync: %q %v", kind, err)
+	}
+	if len(x.byIndex) != len(nodes) {
+		t.Fatalf("first upload holds %d of the store's %d nodes", len(x.byIndex), len(nodes))
+	}
+	b, err := NewHostBatch(len(pods))
+	if err != nil {
+		t.Fatal(err)
+	}
+	got, err := x.ScheduleBatch(pods, b)
+	if err != nil {
+		t.Fatal(err)
+	}
+	compare(t, rp, got, pods, x.byIndex)
+	for i := len(nodes) / 3; i < len(nodes); i++ { // the late handler calls
+		snap.OnAdd(&nodes[i])
+	}
+	if kind, err := snap.Sync(x); err != nil || kind != "patch" {
+		t.Fatalf("late adds: want patch, got %q %v", kind, err)
+	}
+	again, err := x.ScheduleBatch(pods, b)
+	if err != nil {
+		t.Fatal(err)
+	}
+	for j := range got {
+		if got[j].Node != again[j].Node && (got[j].Node == nil || again[j].Node == nil || got[j].Node.Name != again[j].Node.Name) {
+			t.Fatalf("pod %d: %v before the late adds, %v after", j, got[j].Node, again[j].Node)
+		}
+	}
 }
 
 // An upload between Submit and Wait must not change how the batch in flight decodes (advisor r3):
