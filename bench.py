@@ -6,27 +6,29 @@ A step = one pass of the hot path (filter -> prescore -> score -> select, i.e.
 minisched/minisched.go:50-87 for every pod of a batch) over one batch of synthetic pods with
 inputs already resident in HBM.
 
+Plugins: BASELINE C3's "nodenumber prescore/score + weighted NormalizeScore": filter=[NodeUnschedulable],
+prescore=[NodeNumber], score=[NodeNumber weight 3, DefaultNormalizeScore] (HEADLINE_WEIGHT / HEADLINE_NORM);
+the reference's own w = 1 list without a normalizer is timed beside it.
+
 Modes (the headline line)
-  batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per batch per GPU, on pair_kernel, the
-              per-pair kernel (every (pod, node) pair's filter and score evaluated from the node's and
-              the pod's own bits, 32 pairs per 32-bit lane-op). With N GPUs the pods are sharded (each
-              rank its own 100k batches; no data-path collective) -> weak scaling. The K steps are K
-              independent batches (32 distinct pod batches, each with its own outputs, used in turn)
-              submitted from one host thread on one HIP stream through msh_schedule_batches_device,
-              MSH_BATCHES_PER_LAUNCH (32) batches per kernel launch: the submission a caller with
-              several drained batches ready makes.
+  batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per batch per GPU, on the per-pair kernel
+              (every (pod, node) pair's filter and score evaluated from the node's and the pod's own bits,
+              32 pairs per 32-bit lane-op). With N GPUs the pods are sharded (each rank its own 100k
+              batches; no data-path collective) -> weak scaling. The K steps are K independent batches
+              (32 distinct pod batches, each with its own outputs, used in turn) submitted from one host
+              thread on one HIP stream through msh_schedule_batches_device, MSH_BATCHES_PER_LAUNCH (32)
+              batches per kernel launch: the submission a caller with several drained batches ready makes.
   sequential  BASELINE C5: same sizes, one pod at a time with node-state commits.
   nodeshard   BASELINE C4 shape: the node table split over the ranks, per-pod first keys of every
               shard merged with an RCCL all-reduce(MAX), then decoded (--nodes 100000 --pods 1000000).
 
 With one GPU, rank 0 also measures, after the timed region, and reports as extra keys of the same
-line: generic_kernel (the explicit int64 score per pair, north_star's five stages) on the reference
-plugin list and on NodeNumber + a DEFAULT-normalized score column; the opt-in class-row kernel
-(pod verdicts read from per-class tables: reported apart, never as `value`); C3 with weight 3 +
-DefaultNormalizeScore, MIN-MAX and REVERSE; C5 sequential; C4 (100k nodes x 1M pods) on one GPU;
-C2; and the host-buffer path (e2e: the C-ABI call a cgo caller makes, PCIe included). Each is checked
-bit-exact against an independent checker (tests/closed_form.py; a sampled direct evaluation for the
-score-column list).
+line: the reference's w = 1 list and MIN-MAX / REVERSE at w = 3 on the same launches; generic_kernel
+(the explicit int64 score per pair, north_star's five stages) on the reference plugin list and on
+NodeNumber + a DEFAULT-normalized score column; the node-table maintenance (f2: msh_patch_nodes and
+msh_upload_nodes); C5 sequential; C4 (100k nodes x 1M pods) on one GPU; C2; and the host-buffer path
+(e2e: the C-ABI call a cgo caller makes, PCIe included). Each is checked bit-exact against an
+independent checker (tests/closed_form.py; a sampled direct evaluation for the score-column list).
 
 Launch: `python bench.py` (1 GPU) or
 `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N`.
@@ -65,10 +67,12 @@ PAIR_VALU_PER_WORD_LDS = 5.625
 # nearly every wave, so the other groups drop that reduction (5.5), and with the tolerates compaction 7
 # of a workgroup's 8 pod blocks fold X & nT into the first code compare (4.625)
 PAIR_VALU_PER_WORD_LDS_KX = 4.625
-# generic_kernel's main sweep on the reference list (NodeNumber only): per pair v_cmp_eq (suffix
-# digits), 2 v_cndmask (the lane's two weighted values), v_cmp_gt_i64 (strict first max), 3 v_cndmask
-# (best total, chunk-relative index): 7 VALU lane-ops per pair
-GEN_VALU_PER_PAIR_REF = 7.0
+# generic_kernel's main loop on the reference list (NodeNumber only, 32-bit keys; the ISA of
+# generic_kernel<0, false, false, 0, false>): per 16 nodes and 2 pod blocks, 32 v_cmp_eq_u32 (suffix digits),
+# 32 v_cndmask_b32 (the lane's two weighted keys), 32 v_bitop3_b32 (NodeUnschedulable clears an infeasible
+# key), 16 v_max3_u32 (the running maximum), 2 x (v_cmp_gt_u32 + v_cndmask_b32) for the chunk and a
+# v_mov_b64: 117 VALU per 32 pairs
+GEN_VALU_PER_PAIR_REF = 117 / 32
 PAIR_LDS_MAX_GROUPS = 128          # msh_pair.hip: tables the LDS-staged pair kernel takes (4-wave workgroups)
 PAIR_LDS_BIG_GROUPS = 416          # ... and with 16-wave workgroups
 PMC_FILE = ROOT / "profiles" / "r5_pmc_c3.json"
@@ -554,8 +558,8 @@ def median_us(fn, k: int) -> float:
 
 
 def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
-    """Secondary BASELINE configs, the generic and class-row kernels, and the host-buffer path, each
-    timed and checked bit-exact."""
+    """Secondary BASELINE configs, the other plugin lists, the generic kernel, the node-table maintenance
+    and the host-buffer path, each timed and checked bit-exact."""
     from closed_form import direct_plugins
     out = {}
     G = msh._native.BATCHES_PER_LAUNCH
@@ -638,8 +642,9 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     kname = "void msh::generic_kernel<0, false, false, 0, false>"
     rl = valu_roofline(kname, ms, float(n) * p * G, GEN_VALU_PER_PAIR_REF, cus,
                        pmc_entry("generic_ref", kname, n, p, G),
-                       "7 VALU per pair (generic_kernel's main sweep, NodeNumber only: v_cmp_eq, 2 v_cndmask for "
-                       "the weighted score, v_cmp_gt_i64, 3 v_cndmask for the running first maximum)")
+                       "3.66 VALU per pair (generic_kernel's main loop, NodeNumber only, 32-bit keys: v_cmp_eq, "
+                       "v_cndmask for the weighted key, v_bitop3 for NodeUnschedulable, half a v_max3 for the running "
+                       "maximum, 3 VALU per 16-node chunk and block)")
     gen["reference_list"] = {"kernel": kname, "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G,
                              "evals_per_s": n * p * G / (ms * 1e-3), "pods_per_s": p * G / (ms * 1e-3),
                              "check": "bit-exact vs closed form" if check_all() else "MISMATCH", "roofline": rl}
@@ -798,6 +803,8 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
                 state[0] ^= 1
 
             row[f"patch_{k}_nodes_us"] = median_us(patch, 50)
+            if state[0]:  # an odd number of flips: flip back to the uploaded table
+                patch()
         # the table after an even number of flips is the uploaded one: check a batch against it
         pd_t, pt_t = synth._make_pods_fast(4096, synth.SEED)[1:]
         ok = same(ctx.schedule_batch(pd_t, pt_t), closed_form_modes(u_t, nd_t, pd_t, pt_t, HEADLINE_WEIGHT, HEADLINE_NORM))
