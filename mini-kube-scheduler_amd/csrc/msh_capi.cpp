@@ -610,6 +610,7 @@ int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   // 32-bit totals when every feasible pair's total is bounded away from +-2^31 (biased by 2^31, the
   // key of a feasible pair is then never 0, the infeasible key); otherwise Go's int64
   g.w64 = bound > (long double)(((int64_t)1 << 31) - 2) ? 1 : 0;
+  g.nn24 = !g.nn_score || (long double)g.nn_weight * 100.0L < (long double)(1 << 24) ? 1 : 0;
   return MSH_OK;
 }
 

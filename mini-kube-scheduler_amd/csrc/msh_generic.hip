@@ -390,9 +390,25 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       }
     }
   }
+  // NodeNumber's key without a compare (32-bit keys, |c1 - c0| < 2^24: a.nn24): base + bit x delta, the bit
+  // (v_bfe_u32) of the pod's one-hot code set at the node's code, base / delta ordered so that delta >= 0,
+  // so the product and the add are one v_mad_u32_u24 and no lane mask (VCC) is written per pair
+  uint32_t nsel[GEN_BPW], nbase[GEN_BPW], ndelta[GEN_BPW];
+#pragma unroll
+  for (int b = 0; b < GEN_BPW; ++b) {
+    const uint32_t k1 = (uint32_t)L[b].k1, k0 = (uint32_t)L[b].k0, one = 1u << pcode[b];
+    const bool up = k1 >= k0;
+    nsel[b] = up ? one : ~one;
+    nbase[b] = up ? k0 : k1;
+    ndelta[b] = (up ? k1 - k0 : k0 - k1) & 0xFFFFFFu;
+  }
   // the key of one pair, from a node's staged (or re-read) values
-  auto pair_key = [&](int b, uint32_t code, uint32_t xm, Key ts, const double (&v)[NC]) -> Key {
-    Key t = code == pcode[b] ? L[b].k1 : L[b].k0;
+  auto pair_key = [&](int b, uint32_t code, uint32_t xm, Key ts, const double (&v)[NC], auto nnfast) -> Key {
+    Key t;
+    if constexpr (decltype(nnfast)::value && !W64)
+      t = nbase[b] + __builtin_amdgcn_ubfe(nsel[b], code, 1) * ndelta[b];
+    else
+      t = code == pcode[b] ? L[b].k1 : L[b].k0;
     if constexpr (TS) t += ts;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -410,48 +426,52 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     best[b] = 0;
     cidx[b] = -1;
   }
-  for (int t = 0; t < n_tiles; ++t) {
-    const int32_t t0 = t * TN, tn = min(TN, n - t0);
-    if (n_tiles > 1 || !staged) {
-      __syncthreads();
-      stage(t0);
-      __syncthreads();
-      staged = true;
-    }
-    int32_t lo, hi;
-    slice_of(tn, lo, hi);
-    auto node = [&](int32_t k, Key (&bst)[GEN_BPW]) {
-      const uint2 cx = s_cx[k];
-      Key ts = 0;
-      if constexpr (TS) ts = s_ts[k];
-      double v[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
-#pragma unroll
-      for (int b = 0; b < GEN_BPW; ++b) {
-        const Key key = pair_key(b, cx.x, cx.y, ts, v);
-        bst[b] = key > bst[b] ? key : bst[b];
+  auto main_pass = [&](auto nnfast) {
+    for (int t = 0; t < n_tiles; ++t) {
+      const int32_t t0 = t * TN, tn = min(TN, n - t0);
+      if (n_tiles > 1 || !staged) {
+        __syncthreads();
+        stage(t0);
+        __syncthreads();
+        staged = true;
       }
-    };
-    int32_t k = lo;
-    for (; k + GEN_CHUNK <= hi; k += GEN_CHUNK) {
-      Key prev[GEN_BPW];
+      int32_t lo, hi;
+      slice_of(tn, lo, hi);
+      auto node = [&](int32_t k, Key (&bst)[GEN_BPW]) {
+        const uint2 cx = s_cx[k];
+        Key ts = 0;
+        if constexpr (TS) ts = s_ts[k];
+        double v[NC];
 #pragma unroll
-      for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
+        for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
 #pragma unroll
-      for (int q = 0; q < GEN_CHUNK; ++q) node(k + q, best);
+        for (int b = 0; b < GEN_BPW; ++b) {
+          const Key key = pair_key(b, cx.x, cx.y, ts, v, nnfast);
+          bst[b] = key > bst[b] ? key : bst[b];
+        }
+      };
+      int32_t k = lo;
+      for (; k + GEN_CHUNK <= hi; k += GEN_CHUNK) {
+        Key prev[GEN_BPW];
 #pragma unroll
-      for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
+        for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
+#pragma unroll
+        for (int q = 0; q < GEN_CHUNK; ++q) node(k + q, best);
+#pragma unroll
+        for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
+      }
+      if (k < hi) {  // the slice's last, partial chunk
+        Key prev[GEN_BPW];
+#pragma unroll
+        for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
+        for (int32_t q = k; q < hi; ++q) node(q, best);
+#pragma unroll
+        for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
+      }
     }
-    if (k < hi) {  // the slice's last, partial chunk
-      Key prev[GEN_BPW];
-#pragma unroll
-      for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
-      for (int32_t q = k; q < hi; ++q) node(q, best);
-#pragma unroll
-      for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
-    }
-  }
+  };
+  if (!W64 && a.nn24) main_pass(std::true_type{});
+  else main_pass(std::false_type{});
   // the exact node: the first of the winning chunk whose key is the maximum (re-read from the uploaded
   // columns, the same arithmetic as the staged values)
   int32_t bidx[GEN_BPW];
@@ -471,7 +491,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
 #pragma unroll
       for (int c = 0; c < NC; ++c)
         v[c] = c < nnc ? 100.0 * (double)a.cols[(size_t)a.ncc[c] * a.col_stride + i] : 0.0;
-      if (pair_key(b, code, xm, ts, v) == best[b]) {
+      if (pair_key(b, code, xm, ts, v, std::false_type{}) == best[b]) {
         bidx[b] = i;
         break;
       }

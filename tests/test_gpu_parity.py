@@ -810,7 +810,9 @@ def test_multi_batch_full_launch(msh, oracle, n, norm, monkeypatch):
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(4242 + n + norm)
-    sizes = [100_000, 99_937, 100_003, 64, 0, 1, 99_999, 98_304] + [100_000 - 7 * k for k in range(24)]
+    # 32 batches of ~100k pods; at 40,000 nodes ~20k (still 10,000 waves: the 16-wave form's launch)
+    f = 1 if n <= 8192 else 5
+    sizes = [x // f for x in [100_000, 99_937, 100_003, 64, 0, 1, 99_999, 98_304] + [100_000 - 7 * k for k in range(24)]]
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
     u, nd, _, _ = _rand_case(rng, n, 1)
     pods = [_rand_case(rng, 1, p)[2:] for p in sizes]
