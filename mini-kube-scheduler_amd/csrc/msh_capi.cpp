@@ -610,7 +610,8 @@ int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   // 32-bit totals when every feasible pair's total is bounded away from +-2^31 (biased by 2^31, the
   // key of a feasible pair is then never 0, the infeasible key); otherwise Go's int64
   g.w64 = bound > (long double)(((int64_t)1 << 31) - 2) ? 1 : 0;
-  g.nn24 = !g.nn_score || (long double)g.nn_weight * 100.0L < (long double)(1 << 24) ? 1 : 0;
+  // NodeNumber's key without a compare (base + bit * delta on the 24-bit multiplier) when weight*100 fits
+  g.nn24 = c->dev.gen_nnkey && (!g.nn_score || (long double)g.nn_weight * 100.0L < (long double)(1 << 24)) ? 1 : 0;
   return MSH_OK;
 }
 
@@ -764,7 +765,8 @@ bool read_knobs(msh::DeviceInfo& d, std::string* err) {
                   knob("MSH_HOST_SYNC", {{"wait", 0}, {"poll", 1}}, &poll, err) &&
                   knob("MSH_BATCH_KERNEL", {{"pair", 0}, {"generic", 2}}, &d.batch_kernel, err) &&
                   knob("MSH_PAIR_PLANES", {{"auto", 0}, {"sgpr", 1}, {"lds", 2}}, &d.pair_planes, err) &&
-                  knob("MSH_PAIR_NOAX", {{"auto", -1}, {"1", 1}, {"0", 0}}, &d.pair_noax, err);
+                  knob("MSH_PAIR_NOAX", {{"auto", -1}, {"1", 1}, {"0", 0}}, &d.pair_noax, err) &&
+                  knob("MSH_GEN_NNKEY", {{"auto", 1}, {"select", 0}}, &d.gen_nnkey, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;
   d.host_sync_poll = poll;

@@ -35,6 +35,7 @@ namespace msh {
 constexpr int GEN_W = 8;       // waves per workgroup
 constexpr int GEN_BPW = 2;     // 64-pod blocks per wave: one LDS read of a node serves both
 constexpr int GEN_CHUNK = 16;  // nodes per first-maximum chunk
+constexpr uint32_t GEN_CODE_NONE = 10u;  // a node name without a suffix digit (matches no pod's code)
 constexpr double GEN_RCP_BIAS = 1.0 + 0x1p-49;
 constexpr uint32_t GEN_NONE = 0xFFFFFFFFu;
 
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       if (in) {
         const int dg = a.digit[i];
         xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
-        s_cx[k] = make_uint2((dg >= 0 && dg <= 9) ? (uint32_t)dg : CODE_NONE_NODE, xm);
+        s_cx[k] = make_uint2((dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE, xm);
         if constexpr (TS) {  // the node-only part: weight x raw of the columns without a normalizer
           Key ts = 0;
           for (int c = 0; c < a.nts; ++c) ts += (Key)a.cols[(size_t)a.tcc[c] * a.col_stride + i] * (Key)a.tw[c];
@@ -203,10 +204,21 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     int32_t mxn[GEN_BPW];   // NodeNumber: the largest raw score (10 / 0) over feasible nodes, -1 none
     uint32_t mnn[GEN_BPW];  // the smallest, all-ones none
     double dmx[GEN_BPW][NC], dmn[GEN_BPW][NC];
+    // NodeNumber's extents by pair flags: a node's class nk = code | 16 x unschedulable (code 0..9, 10 for
+    // none: nk < 27) selects, per pod, bit nk of a 64-bit map {hi, lo} holding at bit nk "feasible and
+    // matches" and at bit 31 + nk "feasible and does not match"; v_alignbit_b32 (the 64-bit funnel shift
+    // by nk) brings both to bits 0 and 31 of one dword, ORed into the pod's flags: 2 VALU per pair
+    uint32_t fhi[GEN_BPW], flo[GEN_BPW], fl[GEN_BPW];
 #pragma unroll
     for (int b = 0; b < GEN_BPW; ++b) {
       mxn[b] = -1;
       mnn[b] = 0xFFFFFFFFu;
+      const uint32_t mt = pcode[b] <= 9 ? (0x10001u << pcode[b]) : 0u;  // the pod's code, either unschedulable bit
+      const uint32_t fe = ntol[b] ? 0x7FFu : 0x7FF07FFu;                 // the classes that pass the filter
+      const uint32_t m = mt & fe, nm = ~mt & fe;
+      flo[b] = m | (nm << 31);
+      fhi[b] = nm >> 1;
+      fl[b] = 0u;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         dmx[b][c] = -__builtin_inf();
@@ -225,18 +237,16 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
         }
         int32_t lo, hi;
         slice_of(tn, lo, hi);
+#pragma unroll 8
         for (int32_t k = lo; k < hi; ++k) {
           const uint2 cx = s_cx[k];
+          const uint32_t nk = bop3_or_and(cx.x, cx.y, 16u);  // code | (xm & 16)
           double v[NC];
 #pragma unroll
           for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
 #pragma unroll
           for (int b = 0; b < GEN_BPW; ++b) {
-            if constexpr (NNX) {  // NodeNumber's raw score, all-ones where the pair is infeasible
-              const uint32_t raw = bop3_or_and(cx.x == pcode[b] ? 10u : 0u, cx.y, ntol[b]);
-              mxn[b] = max(mxn[b], (int32_t)raw);
-              mnn[b] = umin(mnn[b], raw);
-            }
+            if constexpr (NNX) fl[b] |= __builtin_amdgcn_alignbit(fhi[b], flo[b], nk);
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
               if (c >= nnc) break;
@@ -250,6 +260,12 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     };
     if (nn_ext) ext_scan(std::true_type{});
     else ext_scan(std::false_type{});
+#pragma unroll
+    for (int b = 0; b < GEN_BPW; ++b) {  // raw 10 on a feasible match, 0 on a feasible non-match
+      const bool fm = fl[b] & 1u, fnm = fl[b] >> 31;
+      mxn[b] = fm ? 10 : (fnm ? 0 : -1);
+      mnn[b] = fnm ? 0u : (fm ? 10u : 0xFFFFFFFFu);
+    }
     // slice waves of a pod group meet in LDS (every wave of the group takes the merged extents)
     if (S > 1) {
       int32_t* m_nn = reinterpret_cast<int32_t*>(s_merge);                       // [GEN_W][BPW][2][64]
@@ -482,7 +498,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     const int32_t e = min(cidx[b] + GEN_CHUNK, n);
     for (int32_t i = cidx[b]; i < e; ++i) {
       const int dg = a.digit[i];
-      const uint32_t code = (dg >= 0 && dg <= 9) ? (uint32_t)dg : CODE_NONE_NODE;
+      const uint32_t code = (dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE;
       const uint32_t xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
       Key ts = 0;
       if constexpr (TS)

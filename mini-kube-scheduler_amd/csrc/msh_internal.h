@@ -54,6 +54,7 @@ struct DeviceInfo {
   // against 89.0 us per 32-batch C3 launch), 0 for the identity-like modes (77.3-78.3 against
   // 80.9-81.2), profiles/r4_ab_pair_planes.txt
   int pair_noax = -1;
+  int gen_nnkey = 1;  // MSH_GEN_NNKEY: generic_kernel's compare-free NodeNumber key (1) or the select (0)
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit

@@ -522,9 +522,12 @@ __device__ __forceinline__ void group_firsts_lds(const uint4* __restrict__ s_tab
 // 4-wave workgroups (2% faster; in 16-wave ones its 8.3 KB of static LDS on top of a table of up to 78 KB
 // would leave one workgroup per CU) and load both groups' scalar planes of a step under one wait (HY 2,
 // 3% faster); the identity-like modes wait per group (HY 1).
-// (A software-pipelined scan — group g-1's LDS and scalar planes requested by one asm block before group
-// g's v_bitop3 chains, one explicit wait per group — ran slower: 81.4 against 76.7 us per 32-batch C3
-// launch in the identity-like modes, 80.3 against 80.0 in MINMAX, gpurun_out r5c / DESIGN.md §4.2.)
+// (Two attempts to hide the LDS broadcast latency lost their A/B, DESIGN.md §4.2: a software-pipelined
+// scan — group g-1's LDS and scalar planes requested by one asm block before group g's v_bitop3 chains,
+// one explicit wait per group — ran 81.4 against 76.7 us per 32-batch C3 launch in the identity-like
+// modes, 80.3 against 80.0 in MINMAX; the identity-like 4-wave form compiled for 8 waves per SIMD
+// (amdgpu_waves_per_eu(8): 64 VGPRs, 36 B of spills outside the scan loop, against 78 VGPRs and 6 waves)
+// ran 78.1 against 78.0 at w=3 DEFAULT and 78.6 against 78.2 at w=1 NONE.)
 template <bool SHARD, bool KX, int W>
 __global__ __launch_bounds__(W * WAVE) void pair_lds_kernel(PairArgs a) {
   constexpr bool CMP = KX && W == PL_WAVES;

@@ -1034,6 +1034,7 @@ W32_LISTS = [
     [("NodeNumber", 1, 1), ("ScoreColumn3", 5, 0)],           # a column without a normalizer (node-only sum)
     [("ScoreColumn2", 2, 0), ("ScoreColumn1", 1, 3), ("ScoreColumn3", 3, 0), ("NodeNumber", 4, 2)],
     [("ScoreColumn1", 1, 1), ("ScoreColumn3", 1, 3)],         # two normalizing columns: the general form
+    [("NodeNumber", 200_000, 1)],  # weight x 100 >= 2^24: NodeNumber's key by the select, not base + bit x delta
 ]
 
 
@@ -1058,6 +1059,31 @@ def test_generic_small_totals(msh, gpu_ctx, oracle, lst):
             gpu_ctx.upload_score_column(f"ScoreColumn{k}", cols[k])
         _assert_same(gpu_ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols),
                      f"w32 {pl} n={n} p={p}")
+
+
+@pytest.mark.parametrize("lst", [0, 1, 3])
+def test_generic_nn_key_select(msh, oracle, lst, monkeypatch):
+    """MSH_GEN_NNKEY=select (read once by msh_create): NodeNumber's key by the compare and select instead of
+    the compare-free base + bit x delta, on the 32-bit lists, at C3 size and on a multi-tile table."""
+    monkeypatch.setenv("MSH_GEN_NNKEY", "select")
+    rng = np.random.default_rng(900 + lst)
+    pl = W32_LISTS[lst]
+    names = [nm for nm, _, _ in pl]
+    ps = oracle.PluginSet(filters=["NodeUnschedulable"], prescore=["NodeNumber"], score=names,
+                          weights=[w for _, w, _ in pl], normalize=[m for _, _, m in pl])
+    with msh.DeviceContext(0) as ctx:
+        ctx.set_plugins(ps.filters, ps.prescore, [msh.ScorePluginConfig(nm, w, msh.Normalize(m)) for nm, w, m in pl])
+        for n, p in [(5000, 100_000), (33_000, 700)]:
+            u, nd, pd, pt = _rand_case(rng, n, p, p_unsched=0.3, p_tol=0.2)
+            cols = _cols(rng, n)
+            ctx.upload_nodes(u, nd)
+            for k in range(4):
+                ctx.upload_score_column(f"ScoreColumn{k}", cols[k])
+            _assert_same(ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols, threads=8),
+                         f"select {pl} n={n} p={p}")
+    monkeypatch.setenv("MSH_GEN_NNKEY", "bfe")
+    with pytest.raises(msh.MshError):
+        msh.DeviceContext(0)
 
 
 def test_generic_int64_min_totals(msh, gpu_ctx, oracle):
