@@ -642,12 +642,23 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     kname = "void msh::generic_kernel<0, false, false, 0, false>"
     rl = valu_roofline(kname, ms, float(n) * p * G, GEN_VALU_PER_PAIR_REF, cus,
                        pmc_entry("generic_ref", kname, n, p, G),
-                       "3.66 VALU per pair (generic_kernel's main loop, NodeNumber only, 32-bit keys: v_cmp_eq, "
-                       "v_cndmask for the weighted key, v_bitop3 for NodeUnschedulable, half a v_max3 for the running "
-                       "maximum, 3 VALU per 16-node chunk and block)")
+                       "3.66 VALU per pair (generic_kernel's main loop, NodeNumber only, 32-bit keys: v_bfe_u32 and "
+                       "v_mad_u32_u24 for the weighted key, v_bitop3 for NodeUnschedulable, half a v_max3 for the "
+                       "running maximum, 3 VALU per 16-node chunk and block)")
     gen["reference_list"] = {"kernel": kname, "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G,
                              "evals_per_s": n * p * G / (ms * 1e-3), "pods_per_s": p * G / (ms * 1e-3),
                              "check": "bit-exact vs closed form" if check_all() else "MISMATCH", "roofline": rl}
+    # the headline list on generic_kernel: the extents pass (NodeNumber's pair flags: v_alignbit + v_or per
+    # pair, one v_bitop3 per node and wave) before the main pass
+    gctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                     [msh.ScorePluginConfig(msh.NODE_NUMBER, HEADLINE_WEIGHT, msh.Normalize(HEADLINE_NORM))])
+    ms = run_multi(gctx, R=5)
+    entry = pmc_entry("generic_hl", kname, n, p, G, plugin_tag(HEADLINE_WEIGHT, HEADLINE_NORM))
+    gen["headline_list"] = {
+        "kernel": kname, "plugins": f"score=[NodeNumber w={HEADLINE_WEIGHT} normalize={NORM_NAMES[HEADLINE_NORM]}]",
+        "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
+        "lane_ops_per_eval_counter": entry["SQ_INSTS_VALU"] * 64 / (float(n) * p * G) if entry else None,
+        "check": "bit-exact vs closed form" if check_all(HEADLINE_WEIGHT, HEADLINE_NORM) else "MISMATCH"}
     col = (np.arange(n, dtype=np.int64) * 7919) % 1000 - 300
     plugins = [("NodeNumber", 1, 0), ("ScoreColumn0", 2, 1)]
     gctx.upload_score_column("ScoreColumn0", col)

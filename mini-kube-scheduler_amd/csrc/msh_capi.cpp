@@ -578,6 +578,7 @@ int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   g.has_nu = c->pp.has_nu_filter;
   g.nn_prescore = c->pp.nn_prescore;
   long double bound = 0;  // the largest |total| a feasible pair can reach
+  bool c24 = true;        // every normalizing column's weight and normalized score below 2^23 in magnitude
   for (size_t k = 0; k < c->score_ids.size(); ++k) {
     const int32_t id = c->score_ids[k];
     const int32_t mode = c->normalize[k];
@@ -603,13 +604,16 @@ int generic_args(msh_ctx* c, msh::GenericArgs& g) {
         ++g.nts;
       }
       ++g.ncol;
-      bound += (long double)w * score_bound(true, mode, t.col_lo[col], t.col_hi[col]);
+      const long double sb = score_bound(true, mode, t.col_lo[col], t.col_hi[col]);
+      bound += (long double)w * sb;
+      if (mode != MSH_NORMALIZE_NONE) c24 = c24 && w < (1 << 23) && sb < (long double)(1 << 23);
     }
     g.need_ext = g.need_ext || mode != MSH_NORMALIZE_NONE;
   }
   // 32-bit totals when every feasible pair's total is bounded away from +-2^31 (biased by 2^31, the
-  // key of a feasible pair is then never 0, the infeasible key); otherwise Go's int64
-  g.w64 = bound > (long double)(((int64_t)1 << 31) - 2) ? 1 : 0;
+  // key of a feasible pair is then never 0, the infeasible key) and each normalizing column's term is a
+  // 24-bit signed product; otherwise Go's int64
+  g.w64 = bound > (long double)(((int64_t)1 << 31) - 2) || !c24 ? 1 : 0;
   // NodeNumber's key without a compare (base + bit * delta on the 24-bit multiplier) when weight*100 fits
   g.nn24 = c->dev.gen_nnkey && (!g.nn_score || (long double)g.nn_weight * 100.0L < (long double)(1 << 24)) ? 1 : 0;
   return MSH_OK;

@@ -107,9 +107,10 @@ __device__ __forceinline__ GKey<W64> col_term(double v, double b, double r, GKey
     const int64_t n = (int64_t)__builtin_fmin(__builtin_fmax(q, -0x1p62), 0x1p62);
     return (uint64_t)n * cw;
   } else {
-    // |n| within the host's bound on a feasible pair (v_cvt_i32_f64 saturates on the others)
+    // |n| and |w| below 2^23 on a feasible pair (the host's bound, GenericArgs::w64): the signed 24-bit
+    // multiply (full rate, where v_mul_lo_u32 is quarter rate); v_cvt_i32_f64 saturates on the others
     const int32_t n = (int32_t)q;
-    return (uint32_t)n * cw;
+    return (uint32_t)__mul24(n, (int32_t)cw);
   }
 }
 

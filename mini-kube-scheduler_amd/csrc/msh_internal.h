@@ -165,7 +165,8 @@ struct GenericArgs {
   int32_t nts, tcc[GEN_COLS];
   int64_t tw[GEN_COLS];
   int32_t need_ext;        // some plugin normalizes: the extent pass runs
-  int32_t w64;             // 64-bit totals (the host could not bound every feasible total within 31 bits)
+  int32_t w64;             // 64-bit totals (the host could not bound every feasible total within 31 bits, or a
+                           // normalizing column's weight or normalized score reaches 2^23)
   int32_t nn24;            // NodeNumber's two weighted values differ by less than 2^24 (32-bit keys: no compare)
   int32_t nb;              // batches (mode 0: up to MULTI_MAX; sharded modes: 1)
   int64_t node_base;       // sharded modes: global index of local node 0

@@ -8,6 +8,7 @@ only when all of them match what it timed):
   pair_multi_ref  the same with the reference's own list (w=1, no normalizer)
   pair_minmax     the same, MIN-MAX w=3;  pair_reverse: REVERSE w=3
   generic_ref     generic_kernel on the reference list (w=1 NONE), 32 batches
+  generic_hl      generic_kernel on the headline list (w=3 DefaultNormalizeScore: extents pass + main pass), 32 batches
   generic_col     generic_kernel on NodeNumber + a DEFAULT-normalized score column, 32 batches
   sequential      seq_kernel at C5 (headline list)
 FETCH_SIZE / WRITE_SIZE are KiB (x 1024); FETCH_SIZE is reported raw and with MI355X_MICROARCH.md's x2
@@ -57,6 +58,7 @@ for mode, prefix, tags, nb, plug in (
         ("pair_minmax", "msh::pair", ("k_sq", "k_fetch", "k_write"), NB, tag_of(3, 3)),
         ("pair_reverse", "msh::pair", ("v_sq", "v_fetch", "v_write"), NB, tag_of(3, 2)),
         ("generic_ref", "msh::generic_kernel", ("g_sq", "g_sq2", "g_grbm", "g_fetch", "g_write"), NB, tag_of(1, 0)),
+        ("generic_hl", "msh::generic_kernel", ("gh_sq",), NB, tag_of(3, 1)),
         ("generic_col", "msh::generic_kernel", ("gc_sq", "gc_sq2"), NB, tag_of(1, 0) + " + ScoreColumn0 w=2 norm=1"),
         ("sequential", "msh::seq_kernel", ("s_sq",), 1, tag_of(3, 1))):
     e = {"nodes": N, "pods": P, "batches_per_launch": nb, "plugins": plug, "launches_per_counter": {}}
@@ -96,7 +98,8 @@ for mode, prefix, tags, nb, plug in (
 for tag, prefix in (("stats", "msh::pair"), ("stats_k20", "msh::pair"),
                     ("stats_multi", "msh::pair"), ("stats_ref", "msh::pair"), ("stats_kx", "msh::pair"),
                     ("stats_rev", "msh::pair"), ("stats_single", "msh::pair"),
-                    ("stats_generic", "msh::generic_kernel"), ("stats_generic_col", "msh::generic_kernel"),
+                    ("stats_generic", "msh::generic_kernel"), ("stats_generic_hl", "msh::generic_kernel"),
+                    ("stats_generic_col", "msh::generic_kernel"),
                     ("stats_seq", "msh::seq_kernel")):
     name, avg, calls = stats_avg_ns(tag, prefix)
     if name:

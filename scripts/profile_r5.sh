@@ -5,7 +5,8 @@
 #  2. --kernel-trace --stats of each hot kernel alone (scripts/run_batch.py, C3: 5,000 nodes x 100,000
 #     pods per batch): the per-pair kernel 32 batches per launch with the headline plugins (NodeNumber w=3
 #     DefaultNormalizeScore), the reference's w=1 list, MIN-MAX and REVERSE at w=3; generic_kernel on the
-#     reference list and on NodeNumber + a DEFAULT-normalized column; seq_kernel (C5, headline plugins);
+#     reference list, on the headline list and on NodeNumber + a DEFAULT-normalized column; seq_kernel (C5,
+#     headline plugins);
 #  3. one --pmc pass per counter set (never combined with tracing).
 # Summary: scripts/pmc_r5_summary.py -> profiles/r5_pmc_c3.json (bench.py reads it for the counter
 # fractions and the HBM traffic of its roofline).
@@ -36,6 +37,7 @@ if [ "${SKIP_TRACE:-0}" != 1 ]; then
   tr stats_rev multi 3 2 pair || exit 1
   tr stats_single batch 3 1 pair || exit 1
   tr stats_generic generic 1 0 generic || exit 1
+  tr stats_generic_hl generic 3 1 generic || exit 1
   tr stats_generic_col generic_col 1 0 pair || exit 1
   tr stats_seq sequential 3 1 pair || exit 1
 fi
@@ -66,6 +68,7 @@ pass g_sq2 generic 1 0 generic $SQ2 || exit 1
 pass g_grbm generic 1 0 generic GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
 pass g_fetch generic 1 0 generic FETCH_SIZE || exit 1
 pass g_write generic 1 0 generic WRITE_SIZE || exit 1
+pass gh_sq generic 3 1 generic $SQ1 || exit 1
 pass gc_sq generic_col 1 0 pair $SQ1 || exit 1
 pass gc_sq2 generic_col 1 0 pair $SQ2 || exit 1
 pass s_sq sequential 3 1 pair $SQ1 || exit 1
