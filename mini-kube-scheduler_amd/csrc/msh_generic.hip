@@ -37,6 +37,10 @@ constexpr int GEN_BPW = 2;     // 64-pod blocks per wave: one LDS read of a node
 constexpr int GEN_CHUNK = 16;  // nodes per first-maximum chunk
 constexpr uint32_t GEN_CODE_NONE = 10u;  // a node name without a suffix digit (matches no pod's code)
 constexpr double GEN_RCP_BIAS = 1.0 + 0x1p-49;
+// two nodes' staged values per LDS read: ds_read_b128 moves 16 B per lane in 4 LDS cycles, where the
+// ds_read2_b64 the compiler forms from two 8-B reads takes 8 (MI355X_MICROARCH.md §LDS)
+typedef uint32_t gen_u4 __attribute__((ext_vector_type(4)));
+typedef double gen_d2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t GEN_NONE = 0xFFFFFFFFu;
 
 // NormalizeScore of one raw score given the pod's extent of that plugin over its feasible nodes
@@ -238,13 +242,8 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
         }
         int32_t lo, hi;
         slice_of(tn, lo, hi);
-#pragma unroll 8
-        for (int32_t k = lo; k < hi; ++k) {
-          const uint2 cx = s_cx[k];
+        auto ext_node = [&](uint2 cx, const double (&v)[NC]) {
           const uint32_t nk = bop3_or_and(cx.x, cx.y, 16u);  // code | (xm & 16)
-          double v[NC];
-#pragma unroll
-          for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
 #pragma unroll
           for (int b = 0; b < GEN_BPW; ++b) {
             if constexpr (NNX) fl[b] |= __builtin_amdgcn_alignbit(fhi[b], flo[b], nk);
@@ -256,6 +255,28 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
               if (MMX) dmn[b][c] = vmin_f64(dmn[b][c], vv);
             }
           }
+        };
+        int32_t k = lo;  // lo is a multiple of GEN_CHUNK: node pairs are 16-B aligned
+#pragma unroll 4
+        for (; k + 1 < hi; k += 2) {
+          const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k >> 1];
+          double v0[NC], v1[NC];
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            v0[c] = v1[c] = 0.0;
+            if (c >= nnc) continue;
+            const gen_d2 w = reinterpret_cast<const gen_d2*>(s_v + (size_t)c * TN)[k >> 1];
+            v0[c] = w.x;
+            v1[c] = w.y;
+          }
+          ext_node(make_uint2(c2.x, c2.y), v0);
+          ext_node(make_uint2(c2.z, c2.w), v1);
+        }
+        if (k < hi) {
+          double v[NC];
+#pragma unroll
+          for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
+          ext_node(s_cx[k], v);
         }
       }
     };
@@ -454,18 +475,40 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       }
       int32_t lo, hi;
       slice_of(tn, lo, hi);
-      auto node = [&](int32_t k, Key (&bst)[GEN_BPW]) {
-        const uint2 cx = s_cx[k];
+      auto node_v = [&](uint2 cx, Key ts, const double (&v)[NC]) {
+#pragma unroll
+        for (int b = 0; b < GEN_BPW; ++b) {
+          const Key key = pair_key(b, cx.x, cx.y, ts, v, nnfast);
+          best[b] = key > best[b] ? key : best[b];
+        }
+      };
+      auto node = [&](int32_t k) {
         Key ts = 0;
         if constexpr (TS) ts = s_ts[k];
         double v[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
-#pragma unroll
-        for (int b = 0; b < GEN_BPW; ++b) {
-          const Key key = pair_key(b, cx.x, cx.y, ts, v, nnfast);
-          bst[b] = key > bst[b] ? key : bst[b];
+        node_v(s_cx[k], ts, v);
+      };
+      // two nodes per LDS read (k even: a chunk starts at a multiple of GEN_CHUNK)
+      auto node_pair = [&](int32_t k) {
+        const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k >> 1];
+        Key ts0 = 0, ts1 = 0;
+        if constexpr (TS) {
+          ts0 = s_ts[k];
+          ts1 = s_ts[k + 1];
         }
+        double v0[NC], v1[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          v0[c] = v1[c] = 0.0;
+          if (c >= nnc) continue;
+          const gen_d2 w = reinterpret_cast<const gen_d2*>(s_v + (size_t)c * TN)[k >> 1];
+          v0[c] = w.x;
+          v1[c] = w.y;
+        }
+        node_v(make_uint2(c2.x, c2.y), ts0, v0);
+        node_v(make_uint2(c2.z, c2.w), ts1, v1);
       };
       int32_t k = lo;
       for (; k + GEN_CHUNK <= hi; k += GEN_CHUNK) {
@@ -473,7 +516,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
 #pragma unroll
-        for (int q = 0; q < GEN_CHUNK; ++q) node(k + q, best);
+        for (int q = 0; q < GEN_CHUNK; q += 2) node_pair(k + q);
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
       }
@@ -481,7 +524,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
         Key prev[GEN_BPW];
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
-        for (int32_t q = k; q < hi; ++q) node(q, best);
+        for (int32_t q = k; q < hi; ++q) node(q);
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
       }
