@@ -256,22 +256,26 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
             }
           }
         };
-        int32_t k = lo;  // lo is a multiple of GEN_CHUNK: node pairs are 16-B aligned
-#pragma unroll 4
-        for (; k + 1 < hi; k += 2) {
-          const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k >> 1];
+        auto ext_pair = [&](int32_t k2) {  // nodes 2 k2, 2 k2 + 1 (16-B aligned)
+          const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k2];
           double v0[NC], v1[NC];
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
             v0[c] = v1[c] = 0.0;
             if (c >= nnc) continue;
-            const gen_d2 w = reinterpret_cast<const gen_d2*>(s_v + (size_t)c * TN)[k >> 1];
+            const gen_d2 w = reinterpret_cast<const gen_d2*>(s_v + (size_t)c * TN)[k2];
             v0[c] = w.x;
             v1[c] = w.y;
           }
           ext_node(make_uint2(c2.x, c2.y), v0);
           ext_node(make_uint2(c2.z, c2.w), v1);
+        };
+        int32_t k = lo;  // lo is a multiple of GEN_CHUNK
+        for (; k + GEN_CHUNK <= hi; k += GEN_CHUNK) {  // a chunk's reads issued together
+#pragma unroll
+          for (int q = 0; q < GEN_CHUNK / 2; ++q) ext_pair((k >> 1) + q);  // one base, immediate offsets
         }
+        for (; k + 1 < hi; k += 2) ext_pair(k >> 1);
         if (k < hi) {
           double v[NC];
 #pragma unroll
@@ -491,19 +495,19 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
         node_v(s_cx[k], ts, v);
       };
       // two nodes per LDS read (k even: a chunk starts at a multiple of GEN_CHUNK)
-      auto node_pair = [&](int32_t k) {
-        const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k >> 1];
+      auto node_pair = [&](int32_t k2) {  // nodes 2 k2, 2 k2 + 1
+        const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k2];
         Key ts0 = 0, ts1 = 0;
         if constexpr (TS) {
-          ts0 = s_ts[k];
-          ts1 = s_ts[k + 1];
+          ts0 = s_ts[2 * k2];
+          ts1 = s_ts[2 * k2 + 1];
         }
         double v0[NC], v1[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           v0[c] = v1[c] = 0.0;
           if (c >= nnc) continue;
-          const gen_d2 w = reinterpret_cast<const gen_d2*>(s_v + (size_t)c * TN)[k >> 1];
+          const gen_d2 w = reinterpret_cast<const gen_d2*>(s_v + (size_t)c * TN)[k2];
           v0[c] = w.x;
           v1[c] = w.y;
         }
@@ -516,7 +520,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
 #pragma unroll
-        for (int q = 0; q < GEN_CHUNK; q += 2) node_pair(k + q);
+        for (int q = 0; q < GEN_CHUNK / 2; ++q) node_pair((k >> 1) + q);
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
       }
