@@ -520,7 +520,18 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
 #pragma unroll
-        for (int q = 0; q < GEN_CHUNK / 2; ++q) node_pair((k >> 1) + q);
+        for (int q = 0; q < GEN_CHUNK / 2; ++q) {
+          // with score columns two nodes per ds_read_b128 (4.30 against 4.43 ms per 32-batch C3 launch on
+          // NodeNumber + a DEFAULT column, one box); NodeNumber alone keeps the compiler's ds_read2_b64 pairs
+          // (1.54 against 1.57 ms on the reference list; profiles/ab/r5_MSH_GEN_LDS128_*)
+          if constexpr (NNC > 0 || TS) {
+            node_pair((k >> 1) + q);
+          } else {
+            node(k + 2 * q);
+            node(k + 2 * q + 1);
+          }
+        }
+
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) cidx[b] = best[b] > prev[b] ? t0 + k : cidx[b];
       }
