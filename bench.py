@@ -68,11 +68,14 @@ PAIR_VALU_PER_WORD_LDS = 5.625
 # of a workgroup's 8 pod blocks fold X & nT into the first code compare (4.625)
 PAIR_VALU_PER_WORD_LDS_KX = 4.625
 # generic_kernel's main loop on the reference list (NodeNumber only, 32-bit keys; the ISA of
-# generic_kernel<0, false, false, 0, false>): per 16 nodes and 2 pod blocks, 32 v_cmp_eq_u32 (suffix digits),
-# 32 v_cndmask_b32 (the lane's two weighted keys), 32 v_bitop3_b32 (NodeUnschedulable clears an infeasible
-# key), 16 v_max3_u32 (the running maximum), 2 x (v_cmp_gt_u32 + v_cndmask_b32) for the chunk and a
-# v_mov_b64: 117 VALU per 32 pairs
+# generic_kernel<0, false, false, 0, false>): per 16 nodes and 2 pod blocks, 32 v_bfe_u32 (the pod's one-hot
+# code bit at the node's digit), 32 v_mad_u32_u24 (the lane's weighted key), 32 v_bitop3_b32
+# (NodeUnschedulable clears an infeasible key), 16 v_max3_u32 (the running maximum), 2 x (v_cmp_gt_u32 +
+# v_cndmask_b32) for the chunk and a v_mov_b64: 117 VALU per 32 pairs
 GEN_VALU_PER_PAIR_REF = 117 / 32
+# seq_kernel's scan (msh_seq.hip), per 32-node word and pod: v_xor + 3 v_bitop3 (the code compare) + one
+# v_bitop3 (NodeUnschedulable): 5 VALU per 32 pairs
+SEQ_VALU_PER_WORD = 5
 PAIR_LDS_MAX_GROUPS = 128          # msh_pair.hip: tables the LDS-staged pair kernel takes (4-wave workgroups)
 PAIR_LDS_BIG_GROUPS = 416          # ... and with 16-wave workgroups
 PMC_FILE = ROOT / "profiles" / "r5_pmc_c3.json"
@@ -106,14 +109,19 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
     return f"void msh::pair_kernel<{sl}, {b(shard)}, {b(kx)}>"
 
 
-def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
+def seq_shape(n_nodes: int, cap: bool = False):
+    """seq_kernel's register layout for a table (launch_sequential): words per lane RS, scanning waves NW."""
     words = max(-(-n_nodes // 1024) * 1024, 1024) // 32
     rs = lambda nw: -(-words // (nw * 64))
     nw = 1 if rs(1) <= 4 else 4 if rs(4) <= 4 else (16 if cap else 15)
     r = rs(nw)
     rsv = {1: [1, 2, 3, 4], 4: [2, 4]}.get(nw, [4, 8] if cap else [4, 8, 12])
-    r = next(v for v in rsv if r <= v)
-    u = 4 if nw == 1 and not cap else 1  # SEQ_AHEAD
+    return next(v for v in rsv if r <= v), nw
+
+
+def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
+    r, nw = seq_shape(n_nodes, cap)
+    u = 1 if cap else 4  # SEQ_AHEAD: pods decided per step without a capacity
     return f"void msh::seq_kernel<{r}, {nw}, {str(kx).lower()}, {str(cap).lower()}, {u}>"
 
 
@@ -482,11 +490,24 @@ def valu_roofline(kname, launch_ms, evals, model_lane_ops_per_eval, cus, entry, 
     }
 
 
-def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
+def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=False):
     """Roofline of the dominant kernel, per launch: algorithmic work of one launch / the launch's
     average duration, measured with HIP events at the kernel's start and completion (bench.py main),
     the quantity rocprofv3's per-kernel average reports."""
     launch_s = launch_ms * 1e-3
+    if mode == "sequential" and not serial:
+        # Without a capacity the pods run in blocks of consecutive pods, one workgroup each (a wave per
+        # block walks its pods in order, every pod against the whole register-resident table): VALU-bound
+        # over the chip. Model: 5 VALU per 32-node word and pod (the pair evaluation; the first-hit
+        # reduction and the per-pod decode are in the counter form).
+        kname = seq_kernel_label(n_local)
+        r, nw = seq_shape(n_local)
+        model = SEQ_VALU_PER_WORD * nw * 64 * r / float(n_local)
+        return valu_roofline(kname, launch_ms, float(n_local) * p, model, cus,
+                             pmc_entry("sequential", kname, n_local, p, 1, plugin_tag(HEADLINE_WEIGHT, HEADLINE_NORM)),
+                             f"{SEQ_VALU_PER_WORD} VALU per 32-node word and pod (seq_kernel's scan: v_xor and three "
+                             "v_bitop3 for the code compare, one v_bitop3 for NodeUnschedulable), over the "
+                             f"{nw} x 64 lanes x {r} words of the register-resident table")
     if mode == "sequential":
         # One wave decides the pods in order; alone on its SIMD it issues about one instruction per
         # 4 cycles of any kind (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so the floor
@@ -494,7 +515,7 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus):
         # this kernel at C5) x 4 cycles at 2.4 GHz. That is an issue floor of the code as written,
         # not a hardware roofline: reported as issue_floor_frac, not frac.
         kname = seq_kernel_label(n_local)
-        entry = pmc_entry("sequential", kname, n_local, p, 1)
+        entry = pmc_entry("sequential_serial", kname, n_local, p, 1)
         instr = (entry.get("SQ_INSTS_VALU", 0) + entry.get("SQ_INSTS_SALU", 0)) / p if entry else None
         floor_us = instr * 4 / 2.4e3 if instr else None
         achieved = launch_ms * 1e3 / p
@@ -575,13 +596,14 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     def same(a, b):
         return all((x == y).all() for x, y in zip(a, b))
 
-    def new_ctx(kernel=None):
-        if kernel:
-            os.environ["MSH_BATCH_KERNEL"] = kernel  # read once by msh_create
+    def new_ctx(kernel=None, env=None):
+        env = dict(env or {}, **({"MSH_BATCH_KERNEL": kernel} if kernel else {}))
+        os.environ.update(env)  # read once by msh_create
         try:
             c = msh.DeviceContext(dev.index or 0)
         finally:
-            os.environ.pop("MSH_BATCH_KERNEL", None)
+            for k in env:
+                os.environ.pop(k, None)
         c.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                       [msh.ScorePluginConfig(msh.NODE_NUMBER, HEADLINE_WEIGHT, msh.Normalize(HEADLINE_NORM))])
         return c
@@ -778,22 +800,43 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
                    "thread) in front of the pinned call; 'pinned_no_scores' passes out_score = NULL")
     out["e2e"] = e2e
 
-    # ---- C5: 5k x 100k sequential commit (one launch = the whole 100k-pod batch) ----
+    # ---- C5: 5k x 100k sequential commit (one launch = the whole 100k-pod batch), as the product runs
+    # it (no capacity: blocks of consecutive pods, one workgroup each, every block in order) and with
+    # the whole batch in one workgroup (MSH_SEQ_SPLIT=serial: the literal serial order, latency-bound);
+    # each launch timed by its own kernel events ----
     b = dbufs(pd, pt)
-    s1 = Streams(torch, dev, 1)
-    seq = lambda i, sh: ctx.schedule_sequential_device(p, b[0].data_ptr(), b[1].data_ptr(), 0, *[t.data_ptr() for t in b[2:]], sh)
-    s1.time(seq, 1)
-    ctx.reset_node_pod_counts()
-    ms = s1.time(seq, 3)
-    counts = ctx.node_pod_counts()
-    g = got(b)
-    placed = g[2] == 0
-    ok = same(g, want) and (counts == 3 * np.bincount(g[0][placed], minlength=n)).all()
-    out["c5_sequential"] = {"kernel": seq_kernel_label(n), "ms_per_step": ms, "us_per_pod": ms * 1e3 / p,
-                            "pods_per_s": p / (ms * 1e-3), "evals_per_s": n * p / (ms * 1e-3),
-                            "check": ("seq == batch (closed form), node counts == 3 x placements" if ok else "MISMATCH"),
-                            "roofline": make_roofline("sequential", n, p, ms, 1, cus)}
-    ctx.close()
+
+    def c5(c, R):
+        seq = lambda: c.schedule_sequential_device(p, b[0].data_ptr(), b[1].data_ptr(), 0,
+                                                   *[t.data_ptr() for t in b[2:]], sh)
+        seq()
+        torch.cuda.synchronize()
+        c.reset_node_pod_counts()
+        c.timing_begin(R)
+        for _ in range(R):
+            seq()
+        n_t, tot, _ = c.timing_end()
+        torch.cuda.synchronize()
+        ms = tot / max(n_t, 1)
+        counts = c.node_pod_counts()
+        g = got(b)
+        placed = g[2] == 0
+        ok = same(g, want) and (counts == R * np.bincount(g[0][placed], minlength=n)).all()
+        return ms, ok
+
+    for key, c, R, serial in (("c5_sequential", ctx, 20, False),
+                              ("c5_sequential_serial", new_ctx(env={"MSH_SEQ_SPLIT": "serial"}), 3, True)):
+        if serial:
+            c.upload_nodes(u, nd)
+        ms, ok = c5(c, R)
+        out[key] = {"kernel": seq_kernel_label(n), "ms_per_step": ms, "us_per_pod": ms * 1e3 / p,
+                    "pods_per_s": p / (ms * 1e-3), "evals_per_s": n * p / (ms * 1e-3),
+                    "form": ("one workgroup walks all 100,000 pods in order" if serial else
+                             "no capacity: blocks of consecutive pods, one workgroup each, every block in order; "
+                             "node counts added by device atomics"),
+                    "check": (f"seq == batch (closed form), node counts == {R} x placements" if ok else "MISMATCH"),
+                    "roofline": make_roofline("sequential", n, p, ms, 1, cus, serial=serial)}
+        c.close()
 
     # ---- f2: node-table maintenance (an informer Update / Add, eventhandler.go:37-57, replacing the
     # per-cycle LIST of minisched.go:40), host wall time of the synchronous call, median of 50 ----

@@ -770,7 +770,8 @@ bool read_knobs(msh::DeviceInfo& d, std::string* err) {
                   knob("MSH_BATCH_KERNEL", {{"pair", 0}, {"generic", 2}}, &d.batch_kernel, err) &&
                   knob("MSH_PAIR_PLANES", {{"auto", 0}, {"sgpr", 1}, {"lds", 2}}, &d.pair_planes, err) &&
                   knob("MSH_PAIR_NOAX", {{"auto", -1}, {"1", 1}, {"0", 0}}, &d.pair_noax, err) &&
-                  knob("MSH_GEN_NNKEY", {{"auto", 1}, {"select", 0}}, &d.gen_nnkey, err);
+                  knob("MSH_GEN_NNKEY", {{"auto", 1}, {"select", 0}}, &d.gen_nnkey, err) &&
+                  knob("MSH_SEQ_SPLIT", {{"auto", 1}, {"serial", 0}}, &d.seq_split, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;
   d.host_sync_poll = poll;

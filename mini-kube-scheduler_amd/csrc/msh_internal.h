@@ -54,6 +54,9 @@ struct DeviceInfo {
   // against 89.0 us per 32-batch C3 launch), 0 for the identity-like modes (77.3-78.3 against
   // 80.9-81.2), profiles/r4_ab_pair_planes.txt
   int pair_noax = -1;
+  // MSH_SEQ_SPLIT: without a capacity, the sequential kernel's pods in blocks of consecutive pods, one
+  // workgroup each (auto, 1), or all in one workgroup (serial, 0)
+  int seq_split = 1;
   int gen_nnkey = 1;  // MSH_GEN_NNKEY: generic_kernel's compare-free NodeNumber key (1) or the select (0)
 };
 
@@ -196,6 +199,7 @@ struct SeqArgs {
   int32_t* out_idx;
   int64_t* out_score;
   int32_t* out_status;
+  int32_t pods_per_block;    // set by the launcher: pods per workgroup (the whole batch when one workgroup)
 };
 
 hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err);

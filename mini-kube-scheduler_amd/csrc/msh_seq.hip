@@ -120,12 +120,29 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
 
 // U: pods decided per step (U > 1 only for one wave without a capacity; U divides 64).
 template <int RS, int NW, bool KX, bool CAP, int U>
-__global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_kernel(SeqArgs a) {
+__global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_kernel(SeqArgs a0) {
   static_assert(U == 1 || !CAP, "pods are decided ahead of commits only when no commit feeds a decision");
   constexpr bool FIN = !CAP && NW > 1;  // a finalizer wave decodes, keeps the outputs and commits
   constexpr int FINW = FIN ? NW : 0;    // the wave that keeps the outputs
-  constexpr bool LDSC = NW <= 4;        // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32
-                                        // nodes = 32,768 nodes, 128 KB), else in device memory
+  // Without a capacity no commit feeds a later decision, so the launcher may split the pods into
+  // blocks of consecutive pods, one workgroup each (as ranks split them in pod-sharded sequential
+  // mode): each walks its block in order against the whole table, and its commits are added to the
+  // device counts (atomics), which then equal the serial loop's. With a capacity: one workgroup.
+  const bool split = !CAP && gridDim.x > 1;
+  SeqArgs a = a0;
+  if (split) {
+    const int32_t j0 = (int32_t)blockIdx.x * a0.pods_per_block;
+    a.n_pods = min(a0.pods_per_block, a0.n_pods - j0);
+    a.pod_digit += j0;
+    a.pod_tol += j0;
+    a.out_idx += j0;
+    if (a.out_score) a.out_score += j0;
+    a.out_status += j0;
+  }
+  // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB) for one
+  // workgroup, else device-memory atomics
+  constexpr bool LDSC_T = NW <= 4;
+  const bool LDSC = LDSC_T && !split;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first
   // feasible, first feasible non-match]
@@ -420,9 +437,10 @@ namespace {
 constexpr int SEQ_AHEAD = 4;  // pods decided per step without a capacity
 
 template <int RS, int NW, bool CAP>
-hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
+hipError_t launch_seq_rs(const SeqArgs& a, int32_t blocks, hipStream_t s) {
   const dim3 blk((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64);  // + the finalizer wave without a capacity
-  const size_t lds = NW <= 4 ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;  // seq_kernel's LDSC
+  // seq_kernel's LDS counts: one workgroup only
+  const size_t lds = (NW <= 4 && blocks == 1) ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;
   constexpr int U = !CAP ? SEQ_AHEAD : 1;
   auto kx = seq_kernel<RS, NW, true, CAP, U>;
   auto id = seq_kernel<RS, NW, false, CAP, U>;
@@ -431,25 +449,25 @@ hipError_t launch_seq_rs(const SeqArgs& a, hipStream_t s) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  if (needs_kx(a.pp)) MSH_TIMED_LAUNCH(kx, dim3(1), blk, lds, s, a);
-  else MSH_TIMED_LAUNCH(id, dim3(1), blk, lds, s, a);
+  if (needs_kx(a.pp)) MSH_TIMED_LAUNCH(kx, dim3((unsigned)blocks), blk, lds, s, a);
+  else MSH_TIMED_LAUNCH(id, dim3((unsigned)blocks), blk, lds, s, a);
   return hipGetLastError();
 }
 
 template <int NW, bool CAP>
-hipError_t launch_seq_nw(const SeqArgs& a, int rs, hipStream_t s) {
+hipError_t launch_seq_nw(const SeqArgs& a, int rs, int32_t blocks, hipStream_t s) {
   if constexpr (NW == 1) {
-    if (rs <= 1) return launch_seq_rs<1, NW, CAP>(a, s);
-    if (rs <= 2) return launch_seq_rs<2, NW, CAP>(a, s);
-    if (rs <= 3) return launch_seq_rs<3, NW, CAP>(a, s);
-    return launch_seq_rs<4, NW, CAP>(a, s);
+    if (rs <= 1) return launch_seq_rs<1, NW, CAP>(a, blocks, s);
+    if (rs <= 2) return launch_seq_rs<2, NW, CAP>(a, blocks, s);
+    if (rs <= 3) return launch_seq_rs<3, NW, CAP>(a, blocks, s);
+    return launch_seq_rs<4, NW, CAP>(a, blocks, s);
   } else if constexpr (NW == 4) {
-    if (rs <= 2) return launch_seq_rs<2, NW, CAP>(a, s);
-    return launch_seq_rs<4, NW, CAP>(a, s);
+    if (rs <= 2) return launch_seq_rs<2, NW, CAP>(a, blocks, s);
+    return launch_seq_rs<4, NW, CAP>(a, blocks, s);
   } else {
-    if (rs <= 4) return launch_seq_rs<4, NW, CAP>(a, s);
-    if (CAP || rs <= 8) return launch_seq_rs<8, NW, CAP>(a, s);
-    return launch_seq_rs<(CAP ? 8 : 12), NW, CAP>(a, s);  // (CAP at 12 words per lane spills)
+    if (rs <= 4) return launch_seq_rs<4, NW, CAP>(a, blocks, s);
+    if (CAP || rs <= 8) return launch_seq_rs<8, NW, CAP>(a, blocks, s);
+    return launch_seq_rs<(CAP ? 8 : 12), NW, CAP>(a, blocks, s);  // (CAP at 12 words per lane spills)
   }
 }
 }  // namespace
@@ -475,15 +493,26 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
              std::to_string(nw_big * WAVE * rs_max * 32) + " nodes per device" + (cap ? " with a capacity" : "");
     return hipErrorInvalidValue;
   }
-  const SeqArgs& ka = a;
+  SeqArgs ka = a;
+  ka.pods_per_block = a.n_pods;
   if (cap) {
-    if (nw == 1) return launch_seq_nw<1, true>(ka, rs, s);
-    if (nw == 4) return launch_seq_nw<4, true>(ka, rs, s);
-    return launch_seq_nw<16, true>(ka, rs, s);
+    if (nw == 1) return launch_seq_nw<1, true>(ka, rs, 1, s);
+    if (nw == 4) return launch_seq_nw<4, true>(ka, rs, 1, s);
+    return launch_seq_nw<16, true>(ka, rs, 1, s);
   }
-  if (nw == 1) return launch_seq_nw<1, false>(ka, rs, s);
-  if (nw == 4) return launch_seq_nw<4, false>(ka, rs, s);
-  return launch_seq_nw<15, false>(ka, rs, s);
+  // Without a capacity: blocks of consecutive pods (a multiple of 64), about eight per CU, each one
+  // workgroup walking its pods in order (MSH_SEQ_SPLIT=serial: one workgroup for the whole batch)
+  int32_t blocks = 1;
+  if (dev.seq_split) {
+    const int64_t want = (int64_t)dev.cus * 8;
+    int64_t per = (a.n_pods + want - 1) / want;
+    per = std::max<int64_t>(WAVE, (per + WAVE - 1) / WAVE * WAVE);
+    ka.pods_per_block = (int32_t)per;
+    blocks = (int32_t)((a.n_pods + per - 1) / per);
+  }
+  if (nw == 1) return launch_seq_nw<1, false>(ka, rs, blocks, s);
+  if (nw == 4) return launch_seq_nw<4, false>(ka, rs, blocks, s);
+  return launch_seq_nw<15, false>(ka, rs, blocks, s);
 }
 
 }  // namespace msh

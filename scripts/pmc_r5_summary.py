@@ -10,7 +10,8 @@ only when all of them match what it timed):
   generic_ref     generic_kernel on the reference list (w=1 NONE), 32 batches
   generic_hl      generic_kernel on the headline list (w=3 DefaultNormalizeScore: extents pass + main pass), 32 batches
   generic_col     generic_kernel on NodeNumber + a DEFAULT-normalized score column, 32 batches
-  sequential      seq_kernel at C5 (headline list)
+  sequential      seq_kernel at C5 (headline list), pod blocks over workgroups (no capacity: the default)
+  sequential_serial  the same with MSH_SEQ_SPLIT=serial (one workgroup walks all pods)
 FETCH_SIZE / WRITE_SIZE are KiB (x 1024); FETCH_SIZE is reported raw and with MI355X_MICROARCH.md's x2
 gfx950 correction (hbm_bytes_per_launch_fetch_x2 = 2 x FETCH + WRITE, what bench.py's `traffic` quotes)."""
 import csv
@@ -60,7 +61,8 @@ for mode, prefix, tags, nb, plug in (
         ("generic_ref", "msh::generic_kernel", ("g_sq", "g_sq2", "g_grbm", "g_fetch", "g_write"), NB, tag_of(1, 0)),
         ("generic_hl", "msh::generic_kernel", ("gh_sq",), NB, tag_of(3, 1)),
         ("generic_col", "msh::generic_kernel", ("gc_sq", "gc_sq2"), NB, tag_of(1, 0) + " + ScoreColumn0 w=2 norm=1"),
-        ("sequential", "msh::seq_kernel", ("s_sq",), 1, tag_of(3, 1))):
+        ("sequential", "msh::seq_kernel", ("s_sq", "s_grbm"), 1, tag_of(3, 1)),
+        ("sequential_serial", "msh::seq_kernel", ("ss_sq",), 1, tag_of(3, 1))):
     e = {"nodes": N, "pods": P, "batches_per_launch": nb, "plugins": plug, "launches_per_counter": {}}
     for t in tags:
         name, avg, cnt = counters(t, prefix)
@@ -100,7 +102,7 @@ for tag, prefix in (("stats", "msh::pair"), ("stats_k20", "msh::pair"),
                     ("stats_rev", "msh::pair"), ("stats_single", "msh::pair"),
                     ("stats_generic", "msh::generic_kernel"), ("stats_generic_hl", "msh::generic_kernel"),
                     ("stats_generic_col", "msh::generic_kernel"),
-                    ("stats_seq", "msh::seq_kernel")):
+                    ("stats_seq", "msh::seq_kernel"), ("stats_seq_serial", "msh::seq_kernel")):
     name, avg, calls = stats_avg_ns(tag, prefix)
     if name:
         res["stats"][tag] = {"kernel": name, "avg_ns": avg, "calls": calls}

@@ -6,7 +6,7 @@
 #     pods per batch): the per-pair kernel 32 batches per launch with the headline plugins (NodeNumber w=3
 #     DefaultNormalizeScore), the reference's w=1 list, MIN-MAX and REVERSE at w=3; generic_kernel on the
 #     reference list, on the headline list and on NodeNumber + a DEFAULT-normalized column; seq_kernel (C5,
-#     headline plugins);
+#     headline plugins: pod blocks over workgroups, and MSH_SEQ_SPLIT=serial);
 #  3. one --pmc pass per counter set (never combined with tracing).
 # Summary: scripts/pmc_r5_summary.py -> profiles/r5_pmc_c3.json (bench.py reads it for the counter
 # fractions and the HBM traffic of its roofline).
@@ -26,7 +26,7 @@ fi
 # tag mode weight norm kernel
 tr() {
   local tag=$1 mode=$2 w=$3 norm=$4 kern=$5
-  MSH_BATCH_KERNEL=$kern WEIGHT=$w NORM=$norm MODE=$mode PODS=100000 LAUNCHES=30 timeout -k 10 120 rocprofv3 --kernel-trace --stats \
+  MSH_SEQ_SPLIT=${SPLIT:-auto} MSH_BATCH_KERNEL=$kern WEIGHT=$w NORM=$norm MODE=$mode PODS=100000 LAUNCHES=30 timeout -k 10 120 rocprofv3 --kernel-trace --stats \
     -d "$OUT/$tag" -o run --output-format csv -- python3 scripts/run_batch.py > "$OUT/$tag.log" 2>&1
   local rc=$?; echo "[$tag] rc=$rc"; return $rc
 }
@@ -40,10 +40,11 @@ if [ "${SKIP_TRACE:-0}" != 1 ]; then
   tr stats_generic_hl generic 3 1 generic || exit 1
   tr stats_generic_col generic_col 1 0 pair || exit 1
   tr stats_seq sequential 3 1 pair || exit 1
+  SPLIT=serial tr stats_seq_serial sequential 3 1 pair || exit 1
 fi
 pass() {
   local tag=$1 mode=$2 w=$3 norm=$4 kern=$5; shift 5
-  MSH_BATCH_KERNEL=$kern WEIGHT=$w NORM=$norm MODE=$mode PODS=100000 LAUNCHES=10 timeout -s KILL 90 rocprofv3 --pmc "$@" \
+  MSH_SEQ_SPLIT=${SPLIT:-auto} MSH_BATCH_KERNEL=$kern WEIGHT=$w NORM=$norm MODE=$mode PODS=100000 LAUNCHES=10 timeout -s KILL 90 rocprofv3 --pmc "$@" \
     -d "$OUT/$tag" -o run --output-format csv -- python3 scripts/run_batch.py > "$OUT/$tag.log" 2>&1
   local rc=$?; echo "[$tag] rc=$rc"; return $rc
 }
@@ -72,4 +73,6 @@ pass gh_sq generic 3 1 generic $SQ1 || exit 1
 pass gc_sq generic_col 1 0 pair $SQ1 || exit 1
 pass gc_sq2 generic_col 1 0 pair $SQ2 || exit 1
 pass s_sq sequential 3 1 pair $SQ1 || exit 1
+pass s_grbm sequential 3 1 pair GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
+SPLIT=serial pass ss_sq sequential 3 1 pair $SQ1 || exit 1
 python3 scripts/pmc_r5_summary.py "$OUT" "$OUT/r5_pmc_c3.json" > /dev/null && echo profile-r5-done

@@ -9,7 +9,7 @@ MODE
                per launch (MSH_BATCH_KERNEL=generic is set here)
   generic_col  generic_kernel on NodeNumber + ScoreColumn0 (weight 2, DefaultNormalizeScore), 32 batches
                per launch (bench.py's generic.nodenumber_plus_default_column)
-  sequential   C5: one pod at a time (seq_kernel)
+  sequential   C5: each pod in order (seq_kernel; MSH_SEQ_SPLIT=serial: the whole batch in one workgroup)
 NORM / WEIGHT: msh_normalize and weight of the NodeNumber entry (bench.py's headline: WEIGHT=3 NORM=1)."""
 import importlib
 import os

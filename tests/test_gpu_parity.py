@@ -289,6 +289,32 @@ def test_sequential(msh, oracle, n, max_pods, seq_waves, monkeypatch):
             _assert_same(got, ctx.schedule_batch(pd, pt), "seq == batch")
 
 
+@pytest.mark.parametrize("split", ["auto", "serial"])
+@pytest.mark.parametrize("seq_waves,n", [("1", 1000), ("4", 8193), ("16", 40000)])
+def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split, monkeypatch):
+    """Without a capacity the sequential kernel splits the pods into blocks of consecutive pods, one
+    workgroup each (MSH_SEQ_SPLIT=auto), or walks them all in one workgroup (serial): both give the
+    serial loop's placements and node counts, for batch sizes around the 64-pod block edges and with
+    counts carried over between calls (the blocks add theirs with device atomics)."""
+    monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)
+    monkeypatch.setenv("MSH_SEQ_SPLIT", split)
+    rng = np.random.default_rng(n + 77)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, 3)
+    u, nd, pd, pt = _rand_case(rng, n, 20_000, p_unsched=0.2, p_tol=0.1)
+    with msh.DeviceContext(0) as ctx:
+        _set(ctx, msh, ps)
+        ctx.upload_nodes(u, nd)
+        cuts = [0, 1, 64, 65, 191, 9_999, 20_000]
+        parts = [ctx.schedule_sequential(pd[a:b], pt[a:b], 0) for a, b in zip(cuts, cuts[1:])]
+        want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, 0)
+        _assert_same(tuple(np.concatenate(x) for x in zip(*parts)), (want_i, want_s, want_st),
+                     f"seq blocks split={split} waves={seq_waves} n={n}")
+        assert (ctx.node_pod_counts() == want_counts).all()
+    monkeypatch.setenv("MSH_SEQ_SPLIT", "blocks")
+    with pytest.raises(msh.MshError):
+        msh.DeviceContext(0)
+
+
 @pytest.mark.parametrize("seq_waves", ["1", "16"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("combo", range(len(PLUGIN_COMBOS)))
