@@ -139,10 +139,11 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     if (a.out_score) a.out_score += j0;
     a.out_status += j0;
   }
-  // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB) for one
-  // workgroup, else device-memory atomics
-  constexpr bool LDSC_T = NW <= 4;
-  const bool LDSC = LDSC_T && !split;
+  // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
+  // device-memory atomics. Split: each block counts its own commits in LDS and adds the non-zero ones
+  // to the device counts at its end (a digit's pods all land on its first feasible match: per-commit
+  // device atomics from every block would queue on a few addresses).
+  constexpr bool LDSC = NW <= 4;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first
   // feasible, first feasible non-match]
@@ -175,7 +176,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     }
   }
   if (LDSC)  // ordered before the first commit by the first pod's exchange / barrier
-    for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) lcnt[i] = a.counts[i];
+    for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) lcnt[i] = split ? 0 : a.counts[i];
   if (threadIdx.x < 9 * U) (&xs[0][0][0])[threadIdx.x] = NONE;
   // The first feasible node for a pod that does not tolerate the unschedulable taint (V & ~X) and for
   // one that does (V), evaluated here from the register-resident planes once per launch (lanes and
@@ -280,8 +281,21 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
       // Without a capacity no decision reads a count, so the block's placements are committed
       // here, one atomic per lane (NodeInfo.AddPod analogue), instead of one per pod.
       if (!CAP && st == 0) {
-        if (LDSC) atomicAdd(&lcnt[sel], 1);
-        else atomicAdd(&counts[sel], 1);
+        if (LDSC) {
+          atomicAdd(&lcnt[sel], 1);
+        } else if (!split) {
+          atomicAdd(&counts[sel], 1);
+        } else {  // one device atomic per distinct node of the block's 64 placements
+          bool todo = true;
+          while (todo) {  // lanes in the branch only: the rest of the wave is masked off
+            const int lead = __builtin_ctzll(__ballot(true));
+            const int32_t ls = __builtin_amdgcn_readlane(sel, lead);
+            const bool mine = sel == ls;
+            const int cnt = __builtin_popcountll(__ballot(mine));
+            if (lane == lead) atomicAdd(&counts[ls], cnt);
+            if (mine) todo = false;
+          }
+        }
       }
     }
   };
@@ -429,7 +443,10 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   }
   if (LDSC) {
     __syncthreads();
-    for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) a.counts[i] = lcnt[i];
+    for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) {
+      if (!split) a.counts[i] = lcnt[i];
+      else if (lcnt[i] != 0) atomicAdd(&a.counts[i], lcnt[i]);
+    }
   }
 }
 
@@ -439,8 +456,7 @@ constexpr int SEQ_AHEAD = 4;  // pods decided per step without a capacity
 template <int RS, int NW, bool CAP>
 hipError_t launch_seq_rs(const SeqArgs& a, int32_t blocks, hipStream_t s) {
   const dim3 blk((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64);  // + the finalizer wave without a capacity
-  // seq_kernel's LDS counts: one workgroup only
-  const size_t lds = (NW <= 4 && blocks == 1) ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;
+  const size_t lds = NW <= 4 ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;  // seq_kernel's LDSC
   constexpr int U = !CAP ? SEQ_AHEAD : 1;
   auto kx = seq_kernel<RS, NW, true, CAP, U>;
   auto id = seq_kernel<RS, NW, false, CAP, U>;
