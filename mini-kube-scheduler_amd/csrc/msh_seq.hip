@@ -140,13 +140,10 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     a.out_status += j0;
   }
   // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
-  // device-memory atomics. Split, a block of more than 64 pods counts its own commits in LDS and adds
-  // the non-zero ones to the device counts at its end; a 64-pod block, and the large tables, add one
-  // device atomic per distinct node of its placements (a digit's pods all land on its first feasible
-  // match: one device atomic per commit from every block queued on a few addresses, 149 against 27.6 us
-  // per C5 launch)
-  constexpr bool LDSC_T = NW <= 4;
-  const bool LDSC = LDSC_T && (!split || a0.pods_per_block > WAVE);
+  // device-memory atomics. Split: each block counts its own commits in LDS and adds the non-zero ones
+  // to the device counts at its end (a digit's pods all land on its first feasible match: per-commit
+  // device atomics from every block would queue on a few addresses).
+  constexpr bool LDSC = NW <= 4;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first
   // feasible, first feasible non-match]
@@ -459,8 +456,7 @@ constexpr int SEQ_AHEAD = 4;  // pods decided per step without a capacity
 template <int RS, int NW, bool CAP>
 hipError_t launch_seq_rs(const SeqArgs& a, int32_t blocks, hipStream_t s) {
   const dim3 blk((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64);  // + the finalizer wave without a capacity
-  // seq_kernel's LDSC (not for 64-pod blocks)
-  const size_t lds = (NW <= 4 && (blocks == 1 || a.pods_per_block > WAVE)) ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;
+  const size_t lds = NW <= 4 ? (size_t)a.n_words * 32 * sizeof(int32_t) : 0;  // seq_kernel's LDSC
   constexpr int U = !CAP ? SEQ_AHEAD : 1;
   auto kx = seq_kernel<RS, NW, true, CAP, U>;
   auto id = seq_kernel<RS, NW, false, CAP, U>;
