@@ -140,9 +140,9 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     a.out_status += j0;
   }
   // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
-  // device-memory atomics. Split: each block counts its own commits in LDS and adds the non-zero ones
-  // to the device counts at its end (a digit's pods all land on its first feasible match: per-commit
-  // device atomics from every block would queue on a few addresses).
+  // device-memory atomics. Split: each 64-pod block counts its commits in LDS and adds one device
+  // atomic per distinct node (a digit's pods all land on its first feasible match: a device atomic per
+  // commit from every workgroup queues on a few addresses, 149 against 27.6 us per C5 launch).
   constexpr bool LDSC = NW <= 4;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first
@@ -175,8 +175,14 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
       }
     }
   }
-  if (LDSC)  // ordered before the first commit by the first pod's exchange / barrier
-    for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) lcnt[i] = split ? 0 : a.counts[i];
+  if (LDSC) {  // ordered before the first commit by the first pod's exchange / barrier
+    if (split) {
+      for (int32_t i = threadIdx.x; i < a.n_words * 8; i += blockDim.x)
+        reinterpret_cast<int4*>(lcnt)[i] = make_int4(0, 0, 0, 0);
+    } else {
+      for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) lcnt[i] = a.counts[i];
+    }
+  }
   if (threadIdx.x < 9 * U) (&xs[0][0][0])[threadIdx.x] = NONE;
   // The first feasible node for a pod that does not tolerate the unschedulable taint (V & ~X) and for
   // one that does (V), evaluated here from the register-resident planes once per launch (lanes and
@@ -282,7 +288,14 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
       // here, one atomic per lane (NodeInfo.AddPod analogue), instead of one per pod.
       if (!CAP && st == 0) {
         if (LDSC) {
-          atomicAdd(&lcnt[sel], 1);
+          const int32_t old = atomicAdd(&lcnt[sel], 1);
+          if (split && old == 0) {  // split: the lane that counted a node first for this 64-pod block
+            // moves the block's count of it (every lane's add has landed: one wave, LDS in order) to
+            // the device counts and clears it for the next block
+            const int32_t c = lcnt[sel];
+            lcnt[sel] = 0;
+            atomicAdd(&counts[sel], c);
+          }
         } else if (!split) {
           atomicAdd(&counts[sel], 1);
         } else {  // one device atomic per distinct node of the block's 64 placements
@@ -441,12 +454,9 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     const int32_t j0 = (a.n_pods - 1) & ~(WAVE - 1);
     store_block(j0, a.n_pods - j0, pkv);
   }
-  if (LDSC) {
+  if (LDSC && !split) {
     __syncthreads();
-    for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) {
-      if (!split) a.counts[i] = lcnt[i];
-      else if (lcnt[i] != 0) atomicAdd(&a.counts[i], lcnt[i]);
-    }
+    for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) a.counts[i] = lcnt[i];
   }
 }
 
