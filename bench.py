@@ -895,6 +895,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     ctx = new_ctx()
     ctx.upload_nodes(u4, nd4)
     b4 = dbufs(pd4, pt4)
+    s1 = Streams(torch, dev, 1)
     launch = lambda i, sh: ctx.schedule_batch_device(p4, *[t.data_ptr() for t in b4], sh)
     s1.time(launch, 1)
     ms_b = s1.time(launch, 5)
