@@ -300,11 +300,12 @@ def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split, monkeypatch):
     monkeypatch.setenv("MSH_SEQ_SPLIT", split)
     rng = np.random.default_rng(n + 77)
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, 3)
-    u, nd, pd, pt = _rand_case(rng, n, 20_000, p_unsched=0.2, p_tol=0.1)
+    p = 20_000 if n < 10_000 else 6_000  # (the oracle's serial loop is n x p)
+    u, nd, pd, pt = _rand_case(rng, n, p, p_unsched=0.2, p_tol=0.1)
     with msh.DeviceContext(0) as ctx:
         _set(ctx, msh, ps)
         ctx.upload_nodes(u, nd)
-        cuts = [0, 1, 64, 65, 191, 9_999, 20_000]
+        cuts = [0, 1, 64, 65, 191, p // 2 - 1, p]
         parts = [ctx.schedule_sequential(pd[a:b], pt[a:b], 0) for a, b in zip(cuts, cuts[1:])]
         want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, 0)
         _assert_same(tuple(np.concatenate(x) for x in zip(*parts)), (want_i, want_s, want_st),
