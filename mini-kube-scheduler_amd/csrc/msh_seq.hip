@@ -142,7 +142,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
   // device-memory atomics. Split: each 64-pod block counts its commits in LDS and adds one device
   // atomic per distinct node (a digit's pods all land on its first feasible match: a device atomic per
-  // commit from every workgroup queues on a few addresses, 149 against 27.6 us per C5 launch).
+  // commit from every workgroup queues on a few addresses, 149 against 26 us per C5 launch).
   constexpr bool LDSC = NW <= 4;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first
@@ -296,18 +296,8 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
             lcnt[sel] = 0;
             atomicAdd(&counts[sel], c);
           }
-        } else if (!split) {
-          atomicAdd(&counts[sel], 1);
-        } else {  // one device atomic per distinct node of the block's 64 placements
-          bool todo = true;
-          while (todo) {  // lanes in the branch only: the rest of the wave is masked off
-            const int lead = __builtin_ctzll(__ballot(true));
-            const int32_t ls = __builtin_amdgcn_readlane(sel, lead);
-            const bool mine = sel == ls;
-            const int cnt = __builtin_popcountll(__ballot(mine));
-            if (lane == lead) atomicAdd(&counts[ls], cnt);
-            if (mine) todo = false;
-          }
+        } else {
+          atomicAdd(&counts[sel], 1);  // one workgroup (the launcher splits LDS-count tables only)
         }
       }
     }
@@ -527,9 +517,11 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
     return launch_seq_nw<16, true>(ka, rs, 1, s);
   }
   // Without a capacity: blocks of consecutive pods (a multiple of 64), about eight per CU, each one
-  // workgroup walking its pods in order (MSH_SEQ_SPLIT=serial: one workgroup for the whole batch)
+  // workgroup walking its pods in order (MSH_SEQ_SPLIT=serial: one workgroup for the whole batch).
+  // Tables whose counts fit LDS only (up to four scanning waves, 32,768 nodes): a larger table's
+  // blocks would add every commit to the device counts, and a digit's pods all land on one node.
   int32_t blocks = 1;
-  if (dev.seq_split) {
+  if (dev.seq_split && nw <= 4) {
     const int64_t want = (int64_t)dev.cus * 8;
     int64_t per = (a.n_pods + want - 1) / want;
     per = std::max<int64_t>(WAVE, (per + WAVE - 1) / WAVE * WAVE);

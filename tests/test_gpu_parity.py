@@ -293,9 +293,10 @@ def test_sequential(msh, oracle, n, max_pods, seq_waves, monkeypatch):
 @pytest.mark.parametrize("seq_waves,n", [("1", 1000), ("4", 8193), ("16", 40000)])
 def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split, monkeypatch):
     """Without a capacity the sequential kernel splits the pods into blocks of consecutive pods, one
-    workgroup each (MSH_SEQ_SPLIT=auto), or walks them all in one workgroup (serial): both give the
-    serial loop's placements and node counts, for batch sizes around the 64-pod block edges and with
-    counts carried over between calls (the blocks add theirs with device atomics)."""
+    workgroup each (MSH_SEQ_SPLIT=auto, tables up to 32,768 nodes; the 40,000-node table stays in one
+    workgroup), or walks them all in one workgroup (serial): both give the serial loop's placements and
+    node counts, for batch sizes around the 64-pod block edges and with counts carried over between
+    calls (the blocks add theirs with device atomics)."""
     monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)
     monkeypatch.setenv("MSH_SEQ_SPLIT", split)
     rng = np.random.default_rng(n + 77)
