@@ -115,11 +115,6 @@ struct msh_ctx {
   int32_t* d_counts = nullptr;
   size_t counts_cap = 0;
   std::vector<std::pair<hipStream_t, hipEvent_t>> seq_inflight;
-  // pod-block sequential launches: the blocks' published counts and the groups' finish counters
-  // (zeroed at allocation, re-armed by each group's last block)
-  unsigned long long* d_seq_stage = nullptr;
-  int32_t* d_seq_ctr = nullptr;
-  size_t seq_rows_cap = 0;
   // the rewrites' own stream, created with the device's highest priority: HIP gives each priority
   // its own hardware queues, so a rewrite never queues behind other streams' kernels that happen to
   // share a hardware queue with it (GPU_MAX_HW_QUEUES per priority)
@@ -882,8 +877,6 @@ void msh_destroy(msh_ctx* c) {
   }
   destroy_events(c->seq_inflight);
   (void)hipFree(c->d_counts);
-  (void)hipFree(c->d_seq_stage);
-  (void)hipFree(c->d_seq_ctr);
   for (hipEvent_t e : c->async_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -1220,29 +1213,6 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   a.out_idx = d_out_idx;
   a.out_score = d_out_score;
   a.out_status = d_out_status;
-  const int32_t blocks = msh::seq_blocks(a, c->dev);
-  if (blocks > 1) {
-    // the pod blocks share the ctx's staging rows and group counters: one such launch at a time, so
-    // this stream first waits for the sequential launches in flight on the others (device-side)
-    if ((size_t)blocks > c->seq_rows_cap) {
-      wait_events(c->seq_inflight);
-      (void)hipFree(c->d_seq_stage);
-      (void)hipFree(c->d_seq_ctr);
-      c->d_seq_stage = nullptr;
-      c->d_seq_ctr = nullptr;
-      c->seq_rows_cap = 0;
-      const size_t rows = std::max<size_t>((size_t)blocks, 2048);
-      const size_t groups = (rows + msh::SEQ_GROUP - 1) / msh::SEQ_GROUP;
-      MSH_HIP(c, hipMalloc(&c->d_seq_stage, rows * msh::WAVE * sizeof(unsigned long long)));
-      MSH_HIP(c, hipMalloc(&c->d_seq_ctr, groups * sizeof(int32_t)));
-      MSH_HIP(c, hipMemsetAsync(c->d_seq_ctr, 0, groups * sizeof(int32_t), s));  // before the launch on s
-      c->seq_rows_cap = rows;
-    }
-    for (auto& ev : c->seq_inflight)
-      if (ev.first != s) MSH_HIP(c, hipStreamWaitEvent(s, ev.second, 0));
-  }
-  a.stage = c->d_seq_stage;
-  a.group_ctr = c->d_seq_ctr;
   std::string err;
   hipError_t e;
   {

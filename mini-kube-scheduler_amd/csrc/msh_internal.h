@@ -200,16 +200,7 @@ struct SeqArgs {
   int64_t* out_score;
   int32_t* out_status;
   int32_t pods_per_block;    // set by the launcher: pods per workgroup (the whole batch when one workgroup)
-  // pod blocks (no capacity): per block, the (node, count) of each node its 64 commits reached, node in
-  // the low word (all-ones: none), [blocks][64]; per group of SEQ_GROUP blocks, the blocks finished
-  unsigned long long* stage;
-  int32_t* group_ctr;
 };
-
-constexpr int SEQ_GROUP = 32;  // pod blocks per count merge group
-// Workgroups launch_sequential runs the batch on: 64-pod blocks without a capacity on tables whose
-// counts fit LDS (DeviceInfo::seq_split), else 1.
-int32_t seq_blocks(const SeqArgs& a, const DeviceInfo& dev);
 
 hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err);
 

@@ -125,13 +125,9 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   constexpr bool FIN = !CAP && NW > 1;  // a finalizer wave decodes, keeps the outputs and commits
   constexpr int FINW = FIN ? NW : 0;    // the wave that keeps the outputs
   // Without a capacity no commit feeds a later decision, so the launcher may split the pods into
-  // 64-pod blocks of consecutive pods, one workgroup each (as ranks split them in pod-sharded
-  // sequential mode): each walks its block in order against the whole table, and its commits are
-  // added to the device counts, which then equal the serial loop's. With a capacity: one workgroup.
-  // A digit's pods all land on its first feasible match, so a device atomic per commit, or per block
-  // and node, queues on about ten addresses (149 / 26 us per C5 launch against 11 without the adds):
-  // a block publishes its per-node counts in `stage`, and the last block of each group of SEQ_GROUP
-  // merges the group's in LDS and adds them, one device atomic per node and group.
+  // blocks of consecutive pods, one workgroup each (as ranks split them in pod-sharded sequential
+  // mode): each walks its block in order against the whole table, and its commits are added to the
+  // device counts (atomics), which then equal the serial loop's. With a capacity: one workgroup.
   const bool split = !CAP && gridDim.x > 1;
   SeqArgs a = a0;
   if (split) {
@@ -144,7 +140,9 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     a.out_status += j0;
   }
   // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
-  // device-memory atomics (one workgroup only)
+  // device-memory atomics. Split: each 64-pod block counts its commits in LDS and adds one device
+  // atomic per distinct node (a digit's pods all land on its first feasible match: a device atomic per
+  // commit from every workgroup queues on a few addresses, 149 against 26 us per C5 launch).
   constexpr bool LDSC = NW <= 4;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first
@@ -262,10 +260,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   // modes), decoded by the lanes together once per 64 pods; with a capacity the decoded node (o_a)
   // and status | scored << 2 (o_b), since every commit needs them at once
   int32_t o_a = -1, o_b = -1;
-  // split: this lane's entry of the block's per-node counts (the lane that counted a node first)
-  unsigned long long stg = ~0ull;
   auto store_block = [&](int32_t j0, int32_t cnt, uint32_t pk) {  // wave FINW: one coalesced store per array
-    int32_t first = -1;  // split: the node this lane counted first in the block
     if (lane < cnt) {
       int32_t sel, st;
       int64_t sc;
@@ -294,15 +289,17 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
       if (!CAP && st == 0) {
         if (LDSC) {
           const int32_t old = atomicAdd(&lcnt[sel], 1);
-          if (split && old == 0) first = sel;
+          if (split && old == 0) {  // split: the lane that counted a node first for this 64-pod block
+            // moves the block's count of it (every lane's add has landed: one wave, LDS in order) to
+            // the device counts and clears it for the next block
+            const int32_t c = lcnt[sel];
+            lcnt[sel] = 0;
+            atomicAdd(&counts[sel], c);
+          }
         } else {
           atomicAdd(&counts[sel], 1);  // one workgroup (the launcher splits LDS-count tables only)
         }
       }
-    }
-    if (split) {  // every lane's add has landed (one wave, LDS in order): publish the block's counts
-      if (first >= 0) stg = (unsigned long long)(uint32_t)first | ((unsigned long long)(uint32_t)lcnt[first] << 32);
-      a0.stage[(size_t)blockIdx.x * WAVE + lane] = stg;
     }
   };
   // One step: the U pods from pod j on, whose lanes start at jl0 (an int, or without a capacity a
@@ -451,36 +448,6 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     __syncthreads();
     for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) a.counts[i] = lcnt[i];
   }
-  if (split && wv == FINW) {
-    // the group's last block to finish merges its blocks' counts (release: this block's entries;
-    // acquire: the others'), then re-arms the group's counter for the next launch
-    __threadfence();
-    const int32_t g = (int32_t)blockIdx.x / SEQ_GROUP;
-    const int32_t r0 = g * SEQ_GROUP, nr = min(SEQ_GROUP, (int32_t)gridDim.x - r0);
-    int32_t ticket = 0;
-    if (lane == 0) ticket = atomicAdd(&a0.group_ctr[g], 1);
-    ticket = __builtin_amdgcn_readfirstlane(ticket);
-    if (ticket == nr - 1) {
-      __threadfence();
-      if (stg != ~0ull) lcnt[(uint32_t)stg] = 0;  // this block's LDS counts: back to zero
-      unsigned long long v[SEQ_GROUP];
-#pragma unroll
-      for (int k = 0; k < SEQ_GROUP; ++k)
-        v[k] = k < nr ? __hip_atomic_load(&a0.stage[(size_t)(r0 + k) * WAVE + lane], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT)
-                      : ~0ull;
-#pragma unroll
-      for (int k = 0; k < SEQ_GROUP; ++k)
-        if (v[k] != ~0ull) atomicAdd(&lcnt[(uint32_t)v[k]], (int32_t)(v[k] >> 32));
-#pragma unroll
-      for (int k = 0; k < SEQ_GROUP; ++k) {
-        if (v[k] == ~0ull) continue;
-        const int32_t x = atomicExch(&lcnt[(uint32_t)v[k]], 0);  // the first lane of a node takes the sum
-        if (x != 0) atomicAdd(&counts[(uint32_t)v[k]], x);
-      }
-      if (lane == 0) atomicExch(&a0.group_ctr[g], 0);
-    }
-  }
 }
 
 namespace {
@@ -526,32 +493,16 @@ hipError_t launch_seq_nw(const SeqArgs& a, int rs, int32_t blocks, hipStream_t s
 // (368,640 nodes; 6 x 12 plane VGPRs per lane), 16 waves with up to 8 with one (262,144 nodes; the
 // FULL plane makes 7 per word, and 12 words spill). Per-pod latency is one wave's scan plus one DPP
 // reduction; extra waves add an LDS exchange and a barrier.
-namespace {
-int seq_waves_for(const SeqArgs& a, const DeviceInfo& dev) {
+hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err) {
+  if (a.n_pods == 0) return hipSuccess;
   const bool cap = a.max_pods > 0;
   const int nw_big = cap ? 16 : 15;
   auto rs_for = [&](int nw) { return (a.n_words + nw * WAVE - 1) / (nw * WAVE); };
   int nw = dev.seq_waves > 0 ? dev.seq_waves : (rs_for(1) <= 4 ? 1 : rs_for(4) <= 4 ? 4 : nw_big);
   if (nw != 1 && nw != 4) nw = nw_big;
-  if (rs_for(nw) > (nw == nw_big ? (cap ? 8 : 12) : 4)) nw = nw_big;  // an override too small for the table
-  return nw;
-}
-}  // namespace
-
-// Tables whose counts fit LDS only (up to four scanning waves, 32,768 nodes): a larger table's blocks
-// would have no LDS to count in.
-int32_t seq_blocks(const SeqArgs& a, const DeviceInfo& dev) {
-  if (a.max_pods > 0 || !dev.seq_split || a.n_pods <= WAVE || seq_waves_for(a, dev) > 4) return 1;
-  return (a.n_pods + WAVE - 1) / WAVE;
-}
-
-hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err) {
-  if (a.n_pods == 0) return hipSuccess;
-  const bool cap = a.max_pods > 0;
-  const int nw_big = cap ? 16 : 15;
   const int rs_max = cap ? 8 : 12;
-  const int nw = seq_waves_for(a, dev);
-  const int rs = (a.n_words + nw * WAVE - 1) / (nw * WAVE);
+  if (rs_for(nw) > (nw == nw_big ? rs_max : 4)) nw = nw_big;  // an override too small for the table
+  const int rs = rs_for(nw);
   if (rs > rs_max) {
     if (err)
       *err = "sequential mode keeps the node table in registers: at most " +
@@ -565,10 +516,18 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
     if (nw == 4) return launch_seq_nw<4, true>(ka, rs, 1, s);
     return launch_seq_nw<16, true>(ka, rs, 1, s);
   }
-  // Without a capacity: 64-pod blocks of consecutive pods, each one workgroup walking its pods in
-  // order (MSH_SEQ_SPLIT=serial: one workgroup for the whole batch)
-  const int32_t blocks = seq_blocks(a, dev);
-  if (blocks > 1) ka.pods_per_block = WAVE;
+  // Without a capacity: blocks of consecutive pods (a multiple of 64), about eight per CU, each one
+  // workgroup walking its pods in order (MSH_SEQ_SPLIT=serial: one workgroup for the whole batch).
+  // Tables whose counts fit LDS only (up to four scanning waves, 32,768 nodes): a larger table's
+  // blocks would add every commit to the device counts, and a digit's pods all land on one node.
+  int32_t blocks = 1;
+  if (dev.seq_split && nw <= 4) {
+    const int64_t want = (int64_t)dev.cus * 8;
+    int64_t per = (a.n_pods + want - 1) / want;
+    per = std::max<int64_t>(WAVE, (per + WAVE - 1) / WAVE * WAVE);
+    ka.pods_per_block = (int32_t)per;
+    blocks = (int32_t)((a.n_pods + per - 1) / per);
+  }
   if (nw == 1) return launch_seq_nw<1, false>(ka, rs, blocks, s);
   if (nw == 4) return launch_seq_nw<4, false>(ka, rs, blocks, s);
   return launch_seq_nw<15, false>(ka, rs, blocks, s);
