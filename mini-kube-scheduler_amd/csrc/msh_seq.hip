@@ -142,7 +142,10 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
   // device-memory atomics. Split: each 64-pod block counts its commits in LDS and adds one device
   // atomic per distinct node (a digit's pods all land on its first feasible match: a device atomic per
-  // commit from every workgroup queues on a few addresses, 149 against 26 us per C5 launch).
+  // commit from every workgroup queues on a few addresses, 149 against 26 us per C5 launch). (Merging
+  // the blocks' counts per group of 32 blocks before the device atomics, through staging rows and a
+  // last-block-of-the-group ticket, needs an agent-scope release per block, an L2 write-back on
+  // MI355X: 52 us.)
   constexpr bool LDSC = NW <= 4;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first

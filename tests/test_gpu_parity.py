@@ -317,6 +317,32 @@ def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split, monkeypatch):
         msh.DeviceContext(0)
 
 
+def test_sequential_pod_blocks_two_streams(msh, oracle):
+    """Two pod-block sequential launches of one ctx on two streams, back to back (their blocks add to
+    the same device counts): each batch's placements and the summed node counts equal the serial
+    loop's."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(4242)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, 1)
+    u, nd, pd, pt = _rand_case(rng, 3000, 50_000, p_unsched=0.2, p_tol=0.1)
+    halves = [(pd[:20_000], pt[:20_000]), (pd[20_000:], pt[20_000:])]
+    with msh.DeviceContext(0) as ctx:
+        _set(ctx, msh, ps)
+        ctx.upload_nodes(u, nd)
+        bufs = [_dev_batch(torch, dev, a, b) for a, b in halves]
+        streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        torch.cuda.synchronize()
+        for t, st in zip(bufs, streams):
+            ctx.schedule_sequential_device(len(t[0]), t[0].data_ptr(), t[1].data_ptr(), 0, t[2].data_ptr(),
+                                           t[3].data_ptr(), t[4].data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, 0)
+        got = tuple(np.concatenate([t[i].cpu().numpy() for t in bufs]) for i in (2, 3, 4))
+        _assert_same(got, (want_i, want_s, want_st), "two streams")
+        assert (ctx.node_pod_counts() == want_counts).all()
+
+
 @pytest.mark.parametrize("seq_waves", ["1", "16"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("combo", range(len(PLUGIN_COMBOS)))
