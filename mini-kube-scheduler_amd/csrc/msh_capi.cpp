@@ -112,8 +112,11 @@ struct msh_ctx {
   int cur = 0;
   // sequential-mode state (not versioned: carried from call to call): pods committed per node, and
   // the sequential launches in flight that update it
+  // (msh::SEQ_COUNT_REPLICAS arrays of counts_cap; counts_dirty: replicas 1.. may hold counts, folded
+  // into replica 0 by the next one-workgroup launch or count read)
   int32_t* d_counts = nullptr;
   size_t counts_cap = 0;
+  bool counts_dirty = false;
   std::vector<std::pair<hipStream_t, hipEvent_t>> seq_inflight;
   // the rewrites' own stream, created with the device's highest priority: HIP gives each priority
   // its own hardware queues, so a rewrite never queues behind other streams' kernels that happen to
@@ -482,11 +485,12 @@ int rewrite(msh_ctx* c, const Rewrite& w) {
       (void)hipFree(c->d_counts);
       c->d_counts = nullptr;
       c->counts_cap = 0;
-      MSH_HIP(c, hipMalloc(&c->d_counts, (size_t)n_pad * sizeof(int32_t)));
+      MSH_HIP(c, hipMalloc(&c->d_counts, msh::SEQ_COUNT_REPLICAS * (size_t)n_pad * sizeof(int32_t)));
       c->counts_cap = (size_t)n_pad;
     }
     if ((rc = after_seq(c)) != MSH_OK) return rc;
-    MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->counts_cap * sizeof(int32_t), ps));
+    MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, msh::SEQ_COUNT_REPLICAS * c->counts_cap * sizeof(int32_t), ps));
+    c->counts_dirty = false;
   }
   MSH_HIP(c, hipStreamSynchronize(ps));
   c->cur = s;
@@ -1210,6 +1214,14 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   a.pp = c->pp;
   a.max_pods = max_pods_per_node;
   a.counts = c->d_counts;
+  a.count_stride = (int64_t)c->counts_cap;
+  const bool split = msh::seq_blocks(a, c->dev) > 1;
+  a.fold = !split && c->counts_dirty ? 1 : 0;
+  // one sequential launch of a ctx at a time: each commits into (and a fold rewrites) the same counts,
+  // so this stream first waits for the ctx's sequential launches in flight on other streams
+  if (p > 0)
+    for (auto& ev : c->seq_inflight)
+      if (ev.first != s) MSH_HIP(c, hipStreamWaitEvent(s, ev.second, 0));
   a.out_idx = d_out_idx;
   a.out_score = d_out_score;
   a.out_status = d_out_status;
@@ -1223,6 +1235,7 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
     if (!err.empty()) return fail(c, MSH_ERR_UNSUPPORTED, err);
     return hip_fail(c, e, "seq_kernel");
   }
+  if (p > 0) c->counts_dirty = split || (c->counts_dirty && !a.fold);
   return p > 0 ? track_launch(c, s, true) : MSH_OK;
 }
 
@@ -1260,6 +1273,11 @@ int msh_node_pod_counts(msh_ctx* c, int32_t* out_counts) {
   DeviceGuard g(c->device);
   int rc = after_seq(c);  // sequential launches of this ctx in flight update the counts
   if (rc != MSH_OK) return rc;
+  if (c->counts_dirty) {
+    hipError_t e = msh::launch_count_fold(c->d_counts, (int64_t)c->counts_cap, c->n_nodes, c->prep_stream);
+    if (e != hipSuccess) return hip_fail(c, e, "count_fold_kernel");
+    c->counts_dirty = false;
+  }
   MSH_HIP(c, hipMemcpyAsync(out_counts, c->d_counts, (size_t)c->n_nodes * sizeof(int32_t), hipMemcpyDeviceToHost,
                             c->prep_stream));
   MSH_HIP(c, hipStreamSynchronize(c->prep_stream));
@@ -1273,8 +1291,10 @@ int msh_reset_node_pod_counts(msh_ctx* c) {
   DeviceGuard g(c->device);
   int rc = after_seq(c);  // sequential launches of this ctx in flight update the counts
   if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, c->counts_cap * sizeof(int32_t), c->prep_stream));
+  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, msh::SEQ_COUNT_REPLICAS * c->counts_cap * sizeof(int32_t),
+                            c->prep_stream));
   MSH_HIP(c, hipStreamSynchronize(c->prep_stream));
+  c->counts_dirty = false;
   return MSH_OK;
 }
 

@@ -195,12 +195,25 @@ struct SeqArgs {
   int32_t n_pods;
   PluginParams pp;
   int32_t max_pods;
-  int32_t* counts;           // [n_pad] per-node assigned pods (read at start, updated)
+  // per-node assigned pods, SEQ_COUNT_REPLICAS arrays of count_stride: a node's count is its sum over
+  // the replicas (pod blocks add to replica blockIdx % SEQ_COUNT_REPLICAS); read at start, updated
+  int32_t* counts;
+  int64_t count_stride;
+  int32_t fold;              // one workgroup: first fold replicas 1.. into replica 0 (some hold counts)
   int32_t* out_idx;
   int64_t* out_score;
   int32_t* out_status;
   int32_t pods_per_block;    // set by the launcher: pods per workgroup (the whole batch when one workgroup)
 };
+
+// Pod blocks add their commits to one of this many count replicas: a digit's pods all land on its
+// first feasible match, and device atomics from every block onto one address queue
+constexpr int SEQ_COUNT_REPLICAS = 16;
+// Workgroups launch_sequential runs the batch on: 64-pod blocks without a capacity on tables whose
+// counts fit LDS (DeviceInfo::seq_split), else 1.
+int32_t seq_blocks(const SeqArgs& a, const DeviceInfo& dev);
+// counts[i] (replica 0) = the node's sum over the replicas, the others zeroed, for i < n
+hipError_t launch_count_fold(int32_t* counts, int64_t stride, int32_t n, hipStream_t s);
 
 hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err);
 

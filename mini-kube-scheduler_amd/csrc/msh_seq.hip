@@ -141,8 +141,9 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   }
   // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
   // device-memory atomics. Split: each 64-pod block counts its commits in LDS and adds one device
-  // atomic per distinct node (a digit's pods all land on its first feasible match: a device atomic per
-  // commit from every workgroup queues on a few addresses, 149 against 26 us per C5 launch). (Merging
+  // atomic per distinct node to its count replica (a digit's pods all land on its first feasible match:
+  // a device atomic per commit from every workgroup onto one array queues on a few addresses, 149 us
+  // per C5 launch; one per block and node, 26 us). (Merging
   // the blocks' counts per group of 32 blocks before the device atomics, through staging rows and a
   // last-block-of-the-group ticket, needs an agent-scope release per block, an L2 write-back on
   // MI355X: 52 us.)
@@ -156,6 +157,17 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   const int wv = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool scanner = !FIN || wv < NW;
 
+  if (a0.fold && !split) {  // one workgroup: the replicas' counts into replica 0 first
+    for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) {
+      int32_t sum = 0;
+      for (int k = 1; k < SEQ_COUNT_REPLICAS; ++k) {
+        sum += a.counts[k * a.count_stride + i];
+        a.counts[k * a.count_stride + i] = 0;
+      }
+      a.counts[i] += sum;
+    }
+    __syncthreads();
+  }
   uint32_t D0[RS], D1[RS], D2[RS], D3[RS], XX[RS], VV[RS], FULL[RS];
 #pragma unroll
   for (int r = 0; r < RS; ++r) {
@@ -297,7 +309,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
             // the device counts and clears it for the next block
             const int32_t c = lcnt[sel];
             lcnt[sel] = 0;
-            atomicAdd(&counts[sel], c);
+            atomicAdd(&counts[(int64_t)(blockIdx.x % SEQ_COUNT_REPLICAS) * a0.count_stride + sel], c);
           }
         } else {
           atomicAdd(&counts[sel], 1);  // one workgroup (the launcher splits LDS-count tables only)
@@ -496,16 +508,49 @@ hipError_t launch_seq_nw(const SeqArgs& a, int rs, int32_t blocks, hipStream_t s
 // (368,640 nodes; 6 x 12 plane VGPRs per lane), 16 waves with up to 8 with one (262,144 nodes; the
 // FULL plane makes 7 per word, and 12 words spill). Per-pod latency is one wave's scan plus one DPP
 // reduction; extra waves add an LDS exchange and a barrier.
-hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err) {
-  if (a.n_pods == 0) return hipSuccess;
+namespace {
+int seq_waves_for(const SeqArgs& a, const DeviceInfo& dev) {
   const bool cap = a.max_pods > 0;
   const int nw_big = cap ? 16 : 15;
   auto rs_for = [&](int nw) { return (a.n_words + nw * WAVE - 1) / (nw * WAVE); };
   int nw = dev.seq_waves > 0 ? dev.seq_waves : (rs_for(1) <= 4 ? 1 : rs_for(4) <= 4 ? 4 : nw_big);
   if (nw != 1 && nw != 4) nw = nw_big;
+  if (rs_for(nw) > (nw == nw_big ? (cap ? 8 : 12) : 4)) nw = nw_big;  // an override too small for the table
+  return nw;
+}
+
+__global__ void count_fold_kernel(int32_t* counts, int64_t stride, int32_t n) {
+  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  int32_t sum = counts[i];
+  for (int k = 1; k < SEQ_COUNT_REPLICAS; ++k) {
+    sum += counts[k * stride + i];
+    counts[k * stride + i] = 0;
+  }
+  counts[i] = sum;
+}
+}  // namespace
+
+hipError_t launch_count_fold(int32_t* counts, int64_t stride, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  count_fold_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(counts, stride, n);
+  return hipGetLastError();
+}
+
+// Tables whose counts fit LDS only (up to four scanning waves, 32,768 nodes): a larger table's blocks
+// would have no LDS to count in.
+int32_t seq_blocks(const SeqArgs& a, const DeviceInfo& dev) {
+  if (a.max_pods > 0 || !dev.seq_split || a.n_pods <= WAVE || seq_waves_for(a, dev) > 4) return 1;
+  return (a.n_pods + WAVE - 1) / WAVE;
+}
+
+hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err) {
+  if (a.n_pods == 0) return hipSuccess;
+  const bool cap = a.max_pods > 0;
+  const int nw_big = cap ? 16 : 15;
   const int rs_max = cap ? 8 : 12;
-  if (rs_for(nw) > (nw == nw_big ? rs_max : 4)) nw = nw_big;  // an override too small for the table
-  const int rs = rs_for(nw);
+  const int nw = seq_waves_for(a, dev);
+  const int rs = (a.n_words + nw * WAVE - 1) / (nw * WAVE);
   if (rs > rs_max) {
     if (err)
       *err = "sequential mode keeps the node table in registers: at most " +
@@ -519,18 +564,10 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
     if (nw == 4) return launch_seq_nw<4, true>(ka, rs, 1, s);
     return launch_seq_nw<16, true>(ka, rs, 1, s);
   }
-  // Without a capacity: blocks of consecutive pods (a multiple of 64), about eight per CU, each one
-  // workgroup walking its pods in order (MSH_SEQ_SPLIT=serial: one workgroup for the whole batch).
-  // Tables whose counts fit LDS only (up to four scanning waves, 32,768 nodes): a larger table's
-  // blocks would add every commit to the device counts, and a digit's pods all land on one node.
-  int32_t blocks = 1;
-  if (dev.seq_split && nw <= 4) {
-    const int64_t want = (int64_t)dev.cus * 8;
-    int64_t per = (a.n_pods + want - 1) / want;
-    per = std::max<int64_t>(WAVE, (per + WAVE - 1) / WAVE * WAVE);
-    ka.pods_per_block = (int32_t)per;
-    blocks = (int32_t)((a.n_pods + per - 1) / per);
-  }
+  // Without a capacity: 64-pod blocks of consecutive pods, each one workgroup walking its pods in
+  // order (MSH_SEQ_SPLIT=serial: one workgroup for the whole batch)
+  const int32_t blocks = seq_blocks(a, dev);
+  if (blocks > 1) ka.pods_per_block = WAVE;
   if (nw == 1) return launch_seq_nw<1, false>(ka, rs, blocks, s);
   if (nw == 4) return launch_seq_nw<4, false>(ka, rs, blocks, s);
   return launch_seq_nw<15, false>(ka, rs, blocks, s);

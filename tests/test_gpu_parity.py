@@ -317,6 +317,28 @@ def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split, monkeypatch):
         msh.DeviceContext(0)
 
 
+def test_sequential_count_replicas(msh, oracle):
+    """Pod-block launches add their commits to count replicas; the next one-workgroup launch (here a
+    capacity launch, which reads the counts) and msh_node_pod_counts fold them first. Blocks, a small
+    serial batch, blocks again, then a capacity batch, against the oracle's serial loop with a capacity
+    no earlier batch reaches (so it acts only on the last)."""
+    rng = np.random.default_rng(99)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, 0)
+    u, nd, pd, pt = _rand_case(rng, 2000, 31_000, p_unsched=0.2, p_tol=0.1)
+    cuts = [0, 10_000, 10_040, 30_000, 31_000]
+    pre = oracle.c_schedule_sequential(u, nd, pd[:30_000], pt[:30_000], ps, 0)[3]
+    cap = int(pre.max()) + 3
+    want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, cap)
+    with msh.DeviceContext(0) as ctx:
+        _set(ctx, msh, ps)
+        ctx.upload_nodes(u, nd)
+        parts = [ctx.schedule_sequential(pd[a:b], pt[a:b], cap if b == 31_000 else 0)
+                 for a, b in zip(cuts, cuts[1:])]
+        _assert_same(tuple(np.concatenate(x) for x in zip(*parts)), (want_i, want_s, want_st), "replicas")
+        assert (ctx.node_pod_counts() == want_counts).all()
+        assert want_counts.max() == cap  # the capacity did act on the last batch
+
+
 def test_sequential_pod_blocks_two_streams(msh, oracle):
     """Two pod-block sequential launches of one ctx on two streams, back to back (their blocks add to
     the same device counts): each batch's placements and the summed node counts equal the serial
