@@ -125,9 +125,9 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   constexpr bool FIN = !CAP && NW > 1;  // a finalizer wave decodes, keeps the outputs and commits
   constexpr int FINW = FIN ? NW : 0;    // the wave that keeps the outputs
   // Without a capacity no commit feeds a later decision, so the launcher may split the pods into
-  // blocks of consecutive pods, one workgroup each (as ranks split them in pod-sharded sequential
-  // mode): each walks its block in order against the whole table, and its commits are added to the
-  // device counts (atomics), which then equal the serial loop's. With a capacity: one workgroup.
+  // 64-pod blocks of consecutive pods, one workgroup each (as ranks split them in pod-sharded
+  // sequential mode): each walks its block in order against the whole table, and its commits are
+  // added to the device counts, which then equal the serial loop's. With a capacity: one workgroup.
   const bool split = !CAP && gridDim.x > 1;
   SeqArgs a = a0;
   if (split) {
@@ -139,14 +139,14 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
     if (a.out_score) a.out_score += j0;
     a.out_status += j0;
   }
-  // counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
-  // device-memory atomics. Split: each 64-pod block counts its commits in LDS and adds one device
-  // atomic per distinct node to its count replica (a digit's pods all land on its first feasible match:
-  // a device atomic per commit from every workgroup onto one array queues on a few addresses, 149 us
-  // per C5 launch; one per block and node, 26 us). (Merging
-  // the blocks' counts per group of 32 blocks before the device atomics, through staging rows and a
-  // last-block-of-the-group ticket, needs an agent-scope release per block, an L2 write-back on
-  // MI355X: 52 us.)
+  // Counts in LDS (up to 4 waves x 64 lanes x 4 words x 32 nodes = 32,768 nodes, 128 KB), else
+  // device-memory atomics (one workgroup only). Split: a block counts its 64 commits in LDS and adds
+  // one device atomic per node it reached, into count replica blockIdx % SEQ_COUNT_REPLICAS. A digit's
+  // pods all land on its first feasible match, so device atomics from every block onto one array queue
+  // on about ten addresses. Per C5 launch (1,563 blocks): one atomic per commit 149 us, one per block
+  // and node 26 us, the same over 16 replicas 11.6 us (11.3 without any add). (Merging 32 blocks'
+  // counts through staging rows and a last-block ticket needs an agent-scope release per block, an L2
+  // write-back on MI355X: 52 us.)
   constexpr bool LDSC = NW <= 4;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // per-step exchange slots (NW > 1), triple-buffered: [slot][pod of the step][first match, first
