@@ -10,7 +10,8 @@ MODE
   generic_col  generic_kernel on NodeNumber + ScoreColumn0 (weight 2, DefaultNormalizeScore), 32 batches
                per launch (bench.py's generic.nodenumber_plus_default_column)
   sequential   C5: each pod in order (seq_kernel; MSH_SEQ_SPLIT=serial: the whole batch in one workgroup)
-NORM / WEIGHT: msh_normalize and weight of the NodeNumber entry (bench.py's headline: WEIGHT=3 NORM=1)."""
+NORM / WEIGHT: msh_normalize and weight of the NodeNumber entry (bench.py's headline: WEIGHT=3 NORM=1).
+NB: batches per launch in the multi-batch modes (default 32)."""
 import importlib
 import os
 import sys
@@ -45,7 +46,7 @@ else:
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                     [msh.ScorePluginConfig(msh.NODE_NUMBER, weight, msh.Normalize(norm))])
 dev = torch.device("cuda:0")
-nb = msh._native.BATCHES_PER_LAUNCH if mode in ("multi", "generic", "generic_col") else 1
+nb = int(os.environ.get("NB", msh._native.BATCHES_PER_LAUNCH)) if mode in ("multi", "generic", "generic_col") else 1
 bufs = [(torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev), torch.empty(p, dtype=torch.int32, device=dev),
          torch.empty(p, dtype=torch.int64, device=dev), torch.empty(p, dtype=torch.int32, device=dev))
         for _ in range(nb)]
