@@ -686,17 +686,25 @@ hipError_t launch_gen_k(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
   return hipGetLastError();
 }
 
+// At most one normalizing column, 32- or 64-bit totals: {a node-only sum or not} x {no normalizing
+// column, one DEFAULT / REVERSE column, one MIN-MAX column}
+template <int MODE, bool W64>
+hipError_t launch_gen_w(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
+  const bool ts = a.nts > 0;
+  if (a.nnc == 0) return ts ? launch_gen_k<MODE, W64, true, 0, false>(a, bx, lds, s)
+                            : launch_gen_k<MODE, W64, false, 0, false>(a, bx, lds, s);
+  const bool mm = a.nmode[0] == 3;
+  if (ts) return mm ? launch_gen_k<MODE, W64, true, 1, true>(a, bx, lds, s)
+                    : launch_gen_k<MODE, W64, true, 1, false>(a, bx, lds, s);
+  return mm ? launch_gen_k<MODE, W64, false, 1, true>(a, bx, lds, s)
+            : launch_gen_k<MODE, W64, false, 1, false>(a, bx, lds, s);
+}
+
 template <int MODE>
 hipError_t launch_gen_mode(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
-  const bool ts = a.nts > 0;
-  if (a.w64 || a.nnc > 1) return launch_gen_k<MODE, true, true, 4, true>(a, bx, lds, s);  // the general form
-  if (a.nnc == 0) return ts ? launch_gen_k<MODE, false, true, 0, false>(a, bx, lds, s)
-                            : launch_gen_k<MODE, false, false, 0, false>(a, bx, lds, s);
-  const bool mm = a.nmode[0] == 3;
-  if (ts) return mm ? launch_gen_k<MODE, false, true, 1, true>(a, bx, lds, s)
-                    : launch_gen_k<MODE, false, true, 1, false>(a, bx, lds, s);
-  return mm ? launch_gen_k<MODE, false, false, 1, true>(a, bx, lds, s)
-            : launch_gen_k<MODE, false, false, 1, false>(a, bx, lds, s);
+  // two or more normalizing columns: the general form (64-bit totals, a runtime column count)
+  if (a.nnc > 1) return launch_gen_k<MODE, true, true, 4, true>(a, bx, lds, s);
+  return a.w64 ? launch_gen_w<MODE, true>(a, bx, lds, s) : launch_gen_w<MODE, false>(a, bx, lds, s);
 }
 }  // namespace
 
@@ -711,8 +719,8 @@ hipError_t launch_generic(GenericArgs& a, int mode, const DeviceInfo& dev, hipSt
     groups += (a.d[b].n_pods + GEN_BPW * WAVE - 1) / (GEN_BPW * WAVE);
   }
   if (maxp == 0) return hipSuccess;
-  const bool general = a.w64 || a.nnc > 1;
-  const size_t key = general ? 8 : 4;
+  const bool general = a.nnc > 1;  // launch_gen_mode's general form
+  const size_t key = (general || a.w64) ? 8 : 4;
   const int nnc = general ? a.nnc : std::min(a.nnc, 1);
   // bytes per staged node: the record, the node-only sum (the general form always stages it), the
   // normalizing columns
