@@ -698,6 +698,22 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
         "lane_ops_per_eval_counter": entry["SQ_INSTS_VALU"] * 64 / (float(n) * p * G) if entry else None,
         "check": "sampled (1,500 pods of 2 batches) bit-exact vs a direct evaluation" if ok else "MISMATCH"}
+    # a column over the whole int32 range: no 32-bit bound on the totals, generic_kernel's 64-bit form
+    wide = ((np.arange(n, dtype=np.int64) * 2654435761) % (1 << 32)) - (1 << 31)
+    gctx.upload_score_column("ScoreColumn0", wide)
+    for key, cn in (("wide_column_none", 0), ("wide_column_default", 1)):
+        plugins = [("NodeNumber", 1, 0), ("ScoreColumn0", 1, cn)]
+        gctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                         [msh.ScorePluginConfig(nm, w, msh.Normalize(m)) for nm, w, m in plugins])
+        ms = run_multi(gctx, R=5)
+        ok = all(same(tuple(x[sample] for x in got(b)),
+                      direct_plugins(u, nd, pp[0][sample], pp[1][sample], plugins, {0: wide}))
+                 for b, pp in list(zip(bufs, pods))[:2])
+        gen[key] = {"kernel": f"void msh::generic_kernel<0, true, {'true' if cn == 0 else 'false'}, {0 if cn == 0 else 1}, false>",
+                    "plugins": f"score=[NodeNumber w=1, ScoreColumn0 w=1 {NORM_NAMES[cn]}] (column over the whole int32 range)",
+                    "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G,
+                    "evals_per_s": n * p * G / (ms * 1e-3),
+                    "check": "sampled (1,500 pods of 2 batches) bit-exact vs a direct evaluation" if ok else "MISMATCH"}
     out["generic"] = gen
     gctx.close()
 
