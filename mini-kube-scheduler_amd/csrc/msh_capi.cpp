@@ -112,10 +112,12 @@ struct msh_ctx {
   int cur = 0;
   // sequential-mode state (not versioned: carried from call to call): pods committed per node, and
   // the sequential launches in flight that update it
-  // (msh::SEQ_COUNT_REPLICAS arrays of counts_cap; counts_dirty: replicas 1.. may hold counts, folded
-  // into replica 0 by the next one-workgroup launch or count read)
+  // (counts_replicas arrays of counts_cap: msh::SEQ_COUNT_REPLICAS for tables pod blocks can take, else
+  // 1; counts_dirty: replicas 1.. may hold counts, folded into replica 0 by the next one-workgroup
+  // launch or count read)
   int32_t* d_counts = nullptr;
   size_t counts_cap = 0;
+  int32_t counts_replicas = 1;
   bool counts_dirty = false;
   std::vector<std::pair<hipStream_t, hipEvent_t>> seq_inflight;
   // the rewrites' own stream, created with the device's highest priority: HIP gives each priority
@@ -480,16 +482,19 @@ int rewrite(msh_ctx* c, const Rewrite& w) {
   }
   // an upload zeroes the sequential-mode counts (after the sequential launches in flight)
   if (up) {
-    if ((size_t)n_pad > c->counts_cap) {
+    const int32_t replicas = n_pad <= msh::SEQ_SPLIT_MAX_NODES ? msh::SEQ_COUNT_REPLICAS : 1;
+    if ((size_t)n_pad > c->counts_cap || replicas > c->counts_replicas) {
       wait_events(c->seq_inflight);
       (void)hipFree(c->d_counts);
       c->d_counts = nullptr;
       c->counts_cap = 0;
-      MSH_HIP(c, hipMalloc(&c->d_counts, msh::SEQ_COUNT_REPLICAS * (size_t)n_pad * sizeof(int32_t)));
+      c->counts_replicas = 1;
+      MSH_HIP(c, hipMalloc(&c->d_counts, (size_t)replicas * (size_t)n_pad * sizeof(int32_t)));
       c->counts_cap = (size_t)n_pad;
+      c->counts_replicas = replicas;
     }
     if ((rc = after_seq(c)) != MSH_OK) return rc;
-    MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, msh::SEQ_COUNT_REPLICAS * c->counts_cap * sizeof(int32_t), ps));
+    MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, (size_t)c->counts_replicas * c->counts_cap * sizeof(int32_t), ps));
     c->counts_dirty = false;
   }
   MSH_HIP(c, hipStreamSynchronize(ps));
@@ -1215,6 +1220,7 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   a.max_pods = max_pods_per_node;
   a.counts = c->d_counts;
   a.count_stride = (int64_t)c->counts_cap;
+  a.count_replicas = c->counts_replicas;
   const bool split = msh::seq_blocks(a, c->dev) > 1;
   a.fold = !split && c->counts_dirty ? 1 : 0;
   // one sequential launch of a ctx at a time: each commits into (and a fold rewrites) the same counts,
@@ -1274,7 +1280,8 @@ int msh_node_pod_counts(msh_ctx* c, int32_t* out_counts) {
   int rc = after_seq(c);  // sequential launches of this ctx in flight update the counts
   if (rc != MSH_OK) return rc;
   if (c->counts_dirty) {
-    hipError_t e = msh::launch_count_fold(c->d_counts, (int64_t)c->counts_cap, c->n_nodes, c->prep_stream);
+    hipError_t e = msh::launch_count_fold(c->d_counts, (int64_t)c->counts_cap, c->counts_replicas, c->n_nodes,
+                                          c->prep_stream);
     if (e != hipSuccess) return hip_fail(c, e, "count_fold_kernel");
     c->counts_dirty = false;
   }
@@ -1291,7 +1298,7 @@ int msh_reset_node_pod_counts(msh_ctx* c) {
   DeviceGuard g(c->device);
   int rc = after_seq(c);  // sequential launches of this ctx in flight update the counts
   if (rc != MSH_OK) return rc;
-  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, msh::SEQ_COUNT_REPLICAS * c->counts_cap * sizeof(int32_t),
+  MSH_HIP(c, hipMemsetAsync(c->d_counts, 0, (size_t)c->counts_replicas * c->counts_cap * sizeof(int32_t),
                             c->prep_stream));
   MSH_HIP(c, hipStreamSynchronize(c->prep_stream));
   c->counts_dirty = false;

@@ -195,10 +195,11 @@ struct SeqArgs {
   int32_t n_pods;
   PluginParams pp;
   int32_t max_pods;
-  // per-node assigned pods, SEQ_COUNT_REPLICAS arrays of count_stride: a node's count is its sum over
-  // the replicas (pod blocks add to replica blockIdx % SEQ_COUNT_REPLICAS); read at start, updated
+  // per-node assigned pods, count_replicas arrays of count_stride: a node's count is its sum over the
+  // replicas (pod blocks add to replica blockIdx % SEQ_COUNT_REPLICAS); read at start, updated
   int32_t* counts;
   int64_t count_stride;
+  int32_t count_replicas;    // 1, or SEQ_COUNT_REPLICAS (pod blocks need them all)
   int32_t fold;              // one workgroup: first fold replicas 1.. into replica 0 (some hold counts)
   int32_t* out_idx;
   int64_t* out_score;
@@ -207,13 +208,15 @@ struct SeqArgs {
 };
 
 // Pod blocks add their commits to one of this many count replicas: a digit's pods all land on its
-// first feasible match, and device atomics from every block onto one address queue
+// first feasible match, and device atomics from every block onto one address queue. Tables up to
+// SEQ_SPLIT_MAX_NODES only (pod blocks count in LDS), so larger ones keep one count array.
 constexpr int SEQ_COUNT_REPLICAS = 16;
+constexpr int32_t SEQ_SPLIT_MAX_NODES = 4 * 64 * 4 * 32;  // four scanning waves x 64 lanes x 4 words
 // Workgroups launch_sequential runs the batch on: 64-pod blocks without a capacity on tables whose
 // counts fit LDS (DeviceInfo::seq_split), else 1.
 int32_t seq_blocks(const SeqArgs& a, const DeviceInfo& dev);
 // counts[i] (replica 0) = the node's sum over the replicas, the others zeroed, for i < n
-hipError_t launch_count_fold(int32_t* counts, int64_t stride, int32_t n, hipStream_t s);
+hipError_t launch_count_fold(int32_t* counts, int64_t stride, int32_t replicas, int32_t n, hipStream_t s);
 
 hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err);
 

@@ -160,7 +160,7 @@ __global__ __launch_bounds__((NW + ((!CAP && NW > 1) ? 1 : 0)) * 64) void seq_ke
   if (a0.fold && !split) {  // one workgroup: the replicas' counts into replica 0 first
     for (int32_t i = threadIdx.x; i < a.n_words * 32; i += blockDim.x) {
       int32_t sum = 0;
-      for (int k = 1; k < SEQ_COUNT_REPLICAS; ++k) {
+      for (int k = 1; k < a.count_replicas; ++k) {
         sum += a.counts[k * a.count_stride + i];
         a.counts[k * a.count_stride + i] = 0;
       }
@@ -519,11 +519,11 @@ int seq_waves_for(const SeqArgs& a, const DeviceInfo& dev) {
   return nw;
 }
 
-__global__ void count_fold_kernel(int32_t* counts, int64_t stride, int32_t n) {
+__global__ void count_fold_kernel(int32_t* counts, int64_t stride, int32_t replicas, int32_t n) {
   const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
   if (i >= n) return;
   int32_t sum = counts[i];
-  for (int k = 1; k < SEQ_COUNT_REPLICAS; ++k) {
+  for (int k = 1; k < replicas; ++k) {
     sum += counts[k * stride + i];
     counts[k * stride + i] = 0;
   }
@@ -531,16 +531,18 @@ __global__ void count_fold_kernel(int32_t* counts, int64_t stride, int32_t n) {
 }
 }  // namespace
 
-hipError_t launch_count_fold(int32_t* counts, int64_t stride, int32_t n, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  count_fold_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(counts, stride, n);
+hipError_t launch_count_fold(int32_t* counts, int64_t stride, int32_t replicas, int32_t n, hipStream_t s) {
+  if (n <= 0 || replicas <= 1) return hipSuccess;
+  count_fold_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(counts, stride, replicas, n);
   return hipGetLastError();
 }
 
 // Tables whose counts fit LDS only (up to four scanning waves, 32,768 nodes): a larger table's blocks
 // would have no LDS to count in.
 int32_t seq_blocks(const SeqArgs& a, const DeviceInfo& dev) {
-  if (a.max_pods > 0 || !dev.seq_split || a.n_pods <= WAVE || seq_waves_for(a, dev) > 4) return 1;
+  if (a.max_pods > 0 || !dev.seq_split || a.n_pods <= WAVE || a.count_replicas < SEQ_COUNT_REPLICAS ||
+      seq_waves_for(a, dev) > 4)
+    return 1;
   return (a.n_pods + WAVE - 1) / WAVE;
 }
 

@@ -321,7 +321,8 @@ def test_sequential_count_replicas(msh, oracle):
     """Pod-block launches add their commits to count replicas; the next one-workgroup launch (here a
     capacity launch, which reads the counts) and msh_node_pod_counts fold them first. Blocks, a small
     serial batch, blocks again, then a capacity batch, against the oracle's serial loop with a capacity
-    no earlier batch reaches (so it acts only on the last)."""
+    no earlier batch reaches (so it acts only on the last); the ctx held a table too large for pod
+    blocks (one count array) before, so the upload reallocates the counts with their replicas."""
     rng = np.random.default_rng(99)
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, 0)
     u, nd, pd, pt = _rand_case(rng, 2000, 31_000, p_unsched=0.2, p_tol=0.1)
@@ -331,6 +332,10 @@ def test_sequential_count_replicas(msh, oracle):
     want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, cap)
     with msh.DeviceContext(0) as ctx:
         _set(ctx, msh, ps)
+        # a table past the pod-block limit first (one count array), then this one (the replicas)
+        ub, ndb = _rand_case(rng, 40_000, 10)[:2]
+        ctx.upload_nodes(ub, ndb)
+        ctx.schedule_sequential(pd[:300], pt[:300], 0)
         ctx.upload_nodes(u, nd)
         parts = [ctx.schedule_sequential(pd[a:b], pt[a:b], cap if b == 31_000 else 0)
                  for a, b in zip(cuts, cuts[1:])]
