@@ -1,0 +1,103 @@
+"""Randomised GPU parity sweep (opt-in: MSH_FUZZ=<cases>; skipped otherwise, so the regular suite never
+runs it).
+
+Each case draws a table size, a pod count, the filter / prescore lists, a score list of NodeNumber and up to
+three score-column plugins with random weights and NormalizeScore modes, columns of random range (small,
+signed, the whole int32 range, constant) and random unschedulable / tolerates / no-digit rates, then runs
+the batch entry point and, for lists without score columns, the sequential one with and without a
+capacity, against the oracle (oracle/msh_oracle.c, the restatement of minisched/minisched.go:115-199,
+304-325): idx / score / status bit-exact, and the sequential node counts. The summary (cases per
+category, any mismatch with its seed) goes to $MSH_FUZZ_OUT (default gpurun_out/fuzz_summary.json).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = int(os.environ.get("MSH_FUZZ", "0"))
+COLS = ["ScoreColumn0", "ScoreColumn1", "ScoreColumn2", "ScoreColumn3"]
+WEIGHTS = [1, 2, 3, 7, 100, 1 << 16, 1 << 32]
+
+
+def _case(rng):
+    n = int(np.exp(rng.uniform(0, np.log(60_000))))
+    p = int(np.exp(rng.uniform(0, np.log(30_000))))
+    while n * p > 1.5e8:
+        p //= 2
+    p = max(p, 1)
+    unsched = (rng.random(n) < rng.choice([0.0, 0.1, 0.5, 1.0])).astype(np.uint8)
+    nd = rng.integers(0, 10, n).astype(np.int8)
+    nd[rng.random(n) < rng.choice([0.0, 0.1, 1.0])] = -1
+    pd = rng.integers(0, 10, p).astype(np.int8)
+    pd[rng.random(p) < rng.choice([0.0, 0.1, 1.0])] = -1
+    pt = (rng.random(p) < rng.choice([0.0, 0.05, 0.5, 1.0])).astype(np.uint8)
+    filters = ["NodeUnschedulable"] if rng.random() < 0.8 else []
+    prescore = ["NodeNumber"] if rng.random() < 0.8 else []
+    pool = ["NodeNumber"] + list(rng.choice(COLS, size=int(rng.integers(0, 4)), replace=False))
+    score = [s for s in rng.permutation(pool) if s != "NodeNumber" or rng.random() < 0.85]
+    weights = [int(rng.choice(WEIGHTS)) for _ in score]
+    norms = [int(rng.integers(0, 4)) for _ in score]
+    cols = {}
+    for k in range(4):
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            cols[k] = rng.integers(0, 101, n)
+        elif kind == 1:
+            cols[k] = rng.integers(-50, 51, n)
+        elif kind == 2:
+            cols[k] = rng.integers(-(1 << 31), (1 << 31) + 1, n)
+        else:
+            cols[k] = np.full(n, int(rng.integers(-5, 6)))
+    return n, p, unsched, nd, pd, pt, filters, prescore, score, weights, norms, cols
+
+
+@pytest.mark.skipif(CASES <= 0, reason="opt-in sweep: set MSH_FUZZ=<cases>")
+def test_fuzz_parity(msh, oracle):
+    out = Path(os.environ.get("MSH_FUZZ_OUT", "gpurun_out/fuzz_summary.json"))
+    out.parent.mkdir(parents=True, exist_ok=True)
+    seed0 = int(os.environ.get("MSH_FUZZ_SEED", "20261018"))
+    stats = {"batch": 0, "batch_w_columns": 0, "sequential": 0, "sequential_capacity": 0, "pairs": 0}
+    fails = []
+    t0 = time.time()
+    with msh.DeviceContext(0) as ctx:
+        for c in range(CASES):
+            seed = seed0 + c
+            rng = np.random.default_rng(seed)
+            n, p, u, nd, pd, pt, fl, pre, sc, w, nm, cols = _case(rng)
+            ps = oracle.PluginSet(filters=fl, prescore=pre, score=sc, weights=w, normalize=nm)
+            ctx.set_plugins(fl, pre, [msh.ScorePluginConfig(s, ww, msh.Normalize(m)) for s, ww, m in zip(sc, w, nm)])
+            ctx.upload_nodes(u, nd)
+            has_cols = any(s in COLS for s in sc)
+            for k in range(4):
+                if COLS[k] in sc:
+                    ctx.upload_score_column(COLS[k], cols[k])
+            got = ctx.schedule_batch(pd, pt)
+            want = oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=16, cols=cols)
+            stats["batch_w_columns" if has_cols else "batch"] += 1
+            stats["pairs"] += n * p
+            desc = {"seed": seed, "n": n, "p": p, "filters": fl, "prescore": pre, "score": sc, "weights": w,
+                    "normalize": nm}
+            if not all((g == x).all() for g, x in zip(got, want[:3])):
+                fails.append(dict(desc, mode="batch"))
+            if not has_cols:
+                cap = int(rng.choice([0, 0, 1, 3]))
+                ctx.reset_node_pod_counts()
+                got = ctx.schedule_sequential(pd, pt, cap)
+                want = oracle.c_schedule_sequential(u, nd, pd, pt, ps, cap)
+                stats["sequential_capacity" if cap else "sequential"] += 1
+                if not (all((g == x).all() for g, x in zip(got, want[:3]))
+                        and (ctx.node_pod_counts() == want[3]).all()):
+                    fails.append(dict(desc, mode="sequential", capacity=cap))
+            if (c + 1) % 25 == 0:
+                print(f"fuzz: {c + 1}/{CASES} cases, {len(fails)} mismatches, {time.time() - t0:.0f} s", flush=True)
+    summary = {"cases": CASES, "seed0": seed0, "counts": stats, "mismatches": fails,
+               "seconds": round(time.time() - t0, 1)}
+    out.write_text(json.dumps(summary, indent=1))
+    assert not fails, fails[:3]
