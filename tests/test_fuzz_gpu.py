@@ -4,8 +4,9 @@ runs it).
 Each case draws a table size, a pod count, the filter / prescore lists, a score list of NodeNumber and up to
 three score-column plugins with random weights and NormalizeScore modes, columns of random range (small,
 signed, the whole int32 range, constant) and random unschedulable / tolerates / no-digit rates, then runs
-the batch entry point and, for lists without score columns, the sequential one with and without a
-capacity, against the oracle (oracle/msh_oracle.c, the restatement of minisched/minisched.go:115-199,
+the batch entry point, then patches random nodes (msh_patch_nodes) and runs the multi-batch device
+entry point on 1-5 slices of the pods, and, for lists without score columns, the sequential one with
+and without a capacity, against the oracle (oracle/msh_oracle.c, the restatement of minisched/minisched.go:115-199,
 304-325): idx / score / status bit-exact, and the sequential node counts. The summary (cases per
 category, any mismatch with its seed) goes to $MSH_FUZZ_OUT (default gpurun_out/fuzz_summary.json).
 """
@@ -63,7 +64,9 @@ def test_fuzz_parity(msh, oracle):
     out = Path(os.environ.get("MSH_FUZZ_OUT", "gpurun_out/fuzz_summary.json"))
     out.parent.mkdir(parents=True, exist_ok=True)
     seed0 = int(os.environ.get("MSH_FUZZ_SEED", "20261018"))
-    stats = {"batch": 0, "batch_w_columns": 0, "sequential": 0, "sequential_capacity": 0, "pairs": 0}
+    torch = pytest.importorskip("torch")
+    stats = {"batch": 0, "batch_w_columns": 0, "patch_then_multi_batch": 0, "sequential": 0, "sequential_capacity": 0,
+             "pairs": 0}
     fails = []
     t0 = time.time()
     with msh.DeviceContext(0) as ctx:
@@ -86,6 +89,29 @@ def test_fuzz_parity(msh, oracle):
                     "normalize": nm}
             if not all((g == x).all() for g, x in zip(got, want[:3])):
                 fails.append(dict(desc, mode="batch"))
+            # a patch of random nodes (a cordon flip / digit change: msh_patch_nodes, inline or scattered),
+            # then the multi-batch device entry point on 1-5 slices of the pods
+            k = int(min(n, rng.choice([1, 5, 64, 65, 2000])))
+            pidx = rng.choice(n, size=k, replace=False).astype(np.int32)
+            u2, nd2 = u.copy(), nd.copy()
+            u2[pidx] = rng.integers(0, 2, k)
+            nd2[pidx] = rng.integers(-1, 10, k)
+            ctx.patch_nodes(pidx, u2[pidx], nd2[pidx])
+            cuts = np.unique(np.concatenate([[0, p], rng.integers(0, p + 1, int(rng.integers(0, 5)))]))
+            dev = torch.device("cuda:0")
+            bufs = [[torch.from_numpy(pd[x:y]).to(dev), torch.from_numpy(pt[x:y]).to(dev),
+                     torch.full((y - x,), -7, dtype=torch.int32, device=dev),
+                     torch.full((y - x,), -7, dtype=torch.int64, device=dev),
+                     torch.full((y - x,), -7, dtype=torch.int32, device=dev)] for x, y in zip(cuts, cuts[1:])]
+            descs = ctx.batch_descs([(len(b[0]), *[t.data_ptr() for t in b]) for b in bufs])
+            ctx.schedule_batches_device(descs, stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            got = tuple(np.concatenate([b[i].cpu().numpy() for b in bufs]) for i in (2, 3, 4))
+            want = oracle.c_schedule_batch(u2, nd2, pd, pt, ps, threads=16, cols=cols)
+            stats["patch_then_multi_batch"] += 1
+            if not all((g == x).all() for g, x in zip(got, want[:3])):
+                fails.append(dict(desc, mode="patch+multi", patched=k, batches=len(bufs)))
+            u, nd = u2, nd2
             if not has_cols:
                 cap = int(rng.choice([0, 0, 1, 3]))
                 ctx.reset_node_pod_counts()
