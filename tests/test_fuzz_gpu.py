@@ -5,8 +5,9 @@ Each case draws a table size, a pod count, the filter / prescore lists, a score 
 three score-column plugins with random weights and NormalizeScore modes, columns of random range (small,
 signed, the whole int32 range, constant) and random unschedulable / tolerates / no-digit rates, then runs
 the batch entry point, then patches random nodes (msh_patch_nodes) and runs the multi-batch device
-entry point on 1-5 slices of the pods, and, for lists without score columns, the sequential one with
-and without a capacity, against the oracle (oracle/msh_oracle.c, the restatement of minisched/minisched.go:115-199,
+entry point on 1-5 slices of the pods, then the node-sharded path over 2-4 shards at random bounds
+(merged in-process as the collectives would), and, for lists without score columns, the sequential one
+with and without a capacity, against the oracle (oracle/msh_oracle.c, the restatement of minisched/minisched.go:115-199,
 304-325): idx / score / status bit-exact, and the sequential node counts. The summary (cases per
 category, any mismatch with its seed) goes to $MSH_FUZZ_OUT (default gpurun_out/fuzz_summary.json).
 """
@@ -65,8 +66,8 @@ def test_fuzz_parity(msh, oracle):
     out.parent.mkdir(parents=True, exist_ok=True)
     seed0 = int(os.environ.get("MSH_FUZZ_SEED", "20261018"))
     torch = pytest.importorskip("torch")
-    stats = {"batch": 0, "batch_w_columns": 0, "patch_then_multi_batch": 0, "sequential": 0, "sequential_capacity": 0,
-             "pairs": 0}
+    stats = {"batch": 0, "batch_w_columns": 0, "patch_then_multi_batch": 0, "node_sharded": 0, "sequential": 0,
+             "sequential_capacity": 0, "pairs": 0}
     fails = []
     t0 = time.time()
     with msh.DeviceContext(0) as ctx:
@@ -112,6 +113,65 @@ def test_fuzz_parity(msh, oracle):
             if not all((g == x).all() for g, x in zip(got, want[:3])):
                 fails.append(dict(desc, mode="patch+multi", patched=k, batches=len(bufs)))
             u, nd = u2, nd2
+            # the node-sharded path on 2-4 shards at random List-order bounds, merged here as the
+            # collectives would (MAX / MIN over the shards' device buffers): the reference lists through
+            # msh_shard_keys_device + msh_decode_keys_device, score-column lists through msh_generic_*
+            if n >= 4:
+                nsh = int(rng.integers(2, 5))
+                bounds = [0] + sorted(int(x) for x in rng.choice(np.arange(1, n), size=nsh - 1, replace=False)) + [n]
+                d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
+                shards = []
+                for lo, hi in zip(bounds, bounds[1:]):
+                    c2 = msh.DeviceContext(0)
+                    c2.set_plugins(fl, pre, [msh.ScorePluginConfig(s_, ww, msh.Normalize(m)) for s_, ww, m in zip(sc, w, nm)])
+                    c2.upload_nodes(u[lo:hi], nd[lo:hi])
+                    for kk in range(4):
+                        if COLS[kk] in sc:
+                            c2.upload_score_column(COLS[kk], cols[kk][lo:hi])
+                    shards.append((c2, lo))
+                hs = torch.cuda.current_stream().cuda_stream
+                oi = torch.empty(p, dtype=torch.int32, device=dev)
+                osc = torch.empty(p, dtype=torch.int64, device=dev)
+                ost = torch.empty(p, dtype=torch.int32, device=dev)
+                if not has_cols:
+                    merged = None
+                    for c2, lo in shards:
+                        keys = torch.empty(c2.shard_keys_len(p), dtype=torch.int32, device=dev)
+                        c2.shard_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), lo, keys.data_ptr(), hs)
+                        merged = keys if merged is None else torch.maximum(merged, keys)
+                    shards[0][0].decode_keys_device(p, d_pd.data_ptr(), d_pt.data_ptr(), merged.data_ptr(),
+                                                    oi.data_ptr(), osc.data_ptr(), ost.data_ptr(), hs)
+                else:
+                    n_ext = shards[0][0].generic_ext_len(p)
+                    ext = None
+                    if n_ext:
+                        exts = []
+                        for c2, lo in shards:
+                            e_ = torch.empty(n_ext, dtype=torch.int64, device=dev)
+                            c2.generic_extents_device(p, d_pd.data_ptr(), d_pt.data_ptr(), e_.data_ptr(), hs)
+                            exts.append(e_)
+                        ext = torch.stack(exts).max(dim=0).values.contiguous()
+                    tots, idxs = [], []
+                    for c2, lo in shards:
+                        t_ = torch.empty(p, dtype=torch.int64, device=dev)
+                        i_ = torch.empty(p, dtype=torch.int32, device=dev)
+                        c2.generic_best_device(p, d_pd.data_ptr(), d_pt.data_ptr(), ext.data_ptr() if ext is not None else 0,
+                                               lo, t_.data_ptr(), i_.data_ptr(), hs)
+                        tots.append(t_)
+                        idxs.append(i_)
+                    mt = torch.stack(tots).max(dim=0).values.contiguous()
+                    for (c2, lo), t_, i_ in zip(shards, tots, idxs):
+                        c2.generic_candidates_device(p, t_.data_ptr(), mt.data_ptr(), i_.data_ptr(), hs)
+                    mi = torch.stack(idxs).min(dim=0).values.contiguous()
+                    shards[0][0].generic_decode_device(p, d_pd.data_ptr(), mt.data_ptr(), mi.data_ptr(), oi.data_ptr(),
+                                                       osc.data_ptr(), ost.data_ptr(), hs)
+                torch.cuda.synchronize()
+                got = (oi.cpu().numpy(), osc.cpu().numpy(), ost.cpu().numpy())
+                stats["node_sharded"] += 1
+                if not all((g == x).all() for g, x in zip(got, want[:3])):
+                    fails.append(dict(desc, mode="node-sharded", bounds=bounds))
+                for c2, _ in shards:
+                    c2.close()
             if not has_cols:
                 cap = int(rng.choice([0, 0, 1, 3]))
                 ctx.reset_node_pod_counts()
