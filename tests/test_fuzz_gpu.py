@@ -181,8 +181,10 @@ def test_fuzz_parity(msh, oracle):
                 if not (all((g == x).all() for g, x in zip(got, want[:3]))
                         and (ctx.node_pod_counts() == want[3]).all()):
                     fails.append(dict(desc, mode="sequential", capacity=cap))
-            if (c + 1) % 25 == 0:
-                print(f"fuzz: {c + 1}/{CASES} cases, {len(fails)} mismatches, {time.time() - t0:.0f} s", flush=True)
+            if (c + 1) % 25 == 0:  # progress to a file too: pytest holds the test's stdout until it ends
+                line = f"fuzz: {c + 1}/{CASES} cases, {len(fails)} mismatches, {time.time() - t0:.0f} s"
+                print(line, flush=True)
+                out.with_suffix(".progress").write_text(line + "\n")
     summary = {"cases": CASES, "seed0": seed0, "counts": stats, "mismatches": fails,
                "seconds": round(time.time() - t0, 1)}
     out.write_text(json.dumps(summary, indent=1))
