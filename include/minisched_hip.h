@@ -228,14 +228,17 @@ typedef struct msh_batch {
 int msh_schedule_batches_device(msh_ctx* ctx, int32_t nb, const msh_batch* batches, void* stream);
 
 /* Sequential-commit mode (one pod at a time, node state committed between placements).
- * The node table stays in registers of one workgroup: up to 368,640 nodes without a capacity,
+ * The node table stays in the registers of a workgroup: up to 368,640 nodes without a capacity,
  * 262,144 with one (larger tables: MSH_ERR_UNSUPPORTED).
  * The commit increments the selected node's assigned-pod count on the device (the
  * NodeInfo.AddPod analogue). max_pods_per_node > 0 additionally makes a node infeasible
- * once it holds that many pods (build extension); 0 = reference semantics, where the
- * placements equal msh_schedule_batch's. `commit_cb` (may be NULL) is replayed on the host
- * after the device run, in placement order, once per PLACED pod. The counts carry over from
- * call to call, so sequential launches on one ctx must not overlap: keep them on one stream. */
+ * once it holds that many pods (build extension): one workgroup walks the whole batch. 0 =
+ * reference semantics, where no commit feeds a later decision and the placements equal
+ * msh_schedule_batch's: tables up to 32,768 nodes then run as 64-pod blocks of consecutive pods,
+ * one workgroup each, every block in order (MSH_SEQ_SPLIT=serial: one workgroup), with the same
+ * placements and counts. `commit_cb` (may be NULL) is replayed on the host after the device run, in
+ * placement order, once per PLACED pod. The counts carry over from call to call; sequential launches
+ * of one ctx on different streams are ordered by the library (each waits for the ones in flight). */
 typedef void (*msh_commit_cb)(void* user, int32_t pod, int32_t node_idx, int64_t score);
 int msh_schedule_sequential(msh_ctx* ctx, int32_t p, const int8_t* pod_digit,
                             const uint8_t* pod_tol, int32_t max_pods_per_node,
