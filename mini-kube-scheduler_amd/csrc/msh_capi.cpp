@@ -623,6 +623,9 @@ int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   // key of a feasible pair is then never 0, the infeasible key) and each normalizing column's term is a
   // 24-bit signed product; otherwise Go's int64
   g.w64 = bound > (long double)(((int64_t)1 << 31) - 2) || !c24 ? 1 : 0;
+  // 64-bit totals below 2^53 in magnitude: every term and partial sum is an integer a double holds
+  // exactly, so the keys are the totals as doubles (MSH_GEN_F53=0: the uint64_t keys)
+  g.f53 = g.w64 && c->dev.gen_f53 && bound <= (long double)(((int64_t)1 << 53) - 2) ? 1 : 0;
   // NodeNumber's key without a compare (base + bit * delta on the 24-bit multiplier) when weight*100 fits
   g.nn24 = c->dev.gen_nnkey && (!g.nn_score || (long double)g.nn_weight * 100.0L < (long double)(1 << 24)) ? 1 : 0;
   return MSH_OK;
@@ -780,6 +783,7 @@ bool read_knobs(msh::DeviceInfo& d, std::string* err) {
                   knob("MSH_PAIR_PLANES", {{"auto", 0}, {"sgpr", 1}, {"lds", 2}}, &d.pair_planes, err) &&
                   knob("MSH_PAIR_NOAX", {{"auto", -1}, {"1", 1}, {"0", 0}}, &d.pair_noax, err) &&
                   knob("MSH_GEN_NNKEY", {{"auto", 1}, {"select", 0}}, &d.gen_nnkey, err) &&
+                  knob("MSH_GEN_F53", {{"1", 1}, {"0", 0}}, &d.gen_f53, err) &&
                   knob("MSH_SEQ_SPLIT", {{"auto", 1}, {"serial", 0}}, &d.seq_split, err);
   d.host_io_dma = io == 2;
   d.host_io_zc_in = io == 0;

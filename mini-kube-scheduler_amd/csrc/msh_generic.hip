@@ -5,7 +5,7 @@
 //
 // "Lanes = pods": lane l of a wave holds one pod of each of its two 64-pod blocks. The node table is
 // streamed through LDS in tiles shared by the workgroup's waves (stage 5): per node a record {code, xm}
-// (the NodeNumber code — suffix digit, or 15 — and xm = all-ones when NodeUnschedulable rejects the node
+// (the NodeNumber code — suffix digit, or 10 — and xm = all-ones when NodeUnschedulable rejects the node
 // for pods that do not tolerate the taint), the node-only sum of the columns without a normalizer, and
 // 100 x raw as an exact double per normalizing column; the waves read them as wave-uniform ds_read_b128
 // broadcasts into VGPRs. Per pair, everything is VGPR-only vector work:
@@ -19,12 +19,14 @@
 //      compare + select between the pod's two weighted values; a normalizing column is
 //      q = (100 raw - b) x r with the pod's exact reciprocal r, truncated; the
 //      columns without a normalizer are the staged node-only sum;
-//   4. selectHost: the total as an unsigned key (total + 2^31, or total ^ 2^63 with 64-bit totals; 0 =
-//      infeasible), a running v_max per lane, and per 16-node chunk the chunk where the maximum last rose;
-//      after the scan the winner's chunk is re-evaluated for the first node with that key (the first
-//      maximum in List order: strict '>' as selectHost's scan, minisched.go:311-315).
-// Totals are 32-bit (W64 = false) when the host has bounded every feasible pair's |total| below 2^31 - 1
-// from the weights, the modes and the uploaded columns' range; otherwise 64-bit (Go's wrapping int64).
+//   4. selectHost: the total as a key (total + 2^31 or total ^ 2^63 unsigned, 0 = infeasible; or the
+//      total itself as a double, NaN = infeasible), a running v_max per lane, and per 16-node chunk the
+//      chunk where the maximum last rose; after the scan the winner's chunk is re-evaluated for the first
+//      node with that key (the first maximum in List order: strict '>' as selectHost's scan,
+//      minisched.go:311-315).
+// Key type KT: 0, 32-bit totals, when the host has bounded every feasible pair's |total| below 2^31 - 1
+// from the weights, the modes and the uploaded columns' range; 2, doubles, when below 2^53 (every term
+// and partial sum is an integer a double holds exactly); else 1, 64-bit (Go's wrapping int64).
 // MODE 0: the whole batch (status, node, score per pod). Node-sharded mode (msh_generic_*): MODE 1 writes
 // each pod's extents over this shard's nodes (ext, mins negated: one all-reduce MAX merges them), MODE 2
 // takes the merged extents and writes each pod's best (total, global node index) over the shard.
@@ -80,14 +82,17 @@ __device__ __forceinline__ double nan_if(double v, uint32_t x, uint32_t nt) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | (uint32_t)b);
 }
 
-// Per-pair key of the main pass: Key = uint32_t (32-bit totals, biased by 2^31) or uint64_t (biased by
-// 2^63); 0 = infeasible.
-template <bool W64>
-using GKey = typename std::conditional<W64, uint64_t, uint32_t>::type;
+// Per-pair key of the main pass (KT): uint32_t (32-bit totals, biased by 2^31) or uint64_t (biased by
+// 2^63), 0 = infeasible; or double (the total, |total| < 2^53), NaN = infeasible (v_max_f64 skips it).
+template <int KT>
+using GKey = typename std::conditional<KT == 0, uint32_t,
+                                       typename std::conditional<KT == 1, uint64_t, double>::type>::type;
 
-template <bool W64>
-__device__ __forceinline__ GKey<W64> key_mask(GKey<W64> t, uint32_t xm, uint32_t nt) {
-  if constexpr (W64) {
+template <int KT>
+__device__ __forceinline__ GKey<KT> key_mask(GKey<KT> t, uint32_t xm, uint32_t nt) {
+  if constexpr (KT == 2) {
+    return nan_if(t, xm, nt);
+  } else if constexpr (KT == 1) {
     const uint32_t lo = bop3_andn_of_and((uint32_t)t, xm, nt), hi = bop3_andn_of_and((uint32_t)(t >> 32), xm, nt);
     return ((uint64_t)hi << 32) | lo;
   } else {
@@ -96,17 +101,20 @@ __device__ __forceinline__ GKey<W64> key_mask(GKey<W64> t, uint32_t xm, uint32_t
 }
 
 // One lane's scoring state of one 64-pod block (main pass).
-template <bool W64, int NC>
+template <int KT, int NC>
 struct GLane {
-  GKey<W64> k1, k0;  // NodeNumber's weighted normalized value on a digit match / otherwise, biased
+  GKey<KT> k1, k0;  // NodeNumber's weighted normalized value on a digit match / otherwise, biased
   double rr[NC], bb[NC];  // per normalizing column: the reciprocal and the min-max offset
 };
 
 // The contribution of normalizing column c to a pair's total: w x trunc((v - b) x r), v = 100 x raw.
-template <bool W64, bool SUB>
-__device__ __forceinline__ GKey<W64> col_term(double v, double b, double r, GKey<W64> cw) {
+template <int KT, bool SUB>
+__device__ __forceinline__ GKey<KT> col_term(double v, double b, double r, GKey<KT> cw) {
   const double q = (SUB ? v - b : v) * r;
-  if constexpr (W64) {
+  if constexpr (KT == 2) {
+    // |trunc(q) x w| is within the host's 2^53 bound on a feasible pair: exact (the others are masked)
+    return __builtin_trunc(q) * cw;
+  } else if constexpr (KT == 1) {
     // |q| < 2^40 on a feasible pair; an infeasible pair's value is clamped, converted and masked out
     const int64_t n = (int64_t)__builtin_fmin(__builtin_fmax(q, -0x1p62), 0x1p62);
     return (uint64_t)n * cw;
@@ -118,9 +126,23 @@ __device__ __forceinline__ GKey<W64> col_term(double v, double b, double r, GKey
   }
 }
 
-template <int MODE, bool W64, bool TS, int NNC, bool MMX>
+template <int MODE, int KT, bool TS, int NNC, bool MMX>
 __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
-  using Key = GKey<W64>;
+  using Key = GKey<KT>;
+  constexpr bool W64 = KT != 0;  // 8-byte keys
+  // the node-only sum of the columns without a normalizer (exact in int64 for the double keys, whose
+  // host bound keeps every term and the sum below 2^53)
+  auto node_sum = [&](int32_t i) -> Key {
+    if constexpr (KT == 2) {
+      int64_t t = 0;
+      for (int c = 0; c < a.nts; ++c) t += a.cols[(size_t)a.tcc[c] * a.col_stride + i] * a.tw[c];
+      return (double)t;
+    } else {
+      Key t = 0;
+      for (int c = 0; c < a.nts; ++c) t += (Key)a.cols[(size_t)a.tcc[c] * a.col_stride + i] * (Key)a.tw[c];
+      return t;
+    }
+  };
   constexpr int NC = NNC > 0 ? NNC : 1;
   extern __shared__ uint4 s_dyn[];
   __shared__ uint32_t s_ffs;  // the first node NodeUnschedulable passes for every pod (GEN_NONE: none)
@@ -174,11 +196,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
         const int dg = a.digit[i];
         xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
         s_cx[k] = make_uint2((dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE, xm);
-        if constexpr (TS) {  // the node-only part: weight x raw of the columns without a normalizer
-          Key ts = 0;
-          for (int c = 0; c < a.nts; ++c) ts += (Key)a.cols[(size_t)a.tcc[c] * a.col_stride + i] * (Key)a.tw[c];
-          s_ts[k] = ts;
-        }
+        if constexpr (TS) s_ts[k] = node_sum(i);  // the node-only part: weight x raw, columns without a normalizer
 #pragma unroll
         for (int c = 0; c < NC; ++c)
           if (c < nnc) s_v[(size_t)c * TN + k] = 100.0 * (double)a.cols[(size_t)a.ncc[c] * a.col_stride + i];
@@ -391,10 +409,11 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     cw[c] = 0;
     if (c >= nnc) break;
     const bool rev = a.nmode[c] == 2;
-    cw[c] = rev ? (Key)(0 - (uint64_t)a.nw[c]) : (Key)a.nw[c];
+    if constexpr (KT == 2) cw[c] = rev ? -(double)a.nw[c] : (double)a.nw[c];
+    else cw[c] = rev ? (Key)(0 - (uint64_t)a.nw[c]) : (Key)a.nw[c];
     if (rev) tot0 += (uint64_t)100 * (uint64_t)a.nw[c];
   }
-  GLane<W64, NC> L[GEN_BPW];
+  GLane<KT, NC> L[GEN_BPW];
 #pragma unroll
   for (int b = 0; b < GEN_BPW; ++b) {
     int64_t c1 = 0, c0 = 0;
@@ -404,7 +423,10 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     } else if (a.nn_score) {
       c1 = (int64_t)((uint64_t)10 * (uint64_t)a.nn_weight);  // NONE: raw x weight
     }
-    if constexpr (W64) {
+    if constexpr (KT == 2) {
+      L[b].k1 = (double)(c1 + (int64_t)tot0);
+      L[b].k0 = (double)(c0 + (int64_t)tot0);
+    } else if constexpr (KT == 1) {
       L[b].k1 = ((uint64_t)c1 + tot0) ^ 0x8000000000000000ull;
       L[b].k0 = ((uint64_t)c0 + tot0) ^ 0x8000000000000000ull;
     } else {
@@ -455,9 +477,9 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       if (c >= nnc) break;
-      t += col_term<W64, MMX>(v[c], L[b].bb[c], L[b].rr[c], cw[c]);
+      t += col_term<KT, MMX>(v[c], L[b].bb[c], L[b].rr[c], cw[c]);
     }
-    return key_mask<W64>(t, xm, ntol[b]);
+    return key_mask<KT>(t, xm, ntol[b]);
   };
 
   // ---- stages 1, 2, 4: feasibility, the total, the first maximum ----
@@ -465,7 +487,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
   int32_t cidx[GEN_BPW];
 #pragma unroll
   for (int b = 0; b < GEN_BPW; ++b) {
-    best[b] = 0;
+    best[b] = KT == 2 ? Key(-__builtin_inf()) : Key(0);  // below every feasible key
     cidx[b] = -1;
   }
   auto main_pass = [&](auto nnfast) {
@@ -483,7 +505,8 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) {
           const Key key = pair_key(b, cx.x, cx.y, ts, v, nnfast);
-          best[b] = key > best[b] ? key : best[b];
+          if constexpr (KT == 2) best[b] = vmax_f64(best[b], key);  // an infeasible (NaN) key is skipped
+          else best[b] = key > best[b] ? key : best[b];
         }
       };
       auto node = [&](int32_t k) {
@@ -553,15 +576,14 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
 #pragma unroll
   for (int b = 0; b < GEN_BPW; ++b) {
     bidx[b] = INT32_MAX;
-    if (best[b] == 0 || jj[b] >= np) continue;
+    if (best[b] == (KT == 2 ? Key(-__builtin_inf()) : Key(0)) || jj[b] >= np) continue;
     const int32_t e = min(cidx[b] + GEN_CHUNK, n);
     for (int32_t i = cidx[b]; i < e; ++i) {
       const int dg = a.digit[i];
       const uint32_t code = (dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE;
       const uint32_t xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
       Key ts = 0;
-      if constexpr (TS)
-        for (int c = 0; c < a.nts; ++c) ts += (Key)a.cols[(size_t)a.tcc[c] * a.col_stride + i] * (Key)a.tw[c];
+      if constexpr (TS) ts = node_sum(i);
       double v[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c)
@@ -609,7 +631,10 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     const bool found = ff != GEN_NONE;
     int64_t total;
     int32_t idx;
-    if (best[b] == 0) {  // every feasible total is INT64_MIN (64-bit totals only): the first feasible node
+    if constexpr (KT == 2) {  // a found pod has a finite best total
+      total = found ? (int64_t)best[b] : 0;
+      idx = bidx[b];
+    } else if (best[b] == 0) {  // every feasible total is INT64_MIN (64-bit totals only): the first feasible node
       total = INT64_MIN;
       idx = (int32_t)ff;
     } else {
@@ -674,9 +699,9 @@ int gen_slices(int64_t groups, int32_t n, const DeviceInfo& dev) {
   return sl;
 }
 
-template <int MODE, bool W64, bool TS, int NNC, bool MMX>
+template <int MODE, int KT, bool TS, int NNC, bool MMX>
 hipError_t launch_gen_k(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
-  auto k = generic_kernel<MODE, W64, TS, NNC, MMX>;
+  auto k = generic_kernel<MODE, KT, TS, NNC, MMX>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
@@ -686,25 +711,31 @@ hipError_t launch_gen_k(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
   return hipGetLastError();
 }
 
-// At most one normalizing column, 32- or 64-bit totals: {a node-only sum or not} x {no normalizing
-// column, one DEFAULT / REVERSE column, one MIN-MAX column}
-template <int MODE, bool W64>
+// At most one normalizing column, each key type: {a node-only sum or not} x {no normalizing column, one
+// DEFAULT / REVERSE column, one MIN-MAX column}
+template <int MODE, int KT>
 hipError_t launch_gen_w(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
   const bool ts = a.nts > 0;
-  if (a.nnc == 0) return ts ? launch_gen_k<MODE, W64, true, 0, false>(a, bx, lds, s)
-                            : launch_gen_k<MODE, W64, false, 0, false>(a, bx, lds, s);
+  if (a.nnc == 0) return ts ? launch_gen_k<MODE, KT, true, 0, false>(a, bx, lds, s)
+                            : launch_gen_k<MODE, KT, false, 0, false>(a, bx, lds, s);
   const bool mm = a.nmode[0] == 3;
-  if (ts) return mm ? launch_gen_k<MODE, W64, true, 1, true>(a, bx, lds, s)
-                    : launch_gen_k<MODE, W64, true, 1, false>(a, bx, lds, s);
-  return mm ? launch_gen_k<MODE, W64, false, 1, true>(a, bx, lds, s)
-            : launch_gen_k<MODE, W64, false, 1, false>(a, bx, lds, s);
+  if (ts) return mm ? launch_gen_k<MODE, KT, true, 1, true>(a, bx, lds, s)
+                    : launch_gen_k<MODE, KT, true, 1, false>(a, bx, lds, s);
+  return mm ? launch_gen_k<MODE, KT, false, 1, true>(a, bx, lds, s)
+            : launch_gen_k<MODE, KT, false, 1, false>(a, bx, lds, s);
 }
 
 template <int MODE>
 hipError_t launch_gen_mode(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
   // two or more normalizing columns: the general form (64-bit totals, a runtime column count)
-  if (a.nnc > 1) return launch_gen_k<MODE, true, true, 4, true>(a, bx, lds, s);
-  return a.w64 ? launch_gen_w<MODE, true>(a, bx, lds, s) : launch_gen_w<MODE, false>(a, bx, lds, s);
+  if (a.nnc > 1) return launch_gen_k<MODE, 1, true, 4, true>(a, bx, lds, s);
+  if (!a.w64) return launch_gen_w<MODE, 0>(a, bx, lds, s);
+  // 8-byte keys: doubles when the host bounds the totals below 2^53, else uint64_t; the extents mode
+  // computes no key (the 8-byte staging is the same), so it shares the uint64_t instances
+  if constexpr (MODE != 1) {
+    if (a.f53) return launch_gen_w<MODE, 2>(a, bx, lds, s);
+  }
+  return launch_gen_w<MODE, 1>(a, bx, lds, s);
 }
 }  // namespace
 

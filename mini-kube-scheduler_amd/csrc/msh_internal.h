@@ -57,6 +57,7 @@ struct DeviceInfo {
   // MSH_SEQ_SPLIT: without a capacity, the sequential kernel's pods in blocks of consecutive pods, one
   // workgroup each (auto, 1), or all in one workgroup (serial, 0)
   int seq_split = 1;
+  int gen_f53 = 1;    // MSH_GEN_F53: generic_kernel's double keys for 64-bit totals below 2^53 (1) or uint64_t (0)
   int gen_nnkey = 1;  // MSH_GEN_NNKEY: generic_kernel's compare-free NodeNumber key (1) or the select (0)
 };
 
@@ -170,6 +171,7 @@ struct GenericArgs {
   int32_t need_ext;        // some plugin normalizes: the extent pass runs
   int32_t w64;             // 64-bit totals (the host could not bound every feasible total within 31 bits, or a
                            // normalizing column's weight or normalized score reaches 2^23)
+  int32_t f53;             // w64 and every feasible |total| below 2^53: double keys (exact integers)
   int32_t nn24;            // NodeNumber's two weighted values differ by less than 2^24 (32-bit keys: no compare)
   int32_t nb;              // batches (mode 0: up to MULTI_MAX; sharded modes: 1)
   int64_t node_base;       // sharded modes: global index of local node 0
