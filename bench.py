@@ -68,7 +68,7 @@ PAIR_VALU_PER_WORD_LDS = 5.625
 # of a workgroup's 8 pod blocks fold X & nT into the first code compare (4.625)
 PAIR_VALU_PER_WORD_LDS_KX = 4.625
 # generic_kernel's main loop on the reference list (NodeNumber only, 32-bit keys; the ISA of
-# generic_kernel<0, false, false, 0, false>): per 16 nodes and 2 pod blocks, 32 v_bfe_u32 (the pod's one-hot
+# generic_kernel<0, 0, false, 0, false>): per 16 nodes and 2 pod blocks, 32 v_bfe_u32 (the pod's one-hot
 # code bit at the node's digit), 32 v_mad_u32_u24 (the lane's weighted key), 32 v_bitop3_b32
 # (NodeUnschedulable clears an infeasible key), 16 v_max3_u32 (the running maximum), 2 x (v_cmp_gt_u32 +
 # v_cndmask_b32) for the chunk and a v_mov_b64: 117 VALU per 32 pairs
@@ -661,7 +661,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     gctx.upload_nodes(u, nd)
     gctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
     ms = run_multi(gctx, R=5)
-    kname = "void msh::generic_kernel<0, false, false, 0, false>"
+    kname = "void msh::generic_kernel<0, 0, false, 0, false>"
     rl = valu_roofline(kname, ms, float(n) * p * G, GEN_VALU_PER_PAIR_REF, cus,
                        pmc_entry("generic_ref", kname, n, p, G),
                        "3.66 VALU per pair (generic_kernel's main loop, NodeNumber only, 32-bit keys: v_bfe_u32 and "
@@ -691,7 +691,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     ok = all(same(tuple(x[sample] for x in got(b)),
                   direct_plugins(u, nd, pp[0][sample], pp[1][sample], plugins, {0: col}))
              for b, pp in list(zip(bufs, pods))[:2])
-    kname = "void msh::generic_kernel<0, false, false, 1, false>"
+    kname = "void msh::generic_kernel<0, 0, false, 1, false>"
     entry = pmc_entry("generic_col", kname, n, p, G)
     gen["nodenumber_plus_default_column"] = {
         "kernel": kname, "plugins": "score=[NodeNumber w=1, ScoreColumn0 w=2 DefaultNormalizeScore]",
@@ -709,7 +709,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         ok = all(same(tuple(x[sample] for x in got(b)),
                       direct_plugins(u, nd, pp[0][sample], pp[1][sample], plugins, {0: wide}))
                  for b, pp in list(zip(bufs, pods))[:2])
-        gen[key] = {"kernel": f"void msh::generic_kernel<0, true, {'true' if cn == 0 else 'false'}, {0 if cn == 0 else 1}, false>",
+        gen[key] = {"kernel": f"void msh::generic_kernel<0, 2, {'true' if cn == 0 else 'false'}, {0 if cn == 0 else 1}, false>",
                     "plugins": f"score=[NodeNumber w=1, ScoreColumn0 w=1 {NORM_NAMES[cn]}] (column over the whole int32 range)",
                     "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G,
                     "evals_per_s": n * p * G / (ms * 1e-3),

@@ -1167,6 +1167,39 @@ def test_generic_nn_key_select(msh, oracle, lst, monkeypatch):
         msh.DeviceContext(0)
 
 
+@pytest.mark.parametrize("f53", ["1", "0"])
+def test_generic_f53_bounds(msh, oracle, f53, monkeypatch):
+    """64-bit totals as double keys (MSH_GEN_F53=1, the default) when the host bounds them below 2^53, else
+    uint64_t keys: a column over the whole int32 range at weight 2^21 (bound 2^52: doubles) and 2^22 (2^53:
+    uint64_t), with NodeNumber DEFAULT and a DEFAULT column beside it, on one- and multi-tile tables; and
+    the same lists on the uint64_t keys throughout (MSH_GEN_F53=0)."""
+    monkeypatch.setenv("MSH_GEN_F53", f53)
+    rng = np.random.default_rng(53)
+    lists = [[("ScoreColumn0", 1 << 21, 0), ("NodeNumber", 1, 1)],
+             [("ScoreColumn0", 1 << 22, 0), ("NodeNumber", 3, 0)],
+             [("ScoreColumn0", 7, 1), ("NodeNumber", 2, 3), ("ScoreColumn1", 1 << 20, 0)],
+             [("ScoreColumn0", 1, 2)]]
+    with msh.DeviceContext(0) as ctx:
+        for pl in lists:
+            names = [nm for nm, _, _ in pl]
+            pre = ["NodeNumber"] if "NodeNumber" in names else []
+            ps = oracle.PluginSet(filters=["NodeUnschedulable"], prescore=pre, score=names,
+                                  weights=[w for _, w, _ in pl], normalize=[m for _, _, m in pl])
+            ctx.set_plugins(ps.filters, ps.prescore, [msh.ScorePluginConfig(nm, w, msh.Normalize(m)) for nm, w, m in pl])
+            for n, p in [(700, 3000), (20_000, 2000)]:
+                u, nd, pd, pt = _rand_case(rng, n, p, p_unsched=0.3, p_tol=0.2)
+                cols = {0: rng.integers(-(1 << 31), (1 << 31) + 1, n), 1: rng.integers(-(1 << 31), (1 << 31) + 1, n),
+                        2: np.zeros(n, np.int64), 3: np.zeros(n, np.int64)}
+                ctx.upload_nodes(u, nd)
+                for k in range(2):
+                    ctx.upload_score_column(f"ScoreColumn{k}", cols[k])
+                _assert_same(ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols, threads=8),
+                             f"f53={f53} {pl} n={n}")
+    monkeypatch.setenv("MSH_GEN_F53", "2")
+    with pytest.raises(msh.MshError):
+        msh.DeviceContext(0)
+
+
 def test_generic_int64_min_totals(msh, gpu_ctx, oracle):
     """64-bit totals equal to INT64_MIN (weight 2^32 x raw -2^31): such a pair's key collides with the
     infeasible key 0, so a pod whose every feasible total is INT64_MIN takes its first feasible node
