@@ -623,9 +623,9 @@ int generic_args(msh_ctx* c, msh::GenericArgs& g) {
   // key of a feasible pair is then never 0, the infeasible key) and each normalizing column's term is a
   // 24-bit signed product; otherwise Go's int64
   g.w64 = bound > (long double)(((int64_t)1 << 31) - 2) || !c24 ? 1 : 0;
-  // 64-bit totals below 2^53 in magnitude: every term and partial sum is an integer a double holds
-  // exactly, so the keys are the totals as doubles (MSH_GEN_F53=0: the uint64_t keys)
-  g.f53 = g.w64 && c->dev.gen_f53 && bound <= (long double)(((int64_t)1 << 53) - 2) ? 1 : 0;
+  // totals below 2^53 in magnitude: every term and partial sum is an integer a double holds exactly, so
+  // the 8-byte keys (64-bit totals, or the general form) are the totals as doubles (MSH_GEN_F53=0: uint64_t)
+  g.f53 = c->dev.gen_f53 && bound <= (long double)(((int64_t)1 << 53) - 2) ? 1 : 0;
   // NodeNumber's key without a compare (base + bit * delta on the 24-bit multiplier) when weight*100 fits
   g.nn24 = c->dev.gen_nnkey && (!g.nn_score || (long double)g.nn_weight * 100.0L < (long double)(1 << 24)) ? 1 : 0;
   return MSH_OK;

@@ -727,8 +727,14 @@ hipError_t launch_gen_w(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
 
 template <int MODE>
 hipError_t launch_gen_mode(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s) {
-  // two or more normalizing columns: the general form (64-bit totals, a runtime column count)
-  if (a.nnc > 1) return launch_gen_k<MODE, 1, true, 4, true>(a, bx, lds, s);
+  // two or more normalizing columns: the general form (8-byte keys, a runtime column count): doubles when
+  // the host bounds the totals below 2^53, else uint64_t (the extents mode computes no key)
+  if (a.nnc > 1) {
+    if constexpr (MODE != 1) {
+      if (a.f53) return launch_gen_k<MODE, 2, true, 4, true>(a, bx, lds, s);
+    }
+    return launch_gen_k<MODE, 1, true, 4, true>(a, bx, lds, s);
+  }
   if (!a.w64) return launch_gen_w<MODE, 0>(a, bx, lds, s);
   // 8-byte keys: doubles when the host bounds the totals below 2^53, else uint64_t; the extents mode
   // computes no key (the 8-byte staging is the same), so it shares the uint64_t instances

@@ -171,7 +171,7 @@ struct GenericArgs {
   int32_t need_ext;        // some plugin normalizes: the extent pass runs
   int32_t w64;             // 64-bit totals (the host could not bound every feasible total within 31 bits, or a
                            // normalizing column's weight or normalized score reaches 2^23)
-  int32_t f53;             // w64 and every feasible |total| below 2^53: double keys (exact integers)
+  int32_t f53;             // every feasible |total| below 2^53: 8-byte keys as doubles (exact integers)
   int32_t nn24;            // NodeNumber's two weighted values differ by less than 2^24 (32-bit keys: no compare)
   int32_t nb;              // batches (mode 0: up to MULTI_MAX; sharded modes: 1)
   int64_t node_base;       // sharded modes: global index of local node 0

@@ -9,6 +9,7 @@ MODE
                per launch (MSH_BATCH_KERNEL=generic is set here)
   generic_col  generic_kernel on NodeNumber + ScoreColumn0 (weight 2, DefaultNormalizeScore), 32 batches
                per launch (bench.py's generic.nodenumber_plus_default_column)
+  generic_2col generic_kernel's general form: NodeNumber + a DEFAULT and a MIN-MAX column, 32 batches per launch
   generic_w64  generic_kernel's 64-bit form: NodeNumber + ScoreColumn0 over the whole int32 range (COLNORM:
                the column's normalizer), 32 batches per launch
   sequential   C5: each pod in order (seq_kernel; MSH_SEQ_SPLIT=serial: the whole batch in one workgroup)
@@ -44,6 +45,14 @@ if mode == "generic_col":
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                     [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm)),
                      msh.ScorePluginConfig(msh.SCORE_COLUMNS[0], 2, msh.Normalize(1))])
+elif mode == "generic_2col":
+    # two normalizing columns of small range: generic_kernel's general form (a runtime column count)
+    ctx.upload_score_column(msh.SCORE_COLUMNS[0], (np.arange(n, dtype=np.int64) * 7919) % 1000 - 300)
+    ctx.upload_score_column(msh.SCORE_COLUMNS[1], (np.arange(n, dtype=np.int64) * 104729) % 101)
+    ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                    [msh.ScorePluginConfig(msh.NODE_NUMBER, 1, msh.Normalize(norm)),
+                     msh.ScorePluginConfig(msh.SCORE_COLUMNS[0], 2, msh.Normalize(1)),
+                     msh.ScorePluginConfig(msh.SCORE_COLUMNS[1], 1, msh.Normalize(3))])
 elif mode == "generic_w64":
     # a column over the whole int32 range: no 32-bit bound, generic_kernel's 64-bit general form
     ctx.upload_score_column(msh.SCORE_COLUMNS[0], ((np.arange(n, dtype=np.int64) * 2654435761) % (1 << 32)) - (1 << 31))
@@ -54,7 +63,7 @@ else:
     ctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                     [msh.ScorePluginConfig(msh.NODE_NUMBER, weight, msh.Normalize(norm))])
 dev = torch.device("cuda:0")
-nb = int(os.environ.get("NB", msh._native.BATCHES_PER_LAUNCH)) if mode in ("multi", "generic", "generic_col", "generic_w64") else 1
+nb = int(os.environ.get("NB", msh._native.BATCHES_PER_LAUNCH)) if mode in ("multi", "generic", "generic_col", "generic_w64", "generic_2col") else 1
 bufs = [(torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev), torch.empty(p, dtype=torch.int32, device=dev),
          torch.empty(p, dtype=torch.int64, device=dev), torch.empty(p, dtype=torch.int32, device=dev))
         for _ in range(nb)]

@@ -1169,16 +1169,20 @@ def test_generic_nn_key_select(msh, oracle, lst, monkeypatch):
 
 @pytest.mark.parametrize("f53", ["1", "0"])
 def test_generic_f53_bounds(msh, oracle, f53, monkeypatch):
-    """64-bit totals as double keys (MSH_GEN_F53=1, the default) when the host bounds them below 2^53, else
+    """8-byte keys as doubles (MSH_GEN_F53=1, the default) when the host bounds the totals below 2^53, else
     uint64_t keys: a column over the whole int32 range at weight 2^21 (bound 2^52: doubles) and 2^22 (2^53:
-    uint64_t), with NodeNumber DEFAULT and a DEFAULT column beside it, on one- and multi-tile tables; and
-    the same lists on the uint64_t keys throughout (MSH_GEN_F53=0)."""
+    uint64_t), with NodeNumber DEFAULT and a DEFAULT column beside it; two normalizing columns (the general
+    form) below and past the bound; on one- and multi-tile tables; and the same lists on the uint64_t keys
+    throughout (MSH_GEN_F53=0)."""
     monkeypatch.setenv("MSH_GEN_F53", f53)
     rng = np.random.default_rng(53)
     lists = [[("ScoreColumn0", 1 << 21, 0), ("NodeNumber", 1, 1)],
              [("ScoreColumn0", 1 << 22, 0), ("NodeNumber", 3, 0)],
              [("ScoreColumn0", 7, 1), ("NodeNumber", 2, 3), ("ScoreColumn1", 1 << 20, 0)],
-             [("ScoreColumn0", 1, 2)]]
+             [("ScoreColumn0", 1, 2)],
+             # two normalizing columns (the general form): below and past the 2^53 bound
+             [("ScoreColumn0", 3, 1), ("ScoreColumn1", 2, 3), ("NodeNumber", 1, 2)],
+             [("ScoreColumn1", 1 << 31, 1), ("NodeNumber", 5, 0), ("ScoreColumn0", 1, 2)]]
     with msh.DeviceContext(0) as ctx:
         for pl in lists:
             names = [nm for nm, _, _ in pl]
