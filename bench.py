@@ -698,6 +698,21 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
         "lane_ops_per_eval_counter": entry["SQ_INSTS_VALU"] * 64 / (float(n) * p * G) if entry else None,
         "check": "sampled (1,500 pods of 2 batches) bit-exact vs a direct evaluation" if ok else "MISMATCH"}
+    # two normalizing columns: generic_kernel's general form (a runtime column count, double keys)
+    col1 = (np.arange(n, dtype=np.int64) * 104729) % 101
+    gctx.upload_score_column("ScoreColumn1", col1)
+    plugins = [("NodeNumber", 1, 0), ("ScoreColumn0", 2, 1), ("ScoreColumn1", 1, 3)]
+    gctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
+                     [msh.ScorePluginConfig(nm, w, msh.Normalize(m)) for nm, w, m in plugins])
+    ms = run_multi(gctx, R=3)
+    ok = all(same(tuple(x[sample] for x in got(b)),
+                  direct_plugins(u, nd, pp[0][sample], pp[1][sample], plugins, {0: col, 1: col1}))
+             for b, pp in list(zip(bufs, pods))[:2])
+    gen["two_normalizing_columns"] = {
+        "kernel": "void msh::generic_kernel<0, 2, true, 4, true>",
+        "plugins": "score=[NodeNumber w=1, ScoreColumn0 w=2 DefaultNormalizeScore, ScoreColumn1 w=1 min-max]",
+        "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
+        "check": "sampled (1,500 pods of 2 batches) bit-exact vs a direct evaluation" if ok else "MISMATCH"}
     # a column over the whole int32 range: no 32-bit bound on the totals, generic_kernel's 64-bit form
     wide = ((np.arange(n, dtype=np.int64) * 2654435761) % (1 << 32)) - (1 << 31)
     gctx.upload_score_column("ScoreColumn0", wide)
