@@ -731,7 +731,9 @@ hipError_t launch_gen_mode(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s
   // the host bounds the totals below 2^53, else uint64_t (the extents mode computes no key)
   if (a.nnc > 1) {
     if constexpr (MODE != 1) {
-      if (a.f53) return launch_gen_k<MODE, 2, true, 4, true>(a, bx, lds, s);
+      // exactly two normalizing columns (compile-time count) or up to four (a runtime count)
+      if (a.f53) return a.nnc == 2 ? launch_gen_k<MODE, 2, true, 2, true>(a, bx, lds, s)
+                                   : launch_gen_k<MODE, 2, true, 4, true>(a, bx, lds, s);
     }
     return launch_gen_k<MODE, 1, true, 4, true>(a, bx, lds, s);
   }
