@@ -730,6 +730,8 @@ hipError_t launch_gen_mode(GenericArgs& a, int32_t bx, size_t lds, hipStream_t s
   // two or more normalizing columns: the general form (8-byte keys, a runtime column count): doubles when
   // the host bounds the totals below 2^53, else uint64_t (the extents mode computes no key)
   if (a.nnc > 1) {
+    // exactly two normalizing columns under the 32-bit bound: 32-bit keys, a compile-time count
+    if (a.nnc == 2 && !a.w64) return launch_gen_k<MODE, 0, true, 2, true>(a, bx, lds, s);
     if constexpr (MODE != 1) {
       // exactly two normalizing columns (compile-time count) or up to four (a runtime count)
       if (a.f53) return a.nnc == 2 ? launch_gen_k<MODE, 2, true, 2, true>(a, bx, lds, s)
@@ -758,8 +760,8 @@ hipError_t launch_generic(GenericArgs& a, int mode, const DeviceInfo& dev, hipSt
     groups += (a.d[b].n_pods + GEN_BPW * WAVE - 1) / (GEN_BPW * WAVE);
   }
   if (maxp == 0) return hipSuccess;
-  const bool general = a.nnc > 1;  // launch_gen_mode's general form
-  const size_t key = (general || a.w64) ? 8 : 4;
+  const bool general = a.nnc > 1;  // launch_gen_mode's forms for two or more normalizing columns
+  const size_t key = (a.w64 || (general && a.nnc > 2)) ? 8 : 4;  // launch_gen_mode's key type
   const int nnc = general ? a.nnc : std::min(a.nnc, 1);
   // bytes per staged node: the record, the node-only sum (the general form always stages it), the
   // normalizing columns
