@@ -709,7 +709,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
                   direct_plugins(u, nd, pp[0][sample], pp[1][sample], plugins, {0: col, 1: col1}))
              for b, pp in list(zip(bufs, pods))[:2])
     gen["two_normalizing_columns"] = {
-        "kernel": "void msh::generic_kernel<0, 2, true, 2, true>",
+        "kernel": "void msh::generic_kernel<0, 0, true, 2, true>",
         "plugins": "score=[NodeNumber w=1, ScoreColumn0 w=2 DefaultNormalizeScore, ScoreColumn1 w=1 min-max]",
         "kernel_ms": ms, "batches_per_launch": G, "ms_per_batch": ms / G, "evals_per_s": n * p * G / (ms * 1e-3),
         "check": "sampled (1,500 pods of 2 batches) bit-exact vs a direct evaluation" if ok else "MISMATCH"}
