@@ -232,6 +232,15 @@ def main():
         sharded = D.NodeShardedScheduler(ctx, unsched, node_digit, world, rank)
         node_base = sharded.shard.lo
         batches = [tuple(synth._make_pods_fast(p_total, synth.SEED)[1:])]
+        if world > 1 and not rehearse:
+            # the library's own RCCL communicator (msh_comm_*): rank 0 makes the id and the process group
+            # only ships its 128 bytes (a Go scheduler would use its own channel); every step then merges
+            # inside msh_schedule_nodeshard_device
+            idt = torch.zeros(msh._native.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+            if rank == 0:
+                idt.copy_(torch.tensor(list(msh.DeviceContext.comm_unique_id()), dtype=torch.uint8))
+            dist.broadcast(idt, 0)
+            ctx.comm_init(bytes(idt.cpu().tolist()), world, rank)
     else:
         ctx.upload_nodes(unsched, node_digit)
         node_base = 0
@@ -279,7 +288,13 @@ def main():
             elif mode == "sequential":
                 ctx.schedule_sequential_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), 0, b["idx"].data_ptr(),
                                                b["score"].data_ptr(), b["status"].data_ptr(), sh)
-            else:  # per-shard keys, RCCL all-reduce(MAX) on the same stream, then decode
+            elif not rehearse:  # per-shard keys, RCCL all-reduce(MAX) and decode, all inside the library
+                rc = fast.schedule_nodeshard_device(handle, p, b["pd"].data_ptr(), b["pt"].data_ptr(), node_base,
+                                                    b["idx"].data_ptr(), b["score"].data_ptr(), b["status"].data_ptr(),
+                                                    sh or None)
+                if rc:
+                    ctx._check(rc)
+            else:  # rehearsal (every rank on one GPU: no RCCL communicator): the keys merged over gloo
                 ctx.shard_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), node_base, b["keys"].data_ptr(), sh)
                 D.merge_shard_keys_(b["keys"][:klen], stream=stream)
                 ctx.decode_keys_device(p, b["pd"].data_ptr(), b["pt"].data_ptr(), b["keys"].data_ptr(),
@@ -390,7 +405,8 @@ def main():
         elif mode == "sequential":
             wl = f"C5 sequential-commit: {n_total} nodes x {p} pods per GPU, one pod at a time"
         else:
-            wl = f"C4 node-sharded: {n_total} nodes over {world} GPU x {p_total} pods, RCCL allreduce(MAX) merge"
+            wl = (f"C4 node-sharded: {n_total} nodes over {world} GPU x {p_total} pods, msh_schedule_nodeshard_device "
+                  "(shard keys, RCCL allreduce(MAX) on the library's communicator, decode)")
         line = {
             "metric": METRIC,
             "value": value,
@@ -596,14 +612,8 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     def same(a, b):
         return all((x == y).all() for x, y in zip(a, b))
 
-    def new_ctx(kernel=None, env=None):
-        env = dict(env or {}, **({"MSH_BATCH_KERNEL": kernel} if kernel else {}))
-        os.environ.update(env)  # read once by msh_create
-        try:
-            c = msh.DeviceContext(dev.index or 0)
-        finally:
-            for k in env:
-                os.environ.pop(k, None)
+    def new_ctx(options=None):
+        c = msh.DeviceContext(dev.index or 0, options)  # msh_options overrides (msh_create_ex), A/B only
         c.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER],
                       [msh.ScorePluginConfig(msh.NODE_NUMBER, HEADLINE_WEIGHT, msh.Normalize(HEADLINE_NORM))])
         return c
@@ -657,7 +667,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
 
     # ---- generic_kernel: an explicit int64 score per (pod, node) pair (north_star's five stages) ----
     gen = {}
-    gctx = new_ctx("generic")  # every plugin list on generic_kernel (the reference list included)
+    gctx = new_ctx({"batch_kernel": "generic"})  # every plugin list on generic_kernel (the reference list included)
     gctx.upload_nodes(u, nd)
     gctx.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
     ms = run_multi(gctx, R=5)
@@ -856,7 +866,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         return ms, ok
 
     for key, c, R, serial in (("c5_sequential", ctx, 20, False),
-                              ("c5_sequential_serial", new_ctx(env={"MSH_SEQ_SPLIT": "serial"}), 3, True)):
+                              ("c5_sequential_serial", new_ctx({"seq_split": "serial"}), 3, True)):
         if serial:
             c.upload_nodes(u, nd)
         ms, ok = c5(c, R)

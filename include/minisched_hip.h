@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSH_ABI_VERSION 7
+#define MSH_ABI_VERSION 8
 
 /* ---- error codes (return values) ---- */
 typedef enum msh_err {
@@ -112,12 +112,28 @@ void msh_host_free(void* ptr);
 
 /* Create/destroy a context on `device`. Default plugin set = the reference's
  * (initialize.go:80-123): filter=[NodeUnschedulable], prescore=[NodeNumber],
- * score=[NodeNumber] weight 1, normalize NONE. msh_create reads the library's test / A-B switches
- * (MSH_* environment variables) once; a value outside a switch's set is MSH_ERR_INVALID. msh_destroy
- * first waits for the launches this ctx queued with the *_device entry points (they read the ctx's
- * tables), not for the rest of the device. */
+ * score=[NodeNumber] weight 1, normalize NONE. msh_create picks every kernel automatically; the
+ * library reads no environment variable. msh_destroy first waits for the launches this ctx queued
+ * with the *_device entry points (they read the ctx's tables), not for the rest of the device. */
 int msh_create(int device, msh_ctx** out_ctx);
 void msh_destroy(msh_ctx* ctx);
+
+/* Kernel-selection overrides (ABI v8), for parity tests and A/B measurement only: a scheduler calls
+ * msh_create. Every field's 0 is the automatic choice, so a zeroed struct (with struct_size set) is
+ * msh_create. A value outside a field's set is MSH_ERR_INVALID (message in msh_last_error(NULL)).
+ * Results never depend on the options; only which kernel instance computes them does. */
+typedef struct msh_options {
+  int32_t struct_size;  /* sizeof(msh_options) */
+  int32_t batch_kernel; /* 0 auto | 1 generic_kernel (explicit int64 score per pair) for every plugin list */
+  int32_t pair_planes;  /* 0 auto | 1 node planes by scalar loads | 2 staged in LDS (tables that fit) */
+  int32_t pair_noax;    /* 0 auto | 1 LDS form: group 0 first, settled reductions dropped | 2 group 0 last */
+  int32_t pair_slices;  /* 0 auto | 1, 2, 4 slice waves per 64-pod block (and generic_kernel pod group) */
+  int32_t seq_waves;    /* 0 auto | 1, 4, 15, 16 scanning waves of the sequential kernel (raised when too few) */
+  int32_t seq_split;    /* 0 auto (no capacity: 64-pod blocks) | 1 one workgroup walks the whole batch */
+  int32_t gen_keys;     /* 0 auto (64-bit totals below 2^53 as double keys) | 1 uint64 keys */
+  int32_t gen_nnkey;    /* 0 auto (compare-free NodeNumber key) | 1 compare + select */
+} msh_options;
+int msh_create_ex(int device, const msh_options* opts, msh_ctx** out_ctx);
 
 /* Message for the last failing call on this ctx ("" if none). Valid until the next call. With a
  * NULL ctx: the message of the last failed msh_create on the calling thread. */
@@ -235,8 +251,10 @@ int msh_schedule_batches_device(msh_ctx* ctx, int32_t nb, const msh_batch* batch
  * once it holds that many pods (build extension): one workgroup walks the whole batch. 0 =
  * reference semantics, where no commit feeds a later decision and the placements equal
  * msh_schedule_batch's: tables up to 32,768 nodes then run as 64-pod blocks of consecutive pods,
- * one workgroup each, every block in order (MSH_SEQ_SPLIT=serial: one workgroup), with the same
- * placements and counts. `commit_cb` (may be NULL) is replayed on the host after the device run, in
+ * one workgroup each. The blocks run CONCURRENTLY and only the pods within one block are ordered: a
+ * no-capacity shortcut, exact because the counts the blocks add are the same in any order
+ * (msh_options.seq_split = 1 walks the whole batch in one workgroup, in order, as a capacity does).
+ * `commit_cb` (may be NULL) is replayed on the host after the device run, in
  * placement order, once per PLACED pod. The counts carry over from call to call; sequential launches
  * of one ctx on different streams are ordered by the library (each waits for the ones in flight). */
 typedef void (*msh_commit_cb)(void* user, int32_t pod, int32_t node_idx, int64_t score);
@@ -302,6 +320,55 @@ int msh_generic_candidates_device(msh_ctx* ctx, int32_t p, const int64_t* d_loca
 int msh_generic_decode_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit, const int64_t* d_merged_total,
                               const int32_t* d_merged_idx, int32_t* d_out_idx, int64_t* d_out_score,
                               int32_t* d_out_status, void* stream);
+
+/* ---- node-sharded scheduling with the merge inside the library (ABI v8) ----
+ * The entry points above leave the cross-shard merge to the caller. These own it, in the two shapes a
+ * scheduler process takes; both give exactly msh_schedule_batch over the whole List-order table
+ * (selectHost's first maximum, minisched.go:304-325, across shards), for every plugin list.
+ *
+ * (1) One process per GPU: an RCCL communicator inside the ctx (librccl.so.1, loaded on the first
+ *     msh_comm_* call). Rank 0 makes an id with msh_comm_unique_id; the caller ships its
+ *     MSH_COMM_ID_BYTES bytes to every rank over any channel (a Go scheduler: its own RPC or a file);
+ *     every rank then calls msh_comm_init (collective: it returns once all `world` ranks have joined).
+ *     msh_schedule_nodeshard_device runs, on `stream`: the shard kernel over this ctx's slice, the
+ *     all-reduce(s) over xGMI (ncclAllReduce on the same stream), and the decode; every rank ends with
+ *     every pod's decision. The reference plugins take one all-reduce(MAX) of 8 B per pod; a list with
+ *     score columns or a normalizer takes the generic form's three (extents MAX, totals MAX, indices
+ *     MIN). All ranks must make the same sequence of calls with the same p. A ctx without a
+ *     communicator runs the same path as a world of one. node_base = the global List index of this
+ *     ctx's first node. The ctx's merge buffers are shared by its node-sharded launches: a launch on
+ *     another stream first waits for the previous one. */
+#define MSH_COMM_ID_BYTES 128
+int msh_comm_unique_id(uint8_t* out_id); /* out_id: MSH_COMM_ID_BYTES bytes (ncclGetUniqueId) */
+int msh_comm_init(msh_ctx* ctx, const uint8_t* id, int32_t world, int32_t rank);
+/* world / rank of the ctx's communicator (world 0, rank 0 when msh_comm_init has not been called). */
+int msh_comm_info(const msh_ctx* ctx, int32_t* out_world, int32_t* out_rank);
+int msh_schedule_nodeshard_device(msh_ctx* ctx, int32_t p, const int8_t* d_pod_digit, const uint8_t* d_pod_tol,
+                                  int64_t node_base, int32_t* d_out_idx, int64_t* d_out_score,
+                                  int32_t* d_out_status, void* stream);
+/* The same from host buffers (the cgo form), synchronous: the pod columns go to the device and the
+ * decisions come back as in msh_schedule_batch. */
+int msh_schedule_nodeshard(msh_ctx* ctx, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                           int64_t node_base, int32_t* out_idx, int64_t* out_score, int32_t* out_status);
+
+/* (2) One process driving several devices (the reference's single scheduling loop, minisched.go:28-30,
+ *     with its node table split over the node's GPUs): a group of shard ctxs, shards[k] holding the k-th
+ *     contiguous slice of the List order (node_base = the node counts of shards[0..k) at call time).
+ *     The ctxs stay owned by the caller (destroy the group first) and may sit on any devices, the same
+ *     one included; shards on different devices need peer access to shards[0]'s device (xGMI; else
+ *     MSH_ERR_UNSUPPORTED at msh_group_create). Every shard must hold the same plugin lists (checked per
+ *     call: MSH_ERR_STATE). msh_group_schedule_batch: the pod columns are copied to every shard device,
+ *     each shard runs its kernel on its own stream, and the merge runs on shards[0]'s device as one
+ *     kernel that reads every shard's per-pod result over xGMI (peer loads) and decodes; a list with
+ *     normalizers first merges the per-pod extents the same way and every shard reads them back. Host
+ *     buffers, synchronous. Up to MSH_GROUP_MAX_SHARDS shards. */
+#define MSH_GROUP_MAX_SHARDS 16
+typedef struct msh_group msh_group;
+int msh_group_create(msh_ctx* const* shards, int32_t n, msh_group** out_group);
+void msh_group_destroy(msh_group* group);
+const char* msh_group_last_error(const msh_group* group); /* NULL group: the last failed msh_group_create */
+int msh_group_schedule_batch(msh_group* group, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol,
+                             int32_t* out_idx, int64_t* out_score, int32_t* out_status);
 
 /* ---- kernel timing (measurement hook) ----
  * msh_timing_begin arms up to max_launches (1..4096) event pairs: each following hot-kernel launch of

@@ -11,7 +11,7 @@ from . import _native
 from ._native import MshError, device_count
 from .framework import (MAX_NODE_SCORE, NODE_NUMBER, NODE_UNSCHEDULABLE, SCORE_COLUMNS, Code, NodeScore, Normalize,
                         Outcome, ScheduleResult)
-from .scheduler import DeviceContext, Scheduler, ScorePluginConfig, pinned_empty
+from .scheduler import DeviceContext, DeviceGroup, Scheduler, ScorePluginConfig, pinned_empty
 from .snapshot import NodeTable, PodTable, pack_nodes, pack_pods
 from .queue import (ActionType, ClusterEvent, PodBatch, SchedulingQueue, calculate_backoff_duration,
                     events_to_register)
@@ -22,7 +22,7 @@ from .resultstore import ResultStore
 
 __all__ = [
     "MAX_NODE_SCORE", "NODE_NUMBER", "NODE_UNSCHEDULABLE", "Code", "NodeScore", "Normalize", "Outcome",
-    "ScheduleResult", "DeviceContext", "Scheduler", "ScorePluginConfig", "pinned_empty", "NodeTable", "PodTable",
+    "ScheduleResult", "DeviceContext", "DeviceGroup", "Scheduler", "ScorePluginConfig", "pinned_empty", "NodeTable", "PodTable",
     "pack_nodes", "pack_pods", "MshError", "device_count", "_native",
     "ActionType", "ClusterEvent", "PodBatch", "SchedulingQueue", "calculate_backoff_duration",
     "events_to_register", "NodeCache", "PermitBinder", "CycleReport", "SchedulingLoop",

@@ -49,7 +49,8 @@ MSH_NORMALIZE_MINMAX = 3
 
 # Every symbol include/minisched_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = (
-    "msh_abi_version", "msh_device_count", "msh_host_alloc", "msh_host_free", "msh_create", "msh_destroy", "msh_last_error",
+    "msh_abi_version", "msh_device_count", "msh_host_alloc", "msh_host_free", "msh_create", "msh_create_ex",
+    "msh_destroy", "msh_last_error",
     "msh_set_plugins", "msh_set_plugins_ex", "msh_upload_nodes", "msh_upload_score_column", "msh_num_nodes",
     "msh_patch_nodes", "msh_export_results",
     "msh_schedule_batch", "msh_schedule_batch_async", "msh_wait", "msh_schedule_batch_device",
@@ -58,6 +59,8 @@ EXPORTED = (
     "msh_shard_keys_len", "msh_shard_keys_device", "msh_decode_keys_device", "msh_keys_slot1_is_any",
     "msh_generic_ext_len", "msh_generic_extents_device", "msh_generic_best_device",
     "msh_generic_candidates_device", "msh_generic_decode_device",
+    "msh_comm_unique_id", "msh_comm_init", "msh_comm_info", "msh_schedule_nodeshard_device", "msh_schedule_nodeshard",
+    "msh_group_create", "msh_group_destroy", "msh_group_last_error", "msh_group_schedule_batch",
     "msh_timing_begin", "msh_timing_end",
     "msh_pack_nodes", "msh_pack_pods", "msh_toleration_tolerates_unschedulable",
 )
@@ -80,6 +83,43 @@ class Batch(C.Structure):
                 ("out_idx", C.c_void_p), ("out_score", C.c_void_p), ("out_status", C.c_void_p)]
 
 
+class Options(C.Structure):
+    """msh_options (ABI v8): kernel-selection overrides for msh_create_ex, 0 = automatic."""
+    _fields_ = [("struct_size", C.c_int32), ("batch_kernel", C.c_int32), ("pair_planes", C.c_int32),
+                ("pair_noax", C.c_int32), ("pair_slices", C.c_int32), ("seq_waves", C.c_int32),
+                ("seq_split", C.c_int32), ("gen_keys", C.c_int32), ("gen_nnkey", C.c_int32)]
+
+
+# Named values of the msh_options fields (an int passes through unchanged, for the library to check).
+OPTION_NAMES = {
+    "batch_kernel": {"auto": 0, "pair": 0, "generic": 1},
+    "pair_planes": {"auto": 0, "sgpr": 1, "lds": 2},
+    "pair_noax": {"auto": 0, "noax": 1, "axlast": 2},
+    "pair_slices": {"auto": 0},
+    "seq_waves": {"auto": 0},
+    "seq_split": {"auto": 0, "serial": 1},
+    "gen_keys": {"auto": 0, "f53": 0, "u64": 1},
+    "gen_nnkey": {"auto": 0, "select": 1},
+}
+
+
+def make_options(opts: dict | None) -> "Options | None":
+    """msh_options from {field: value}: a name of OPTION_NAMES[field], or an int (digit strings too)."""
+    if not opts:
+        return None
+    o = Options()
+    o.struct_size = C.sizeof(Options)
+    for k, v in opts.items():
+        if k not in OPTION_NAMES:
+            raise ValueError(f"unknown msh_options field {k!r}")
+        if isinstance(v, str):
+            v = OPTION_NAMES[k][v] if v in OPTION_NAMES[k] else int(v)
+        setattr(o, k, int(v))
+    return o
+
+
+COMM_ID_BYTES = 128  # MSH_COMM_ID_BYTES
+GROUP_MAX_SHARDS = 16  # MSH_GROUP_MAX_SHARDS
 BATCHES_PER_LAUNCH = 32  # MSH_BATCHES_PER_LAUNCH
 ASYNC_DEPTH = 4  # MSH_ASYNC_DEPTH
 
@@ -95,6 +135,7 @@ _SIGS = {
     "msh_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(_P)]),
     "msh_host_free": (None, [_P]),
     "msh_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "msh_create_ex": (C.c_int, [C.c_int, C.POINTER(Options), C.POINTER(_P)]),
     "msh_destroy": (None, [_P]),
     "msh_last_error": (C.c_char_p, [_P]),
     "msh_set_plugins": (C.c_int, [_P, _P, _I32, _P, _P, _I32]),
@@ -124,6 +165,15 @@ _SIGS = {
     "msh_generic_best_device": (C.c_int, [_P, _I32, _P, _P, _P, _I64, _P, _P, _P]),
     "msh_generic_candidates_device": (C.c_int, [_P, _I32, _P, _P, _P, _P]),
     "msh_generic_decode_device": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "msh_comm_unique_id": (C.c_int, [_P]),
+    "msh_comm_init": (C.c_int, [_P, _P, _I32, _I32]),
+    "msh_comm_info": (C.c_int, [_P, C.POINTER(_I32), C.POINTER(_I32)]),
+    "msh_schedule_nodeshard_device": (C.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _P, _P]),
+    "msh_schedule_nodeshard": (C.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _P]),
+    "msh_group_create": (C.c_int, [C.POINTER(_P), _I32, C.POINTER(_P)]),
+    "msh_group_destroy": (None, [_P]),
+    "msh_group_last_error": (C.c_char_p, [_P]),
+    "msh_group_schedule_batch": (C.c_int, [_P, _I32, _P, _P, _P, _P, _P]),
     "msh_pack_nodes": (C.c_int, [_I32, C.c_char_p, _P, _P, _P, _P, _P]),
     "msh_pack_pods": (C.c_int, [_I32, C.c_char_p, _P, C.POINTER(Toleration), _P, _P, _P]),
     "msh_toleration_tolerates_unschedulable": (C.c_int, [C.POINTER(Toleration)]),

@@ -8,10 +8,14 @@ snapshot to the GPU box.
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import shutil
+import socket
 import subprocess
 import sysconfig
+import time
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -29,9 +33,11 @@ SOURCES = [
     ("msh_seq.hip", "hipcc", ["-x", "hip"]),
     ("msh_prep.hip", "hipcc", ["-x", "hip"]),
     ("msh_capi.cpp", "hipcc", []),
+    ("msh_shard.cpp", "hipcc", []),
     ("msh_pack.cpp", "g++", []),
 ]
-HEADERS = [CSRC / "msh_internal.h", CSRC / "msh_device.h", CSRC / "msh_pool.h", INCLUDE / "minisched_hip.h"]
+HEADERS = [CSRC / "msh_internal.h", CSRC / "msh_device.h", CSRC / "msh_pool.h", CSRC / "msh_ctx.h",
+           INCLUDE / "minisched_hip.h"]
 
 
 def _hipcc() -> str:
@@ -50,15 +56,54 @@ def _stale(target: Path, deps: list[Path]) -> bool:
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the kernels + C-ABI for gfx950, link libminisched_hip.so, and the CPython
-    fast-call module on top of it."""
-    _build_lib(force, verbose)
+    fast-call module on top of it. A build that compiled the library records its provenance
+    (PROVENANCE: this machine's hipcc, the sources' digest, the seconds it took)."""
+    t0 = time.time()
+    compiled = _build_lib(force, verbose)
     build_fast(force, verbose)
+    if compiled:
+        _write_provenance(time.time() - t0, force)
     return LIB
 
 
-def _build_lib(force: bool, verbose: bool) -> None:
+# Where the last build that compiled the library wrote what it built from (build/ never travels to the
+# GPU box: it is in .gpurunignore, so a provenance file there was written by a build on that machine).
+PROVENANCE = OBJ / "provenance.json"
+
+
+def sources_digest() -> str:
+    """sha256 over the library's sources and headers (name + bytes, sorted by name)."""
+    h = hashlib.sha256()
+    for f in sorted({CSRC / s for s, _, _ in SOURCES} | set(HEADERS) | {FAST_SRC}, key=lambda x: x.name):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def hipcc_version() -> str:
+    out = subprocess.run([_hipcc(), "--version"], capture_output=True, text=True).stdout
+    keep = [ln.strip() for ln in out.splitlines() if ln.startswith(("HIP version", "AMD clang version"))]
+    return "; ".join(keep) or out.strip().splitlines()[0]
+
+
+def _write_provenance(seconds: float, forced: bool) -> None:
+    rec = {"library": str(LIB), "built_at": time.strftime("%Y-%m-%dT%H:%M:%S%z"), "host": socket.gethostname(),
+           "hipcc": hipcc_version(), "offload_arch": ARCH, "seconds": round(seconds, 1), "forced": forced,
+           "sources_sha256": sources_digest(), "lib_sha256": hashlib.sha256(LIB.read_bytes()).hexdigest()}
+    OBJ.mkdir(exist_ok=True)
+    PROVENANCE.write_text(json.dumps(rec, indent=1) + "\n")
+
+
+def load_provenance() -> dict | None:
+    try:
+        return json.loads(PROVENANCE.read_text())
+    except (OSError, ValueError):
+        return None
+
+
+def _build_lib(force: bool, verbose: bool) -> bool:
     if not force and not _stale(LIB, [CSRC / src for src, _, _ in SOURCES] + HEADERS):
-        return  # up to date (objects need not be present, e.g. on the GPU box)
+        return False  # up to date (objects need not be present, e.g. on the GPU box)
     OBJ.mkdir(exist_ok=True)
     objs, jobs = [], []
     for src, cc, extra in SOURCES:
@@ -80,10 +125,11 @@ def _build_lib(force: bool, verbose: bool) -> None:
     if failed:
         raise RuntimeError(f"compile failed: {', '.join(failed)}")
     if force or _stale(LIB, objs):
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-ldl", "-o", str(LIB)]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+    return True
 
 
 FAST_SRC = CSRC / "msh_pyfast.c"

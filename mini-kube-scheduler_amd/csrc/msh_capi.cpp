@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../../include/minisched_hip.h"
+#include "msh_ctx.h"
 #include "msh_internal.h"
 #include "msh_pool.h"
 
@@ -76,84 +77,7 @@ void par_copy(const CopyJob* jobs, int n_jobs) {
 
 }  // namespace
 
-// One version of the node-side device tables (List order, padded to cap nodes).
-struct NodeTable {
-  size_t cap = 0;
-  uint8_t* d_unsched = nullptr;  // the uploaded columns (read by generic_kernel and the export as they are)
-  int8_t* d_digit = nullptr;
-  uint32_t* d_planes = nullptr;  // bit-sliced node table (msh_internal.h PLANE_* layout): pair / seq kernels
-  // score-column plugins (generic pipeline): GEN_COLS x cap int64, column k valid when col_ok[k], with the
-  // range of its values (host side: the generic launch bounds the totals from it)
-  int64_t* d_cols = nullptr;
-  bool col_ok[msh::GEN_COLS] = {};
-  int64_t col_lo[msh::GEN_COLS] = {}, col_hi[msh::GEN_COLS] = {};
-  // launches that read this version: one event per caller stream, re-recorded after each launch
-  std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
-};
-
-struct msh_ctx {
-  int device = 0;
-  std::string err;
-  msh::DeviceInfo dev;
-  hipStream_t stream = nullptr;  // used by the synchronous host-buffer entry points
-
-  // plugin descriptor
-  std::vector<int32_t> filter_ids, prescore_ids, score_ids, normalize;
-  std::vector<int64_t> weights;
-  PluginParams pp{1, 1, 1, 0, 1};
-
-  // node table: two versions. Launches read tab[cur]; a rewrite (upload, patch, plugin change,
-  // score column) builds the other version on prep_stream and then publishes it, so it never waits
-  // for launches in flight on the version they read (only for those of two rewrites ago, on the
-  // version it overwrites, long done in practice).
-  bool have_nodes = false;
-  int32_t n_nodes = 0, n_pad = 0;
-  NodeTable tab[2];
-  int cur = 0;
-  // sequential-mode state (not versioned: carried from call to call): pods committed per node, and
-  // the sequential launches in flight that update it
-  // (counts_replicas arrays of counts_cap: msh::SEQ_COUNT_REPLICAS for tables pod blocks can take, else
-  // 1; counts_dirty: replicas 1.. may hold counts, folded into replica 0 by the next one-workgroup
-  // launch or count read)
-  int32_t* d_counts = nullptr;
-  size_t counts_cap = 0;
-  int32_t counts_replicas = 1;
-  bool counts_dirty = false;
-  std::vector<std::pair<hipStream_t, hipEvent_t>> seq_inflight;
-  // the rewrites' own stream, created with the device's highest priority: HIP gives each priority
-  // its own hardware queues, so a rewrite never queues behind other streams' kernels that happen to
-  // share a hardware queue with it (GPU_MAX_HW_QUEUES per priority)
-  hipStream_t prep_stream = nullptr;
-  bool generic = false;  // the score list names a score-column plugin
-
-  // host-path buffers
-  size_t pod_cap = 0;
-  int8_t* d_pd = nullptr;         // device scratch for the pod columns
-  uint8_t* d_pt = nullptr;
-  int32_t* d_oi = nullptr;        // device scratch for the outputs (MSH_HOST_IO=dma only)
-  int64_t* d_os = nullptr;
-  int32_t* d_ost = nullptr;
-  size_t stage_cap = 0;
-  unsigned char* h_stage = nullptr;  // page-locked: digit p | tol p | idx 4p | score 8p | status 4p
-  hipEvent_t done_ev = nullptr;  // MSH_HOST_SYNC=poll
-  // msh_schedule_batch_async: a ring of MSH_ASYNC_DEPTH events on the ctx's stream; ticket t's event
-  // is async_ev[t % MSH_ASYNC_DEPTH]; every ticket <= async_done has completed
-  hipEvent_t async_ev[MSH_ASYNC_DEPTH] = {};
-  uint64_t async_issued = 0, async_done = 0;
-  size_t patch_cap = 0;
-  unsigned long long* d_patch = nullptr;  // msh_patch_nodes entries
-  std::vector<unsigned long long> h_patch;
-  // page-locked staging of node columns / patch entries (uploads copy from it, never from pageable
-  // memory: a pageable copy may wait for more than this ctx's stream)
-  size_t nstage_cap = 0;
-  unsigned char* h_nstage = nullptr;
-  // msh_timing_begin / _end: kernel start / stop event pairs for the next hot-kernel launches
-  bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
-  size_t t_next = 0;
-};
-
-namespace {
+namespace msh::capi {
 
 int fail(msh_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -164,12 +88,6 @@ int hip_fail(msh_ctx* c, hipError_t e, const char* what) {
   std::string m = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
   return fail(c, MSH_ERR_HIP, m);
 }
-
-#define MSH_HIP(ctx, call)                               \
-  do {                                                   \
-    hipError_t e_ = (call);                              \
-    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
-  } while (0)
 
 NodeTable& cur_table(msh_ctx* c) { return c->tab[c->cur]; }
 
@@ -194,35 +112,6 @@ void wait_events(const std::vector<std::pair<hipStream_t, hipEvent_t>>& evs) {
 void destroy_events(std::vector<std::pair<hipStream_t, hipEvent_t>>& evs) {
   for (auto& e : evs) (void)hipEventDestroy(e.second);
   evs.clear();
-}
-
-void free_pods(msh_ctx* c) {
-  (void)hipFree(c->d_pd);
-  (void)hipFree(c->d_pt);
-  (void)hipFree(c->d_oi);
-  (void)hipFree(c->d_os);
-  (void)hipFree(c->d_ost);
-  c->d_pd = nullptr;
-  c->d_pt = nullptr;
-  c->d_oi = nullptr;
-  c->d_os = nullptr;
-  c->d_ost = nullptr;
-  c->pod_cap = 0;
-}
-
-int ensure_pod_scratch(msh_ctx* c, int32_t p) {
-  if ((size_t)p <= c->pod_cap) return MSH_OK;
-  free_pods(c);
-  const size_t cap = std::max<size_t>((size_t)p, 1024);
-  MSH_HIP(c, hipMalloc(&c->d_pd, cap));
-  MSH_HIP(c, hipMalloc(&c->d_pt, cap));
-  if (c->dev.host_io_dma) {
-    MSH_HIP(c, hipMalloc(&c->d_oi, cap * sizeof(int32_t)));
-    MSH_HIP(c, hipMalloc(&c->d_os, cap * sizeof(int64_t)));
-    MSH_HIP(c, hipMalloc(&c->d_ost, cap * sizeof(int32_t)));
-  }
-  c->pod_cap = cap;
-  return MSH_OK;
 }
 
 // layout of the page-locked stage for p pods (16-byte aligned sections)
@@ -323,7 +212,7 @@ int record_on(msh_ctx* c, std::vector<std::pair<hipStream_t, hipEvent_t>>& evs, 
 
 // After a launch on caller stream s that reads the current table version (seq: and updates the
 // sequential-mode counts).
-int track_launch(msh_ctx* c, hipStream_t s, bool seq = false) {
+int track_launch(msh_ctx* c, hipStream_t s, bool seq) {
   int rc = record_on(c, cur_table(c).readers, s);
   if (rc == MSH_OK && seq) rc = record_on(c, c->seq_inflight, s);
   return rc;
@@ -505,31 +394,24 @@ int rewrite(msh_ctx* c, const Rewrite& w) {
   return MSH_OK;
 }
 
-// One hot-kernel launch under msh_timing_begin: arms the next event pair for the launcher on this
-// thread; a launcher that launched nothing leaves it unused.
-struct TimedLaunch {
-  msh_ctx* c;
-  bool armed = false;
-  explicit TimedLaunch(msh_ctx* ctx) : c(ctx) {
-    if (c->timing && c->t_next < c->tev.size()) {
-      msh::set_launch_events(c->tev[c->t_next].first, c->tev[c->t_next].second);
-      armed = true;
-    }
+TimedLaunch::TimedLaunch(msh_ctx* ctx) : c(ctx) {
+  if (c->timing && c->t_next < c->tev.size()) {
+    msh::set_launch_events(c->tev[c->t_next].first, c->tev[c->t_next].second);
+    armed = true;
   }
-  ~TimedLaunch() {
-    if (!armed) return;
-    if (msh::launch_events_pending()) msh::set_launch_events(nullptr, nullptr);
-    else ++c->t_next;
-  }
-};
+}
 
-// Launch-path check: the tables are always published ready (rewrites are synchronous).
+TimedLaunch::~TimedLaunch() {
+  if (!armed) return;
+  if (msh::launch_events_pending()) msh::set_launch_events(nullptr, nullptr);
+  else ++c->t_next;
+}
+
 int ready(msh_ctx* c) {
   if (!c->have_nodes) return fail(c, MSH_ERR_STATE, "msh_upload_nodes has not been called");
   return MSH_OK;
 }
 
-// pair_kernel's arguments for the current table (the batches are filled in by the caller).
 msh::PairArgs pair_args(msh_ctx* c) {
   msh::PairArgs a{};
   const NodeTable& t = cur_table(c);
@@ -560,7 +442,7 @@ int launch_batch_descs(msh_ctx* c, const msh::BatchDesc* d, int32_t nb, hipStrea
 
 // The generic pipeline runs the batch entry points when the score list names a score column (or
 // for every list with MSH_BATCH_KERNEL=generic, an A/B switch).
-bool use_generic(const msh_ctx* c) { return c->generic || c->dev.batch_kernel == 2; }
+bool use_generic(const msh_ctx* c) { return c->generic || c->dev.batch_kernel == 1; }
 
 // The largest |NormalizeScore(raw)| one plugin can give a feasible pair: NodeNumber's raw
 // scores are 0 / 10; a column's raw scores lie in [lo, hi] (its upload). DefaultNormalizeScore gives
@@ -646,39 +528,9 @@ int launch_generic_descs(msh_ctx* c, const msh::BatchDesc* d, int32_t nb, hipStr
   return MSH_OK;
 }
 
-// The ctx's device current for the call, the caller's restored after it (no switch at all in the
-// common case of a caller already on that device).
-struct DeviceGuard {
-  int prev = -1, want;
-  explicit DeviceGuard(int d) : want(d) {
-    if (hipGetDevice(&prev) != hipSuccess || prev != d) (void)hipSetDevice(d);
-  }
-  ~DeviceGuard() {
-    if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
-  }
-};
-
-// Host-buffer I/O of one synchronous call: pod columns and outputs in page-locked host memory,
-// read and written by the kernel (default; the A/B modes of DeviceInfo DMA them through device
-// scratch); then, for a pageable caller, outputs copied from the stage into the caller's arrays.
-struct HostIO {
-  int8_t* d_pd = nullptr;
-  uint8_t* d_pt = nullptr;
-  int32_t* o_idx = nullptr;    // what the kernel writes (device-visible)
-  int64_t* o_score = nullptr;
-  int32_t* o_status = nullptr;
-  int32_t* h_idx = nullptr;    // page-locked destination: the caller's arrays or the stage
-  int64_t* h_score = nullptr;
-  int32_t* h_status = nullptr;
-  bool staged = false;
-};
-
 int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t* pod_tol, int32_t* out_idx,
                   int64_t* out_score, int32_t* out_status, HostIO& io) {
-  int rc = ensure_pod_scratch(c, p);
-  if (rc != MSH_OK) return rc;
-  io.d_pd = c->d_pd;
-  io.d_pt = c->d_pt;
+  int rc = MSH_OK;
   // out_score is optional (NULL: scores not written, 8 B per pod less over PCIe)
   void* di = pinned_device_ptr(out_idx);
   void* ds = (di && out_score) ? pinned_device_ptr(out_score) : nullptr;
@@ -698,14 +550,11 @@ int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t*
     src_pd = reinterpret_cast<const int8_t*>(c->h_stage + L.pd);
     src_pt = c->h_stage + L.pt;
   }
-  if (c->dev.host_io_zc_in) {  // the kernel reads the page-locked columns itself
-    io.d_pd = static_cast<int8_t*>(pinned_device_ptr(src_pd));
-    io.d_pt = static_cast<uint8_t*>(pinned_device_ptr(src_pt));
-    if (!io.d_pd || !io.d_pt) return fail(c, MSH_ERR_HIP, "page-locked pod columns without a device address");
-  } else {  // DMA into device scratch
-    MSH_HIP(c, hipMemcpyAsync(c->d_pd, src_pd, (size_t)p, hipMemcpyHostToDevice, c->stream));
-    MSH_HIP(c, hipMemcpyAsync(c->d_pt, src_pt, (size_t)p, hipMemcpyHostToDevice, c->stream));
-  }
+  // the kernel reads the page-locked columns itself (zero-copy: no DMA command; 56.6 us per C3 call
+  // against 73 us with the columns DMA'd, profiles/ab/r2_e2e_host2.jsonl)
+  io.d_pd = static_cast<int8_t*>(pinned_device_ptr(src_pd));
+  io.d_pt = static_cast<uint8_t*>(pinned_device_ptr(src_pt));
+  if (!io.d_pd || !io.d_pt) return fail(c, MSH_ERR_HIP, "page-locked pod columns without a device address");
   if (io.staged) {
     io.h_idx = reinterpret_cast<int32_t*>(c->h_stage + L.idx);
     io.h_score = out_score ? reinterpret_cast<int64_t*>(c->h_stage + L.score) : nullptr;
@@ -721,31 +570,12 @@ int host_io_begin(msh_ctx* c, int32_t p, const int8_t* pod_digit, const uint8_t*
     io.o_score = static_cast<int64_t*>(ds);
     io.o_status = static_cast<int32_t*>(dt);
   }
-  if (c->dev.host_io_dma) {
-    io.o_idx = c->d_oi;
-    io.o_score = out_score ? c->d_os : nullptr;
-    io.o_status = c->d_ost;
-  }
   return MSH_OK;
 }
 
 int host_io_end(msh_ctx* c, int32_t p, int32_t* out_idx, int64_t* out_score, int32_t* out_status,
                 const HostIO& io) {
-  if (c->dev.host_io_dma) {
-    MSH_HIP(c, hipMemcpyAsync(io.h_idx, c->d_oi, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    if (out_score)
-      MSH_HIP(c, hipMemcpyAsync(io.h_score, c->d_os, (size_t)p * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-    MSH_HIP(c, hipMemcpyAsync(io.h_status, c->d_ost, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  }
-  if (c->dev.host_sync_poll) {
-    if (!c->done_ev) MSH_HIP(c, hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming));
-    MSH_HIP(c, hipEventRecord(c->done_ev, c->stream));
-    hipError_t q;
-    while ((q = hipEventQuery(c->done_ev)) == hipErrorNotReady) std::this_thread::yield();
-    if (q != hipSuccess) return hip_fail(c, q, "hipEventQuery");
-  } else {
-    MSH_HIP(c, hipStreamSynchronize(c->stream));
-  }
+  MSH_HIP(c, hipStreamSynchronize(c->stream));
   c->async_done = c->async_issued;  // the ctx's stream is drained: every async batch is done too
   if (io.staged) {
     const CopyJob jobs[3] = {{out_idx, io.h_idx, (size_t)p * sizeof(int32_t)},
@@ -759,39 +589,35 @@ int host_io_end(msh_ctx* c, int32_t p, int32_t* out_idx, int64_t* out_score, int
 // The message of the last failed msh_create on this thread (msh_last_error(NULL)).
 thread_local std::string g_create_err;
 
-// One A/B switch: unset leaves *out alone; a value outside `allowed` fails with a message.
-bool knob(const char* name, std::initializer_list<std::pair<const char*, int>> allowed, int* out, std::string* err) {
-  const char* v = getenv(name);
-  if (!v) return true;
-  for (const auto& a : allowed)
-    if (strcmp(v, a.first) == 0) {
-      *out = a.second;
-      return true;
-    }
-  *err = std::string(name) + "=" + v + ": not one of";
-  for (const auto& a : allowed) *err += std::string(" ") + a.first;
-  return false;
+// msh_create_ex's options into the ctx's launch choices: every field's 0 is the automatic choice, a
+// value outside a field's set fails with a message (never mapped to another setting).
+bool apply_options(const msh_options& o, msh::DeviceInfo& d, std::string* err) {
+  auto in = [&](const char* name, int32_t v, std::initializer_list<int32_t> allowed) {
+    for (int32_t a : allowed)
+      if (v == a) return true;
+    *err = std::string("msh_options.") + name + " = " + std::to_string(v) + ": not one of";
+    for (int32_t a : allowed) *err += " " + std::to_string(a);
+    return false;
+  };
+  if (!in("batch_kernel", o.batch_kernel, {0, 1}) || !in("pair_planes", o.pair_planes, {0, 1, 2}) ||
+      !in("pair_noax", o.pair_noax, {0, 1, 2}) || !in("pair_slices", o.pair_slices, {0, 1, 2, 4}) ||
+      !in("seq_waves", o.seq_waves, {0, 1, 4, 15, 16}) || !in("seq_split", o.seq_split, {0, 1}) ||
+      !in("gen_keys", o.gen_keys, {0, 1}) || !in("gen_nnkey", o.gen_nnkey, {0, 1}))
+    return false;
+  d.batch_kernel = o.batch_kernel;
+  d.pair_planes = o.pair_planes;
+  d.pair_noax = o.pair_noax == 0 ? -1 : (o.pair_noax == 1 ? 1 : 0);
+  d.bits_slices = o.pair_slices;
+  d.seq_waves = o.seq_waves;
+  d.seq_split = o.seq_split == 0 ? 1 : 0;
+  d.gen_f53 = o.gen_keys == 0 ? 1 : 0;
+  d.gen_nnkey = o.gen_nnkey == 0 ? 1 : 0;
+  return true;
 }
 
-bool read_knobs(msh::DeviceInfo& d, std::string* err) {
-  int io = 0, poll = 0;
-  const bool ok = knob("MSH_BITS_SLICES", {{"0", 0}, {"1", 1}, {"2", 2}, {"4", 4}}, &d.bits_slices, err) &&
-                  knob("MSH_SEQ_WAVES", {{"0", 0}, {"1", 1}, {"4", 4}, {"15", 15}, {"16", 16}}, &d.seq_waves, err) &&
-                  knob("MSH_HOST_IO", {{"zero-copy", 0}, {"zc", 1}, {"dma", 2}}, &io, err) &&
-                  knob("MSH_HOST_SYNC", {{"wait", 0}, {"poll", 1}}, &poll, err) &&
-                  knob("MSH_BATCH_KERNEL", {{"pair", 0}, {"generic", 2}}, &d.batch_kernel, err) &&
-                  knob("MSH_PAIR_PLANES", {{"auto", 0}, {"sgpr", 1}, {"lds", 2}}, &d.pair_planes, err) &&
-                  knob("MSH_PAIR_NOAX", {{"auto", -1}, {"1", 1}, {"0", 0}}, &d.pair_noax, err) &&
-                  knob("MSH_GEN_NNKEY", {{"auto", 1}, {"select", 0}}, &d.gen_nnkey, err) &&
-                  knob("MSH_GEN_F53", {{"1", 1}, {"0", 0}}, &d.gen_f53, err) &&
-                  knob("MSH_SEQ_SPLIT", {{"auto", 1}, {"serial", 0}}, &d.seq_split, err);
-  d.host_io_dma = io == 2;
-  d.host_io_zc_in = io == 0;
-  d.host_sync_poll = poll;
-  return ok;
-}
+}  // namespace msh::capi
 
-}  // namespace
+using namespace msh::capi;
 
 extern "C" {
 
@@ -833,10 +659,21 @@ void msh_host_free(void* ptr) {
   (void)hipHostFree(ptr);
 }
 
-int msh_create(int device, msh_ctx** out_ctx) {
+int msh_create(int device, msh_ctx** out_ctx) { return msh_create_ex(device, nullptr, out_ctx); }
+
+int msh_create_ex(int device, const msh_options* opts, msh_ctx** out_ctx) {
   g_create_err.clear();
   if (!out_ctx) return MSH_ERR_INVALID;
   *out_ctx = nullptr;
+  msh::DeviceInfo info;
+  if (opts) {
+    // kernel-selection overrides (tests / A-B), resolved here once, never on a launch path
+    if (opts->struct_size != (int32_t)sizeof(msh_options)) {
+      g_create_err = "msh_options.struct_size != sizeof(msh_options)";
+      return MSH_ERR_INVALID;
+    }
+    if (!apply_options(*opts, info, &g_create_err)) return MSH_ERR_INVALID;
+  }
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MSH_ERR_NO_DEVICE;
   if (device < 0 || device >= n) return MSH_ERR_NO_DEVICE;
@@ -846,17 +683,10 @@ int msh_create(int device, msh_ctx** out_ctx) {
   msh_ctx* c = new (std::nothrow) msh_ctx();
   if (!c) return MSH_ERR_NOMEM;
   c->device = device;
+  c->dev = info;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->dev.cus = prop.multiProcessorCount;
-  // test / A-B switches, read once here (never on a launch path); a value outside a switch's set is
-  // rejected (MSH_ERR_INVALID, message in msh_last_error(NULL)), never mapped to another setting
-  std::string bad;
-  if (!read_knobs(c->dev, &bad)) {
-    delete c;
-    g_create_err = bad;
-    return MSH_ERR_INVALID;
-  }
   int lo_prio = 0, hi_prio = 0;  // numerically lower = higher priority
   if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) hi_prio = 0;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -882,6 +712,7 @@ void msh_destroy(msh_ctx* c) {
   // launches this ctx queued on caller streams (the *_device entry points) may still read the tables
   for (NodeTable& t : c->tab) wait_events(t.readers);
   wait_events(c->seq_inflight);
+  msh_shard_release(c);  // its node-sharded launch in flight, merge buffers and communicator
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->prep_stream) (void)hipStreamSynchronize(c->prep_stream);
   for (NodeTable& t : c->tab) {
@@ -892,12 +723,10 @@ void msh_destroy(msh_ctx* c) {
   (void)hipFree(c->d_counts);
   for (hipEvent_t e : c->async_ev)
     if (e) (void)hipEventDestroy(e);
-  if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   for (auto& e : c->tev) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
   }
-  free_pods(c);
   (void)hipHostFree(c->h_stage);
   (void)hipHostFree(c->h_nstage);
   (void)hipFree(c->d_patch);

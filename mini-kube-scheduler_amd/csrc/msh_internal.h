@@ -29,36 +29,32 @@ inline bool needs_kx(const PluginParams& pp) {
   return pp.has_nn_score && pp.nn_prescore && (pp.mode == 2 || pp.mode == 3);
 }
 
-// Device facts and launch choices, resolved once in msh_create (never on the launch path).
+// Device facts and launch choices, resolved once in msh_create / msh_create_ex (never on the launch
+// path). The overrides come only from msh_create_ex's msh_options (tests and A/B measurement); the
+// library reads no environment variable.
 struct DeviceInfo {
   int cus = 256;
-  int bits_slices = 0;   // tests / A-B only (MSH_BITS_SLICES at msh_create): pair_kernel slice waves per pod block
-                         // (1, 2, 4), 0 = auto
-  int seq_waves = 0;     // tests / A-B only (MSH_SEQ_WAVES at msh_create): sequential scanning waves, 0 = auto
-  // Host-buffer calls (msh_schedule_batch / _sequential): the kernel reads the pod columns from and
-  // writes the outputs to page-locked host memory (default). A/B only, MSH_HOST_IO at msh_create:
-  // "dma" = columns and outputs DMA'd through device scratch, "zc" = columns DMA'd, outputs zero-copy.
-  int host_io_dma = 0;
-  int host_io_zc_in = 1;
-  int host_sync_poll = 0;  // A/B only (MSH_HOST_SYNC=poll): poll an event instead of hipStreamSynchronize
-  // Batch kernel (MSH_BATCH_KERNEL at msh_create): 0 = the per-pair bit-plane kernels for the reference's
-  // plugins (default); 2 = generic_kernel for every plugin list ("generic", A/B and cross-check)
+  int bits_slices = 0;   // msh_options.pair_slices: pair_kernel slice waves per pod block (1, 2, 4) and
+                         // generic_kernel waves per pod group, 0 = auto
+  int seq_waves = 0;     // msh_options.seq_waves: sequential scanning waves, 0 = auto
+  // msh_options.batch_kernel: 0 = the per-pair bit-plane kernels for the reference's plugins (default);
+  // 1 = generic_kernel for every plugin list (A/B and cross-check)
   int batch_kernel = 0;
-  // Where pair_kernel's node planes come from (MSH_PAIR_PLANES at msh_create): 0 = auto (LDS-staged
-  // for tables up to PAIR_LDS_BIG_GROUPS groups and launches that fill the chip, scalar loads
-  // otherwise), 1 = scalar loads into SGPRs, 2 = LDS-staged (tables that fit)
+  // msh_options.pair_planes, where pair_kernel's node planes come from: 0 = auto (LDS-staged for tables
+  // up to PAIR_LDS_BIG_GROUPS groups and launches that fill the chip, scalar loads otherwise), 1 = scalar
+  // loads into SGPRs, 2 = LDS-staged (tables that fit)
   int pair_planes = 0;
-  // MSH_PAIR_NOAX: the LDS-staged form scans group 0 first and drops the non-match / feasible
+  // msh_options.pair_noax: the LDS-staged form scans group 0 first and drops the non-match / feasible
   // reduction from the scan of the other groups when group 0 has settled it for every lane of the
   // wave (1), or scans group 0 last and never drops it (0). -1 = auto: 1 for REVERSE / MINMAX (78.1
   // against 89.0 us per 32-batch C3 launch), 0 for the identity-like modes (77.3-78.3 against
   // 80.9-81.2), profiles/r4_ab_pair_planes.txt
   int pair_noax = -1;
-  // MSH_SEQ_SPLIT: without a capacity, the sequential kernel's pods in blocks of consecutive pods, one
-  // workgroup each (auto, 1), or all in one workgroup (serial, 0)
+  // msh_options.seq_split: without a capacity, the sequential kernel's pods in blocks of consecutive
+  // pods, one workgroup each (auto, 1), or all in one workgroup (serial, 0)
   int seq_split = 1;
-  int gen_f53 = 1;    // MSH_GEN_F53: generic_kernel's double keys for 64-bit totals below 2^53 (1) or uint64_t (0)
-  int gen_nnkey = 1;  // MSH_GEN_NNKEY: generic_kernel's compare-free NodeNumber key (1) or the select (0)
+  int gen_f53 = 1;    // msh_options.gen_keys: generic_kernel's double keys for 64-bit totals below 2^53 (1) or uint64_t (0)
+  int gen_nnkey = 1;  // msh_options.gen_nnkey: generic_kernel's compare-free NodeNumber key (1) or the select (0)
 };
 
 // NodeNumber codes: a node's suffix digit 0..9, or CODE_NONE_NODE when its name has no digit
@@ -144,6 +140,24 @@ hipError_t launch_pairs(PairArgs& a, bool shard, const DeviceInfo& dev, hipStrea
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, int32_t p, const int32_t* keys, PluginParams pp,
                               int32_t* out_idx, int64_t* out_score, int32_t* out_status, hipStream_t s);
+
+// Device groups (msh_group_*, msh_prep.hip): the merge on the home device over every shard's per-pod
+// buffers (peer-mapped pointers, one per shard, List order of the shards).
+constexpr int GROUP_MAX = 16;  // MSH_GROUP_MAX_SHARDS
+struct GroupPtrs {
+  const int32_t* keys[GROUP_MAX];  // shard keys, 2p each (group_keys_decode)
+  const int64_t* v[GROUP_MAX];     // extents (group_max_i64) or best totals (group_best_merge)
+  const int32_t* idx[GROUP_MAX];   // best global indices (group_best_merge)
+  int32_t n;
+};
+// element-wise MAX of the shards' keys, then decode_pod (msh_decode_keys_device's decode)
+hipError_t launch_group_keys_decode(const GroupPtrs& g, const int8_t* pod_digit, int32_t p, PluginParams pp,
+                                    int32_t* out_idx, int64_t* out_score, int32_t* out_status, hipStream_t s);
+// element-wise MAX of the shards' len int64 (the generic extents: maxima and negated minima)
+hipError_t launch_group_max_i64(const GroupPtrs& g, int64_t len, int64_t* out, hipStream_t s);
+// per pod: the largest total, then the lowest global index among the shards holding it
+hipError_t launch_group_best_merge(const GroupPtrs& g, int32_t p, int64_t* out_total, int32_t* out_idx,
+                                   hipStream_t s);
 
 // ---- generic score pipeline (any score plugin list; generic_kernel) ----
 constexpr int GEN_MAX_SCORE = 5;  // score plugins per list: NodeNumber + up to four score columns

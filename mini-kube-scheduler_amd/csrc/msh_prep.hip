@@ -185,6 +185,89 @@ hipError_t launch_decode_keys(const int8_t* pod_digit, int32_t p, const int32_t*
 }
 
 // ---------------------------------------------------------------------------------------
+// Device groups (msh_group_*): the cross-shard merge on the home device. Every shard's per-pod result
+// stays in its own HBM; one thread per pod loads it from each shard through the peer mapping (xGMI reads,
+// coalesced: consecutive pods, consecutive addresses), merges, and decodes. The merge replaces the
+// all-reduce of the one-process-per-GPU form; the reduction is the same (MAX of the keys / extents; MAX
+// total then MIN index), so the decisions are the same.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void group_keys_decode_kernel(GroupPtrs g, const int8_t* __restrict__ pod_digit,
+                                                                int32_t p, PluginParams pp,
+                                                                int32_t* __restrict__ out_idx,
+                                                                int64_t* __restrict__ out_score,
+                                                                int32_t* __restrict__ out_status) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p) return;
+  int32_t k0 = 0, k1 = 0;  // 0 = no node (every real key is positive)
+  for (int s = 0; s < g.n; ++s) {
+    const int32_t* k = g.keys[s];
+    k0 = max(k0, k[j]);
+    k1 = max(k1, k[(size_t)p + j]);
+  }
+  const int32_t ka = k0 > k1 ? k0 : k1;
+  auto idx_of = [](int32_t k) -> int64_t { return k ? (int64_t)(GKEY_MAX - k) : -1; };
+  const int d = pod_digit[j];
+  int32_t oi, ost;
+  int64_t osc;
+  decode_pod(idx_of(k0), idx_of(k1), idx_of(ka), d >= 0 && d <= 9, pp, &oi, &osc, &ost);
+  out_idx[j] = oi;
+  if (out_score) out_score[j] = osc;
+  out_status[j] = ost;
+}
+
+__global__ __launch_bounds__(256) void group_max_i64_kernel(GroupPtrs g, int64_t len, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  int64_t m = INT64_MIN;
+  for (int s = 0; s < g.n; ++s) m = max(m, g.v[s][i]);
+  out[i] = m;
+}
+
+// Per pod: the largest total over the shards, the lowest global index among the shards that hold it
+// (selectHost's first maximum across shards); INT64_MIN / INT32_MAX when no shard has a feasible node.
+__global__ __launch_bounds__(256) void group_best_merge_kernel(GroupPtrs g, int32_t p, int64_t* __restrict__ out_total,
+                                                               int32_t* __restrict__ out_idx) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p) return;
+  int64_t best = INT64_MIN;
+  int32_t bi = INT32_MAX;
+  for (int s = 0; s < g.n; ++s) {
+    const int32_t i = g.idx[s][j];
+    const int64_t t = g.v[s][j];
+    if (i != INT32_MAX && (bi == INT32_MAX || t > best || (t == best && i < bi))) {
+      best = t;
+      bi = i;
+    }
+  }
+  out_total[j] = best;
+  out_idx[j] = bi;
+}
+
+hipError_t launch_group_keys_decode(const GroupPtrs& g, const int8_t* pod_digit, int32_t p, PluginParams pp,
+                                    int32_t* out_idx, int64_t* out_score, int32_t* out_status, hipStream_t s) {
+  if (p <= 0) return hipSuccess;
+  if (g.n < 1 || g.n > GROUP_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(group_keys_decode_kernel, dim3((p + 255) / 256), dim3(256), 0, s, g, pod_digit, p, pp, out_idx,
+                     out_score, out_status);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_max_i64(const GroupPtrs& g, int64_t len, int64_t* out, hipStream_t s) {
+  if (len <= 0) return hipSuccess;
+  if (g.n < 1 || g.n > GROUP_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(group_max_i64_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, g, len, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_best_merge(const GroupPtrs& g, int32_t p, int64_t* out_total, int32_t* out_idx,
+                                   hipStream_t s) {
+  if (p <= 0) return hipSuccess;
+  if (g.n < 1 || g.n > GROUP_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(group_best_merge_kernel, dim3((p + 255) / 256), dim3(256), 0, s, g, p, out_total, out_idx);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // Per-pair plugin results (debug / simulator result store). One workgroup per pod:
 // pass 1 ORs "feasible match" / "feasible non-match" over the List to get the extent NormalizeScore
 // needs; pass 2 writes, for every node i,

@@ -112,6 +112,22 @@ static PyObject* py_decode_keys_device(PyObject* self, PyObject* const* a, Py_ss
   return PyLong_FromLong(rc);
 }
 
+/* schedule_nodeshard_device(ctx, p, d_pod_digit, d_pod_tol, node_base, d_out_idx, d_out_score,
+ * d_out_status, stream) -> rc */
+static PyObject* py_schedule_nodeshard_device(PyObject* self, PyObject* const* a, Py_ssize_t n) {
+  (void)self;
+  void *ctx, *pd, *pt, *oi, *os, *ost, *st;
+  long long p, base;
+  if (want_args(n, 9, "schedule_nodeshard_device") || as_ptr(a[0], &ctx) || as_i64(a[1], &p) ||
+      as_ptr(a[2], &pd) || as_ptr(a[3], &pt) || as_i64(a[4], &base) || as_ptr(a[5], &oi) || as_ptr(a[6], &os) ||
+      as_ptr(a[7], &ost) || as_ptr(a[8], &st))
+    return NULL;
+  if (p < INT32_MIN || p > INT32_MAX) return PyErr_Format(PyExc_OverflowError, "pod count out of range");
+  const int rc = msh_schedule_nodeshard_device((msh_ctx*)ctx, (int32_t)p, (const int8_t*)pd, (const uint8_t*)pt,
+                                               (int64_t)base, (int32_t*)oi, (int64_t*)os, (int32_t*)ost, st);
+  return PyLong_FromLong(rc);
+}
+
 /* ---- host-buffer calls: numpy arrays (or any C-contiguous buffer) by the buffer protocol ----
  * Taking an array's address through numpy's ctypes interface costs ~3 us per array in Python,
  * five per call; PyObject_GetBuffer costs ~0.1 us. The GIL is released during the call. */
@@ -229,6 +245,9 @@ static PyMethodDef methods[] = {
      "out_status, stream) -> rc"},
     {"shard_keys_device", (PyCFunction)(void (*)(void))py_shard_keys_device, METH_FASTCALL,
      "msh_shard_keys_device(ctx, p, pod_digit, pod_tol, node_base, keys, stream) -> rc"},
+    {"schedule_nodeshard_device", (PyCFunction)(void (*)(void))py_schedule_nodeshard_device, METH_FASTCALL,
+     "msh_schedule_nodeshard_device(ctx, p, pod_digit, pod_tol, node_base, out_idx, out_score, out_status, "
+     "stream) -> rc"},
     {"decode_keys_device", (PyCFunction)(void (*)(void))py_decode_keys_device, METH_FASTCALL,
      "msh_decode_keys_device(ctx, p, pod_digit, pod_tol, keys, out_idx, out_score, out_status, stream) -> rc"},
     {NULL, NULL, 0, NULL},

@@ -567,7 +567,7 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
     return launch_seq_nw<16, true>(ka, rs, 1, s);
   }
   // Without a capacity: 64-pod blocks of consecutive pods, each one workgroup walking its pods in
-  // order (MSH_SEQ_SPLIT=serial: one workgroup for the whole batch)
+  // order (msh_options.seq_split = MSH_SEQ_SERIAL: one workgroup for the whole batch)
   const int32_t blocks = seq_blocks(a, dev);
   if (blocks > 1) ka.pods_per_block = WAVE;
   if (nw == 1) return launch_seq_nw<1, false>(ka, rs, blocks, s);

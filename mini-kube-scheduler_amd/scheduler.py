@@ -71,13 +71,24 @@ def _ids(names: Sequence[str], table: dict, what: str) -> np.ndarray:
 
 
 class DeviceContext:
-    """One msh_ctx bound to one HIP device."""
+    """One msh_ctx bound to one HIP device.
 
-    def __init__(self, device: int = 0):
+    `options` (tests and A/B measurement only): msh_options overrides for msh_create_ex, e.g.
+    {"batch_kernel": "generic", "seq_waves": 16, "seq_split": "serial"} (names in _native.OPTION_NAMES,
+    ints as they are; a value outside a field's set is MSH_ERR_INVALID from the library)."""
+
+    def __init__(self, device: int = 0, options: dict | None = None):
         self._lib = N.lib()
         self._fast = N.fast()
         h = C.c_void_p()
-        N.check(self._lib.msh_create(device, C.byref(h)))
+        opts = N.make_options(options)
+        if opts is None:
+            rc = self._lib.msh_create(device, C.byref(h))
+        else:
+            rc = self._lib.msh_create_ex(device, C.byref(opts), C.byref(h))
+        if rc != N.MSH_OK:
+            raw = self._lib.msh_last_error(None)
+            raise N.MshError(rc, raw.decode() if raw else "")
         self.handle = h
         self.device = device
         self.n_nodes = 0
@@ -290,6 +301,45 @@ class DeviceContext:
         self._check(self._lib.msh_keys_slot1_is_any(self.handle, C.byref(v)))
         return bool(v.value)
 
+    # -- node-sharded scheduling with the merge in the library (ABI v8: RCCL communicator) --
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """msh_comm_unique_id: the MSH_COMM_ID_BYTES id rank 0 makes and ships to every rank."""
+        buf = (C.c_uint8 * N.COMM_ID_BYTES)()
+        N.check(N.lib().msh_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, comm_id: bytes, world: int, rank: int) -> None:
+        """msh_comm_init (collective over the `world` ranks)."""
+        if len(comm_id) != N.COMM_ID_BYTES:
+            raise ValueError(f"a comm id is {N.COMM_ID_BYTES} bytes")
+        buf = (C.c_uint8 * N.COMM_ID_BYTES).from_buffer_copy(comm_id)
+        self._check(self._lib.msh_comm_init(self.handle, buf, int(world), int(rank)))
+
+    def comm_info(self) -> tuple[int, int]:
+        w, r = C.c_int32(), C.c_int32()
+        self._check(self._lib.msh_comm_info(self.handle, C.byref(w), C.byref(r)))
+        return w.value, r.value
+
+    def schedule_nodeshard_device(self, p: int, d_pod_digit: int, d_pod_tol: int, node_base: int, d_idx: int,
+                                  d_score: int, d_status: int, stream: int = 0) -> None:
+        """msh_schedule_nodeshard_device: shard kernel, all-reduce(s) over the communicator, decode, on
+        `stream`; every rank ends with the global decisions."""
+        rc = self._fast.schedule_nodeshard_device(self._hv(), p, d_pod_digit, d_pod_tol, int(node_base), d_idx,
+                                                  d_score, d_status, stream or None)
+        if rc:
+            self._check(rc)
+
+    def schedule_nodeshard(self, pod_digit: np.ndarray, pod_tol: np.ndarray, node_base: int, out=None):
+        """msh_schedule_nodeshard: the host-buffer form (synchronous)."""
+        pod_digit = np.ascontiguousarray(pod_digit, np.int8)
+        pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
+        p = _same_len("schedule_nodeshard", pod_digit, pod_tol)
+        idx, score, status = self._outputs(p, out)
+        self._check(self._lib.msh_schedule_nodeshard(self.handle, p, N.ptr(pod_digit), N.ptr(pod_tol), int(node_base),
+                                                     N.ptr(idx), N.ptr(score), N.ptr(status)))
+        return idx, score, status
+
     # -- node-sharded generic pipeline (msh_generic_*: any plugin list, score columns included) --
     def generic_ext_len(self, p: int) -> int:
         """int64 entries of the per-pod extents msh_generic_extents_device writes (0: no plugin
@@ -317,6 +367,52 @@ class DeviceContext:
         self._check(self._lib.msh_generic_decode_device(self.handle, int(p), d_pod_digit, d_merged_total,
                                                         d_merged_idx, d_idx, d_score or None, d_status,
                                                         stream or None))
+
+
+class DeviceGroup:
+    """msh_group: shard ctxs in List order (ctxs[k] holds the k-th contiguous slice of the node table), any
+    devices; the merge runs on ctxs[0]'s device. The ctxs stay owned by the caller: close the group first."""
+
+    def __init__(self, ctxs: Sequence[DeviceContext]):
+        self._lib = N.lib()
+        self.ctxs = list(ctxs)
+        arr = (C.c_void_p * len(self.ctxs))(*[c.handle for c in self.ctxs])
+        h = C.c_void_p()
+        rc = self._lib.msh_group_create(arr, len(self.ctxs), C.byref(h))
+        if rc != N.MSH_OK:
+            raw = self._lib.msh_group_last_error(None)
+            raise N.MshError(rc, raw.decode() if raw else "")
+        self.handle = h
+
+    def close(self) -> None:
+        if self.handle:
+            self._lib.msh_group_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def schedule_batch(self, pod_digit: np.ndarray, pod_tol: np.ndarray, scores: bool = True):
+        """msh_group_schedule_batch: the decisions over the whole (sharded) table."""
+        pod_digit = np.ascontiguousarray(pod_digit, np.int8)
+        pod_tol = np.ascontiguousarray(pod_tol, np.uint8)
+        p = _same_len("group schedule_batch", pod_digit, pod_tol)
+        idx, score, status = np.empty(p, np.int32), (np.empty(p, np.int64) if scores else None), np.empty(p, np.int32)
+        rc = self._lib.msh_group_schedule_batch(self.handle, p, N.ptr(pod_digit), N.ptr(pod_tol), N.ptr(idx),
+                                                N.ptr(score), N.ptr(status))
+        if rc != N.MSH_OK:
+            raw = self._lib.msh_group_last_error(self.handle)
+            raise N.MshError(rc, raw.decode() if raw else "")
+        return idx, score, status
 
 
 class Scheduler:

@@ -34,7 +34,7 @@ def test_fast_call_module(msh):
     (MSH_ERR_INVALID, no device call)."""
     fast = msh._native.fast()
     names = ["schedule_batch_device", "schedule_batches_device", "schedule_sequential_device", "shard_keys_device",
-             "decode_keys_device"]
+             "decode_keys_device", "schedule_nodeshard_device"]
     assert all(callable(getattr(fast, n)) for n in names)
     inv = msh._native.MSH_ERR_INVALID
     assert fast.schedule_batch_device(None, 0, None, None, None, None, None, None) == inv
@@ -63,7 +63,64 @@ def test_fast_call_module(msh):
 def test_abi_version(msh):
     header = (ROOT / "include" / "minisched_hip.h").read_text()
     assert f"#define MSH_ABI_VERSION {msh._native.lib().msh_abi_version()}" in header
-    assert msh._native.lib().msh_abi_version() == 7
+    assert msh._native.lib().msh_abi_version() == 8
+
+
+def test_library_reads_no_environment(msh):
+    """Kernel choices come only from msh_create_ex's msh_options (verdict r5, next #4): no source of the
+    library calls getenv, and the linked library imports no environment reader."""
+    import subprocess
+    for f in (ROOT / "mini-kube-scheduler_amd" / "csrc").glob("*"):
+        if f.suffix in (".cpp", ".hip", ".h") and f.is_file():
+            assert "getenv" not in f.read_text(), f
+    lib = importlib.import_module("mini-kube-scheduler_amd.build").LIB
+    und = subprocess.run(["nm", "-D", "-u", str(lib)], capture_output=True, text=True, check=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", und), und
+
+
+def test_options_are_checked_before_any_device_call(msh):
+    """msh_create_ex rejects an option outside its field's set, or a wrong struct_size, with
+    MSH_ERR_INVALID and a message (before it asks for a device, so this runs on CPU); a zeroed struct
+    is msh_create (here: MSH_ERR_NO_DEVICE on a machine without a GPU)."""
+    N = msh._native
+    lib = N.lib()
+    h = C.c_void_p()
+    for field, bad in (("batch_kernel", 2), ("pair_planes", 3), ("pair_noax", -1), ("pair_slices", 3),
+                       ("seq_waves", 2), ("seq_split", 2), ("gen_keys", 5), ("gen_nnkey", 9)):
+        o = N.make_options({field: bad})
+        assert lib.msh_create_ex(0, C.byref(o), C.byref(h)) == N.MSH_ERR_INVALID, field
+        assert field in lib.msh_last_error(None).decode()
+        assert not h.value
+    o = N.make_options({"seq_waves": 16})
+    o.struct_size = 4
+    assert lib.msh_create_ex(0, C.byref(o), C.byref(h)) == N.MSH_ERR_INVALID
+    with pytest.raises(ValueError):
+        N.make_options({"no_such_field": 1})
+    if msh.device_count() == 0:
+        o = N.make_options({"seq_waves": "auto"})
+        assert lib.msh_create_ex(0, C.byref(o), C.byref(h)) == N.MSH_ERR_NO_DEVICE
+
+
+def test_sharded_entry_points_check_arguments(msh):
+    """ABI v8's node-sharded entry points: a NULL ctx / group / list is MSH_ERR_INVALID with no device call."""
+    N = msh._native
+    lib = N.lib()
+    inv = N.MSH_ERR_INVALID
+    w, r = C.c_int32(), C.c_int32()
+    assert lib.msh_comm_info(None, C.byref(w), C.byref(r)) == inv
+    assert lib.msh_comm_init(None, None, 1, 0) == inv
+    assert lib.msh_comm_unique_id(None) == inv
+    assert lib.msh_schedule_nodeshard_device(None, 0, None, None, 0, None, None, None, None) == inv
+    assert lib.msh_schedule_nodeshard(None, 0, None, None, 0, None, None, None) == inv
+    assert msh._native.fast().schedule_nodeshard_device(None, 0, None, None, 0, None, None, None, None) == inv
+    g = C.c_void_p()
+    assert lib.msh_group_create(None, 1, C.byref(g)) == inv and not g.value
+    arr = (C.c_void_p * 2)(None, None)
+    assert lib.msh_group_create(arr, 2, C.byref(g)) == inv
+    assert lib.msh_group_last_error(None).decode()
+    arr17 = (C.c_void_p * 17)()
+    assert lib.msh_group_create(arr17, 17, C.byref(g)) == inv
+    assert lib.msh_group_schedule_batch(None, 0, None, None, None, None, None) == inv
 
 
 def test_no_device_is_an_error_not_a_fallback(msh):

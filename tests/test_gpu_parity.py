@@ -40,13 +40,12 @@ def _set(ctx, msh, ps):
                     [msh.ScorePluginConfig(s, w, msh.Normalize(m)) for s, w, m in zip(ps.score, ps.weights, ps.normalize)])
 
 
-def _pair_env(monkeypatch, spec):
-    """Pair-kernel switches from a spec "planes[-noax|-axlast]" (planes: sgpr, lds or auto; noax / axlast:
-    MSH_PAIR_NOAX 1 / 0 — group 0 scanned first and the non-match / feasible reduction dropped where it
-    settled it, or never — else auto: 1 for REVERSE / MINMAX, 0 for the identity-like modes)."""
+def _pair_opts(spec):
+    """msh_options for the pair kernel from a spec "planes[-noax|-axlast]" (planes: sgpr, lds or auto;
+    noax / axlast: group 0 scanned first and the non-match / feasible reduction dropped where it settled
+    it, or never — else auto: the first for REVERSE / MINMAX, the second for the identity-like modes)."""
     parts = spec.split("-")
-    monkeypatch.setenv("MSH_PAIR_PLANES", parts[0])
-    monkeypatch.setenv("MSH_PAIR_NOAX", "1" if "noax" in parts else "0" if "axlast" in parts else "auto")
+    return {"pair_planes": parts[0], "pair_noax": "noax" if "noax" in parts else "axlast" if "axlast" in parts else "auto"}
 
 
 def _assert_same(got, want, what=""):
@@ -268,16 +267,15 @@ SEQ_CASES = ([("0", n) for n in (1, 70, 1000, 5000, 8192, 8193, 12289, 32768, 40
 
 @pytest.mark.parametrize("max_pods", [0, 1, 3])
 @pytest.mark.parametrize("seq_waves,n", SEQ_CASES)
-def test_sequential(msh, oracle, n, max_pods, seq_waves, monkeypatch):
+def test_sequential(msh, oracle, n, max_pods, seq_waves):
     """Sequential commit against the oracle's serial loop, node counts included; one scanning wave
-    up to 8,192 nodes, four up to 32,768, then 15 (+ finalizer) / 16 (MSH_SEQ_WAVES, read once by
-    msh_create, forces a count; one too small for the table is raised: the last case). Auto at every
+    up to 8,192 nodes, four up to 32,768, then 15 (+ finalizer) / 16 (msh_options.seq_waves, read once by
+    msh_create_ex, forces a count; one too small for the table is raised: the last case). Auto at every
     table size, each forced count at the sizes around its limits."""
-    monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)
     rng = np.random.default_rng(n + max_pods)
     ps = oracle.PluginSet()
     u, nd, pd, pt = _rand_case(rng, n, 3001)  # not a multiple of the 4 pods one wave decides per step
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, {"seq_waves": seq_waves}) as ctx:
         _set(ctx, msh, ps)
         ctx.upload_nodes(u, nd)
         got = ctx.schedule_sequential(pd, pt, max_pods)
@@ -291,19 +289,17 @@ def test_sequential(msh, oracle, n, max_pods, seq_waves, monkeypatch):
 
 @pytest.mark.parametrize("split", ["auto", "serial"])
 @pytest.mark.parametrize("seq_waves,n", [("1", 1000), ("4", 8193), ("16", 40000)])
-def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split, monkeypatch):
+def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split):
     """Without a capacity the sequential kernel splits the pods into blocks of consecutive pods, one
-    workgroup each (MSH_SEQ_SPLIT=auto, tables up to 32,768 nodes; the 40,000-node table stays in one
+    workgroup each (msh_options.seq_split auto, tables up to 32,768 nodes; the 40,000-node table stays in one
     workgroup), or walks them all in one workgroup (serial): both give the serial loop's placements and
     node counts, for batch sizes around the 64-pod block edges and with counts carried over between
     calls (the blocks add theirs with device atomics)."""
-    monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)
-    monkeypatch.setenv("MSH_SEQ_SPLIT", split)
     rng = np.random.default_rng(n + 77)
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, 3)
     p = 20_000 if n < 10_000 else 6_000  # (the oracle's serial loop is n x p)
     u, nd, pd, pt = _rand_case(rng, n, p, p_unsched=0.2, p_tol=0.1)
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, {"seq_waves": seq_waves, "seq_split": split}) as ctx:
         _set(ctx, msh, ps)
         ctx.upload_nodes(u, nd)
         cuts = [0, 1, 64, 65, 191, p // 2 - 1, p]
@@ -312,9 +308,8 @@ def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split, monkeypatch):
         _assert_same(tuple(np.concatenate(x) for x in zip(*parts)), (want_i, want_s, want_st),
                      f"seq blocks split={split} waves={seq_waves} n={n}")
         assert (ctx.node_pod_counts() == want_counts).all()
-    monkeypatch.setenv("MSH_SEQ_SPLIT", "blocks")
-    with pytest.raises(msh.MshError):
-        msh.DeviceContext(0)
+    with pytest.raises(msh.MshError, match="seq_split"):
+        msh.DeviceContext(0, {"seq_split": 7})
 
 
 def test_sequential_count_replicas(msh, oracle):
@@ -373,16 +368,15 @@ def test_sequential_pod_blocks_two_streams(msh, oracle):
 @pytest.mark.parametrize("seq_waves", ["1", "16"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("combo", range(len(PLUGIN_COMBOS)))
-def test_sequential_plugin_sets(msh, oracle, combo, norm, seq_waves, monkeypatch):
+def test_sequential_plugin_sets(msh, oracle, combo, norm, seq_waves):
     """Sequential commit for every plugin-list combination and normalize mode (the KX decode
     included), at 1 and 16 scanning waves (4 in test_sequential), with and without a capacity, on
     tables where whole pod classes have no feasible node (FitError) and pods without a digit (score
     error)."""
-    monkeypatch.setenv("MSH_SEQ_WAVES", seq_waves)
     rng = np.random.default_rng(500 + 10 * combo + norm)
     f, pre, sc = PLUGIN_COMBOS[combo]
     ps = _plugins(oracle, f, pre, sc, 3, norm)
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, {"seq_waves": seq_waves}) as ctx:
         _set(ctx, msh, ps)
         for n, p_unsched in ((300, 1.0), (300, 0.0), (2000, 0.5)):
             u, nd, pd, pt = _rand_case(rng, n, 1001, p_unsched=p_unsched, p_tol=0.3)
@@ -706,20 +700,19 @@ def test_maximum_node_table(msh, gpu_ctx, synth):
 
 @pytest.mark.parametrize("slices", ["1", "2", "4"])
 @pytest.mark.parametrize("n", [20_000, 70_000])
-def test_pair_slices(msh, oracle, n, slices, monkeypatch):
+def test_pair_slices(msh, oracle, n, slices):
     """Few pods against a large table: SLICES waves of pair_kernel share each 64-pod block, each
     scanning a range of 256-node groups, firsts merged by min in LDS. Every slice count
-    (MSH_BITS_SLICES, read once by msh_create) against the oracle, for the batch and the shard-key
+    (msh_options.pair_slices, read once by msh_create_ex) against the oracle, for the batch and the shard-key
     entry points, in the identity-like and the non-match (MINMAX) modes."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_BITS_SLICES", slices)
     rng = np.random.default_rng(n + int(slices))
     u, nd, pd, pt = _rand_case(rng, n, 1537, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4  # digit 3 only in the second half: late first matches
     dev = torch.device("cuda:0")
     d_pd, d_pt = torch.from_numpy(pd).to(dev), torch.from_numpy(pt).to(dev)
     p = len(pd)
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, {"pair_slices": slices}) as ctx:
         for norm in (0, 3):
             ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, norm)
             _set(ctx, msh, ps)
@@ -883,7 +876,7 @@ def test_multi_batch_launch(msh, gpu_ctx, oracle, norm, nb):
 
 
 @pytest.mark.parametrize("n,norm", [(5000, 0), (5000, 3), (8192, 1), (40_000, 2)])
-def test_multi_batch_full_launch(msh, oracle, n, norm, monkeypatch):
+def test_multi_batch_full_launch(msh, oracle, n, norm):
     """A full multi-batch launch (32 batches of ~100k pods, ragged, empty and one-pod batches among them)
     on the per-pair kernel with its planes staged in LDS (auto: the launch fills the chip; 4-wave
     workgroups up to 32,768 nodes, 16-wave ones above) and with scalar-loaded planes; every batch
@@ -899,8 +892,7 @@ def test_multi_batch_full_launch(msh, oracle, n, norm, monkeypatch):
     pods = [_rand_case(rng, 1, p)[2:] for p in sizes]
     wants = [oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=16) for pd, pt in pods]
     for planes in ("auto", "sgpr"):
-        monkeypatch.setenv("MSH_PAIR_PLANES", planes)
-        with msh.DeviceContext(0) as ctx:
+        with msh.DeviceContext(0, {"pair_planes": planes}) as ctx:
             _set(ctx, msh, ps)
             ctx.upload_nodes(u, nd)
             bufs = [_dev_batch(torch, dev, pd, pt, scores=(k % 5 != 4)) for k, (pd, pt) in enumerate(pods)]
@@ -916,22 +908,22 @@ def test_multi_batch_full_launch(msh, oracle, n, norm, monkeypatch):
 @pytest.mark.parametrize("noax", ["auto", "flip"])
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 @pytest.mark.parametrize("n", [7000, 40_000])
-def test_multi_batch_launch_lds(msh, oracle, n, norm, noax, monkeypatch):
-    """The LDS-staged pair kernel forced on small ragged multi-batch launches (MSH_PAIR_PLANES=lds): each
+def test_multi_batch_launch_lds(msh, oracle, n, norm, noax):
+    """The LDS-staged pair kernel forced on small ragged multi-batch launches (pair_planes lds): each
     built instance — 4-wave workgroups (7,000 nodes) and 16-wave ones (40,000), identity-like and
-    REVERSE / MINMAX — in every normalize mode, with group 0 scanned first and last (MSH_PAIR_NOAX auto
+    REVERSE / MINMAX — in every normalize mode, with group 0 scanned first and last (pair_noax auto
     and the other value); workgroups whose blocks end inside or before a batch, empty and one-pod batches,
     NULL scores."""
     torch = pytest.importorskip("torch")
     kx = norm in (2, 3)
-    _pair_env(monkeypatch, "lds" + ("" if noax == "auto" else ("-axlast" if kx else "-noax")))
+    opts = _pair_opts("lds" + ("" if noax == "auto" else ("-axlast" if kx else "-noax")))
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(99 * n + norm)
     sizes = [0, 1, 64, 65, 255, 257, 20_003, 5000, 333, 4096, 1, 2, 700, 64, 128, 1025, 999] * 2
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, norm)
     u, nd, _, _ = _rand_case(rng, n, 1)
     pods = [_rand_case(rng, 1, p)[2:] for p in sizes]
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, opts) as ctx:
         _set(ctx, msh, ps)
         ctx.upload_nodes(u, nd)
         bufs = [_dev_batch(torch, dev, pd, pt, scores=(k % 4 != 3)) for k, (pd, pt) in enumerate(pods)]
@@ -962,20 +954,20 @@ def test_multi_batch_invalid(msh, gpu_ctx):
 
 @pytest.mark.parametrize("planes", ["sgpr", "lds", "lds-noax", "lds-axlast"])
 @pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 32_768, 70_000, 106_496, 106_497])
-def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
+def test_pair_kernel_late_matches(msh, oracle, n, planes):
     """pair_kernel re-reads the first group with a hit from memory when it lies above the lowest group
     of the wave's range (kept in registers): digit 3 only in the second half of the table makes those
     pods' first matches late. Batch, multi-batch and shard-key entry points, NONE and MINMAX, on tables
     with and without a padded top group."""
     torch = pytest.importorskip("torch")
-    _pair_env(monkeypatch, planes)  # lds: 4-wave workgroups up to 32,768 nodes, 16-wave up to
+    opts = _pair_opts(planes)  # lds: 4-wave workgroups up to 32,768 nodes, 16-wave up to
     # 106,496 (106,497 falls back to scalar-loaded planes)
     rng = np.random.default_rng(n + 4)
     u, nd, pd, pt = _rand_case(rng, n, 3000, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4
     dev = torch.device("cuda:0")
     p = len(pd)
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, opts) as ctx:
         for norm in (0, 3):
             ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 1, norm)
             _set(ctx, msh, ps)
@@ -1002,15 +994,14 @@ def test_pair_kernel_late_matches(msh, oracle, n, planes, monkeypatch):
 @pytest.mark.parametrize("planes,slices", [("sgpr", 0), ("sgpr", 1), ("sgpr", 2), ("sgpr", 4), ("lds", 0),
                                            ("lds-noax", 0), ("lds-axlast", 0)])
 @pytest.mark.parametrize("n", [1000, 5000, 20_000])
-def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices, monkeypatch):
+def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices):
     """The identity-like modes take a pod's first feasible node from the scalar unit's per-group
     feasibility (V & ~X, V): with the first 60% of the table unschedulable and digit 7 only there,
     a non-tolerating pod of digit 7 has no feasible match and its first feasible node lies far above
     the lowest group of every slice; tolerating pods match early. NONE, DEFAULT, no NodeNumber score,
     MINMAX; batch and shard keys; every slice count."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_BITS_SLICES", str(slices))
-    _pair_env(monkeypatch, planes)  # "lds": the LDS-staged form at any launch size
+    opts = {**_pair_opts(planes), "pair_slices": slices}  # "lds": the LDS-staged form at any launch size
     rng = np.random.default_rng(n + slices)
     u, nd, pd, pt = _rand_case(rng, n, 2000, p_unsched=0.0, p_tol=0.2)
     cut = int(n * 0.6)
@@ -1020,7 +1011,7 @@ def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices, monkeypatch):
     dev = torch.device("cuda:0")
     p = len(pd)
     lists = [(["NodeNumber"], 1, 0), (["NodeNumber"], 2, 1), ([], 1, 0), (["NodeNumber"], 1, 3)]
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, opts) as ctx:
         for score, w, norm in lists:
             ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], score, w, norm)
             _set(ctx, msh, ps)
@@ -1039,16 +1030,15 @@ def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices, monkeypatch):
 
 
 @pytest.mark.parametrize("kernel", ["pair", "generic"])
-def test_batch_kernel_ab(msh, oracle, kernel, monkeypatch):
-    """The default per-pair kernel and generic_kernel (MSH_BATCH_KERNEL=generic, read once by msh_create:
-    explicit int64 totals for the reference list) place identically at C3 size, multi-batch included; the
-    retired class-row kernel's switch value is rejected at msh_create."""
+def test_batch_kernel_ab(msh, oracle, kernel):
+    """The default per-pair kernel and generic_kernel (msh_options.batch_kernel generic, read once by
+    msh_create_ex: explicit int64 totals for the reference list) place identically at C3 size, multi-batch
+    included; a value outside the field's set is rejected at msh_create_ex."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MSH_BATCH_KERNEL", kernel)
     rng = np.random.default_rng(5)
     u, nd, pd, pt = _rand_case(rng, 5000, 100_000, p_unsched=0.1, p_tol=0.05)
     dev = torch.device("cuda:0")
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, {"batch_kernel": kernel}) as ctx:
         ctx.upload_nodes(u, nd)
         want = oracle.c_schedule_batch(u, nd, pd, pt, threads=8)
         _assert_same(ctx.schedule_batch(pd, pt), want, kernel)
@@ -1058,9 +1048,8 @@ def test_batch_kernel_ab(msh, oracle, kernel, monkeypatch):
         torch.cuda.synchronize()
         for t in ts:
             _assert_same([t[i].cpu().numpy() for i in (2, 3, 4)], want, f"{kernel} multi")
-    monkeypatch.setenv("MSH_BATCH_KERNEL", "classrows")
-    with pytest.raises(msh.MshError):
-        msh.DeviceContext(0)
+    with pytest.raises(msh.MshError, match="batch_kernel"):
+        msh.DeviceContext(0, {"batch_kernel": 2})
 
 
 # ---- the generic score pipeline (score-column plugins; north_star stages 1-5 with explicit int64 scores)
@@ -1143,16 +1132,15 @@ def test_generic_small_totals(msh, gpu_ctx, oracle, lst):
 
 
 @pytest.mark.parametrize("lst", [0, 1, 3])
-def test_generic_nn_key_select(msh, oracle, lst, monkeypatch):
-    """MSH_GEN_NNKEY=select (read once by msh_create): NodeNumber's key by the compare and select instead of
+def test_generic_nn_key_select(msh, oracle, lst):
+    """msh_options.gen_nnkey select (read once by msh_create_ex): NodeNumber's key by the compare and select instead of
     the compare-free base + bit x delta, on the 32-bit lists, at C3 size and on a multi-tile table."""
-    monkeypatch.setenv("MSH_GEN_NNKEY", "select")
     rng = np.random.default_rng(900 + lst)
     pl = W32_LISTS[lst]
     names = [nm for nm, _, _ in pl]
     ps = oracle.PluginSet(filters=["NodeUnschedulable"], prescore=["NodeNumber"], score=names,
                           weights=[w for _, w, _ in pl], normalize=[m for _, _, m in pl])
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, {"gen_nnkey": "select"}) as ctx:
         ctx.set_plugins(ps.filters, ps.prescore, [msh.ScorePluginConfig(nm, w, msh.Normalize(m)) for nm, w, m in pl])
         for n, p in [(5000, 100_000), (33_000, 700)]:
             u, nd, pd, pt = _rand_case(rng, n, p, p_unsched=0.3, p_tol=0.2)
@@ -1162,19 +1150,17 @@ def test_generic_nn_key_select(msh, oracle, lst, monkeypatch):
                 ctx.upload_score_column(f"ScoreColumn{k}", cols[k])
             _assert_same(ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols, threads=8),
                          f"select {pl} n={n} p={p}")
-    monkeypatch.setenv("MSH_GEN_NNKEY", "bfe")
-    with pytest.raises(msh.MshError):
-        msh.DeviceContext(0)
+    with pytest.raises(msh.MshError, match="gen_nnkey"):
+        msh.DeviceContext(0, {"gen_nnkey": 2})
 
 
-@pytest.mark.parametrize("f53", ["1", "0"])
-def test_generic_f53_bounds(msh, oracle, f53, monkeypatch):
-    """8-byte keys as doubles (MSH_GEN_F53=1, the default) when the host bounds the totals below 2^53, else
+@pytest.mark.parametrize("f53", ["f53", "u64"])
+def test_generic_f53_bounds(msh, oracle, f53):
+    """8-byte keys as doubles (msh_options.gen_keys auto, the default) when the host bounds the totals below 2^53, else
     uint64_t keys: a column over the whole int32 range at weight 2^21 (bound 2^52: doubles) and 2^22 (2^53:
     uint64_t), with NodeNumber DEFAULT and a DEFAULT column beside it; two normalizing columns (the general
     form) below and past the bound; on one- and multi-tile tables; and the same lists on the uint64_t keys
-    throughout (MSH_GEN_F53=0)."""
-    monkeypatch.setenv("MSH_GEN_F53", f53)
+    throughout (gen_keys u64)."""
     rng = np.random.default_rng(53)
     lists = [[("ScoreColumn0", 1 << 21, 0), ("NodeNumber", 1, 1)],
              [("ScoreColumn0", 1 << 22, 0), ("NodeNumber", 3, 0)],
@@ -1183,7 +1169,7 @@ def test_generic_f53_bounds(msh, oracle, f53, monkeypatch):
              # two normalizing columns (the general form): below and past the 2^53 bound
              [("ScoreColumn0", 3, 1), ("ScoreColumn1", 2, 3), ("NodeNumber", 1, 2)],
              [("ScoreColumn1", 1 << 31, 1), ("NodeNumber", 5, 0), ("ScoreColumn0", 1, 2)]]
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, {"gen_keys": f53}) as ctx:
         for pl in lists:
             names = [nm for nm, _, _ in pl]
             pre = ["NodeNumber"] if "NodeNumber" in names else []
@@ -1199,9 +1185,8 @@ def test_generic_f53_bounds(msh, oracle, f53, monkeypatch):
                     ctx.upload_score_column(f"ScoreColumn{k}", cols[k])
                 _assert_same(ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols, threads=8),
                              f"f53={f53} {pl} n={n}")
-    monkeypatch.setenv("MSH_GEN_F53", "2")
-    with pytest.raises(msh.MshError):
-        msh.DeviceContext(0)
+    with pytest.raises(msh.MshError, match="gen_keys"):
+        msh.DeviceContext(0, {"gen_keys": 2})
 
 
 def test_generic_int64_min_totals(msh, gpu_ctx, oracle):
@@ -1275,16 +1260,15 @@ def test_generic_pipeline_entry_points_and_errors(msh, oracle):
 
 @pytest.mark.parametrize("combo", range(len(PLUGIN_COMBOS)))
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
-def test_generic_kernel_cross_checks_bitmap_kernel(msh, oracle, combo, norm, monkeypatch):
-    """MSH_BATCH_KERNEL=generic runs the reference plugin lists on generic_kernel too (explicit
+def test_generic_kernel_cross_checks_bitmap_kernel(msh, oracle, combo, norm):
+    """msh_options.batch_kernel generic runs the reference plugin lists on generic_kernel too (explicit
     int64 scores, real NormalizeScore over the feasible list) instead of the bitmap kernel's closed
     forms: both place identically, and both equal the oracle (BASELINE C2 size, weight 3)."""
-    monkeypatch.setenv("MSH_BATCH_KERNEL", "generic")
     rng = np.random.default_rng(500 + 10 * combo + norm)
     f, pre, s = PLUGIN_COMBOS[combo]
     ps = _plugins(oracle, f, pre, s, 3, norm)
     u, nd, pd, pt = _rand_case(rng, 1000, 10_000, p_unsched=0.3, p_tol=0.1)
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, {"batch_kernel": "generic"}) as ctx:
         _set(ctx, msh, ps)
         ctx.upload_nodes(u, nd)
         _assert_same(ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=8),
@@ -1298,19 +1282,18 @@ def _c3_cols(n):
 
 
 @pytest.mark.parametrize("kernel", ["pair", "pair-sgpr", "generic"])
-def test_c3_reference_list_vs_oracle(msh, oracle, synth, kernel, monkeypatch):
+def test_c3_reference_list_vs_oracle(msh, oracle, synth, kernel):
     """5,000 nodes x 100,000 pods (BASELINE C3, the headline workload), the reference plugin list,
     weight 1, no normalizer, through the batch and the 32-batch entry points of the per-pair kernel
-    (pair_kernel, the headline) and of generic_kernel (explicit int64 scores, MSH_BATCH_KERNEL=generic):
+    (pair_kernel, the headline) and of generic_kernel (explicit int64 scores, batch_kernel generic):
     bit-exact vs oracle.c_schedule_batch (the restatement of minisched.go:115-199,304-325)."""
     torch = pytest.importorskip("torch")
-    _pair_env(monkeypatch, kernel.split("-")[1] if "-" in kernel else "auto")
+    opts = {**_pair_opts(kernel.split("-")[1] if "-" in kernel else "auto"), "batch_kernel": kernel.split("-")[0]}
     kernel = kernel.split("-")[0]
-    monkeypatch.setenv("MSH_BATCH_KERNEL", kernel)
     u, nd, pd, pt = synth.make_soa(5000, 100_000)
     want = oracle.c_schedule_batch(u, nd, pd, pt, oracle.PluginSet(), threads=16)
     dev = torch.device("cuda:0")
-    with msh.DeviceContext(0) as ctx:
+    with msh.DeviceContext(0, opts) as ctx:
         ctx.upload_nodes(u, nd)
         _assert_same(ctx.schedule_batch(pd, pt), want, f"C3 {kernel}")
         # 12 batches: enough waves for the launcher's LDS-staged pair kernel (bench.py's 32-batch launch)
@@ -1336,3 +1319,34 @@ def test_c3_score_column_vs_oracle(msh, gpu_ctx, oracle, synth, norm, weight):
     gpu_ctx.upload_score_column("ScoreColumn0", cols[0])
     _assert_same(gpu_ctx.schedule_batch(pd, pt), want, f"C3 column norm={norm} w={weight}")
     gpu_ctx.set_plugins(["NodeUnschedulable"], ["NodeNumber"], [msh.ScorePluginConfig("NodeNumber")])
+
+
+# ---- the exact headline launch of bench.py, against the oracle (verdict r5, next #2) ----
+@pytest.mark.parametrize("weight,norm", [(3, 1), (3, 3), (3, 2), (1, 0)],
+                         ids=["headline-w3-default", "w3-minmax", "w3-reverse", "reference-w1"])
+def test_headline_launch_vs_oracle(msh, oracle, synth, weight, norm):
+    """bench.py's timed step at N = 1, reproduced: the C3 snapshot (synth.make_nodes(5000)), 32 distinct
+    100,000-pod batches cut from one synthetic pod stream exactly as bench.py cuts them for rank 0, all
+    32 in ONE msh_schedule_batches_device call (the launch shape that selects
+    pair_lds_kernel<false, false, 4> for the identity-like modes and <false, true, 4> for REVERSE /
+    MINMAX); every batch's idx / score / status bit-exact vs oracle.c_schedule_batch over the whole table
+    (minisched.go:115-199, 304-325). The headline list (NodeNumber w=3 DefaultNormalizeScore), the two
+    other normalizers bench.py times beside it, and the reference's own w=1 list."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    G, p = msh._native.BATCHES_PER_LAUNCH, 100_000
+    u, nd = synth.make_nodes(5000)[1:]
+    pd_all, pt_all = synth._make_pods_fast(p * G, synth.SEED)[1:]
+    pods = [(np.ascontiguousarray(pd_all[i * p:(i + 1) * p]), np.ascontiguousarray(pt_all[i * p:(i + 1) * p]))
+            for i in range(G)]
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], weight, norm)
+    with msh.DeviceContext(0) as ctx:
+        _set(ctx, msh, ps)
+        ctx.upload_nodes(u, nd)
+        bufs = [_dev_batch(torch, dev, pd, pt) for pd, pt in pods]
+        ctx.schedule_batches_device(ctx.batch_descs([_desc(t) for t in bufs]),
+                                    stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = [[t[i].cpu().numpy() for i in (2, 3, 4)] for t in bufs]
+    for k, (pd, pt) in enumerate(pods):
+        _assert_same(got[k], oracle.c_schedule_batch(u, nd, pd, pt, ps, threads=16), f"headline batch {k} w={weight} norm={norm}")
