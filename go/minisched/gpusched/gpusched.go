@@ -509,6 +509,176 @@ func (x *Ctx) ScheduleSequential(pods []*v1.Pod, b *HostBatch, maxPodsPerNode in
 	return x.results(b), nil
 }
 
+// ---- node sharding (ABI v8): the node table split over GPUs, the cross-shard merge inside the library ----
+//
+// The reference's selectHost keeps the first maximum of the whole List-order node list
+// (minisched.go:304-325). Split into contiguous slices, each shard finds its own first maximum per pod,
+// and the library merges them back into the global one: in one process over several devices (Group), or
+// one process per GPU over an RCCL communicator (Ctx.InitComm + ScheduleNodeShard).
+
+// sortedNodes is the List order of nodes (byte-sorted names, the apiserver's etcd key order).
+func sortedNodes(nodes []v1.Node) []*v1.Node {
+	sorted := make([]*v1.Node, len(nodes))
+	for i := range nodes {
+		sorted[i] = &nodes[i]
+	}
+	sort.Slice(sorted, func(a, b int) bool { return sorted[a].Name < sorted[b].Name })
+	return sorted
+}
+
+// shardRange is the contiguous slice [lo, hi) of n List positions that shard k of w holds.
+func shardRange(n, w, k int) (int, int) { return n * k / w, n * (k + 1) / w }
+
+// uploadSlice uploads List positions [lo, hi) of sorted as x's table.
+func (x *Ctx) uploadSlice(sorted []*v1.Node, lo, hi int) error {
+	uns := make([]C.uint8_t, hi-lo)
+	dig := make([]C.int8_t, hi-lo)
+	for i, n := range sorted[lo:hi] {
+		if n.Spec.Unschedulable {
+			uns[i] = 1
+		}
+		dig[i] = C.int8_t(suffixDigit(n.Name))
+	}
+	if rc := C.msh_upload_nodes(x.c, C.int32_t(hi-lo), ptrU8(uns), ptrI8(dig)); rc != C.MSH_OK {
+		return x.lastErr("msh_upload_nodes", rc)
+	}
+	x.hasNodes = true
+	return nil
+}
+
+// Group is one scheduler process driving several GPUs (msh_group_*): shard k (a Ctx on devices[k])
+// holds the k-th contiguous slice of the List order; msh_group_schedule_batch runs every shard's kernel
+// on its own device and merges on devices[0], reading the shards' per-pod results over xGMI.
+type Group struct {
+	g       *C.msh_group
+	shards  []*Ctx
+	byIndex []*v1.Node // global List order
+}
+
+// NewGroup creates one shard Ctx per device (the same plugin lists on each) and the group over them.
+func NewGroup(devices []int, filters []framework.FilterPlugin, preScores []framework.PreScorePlugin,
+	scores []ScoreConfig) (*Group, error) {
+	if len(devices) < 1 || len(devices) > C.MSH_GROUP_MAX_SHARDS {
+		return nil, fmt.Errorf("gpusched: 1..%d devices", int(C.MSH_GROUP_MAX_SHARDS))
+	}
+	gr := &Group{}
+	for _, d := range devices {
+		x, err := New(d, filters, preScores, scores)
+		if err != nil {
+			gr.Close()
+			return nil, err
+		}
+		gr.shards = append(gr.shards, x)
+	}
+	cs := make([]*C.msh_ctx, len(gr.shards)) // C memory holds no Go pointer: the handles are C pointers
+	for k, x := range gr.shards {
+		cs[k] = x.c
+	}
+	if rc := C.msh_group_create(&cs[0], C.int32_t(len(cs)), &gr.g); rc != C.MSH_OK {
+		err := fmt.Errorf("msh_group_create: %d: %s", int(rc), C.GoString(C.msh_group_last_error(nil)))
+		gr.Close()
+		return nil, err
+	}
+	runtime.SetFinalizer(gr, (*Group).Close)
+	return gr, nil
+}
+
+// Close releases the group, then its shard contexts.
+func (gr *Group) Close() {
+	if gr.g != nil {
+		C.msh_group_destroy(gr.g)
+		gr.g = nil
+	}
+	for _, x := range gr.shards {
+		x.Close()
+	}
+	gr.shards = nil
+	runtime.SetFinalizer(gr, nil)
+}
+
+// UploadNodes puts the nodes in List order and uploads slice k to shard k (replacing minisched.go:40).
+func (gr *Group) UploadNodes(nodes []v1.Node) error {
+	sorted := sortedNodes(nodes)
+	for k, x := range gr.shards {
+		lo, hi := shardRange(len(sorted), len(gr.shards), k)
+		if err := x.uploadSlice(sorted, lo, hi); err != nil {
+			return err
+		}
+	}
+	gr.byIndex = sorted
+	return nil
+}
+
+// ScheduleBatch runs minisched.go:50-87 for every pod against the whole (sharded) table, synchronously.
+func (gr *Group) ScheduleBatch(pods []*v1.Pod, b *HostBatch) ([]Result, error) {
+	if gr.byIndex == nil {
+		return nil, errors.New("gpusched: UploadNodes has not been called")
+	}
+	x := &Ctx{byIndex: gr.byIndex} // packing and decoding against the global List order
+	if err := x.pack(b, pods); err != nil {
+		return nil, err
+	}
+	p := len(pods)
+	if rc := C.msh_group_schedule_batch(gr.g, C.int32_t(p), ptrI8(b.pd[:p]), ptrU8(b.pt[:p]), ptrI32(b.idx[:p]),
+		ptrI64(b.score[:p]), ptrI32(b.status[:p])); rc != C.MSH_OK {
+		return nil, fmt.Errorf("msh_group_schedule_batch: %d: %s", int(rc), C.GoString(C.msh_group_last_error(gr.g)))
+	}
+	return x.results(b), nil
+}
+
+// CommID makes the id of a new RCCL communicator (msh_comm_unique_id): rank 0 calls it and ships the
+// bytes to every rank (over the scheduler's own channel).
+func CommID() ([]byte, error) {
+	buf := make([]byte, C.MSH_COMM_ID_BYTES)
+	if rc := C.msh_comm_unique_id((*C.uint8_t)(unsafe.Pointer(&buf[0]))); rc != C.MSH_OK {
+		return nil, fmt.Errorf("msh_comm_unique_id: %d", int(rc))
+	}
+	return buf, nil
+}
+
+// InitComm joins x to the communicator `id` as rank `rank` of `world` (one process per GPU); it returns
+// once every rank has joined.
+func (x *Ctx) InitComm(id []byte, world, rank int) error {
+	if len(id) != C.MSH_COMM_ID_BYTES {
+		return fmt.Errorf("gpusched: a comm id is %d bytes", int(C.MSH_COMM_ID_BYTES))
+	}
+	cid := C.CBytes(id) // C memory: the library reads it during the call
+	defer C.free(cid)
+	if rc := C.msh_comm_init(x.c, (*C.uint8_t)(cid), C.int32_t(world), C.int32_t(rank)); rc != C.MSH_OK {
+		return x.lastErr("msh_comm_init", rc)
+	}
+	return nil
+}
+
+// UploadNodeShard keeps the whole List order for decoding (every rank's informer holds every node) and
+// uploads this rank's slice; it returns the slice's global base for ScheduleNodeShard.
+func (x *Ctx) UploadNodeShard(nodes []v1.Node, world, rank int) (int64, error) {
+	sorted := sortedNodes(nodes)
+	lo, hi := shardRange(len(sorted), world, rank)
+	if err := x.uploadSlice(sorted, lo, hi); err != nil {
+		return 0, err
+	}
+	x.byIndex = sorted
+	return int64(lo), nil
+}
+
+// ScheduleNodeShard is ScheduleBatch over the table split across the communicator's ranks
+// (msh_schedule_nodeshard): every rank calls it with the same pods and gets every pod's decision.
+func (x *Ctx) ScheduleNodeShard(pods []*v1.Pod, b *HostBatch, nodeBase int64) ([]Result, error) {
+	if !x.hasNodes {
+		return nil, errors.New("gpusched: UploadNodeShard has not been called")
+	}
+	if err := x.pack(b, pods); err != nil {
+		return nil, err
+	}
+	p := len(pods)
+	if rc := C.msh_schedule_nodeshard(x.c, C.int32_t(p), ptrI8(b.pd[:p]), ptrU8(b.pt[:p]), C.int64_t(nodeBase),
+		ptrI32(b.idx[:p]), ptrI64(b.score[:p]), ptrI32(b.status[:p])); rc != C.MSH_OK {
+		return nil, x.lastErr("msh_schedule_nodeshard", rc)
+	}
+	return x.results(b), nil
+}
+
 // suffixDigit is strconv.Atoi(name[len(name)-1:]) (nodenumber.go:51-56, :81-87): only '0'..'9' parse.
 func suffixDigit(name string) int {
 	if name == "" {

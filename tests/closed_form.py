@@ -135,3 +135,46 @@ def direct_plugins(unsched, node_digit, pod_digit, pod_tol, plugins, cols=None, 
             b = int(np.argmax(tot))  # the first maximum
             idx[j], score[j] = f[b], tot[b]
     return idx, score, status
+
+
+def closed_form_capacity(unsched, node_digit, pod_digit, pod_tol, weight: int = 1, cap: int = 0, counts=None):
+    """The reference plugin set (NONE, weight w) in sequential-commit order with a capacity: a node that
+    holds `cap` pods is infeasible for every later pod (the build's capacity filter). Per pod, in order:
+    the first feasible non-full node whose digit matches, else the first feasible non-full node; FitError
+    when every feasible node is full (or none is feasible); the NodeNumber score error for a pod without
+    a digit. Each (tolerates, digit) list and each tolerates list keeps a pointer to its first non-full
+    node, which only moves forward (counts only grow): O(P + N) overall, not the oracle's O(P x N) loop.
+    Returns (idx, score, status, counts)."""
+    unsched = np.asarray(unsched, bool)
+    node_digit = np.asarray(node_digit, np.int16)
+    pod_digit, pod_tol = np.asarray(pod_digit), np.asarray(pod_tol)
+    n, p = len(unsched), len(pod_digit)
+    counts = np.zeros(n, np.int64) if counts is None else np.array(counts, np.int64)
+    feas = {0: np.flatnonzero(~unsched), 1: np.arange(n)}
+    match = {(t, d): f[node_digit[f] == d] for t, f in feas.items() for d in range(10)}
+    ptr = {}
+    idx = np.full(p, -1, np.int32)
+    score = np.zeros(p, np.int64)
+    status = np.zeros(p, np.int32)
+    full = (lambda i: counts[i] >= cap) if cap > 0 else (lambda i: False)
+
+    def first(key, lst):
+        k = ptr.get(key, 0)
+        while k < len(lst) and full(lst[k]):
+            k += 1
+        ptr[key] = k
+        return int(lst[k]) if k < len(lst) else -1
+
+    for j in range(p):
+        t, d = int(pod_tol[j] != 0), int(pod_digit[j])
+        ia = first(("f", t), feas[t])
+        if ia < 0:
+            status[j] = 1
+            continue
+        if not 0 <= d <= 9:
+            status[j] = 2
+            continue
+        im = first(("m", t, d), match[(t, d)])
+        idx[j], score[j] = (im, 10 * weight) if im >= 0 else (ia, 0)
+        counts[idx[j]] += 1
+    return idx, score, status, counts.astype(np.int32)

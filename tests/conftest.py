@@ -49,7 +49,9 @@ def pytest_terminal_summary(terminalreporter):
     if not _BUILT:
         return
     prov = _BUILT.get("provenance") or {}
-    fresh = bool(prov) and prov.get("built_at") and _BUILT["forced"]
+    if not prov:
+        return  # a CPU session on a library built earlier, with no record
+    fresh = bool(prov.get("built_at")) and _BUILT["forced"]
     terminalreporter.write_line(
         "[build provenance] " + ("rebuilt from source in this session: " if fresh else "prebuilt library: ")
         + ", ".join(f"{k}={prov.get(k)}" for k in ("host", "hipcc", "seconds", "sources_sha256", "lib_sha256")))

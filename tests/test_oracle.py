@@ -140,3 +140,23 @@ def test_score_columns_both_restatements(oracle, seed):
             assert [r.index for r in res] == ci.tolist(), (modes, weights)
             assert [r.score for r in res] == cs.tolist(), (modes, weights)
             assert [r.status for r in res] == cst.tolist(), (modes, weights)
+
+
+def test_capacity_closed_form_matches_oracle_serial_loop():
+    """tests/closed_form.closed_form_capacity (bench.py's checker of the capacity form of C5) against the
+    oracle's serial loop (oracle_schedule_sequential: minisched.go:28-30 with the capacity filter) on
+    random tables with unschedulable nodes, digit-less names and tolerating pods, counts included."""
+    import importlib
+    import numpy as np
+    from closed_form import closed_form_capacity
+    importlib.import_module("oracle.build").build_oracle()
+    O = importlib.import_module("oracle.oracle")
+    rng = np.random.default_rng(15)
+    for n, p, cap in [(1, 10, 1), (300, 4000, 3), (1000, 20_000, 7), (50, 3000, 2), (2000, 5000, 0), (64, 64, 64)]:
+        u = (rng.random(n) < 0.3).astype(np.uint8)
+        nd = rng.integers(-1, 10, n).astype(np.int8)
+        pd = rng.integers(-1, 10, p).astype(np.int8)
+        pt = (rng.random(p) < 0.2).astype(np.uint8)
+        got = closed_form_capacity(u, nd, pd, pt, 1, cap)
+        want = O.c_schedule_sequential(u, nd, pd, pt, O.PluginSet(), cap)
+        assert all((g == w).all() for g, w in zip(got, want)), (n, p, cap)
