@@ -506,7 +506,7 @@ def valu_roofline(kname, launch_ms, evals, model_lane_ops_per_eval, cus, entry, 
     }
 
 
-def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=False):
+def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=False, cap=0):
     """Roofline of the dominant kernel, per launch: algorithmic work of one launch / the launch's
     average duration, measured with HIP events at the kernel's start and completion (bench.py main),
     the quantity rocprofv3's per-kernel average reports."""
@@ -530,8 +530,8 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=F
         # of the per-pod latency is its instruction count (VALU + SALU, counted by rocprofv3 for
         # this kernel at C5) x 4 cycles at 2.4 GHz. That is an issue floor of the code as written,
         # not a hardware roofline: reported as issue_floor_frac, not frac.
-        kname = seq_kernel_label(n_local)
-        entry = pmc_entry("sequential_serial", kname, n_local, p, 1)
+        kname = seq_kernel_label(n_local, cap=cap > 0)
+        entry = pmc_entry("sequential_capacity" if cap else "sequential_serial", kname, n_local, p, 1)
         instr = (entry.get("SQ_INSTS_VALU", 0) + entry.get("SQ_INSTS_SALU", 0)) / p if entry else None
         floor_us = instr * 4 / 2.4e3 if instr else None
         achieved = launch_ms * 1e3 / p
@@ -878,6 +878,41 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
                     "check": (f"seq == batch (closed form), node counts == {R} x placements" if ok else "MISMATCH"),
                     "roofline": make_roofline("sequential", n, p, ms, 1, cus, serial=serial)}
         c.close()
+
+    # ---- C5 with a capacity (15 pods per node, the reference list): the one sequential form in which a
+    # commit changes a later decision (a node that fills becomes infeasible), so one workgroup walks all
+    # 100,000 pods in order; the counts are reset before each launch (each sees the same empty cluster) ----
+    from closed_form import closed_form_capacity
+    CAP = 15
+    cc = new_ctx()
+    cc.set_plugins([msh.NODE_UNSCHEDULABLE], [msh.NODE_NUMBER], [msh.ScorePluginConfig(msh.NODE_NUMBER, 1)])
+    cc.upload_nodes(u, nd)
+    seqc = lambda: cc.schedule_sequential_device(p, b[0].data_ptr(), b[1].data_ptr(), CAP,
+                                                 *[t.data_ptr() for t in b[2:]], sh)
+    cc.reset_node_pod_counts()
+    seqc()
+    torch.cuda.synchronize()
+    R, tot = 3, 0.0
+    for _ in range(R):
+        cc.reset_node_pod_counts()
+        cc.timing_begin(1)
+        seqc()
+        n_t, t_ms, _ = cc.timing_end()
+        tot += t_ms / max(n_t, 1)
+    ms = tot / R
+    wi, ws, wst, wcounts = closed_form_capacity(u, nd, pd, pt, 1, CAP)
+    ok = same(got(b), (wi, ws, wst)) and (cc.node_pod_counts() == wcounts).all() and wcounts.max() == CAP
+    rl = make_roofline("sequential", n, p, ms, 1, cus, serial=True, cap=CAP)
+    out["c5_sequential_capacity"] = {
+        "kernel": seq_kernel_label(n, cap=True), "plugins": "score=[NodeNumber w=1] (the reference list)",
+        "max_pods_per_node": CAP, "ms_per_step": ms, "us_per_pod": ms * 1e3 / p, "pods_per_s": p / (ms * 1e-3),
+        "evals_per_s": n * p / (ms * 1e-3),
+        "form": "one workgroup walks all 100,000 pods in order; a commit that fills a node makes it infeasible "
+                "for the next pod",
+        "check": (f"bit-exact vs an independent serial capacity simulation (tests/closed_form.py), node counts "
+                  f"equal, fullest node = {CAP}" if ok else "MISMATCH"),
+        "roofline": rl}
+    cc.close()
 
     # ---- f2: node-table maintenance (an informer Update / Add, eventhandler.go:37-57, replacing the
     # per-cycle LIST of minisched.go:40), host wall time of the synchronous call, median of 50 ----

@@ -12,9 +12,11 @@ MODE
   generic_2col generic_kernel's general form: NodeNumber + a DEFAULT and a MIN-MAX column, 32 batches per launch
   generic_w64  generic_kernel's 64-bit form: NodeNumber + ScoreColumn0 over the whole int32 range (COLNORM:
                the column's normalizer), 32 batches per launch
-  sequential   C5: each pod in order (seq_kernel; MSH_SEQ_SPLIT=serial: the whole batch in one workgroup)
+  sequential   C5: each pod in order (seq_kernel; SPLIT=serial: the whole batch in one workgroup; CAP=k: a
+               capacity of k pods per node, the counts reset before every launch)
 NORM / WEIGHT: msh_normalize and weight of the NodeNumber entry (bench.py's headline: WEIGHT=3 NORM=1).
-NB: batches per launch in the multi-batch modes (default 32)."""
+NB: batches per launch in the multi-batch modes (default 32).
+Kernel overrides go to msh_create_ex as msh_options (the library reads no environment variable)."""
 import importlib
 import os
 import sys
@@ -23,8 +25,12 @@ from pathlib import Path
 import numpy as np
 
 mode = os.environ.get("MODE", "multi")
+options = {}
 if mode == "generic":
-    os.environ["MSH_BATCH_KERNEL"] = "generic"  # read by msh_create
+    options["batch_kernel"] = "generic"
+if os.environ.get("SPLIT", "auto") == "serial":
+    options["seq_split"] = "serial"
+cap = int(os.environ.get("CAP", 0))
 
 import torch  # noqa: E402
 
@@ -37,7 +43,7 @@ p = int(os.environ.get("PODS", 100000))
 k = int(os.environ.get("LAUNCHES", 20))
 norm = int(os.environ.get("NORM", 0))
 weight = int(os.environ.get("WEIGHT", 1))
-ctx = msh.DeviceContext(0)
+ctx = msh.DeviceContext(0, options or None)
 u, nd, pd, pt = synth.make_soa(n, p)
 ctx.upload_nodes(u, nd)
 if mode == "generic_col":
@@ -76,6 +82,8 @@ for _ in range(k):
     elif mode == "batch":
         ctx.schedule_batch_device(p, *[t.data_ptr() for t in b], s)
     else:
-        ctx.schedule_sequential_device(p, b[0].data_ptr(), b[1].data_ptr(), 0, *[t.data_ptr() for t in b[2:]], s)
+        if cap:
+            ctx.reset_node_pod_counts()
+        ctx.schedule_sequential_device(p, b[0].data_ptr(), b[1].data_ptr(), cap, *[t.data_ptr() for t in b[2:]], s)
 torch.cuda.synchronize()
 print("ok", n, p, k, mode, nb, os.environ.get("MSH_BATCH_KERNEL", "pair"), f"NodeNumber w={weight} norm={norm}")
