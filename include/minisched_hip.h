@@ -130,6 +130,7 @@ typedef struct msh_options {
   int32_t pair_slices;  /* 0 auto | 1, 2, 4 slice waves per 64-pod block (and generic_kernel pod group) */
   int32_t seq_waves;    /* 0 auto | 1, 4, 15, 16 scanning waves of the sequential kernel (raised when too few) */
   int32_t seq_split;    /* 0 auto (no capacity: 64-pod blocks) | 1 one workgroup walks the whole batch */
+  int32_t seq_pod_waves; /* 0 auto | 1, 2, 4, 8 waves sharing a 64-pod block (one scanning wave, no capacity) */
   int32_t gen_keys;     /* 0 auto (64-bit totals below 2^53 as double keys) | 1 uint64 keys */
   int32_t gen_nnkey;    /* 0 auto (compare-free NodeNumber key) | 1 compare + select */
 } msh_options;

@@ -87,7 +87,8 @@ class Options(C.Structure):
     """msh_options (ABI v8): kernel-selection overrides for msh_create_ex, 0 = automatic."""
     _fields_ = [("struct_size", C.c_int32), ("batch_kernel", C.c_int32), ("pair_planes", C.c_int32),
                 ("pair_noax", C.c_int32), ("pair_slices", C.c_int32), ("seq_waves", C.c_int32),
-                ("seq_split", C.c_int32), ("gen_keys", C.c_int32), ("gen_nnkey", C.c_int32)]
+                ("seq_split", C.c_int32), ("seq_pod_waves", C.c_int32), ("gen_keys", C.c_int32),
+                ("gen_nnkey", C.c_int32)]
 
 
 # Named values of the msh_options fields (an int passes through unchanged, for the library to check).
@@ -98,6 +99,7 @@ OPTION_NAMES = {
     "pair_slices": {"auto": 0},
     "seq_waves": {"auto": 0},
     "seq_split": {"auto": 0, "serial": 1},
+    "seq_pod_waves": {"auto": 0},
     "gen_keys": {"auto": 0, "f53": 0, "u64": 1},
     "gen_nnkey": {"auto": 0, "select": 1},
 }

@@ -31,12 +31,13 @@ SOURCES = [
     ("msh_pair.hip", "hipcc", ["-x", "hip"]),
     ("msh_generic.hip", "hipcc", ["-x", "hip"]),
     ("msh_seq.hip", "hipcc", ["-x", "hip"]),
+    ("msh_seq_cap.hip", "hipcc", ["-x", "hip"]),
     ("msh_prep.hip", "hipcc", ["-x", "hip"]),
     ("msh_capi.cpp", "hipcc", []),
     ("msh_shard.cpp", "hipcc", []),
     ("msh_pack.cpp", "g++", []),
 ]
-HEADERS = [CSRC / "msh_internal.h", CSRC / "msh_device.h", CSRC / "msh_pool.h", CSRC / "msh_ctx.h",
+HEADERS = [CSRC / "msh_internal.h", CSRC / "msh_device.h", CSRC / "msh_pool.h", CSRC / "msh_ctx.h", CSRC / "msh_seq_kernel.h",
            INCLUDE / "minisched_hip.h"]
 
 

@@ -602,6 +602,7 @@ bool apply_options(const msh_options& o, msh::DeviceInfo& d, std::string* err) {
   if (!in("batch_kernel", o.batch_kernel, {0, 1}) || !in("pair_planes", o.pair_planes, {0, 1, 2}) ||
       !in("pair_noax", o.pair_noax, {0, 1, 2}) || !in("pair_slices", o.pair_slices, {0, 1, 2, 4}) ||
       !in("seq_waves", o.seq_waves, {0, 1, 4, 15, 16}) || !in("seq_split", o.seq_split, {0, 1}) ||
+      !in("seq_pod_waves", o.seq_pod_waves, {0, 1, 2, 4, 8}) ||
       !in("gen_keys", o.gen_keys, {0, 1}) || !in("gen_nnkey", o.gen_nnkey, {0, 1}))
     return false;
   d.batch_kernel = o.batch_kernel;
@@ -610,6 +611,7 @@ bool apply_options(const msh_options& o, msh::DeviceInfo& d, std::string* err) {
   d.bits_slices = o.pair_slices;
   d.seq_waves = o.seq_waves;
   d.seq_split = o.seq_split == 0 ? 1 : 0;
+  d.seq_pod_waves = o.seq_pod_waves;
   d.gen_f53 = o.gen_keys == 0 ? 1 : 0;
   d.gen_nnkey = o.gen_nnkey == 0 ? 1 : 0;
   return true;

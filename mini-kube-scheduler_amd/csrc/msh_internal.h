@@ -53,6 +53,7 @@ struct DeviceInfo {
   // msh_options.seq_split: without a capacity, the sequential kernel's pods in blocks of consecutive
   // pods, one workgroup each (auto, 1), or all in one workgroup (serial, 0)
   int seq_split = 1;
+  int seq_pod_waves = 0;  // msh_options.seq_pod_waves: pod waves per pod-block workgroup (1, 2, 4, 8), 0 = auto
   int gen_f53 = 1;    // msh_options.gen_keys: generic_kernel's double keys for 64-bit totals below 2^53 (1) or uint64_t (0)
   int gen_nnkey = 1;  // msh_options.gen_nnkey: generic_kernel's compare-free NodeNumber key (1) or the select (0)
 };
@@ -235,6 +236,11 @@ int32_t seq_blocks(const SeqArgs& a, const DeviceInfo& dev);
 hipError_t launch_count_fold(int32_t* counts, int64_t stride, int32_t replicas, int32_t n, hipStream_t s);
 
 hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_t s, std::string* err);
+// The capacity form (msh_seq_cap.hip): nw scanning waves with rs words per lane, one workgroup.
+hipError_t launch_seq_capacity(const SeqArgs& a, int nw, int rs, hipStream_t s);
+// Pod waves per pod-block workgroup without a capacity (one scanning wave): each walks 64 / this many pods.
+constexpr int SEQ_POD_WAVES = 4;
+int seq_pod_waves(const DeviceInfo& dev);
 
 // Launch timing (msh_timing_begin / _end): the next hot-kernel launch on this thread (batch, multi-
 // batch, generic, sequential kernels) records `start` / `stop` at the kernel's own start and end.

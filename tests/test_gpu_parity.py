@@ -312,6 +312,28 @@ def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split):
         msh.DeviceContext(0, {"seq_split": 7})
 
 
+@pytest.mark.parametrize("pod_waves", [1, 2, 4, 8])
+@pytest.mark.parametrize("norm", [0, 1, 3])
+def test_sequential_pod_waves(msh, oracle, pod_waves, norm):
+    """Pod-block workgroups of the one-scanning-wave form (tables up to 8,192 nodes, no capacity) shared by
+    1, 2, 4 or 8 pod waves (msh_options.seq_pod_waves; 4 is the automatic choice): each wave holds the
+    whole table and walks 64 / waves consecutive pods in order, the waves add their commits to the
+    workgroup's LDS counts, flushed to the device count replicas at the end. Ragged batches (the last
+    block's trailing waves get no pod), counts carried over calls, vs the oracle's serial loop."""
+    rng = np.random.default_rng(31 * pod_waves + norm)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
+    u, nd, pd, pt = _rand_case(rng, 3000, 20_037, p_unsched=0.2, p_tol=0.1)
+    with msh.DeviceContext(0, {"seq_pod_waves": pod_waves}) as ctx:
+        _set(ctx, msh, ps)
+        ctx.upload_nodes(u, nd)
+        cuts = [0, 1, 64, 65, 70, 191, 10_000, 20_037]
+        parts = [ctx.schedule_sequential(pd[a:b], pt[a:b], 0) for a, b in zip(cuts, cuts[1:])]
+        want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, 0)
+        _assert_same(tuple(np.concatenate(x) for x in zip(*parts)), (want_i, want_s, want_st),
+                     f"pod waves={pod_waves} norm={norm}")
+        assert (ctx.node_pod_counts() == want_counts).all()
+
+
 def test_sequential_count_replicas(msh, oracle):
     """Pod-block launches add their commits to count replicas; the next one-workgroup launch (here a
     capacity launch, which reads the counts) and msh_node_pod_counts fold them first. Blocks, a small
