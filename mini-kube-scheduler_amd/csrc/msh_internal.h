@@ -239,7 +239,7 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
 // The capacity form (msh_seq_cap.hip): nw scanning waves with rs words per lane, one workgroup.
 hipError_t launch_seq_capacity(const SeqArgs& a, int nw, int rs, hipStream_t s);
 // Pod waves per pod-block workgroup without a capacity (one scanning wave): each walks 64 / this many pods.
-constexpr int SEQ_POD_WAVES = 4;
+constexpr int SEQ_POD_WAVES = 1;  // measured: 1 / 2 / 4 / 8 waves 11.6 / 14.2 / 13.2 / 18.3 us per C5 launch (profiles/ab/r6_seq_pod_waves.jsonl)
 int seq_pod_waves(const DeviceInfo& dev);
 
 // Launch timing (msh_timing_begin / _end): the next hot-kernel launch on this thread (batch, multi-

@@ -316,7 +316,7 @@ def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split):
 @pytest.mark.parametrize("norm", [0, 1, 3])
 def test_sequential_pod_waves(msh, oracle, pod_waves, norm):
     """Pod-block workgroups of the one-scanning-wave form (tables up to 8,192 nodes, no capacity) shared by
-    1, 2, 4 or 8 pod waves (msh_options.seq_pod_waves; 4 is the automatic choice): each wave holds the
+    1, 2, 4 or 8 pod waves (msh_options.seq_pod_waves; 1 is the automatic choice): each wave holds the
     whole table and walks 64 / waves consecutive pods in order, the waves add their commits to the
     workgroup's LDS counts, flushed to the device count replicas at the end. Ragged batches (the last
     block's trailing waves get no pod), counts carried over calls, vs the oracle's serial loop."""
