@@ -103,9 +103,16 @@ __global__ __launch_bounds__(64) void seq_cap1_kernel(SeqArgs a) {
   for (int32_t jb = 0; jb < a.n_pods; jb += WAVE) {
     if (jb > 0) store_block(jb - WAVE, WAVE);
     {
+      // lane word: code | does-not-tolerate << 4 | score error << 5. The identity-like decode is folded in
+      // here, once per 64 pods by the lanes: a pod whose NodeNumber score errors (no PreScore state, or a
+      // name without a digit; decode_ident) or is not scored at all never takes a match, so its code
+      // becomes CODE_NONE_POD and its scan finds none; per pod the scalar unit then only picks the match
+      // or the class's first available node.
       const bool ok = jb + lane < a.n_pods;
       const bool dig = ok && dn >= 0 && dn <= 9, tl = ok && tn != 0;
-      pkv = (dig ? (uint32_t)dn : CODE_NONE_POD) | (tl ? 0u : 16u);
+      const bool serr = !KX && (idec.err_all || (idec.err_nodigit && !dig));
+      const bool code = KX ? dig : (dig && idec.use_im && !serr);
+      pkv = (code ? (uint32_t)dn : CODE_NONE_POD) | (tl ? 0u : 16u) | (serr ? 32u : 0u);
     }
     load_raw(jb + WAVE, dn, tn);
     const int32_t je = min(jb + WAVE, a.n_pods);
@@ -155,16 +162,21 @@ __global__ __launch_bounds__(64) void seq_cap1_kernel(SeqArgs a) {
         }
       }
       const uint32_t ca = tol ? ca1 : ca0;
-      const int64_t im = cm != NONE ? (int64_t)cm : -1, ia = ca != NONE ? (int64_t)ca : -1;
-      const bool pd_ok = (pk & 15u) != CODE_NONE_POD;
       int32_t sel, st;
-      int64_t sc;
-      if (KX) decode_pod(im, cx != NONE ? (int64_t)cx : -1, ia, pd_ok, pp, &sel, &sc, &st);
-      else decode_ident(im, ia, pd_ok, idec, &sel, &sc, &st);
+      if constexpr (KX) {
+        int64_t sc;
+        decode_pod(cm != NONE ? (int64_t)cm : -1, cx != NONE ? (int64_t)cx : -1, ca != NONE ? (int64_t)ca : -1,
+                   (pk & 15u) != CODE_NONE_POD, pp, &sel, &sc, &st);
+        st |= sc != 0 ? 4 : 0;
+      } else {  // decode_ident with the score error from the lane word (a pod with one has no match)
+        const bool fit = ca == NONE, serr = (pk >> 5) & 1u, hit = cm != NONE;
+        st = fit ? 1 : (serr ? 2 : (hit ? 4 : 0));
+        sel = st & 3 ? -1 : (int32_t)(hit ? cm : ca);
+      }
       // wave-uniform by construction (every input is): kept in SGPRs, so the commit and the next pod's
       // resolve branch on the scalar unit instead of masking lanes
       sel = __builtin_amdgcn_readfirstlane(sel);
-      st = __builtin_amdgcn_readfirstlane(st | (sc != 0 ? 4 : 0));
+      st = __builtin_amdgcn_readfirstlane(st);
       write_lane2(o_a, o_b, sel, st, jl);
       st &= 3;
       // commit (NodeInfo.AddPod): the node's count is read now and used after the next scan; the read is
