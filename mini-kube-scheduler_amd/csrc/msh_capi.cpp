@@ -497,6 +497,8 @@ int generic_args(msh_ctx* c, msh::GenericArgs& g) {
       ++g.ncol;
       const long double sb = score_bound(true, mode, t.col_lo[col], t.col_hi[col]);
       bound += (long double)w * sb;
+      // c24 is what keeps col_term<KT = 0>'s __mul24 operands (weight, normalized score) inside the signed
+      // 24-bit range (msh_generic.hip); any other term multiplied there must be checked here too
       if (mode != MSH_NORMALIZE_NONE) c24 = c24 && w < (1 << 23) && sb < (long double)(1 << 23);
     }
     g.need_ext = g.need_ext || mode != MSH_NORMALIZE_NONE;

@@ -120,7 +120,10 @@ __device__ __forceinline__ GKey<KT> col_term(double v, double b, double r, GKey<
     return (uint64_t)n * cw;
   } else {
     // |n| and |w| below 2^23 on a feasible pair (the host's bound, GenericArgs::w64): the signed 24-bit
-    // multiply (full rate, where v_mul_lo_u32 is quarter rate); v_cvt_i32_f64 saturates on the others
+    // multiply (full rate, where v_mul_lo_u32 is quarter rate); v_cvt_i32_f64 saturates on the others.
+    // That operand range is guaranteed ONLY by generic_args' c24 check (msh_capi.cpp): every normalizing
+    // column's weight and normalized-score bound below 2^23, else the launch takes 64-bit keys. A new term
+    // multiplied here must be added to that check.
     const int32_t n = (int32_t)q;
     return (uint32_t)__mul24(n, (int32_t)cw);
   }

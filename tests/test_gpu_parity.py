@@ -1153,6 +1153,43 @@ def test_generic_small_totals(msh, gpu_ctx, oracle, lst):
                      f"w32 {pl} n={n} p={p}")
 
 
+W32_EDGES = [
+    # (plugins, column ranges) at the edges of generic_kernel's 32-bit keys: a DEFAULT and a
+    # REVERSE column at weight 2^23 - 1 (the largest __mul24 operand, totals near 2^31; the REVERSE weight
+    # is negated in the kernel); a MIN-MAX column at 2^23 - 1; a NONE column whose weight x max|raw| is just
+    # below 2^31 - 2 (32-bit keys) and just above it (the 64-bit fallback); the same NONE column beside a
+    # DEFAULT column at weight 2^23 (past the 24-bit operand limit: 64-bit keys)
+    ([("ScoreColumn1", (1 << 23) - 1, 1), ("ScoreColumn2", (1 << 23) - 1, 2)], {1: (0, 45), 2: (-3, 40)}),
+    ([("ScoreColumn1", (1 << 23) - 1, 3), ("NodeNumber", 7, 0)], {1: (-1000, 1000)}),
+    ([("ScoreColumn3", ((1 << 31) - 2) // 1000, 0)], {3: (-1000, 1001)}),
+    ([("ScoreColumn3", ((1 << 31) - 2) // 1000 + 1, 0)], {3: (-1000, 1001)}),
+    ([("ScoreColumn3", 3, 0), ("ScoreColumn1", 1 << 23, 1)], {1: (0, 50), 3: (-1000, 1001)}),
+]
+
+
+@pytest.mark.parametrize("case", range(len(W32_EDGES)))
+def test_generic_key_width_edges(msh, gpu_ctx, oracle, case):
+    """generic_kernel at the edges of its 32-bit key instances (totals near +-(2^31 - 2), the signed 24-bit
+    multiply at its largest operands) and just past them (the 64-bit form), each against the oracle."""
+    rng = np.random.default_rng(2300 + case)
+    pl, ranges = W32_EDGES[case]
+    names = [nm for nm, _, _ in pl]
+    pre = ["NodeNumber"] if "NodeNumber" in names else []
+    ps = oracle.PluginSet(filters=["NodeUnschedulable"], prescore=pre, score=names,
+                          weights=[w for _, w, _ in pl], normalize=[m for _, _, m in pl])
+    gpu_ctx.set_plugins(ps.filters, ps.prescore, [msh.ScorePluginConfig(nm, w, msh.Normalize(m)) for nm, w, m in pl])
+    for n, p in [(70, 300), (5000, 20_000), (33_000, 513)]:
+        u, nd, pd, pt = _rand_case(rng, n, p, p_unsched=0.3, p_tol=0.2)
+        cols = {k: rng.integers(lo, hi, n) for k, (lo, hi) in ranges.items()}
+        for k, (lo, hi) in ranges.items():
+            cols[k][rng.integers(0, n)] = hi - 1  # the range's top is present
+        gpu_ctx.upload_nodes(u, nd)
+        for k, col in cols.items():
+            gpu_ctx.upload_score_column(f"ScoreColumn{k}", col)
+        _assert_same(gpu_ctx.schedule_batch(pd, pt), oracle.c_schedule_batch(u, nd, pd, pt, ps, cols=cols, threads=8),
+                     f"edge {pl} n={n} p={p}")
+
+
 @pytest.mark.parametrize("lst", [0, 1, 3])
 def test_generic_nn_key_select(msh, oracle, lst):
     """msh_options.gen_nnkey select (read once by msh_create_ex): NodeNumber's key by the compare and select instead of
