@@ -11,10 +11,11 @@
 // broadcasts into VGPRs. Per pair, everything is VGPR-only vector work:
 //   1. feasibility: NodeUnschedulable's verdict, infeasible = xm & ~tolerates, clears the pair's key
 //      (one v_bitop3): an infeasible pair never becomes a pod's maximum;
-//   3. extents (max, min) of every normalizing plugin's raw score over the pod's feasible nodes: a pass
-//      of its own, only when some plugin normalizes (an infeasible pair's column value becomes a quiet
-//      NaN, which v_max_f64 / v_min_f64 skip; NodeNumber's 0 / 10 becomes all-ones); slice waves meet in
-//      an LDS reduction;
+//   3. extents (max, min) of every normalizing plugin's raw score over the pod's feasible nodes, only
+//      when some plugin normalizes. The filter list is [NodeUnschedulable] or empty, so a pod's feasible
+//      nodes are those of its tolerates class (all nodes, or the schedulable ones): the workgroup reduces
+//      the table once per class (a strided pass, wave shuffles, an LDS reduction over the waves) and each
+//      pod takes its class's extents — NodeNumber's from the codes present in the class;
 //   2. the total of each pair: Σ weight x NormalizeScore(raw) in Go int64 arithmetic. NodeNumber is one
 //      compare + select between the pod's two weighted values; a normalizing column is
 //      q = (100 raw - b) x r with the pod's exact reciprocal r, truncated; the
@@ -63,16 +64,11 @@ __device__ __forceinline__ int64_t gen_normalize(int64_t raw, int32_t mode, int6
   }
 }
 
-// v_max_f64 / v_min_f64 as the instructions (fmax adds a NaN canonicalisation per operand): IEEE mode,
+// v_max_f64 as the instruction (fmax adds a NaN canonicalisation per operand): IEEE mode,
 // a quiet NaN operand yields the other one
 __device__ __forceinline__ double vmax_f64(double a, double b) {
   double r;
   asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ double vmin_f64(double a, double b) {
-  double r;
-  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
 // v with its high dword ORed with m: m all-ones turns it into a quiet NaN (exponent and quiet bit set)
@@ -225,139 +221,102 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       emn[b][e] = INT64_MAX;
     }
   const bool nn_ext = a.nn_score && a.nn_mode != 0;
-  bool staged = false;  // the one tile of a single-tile table is staged once for both passes
+  bool staged = false;  // the main pass stages each tile (a single-tile table once)
   if (MODE != 2 && a.need_ext) {
-    int32_t mxn[GEN_BPW];   // NodeNumber: the largest raw score (10 / 0) over feasible nodes, -1 none
-    uint32_t mnn[GEN_BPW];  // the smallest, all-ones none
-    double dmx[GEN_BPW][NC], dmn[GEN_BPW][NC];
-    // NodeNumber's extents by pair flags: a node's class nk = code | 16 x unschedulable (code 0..9, 10 for
-    // none: nk < 27) selects, per pod, bit nk of a 64-bit map {hi, lo} holding at bit nk "feasible and
-    // matches" and at bit 31 + nk "feasible and does not match"; v_alignbit_b32 (the 64-bit funnel shift
-    // by nk) brings both to bits 0 and 31 of one dword, ORed into the pod's flags: 2 VALU per pair
-    uint32_t fhi[GEN_BPW], flo[GEN_BPW], fl[GEN_BPW];
+    // A pod's feasible nodes are one of two sets: the filter list is [NodeUnschedulable] or empty, so they
+    // are every node for a pod that tolerates the unschedulable taint and the schedulable ones for a pod
+    // that does not. Every extent a pod needs is therefore its tolerates class's: the workgroup reduces
+    // the (shard's) table once per class, in LDS, instead of each pod scanning every node:
+    //  * each normalizing column's (max, min) raw score over the class's nodes;
+    //  * NodeNumber: the codes present among the class's nodes (bit code, 10 = no digit); a pod of code d
+    //    has a feasible match iff bit d is set, a feasible non-match iff any other bit is.
+    __shared__ int64_t s_cext[GEN_W][2][2][GEN_COLS];  // [wave][class: 0 schedulable, 1 all][max, -min][column]
+    __shared__ uint32_t s_cpres[GEN_W][2];
+    int64_t cmx[2][NC], cmn[2][NC];
+    uint32_t pres[2] = {0u, 0u};
 #pragma unroll
-    for (int b = 0; b < GEN_BPW; ++b) {
-      mxn[b] = -1;
-      mnn[b] = 0xFFFFFFFFu;
-      const uint32_t mt = pcode[b] <= 9 ? (0x10001u << pcode[b]) : 0u;  // the pod's code, either unschedulable bit
-      const uint32_t fe = ntol[b] ? 0x7FFu : 0x7FF07FFu;                 // the classes that pass the filter
-      const uint32_t m = mt & fe, nm = ~mt & fe;
-      flo[b] = m | (nm << 31);
-      fhi[b] = nm >> 1;
-      fl[b] = 0u;
+    for (int c = 0; c < NC; ++c) {
+      cmx[0][c] = cmx[1][c] = INT64_MIN;
+      cmn[0][c] = cmn[1][c] = INT64_MAX;
+    }
+    for (int32_t i = threadIdx.x; i < n; i += GEN_W * WAVE) {
+      const int dg = a.digit[i];
+      const bool sched = !(a.has_nu && a.unsched[i]);
+      const uint32_t bit = 1u << ((dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE);
+      pres[1] |= bit;
+      pres[0] |= sched ? bit : 0u;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        dmx[b][c] = -__builtin_inf();
-        dmn[b][c] = __builtin_inf();
-      }
-    }
-    auto ext_scan = [&](auto nnx) {
-      constexpr bool NNX = decltype(nnx)::value;
-      for (int t = 0; t < n_tiles; ++t) {
-        const int32_t t0 = t * TN, tn = min(TN, n - t0);
-        if (n_tiles > 1 || !staged) {
-          if (t > 0) __syncthreads();  // every wave is done with the previous tile
-          stage(t0);
-          __syncthreads();
-          staged = true;
-        }
-        int32_t lo, hi;
-        slice_of(tn, lo, hi);
-        auto ext_node = [&](uint2 cx, const double (&v)[NC]) {
-          const uint32_t nk = bop3_or_and(cx.x, cx.y, 16u);  // code | (xm & 16)
-#pragma unroll
-          for (int b = 0; b < GEN_BPW; ++b) {
-            if constexpr (NNX) fl[b] |= __builtin_amdgcn_alignbit(fhi[b], flo[b], nk);
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-              if (c >= nnc) break;
-              const double vv = nan_if(v[c], cx.y, ntol[b]);
-              dmx[b][c] = vmax_f64(dmx[b][c], vv);
-              if (MMX) dmn[b][c] = vmin_f64(dmn[b][c], vv);
-            }
-          }
-        };
-        auto ext_pair = [&](int32_t k2) {  // nodes 2 k2, 2 k2 + 1 (16-B aligned)
-          const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k2];
-          double v0[NC], v1[NC];
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            v0[c] = v1[c] = 0.0;
-            if (c >= nnc) continue;
-            const gen_d2 w = reinterpret_cast<const gen_d2*>(s_v + (size_t)c * TN)[k2];
-            v0[c] = w.x;
-            v1[c] = w.y;
-          }
-          ext_node(make_uint2(c2.x, c2.y), v0);
-          ext_node(make_uint2(c2.z, c2.w), v1);
-        };
-        int32_t k = lo;  // lo is a multiple of GEN_CHUNK
-        for (; k + GEN_CHUNK <= hi; k += GEN_CHUNK) {  // a chunk's reads issued together
-#pragma unroll
-          for (int q = 0; q < GEN_CHUNK / 2; ++q) ext_pair((k >> 1) + q);  // one base, immediate offsets
-        }
-        for (; k + 1 < hi; k += 2) ext_pair(k >> 1);
-        if (k < hi) {
-          double v[NC];
-#pragma unroll
-          for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
-          ext_node(s_cx[k], v);
+        if (c >= nnc) break;
+        const int64_t v = a.cols[(size_t)a.ncc[c] * a.col_stride + i];
+        cmx[1][c] = max(cmx[1][c], v);
+        cmn[1][c] = min(cmn[1][c], v);
+        if (sched) {
+          cmx[0][c] = max(cmx[0][c], v);
+          cmn[0][c] = min(cmn[0][c], v);
         }
       }
-    };
-    if (nn_ext) ext_scan(std::true_type{});
-    else ext_scan(std::false_type{});
-#pragma unroll
-    for (int b = 0; b < GEN_BPW; ++b) {  // raw 10 on a feasible match, 0 on a feasible non-match
-      const bool fm = fl[b] & 1u, fnm = fl[b] >> 31;
-      mxn[b] = fm ? 10 : (fnm ? 0 : -1);
-      mnn[b] = fnm ? 0u : (fm ? 10u : 0xFFFFFFFFu);
     }
-    // slice waves of a pod group meet in LDS (every wave of the group takes the merged extents)
-    if (S > 1) {
-      int32_t* m_nn = reinterpret_cast<int32_t*>(s_merge);                       // [GEN_W][BPW][2][64]
-      double* m_col = reinterpret_cast<double*>(s_merge + GEN_W * GEN_BPW * 2 * WAVE * 4);  // [GEN_W][BPW][NC][2][64]
-      __syncthreads();
+    // the wave's, then the workgroup's
 #pragma unroll
-      for (int b = 0; b < GEN_BPW; ++b) {
-        m_nn[((wv * GEN_BPW + b) * 2 + 0) * WAVE + lane] = mxn[b];
-        m_nn[((wv * GEN_BPW + b) * 2 + 1) * WAVE + lane] = (int32_t)mnn[b];
+    for (int off = 1; off < WAVE; off <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        pres[k] |= (uint32_t)__shfl_xor((int)pres[k], off);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           if (c >= nnc) break;
-          m_col[(((wv * GEN_BPW + b) * NC + c) * 2 + 0) * WAVE + lane] = dmx[b][c];
-          m_col[(((wv * GEN_BPW + b) * NC + c) * 2 + 1) * WAVE + lane] = dmn[b][c];
+          cmx[k][c] = max(cmx[k][c], (int64_t)__shfl_xor((long long)cmx[k][c], off));
+          cmn[k][c] = min(cmn[k][c], (int64_t)__shfl_xor((long long)cmn[k][c], off));
         }
       }
-      __syncthreads();
-      for (int k = 0; k < S; ++k) {
-        const int ow = pg * S + k;
-#pragma unroll
-        for (int b = 0; b < GEN_BPW; ++b) {
-          mxn[b] = max(mxn[b], m_nn[((ow * GEN_BPW + b) * 2 + 0) * WAVE + lane]);
-          mnn[b] = umin(mnn[b], (uint32_t)m_nn[((ow * GEN_BPW + b) * 2 + 1) * WAVE + lane]);
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            if (c >= nnc) break;
-            dmx[b][c] = vmax_f64(dmx[b][c], m_col[(((ow * GEN_BPW + b) * NC + c) * 2 + 0) * WAVE + lane]);
-            dmn[b][c] = vmin_f64(dmn[b][c], m_col[(((ow * GEN_BPW + b) * NC + c) * 2 + 1) * WAVE + lane]);
-          }
-        }
-      }
-      __syncthreads();  // the merge area is reused by the main pass
     }
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        s_cpres[wv][k] = pres[k];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (c >= nnc) break;
+          s_cext[wv][k][0][c] = cmx[k][c];
+          s_cext[wv][k][1][c] = -cmn[k][c];  // negated: one max merges both (cmn <= INT64_MAX)
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      pres[k] = 0u;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) cmx[k][c] = cmn[k][c] = INT64_MIN;  // cmn negated here
+      for (int w = 0; w < GEN_W; ++w) {
+        pres[k] |= s_cpres[w][k];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (c >= nnc) break;
+          cmx[k][c] = max(cmx[k][c], s_cext[w][k][0][c]);
+          cmn[k][c] = max(cmn[k][c], s_cext[w][k][1][c]);
+        }
+      }
+    }
+    // every pod takes its class's extents
 #pragma unroll
     for (int b = 0; b < GEN_BPW; ++b) {
-      if (nn_ext && mxn[b] >= 0) {  // NodeNumber's raw scores are 10 / 0
-        emx[b][0] = mxn[b];
-        emn[b][0] = (int64_t)mnn[b];
+      const int k = ntol[b] ? 0 : 1;
+      if (nn_ext) {  // NodeNumber's raw scores over the feasible nodes: 10 on a match, 0 otherwise
+        const uint32_t pb = pcode[b] <= 9 ? 1u << pcode[b] : 0u;
+        const bool fm = (pres[k] & pb) != 0, fnm = (pres[k] & ~pb) != 0;
+        if (fm || fnm) {
+          emx[b][0] = fm ? 10 : 0;
+          emn[b][0] = fnm ? 0 : 10;
+        }
       }
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         if (c >= nnc) break;
-        if (dmx[b][c] != -__builtin_inf()) {  // 100 x raw / 100: exact (|raw| <= 2^31)
-          emx[b][1 + c] = (int64_t)(dmx[b][c] * 0.01);
-          emn[b][1 + c] = MMX ? (int64_t)(dmn[b][c] * 0.01) : INT64_MAX;
+        if (cmx[k][c] != INT64_MIN) {
+          emx[b][1 + c] = cmx[k][c];
+          emn[b][1 + c] = MMX ? -cmn[k][c] : INT64_MAX;
         }
       }
     }
@@ -773,10 +732,8 @@ hipError_t launch_generic(GenericArgs& a, int mode, const DeviceInfo& dev, hipSt
   tile = std::max<int32_t>(GEN_CHUNK, std::min<int32_t>(tile, (a.n_nodes + GEN_CHUNK - 1) & ~(GEN_CHUNK - 1)));
   a.tile = tile;
   a.slices = gen_slices(groups, a.n_nodes, dev);
-  // the slice merge (S > 1): the extents (NodeNumber's two int32, (max, min) per column of the
-  // instance's column array), then (key, index)
-  const size_t ncx = general ? 4 : 1;
-  const size_t merge = a.slices > 1 ? (size_t)GEN_W * GEN_BPW * WAVE * std::max<size_t>(8 + 16 * ncx, key + 4) : 0;
+  // the slice merge (S > 1): (key, index) per pod
+  const size_t merge = a.slices > 1 ? (size_t)GEN_W * GEN_BPW * WAVE * (key + 4) : 0;
   const size_t lds = (size_t)tile * per_node + merge;
   const int pgs = GEN_W / a.slices;
   const int32_t bx = (maxp + pgs * GEN_BPW * WAVE - 1) / (pgs * GEN_BPW * WAVE);
