@@ -96,11 +96,11 @@ __device__ __forceinline__ GKey<KT> key_mask(GKey<KT> t, uint32_t xm, uint32_t n
   }
 }
 
-// One lane's scoring state of one 64-pod block (main pass).
-template <int KT, int NC>
+// One lane's scoring state of one 64-pod block (main pass): NodeNumber's weighted normalized value on a
+// digit match / otherwise, biased (the score columns' part is the node's class term, staged per tile).
+template <int KT>
 struct GLane {
-  GKey<KT> k1, k0;  // NodeNumber's weighted normalized value on a digit match / otherwise, biased
-  double rr[NC], bb[NC];  // per normalizing column: the reciprocal and the min-max offset
+  GKey<KT> k1, k0;
 };
 
 // The contribution of normalizing column c to a pair's total: w x trunc((v - b) x r), v = 100 x raw.
@@ -156,12 +156,23 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
   if (wg0 >= np) return;  // the whole workgroup lies past its batch's end
   const int32_t n = a.n_nodes, TN = a.tile;
   const int nnc = NNC == 4 ? a.nnc : NNC;  // normalizing columns (the general instance: a runtime count)
-  // dynamic LDS: the tile (records, node-only sums, normalizing columns), then the slice-merge area
+  // The score columns' part of a pair's total depends on the node and on the pod's tolerates class alone
+  // (stage 3: the class fixes the extents, hence every normalized value): the CLASS TERM of node i for
+  // class k, Σ over the columns of weight x NormalizeScore(raw), is staged with the node, once per class.
+  constexpr bool CT = TS || NNC > 0;
+  // dynamic LDS: the tile (records, then [TN][2] class terms when the list has score columns), then the
+  // slice-merge area
   uint2* s_cx = reinterpret_cast<uint2*>(s_dyn);
-  Key* s_ts = reinterpret_cast<Key*>(s_cx + TN);
-  double* s_v = reinterpret_cast<double*>(reinterpret_cast<char*>(s_ts) + (TS ? (size_t)TN * sizeof(Key) : 0));
-  char* s_merge = reinterpret_cast<char*>(s_v + (size_t)nnc * TN);
+  Key* s_ct = reinterpret_cast<Key*>(s_cx + TN);
+  char* s_merge = reinterpret_cast<char*>(s_ct + (CT ? 2 * (size_t)TN : 0));
+  // per class (0: pods that do not tolerate the unschedulable taint, 1: pods that do) and normalizing
+  // column: the reciprocal and the min-max offset of its NormalizeScore
+  __shared__ double s_crr[2][NC], s_cbb[2][NC];
   if (threadIdx.x == 0) s_ffs = GEN_NONE;
+  if (threadIdx.x < 2 * NC) {
+    (&s_crr[0][0])[threadIdx.x] = 0.0;
+    (&s_cbb[0][0])[threadIdx.x] = 0.0;
+  }
   __syncthreads();
 
   // ---- the lane's pods ----
@@ -183,27 +194,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     ntol[b] = tq ? 0u : 0xFFFFFFFFu;
   }
 
-  // ---- stage 5: tiles of the node table through LDS, shared by the workgroup's waves ----
   const int n_tiles = n > 0 ? (n + TN - 1) / TN : 0;
-  auto stage = [&](int32_t t0) {
-    const int32_t tn = min(TN, n - t0);
-    for (int32_t k = threadIdx.x; k < ((tn + WAVE - 1) & ~(WAVE - 1)); k += GEN_W * WAVE) {
-      const int32_t i = t0 + k;
-      const bool in = k < tn;
-      uint32_t xm = 0u;
-      if (in) {
-        const int dg = a.digit[i];
-        xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
-        s_cx[k] = make_uint2((dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE, xm);
-        if constexpr (TS) s_ts[k] = node_sum(i);  // the node-only part: weight x raw, columns without a normalizer
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-          if (c < nnc) s_v[(size_t)c * TN + k] = 100.0 * (double)a.cols[(size_t)a.ncc[c] * a.col_stride + i];
-      }
-      const uint64_t m = __ballot(in && xm == 0u);
-      if (m && lane == 0) atomicMin(&s_ffs, (uint32_t)(i - lane) + (uint32_t)__builtin_ctzll(m));
-    }
-  };
   // the wave's slice of a tile of tn nodes: [lo, hi)
   auto slice_of = [&](int32_t tn, int32_t& lo, int32_t& hi) {
     const int32_t L = (((tn + S - 1) / S) + GEN_CHUNK - 1) & ~(GEN_CHUNK - 1);
@@ -375,7 +366,7 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     else cw[c] = rev ? (Key)(0 - (uint64_t)a.nw[c]) : (Key)a.nw[c];
     if (rev) tot0 += (uint64_t)100 * (uint64_t)a.nw[c];
   }
-  GLane<KT, NC> L[GEN_BPW];
+  GLane<KT> L[GEN_BPW];
 #pragma unroll
   for (int b = 0; b < GEN_BPW; ++b) {
     int64_t c1 = 0, c0 = 0;
@@ -395,27 +386,68 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       L[b].k1 = (uint32_t)((uint64_t)c1 + tot0) + 0x80000000u;
       L[b].k0 = (uint32_t)((uint64_t)c0 + tot0) + 0x80000000u;
     }
+    // the class's NormalizeScore parameters: every pod of a class has the same extents, so the lanes of
+    // a class write the same values (a class without a pod in the workgroup keeps r = 0: never read)
+    if (jj[b] >= np) continue;
+    const int kc = ntol[b] ? 0 : 1;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      L[b].rr[c] = 0.0;
-      L[b].bb[c] = 0.0;
       if (c >= nnc) break;
       const int32_t md = a.nmode[c];
       const int64_t mx = emx[b][1 + c], mn = emn[b][1 + c];
       if (mx == INT64_MIN) continue;  // no feasible node
+      double rr = 0.0, bb = 0.0;
       if (md == 3) {                  // min-max: (raw - mn) x 100 / (mx - mn), 0 when mx == mn
         if (mx != mn) {
-          L[b].rr[c] = (1.0 / (double)(mx - mn)) * GEN_RCP_BIAS;
-          L[b].bb[c] = 100.0 * (double)mn;
+          rr = (1.0 / (double)(mx - mn)) * GEN_RCP_BIAS;
+          bb = 100.0 * (double)mn;
         }
       } else {  // DefaultNormalizeScore: 100 raw / max(mx, 0); DEFAULT leaves an all-zero list (m = 0 -> raw)
         const int64_t m = mx > 0 ? mx : 0;
-        if (m != 0) L[b].rr[c] = (1.0 / (double)m) * GEN_RCP_BIAS;
-        else if (md == 1) L[b].rr[c] = 0.01 * GEN_RCP_BIAS;
+        if (m != 0) rr = (1.0 / (double)m) * GEN_RCP_BIAS;
+        else if (md == 1) rr = 0.01 * GEN_RCP_BIAS;
         // REVERSE with m == 0: r = 0, 100 - 0 = 100 for every node
       }
+      s_crr[kc][c] = rr;
+      s_cbb[kc][c] = bb;
     }
   }
+  __syncthreads();  // the class parameters, before any class term is staged
+  // The class term of node i for class kc from the uploaded columns: the node-only sum of the columns
+  // without a normalizer, plus weight x trunc((100 raw - b) x r) per normalizing column (the exact
+  // truncation of DESIGN.md §4.3). The staged tiles and the re-evaluation of the winning chunk use it alike.
+  auto class_term = [&](int kc, int32_t i) -> Key {
+    Key t = 0;
+    if constexpr (TS) t = node_sum(i);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (c >= nnc) break;
+      const double v = 100.0 * (double)a.cols[(size_t)a.ncc[c] * a.col_stride + i];
+      t += col_term<KT, MMX>(v, s_cbb[kc][c], s_crr[kc][c], cw[c]);
+    }
+    return t;
+  };
+
+  // ---- stage 5: tiles of the node table through LDS, shared by the workgroup's waves ----
+  auto stage = [&](int32_t t0) {
+    const int32_t tn = min(TN, n - t0);
+    for (int32_t k = threadIdx.x; k < ((tn + WAVE - 1) & ~(WAVE - 1)); k += GEN_W * WAVE) {
+      const int32_t i = t0 + k;
+      const bool in = k < tn;
+      uint32_t xm = 0u;
+      if (in) {
+        const int dg = a.digit[i];
+        xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
+        s_cx[k] = make_uint2((dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE, xm);
+        if constexpr (CT) {
+          s_ct[2 * k] = class_term(0, i);
+          s_ct[2 * k + 1] = class_term(1, i);
+        }
+      }
+      const uint64_t m = __ballot(in && xm == 0u);
+      if (m && lane == 0) atomicMin(&s_ffs, (uint32_t)(i - lane) + (uint32_t)__builtin_ctzll(m));
+    }
+  };
   // NodeNumber's key without a compare (32-bit keys, |c1 - c0| < 2^24: a.nn24): base + bit x delta, the bit
   // (v_bfe_u32) of the pod's one-hot code set at the node's code, base / delta ordered so that delta >= 0,
   // so the product and the add are one v_mad_u32_u24 and no lane mask (VCC) is written per pair
@@ -428,19 +460,15 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
     nbase[b] = up ? k0 : k1;
     ndelta[b] = (up ? k1 - k0 : k0 - k1) & 0xFFFFFFu;
   }
-  // the key of one pair, from a node's staged (or re-read) values
-  auto pair_key = [&](int b, uint32_t code, uint32_t xm, Key ts, const double (&v)[NC], auto nnfast) -> Key {
+  // the key of one pair, from a node's staged (or re-read) values: NodeNumber's part, plus the node's
+  // class term for the pod's class (ct0: pods that do not tolerate the taint, ct1: pods that do)
+  auto pair_key = [&](int b, uint32_t code, uint32_t xm, Key ct0, Key ct1, auto nnfast) -> Key {
     Key t;
     if constexpr (decltype(nnfast)::value && !W64)
       t = nbase[b] + __builtin_amdgcn_ubfe(nsel[b], code, 1) * ndelta[b];
     else
       t = code == pcode[b] ? L[b].k1 : L[b].k0;
-    if constexpr (TS) t += ts;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      if (c >= nnc) break;
-      t += col_term<KT, MMX>(v[c], L[b].bb[c], L[b].rr[c], cw[c]);
-    }
+    if constexpr (CT) t += ntol[b] ? ct0 : ct1;
     return key_mask<KT>(t, xm, ntol[b]);
   };
 
@@ -463,41 +491,38 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       }
       int32_t lo, hi;
       slice_of(tn, lo, hi);
-      auto node_v = [&](uint2 cx, Key ts, const double (&v)[NC]) {
+      auto node_v = [&](uint2 cx, Key ct0, Key ct1) {
 #pragma unroll
         for (int b = 0; b < GEN_BPW; ++b) {
-          const Key key = pair_key(b, cx.x, cx.y, ts, v, nnfast);
+          const Key key = pair_key(b, cx.x, cx.y, ct0, ct1, nnfast);
           if constexpr (KT == 2) best[b] = vmax_f64(best[b], key);  // an infeasible (NaN) key is skipped
           else best[b] = key > best[b] ? key : best[b];
         }
       };
       auto node = [&](int32_t k) {
-        Key ts = 0;
-        if constexpr (TS) ts = s_ts[k];
-        double v[NC];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) v[c] = c < nnc ? s_v[(size_t)c * TN + k] : 0.0;
-        node_v(s_cx[k], ts, v);
+        Key ct0 = 0, ct1 = 0;
+        if constexpr (CT) {
+          ct0 = s_ct[2 * k];
+          ct1 = s_ct[2 * k + 1];
+        }
+        node_v(s_cx[k], ct0, ct1);
       };
       // two nodes per LDS read (k even: a chunk starts at a multiple of GEN_CHUNK)
       auto node_pair = [&](int32_t k2) {  // nodes 2 k2, 2 k2 + 1
         const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k2];
-        Key ts0 = 0, ts1 = 0;
-        if constexpr (TS) {
-          ts0 = s_ts[2 * k2];
-          ts1 = s_ts[2 * k2 + 1];
-        }
-        double v0[NC], v1[NC];
+        Key ct[4] = {0, 0, 0, 0};  // node 2 k2's class terms, then node 2 k2 + 1's
+        if constexpr (CT && !W64) {
+          const gen_u4 t4 = reinterpret_cast<const gen_u4*>(s_ct)[k2];
+          ct[0] = t4.x;
+          ct[1] = t4.y;
+          ct[2] = t4.z;
+          ct[3] = t4.w;
+        } else if constexpr (CT) {
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          v0[c] = v1[c] = 0.0;
-          if (c >= nnc) continue;
-          const gen_d2 w = reinterpret_cast<const gen_d2*>(s_v + (size_t)c * TN)[k2];
-          v0[c] = w.x;
-          v1[c] = w.y;
+          for (int q = 0; q < 4; ++q) ct[q] = s_ct[4 * k2 + q];
         }
-        node_v(make_uint2(c2.x, c2.y), ts0, v0);
-        node_v(make_uint2(c2.z, c2.w), ts1, v1);
+        node_v(make_uint2(c2.x, c2.y), ct[0], ct[1]);
+        node_v(make_uint2(c2.z, c2.w), ct[2], ct[3]);
       };
       int32_t k = lo;
       for (; k + GEN_CHUNK <= hi; k += GEN_CHUNK) {
@@ -506,10 +531,10 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
         for (int b = 0; b < GEN_BPW; ++b) prev[b] = best[b];
 #pragma unroll
         for (int q = 0; q < GEN_CHUNK / 2; ++q) {
-          // with score columns two nodes per ds_read_b128 (4.30 against 4.43 ms per 32-batch C3 launch on
-          // NodeNumber + a DEFAULT column, one box); NodeNumber alone keeps the compiler's ds_read2_b64 pairs
-          // (1.54 against 1.57 ms on the reference list; profiles/ab/r5_MSH_GEN_LDS128_*)
-          if constexpr (NNC > 0 || TS) {
+          // with score columns two nodes' records per ds_read_b128 (4.30 against 4.43 ms per 32-batch C3
+          // launch on NodeNumber + a DEFAULT column, one box); NodeNumber alone keeps the compiler's
+          // ds_read2_b64 pairs (1.54 against 1.57 ms on the reference list; profiles/ab/r5_MSH_GEN_LDS128_*)
+          if constexpr (CT) {
             node_pair((k >> 1) + q);
           } else {
             node(k + 2 * q);
@@ -544,13 +569,9 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       const int dg = a.digit[i];
       const uint32_t code = (dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE;
       const uint32_t xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
-      Key ts = 0;
-      if constexpr (TS) ts = node_sum(i);
-      double v[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        v[c] = c < nnc ? 100.0 * (double)a.cols[(size_t)a.ncc[c] * a.col_stride + i] : 0.0;
-      if (pair_key(b, code, xm, ts, v, std::false_type{}) == best[b]) {
+      Key ct = 0;
+      if constexpr (CT) ct = class_term(ntol[b] ? 0 : 1, i);
+      if (pair_key(b, code, xm, ct, ct, std::false_type{}) == best[b]) {
         bidx[b] = i;
         break;
       }
@@ -724,10 +745,9 @@ hipError_t launch_generic(GenericArgs& a, int mode, const DeviceInfo& dev, hipSt
   if (maxp == 0) return hipSuccess;
   const bool general = a.nnc > 1;  // launch_gen_mode's forms for two or more normalizing columns
   const size_t key = (a.w64 || (general && a.nnc > 2)) ? 8 : 4;  // launch_gen_mode's key type
-  const int nnc = general ? a.nnc : std::min(a.nnc, 1);
-  // bytes per staged node: the record, the node-only sum (the general form always stages it), the
-  // normalizing columns
-  const size_t per_node = 8 + ((general || a.nts > 0) ? key : 0) + 8 * (size_t)nnc;
+  // bytes per staged node: the record, and the two class terms when the list has score columns (the kernel's
+  // CT: the general form, a node-only sum or a normalizing column)
+  const size_t per_node = 8 + ((general || a.nts > 0 || a.nnc > 0) ? 2 * key : 0);
   int32_t tile = (int32_t)(GEN_LDS_BUDGET / per_node) & ~(GEN_CHUNK - 1);
   tile = std::max<int32_t>(GEN_CHUNK, std::min<int32_t>(tile, (a.n_nodes + GEN_CHUNK - 1) & ~(GEN_CHUNK - 1)));
   a.tile = tile;

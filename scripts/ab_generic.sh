@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${OUT:-gpurun_out/r6f}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for variant in ${VARIANTS:-cur old_gen}; do
+for variant in ${VARIANTS:-cur gen_s3 old_gen}; do
   lib=$PWD/mini-kube-scheduler_amd/libminisched_hip.so
   [ "$variant" != cur ] && lib=$PWD/scripts/expt/$variant/libminisched_hip.so
   for m in "generic_col 1 0" "generic_2col 1 0" "generic 3 1" "generic 1 0"; do
