@@ -78,7 +78,7 @@ GEN_VALU_PER_PAIR_REF = 117 / 32
 SEQ_VALU_PER_WORD = 5
 PAIR_LDS_MAX_GROUPS = 128          # msh_pair.hip: tables the LDS-staged pair kernel takes (4-wave workgroups)
 PAIR_LDS_BIG_GROUPS = 416          # ... and with 16-wave workgroups
-PMC_FILE = ROOT / "profiles" / "r5_pmc_c3.json"
+PMC_FILE = ROOT / "profiles" / "r6_pmc_c3.json"
 # The headline plugin set (BASELINE C3: "nodenumber prescore/score + weighted NormalizeScore"): the
 # reference's filter and prescore lists, NodeNumber scored at weight 3 with upstream's
 # helper.DefaultNormalizeScore (MaxNodeScore 100) as its NormalizeScore. The reference itself has no
@@ -121,6 +121,8 @@ def seq_shape(n_nodes: int, cap: bool = False):
 
 def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
     r, nw = seq_shape(n_nodes, cap)
+    if cap and nw == 1:  # msh_seq_cap.hip: one wave, counts in LDS, availability planes in registers
+        return f"void msh::seq_cap1_kernel<{r}, {str(kx).lower()}>"
     u = 1 if cap else 4  # SEQ_AHEAD: pods decided per step without a capacity
     return f"void msh::seq_kernel<{r}, {nw}, {str(kx).lower()}, {str(cap).lower()}, {u}>"
 
@@ -449,12 +451,12 @@ def load_valu_peak():
 
 
 def plugin_tag(weight: int, norm: int) -> str:
-    """The NodeNumber score entry as profiles/r5_pmc_c3.json records it (scripts/run_batch.py)."""
+    """The NodeNumber score entry as profiles/r6_pmc_c3.json records it (scripts/run_batch.py)."""
     return f"NodeNumber w={weight} norm={norm}"
 
 
 def pmc_entry(key: str, kname: str, n_local: int, p: int, nb: int, plugins: str | None = None):
-    """The profiles/r5_pmc_c3.json entry for this kernel, size, batch count and plugin list (None if
+    """The profiles/r6_pmc_c3.json entry for this kernel, size, batch count and plugin list (None if
     it does not match what this run timed)."""
     e = (load_json(PMC_FILE) or {}).get("kernels", {}).get(key, {})
     ok = (e.get("kernel") == kname and e.get("nodes") == n_local and e.get("pods") == p
@@ -642,7 +644,7 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
     ctx.upload_nodes(u, nd)
     # the other NormalizeScore modes and the reference's own list (w = 1, no normalizer) on the same
     # 32-batch launches as the headline, each with its VALU roofline (the counter form from its own
-    # profiles/r5_pmc_c3.json entry)
+    # profiles/r6_pmc_c3.json entry)
     variants = {}
     for name, key, weight, norm in (("reference_weight1_none", "pair_multi_ref", 1, 0),
                                     ("minmax_weight3", "pair_minmax", 3, 3),

@@ -64,7 +64,7 @@ for mode, prefix, tags, nb, plug in (
         ("generic_col", "msh::generic_kernel", ("gc_sq", "gc_sq2"), NB, tag_of(1, 0) + " + ScoreColumn0 w=2 norm=1"),
         ("sequential", "msh::seq_kernel", ("s_sq", "s_sq2"), 1, tag_of(3, 1)),
         ("sequential_serial", "msh::seq_kernel", ("ss_sq",), 1, tag_of(3, 1)),
-        ("sequential_capacity", "msh::seq_kernel", ("c_sq", "c_sq2", "c_fetch"), 1, tag_of(1, 0) + " cap=15")):
+        ("sequential_capacity", "msh::seq_cap", ("c_sq", "c_sq2", "c_fetch"), 1, tag_of(1, 0) + " cap=15")):
     e = {"nodes": N, "pods": P, "batches_per_launch": nb, "plugins": plug, "launches_per_counter": {}}
     for t in tags:
         name, avg, cnt = counters(t, prefix)
@@ -107,7 +107,7 @@ for tag, prefix in (("stats", "msh::pair"), ("stats_k20", "msh::pair"),
                     ("stats_generic", "msh::generic_kernel"), ("stats_generic_hl", "msh::generic_kernel"),
                     ("stats_generic_col", "msh::generic_kernel"),
                     ("stats_seq", "msh::seq_kernel"), ("stats_seq_serial", "msh::seq_kernel"),
-                    ("stats_seq_cap", "msh::seq_kernel")):
+                    ("stats_seq_cap", "msh::seq_cap")):
     name, avg, calls = stats_avg_ns(tag, prefix)
     if name:
         res["stats"][tag] = {"kernel": name, "avg_ns": avg, "calls": calls}
