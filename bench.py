@@ -6,9 +6,12 @@ A step = one pass of the hot path (filter -> prescore -> score -> select, i.e.
 minisched/minisched.go:50-87 for every pod of a batch) over one batch of synthetic pods with
 inputs already resident in HBM.
 
-Plugins: BASELINE C3's "nodenumber prescore/score + weighted NormalizeScore": filter=[NodeUnschedulable],
-prescore=[NodeNumber], score=[NodeNumber weight 3, DefaultNormalizeScore] (HEADLINE_WEIGHT / HEADLINE_NORM);
-the reference's own w = 1 list without a normalizer is timed beside it.
+Plugins: BASELINE.json configs[2]'s "nodenumber prescore/score + weighted NormalizeScore":
+filter=[NodeUnschedulable], prescore=[NodeNumber], score=[NodeNumber weight 3, DefaultNormalizeScore]
+(HEADLINE_WEIGHT / HEADLINE_NORM). This departs from BASELINE.md's plugin table (weight 1, and its C3 row's
+"weight 3 + identity normalize"): DefaultNormalizeScore maps 10 to 100, so it is not an identity. The
+reference's own w = 1 list without a normalizer, BASELINE.md's definition and round 4's `value`, runs on the
+same launches and is reported beside it (c3_plugin_variants.reference_weight1_none); the two time alike.
 
 Modes (the headline line)
   batch       (default) BASELINE C3: 5,000 nodes x 100,000 pods per batch per GPU, on the per-pair kernel
