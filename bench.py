@@ -124,8 +124,8 @@ def seq_shape(n_nodes: int, cap: bool = False):
 
 def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
     r, nw = seq_shape(n_nodes, cap)
-    if cap and nw == 1:  # msh_seq_cap.hip: one wave, counts in LDS, availability planes in registers
-        return f"void msh::seq_cap1_kernel<{r}, {str(kx).lower()}>"
+    if cap and nw == 1:  # msh_seq_cap.hip: one wave, 4 pods per step, counts in LDS, availability planes
+        return f"void msh::seq_capu_kernel<{r}, {str(kx).lower()}, 4>"
     u = 1 if cap else 4  # SEQ_AHEAD: pods decided per step without a capacity
     return f"void msh::seq_kernel<{r}, {nw}, {str(kx).lower()}, {str(cap).lower()}, {u}>"
 

@@ -7,27 +7,27 @@
 namespace msh {
 
 // ---------------------------------------------------------------------------------------
-// seq_cap1_kernel: the capacity form on ONE wave (tables up to 8,192 nodes: RS <= 4 words per lane).
-// The general seq_kernel<..., CAP> decides a pod, then commits it and waits for the LDS count to come
-// back before the next pod may scan (the FULL bit it may set is read by that scan), and scans a second
-// first-hit chain (the first feasible node) per pod. Here:
-//  * per tolerates class, an availability plane AV = V & ~FULL (& ~X for pods that do not tolerate the
-//    unschedulable taint) per word: a pod's first available match is its code compare (4 VALU per word)
-//    ANDed into AV and one first-hit step;
-//  * the first available node of each class (the fallback of a pod without a match, and its FitError
-//    when there is none) is kept as two wave-uniform scalars, recomputed only when that very node fills;
-//  * the commit's count update (an LDS atomic) is resolved one pod LATE: pod j + 1 scans while pod j's
-//    atomic is in flight, and only then reads the old count back. A node that fills removes ONE candidate,
-//    which changes pod j + 1's choice only if pod j + 1 chose that node: then (rarely) its scan is redone.
-//    The decisions are exactly the serial loop's.
+// seq_capu_kernel: the capacity form on ONE wave, U pods per step. A commit changes a later decision only
+// when it FILLS a node (the node leaves the availability planes), and then only for a pod whose first
+// available match (or non-match) or class fallback was that very node. So the U pods of a step are
+// scanned together against the state at the step's start (U independent chains, interleaved word by
+// word), then resolved in order on the scalar unit:
+//  * a pod whose scan result is a node an earlier pod of the step filled is scanned again (rare: a fill is
+//    one commit in max_pods), the class fallbacks are the current scalars;
+//  * the count of the committed node was read for the step's predicted placements in one batch of LDS
+//    reads; a pod adds the commits of earlier pods of the step to the same node (their writes follow the
+//    read), and reads again only when its placement differs from the prediction.
+// The decisions are exactly the serial loop's. Per pod the scalar unit only picks the placement and
+// commits; the identity-like decode (status, score) is done by the lanes once per 64 pods from the
+// scan's first match and the class fallback kept in each pod's lane.
 // ---------------------------------------------------------------------------------------
-template <int RS, bool KX>
-__global__ __launch_bounds__(64) void seq_cap1_kernel(SeqArgs a) {
+template <int RS, bool KX, int U>
+__global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
+  static_assert(WAVE % U == 0, "a step never straddles a 64-pod block");
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   extern __shared__ int32_t lcnt[];  // [n_words * 32] pods per node: carried in, updated, written back
   const int lane = threadIdx.x;
   const int32_t slots = a.n_words * 32;
-  // the counts (with the replicas of earlier pod-block launches folded in, a.fold) into LDS
   for (int32_t i = lane; i < slots; i += WAVE) {
     int32_t c = a.counts[i];
     if (a.fold) {
@@ -41,7 +41,6 @@ __global__ __launch_bounds__(64) void seq_cap1_kernel(SeqArgs a) {
   __syncthreads();
   int32_t max_pods = a.max_pods;
   asm volatile("" : "+s"(max_pods));
-  // the table in registers: lane l holds words l * RS .. l * RS + RS - 1 (List order across lanes)
   const uint32_t lane_base = (uint32_t)(lane * RS) << 5;  // node index of bit 0 of slot 0's word
   uint32_t D0[RS], D1[RS], D2[RS], D3[RS], AV0[RS], AV1[RS];
 #pragma unroll
@@ -61,23 +60,20 @@ __global__ __launch_bounds__(64) void seq_cap1_kernel(SeqArgs a) {
       AV0[r] = AV1[r] & ~g[PLANE_X * PLANE_GW];
     }
   }
-  // The first available node of a class: the lanes' first (slots ascend), then the wave's first lane.
   auto first_avail = [&](const uint32_t (&av)[RS]) -> uint32_t {
     uint32_t f = NONE;
 #pragma unroll
     for (int r = RS - 1; r >= 0; --r) f = umin(f, (lane_base + (uint32_t)(32 * r)) | ffbl(av[r]));
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_first(f));
   };
-  uint32_t ca0 = first_avail(AV0), ca1 = first_avail(AV1);
-  __builtin_amdgcn_s_waitcnt(0);  // the table loads drained here, not inside the loop
+  uint32_t ca0 = first_avail(AV0), ca1 = first_avail(AV1);  // each class's first available node
+  __builtin_amdgcn_s_waitcnt(0);
 
   PluginParams pp = a.pp;
   asm volatile("" : "+s"(pp.has_nu_filter), "+s"(pp.has_nn_score), "+s"(pp.nn_prescore), "+s"(pp.mode),
                "+s"(pp.weight));
   const IdentDecode idec = make_ident_decode(pp);
-  const int64_t sm = KX ? 100 * pp.weight : idec.sm;  // the one non-zero score a decode gives
-  // pods in lanes, 64 at a time: raw bytes loaded one block ahead, then one lane word per pod:
-  // code | does-not-tolerate << 4
+  const int64_t sm = KX ? 100 * pp.weight : idec.sm;
   auto load_raw = [&](int32_t j0, int32_t& dr, int32_t& tr) {
     const int32_t jj = min(j0 + lane, a.n_pods - 1);
     dr = a.pod_digit[jj];
@@ -85,108 +81,174 @@ __global__ __launch_bounds__(64) void seq_cap1_kernel(SeqArgs a) {
   };
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
-  // lane jl of the block's outputs: the selected node (o_a) and status | scored << 2 (o_b)
+  // Per lane (pod jl of the block): the code bits as all-ones / all-zero masks, ~tolerates, and flags
+  // (bit 0: no commit — a score error, or past the batch's end; bit 1: the pod's code is a digit).
+  uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, NT = 0, FL = 0;
+  // The block's outputs, lane jl = pod jl: identity-like modes keep the scan's first available match (o_a)
+  // and the class fallback at the decision (o_b), decoded by the lanes at the store; KX modes keep the
+  // decoded node (o_a) and status | scored << 2 (o_b).
   int32_t o_a = -1, o_b = 0;
+  uint32_t fl_done = 0;  // the stored block's flags
   auto store_block = [&](int32_t j0, int32_t cnt) {
     if (lane < cnt) {
-      a.out_idx[j0 + lane] = o_a;
-      if (a.out_score) a.out_score[j0 + lane] = (o_b & 4) ? sm : 0;
-      a.out_status[j0 + lane] = o_b & 3;
+      int32_t sel, st;
+      int64_t sc;
+      if constexpr (KX) {
+        sel = o_a;
+        st = o_b & 3;
+        sc = (o_b & 4) ? sm : 0;
+      } else {  // decode_ident: FitError when the class had no available node, then the score error
+        const bool fit = (uint32_t)o_b == NONE, hit = (uint32_t)o_a != NONE;
+        st = fit ? 1 : ((fl_done & 1u) ? 2 : 0);
+        sel = st ? -1 : (hit ? o_a : o_b);
+        sc = (st == 0 && hit) ? sm : 0;
+      }
+      a.out_idx[j0 + lane] = sel;
+      if (a.out_score) a.out_score[j0 + lane] = sc;
+      a.out_status[j0 + lane] = st;
     }
   };
-  // The previous pod's commit, resolved after the next pod's scan: its node (-1: none) and the node's count
-  // before it (an LDS read in flight). The wave alone owns the counts, so the commit is a plain read, then
-  // (one pod later) a write of count + 1: LDS operations of a wave complete in order, so a later pod's read
-  // of the same node, issued after that write, sees it.
-  int32_t pend = -1, pend_cnt = 0;
-  uint32_t pkv = 0;
   for (int32_t jb = 0; jb < a.n_pods; jb += WAVE) {
     if (jb > 0) store_block(jb - WAVE, WAVE);
     {
-      // lane word: code | does-not-tolerate << 4 | score error << 5. The identity-like decode is folded in
-      // here, once per 64 pods by the lanes: a pod whose NodeNumber score errors (no PreScore state, or a
-      // name without a digit; decode_ident) or is not scored at all never takes a match, so its code
-      // becomes CODE_NONE_POD and its scan finds none; per pod the scalar unit then only picks the match
-      // or the class's first available node.
       const bool ok = jb + lane < a.n_pods;
       const bool dig = ok && dn >= 0 && dn <= 9, tl = ok && tn != 0;
-      const bool serr = !KX && (idec.err_all || (idec.err_nodigit && !dig));
+      // KX: decode_pod reads the code (the score error is its own); identity-like: a pod that cannot take
+      // a match (its score errors, or NodeNumber does not score) scans with the code that matches nothing
+      const bool serr = !ok || (!KX && (idec.err_all || (idec.err_nodigit && !dig)));
       const bool code = KX ? dig : (dig && idec.use_im && !serr);
-      pkv = (code ? (uint32_t)dn : CODE_NONE_POD) | (tl ? 0u : 16u) | (serr ? 32u : 0u);
+      const uint32_t c = code ? (uint32_t)dn : CODE_NONE_POD;
+      P0 = 0u - (c & 1u);
+      P1 = 0u - ((c >> 1) & 1u);
+      P2 = 0u - ((c >> 2) & 1u);
+      P3 = 0u - ((c >> 3) & 1u);
+      NT = tl ? 0u : 0xFFFFFFFFu;
+      FL = (serr ? 1u : 0u) | (dig ? 2u : 0u);
     }
+    fl_done = FL;
     load_raw(jb + WAVE, dn, tn);
     const int32_t je = min(jb + WAVE, a.n_pods);
-    for (int32_t j = jb; j < je; ++j) {
-      const int32_t jl = j - jb;
-      const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pkv, jl);
-      const uint32_t p0 = 0u - (pk & 1u), p1 = 0u - ((pk >> 1) & 1u), p2 = 0u - ((pk >> 2) & 1u),
-                     p3 = 0u - ((pk >> 3) & 1u);
-      const bool tol = ((pk >> 4) & 1u) == 0;
-      uint32_t cm = NONE, cx = NONE;  // the first available match / non-match (KX)
-      auto scan = [&](const uint32_t (&av)[RS]) {
-        cm = cx = NONE;
+    for (int32_t j0 = jb; j0 < je; j0 += U) {
+      const int32_t jl0 = j0 - jb;
+      // ---- the U pods' masks (wave-uniform, SGPRs) and scans against the step's starting state ----
+      uint32_t p0[U], p1[U], p2[U], p3[U], nt[U], fl[U], cm[U], cx[U];
 #pragma unroll
-        for (int r = RS - 1; r >= 0; --r) {
-          const uint32_t base = lane_base + (uint32_t)(32 * r);
-          uint32_t dm = D0[r] ^ p0;
-          dm = or_xor_vs(dm, D1[r], p1);
-          dm = or_xor_vs(dm, D2[r], p2);
-          dm = or_xor_vs(dm, D3[r], p3);
-          cm = umin(cm, base | ffbl(bop3_andn(av[r], dm)));
-          if (KX) cx = umin(cx, base | ffbl(av[r] & dm));
-        }
-        cm = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_first(cm));
-        if (KX) cx = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_first(cx));
+      for (int u = 0; u < U; ++u) {
+        p0[u] = (uint32_t)__builtin_amdgcn_readlane((int)P0, jl0 + u);
+        p1[u] = (uint32_t)__builtin_amdgcn_readlane((int)P1, jl0 + u);
+        p2[u] = (uint32_t)__builtin_amdgcn_readlane((int)P2, jl0 + u);
+        p3[u] = (uint32_t)__builtin_amdgcn_readlane((int)P3, jl0 + u);
+        nt[u] = (uint32_t)__builtin_amdgcn_readlane((int)NT, jl0 + u);
+        fl[u] = (uint32_t)__builtin_amdgcn_readlane((int)FL, jl0 + u);
+        cm[u] = cx[u] = NONE;
+      }
+      // one pod's first available match (and non-match) in this lane's words: the class's availability by
+      // a select on ~tolerates (nt ? AV0 : AV1), the code compare ORed over the four code planes
+      auto scan_word = [&](int r, int u, uint32_t& m, uint32_t& x) {
+        const uint32_t base = lane_base + (uint32_t)(32 * r);
+        uint32_t dm = D0[r] ^ p0[u];
+        dm = bop3_or_xor(dm, D1[r], p1[u]);
+        dm = bop3_or_xor(dm, D2[r], p2[u]);
+        dm = bop3_or_xor(dm, D3[r], p3[u]);
+        const uint32_t av = __builtin_amdgcn_bitop3_b32(AV1[r], AV0[r], nt[u], 0xD8);  // nt ? AV0 : AV1
+        m = umin(m, base | ffbl(bop3_andn(av, dm)));
+        if (KX) x = umin(x, base | ffbl(av & dm));
       };
-      if (tol) scan(AV1);
-      else scan(AV0);
-      // the previous pod's commit: did its node just fill?
-      const int32_t c = __builtin_amdgcn_readfirstlane(pend_cnt) + 1;
-      if (pend >= 0) {
-        lcnt[pend] = c;  // every lane stores the same value
-        if (c >= max_pods) {
-          const uint32_t w = (uint32_t)pend >> 5, q = w / RS, rs = w % RS;
-          const uint32_t m = (uint32_t)lane == q ? (1u << (pend & 31)) : 0u;
+#pragma unroll
+      for (int r = RS - 1; r >= 0; --r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) scan_word(r, u, cm[u], cx[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        cm[u] = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_first(cm[u]));
+        if (KX) cx[u] = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_first(cx[u]));
+      }
+      // ---- the placement of pod u from its scan and the current class fallback: node (NONE: no commit);
+      // lane values: identity-like modes the scan's first match and the fallback (decoded per block), KX
+      // modes the decoded node and status | scored << 2 ----
+      auto decide = [&](int u, int32_t& va, int32_t& vb) -> uint32_t {
+        const uint32_t ca = nt[u] ? ca0 : ca1;
+        if constexpr (KX) {
+          int32_t sel, st;
+          int64_t sc;
+          decode_pod(cm[u] != NONE ? (int64_t)cm[u] : -1, cx[u] != NONE ? (int64_t)cx[u] : -1,
+                     ca != NONE ? (int64_t)ca : -1, (fl[u] & 2u) != 0, pp, &sel, &sc, &st);
+          sel = __builtin_amdgcn_readfirstlane(sel);
+          st = __builtin_amdgcn_readfirstlane(st);
+          va = sel;
+          vb = st | (sc != 0 ? 4 : 0);
+          return (st == 0 && !(fl[u] & 1u)) ? (uint32_t)sel : NONE;
+        } else {
+          va = (int32_t)cm[u];
+          vb = (int32_t)ca;
+          return (fl[u] & 1u) ? NONE : (cm[u] != NONE ? cm[u] : ca);  // ca NONE: FitError, no commit
+        }
+      };
+      // the placements at the step's start (final unless an earlier pod of the step fills a node), and
+      // their counts (one batch of LDS reads)
+      uint32_t node[U];
+      int32_t va[U], vb[U], cnt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        node[u] = decide(u, va[u], vb[u]);
+        cnt[u] = lcnt[node[u] != NONE ? node[u] : 0u];
+      }
+      // ---- in pod order: the commit, and a fill's effect on the later pods ----
+      bool filled[U];
+      bool any_fill = false;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        filled[u] = false;
+        bool fresh = false;  // the placement changed since the count was read
+        if (any_fill) {
+          // a scan result an earlier pod of this step filled: scan again against the current planes; the
+          // class fallback may have moved too, so the placement is decided again
+          bool redo = false;
+#pragma unroll
+          for (int v = 0; v < u; ++v)
+            redo = redo || (filled[v] && (node[v] == cm[u] || (KX && node[v] == cx[u])));
+          if (redo) {
+            uint32_t m = NONE, x = NONE;
+#pragma unroll
+            for (int r = RS - 1; r >= 0; --r) scan_word(r, u, m, x);
+            cm[u] = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_first(m));
+            if (KX) cx[u] = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_first(x));
+          }
+          const uint32_t n2 = decide(u, va[u], vb[u]);
+          fresh = n2 != node[u];
+          node[u] = n2;
+        }
+        write_lane2(o_a, o_b, va[u], vb[u], jl0 + u);
+        const uint32_t n = node[u];
+        if (n == NONE) continue;
+        // the node's count before this commit (NodeInfo.AddPod): the step's read plus the earlier pods of
+        // the step that committed to it (their writes follow the read)
+        int32_t c;
+        if (!fresh) {
+          c = __builtin_amdgcn_readfirstlane(cnt[u]);
+#pragma unroll
+          for (int v = 0; v < u; ++v) c += node[v] == n ? 1 : 0;
+        } else {
+          c = __builtin_amdgcn_readfirstlane(lcnt[n]);  // after every earlier commit's write (LDS in order)
+        }
+        lcnt[n] = c + 1;  // every lane stores the same value
+        if (c + 1 >= max_pods) {  // the node is full: out of both classes' availability
+          filled[u] = true;
+          any_fill = true;
+          const uint32_t w = n >> 5, q = w / RS, rs = w % RS;
+          const uint32_t bit = (uint32_t)lane == q ? (1u << (n & 31)) : 0u;
 #pragma unroll
           for (int r = 0; r < RS; ++r)
             if ((uint32_t)r == rs) {
-              AV0[r] &= ~m;
-              AV1[r] &= ~m;
+              AV0[r] &= ~bit;
+              AV1[r] &= ~bit;
             }
-          if (cm == (uint32_t)pend || (KX && cx == (uint32_t)pend)) {  // this pod chose it: decide again
-            if (tol) scan(AV1);
-            else scan(AV0);
-          }
-          if (ca0 == (uint32_t)pend) ca0 = first_avail(AV0);
-          if (ca1 == (uint32_t)pend) ca1 = first_avail(AV1);
+          if (ca0 == n) ca0 = first_avail(AV0);
+          if (ca1 == n) ca1 = first_avail(AV1);
         }
       }
-      const uint32_t ca = tol ? ca1 : ca0;
-      int32_t sel, st;
-      if constexpr (KX) {
-        int64_t sc;
-        decode_pod(cm != NONE ? (int64_t)cm : -1, cx != NONE ? (int64_t)cx : -1, ca != NONE ? (int64_t)ca : -1,
-                   (pk & 15u) != CODE_NONE_POD, pp, &sel, &sc, &st);
-        st |= sc != 0 ? 4 : 0;
-      } else {  // decode_ident with the score error from the lane word (a pod with one has no match)
-        const bool fit = ca == NONE, serr = (pk >> 5) & 1u, hit = cm != NONE;
-        st = fit ? 1 : (serr ? 2 : (hit ? 4 : 0));
-        sel = st & 3 ? -1 : (int32_t)(hit ? cm : ca);
-      }
-      // wave-uniform by construction (every input is): kept in SGPRs, so the commit and the next pod's
-      // resolve branch on the scalar unit instead of masking lanes
-      sel = __builtin_amdgcn_readfirstlane(sel);
-      st = __builtin_amdgcn_readfirstlane(st);
-      write_lane2(o_a, o_b, sel, st, jl);
-      st &= 3;
-      // commit (NodeInfo.AddPod): the node's count is read now and used after the next scan; the read is
-      // issued for every pod (of node 0 when there is no commit), so that exactly one read is in flight
-      // at the resolve and the compiler's wait for it lands there, not earlier
-      pend = st == 0 ? sel : -1;
-      pend_cnt = lcnt[st == 0 ? sel : 0];
     }
   }
-  if (pend >= 0) lcnt[pend] = __builtin_amdgcn_readfirstlane(pend_cnt) + 1;  // the last pod's commit
   if (a.n_pods > 0) {
     const int32_t j0 = (a.n_pods - 1) & ~(WAVE - 1);
     store_block(j0, a.n_pods - j0);
@@ -196,11 +258,13 @@ __global__ __launch_bounds__(64) void seq_cap1_kernel(SeqArgs a) {
 }
 
 namespace {
+constexpr int SEQ_CAP_AHEAD = 4;  // pods per step of seq_capu_kernel
+
 template <int RS>
-hipError_t launch_cap1_rs(const SeqArgs& a, hipStream_t s) {
+hipError_t launch_capu_rs(const SeqArgs& a, hipStream_t s) {
   const size_t lds = (size_t)a.n_words * 32 * sizeof(int32_t);  // <= 32 KB (8,192 nodes)
-  if (needs_kx(a.pp)) MSH_TIMED_LAUNCH((seq_cap1_kernel<RS, true>), dim3(1), dim3(WAVE), lds, s, a);
-  else MSH_TIMED_LAUNCH((seq_cap1_kernel<RS, false>), dim3(1), dim3(WAVE), lds, s, a);
+  if (needs_kx(a.pp)) MSH_TIMED_LAUNCH((seq_capu_kernel<RS, true, SEQ_CAP_AHEAD>), dim3(1), dim3(WAVE), lds, s, a);
+  else MSH_TIMED_LAUNCH((seq_capu_kernel<RS, false, SEQ_CAP_AHEAD>), dim3(1), dim3(WAVE), lds, s, a);
   return hipGetLastError();
 }
 }  // namespace
@@ -208,10 +272,10 @@ hipError_t launch_cap1_rs(const SeqArgs& a, hipStream_t s) {
 hipError_t launch_seq_capacity(const SeqArgs& a, int nw, int rs, hipStream_t s) {
   using seqlaunch::launch_seq_nw;
   if (nw == 1) {
-    if (rs <= 1) return launch_cap1_rs<1>(a, s);
-    if (rs <= 2) return launch_cap1_rs<2>(a, s);
-    if (rs <= 3) return launch_cap1_rs<3>(a, s);
-    return launch_cap1_rs<4>(a, s);
+    if (rs <= 1) return launch_capu_rs<1>(a, s);
+    if (rs <= 2) return launch_capu_rs<2>(a, s);
+    if (rs <= 3) return launch_capu_rs<3>(a, s);
+    return launch_capu_rs<4>(a, s);
   }
   if (nw == 4) return launch_seq_nw<4, true, 1>(a, rs, 1, s);
   return launch_seq_nw<16, true, 1>(a, rs, 1, s);

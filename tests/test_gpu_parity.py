@@ -412,6 +412,30 @@ def test_sequential_plugin_sets(msh, oracle, combo, norm, seq_waves):
                 assert (ctx.node_pod_counts() == want_counts).all(), what
 
 
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+def test_sequential_capacity_fills(msh, gpu_ctx, oracle, norm):
+    """The capacity form decides 4 pods per step against the step's starting state and resolves them in
+    order: a pod whose match, non-match or class fallback an earlier pod of the step fills is decided
+    again, and counts of several pods of one step on one node add up. Capacities 1 and 2 fill nodes
+    inside nearly every step; runs of pods with one digit land on one node; tiny tables run out of
+    nodes (FitError mid-batch); batch sizes are not multiples of 4 or 64; the counts carry over into a
+    second call. Against the oracle's serial loop, in every normalize mode."""
+    rng = np.random.default_rng(1700 + norm)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, norm)
+    _set(gpu_ctx, msh, ps)
+    for n in (1, 33, 64, 500, 8192):
+        u, nd, pd, pt = _rand_case(rng, n, 2003, p_unsched=0.3, p_tol=0.3)
+        pd[100:400] = pd[100]  # a run of one digit
+        for cap in (1, 2, 4, 15):
+            gpu_ctx.upload_nodes(u, nd)  # zeroes the counts
+            a = gpu_ctx.schedule_sequential(pd[:999], pt[:999], cap)
+            b = gpu_ctx.schedule_sequential(pd[999:], pt[999:], cap)
+            want_i, want_s, want_st, want_counts = oracle.c_schedule_sequential(u, nd, pd, pt, ps, cap)
+            what = f"capacity fills norm={norm} n={n} cap={cap}"
+            _assert_same(tuple(np.concatenate([x, y]) for x, y in zip(a, b)), (want_i, want_s, want_st), what)
+            assert (gpu_ctx.node_pod_counts() == want_counts).all(), what
+
+
 @pytest.mark.parametrize("norm", [0, 3])
 def test_sequential_large_tables(msh, gpu_ctx, oracle, norm):
     """Tables far past the round-1 cap of 12,288 nodes: 300,000 nodes (15 scanning waves x 10 words
