@@ -160,11 +160,13 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
   // (stage 3: the class fixes the extents, hence every normalized value): the CLASS TERM of node i for
   // class k, Σ over the columns of weight x NormalizeScore(raw), is staged with the node, once per class.
   constexpr bool CT = TS || NNC > 0;
-  // dynamic LDS: the tile (records, then [TN][2] class terms when the list has score columns), then the
-  // slice-merge area
+  // staged terms per node: one per class with a normalizing column; without one the columns' part is the
+  // node-only sum, the same for both classes: one
+  constexpr int NCT = NNC > 0 ? 2 : (TS ? 1 : 0);
+  // dynamic LDS: the tile (records, then [TN][NCT] class terms), then the slice-merge area
   uint2* s_cx = reinterpret_cast<uint2*>(s_dyn);
   Key* s_ct = reinterpret_cast<Key*>(s_cx + TN);
-  char* s_merge = reinterpret_cast<char*>(s_ct + (CT ? 2 * (size_t)TN : 0));
+  char* s_merge = reinterpret_cast<char*>(s_ct + NCT * (size_t)TN);
   // per class (0: pods that do not tolerate the unschedulable taint, 1: pods that do) and normalizing
   // column: the reciprocal and the min-max offset of its NormalizeScore
   __shared__ double s_crr[2][NC], s_cbb[2][NC];
@@ -439,9 +441,11 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
         const int dg = a.digit[i];
         xm = (a.has_nu && a.unsched[i]) ? 0xFFFFFFFFu : 0u;
         s_cx[k] = make_uint2((dg >= 0 && dg <= 9) ? (uint32_t)dg : GEN_CODE_NONE, xm);
-        if constexpr (CT) {
+        if constexpr (NCT == 2) {
           s_ct[2 * k] = class_term(0, i);
           s_ct[2 * k + 1] = class_term(1, i);
+        } else if constexpr (NCT == 1) {
+          s_ct[k] = class_term(0, i);
         }
       }
       const uint64_t m = __ballot(in && xm == 0u);
@@ -468,7 +472,8 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       t = nbase[b] + __builtin_amdgcn_ubfe(nsel[b], code, 1) * ndelta[b];
     else
       t = code == pcode[b] ? L[b].k1 : L[b].k0;
-    if constexpr (CT) t += ntol[b] ? ct0 : ct1;
+    if constexpr (NCT == 2) t += ntol[b] ? ct0 : ct1;
+    else if constexpr (NCT == 1) t += ct0;
     return key_mask<KT>(t, xm, ntol[b]);
   };
 
@@ -501,9 +506,11 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       };
       auto node = [&](int32_t k) {
         Key ct0 = 0, ct1 = 0;
-        if constexpr (CT) {
+        if constexpr (NCT == 2) {
           ct0 = s_ct[2 * k];
           ct1 = s_ct[2 * k + 1];
+        } else if constexpr (NCT == 1) {
+          ct0 = ct1 = s_ct[k];
         }
         node_v(s_cx[k], ct0, ct1);
       };
@@ -511,15 +518,18 @@ __global__ __launch_bounds__(GEN_W * WAVE) void generic_kernel(GenericArgs a) {
       auto node_pair = [&](int32_t k2) {  // nodes 2 k2, 2 k2 + 1
         const gen_u4 c2 = reinterpret_cast<const gen_u4*>(s_cx)[k2];
         Key ct[4] = {0, 0, 0, 0};  // node 2 k2's class terms, then node 2 k2 + 1's
-        if constexpr (CT && !W64) {
+        if constexpr (NCT == 2 && !W64) {
           const gen_u4 t4 = reinterpret_cast<const gen_u4*>(s_ct)[k2];
           ct[0] = t4.x;
           ct[1] = t4.y;
           ct[2] = t4.z;
           ct[3] = t4.w;
-        } else if constexpr (CT) {
+        } else if constexpr (NCT == 2) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) ct[q] = s_ct[4 * k2 + q];
+        } else if constexpr (NCT == 1) {  // one term per node: both classes read it
+          ct[0] = ct[1] = s_ct[2 * k2];
+          ct[2] = ct[3] = s_ct[2 * k2 + 1];
         }
         node_v(make_uint2(c2.x, c2.y), ct[0], ct[1]);
         node_v(make_uint2(c2.z, c2.w), ct[2], ct[3]);
@@ -745,9 +755,9 @@ hipError_t launch_generic(GenericArgs& a, int mode, const DeviceInfo& dev, hipSt
   if (maxp == 0) return hipSuccess;
   const bool general = a.nnc > 1;  // launch_gen_mode's forms for two or more normalizing columns
   const size_t key = (a.w64 || (general && a.nnc > 2)) ? 8 : 4;  // launch_gen_mode's key type
-  // bytes per staged node: the record, and the two class terms when the list has score columns (the kernel's
-  // CT: the general form, a node-only sum or a normalizing column)
-  const size_t per_node = 8 + ((general || a.nts > 0 || a.nnc > 0) ? 2 * key : 0);
+  // bytes per staged node: the record, and the kernel's NCT terms: one per class with a normalizing column
+  // (the general form included), one node-only sum otherwise, none for NodeNumber alone
+  const size_t per_node = 8 + ((general || a.nnc > 0) ? 2 * key : (a.nts > 0 ? key : 0));
   int32_t tile = (int32_t)(GEN_LDS_BUDGET / per_node) & ~(GEN_CHUNK - 1);
   tile = std::max<int32_t>(GEN_CHUNK, std::min<int32_t>(tile, (a.n_nodes + GEN_CHUNK - 1) & ~(GEN_CHUNK - 1)));
   a.tile = tile;

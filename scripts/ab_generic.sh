@@ -6,13 +6,15 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${OUT:-gpurun_out/r6f}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for variant in ${VARIANTS:-cur gen_s3 old_gen}; do
+# LISTS: "mode weight norm colnorm" entries separated by ';'
+IFS=';' read -ra LST <<< "${LISTS:-generic_col 1 0 0;generic_2col 1 0 0;generic 3 1 0;generic 1 0 0;generic_w64 1 0 0;generic_w64 1 0 1}"
+for variant in ${VARIANTS:-cur gen_base}; do
   lib=$PWD/mini-kube-scheduler_amd/libminisched_hip.so
   [ "$variant" != cur ] && lib=$PWD/scripts/expt/$variant/libminisched_hip.so
-  for m in "generic_col 1 0" "generic_2col 1 0" "generic 3 1" "generic 1 0"; do
+  for m in "${LST[@]}"; do
     set -- $m
-    tag=${variant}_$1_$2_$3
-    MSH_LIBRARY=$lib WEIGHT=$2 NORM=$3 MODE=$1 PODS=100000 LAUNCHES=10 timeout -k 10 120 rocprofv3 --kernel-trace --stats \
+    tag=${variant}_$1_$2_$3_$4
+    COLNORM=$4 MSH_LIBRARY=$lib WEIGHT=$2 NORM=$3 MODE=$1 PODS=100000 LAUNCHES=10 timeout -k 10 120 rocprofv3 --kernel-trace --stats \
       -d "$OUT/$tag" -o run --output-format csv -- python3 scripts/run_batch.py > "$OUT/$tag.log" 2>&1 || { echo "[$tag] failed"; exit 1; }
     python3 - "$OUT/$tag" "$tag" <<'PY'
 import csv, sys, pathlib

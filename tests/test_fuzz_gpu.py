@@ -1,5 +1,5 @@
-"""Randomised GPU parity sweep (opt-in: MSH_FUZZ=<cases>; skipped otherwise, so the regular suite never
-runs it).
+"""Randomised GPU parity sweep: a bounded sweep in every GPU run (BOUNDED_CASES cases of at most
+BOUNDED_PAIRS (pod, node) pairs each, a seed base of its own), and the long opt-in sweep (MSH_FUZZ=<cases>).
 
 Each case draws a table size, a pod count, the filter / prescore lists, a score list of NodeNumber and up to
 three score-column plugins with random weights and NormalizeScore modes, columns of random range (small,
@@ -28,10 +28,14 @@ COLS = ["ScoreColumn0", "ScoreColumn1", "ScoreColumn2", "ScoreColumn3"]
 WEIGHTS = [1, 2, 3, 7, 100, 1 << 16, 1 << 32]
 
 
-def _case(rng):
+BOUNDED_CASES = 500
+BOUNDED_PAIRS = 2e7
+
+
+def _case(rng, max_pairs=1.5e8):
     n = int(np.exp(rng.uniform(0, np.log(60_000))))
     p = int(np.exp(rng.uniform(0, np.log(30_000))))
-    while n * p > 1.5e8:
+    while n * p > max_pairs:
         p //= 2
     p = max(p, 1)
     unsched = (rng.random(n) < rng.choice([0.0, 0.1, 0.5, 1.0])).astype(np.uint8)
@@ -60,11 +64,19 @@ def _case(rng):
     return n, p, unsched, nd, pd, pt, filters, prescore, score, weights, norms, cols
 
 
+def test_fuzz_parity_bounded(msh, oracle):
+    """The bounded sweep of every GPU run: fixed seeds 20261100.., cases small enough for well under a minute (120 cases: 1 s on MI355X)."""
+    _sweep(msh, oracle, BOUNDED_CASES, 20261100, BOUNDED_PAIRS, Path("gpurun_out/fuzz_bounded_summary.json"))
+
+
 @pytest.mark.skipif(CASES <= 0, reason="opt-in sweep: set MSH_FUZZ=<cases>")
 def test_fuzz_parity(msh, oracle):
-    out = Path(os.environ.get("MSH_FUZZ_OUT", "gpurun_out/fuzz_summary.json"))
+    _sweep(msh, oracle, CASES, int(os.environ.get("MSH_FUZZ_SEED", "20261018")), 1.5e8,
+           Path(os.environ.get("MSH_FUZZ_OUT", "gpurun_out/fuzz_summary.json")))
+
+
+def _sweep(msh, oracle, CASES, seed0, max_pairs, out):
     out.parent.mkdir(parents=True, exist_ok=True)
-    seed0 = int(os.environ.get("MSH_FUZZ_SEED", "20261018"))
     torch = pytest.importorskip("torch")
     stats = {"batch": 0, "batch_w_columns": 0, "patch_then_multi_batch": 0, "node_sharded": 0, "sequential": 0,
              "sequential_capacity": 0, "pairs": 0}
@@ -74,7 +86,7 @@ def test_fuzz_parity(msh, oracle):
         for c in range(CASES):
             seed = seed0 + c
             rng = np.random.default_rng(seed)
-            n, p, u, nd, pd, pt, fl, pre, sc, w, nm, cols = _case(rng)
+            n, p, u, nd, pd, pt, fl, pre, sc, w, nm, cols = _case(rng, max_pairs)
             ps = oracle.PluginSet(filters=fl, prescore=pre, score=sc, weights=w, normalize=nm)
             ctx.set_plugins(fl, pre, [msh.ScorePluginConfig(s, ww, msh.Normalize(m)) for s, ww, m in zip(sc, w, nm)])
             ctx.upload_nodes(u, nd)
