@@ -25,7 +25,9 @@ template <int RS, bool KX, int U>
 __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
   static_assert(WAVE % U == 0, "a step never straddles a 64-pod block");
   constexpr uint32_t NONE = 0xFFFFFFFFu;
-  extern __shared__ int32_t lcnt[];  // [n_words * 32] pods per node: carried in, updated, written back
+  // [n_words * 32 + 1] pods per node: carried in, updated, written back; the extra slot is the read target
+  // of a placement without a commit (an index min(node, slots), no branch)
+  extern __shared__ int32_t lcnt[];
   const int lane = threadIdx.x;
   const int32_t slots = a.n_words * 32;
   for (int32_t i = lane; i < slots; i += WAVE) {
@@ -38,6 +40,7 @@ __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
     }
     lcnt[i] = c;
   }
+  if (lane == 0) lcnt[slots] = 0;
   __syncthreads();
   int32_t max_pods = a.max_pods;
   asm volatile("" : "+s"(max_pods));
@@ -67,6 +70,7 @@ __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_first(f));
   };
   uint32_t ca0 = first_avail(AV0), ca1 = first_avail(AV1);  // each class's first available node
+  uint32_t cax = ca0 ^ ca1;  // a pod's fallback is ca1 ^ (cax & ~tolerates): two scalar ops, no compare
   __builtin_amdgcn_s_waitcnt(0);
 
   PluginParams pp = a.pp;
@@ -123,7 +127,8 @@ __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
       P2 = 0u - ((c >> 2) & 1u);
       P3 = 0u - ((c >> 3) & 1u);
       NT = tl ? 0u : 0xFFFFFFFFu;
-      FL = (serr ? 1u : 0u) | (dig ? 2u : 0u);
+      // KX: flags (bit 0 no commit, bit 1 a digit); identity-like: the no-commit mask, ORed into the placement
+      FL = KX ? ((serr ? 1u : 0u) | (dig ? 2u : 0u)) : (serr ? NONE : 0u);
     }
     fl_done = FL;
     load_raw(jb + WAVE, dn, tn);
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
       // lane values: identity-like modes the scan's first match and the fallback (decoded per block), KX
       // modes the decoded node and status | scored << 2 ----
       auto decide = [&](int u, int32_t& va, int32_t& vb) -> uint32_t {
-        const uint32_t ca = nt[u] ? ca0 : ca1;
+        const uint32_t ca = ca1 ^ (cax & nt[u]);
         if constexpr (KX) {
           int32_t sel, st;
           int64_t sc;
@@ -181,17 +186,18 @@ __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
         } else {
           va = (int32_t)cm[u];
           vb = (int32_t)ca;
-          return (fl[u] & 1u) ? NONE : (cm[u] != NONE ? cm[u] : ca);  // ca NONE: FitError, no commit
+          return (cm[u] != NONE ? cm[u] : ca) | fl[u];  // ca NONE: FitError; fl all-ones: no commit
         }
       };
       // the placements at the step's start (final unless an earlier pod of the step fills a node), and
       // their counts (one batch of LDS reads)
-      uint32_t node[U];
+      uint32_t node[U], ci[U];
       int32_t va[U], vb[U], cnt[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         node[u] = decide(u, va[u], vb[u]);
-        cnt[u] = lcnt[node[u] != NONE ? node[u] : 0u];
+        ci[u] = umin(node[u], (uint32_t)slots);  // NONE reads the spare slot
+        cnt[u] = lcnt[ci[u]];
       }
       // ---- in pod order: the commit, and a fill's effect on the later pods ----
       bool filled[U];
@@ -229,9 +235,10 @@ __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
 #pragma unroll
           for (int v = 0; v < u; ++v) c += node[v] == n ? 1 : 0;
         } else {
+          ci[u] = n;
           c = __builtin_amdgcn_readfirstlane(lcnt[n]);  // after every earlier commit's write (LDS in order)
         }
-        lcnt[n] = c + 1;  // every lane stores the same value
+        lcnt[ci[u]] = c + 1;  // every lane stores the same value (ci[u] == n here)
         if (c + 1 >= max_pods) {  // the node is full: out of both classes' availability
           filled[u] = true;
           any_fill = true;
@@ -245,6 +252,7 @@ __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
             }
           if (ca0 == n) ca0 = first_avail(AV0);
           if (ca1 == n) ca1 = first_avail(AV1);
+          cax = ca0 ^ ca1;
         }
       }
     }
@@ -262,7 +270,7 @@ constexpr int SEQ_CAP_AHEAD = 4;  // pods per step of seq_capu_kernel
 
 template <int RS>
 hipError_t launch_capu_rs(const SeqArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)a.n_words * 32 * sizeof(int32_t);  // <= 32 KB (8,192 nodes)
+  const size_t lds = ((size_t)a.n_words * 32 + 1) * sizeof(int32_t);  // <= 32 KB + 4 B (8,192 nodes)
   if (needs_kx(a.pp)) MSH_TIMED_LAUNCH((seq_capu_kernel<RS, true, SEQ_CAP_AHEAD>), dim3(1), dim3(WAVE), lds, s, a);
   else MSH_TIMED_LAUNCH((seq_capu_kernel<RS, false, SEQ_CAP_AHEAD>), dim3(1), dim3(WAVE), lds, s, a);
   return hipGetLastError();
