@@ -127,7 +127,8 @@ def seq_kernel_label(n_nodes: int, cap: bool = False, kx: bool = False) -> str:
     if cap and nw == 1:  # msh_seq_cap.hip: one wave, 4 pods per step, counts in LDS, availability planes
         return f"void msh::seq_capu_kernel<{r}, {str(kx).lower()}, 4>"
     u = 1 if cap else 4  # SEQ_AHEAD: pods decided per step without a capacity
-    return f"void msh::seq_kernel<{r}, {nw}, {str(kx).lower()}, {str(cap).lower()}, {u}>"
+    # the last parameter: pod waves per pod-block workgroup (msh_internal.h SEQ_POD_WAVES, 1)
+    return f"void msh::seq_kernel<{r}, {nw}, {str(kx).lower()}, {str(cap).lower()}, {u}, 1>"
 
 
 def parse():
