@@ -30,6 +30,8 @@ if mode == "generic":
     options["batch_kernel"] = "generic"
 if os.environ.get("SPLIT", "auto") == "serial":
     options["seq_split"] = "serial"
+if os.environ.get("SEQ_WAVES"):
+    options["seq_waves"] = os.environ["SEQ_WAVES"]  # msh_options.seq_waves: 1, 4, 15, 16 scanning waves
 cap = int(os.environ.get("CAP", 0))
 
 import torch  # noqa: E402
