@@ -412,6 +412,33 @@ def test_sequential_plugin_sets(msh, oracle, combo, norm, seq_waves):
                 assert (ctx.node_pod_counts() == want_counts).all(), what
 
 
+@pytest.mark.parametrize("norm", [0, 3])
+def test_empty_node_table(msh, gpu_ctx, oracle, norm):
+    """A cluster without nodes (the reference's List returns none, minisched.go:40): every pod is a
+    FitError in the batch, multi-batch and sequential entry points, with and without a capacity, and no
+    node count exists; then a one-node table on the same ctx schedules again."""
+    rng = np.random.default_rng(40 + norm)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, norm)
+    _set(gpu_ctx, msh, ps)
+    u0, nd0 = np.zeros(0, np.uint8), np.zeros(0, np.int8)
+    pd, pt = _rand_case(rng, 1, 700)[2:]
+    gpu_ctx.upload_nodes(u0, nd0)
+    want = oracle.c_schedule_batch(u0, nd0, pd, pt, ps)
+    assert (want[2] == 1).all()
+    _assert_same(gpu_ctx.schedule_batch(pd, pt), want, "empty table batch")
+    for cap in (0, 3):
+        _assert_same(gpu_ctx.schedule_sequential(pd, pt, cap), want, f"empty table seq cap={cap}")
+    assert gpu_ctx.node_pod_counts().size == 0
+    u1, nd1 = np.zeros(1, np.uint8), np.array([int(pd[0]) if pd[0] >= 0 else 4], np.int8)
+    gpu_ctx.upload_nodes(u1, nd1)
+    for cap in (0, 3):
+        gpu_ctx.reset_node_pod_counts()
+        got = gpu_ctx.schedule_sequential(pd, pt, cap)
+        wi, ws, wst, wc = oracle.c_schedule_sequential(u1, nd1, pd, pt, ps, cap)
+        _assert_same(got, (wi, ws, wst), f"one-node table seq cap={cap}")
+        assert (gpu_ctx.node_pod_counts() == wc).all()
+
+
 @pytest.mark.parametrize("norm", [0, 1, 2, 3])
 def test_sequential_capacity_fills(msh, gpu_ctx, oracle, norm):
     """The capacity form decides 4 pods per step against the step's starting state and resolves them in
