@@ -85,8 +85,9 @@ __global__ __launch_bounds__(64) void seq_capu_kernel(SeqArgs a) {
   };
   int32_t dn = 0, tn = 0;
   if (a.n_pods > 0) load_raw(0, dn, tn);
-  // Per lane (pod jl of the block): the code bits as all-ones / all-zero masks, ~tolerates, and flags
-  // (bit 0: no commit — a score error, or past the batch's end; bit 1: the pod's code is a digit).
+  // Per lane (pod jl of the block): the code bits as all-ones / all-zero masks, ~tolerates, and FL: in the
+  // KX modes flags (bit 0: no commit — past the batch's end; bit 1: the pod's code is a digit), in the
+  // identity-like modes the no-commit mask (all-ones for a score error or a pod past the batch's end).
   uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, NT = 0, FL = 0;
   // The block's outputs, lane jl = pod jl: identity-like modes keep the scan's first available match (o_a)
   // and the class fallback at the decision (o_b), decoded by the lanes at the store; KX modes keep the
