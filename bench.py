@@ -116,9 +116,9 @@ def seq_shape(n_nodes: int, cap: bool = False):
     """seq_kernel's register layout for a table (launch_sequential): words per lane RS, scanning waves NW."""
     words = max(-(-n_nodes // 1024) * 1024, 1024) // 32
     rs = lambda nw: -(-words // (nw * 64))
-    nw = 1 if rs(1) <= 4 else 4 if rs(4) <= 4 else (16 if cap else 15)
+    nw = 1 if rs(1) <= (16 if cap else 4) else 4 if rs(4) <= 4 else (16 if cap else 15)
     r = rs(nw)
-    rsv = {1: [1, 2, 3, 4], 4: [2, 4]}.get(nw, [4, 8] if cap else [4, 8, 12])
+    rsv = {1: [1, 2, 3, 4, 6, 8, 12, 16] if cap else [1, 2, 3, 4], 4: [2, 4]}.get(nw, [4, 8] if cap else [4, 8, 12])
     return next(v for v in rsv if r <= v), nw
 
 

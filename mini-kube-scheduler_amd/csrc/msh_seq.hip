@@ -17,9 +17,12 @@ int seq_waves_for(const SeqArgs& a, const DeviceInfo& dev) {
   const bool cap = a.max_pods > 0;
   const int nw_big = cap ? 16 : 15;
   auto rs_for = [&](int nw) { return (a.n_words + nw * WAVE - 1) / (nw * WAVE); };
-  int nw = dev.seq_waves > 0 ? dev.seq_waves : (rs_for(1) <= 4 ? 1 : rs_for(4) <= 4 ? 4 : nw_big);
+  // one wave holds up to 4 words per lane (8,192 nodes), 16 with a capacity (32,768: seq_capu_kernel, whose
+  // one wave outruns the 4- and 16-wave forms, profiles/ab/r6_seq_waves.txt)
+  const int rs1 = cap ? 16 : 4;
+  int nw = dev.seq_waves > 0 ? dev.seq_waves : (rs_for(1) <= rs1 ? 1 : rs_for(4) <= 4 ? 4 : nw_big);
   if (nw != 1 && nw != 4) nw = nw_big;
-  if (rs_for(nw) > (nw == nw_big ? (cap ? 8 : 12) : 4)) nw = nw_big;  // an override too small for the table
+  if (rs_for(nw) > (nw == nw_big ? (cap ? 8 : 12) : nw == 1 ? rs1 : 4)) nw = nw_big;  // an override too small for the table
   return nw;
 }
 
@@ -60,7 +63,9 @@ hipError_t launch_sequential(const SeqArgs& a, const DeviceInfo& dev, hipStream_
   const int rs_max = cap ? 8 : 12;
   const int nw = seq_waves_for(a, dev);
   const int rs = (a.n_words + nw * WAVE - 1) / (nw * WAVE);
-  if (rs > rs_max) {
+  // words per lane each form holds: one wave 16 with a capacity (seq_capu_kernel) and 4 without, four
+  // waves 4, the big form rs_max (seq_waves_for only picks a form the table fits, the big one last)
+  if (rs > (nw == 1 ? (cap ? 16 : 4) : nw == 4 ? 4 : rs_max)) {
     if (err)
       *err = "sequential mode keeps the node table in registers: at most " +
              std::to_string(nw_big * WAVE * rs_max * 32) + " nodes per device" + (cap ? " with a capacity" : "");

@@ -271,9 +271,16 @@ constexpr int SEQ_CAP_AHEAD = 4;  // pods per step of seq_capu_kernel
 
 template <int RS>
 hipError_t launch_capu_rs(const SeqArgs& a, hipStream_t s) {
-  const size_t lds = ((size_t)a.n_words * 32 + 1) * sizeof(int32_t);  // <= 32 KB + 4 B (8,192 nodes)
-  if (needs_kx(a.pp)) MSH_TIMED_LAUNCH((seq_capu_kernel<RS, true, SEQ_CAP_AHEAD>), dim3(1), dim3(WAVE), lds, s, a);
-  else MSH_TIMED_LAUNCH((seq_capu_kernel<RS, false, SEQ_CAP_AHEAD>), dim3(1), dim3(WAVE), lds, s, a);
+  const size_t lds = ((size_t)a.n_words * 32 + 1) * sizeof(int32_t);  // <= 128 KB + 4 B (32,768 nodes)
+  auto kx = seq_capu_kernel<RS, true, SEQ_CAP_AHEAD>;
+  auto id = seq_capu_kernel<RS, false, SEQ_CAP_AHEAD>;
+  if (lds > 64 * 1024) {
+    const void* k = needs_kx(a.pp) ? reinterpret_cast<const void*>(kx) : reinterpret_cast<const void*>(id);
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  if (needs_kx(a.pp)) MSH_TIMED_LAUNCH(kx, dim3(1), dim3(WAVE), lds, s, a);
+  else MSH_TIMED_LAUNCH(id, dim3(1), dim3(WAVE), lds, s, a);
   return hipGetLastError();
 }
 }  // namespace
@@ -284,7 +291,11 @@ hipError_t launch_seq_capacity(const SeqArgs& a, int nw, int rs, hipStream_t s) 
     if (rs <= 1) return launch_capu_rs<1>(a, s);
     if (rs <= 2) return launch_capu_rs<2>(a, s);
     if (rs <= 3) return launch_capu_rs<3>(a, s);
-    return launch_capu_rs<4>(a, s);
+    if (rs <= 4) return launch_capu_rs<4>(a, s);
+    if (rs <= 6) return launch_capu_rs<6>(a, s);
+    if (rs <= 8) return launch_capu_rs<8>(a, s);
+    if (rs <= 12) return launch_capu_rs<12>(a, s);
+    return launch_capu_rs<16>(a, s);
   }
   if (nw == 4) return launch_seq_nw<4, true, 1>(a, rs, 1, s);
   return launch_seq_nw<16, true, 1>(a, rs, 1, s);

@@ -6,10 +6,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${OUT:-gpurun_out/abw}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for w in 1 4 16; do
-  for cap in 0 15; do
-    tag=w${w}_cap$cap
-    SEQ_WAVES=$w SPLIT=serial CAP=$cap WEIGHT=1 NORM=0 MODE=sequential PODS=100000 LAUNCHES=3 timeout -k 10 120 \
+for w in ${WAVES:-1 4 16}; do
+  for cap in ${CAPS:-0 15}; do
+    tag=n${NODES:-5000}_w${w}_cap$cap
+    NODES=${NODES:-5000} SEQ_WAVES=$w SPLIT=serial CAP=$cap WEIGHT=1 NORM=0 MODE=sequential PODS=100000 LAUNCHES=3 timeout -k 10 120 \
       rocprofv3 --kernel-trace --stats -d "$OUT/$tag" -o run --output-format csv -- python3 scripts/run_batch.py \
       > "$OUT/$tag.log" 2>&1 || { echo "[$tag] failed"; exit 1; }
     python3 - "$OUT/$tag" "$tag" <<'PY'

@@ -450,7 +450,7 @@ def test_sequential_capacity_fills(msh, gpu_ctx, oracle, norm):
     rng = np.random.default_rng(1700 + norm)
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 3, norm)
     _set(gpu_ctx, msh, ps)
-    for n in (1, 33, 64, 500, 8192):
+    for n in (1, 33, 64, 500, 8192, 12289, 16384, 24577, 32768):  # one wave up to 32,768 nodes (16 words per lane)
         u, nd, pd, pt = _rand_case(rng, n, 2003, p_unsched=0.3, p_tol=0.3)
         pd[100:400] = pd[100]  # a run of one digit
         for cap in (1, 2, 4, 15):
