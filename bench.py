@@ -109,7 +109,7 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2
-    return f"void msh::pair_kernel<{sl}, {b(shard)}, {b(kx)}>"
+    return f"void msh::pair_kernel<{sl}, {b(shard)}, {b(kx)}, false>"
 
 
 def seq_shape(n_nodes: int, cap: bool = False):
@@ -512,11 +512,32 @@ def valu_roofline(kname, launch_ms, evals, model_lane_ops_per_eval, cus, entry, 
     }
 
 
-def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=False, cap=0):
+def seq_pair_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False) -> str:
+    """The kernel of a no-capacity sequential launch (msh_capi.cpp msh_schedule_sequential_device, auto):
+    pair_kernel<S, false, KX, true>, the scalar-plane per-pair kernel with the commit epilogue."""
+    groups = max(-(-n_nodes // 1024) * 1024, 1024) // 256
+    waves = -(-n_pods // 64)
+    sl = 1
+    while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
+        sl *= 2
+    return f"void msh::pair_kernel<{sl}, false, {str(kx).lower()}, true>"
+
+
+def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=False, cap=0, form="pair"):
     """Roofline of the dominant kernel, per launch: algorithmic work of one launch / the launch's
     average duration, measured with HIP events at the kernel's start and completion (bench.py main),
     the quantity rocprofv3's per-kernel average reports."""
     launch_s = launch_ms * 1e-3
+    if mode == "sequential" and not serial and not cap and form == "pair":
+        # Without a capacity (auto): the per-pair kernel over the whole batch with the commit epilogue (each
+        # wave adds its placed pods to the node counts, one device atomic per distinct node)
+        kname = seq_pair_label(n_local, p, cus)
+        n_pad = max(-(-n_local // 1024) * 1024, 1024)
+        model = PAIR_VALU_PER_WORD * (n_pad / 32) * (-(-p // 64) * 64) / (float(n_local) * p)
+        return valu_roofline(kname, launch_ms, float(n_local) * p, model, cus,
+                             pmc_entry("sequential_pair", kname, n_local, p, 1, plugin_tag(HEADLINE_WEIGHT, HEADLINE_NORM)),
+                             f"{PAIR_VALU_PER_WORD} VALU per 32-node word and 64-pod wave (pair_kernel's scan, "
+                             "msh_pair.hip); the commit epilogue is in the counter form")
     if mode == "sequential" and not serial:
         # Without a capacity the pods run in blocks of consecutive pods, one workgroup each (a wave per
         # block walks its pods in order, every pod against the whole register-resident table): VALU-bound
@@ -871,18 +892,23 @@ def measure_extras(torch, dev, msh, synth, D, closed_form_modes, cus):
         ok = same(g, want) and (counts == R * np.bincount(g[0][placed], minlength=n)).all()
         return ms, ok
 
-    for key, c, R, serial in (("c5_sequential", ctx, 20, False),
-                              ("c5_sequential_serial", new_ctx({"seq_split": "serial"}), 3, True)):
-        if serial:
+    forms = {"pair": "no capacity (auto): the per-pair batch kernel over the whole batch with the commit epilogue "
+                     "(each wave adds its placed pods to the node counts, one device atomic per distinct node); "
+                     "no commit feeds a later decision, so the placements are the batch's",
+             "blocks": "no capacity (msh_options.seq_split blocks): blocks of 64 consecutive pods, one workgroup "
+                       "each, the pods within a block in order; node counts added by device atomics",
+             "serial": "one workgroup walks all 100,000 pods in order"}
+    for key, form, R in (("c5_sequential", "pair", 20), ("c5_sequential_blocks", "blocks", 20),
+                         ("c5_sequential_serial", "serial", 3)):
+        c = ctx if form == "pair" else new_ctx({"seq_split": form})
+        if form != "pair":
             c.upload_nodes(u, nd)
         ms, ok = c5(c, R)
-        out[key] = {"kernel": seq_kernel_label(n), "ms_per_step": ms, "us_per_pod": ms * 1e3 / p,
-                    "pods_per_s": p / (ms * 1e-3), "evals_per_s": n * p / (ms * 1e-3),
-                    "form": ("one workgroup walks all 100,000 pods in order" if serial else
-                             "no capacity: blocks of consecutive pods, one workgroup each, every block in order; "
-                             "node counts added by device atomics"),
+        kname = seq_pair_label(n, p, cus) if form == "pair" else seq_kernel_label(n)
+        out[key] = {"kernel": kname, "ms_per_step": ms, "us_per_pod": ms * 1e3 / p,
+                    "pods_per_s": p / (ms * 1e-3), "evals_per_s": n * p / (ms * 1e-3), "form": forms[form],
                     "check": (f"seq == batch (closed form), node counts == {R} x placements" if ok else "MISMATCH"),
-                    "roofline": make_roofline("sequential", n, p, ms, 1, cus, serial=serial)}
+                    "roofline": make_roofline("sequential", n, p, ms, 1, cus, serial=form == "serial", form=form)}
         c.close()
 
     # ---- C5 with a capacity (15 pods per node, the reference list): the one sequential form in which a

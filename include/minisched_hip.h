@@ -129,7 +129,8 @@ typedef struct msh_options {
   int32_t pair_noax;    /* 0 auto | 1 LDS form: group 0 first, settled reductions dropped | 2 group 0 last */
   int32_t pair_slices;  /* 0 auto | 1, 2, 4 slice waves per 64-pod block (and generic_kernel pod group) */
   int32_t seq_waves;    /* 0 auto | 1, 4, 15, 16 scanning waves of the sequential kernel (raised when too few) */
-  int32_t seq_split;    /* 0 auto (no capacity: 64-pod blocks) | 1 one workgroup walks the whole batch */
+  int32_t seq_split;    /* 0 auto (no capacity: the batch kernel + counts) | 1 one workgroup walks the
+                           whole batch | 2 64-pod blocks of consecutive pods, one workgroup each */
   int32_t seq_pod_waves; /* 0 auto | 1, 2, 4, 8 waves sharing a 64-pod block (one scanning wave, no capacity) */
   int32_t gen_keys;     /* 0 auto (64-bit totals below 2^53 as double keys) | 1 uint64 keys */
   int32_t gen_nnkey;    /* 0 auto (compare-free NodeNumber key) | 1 compare + select */
@@ -251,10 +252,11 @@ int msh_schedule_batches_device(msh_ctx* ctx, int32_t nb, const msh_batch* batch
  * NodeInfo.AddPod analogue). max_pods_per_node > 0 additionally makes a node infeasible
  * once it holds that many pods (build extension): one workgroup walks the whole batch. 0 =
  * reference semantics, where no commit feeds a later decision and the placements equal
- * msh_schedule_batch's: tables up to 32,768 nodes then run as 64-pod blocks of consecutive pods,
- * one workgroup each. The blocks run CONCURRENTLY and only the pods within one block are ordered: a
- * no-capacity shortcut, exact because the counts the blocks add are the same in any order
- * (msh_options.seq_split = 1 walks the whole batch in one workgroup, in order, as a capacity does).
+ * msh_schedule_batch's: tables up to 32,768 nodes then run on the per-pair batch kernel, whose waves
+ * add their placed pods to the counts (a no-capacity shortcut: the pods are not decided in order, exact
+ * because the counts are the same in any order). msh_options.seq_split = 2 runs 64-pod blocks of
+ * consecutive pods instead, one workgroup each, concurrently, the pods within a block in order; = 1
+ * walks the whole batch in one workgroup, in order, as a capacity does.
  * `commit_cb` (may be NULL) is replayed on the host after the device run, in
  * placement order, once per PLACED pod. The counts carry over from call to call; sequential launches
  * of one ctx on different streams are ordered by the library (each waits for the ones in flight). */

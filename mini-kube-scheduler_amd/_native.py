@@ -98,7 +98,7 @@ OPTION_NAMES = {
     "pair_noax": {"auto": 0, "noax": 1, "axlast": 2},
     "pair_slices": {"auto": 0},
     "seq_waves": {"auto": 0},
-    "seq_split": {"auto": 0, "serial": 1},
+    "seq_split": {"auto": 0, "serial": 1, "blocks": 2},
     "seq_pod_waves": {"auto": 0},
     "gen_keys": {"auto": 0, "f53": 0, "u64": 1},
     "gen_nnkey": {"auto": 0, "select": 1},

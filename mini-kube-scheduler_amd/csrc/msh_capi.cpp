@@ -603,7 +603,7 @@ bool apply_options(const msh_options& o, msh::DeviceInfo& d, std::string* err) {
   };
   if (!in("batch_kernel", o.batch_kernel, {0, 1}) || !in("pair_planes", o.pair_planes, {0, 1, 2}) ||
       !in("pair_noax", o.pair_noax, {0, 1, 2}) || !in("pair_slices", o.pair_slices, {0, 1, 2, 4}) ||
-      !in("seq_waves", o.seq_waves, {0, 1, 4, 15, 16}) || !in("seq_split", o.seq_split, {0, 1}) ||
+      !in("seq_waves", o.seq_waves, {0, 1, 4, 15, 16}) || !in("seq_split", o.seq_split, {0, 1, 2}) ||
       !in("seq_pod_waves", o.seq_pod_waves, {0, 1, 2, 4, 8}) ||
       !in("gen_keys", o.gen_keys, {0, 1}) || !in("gen_nnkey", o.gen_nnkey, {0, 1}))
     return false;
@@ -612,7 +612,7 @@ bool apply_options(const msh_options& o, msh::DeviceInfo& d, std::string* err) {
   d.pair_noax = o.pair_noax == 0 ? -1 : (o.pair_noax == 1 ? 1 : 0);
   d.bits_slices = o.pair_slices;
   d.seq_waves = o.seq_waves;
-  d.seq_split = o.seq_split == 0 ? 1 : 0;
+  d.seq_split = o.seq_split == 0 ? 2 : (o.seq_split == 1 ? 0 : 1);
   d.seq_pod_waves = o.seq_pod_waves;
   d.gen_f53 = o.gen_keys == 0 ? 1 : 0;
   d.gen_nnkey = o.gen_nnkey == 0 ? 1 : 0;
@@ -1058,7 +1058,13 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   a.counts = c->d_counts;
   a.count_stride = (int64_t)c->counts_cap;
   a.count_replicas = c->counts_replicas;
-  const bool split = msh::seq_blocks(a, c->dev) > 1;
+  // Without a capacity no commit feeds a later decision (the counts are read by nothing the plugins
+  // score): the default runs the per-pair batch kernel with the commit epilogue (pair_kernel<CNT>, every
+  // placed pod's count added to a replica), whose placements are msh_schedule_batch's; seq_split = 2 keeps
+  // the sequential kernel's 64-pod blocks, = 1 one workgroup walking the batch in order
+  const bool pair_form = max_pods_per_node == 0 && c->dev.seq_split == 2 && p > msh::WAVE &&
+                         c->counts_replicas == msh::SEQ_COUNT_REPLICAS;
+  const bool split = pair_form || msh::seq_blocks(a, c->dev) > 1;
   a.fold = !split && c->counts_dirty ? 1 : 0;
   // one sequential launch of a ctx at a time: each commits into (and a fold rewrites) the same counts,
   // so this stream first waits for the ctx's sequential launches in flight on other streams
@@ -1070,7 +1076,15 @@ int msh_schedule_sequential_device(msh_ctx* c, int32_t p, const int8_t* d_pod_di
   a.out_status = d_out_status;
   std::string err;
   hipError_t e;
-  {
+  if (pair_form) {
+    msh::PairArgs pa = pair_args(c);
+    pa.nb = 1;
+    pa.d[0] = msh::BatchDesc{d_pod_digit, d_pod_tol, d_out_idx, d_out_score, d_out_status, p, 0};
+    pa.counts = c->d_counts;
+    pa.count_stride = (int64_t)c->counts_cap;
+    TimedLaunch tl(c);
+    e = msh::launch_pairs(pa, false, c->dev, s);
+  } else {
     TimedLaunch tl(c);
     e = msh::launch_sequential(a, c->dev, s, &err);
   }

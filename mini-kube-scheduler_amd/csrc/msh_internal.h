@@ -50,9 +50,10 @@ struct DeviceInfo {
   // against 89.0 us per 32-batch C3 launch), 0 for the identity-like modes (77.3-78.3 against
   // 80.9-81.2), profiles/r4_ab_pair_planes.txt
   int pair_noax = -1;
-  // msh_options.seq_split: without a capacity, the sequential kernel's pods in blocks of consecutive
-  // pods, one workgroup each (auto, 1), or all in one workgroup (serial, 0)
-  int seq_split = 1;
+  // msh_options.seq_split, without a capacity: the per-pair batch kernel with the commit epilogue (auto,
+  // 2), the sequential kernel's 64-pod blocks of consecutive pods, one workgroup each (1), or the whole
+  // batch in one workgroup, in order (serial, 0)
+  int seq_split = 2;
   int seq_pod_waves = 0;  // msh_options.seq_pod_waves: pod waves per pod-block workgroup (1, 2, 4, 8), 0 = auto
   int gen_f53 = 1;    // msh_options.gen_keys: generic_kernel's double keys for 64-bit totals below 2^53 (1) or uint64_t (0)
   int gen_nnkey = 1;  // msh_options.gen_nnkey: generic_kernel's compare-free NodeNumber key (1) or the select (0)
@@ -135,6 +136,10 @@ struct PairArgs {
   PluginParams pp;
   int64_t node_base;       // shard mode: global index of local node 0
   int32_t* keys;           // shard mode: [2 * d[0].n_pods] keys (first feasible match, non-match)
+  // sequential mode without a capacity (one batch): every placed pod adds 1 to its node's count in
+  // replica (64-pod block mod SEQ_COUNT_REPLICAS) of these SEQ_COUNT_REPLICAS arrays; null otherwise
+  int32_t* counts;
+  int64_t count_stride;
   BatchDesc d[MULTI_MAX];
 };
 hipError_t launch_pairs(PairArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s);
@@ -224,10 +229,12 @@ struct SeqArgs {
   int32_t pods_per_block;    // set by the launcher: pods per workgroup (the whole batch when one workgroup)
 };
 
-// Pod blocks add their commits to one of this many count replicas: a digit's pods all land on its
-// first feasible match, and device atomics from every block onto one address queue. Tables up to
-// SEQ_SPLIT_MAX_NODES only (pod blocks count in LDS), so larger ones keep one count array.
-constexpr int SEQ_COUNT_REPLICAS = 16;
+// No-capacity sequential launches (pair_kernel's commit epilogue, seq_kernel's pod blocks) add their
+// commits to one of this many count replicas: a digit's pods all land on its first feasible match, and
+// device atomics from every wave onto one address queue. Per C5 launch (pair_kernel<4, .., true>,
+// profiles/ab/r6_seq_pair_replicas.txt): 16 replicas 15.5 us, 64 8.5 us, 256 8.5 us (6.99 without the
+// epilogue). Tables up to SEQ_SPLIT_MAX_NODES only, so larger ones keep one count array.
+constexpr int SEQ_COUNT_REPLICAS = 64;
 constexpr int32_t SEQ_SPLIT_MAX_NODES = 4 * 64 * 4 * 32;  // four scanning waves x 64 lanes x 4 words
 // Workgroups launch_sequential runs the batch on: 64-pod blocks without a capacity on tables whose
 // counts fit LDS (DeviceInfo::seq_split), else 1.

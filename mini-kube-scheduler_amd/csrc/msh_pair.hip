@@ -168,7 +168,7 @@ __device__ __forceinline__ uint32_t group_first_or_none(const uint32_t* __restri
   return m < GROUP_NODES ? g * GROUP_NODES + m : NOFIT;
 }
 
-template <int S, bool SHARD, bool KX>
+template <int S, bool SHARD, bool KX, bool CNT>
 __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
   constexpr int PB = PAIR_WAVES / S;  // 64-pod blocks per workgroup
   __shared__ uint32_t s_res[S > 1 ? PAIR_WAVES : 1][2][WAVE];
@@ -291,6 +291,23 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
     d.out_idx[j] = oi;
     if (d.out_score) d.out_score[j] = osc;  // optional output (NULL: not written)
     d.out_status[j] = ost;
+    if constexpr (CNT) {
+      // sequential mode without a capacity (msh_schedule_sequential_device): the commit of every placed
+      // pod, NodeInfo.AddPod's count (minisched.go:89-112 binds it), one device atomic per distinct node
+      // of the wave (a digit's pods all land on its first feasible match), into count replica
+      // (block mod SEQ_COUNT_REPLICAS) so that the atomics of many waves do not queue on one address (all
+      // waves reach it at about the same time: 16 replicas cost 8.5 us per C5 launch, 64 cost 1.5)
+      const uint32_t node = ost == 0 ? (uint32_t)oi : NOFIT;
+      uint64_t pend = __ballot(ost == 0);
+      int32_t* cnt = a.counts + (size_t)((((int32_t)blockIdx.x * PB + pb)) % SEQ_COUNT_REPLICAS) * a.count_stride;
+      while (pend) {
+        const int ld = (int)__builtin_ctzll(pend);
+        const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)node, ld);
+        const uint64_t same = __ballot(node == n);
+        if (lane == ld) atomicAdd(cnt + n, (int32_t)__popcll(same));
+        pend &= ~same;
+      }
+    }
   }
 }
 
@@ -757,8 +774,15 @@ int pair_slices(int64_t waves, int32_t n_groups, const DeviceInfo& dev) {
 template <int S, bool SHARD, bool KX>
 hipError_t launch_pair_s(PairArgs& a, int32_t bx, hipStream_t s) {
   a.gps = (a.n_groups + S - 1) / S;
-  MSH_TIMED_LAUNCH((pair_kernel<S, SHARD, KX>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PAIR_WAVES * WAVE), 0, s,
-                   a);
+  if constexpr (!SHARD) {
+    if (a.counts) {
+      MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, true>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PAIR_WAVES * WAVE),
+                       0, s, a);
+      return hipGetLastError();
+    }
+  }
+  MSH_TIMED_LAUNCH((pair_kernel<S, SHARD, KX, false>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PAIR_WAVES * WAVE), 0,
+                   s, a);
   return hipGetLastError();
 }
 
@@ -780,7 +804,8 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   // (big: two 16-wave workgroups per CU fill it from 32 blocks per CU on; 4-wave workgroups from 64 waves
   // per CU)
   const int64_t min_waves = (int64_t)dev.cus * (big ? 2 * PL_WAVES_BIG : 64);
-  const bool lds = (fits || big) && (dev.pair_planes == 2 ||
+  // (counting launches, sequential mode: always scalar-loaded planes, whose kernel has the commit epilogue)
+  const bool lds = !a.counts && (fits || big) && (dev.pair_planes == 2 ||
                                      (dev.pair_planes == 0 && waves >= min_waves && dev.bits_slices == 0));
   if (lds) {
     const int w = big ? PL_WAVES_BIG : PL_WAVES;
@@ -810,7 +835,8 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_pairs(PairArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s) {
-  if (a.nb <= 0 || a.nb > MULTI_MAX || (shard && a.nb != 1)) return hipErrorInvalidValue;
+  if (a.nb <= 0 || a.nb > MULTI_MAX || (shard && a.nb != 1) || (a.counts && (shard || a.nb != 1)))
+    return hipErrorInvalidValue;
   // KX: the normalize mode needs each pod's first feasible non-match (REVERSE, MINMAX)
   if (needs_kx(a.pp)) return shard ? launch_pair_t<true, true>(a, dev, s) : launch_pair_t<false, true>(a, dev, s);
   return shard ? launch_pair_t<true, false>(a, dev, s) : launch_pair_t<false, false>(a, dev, s);

@@ -159,7 +159,8 @@ __global__ __launch_bounds__(seq_threads(NW, CAP, PW)) void seq_kernel(SeqArgs a
   // one device atomic per node it reached, into count replica blockIdx % SEQ_COUNT_REPLICAS. A digit's
   // pods all land on its first feasible match, so device atomics from every block onto one array queue
   // on about ten addresses. Per C5 launch (1,563 blocks): one atomic per commit 149 us, one per block
-  // and node 26 us, the same over 16 replicas 11.6 us (11.3 without any add). (Merging 32 blocks'
+  // and node 26 us, the same over 16 replicas 11.6 us (11.3 without any add; 64 replicas since the
+  // pair form's epilogue needs them, msh_internal.h). (Merging 32 blocks'
   // counts through staging rows and a last-block ticket needs an agent-scope release per block, an L2
   // write-back on MI355X: 52 us.)
   constexpr bool LDSC = NW <= 4;

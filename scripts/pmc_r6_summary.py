@@ -10,7 +10,8 @@ only when all of them match what it timed):
   generic_ref     generic_kernel on the reference list (w=1 NONE), 32 batches
   generic_hl      generic_kernel on the headline list (w=3 DefaultNormalizeScore: extents pass + main pass), 32 batches
   generic_col     generic_kernel on NodeNumber + a DEFAULT-normalized score column, 32 batches
-  sequential      seq_kernel at C5 (headline list), pod blocks over workgroups (no capacity: the default)
+  sequential_pair  C5 (headline list) without a capacity, auto: pair_kernel with the commit epilogue
+  sequential      seq_kernel at C5 (headline list), pod blocks over workgroups (msh_options.seq_split blocks)
   sequential_serial  the same with msh_options.seq_split serial (one workgroup walks all pods)
   sequential_capacity  seq_kernel at C5 with a capacity of 15 pods per node (the reference list, w=1)
 FETCH_SIZE / WRITE_SIZE are KiB (x 1024); FETCH_SIZE is reported raw and with MI355X_MICROARCH.md's x2
@@ -62,6 +63,7 @@ for mode, prefix, tags, nb, plug in (
         ("generic_ref", "msh::generic_kernel", ("g_sq",), NB, tag_of(1, 0)),
         ("generic_hl", "msh::generic_kernel", ("gh_sq",), NB, tag_of(3, 1)),
         ("generic_col", "msh::generic_kernel", ("gc_sq", "gc_sq2"), NB, tag_of(1, 0) + " + ScoreColumn0 w=2 norm=1"),
+        ("sequential_pair", "msh::pair_kernel", ("sp_sq", "sp_sq2"), 1, tag_of(3, 1)),
         ("sequential", "msh::seq_kernel", ("s_sq", "s_sq2"), 1, tag_of(3, 1)),
         ("sequential_serial", "msh::seq_kernel", ("ss_sq",), 1, tag_of(3, 1)),
         ("sequential_capacity", "msh::seq_cap", ("c_sq", "c_sq2", "c_fetch"), 1, tag_of(1, 0) + " cap=15")):
@@ -106,7 +108,7 @@ for tag, prefix in (("stats", "msh::pair"), ("stats_k20", "msh::pair"),
                     ("stats_rev", "msh::pair"), ("stats_single", "msh::pair"),
                     ("stats_generic", "msh::generic_kernel"), ("stats_generic_hl", "msh::generic_kernel"),
                     ("stats_generic_col", "msh::generic_kernel"),
-                    ("stats_seq", "msh::seq_kernel"), ("stats_seq_serial", "msh::seq_kernel"),
+                    ("stats_seq_pair", "msh::pair_kernel"), ("stats_seq", "msh::seq_kernel"), ("stats_seq_serial", "msh::seq_kernel"),
                     ("stats_seq_cap", "msh::seq_cap")):
     name, avg, calls = stats_avg_ns(tag, prefix)
     if name:

@@ -5,8 +5,9 @@
 #  trace  --kernel-trace --stats of each hot kernel alone (scripts/run_batch.py, C3: 5,000 nodes x 100,000
 #         pods per batch): the per-pair kernel, 32 batches per launch, with the headline plugins (NodeNumber
 #         w=3 DefaultNormalizeScore), the reference's w=1 list, MIN-MAX and REVERSE at w=3; generic_kernel on
-#         the reference list, the headline list and NodeNumber + a DEFAULT column; seq_kernel (C5): pod
-#         blocks, one workgroup (serial), and the capacity form (15 pods per node);
+#         the reference list, the headline list and NodeNumber + a DEFAULT column; C5: the auto
+#         no-capacity form (pair_kernel with the commit epilogue), seq_kernel's pod blocks, one workgroup
+#         (serial), and the capacity form (15 pods per node);
 #  pmc    one --pmc pass per counter set (never combined with tracing).
 # Summary: scripts/pmc_r6_summary.py -> $OUT/r6_pmc_c3.json (copied to profiles/; bench.py reads it for
 # the counter fractions and the HBM traffic of its rooflines).
@@ -41,7 +42,8 @@ if has trace; then
   tr stats_generic generic 1 0 || exit 1
   tr stats_generic_hl generic 3 1 || exit 1
   tr stats_generic_col generic_col 1 0 || exit 1
-  tr stats_seq sequential 3 1 || exit 1
+  tr stats_seq_pair sequential 3 1 || exit 1
+  SPLIT=blocks tr stats_seq sequential 3 1 || exit 1
   SPLIT=serial tr stats_seq_serial sequential 3 1 || exit 1
   CAP=15 LAUNCHES=5 tr stats_seq_cap sequential 1 0 || exit 1
 fi
@@ -65,8 +67,10 @@ if has pmc; then
   pass gh_sq generic 3 1 $SQ1 || exit 1
   pass gc_sq generic_col 1 0 $SQ1 || exit 1
   pass gc_sq2 generic_col 1 0 $SQ2 || exit 1
-  pass s_sq sequential 3 1 $SQ1 || exit 1
-  pass s_sq2 sequential 3 1 $SQ2 || exit 1
+  pass sp_sq sequential 3 1 $SQ1 || exit 1
+  pass sp_sq2 sequential 3 1 $SQ2 || exit 1
+  SPLIT=blocks pass s_sq sequential 3 1 $SQ1 || exit 1
+  SPLIT=blocks pass s_sq2 sequential 3 1 $SQ2 || exit 1
   SPLIT=serial pass ss_sq sequential 3 1 $SQ1 || exit 1
   CAP=15 LAUNCHES=3 pass c_sq sequential 1 0 $SQ1 || exit 1
   CAP=15 LAUNCHES=3 pass c_sq2 sequential 1 0 $SQ2 || exit 1

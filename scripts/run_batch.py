@@ -12,8 +12,9 @@ MODE
   generic_2col generic_kernel's general form: NodeNumber + a DEFAULT and a MIN-MAX column, 32 batches per launch
   generic_w64  generic_kernel's 64-bit form: NodeNumber + ScoreColumn0 over the whole int32 range (COLNORM:
                the column's normalizer), 32 batches per launch
-  sequential   C5: each pod in order (seq_kernel; SPLIT=serial: the whole batch in one workgroup; CAP=k: a
-               capacity of k pods per node, the counts reset before every launch)
+  sequential   C5: no capacity, auto: the per-pair kernel with the commit epilogue (SPLIT=blocks: seq_kernel's
+               64-pod blocks; SPLIT=serial: the whole batch in one workgroup, in order; CAP=k: a capacity of k
+               pods per node, the counts reset before every launch)
 NORM / WEIGHT: msh_normalize and weight of the NodeNumber entry (bench.py's headline: WEIGHT=3 NORM=1).
 NB: batches per launch in the multi-batch modes (default 32).
 Kernel overrides go to msh_create_ex as msh_options (the library reads no environment variable)."""
@@ -28,8 +29,8 @@ mode = os.environ.get("MODE", "multi")
 options = {}
 if mode == "generic":
     options["batch_kernel"] = "generic"
-if os.environ.get("SPLIT", "auto") == "serial":
-    options["seq_split"] = "serial"
+if os.environ.get("SPLIT", "auto") in ("serial", "blocks"):
+    options["seq_split"] = os.environ["SPLIT"]
 if os.environ.get("SEQ_WAVES"):
     options["seq_waves"] = os.environ["SEQ_WAVES"]  # msh_options.seq_waves: 1, 4, 15, 16 scanning waves
 cap = int(os.environ.get("CAP", 0))

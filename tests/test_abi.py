@@ -86,7 +86,7 @@ def test_options_are_checked_before_any_device_call(msh):
     lib = N.lib()
     h = C.c_void_p()
     for field, bad in (("batch_kernel", 2), ("pair_planes", 3), ("pair_noax", -1), ("pair_slices", 3),
-                       ("seq_waves", 2), ("seq_split", 2), ("seq_pod_waves", 3), ("gen_keys", 5), ("gen_nnkey", 9)):
+                       ("seq_waves", 2), ("seq_split", 3), ("seq_pod_waves", 3), ("gen_keys", 5), ("gen_nnkey", 9)):
         o = N.make_options({field: bad})
         assert lib.msh_create_ex(0, C.byref(o), C.byref(h)) == N.MSH_ERR_INVALID, field
         assert field in lib.msh_last_error(None).decode()

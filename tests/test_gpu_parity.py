@@ -287,16 +287,18 @@ def test_sequential(msh, oracle, n, max_pods, seq_waves):
             _assert_same(got, ctx.schedule_batch(pd, pt), "seq == batch")
 
 
-@pytest.mark.parametrize("split", ["auto", "serial"])
+@pytest.mark.parametrize("norm", [0, 1, 2, 3])
+@pytest.mark.parametrize("split", ["auto", "blocks", "serial"])
 @pytest.mark.parametrize("seq_waves,n", [("1", 1000), ("4", 8193), ("16", 40000)])
-def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split):
-    """Without a capacity the sequential kernel splits the pods into blocks of consecutive pods, one
-    workgroup each (msh_options.seq_split auto, tables up to 32,768 nodes; the 40,000-node table stays in one
-    workgroup), or walks them all in one workgroup (serial): both give the serial loop's placements and
-    node counts, for batch sizes around the 64-pod block edges and with counts carried over between
-    calls (the blocks add theirs with device atomics)."""
+def test_sequential_pod_blocks(msh, oracle, seq_waves, n, split, norm):
+    """Without a capacity no commit feeds a later decision. Auto (msh_options.seq_split 0) runs the per-pair
+    batch kernel with the commit epilogue (every placed pod's count added to a count replica, tables up to
+    32,768 nodes); "blocks" the sequential kernel's 64-pod blocks of consecutive pods, one workgroup each;
+    "serial" one workgroup walking every pod in order (the 40,000-node table stays in one workgroup in
+    every form). All give the serial loop's placements and node counts, for batch sizes around the
+    64-pod block edges, in every normalize mode, with counts carried over between calls."""
     rng = np.random.default_rng(n + 77)
-    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, 3)
+    ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
     p = 20_000 if n < 10_000 else 6_000  # (the oracle's serial loop is n x p)
     u, nd, pd, pt = _rand_case(rng, n, p, p_unsched=0.2, p_tol=0.1)
     with msh.DeviceContext(0, {"seq_waves": seq_waves, "seq_split": split}) as ctx:
@@ -323,7 +325,7 @@ def test_sequential_pod_waves(msh, oracle, pod_waves, norm):
     rng = np.random.default_rng(31 * pod_waves + norm)
     ps = _plugins(oracle, ["NodeUnschedulable"], ["NodeNumber"], ["NodeNumber"], 2, norm)
     u, nd, pd, pt = _rand_case(rng, 3000, 20_037, p_unsched=0.2, p_tol=0.1)
-    with msh.DeviceContext(0, {"seq_pod_waves": pod_waves}) as ctx:
+    with msh.DeviceContext(0, {"seq_pod_waves": pod_waves, "seq_split": "blocks"}) as ctx:
         _set(ctx, msh, ps)
         ctx.upload_nodes(u, nd)
         cuts = [0, 1, 64, 65, 70, 191, 10_000, 20_037]
