@@ -193,29 +193,46 @@ int check_ids(msh_ctx* c, const int32_t* ids, int32_t n, int kind, const char* w
 
 // After a *_device launch on caller stream s: (re-)record the ctx's event for s. One event per
 // stream the ctx has launched on (a linear search: callers use a handful of streams).
-int record_on(msh_ctx* c, std::vector<std::pair<hipStream_t, hipEvent_t>>& evs, hipStream_t s) {
+// The events only say that launches finished (a table version or the counts may then be rewritten on
+// the device, or freed): no host reads what those launches wrote through them, so they are recorded
+// without the system-scope fence (hipEventDisableSystemFence; a kernel's own end-of-kernel release at
+// agent scope writes back L2 on gfx950). With the fence each record put ~5 us on the stream: one-batch
+// launches back to back 12-14 -> 8-9.5 us each, profiles/ab/r6_event_fence.txt.
+int record_on(msh_ctx* c, std::vector<std::pair<hipStream_t, hipEvent_t>>& evs, hipStream_t s,
+              hipEvent_t* out = nullptr) {
   for (auto& e : evs)
     if (e.first == s) {
       MSH_HIP(c, hipEventRecord(e.second, s));
+      if (out) *out = e.second;
       return MSH_OK;
     }
   hipEvent_t ev = nullptr;
-  MSH_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  MSH_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence));
   hipError_t e = hipEventRecord(ev, s);
   if (e != hipSuccess) {
     (void)hipEventDestroy(ev);
     return hip_fail(c, e, "hipEventRecord");
   }
   evs.emplace_back(s, ev);
+  if (out) *out = ev;
   return MSH_OK;
 }
 
 // After a launch on caller stream s that reads the current table version (seq: and updates the
-// sequential-mode counts).
+// sequential-mode counts). One record per launch: a sequential launch's entry in seq_inflight is the
+// table version's reader event for s itself (a non-owning alias; the readers' events live until
+// msh_destroy, and a later record of the same event on s only marks a later point of the stream).
 int track_launch(msh_ctx* c, hipStream_t s, bool seq) {
-  int rc = record_on(c, cur_table(c).readers, s);
-  if (rc == MSH_OK && seq) rc = record_on(c, c->seq_inflight, s);
-  return rc;
+  hipEvent_t ev = nullptr;
+  int rc = record_on(c, cur_table(c).readers, s, &ev);
+  if (rc != MSH_OK || !seq) return rc;
+  for (auto& e : c->seq_inflight)
+    if (e.first == s) {
+      e.second = ev;
+      return MSH_OK;
+    }
+  c->seq_inflight.emplace_back(s, ev);
+  return MSH_OK;
 }
 
 // Order prep_stream after the sequential launches in flight (device-side waits): they update the
@@ -723,7 +740,7 @@ void msh_destroy(msh_ctx* c) {
     destroy_events(t.readers);
     free_table(t);
   }
-  destroy_events(c->seq_inflight);
+  c->seq_inflight.clear();  // aliases of the readers' events (destroyed above)
   (void)hipFree(c->d_counts);
   for (hipEvent_t e : c->async_ev)
     if (e) (void)hipEventDestroy(e);

@@ -72,6 +72,8 @@ struct msh_ctx {
   size_t counts_cap = 0;
   int32_t counts_replicas = 1;
   bool counts_dirty = false;
+  // per caller stream, the event of its last sequential launch: an alias of a table version's reader
+  // event (not owned here; track_launch)
   std::vector<std::pair<hipStream_t, hipEvent_t>> seq_inflight;
   // the rewrites' own stream, created with the device's highest priority: HIP gives each priority
   // its own hardware queues, so a rewrite never queues behind other streams' kernels that happen to

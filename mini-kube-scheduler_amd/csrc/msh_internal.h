@@ -126,7 +126,7 @@ constexpr int MULTI_MAX = 32;  // batches per launch (kernel-argument descriptor
 
 // The per-pair kernel (pair_kernel): nb (1..MULTI_MAX) batches in one launch, or (shard) the
 // per-pod shard keys of ONE batch, d[0].
-struct PairArgs {
+struct PairCommon {
   const uint32_t* planes;  // bit-sliced node table (PLANE_* layout), n_groups groups
   int32_t n_groups;
   int32_t g_full;          // groups [0, g_full) hold real nodes only (no padding slot)
@@ -140,8 +140,15 @@ struct PairArgs {
   // replica (64-pod block mod SEQ_COUNT_REPLICAS) of these SEQ_COUNT_REPLICAS arrays; null otherwise
   int32_t* counts;
   int64_t count_stride;
-  BatchDesc d[MULTI_MAX];
 };
+// The kernel arguments with room for NB batch descriptors: the host builds PairArgs (MULTI_MAX); a
+// one-batch launch passes PairArgsN<1> (88 B of arguments instead of 1.4 KB: the argument copy of a
+// 1.4 KB block costs ~3-4 us of host time per hipLaunchKernel, profiles/ab/r6_launch_args.txt)
+template <int NB>
+struct PairArgsN : PairCommon {
+  BatchDesc d[NB];
+};
+using PairArgs = PairArgsN<MULTI_MAX>;
 hipError_t launch_pairs(PairArgs& a, bool shard, const DeviceInfo& dev, hipStream_t s);
 
 hipError_t launch_decode_keys(const int8_t* pod_digit, int32_t p, const int32_t* keys, PluginParams pp,

@@ -168,14 +168,14 @@ __device__ __forceinline__ uint32_t group_first_or_none(const uint32_t* __restri
   return m < GROUP_NODES ? g * GROUP_NODES + m : NOFIT;
 }
 
-template <int S, bool SHARD, bool KX, bool CNT>
-__global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgs a) {
+template <int S, bool SHARD, bool KX, bool CNT, int NB>
+__global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgsN<NB> a) {
   constexpr int PB = PAIR_WAVES / S;  // 64-pod blocks per workgroup
   __shared__ uint32_t s_res[S > 1 ? PAIR_WAVES : 1][2][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int sl = wv % S, pb = wv / S;
-  const BatchDesc& d = a.d[blockIdx.y];
+  const BatchDesc& d = a.d[NB == 1 ? 0 : blockIdx.y];
   const int32_t np = d.n_pods;
   if ((int32_t)blockIdx.x * PB * WAVE >= np) return;  // the whole workgroup lies past its batch's end
   const int32_t wbase = ((int32_t)blockIdx.x * PB + pb) * WAVE;
@@ -774,15 +774,19 @@ int pair_slices(int64_t waves, int32_t n_groups, const DeviceInfo& dev) {
 template <int S, bool SHARD, bool KX>
 hipError_t launch_pair_s(PairArgs& a, int32_t bx, hipStream_t s) {
   a.gps = (a.n_groups + S - 1) / S;
-  if constexpr (!SHARD) {
+  const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(PAIR_WAVES * WAVE);
+  if (a.nb == 1) {  // one descriptor's worth of kernel arguments (shard-key and counting launches: always)
+    PairArgsN<1> b;
+    static_cast<PairCommon&>(b) = a;
+    b.d[0] = a.d[0];
     if (a.counts) {
-      MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, true>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PAIR_WAVES * WAVE),
-                       0, s, a);
-      return hipGetLastError();
+      if constexpr (!SHARD) MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, true, 1>), grid, blk, 0, s, b);
+    } else {
+      MSH_TIMED_LAUNCH((pair_kernel<S, SHARD, KX, false, 1>), grid, blk, 0, s, b);
     }
+    return hipGetLastError();
   }
-  MSH_TIMED_LAUNCH((pair_kernel<S, SHARD, KX, false>), dim3((unsigned)bx, (unsigned)a.nb), dim3(PAIR_WAVES * WAVE), 0,
-                   s, a);
+  if constexpr (!SHARD) MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, false, MULTI_MAX>), grid, blk, 0, s, a);
   return hipGetLastError();
 }
 
