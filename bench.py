@@ -111,7 +111,8 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
         sl *= 2
     # the last two parameters: the commit epilogue (sequential mode only) and the descriptor count of the
     # argument block (1 for a one-batch launch, 32 otherwise)
-    return f"void msh::pair_kernel<{sl}, {b(shard)}, {b(kx)}, false, {32 if multi and nb > 1 else 1}>"
+    # planes staged in LDS (the last parameter) for tables up to 128 groups (msh_pair.hip PAIR_SLICE_LDS_GROUPS)
+    return f"void msh::pair_kernel<{sl}, {b(shard)}, {b(kx)}, false, {32 if multi and nb > 1 else 1}, {b(groups <= 128)}>"
 
 
 def seq_shape(n_nodes: int, cap: bool = False):
@@ -522,7 +523,7 @@ def seq_pair_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False) -> str
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2
-    return f"void msh::pair_kernel<{sl}, false, {str(kx).lower()}, true, 1>"
+    return f"void msh::pair_kernel<{sl}, false, {str(kx).lower()}, true, 1, {str(groups <= 128).lower()}>"
 
 
 def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=False, cap=0, form="pair"):

@@ -142,8 +142,8 @@ struct PairCommon {
   int64_t count_stride;
 };
 // The kernel arguments with room for NB batch descriptors: the host builds PairArgs (MULTI_MAX); a
-// one-batch launch passes PairArgsN<1> (88 B of arguments instead of 1.4 KB: the argument copy of a
-// 1.4 KB block costs ~3-4 us of host time per hipLaunchKernel, profiles/ab/r6_launch_args.txt)
+// one-batch launch passes PairArgsN<1> (136 B of arguments instead of 1,624 B: the argument copy of a
+// 1.6 KB block costs ~3-4 us of host time per hipLaunchKernel)
 template <int NB>
 struct PairArgsN : PairCommon {
   BatchDesc d[NB];

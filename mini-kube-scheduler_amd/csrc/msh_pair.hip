@@ -28,6 +28,22 @@ __device__ __forceinline__ void sload_group(u32x8* pl, const uint32_t* src) {
                  "+s"(pl[5]));
 }
 
+// NPL planes of group g: by scalar loads (LDSP false), or (LDSP) from the workgroup's LDS copy of the
+// table as wave-uniform ds_read_b128 (a broadcast) into VGPRs.
+template <int NPL, bool LDSP>
+__device__ __forceinline__ void get_group(u32x8* pl, const uint32_t* planes, const uint4* s_tab, int32_t g) {
+  if constexpr (LDSP) {
+    const uint4* q = s_tab + g * (GROUP_DWORDS / 4);
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const uint4 lo = q[2 * k], hi = q[2 * k + 1];
+      pl[k] = u32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    }
+  } else {
+    sload_group<NPL>(pl, planes + (size_t)g * GROUP_DWORDS);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Per-pair batch kernel: the default batch path (msh_schedule_batch*, msh_schedule_batches_device,
 // msh_shard_keys_device) for the reference's plugins, in every normalize mode.
@@ -168,10 +184,11 @@ __device__ __forceinline__ uint32_t group_first_or_none(const uint32_t* __restri
   return m < GROUP_NODES ? g * GROUP_NODES + m : NOFIT;
 }
 
-template <int S, bool SHARD, bool KX, bool CNT, int NB>
+template <int S, bool SHARD, bool KX, bool CNT, int NB, bool LDSP>
 __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgsN<NB> a) {
   constexpr int PB = PAIR_WAVES / S;  // 64-pod blocks per workgroup
   __shared__ uint32_t s_res[S > 1 ? PAIR_WAVES : 1][2][WAVE];
+  extern __shared__ uint4 s_tabp[];  // LDSP: the table's planes (n_groups x GROUP_DWORDS)
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int sl = wv % S, pb = wv / S;
@@ -186,6 +203,12 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgsN<NB> a
     const int dq = d.pod_digit[j];
     code = (dq >= 0 && dq <= 9) ? (uint32_t)dq : CODE_NONE_POD;  // NodeNumber.PreScore: Atoi of the last byte
     tol = d.pod_tol[j] ? 1u : 0u;
+  }
+  if constexpr (LDSP) {  // the table into LDS, its loads in flight together with the pod loads above
+    const uint4* src = reinterpret_cast<const uint4*>(a.planes);
+    const int32_t n4 = a.n_groups * (GROUP_DWORDS / 4);
+    for (int32_t i = (int32_t)threadIdx.x; i < n4; i += PAIR_WAVES * WAVE) s_tabp[i] = src[i];
+    __syncthreads();
   }
   const uint32_t P0 = 0u - (code & 1u), P1 = 0u - ((code >> 1) & 1u), P2 = 0u - ((code >> 2) & 1u),
                  P3 = 0u - (code >> 3);
@@ -210,11 +233,11 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgsN<NB> a
       u32x8 pl[PLANE_N];
       bool sn, st;
       if (gg < g_full) {
-        sload_group<PLANE_V>(pl, a.planes + (size_t)gg * GROUP_DWORDS);
+        get_group<PLANE_V, LDSP>(pl, a.planes, s_tabp, gg);
         pair_group<false, KX>(pl, P0, P1, P2, P3, nT, am, ax);
         if constexpr (!KX) group_feasible_s<false>(pl, sn, st);
       } else {
-        sload_group<PLANE_N>(pl, a.planes + (size_t)gg * GROUP_DWORDS);
+        get_group<PLANE_N, LDSP>(pl, a.planes, s_tabp, gg);
         pair_group<true, KX>(pl, P0, P1, P2, P3, nT, am, ax);
         if constexpr (!KX) group_feasible_s<true>(pl, sn, st);
       }
@@ -230,7 +253,7 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgsN<NB> a
   if (g_lo < g_hi) {
     uint32_t km[PLANE_GW], kx[PLANE_GW];
     u32x8 pl[PLANE_N];
-    sload_group<PLANE_N>(pl, a.planes + (size_t)g_lo * GROUP_DWORDS);
+    get_group<PLANE_N, LDSP>(pl, a.planes, s_tabp, g_lo);
     if (g_lo < g_full) pair_group_keep<false, KX>(pl, P0, P1, P2, P3, nT, km, kx);
     else pair_group_keep<true, KX>(pl, P0, P1, P2, P3, nT, km, kx);
     const uint32_t am = bop3_and3(bop3_and3(km[0], km[1], km[2]), bop3_and3(km[3], km[4], km[5]), km[6] & km[7]);
@@ -256,12 +279,12 @@ __global__ __launch_bounds__(PAIR_WAVES * WAVE) void pair_kernel(PairArgsN<NB> a
       uint32_t at = group_first_feasible_s<false>(pl, (uint32_t)g_lo);
       if (an == NOFIT && fn != NO_GROUP) {
         u32x8 p2[PLANE_N];
-        sload_group<PLANE_N>(p2, a.planes + (size_t)fn * GROUP_DWORDS);
+        get_group<PLANE_N, LDSP>(p2, a.planes, s_tabp, (int32_t)fn);
         an = group_first_feasible_s<true>(p2, fn);
       }
       if (at == NOFIT && ft != NO_GROUP) {
         u32x8 p2[PLANE_N];
-        sload_group<PLANE_N>(p2, a.planes + (size_t)ft * GROUP_DWORDS);
+        get_group<PLANE_N, LDSP>(p2, a.planes, s_tabp, (int32_t)ft);
         at = group_first_feasible_s<false>(p2, ft);
       }
       rx = tol ? at : an;
@@ -771,23 +794,33 @@ int pair_slices(int64_t waves, int32_t n_groups, const DeviceInfo& dev) {
   return sl;
 }
 
-template <int S, bool SHARD, bool KX>
-hipError_t launch_pair_s(PairArgs& a, int32_t bx, hipStream_t s) {
+template <int S, bool SHARD, bool KX, bool LDSP>
+hipError_t launch_pair_l(PairArgs& a, int32_t bx, hipStream_t s) {
   a.gps = (a.n_groups + S - 1) / S;
   const dim3 grid((unsigned)bx, (unsigned)a.nb), blk(PAIR_WAVES * WAVE);
+  const unsigned lds = LDSP ? (unsigned)(a.n_groups * GROUP_DWORDS * sizeof(uint32_t)) : 0u;
   if (a.nb == 1) {  // one descriptor's worth of kernel arguments (shard-key and counting launches: always)
     PairArgsN<1> b;
     static_cast<PairCommon&>(b) = a;
     b.d[0] = a.d[0];
     if (a.counts) {
-      if constexpr (!SHARD) MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, true, 1>), grid, blk, 0, s, b);
+      if constexpr (!SHARD) MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, true, 1, LDSP>), grid, blk, lds, s, b);
     } else {
-      MSH_TIMED_LAUNCH((pair_kernel<S, SHARD, KX, false, 1>), grid, blk, 0, s, b);
+      MSH_TIMED_LAUNCH((pair_kernel<S, SHARD, KX, false, 1, LDSP>), grid, blk, lds, s, b);
     }
     return hipGetLastError();
   }
-  if constexpr (!SHARD) MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, false, MULTI_MAX>), grid, blk, 0, s, a);
+  if constexpr (!SHARD) MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, false, MULTI_MAX, LDSP>), grid, blk, lds, s, a);
   return hipGetLastError();
+}
+
+// Planes from LDS for tables up to PAIR_SLICE_LDS_GROUPS groups (msh_options.pair_planes = 1 keeps scalar
+// loads): a one-batch C3 launch waited on five dependent scalar-load round trips per wave.
+constexpr int PAIR_SLICE_LDS_GROUPS = 128;  // 32,768 nodes, 24 KB per workgroup
+template <int S, bool SHARD, bool KX>
+hipError_t launch_pair_s(PairArgs& a, int32_t bx, const DeviceInfo& dev, hipStream_t s) {
+  if (dev.pair_planes != 1 && a.n_groups <= PAIR_SLICE_LDS_GROUPS) return launch_pair_l<S, SHARD, KX, true>(a, bx, s);
+  return launch_pair_l<S, SHARD, KX, false>(a, bx, s);
 }
 
 template <bool SHARD, bool KX>
@@ -831,9 +864,9 @@ hipError_t launch_pair_t(PairArgs& a, const DeviceInfo& dev, hipStream_t s) {
   const int32_t blocks = (maxp + WAVE - 1) / WAVE;  // 64-pod blocks of the largest batch
   auto bx = [&](int sl) { return (blocks * sl + PAIR_WAVES - 1) / PAIR_WAVES; };
   switch (S) {
-    case 1: return launch_pair_s<1, SHARD, KX>(a, bx(1), s);
-    case 2: return launch_pair_s<2, SHARD, KX>(a, bx(2), s);
-    default: return launch_pair_s<4, SHARD, KX>(a, bx(4), s);
+    case 1: return launch_pair_s<1, SHARD, KX>(a, bx(1), dev, s);
+    case 2: return launch_pair_s<2, SHARD, KX>(a, bx(2), dev, s);
+    default: return launch_pair_s<4, SHARD, KX>(a, bx(4), dev, s);
   }
 }
 }  // namespace

@@ -8,10 +8,10 @@ OUT=${OUT:-gpurun_out/absingle}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 for sl in ${SLICES:-1 2 4}; do
-  PAIR_SLICES=$sl WEIGHT=3 NORM=1 MODE=${MODE:-batch} PODS=${PODS:-100000} LAUNCHES=40 timeout -k 10 120 \
-    rocprofv3 --kernel-trace --stats -d "$OUT/s$sl" -o run --output-format csv -- python3 scripts/run_batch.py \
-    > "$OUT/s$sl.log" 2>&1 || { echo "[s$sl] failed"; tail -5 "$OUT/s$sl.log"; exit 1; }
-  python3 - "$OUT/s$sl" "slices=$sl" <<'PY'
+  PAIR_PLANES=${PLANES:-auto} PAIR_SLICES=$sl WEIGHT=3 NORM=1 MODE=${MODE:-batch} PODS=${PODS:-100000} LAUNCHES=40 timeout -k 10 120 \
+    rocprofv3 --kernel-trace --stats -d "$OUT/${PLANES:-auto}_s$sl" -o run --output-format csv -- python3 scripts/run_batch.py \
+    > "$OUT/${PLANES:-auto}_s$sl.log" 2>&1 || { echo "[s$sl] failed"; exit 1; }
+  python3 - "$OUT/${PLANES:-auto}_s$sl" "${PLANES:-auto} slices=$sl" <<'PY'
 import csv, sys, pathlib
 for f in pathlib.Path(sys.argv[1]).rglob("*kernel_stats.csv"):
     for r in csv.DictReader(open(f)):
@@ -21,10 +21,10 @@ for f in pathlib.Path(sys.argv[1]).rglob("*kernel_stats.csv"):
 PY
 done
 if [ -n "${PMC:-1}" ]; then
-  WEIGHT=3 NORM=1 MODE=${MODE:-batch} PODS=${PODS:-100000} LAUNCHES=10 timeout -s KILL 120 rocprofv3 --pmc \
+  PAIR_PLANES=${PLANES:-auto} WEIGHT=3 NORM=1 MODE=${MODE:-batch} PODS=${PODS:-100000} LAUNCHES=10 timeout -s KILL 120 rocprofv3 --pmc \
     SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU \
-    -d "$OUT/pmc" -o run --output-format csv -- python3 scripts/run_batch.py > "$OUT/pmc.log" 2>&1 || { echo "[pmc] failed"; exit 1; }
-  python3 - "$OUT/pmc" <<'PY'
+    -d "$OUT/${PLANES:-auto}_pmc" -o run --output-format csv -- python3 scripts/run_batch.py > "$OUT/${PLANES:-auto}_pmc.log" 2>&1 || { echo "[pmc] failed"; exit 1; }
+  python3 - "$OUT/${PLANES:-auto}_pmc" <<'PY'
 import csv, sys, pathlib
 from collections import defaultdict
 acc = defaultdict(list)

@@ -31,6 +31,8 @@ if mode == "generic":
     options["batch_kernel"] = "generic"
 if os.environ.get("SPLIT", "auto") in ("serial", "blocks"):
     options["seq_split"] = os.environ["SPLIT"]
+if os.environ.get("PAIR_PLANES"):
+    options["pair_planes"] = os.environ["PAIR_PLANES"]  # msh_options.pair_planes: auto, sgpr, lds
 if os.environ.get("PAIR_SLICES"):
     options["pair_slices"] = int(os.environ["PAIR_SLICES"])  # msh_options.pair_slices: 1, 2, 4 slice waves per block
 if os.environ.get("SEQ_WAVES"):

@@ -1027,7 +1027,7 @@ def test_multi_batch_invalid(msh, gpu_ctx):
         gpu_ctx.schedule_batches_device(bad)
 
 
-@pytest.mark.parametrize("planes", ["sgpr", "lds", "lds-noax", "lds-axlast"])
+@pytest.mark.parametrize("planes", ["auto", "sgpr", "lds", "lds-noax", "lds-axlast"])
 @pytest.mark.parametrize("n", [1000, 8192, 8193, 20_000, 32_768, 70_000, 106_496, 106_497])
 def test_pair_kernel_late_matches(msh, oracle, n, planes):
     """pair_kernel re-reads the first group with a hit from memory when it lies above the lowest group
@@ -1036,7 +1036,8 @@ def test_pair_kernel_late_matches(msh, oracle, n, planes):
     with and without a padded top group."""
     torch = pytest.importorskip("torch")
     opts = _pair_opts(planes)  # lds: 4-wave workgroups up to 32,768 nodes, 16-wave up to
-    # 106,496 (106,497 falls back to scalar-loaded planes)
+    # 106,496 (106,497 falls back to scalar-loaded planes); auto (3,000 pods: the slice kernel): planes
+    # staged in LDS up to 32,768 nodes, scalar loads above
     rng = np.random.default_rng(n + 4)
     u, nd, pd, pt = _rand_case(rng, n, 3000, p_unsched=0.2, p_tol=0.3)
     nd[: n // 2][nd[: n // 2] == 3] = 4
@@ -1066,7 +1067,8 @@ def test_pair_kernel_late_matches(msh, oracle, n, planes):
             _assert_same([out[i].cpu().numpy() for i in (2, 3, 4)], want, f"keys n={n} norm={norm}")
 
 
-@pytest.mark.parametrize("planes,slices", [("sgpr", 0), ("sgpr", 1), ("sgpr", 2), ("sgpr", 4), ("lds", 0),
+@pytest.mark.parametrize("planes,slices", [("auto", 0), ("auto", 1), ("auto", 2), ("auto", 4),
+                                           ("sgpr", 0), ("sgpr", 1), ("sgpr", 2), ("sgpr", 4), ("lds", 0),
                                            ("lds-noax", 0), ("lds-axlast", 0)])
 @pytest.mark.parametrize("n", [1000, 5000, 20_000])
 def test_pair_kernel_late_feasible(msh, oracle, n, planes, slices):
