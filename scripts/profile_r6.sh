@@ -42,6 +42,7 @@ if has trace; then
   tr stats_generic generic 1 0 || exit 1
   tr stats_generic_hl generic 3 1 || exit 1
   tr stats_generic_col generic_col 1 0 || exit 1
+  tr stats_single batch 3 1 || exit 1
   tr stats_seq_pair sequential 3 1 || exit 1
   SPLIT=blocks tr stats_seq sequential 3 1 || exit 1
   SPLIT=serial tr stats_seq_serial sequential 3 1 || exit 1
