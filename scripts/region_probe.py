@@ -39,6 +39,9 @@ for _ in range(10):
     fast.schedule_batches_device(handle, K, addr, sh or None)
 torch.cuda.synchronize()
 call, wait, region = [], [], []
+# SYNC=stream: wait for the launch stream only (torch.cuda.current_stream().synchronize()), to separate the
+# device-wide synchronize's own cost from the launch's completion latency
+sync = torch.cuda.current_stream(dev).synchronize if __import__("os").environ.get("SYNC") == "stream" else torch.cuda.synchronize
 gap = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0  # seconds of host idle before each region
 for _ in range(R):
     torch.cuda.synchronize()
@@ -47,7 +50,7 @@ for _ in range(R):
     t0 = time.perf_counter()
     fast.schedule_batches_device(handle, K, addr, sh or None)
     t1 = time.perf_counter()
-    torch.cuda.synchronize()
+    sync()
     t2 = time.perf_counter()
     call.append(t1 - t0)
     wait.append(t2 - t1)
