@@ -537,10 +537,17 @@ def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=F
         kname = seq_pair_label(n_local, p, cus)
         n_pad = max(-(-n_local // 1024) * 1024, 1024)
         model = PAIR_VALU_PER_WORD * (n_pad / 32) * (-(-p // 64) * 64) / (float(n_local) * p)
-        return valu_roofline(kname, launch_ms, float(n_local) * p, model, cus,
-                             pmc_entry("sequential_pair", kname, n_local, p, 1, plugin_tag(HEADLINE_WEIGHT, HEADLINE_NORM)),
-                             f"{PAIR_VALU_PER_WORD} VALU per 32-node word and 64-pod wave (pair_kernel's scan, "
-                             "msh_pair.hip); the commit epilogue is in the counter form")
+        entry = pmc_entry("sequential_pair", kname, n_local, p, 1, plugin_tag(HEADLINE_WEIGHT, HEADLINE_NORM))
+        out = valu_roofline(kname, launch_ms, float(n_local) * p, model, cus, entry,
+                            f"{PAIR_VALU_PER_WORD} VALU per 32-node word and 64-pod wave (pair_kernel's scan, "
+                            "msh_pair.hip); the commit epilogue is in the counter form")
+        if entry and "SQ_WAVE_CYCLES" in entry:
+            out["wait_any_frac_of_wave_cycles"] = entry.get("sq_wait_any_frac_of_wave_cycles")
+            out["wave_cycles_per_wave"] = 4 * entry["SQ_WAVE_CYCLES"] / entry["SQ_WAVES"]
+        out["bound_note"] = ("one 100k-pod batch per launch is latency-bound, not issue-bound: each wave lives for "
+                             "thousands of cycles around one memory round trip in and the stores out (DESIGN.md "
+                             "§4.2 LDSP, §9); the VALU fraction is not the binding limit here")
+        return out
     if mode == "sequential" and not serial:
         # Without a capacity the pods run in blocks of consecutive pods, one workgroup each (a wave per
         # block walks its pods in order, every pod against the whole register-resident table): VALU-bound
