@@ -804,13 +804,15 @@ hipError_t launch_pair_l(PairArgs& a, int32_t bx, hipStream_t s) {
     static_cast<PairCommon&>(b) = a;
     b.d[0] = a.d[0];
     if (a.counts) {
-      if constexpr (!SHARD) MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, true, 1, LDSP>), grid, blk, lds, s, b);
+      if constexpr (SHARD) return hipErrorInvalidValue;  // (launch_pairs rejects it first)
+      else MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, true, 1, LDSP>), grid, blk, lds, s, b);
     } else {
       MSH_TIMED_LAUNCH((pair_kernel<S, SHARD, KX, false, 1, LDSP>), grid, blk, lds, s, b);
     }
     return hipGetLastError();
   }
-  if constexpr (!SHARD) MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, false, MULTI_MAX, LDSP>), grid, blk, lds, s, a);
+  if constexpr (SHARD) return hipErrorInvalidValue;  // shard keys: one batch (launch_pairs rejects more first)
+  else MSH_TIMED_LAUNCH((pair_kernel<S, false, KX, false, MULTI_MAX, LDSP>), grid, blk, lds, s, a);
   return hipGetLastError();
 }
 
