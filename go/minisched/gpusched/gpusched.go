@@ -493,7 +493,9 @@ func (x *Ctx) Wait(b *HostBatch) ([]Result, error) {
 
 // ScheduleSequential places the pods one at a time with a node-state commit between placements
 // (the reference's serial Run loop, minisched.go:28-30, on the device). maxPodsPerNode > 0 makes a
-// node infeasible once it holds that many pods (build extension); 0 = reference semantics.
+// node infeasible once it holds that many pods (build extension); 0 = reference semantics, where no
+// commit feeds a later decision: the library then runs the batch kernel and adds the placements to the
+// node counts (a no-capacity shortcut with the serial loop's placements and counts).
 func (x *Ctx) ScheduleSequential(pods []*v1.Pod, b *HostBatch, maxPodsPerNode int32) ([]Result, error) {
 	if !x.hasNodes {
 		return nil, errors.New("gpusched: UploadNodes has not been called")
