@@ -81,6 +81,7 @@ GEN_VALU_PER_PAIR_REF = 117 / 32
 SEQ_VALU_PER_WORD = 5
 PAIR_LDS_MAX_GROUPS = 128          # msh_pair.hip: tables the LDS-staged pair kernel takes (4-wave workgroups)
 PAIR_LDS_BIG_GROUPS = 416          # ... and with 16-wave workgroups
+PAIR_SLICE_LDS_GROUPS = 128        # msh_pair.hip: tables whose planes the slice kernel (pair_kernel) stages in LDS
 PMC_FILE = ROOT / "profiles" / "r6_pmc_c3.json"
 # The headline plugin set (BASELINE C3: "nodenumber prescore/score + weighted NormalizeScore"): the
 # reference's filter and prescore lists, NodeNumber scored at weight 3 with upstream's
@@ -111,8 +112,9 @@ def batch_kernel_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False, sh
         sl *= 2
     # the last two parameters: the commit epilogue (sequential mode only) and the descriptor count of the
     # argument block (1 for a one-batch launch, 32 otherwise)
-    # planes staged in LDS (the last parameter) for tables up to 128 groups (msh_pair.hip PAIR_SLICE_LDS_GROUPS)
-    return f"void msh::pair_kernel<{sl}, {b(shard)}, {b(kx)}, false, {32 if multi and nb > 1 else 1}, {b(groups <= 128)}>"
+    # planes staged in LDS (the last parameter) for tables up to PAIR_SLICE_LDS_GROUPS groups
+    return (f"void msh::pair_kernel<{sl}, {b(shard)}, {b(kx)}, false, {32 if multi and nb > 1 else 1}, "
+            f"{b(groups <= PAIR_SLICE_LDS_GROUPS)}>")
 
 
 def seq_shape(n_nodes: int, cap: bool = False):
@@ -523,7 +525,7 @@ def seq_pair_label(n_nodes: int, n_pods: int, cus: int, kx: bool = False) -> str
     sl = 1
     while sl < 4 and waves * sl < cus * 16 and groups >= 4 * sl:
         sl *= 2
-    return f"void msh::pair_kernel<{sl}, false, {str(kx).lower()}, true, 1, {str(groups <= 128).lower()}>"
+    return f"void msh::pair_kernel<{sl}, false, {str(kx).lower()}, true, 1, {str(groups <= PAIR_SLICE_LDS_GROUPS).lower()}>"
 
 
 def make_roofline(mode, n_local, p, launch_ms, batches_per_launch, cus, serial=False, cap=0, form="pair"):
